@@ -1,0 +1,192 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: fused-HIP PCG throughput on the BASELINE.json headline config.
+
+Metric (BASELINE.json): grid-point updates per second (MLUPS) + iterations-to-tolerance on a
+16384^2 grid at 1/2/4/8 MI355X.  One "step" = one full PCG iteration (halo exchange, A p with
+(Ap,p), w/r update with ||dw|| and (z,r), both all-reduces, p update) -- nothing skipped.
+MLUPS = (M-1)(N-1) * steps / time / 1e6, whole-job aggregate.  The grid is fixed as N grows
+(strong scaling).  Synthetic data = the reference problem itself: F = 1 in the ellipse
+x^2 + 4y^2 < 1, zero initial guess (there is no dataset).
+
+    python bench.py --gpus 1 --steps 200 --warmup 20
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8 --steps 200 --warmup 20
+
+After the timed region a full solve to ||w^{k+1}-w^k|| < 1e-6 reports iters-to-tol and the
+accuracy against the analytic solution (disable with --no-tol-solve).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINE_MLUPS = 2450.0  # best published reference rate: 2x P100, 2400x3200
+METRIC = "grid-point updates/sec (MLUPS) + iters-to-tol, 16384^2 grid at 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--M", type=int, default=16384)
+    ap.add_argument("--N", type=int, default=16384)
+    ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
+    ap.add_argument("--comm", default="native", choices=["native", "torch"])
+    ap.add_argument("--split", default="reference", choices=["reference", "auto", "rows", "cols"])
+    ap.add_argument("--block", type=int, default=256)
+    ap.add_argument("--tile-rows", type=int, default=64)
+    ap.add_argument("--graph-batch", type=int, default=32)
+    ap.add_argument("--exact", action="store_true", help="reference arithmetic order in the fused kernels")
+    ap.add_argument("--tol-solve", dest="tol_solve", action="store_true", default=True)
+    ap.add_argument("--no-tol-solve", dest="tol_solve", action="store_false")
+    ap.add_argument("--tol-time-cap", type=float, default=300.0, help="seconds allowed for the tol solve")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import importlib
+
+    import torch
+    import torch.distributed as dist
+
+    pmx = importlib.import_module("poisson-ellipse-openmp-mpi-cuda-new_amd")
+    from importlib import import_module
+
+    launch = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.parallel.launch")
+    info = launch.init_distributed()
+    world = info.world
+    if world != args.gpus:
+        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs an MI355X (no HIP device visible)")
+    torch.cuda.set_device(info.local_rank)
+
+    problem = pmx.PoissonEllipse(M=args.M, N=args.N)
+    kw = dict(split=args.split, dtype=args.dtype, block=args.block, tile_rows=args.tile_rows, exact=args.exact,
+              graph_batch=args.graph_batch)
+    comm_used = args.comm
+    if world == 1:
+        models = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.models")
+        sess = models.make_session(problem, ranks=1, device=info.local_rank, **kw)
+
+        class Runner:
+            init = sess.init
+            step = sess.step
+            synchronize = sess.synchronize
+
+            @staticmethod
+            def state():
+                return sess.state(0)
+
+        runner = Runner()
+        comm_used = "self"
+    else:
+        ds = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.parallel.dist_solver")
+        try:
+            runner = ds.DistGpuPCG(problem, info, comm=args.comm, rccl_graph=False, **kw)
+        except Exception as e:  # native RCCL bootstrap failed -> portable torch.distributed path
+            if args.comm != "native":
+                raise
+            print(f"[bench] native RCCL comm failed ({e}); falling back to torch.distributed", file=sys.stderr)
+            runner = ds.DistGpuPCG(problem, info, comm="torch", **kw)
+            comm_used = "torch"
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    # ---------------- timed region ----------------
+    runner.init()
+    runner.step(args.warmup)
+    runner.synchronize()
+    st0 = runner.state()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    runner.step(args.steps)
+    runner.synchronize()
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    dt = t1 - t0
+    st1 = runner.state()
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    valid = (not st1["done"]) and (st1["it"] - st0["it"] == args.steps) and not st1["nan"]
+    pts = (args.M - 1) * (args.N - 1)
+    mlups = pts * args.steps / dt / 1e6
+
+    # ---------------- iterations to tolerance ----------------
+    tol = {}
+    if args.tol_solve:
+        runner.init()
+        barrier()
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        launched, batch = 0, max(args.graph_batch, 32)
+        max_iter = problem.effective_max_iter()
+        capped = False
+        while True:
+            runner.step(batch)
+            launched += batch
+            st = runner.state()
+            if st["done"] or launched > max_iter + batch:
+                break
+            if time.perf_counter() - ts > args.tol_time_cap:
+                capped = True
+                break
+        runner.synchronize()
+        barrier()
+        tsolve = time.perf_counter() - ts
+        tol = dict(iters_to_tol=int(st["iters"]) if st["done"] else None, tol_status=st["status"],
+                   tol_final_diff=st["diff"], tol_solve_seconds=round(tsolve, 4),
+                   tol_solve_mlups=round(pts * (st["iters"] if st["done"] else st["it"]) / tsolve / 1e6, 1),
+                   tol_time_capped=capped)
+
+    if info.rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(mlups, 1),
+            "unit": "MLUPS",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": round(mlups / BASELINE_MLUPS, 2),
+            "dtype": args.dtype,
+            "data": "synthetic (reference problem: F=1 in ellipse x^2+4y^2<1, zero initial guess)",
+            "config": {
+                "model": f"fictitious-domain Poisson ellipse, Jacobi-PCG, {args.M}x{args.N}",
+                "global_batch": 1,
+                "seq_len": pts,
+                "parallelism": f"domain{world}" if world > 1 else "single",
+                "grid": [args.M, args.N],
+                "comm": comm_used,
+                "tile": [args.tile_rows, args.block],
+                "graph_batch": args.graph_batch,
+                "exact": args.exact,
+            },
+            "valid": valid,
+            "baseline_mlups": BASELINE_MLUPS,
+            **tol,
+        }
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    launch.shutdown()
+
+
+if __name__ == "__main__":
+    main()

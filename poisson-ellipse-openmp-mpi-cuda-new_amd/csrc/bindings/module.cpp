@@ -1,0 +1,339 @@
+// Python bindings of the native pmx library (module `_pmx`).
+//
+// The binding layer is deliberately thin: device buffers are passed as integer pointers and
+// streams as integer hipStream_t handles, so the Python side can hand in torch tensors
+// (tensor.data_ptr(), torch.cuda.current_stream().cuda_stream) without linking libtorch.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "pmx/common.hpp"
+#include "pmx/cpu_pcg.hpp"
+#include "pmx/decomp.hpp"
+#include "pmx/gpu_solver.hpp"
+#include "pmx/kernels.hpp"
+#include "pmx/session.hpp"
+
+namespace py = pybind11;
+using namespace pmx;
+
+namespace {
+
+hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+py::array_t<double> to_numpy(const std::vector<double>& v, std::vector<py::ssize_t> shape) {
+  py::array_t<double> a(shape);
+  std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(double));
+  return a;
+}
+
+py::dict sd_dict(const Subdomain& s) {
+  py::dict d;
+  d["M"] = s.M; d["N"] = s.N; d["Px"] = s.grid.Px; d["Py"] = s.grid.Py;
+  d["rank"] = s.rank; d["px"] = s.px; d["py"] = s.py;
+  d["i_start"] = s.i_start; d["i_end"] = s.i_end; d["j_start"] = s.j_start; d["j_end"] = s.j_end;
+  d["nx"] = s.nx; d["ny"] = s.ny;
+  d["nb_xlo"] = s.nb_xlo; d["nb_xhi"] = s.nb_xhi; d["nb_ylo"] = s.nb_ylo; d["nb_yhi"] = s.nb_yhi;
+  d["aspect"] = s.aspect();
+  return d;
+}
+
+py::dict result_dict(const SolveResult& r, const ProblemSpec& s, bool with_w) {
+  py::dict d;
+  d["iters"] = r.iters;
+  d["status"] = std::string(status_name(r.status));
+  d["diff"] = r.last_diff;
+  d["seconds"] = r.seconds;
+  if (with_w && !r.w.empty()) d["w"] = to_numpy(r.w, {s.M + 1, s.N + 1});
+  return d;
+}
+
+py::dict state_dict(const PcgState& st) {
+  py::dict d;
+  d["red_a"] = st.red_a[0];
+  d["red_b"] = py::make_tuple(st.red_b[0], st.red_b[1]);
+  d["zr"] = py::make_tuple(st.zr[0], st.zr[1]);
+  d["diff"] = st.diff;
+  d["it"] = st.it;
+  d["iters"] = st.iters;
+  d["done"] = bool(st.done);
+  d["status"] = std::string(status_name(Status(st.status)));
+  d["nan"] = bool(st.nan_flag);
+  return d;
+}
+
+py::dict stats_dict(const RunStats& r) {
+  py::dict d;
+  d["iters"] = r.iters;
+  d["status"] = std::string(status_name(r.status));
+  d["diff"] = r.diff;
+  d["init_seconds"] = r.init_seconds;
+  d["solve_seconds"] = r.solve_seconds;
+  d["launched"] = r.launched;
+  d["nan"] = r.nan;
+  d["t_kernel_a"] = r.t_kernel_a;
+  d["t_kernel_b"] = r.t_kernel_b;
+  d["t_comm"] = r.t_comm;
+  return d;
+}
+
+py::dict layout_dict(const CommLayout& L) {
+  py::dict d;
+  d["state_off"] = L.state_off;
+  d["send_off"] = py::make_tuple(L.send_off[0], L.send_off[1], L.send_off[2], L.send_off[3]);
+  d["recv_off"] = py::make_tuple(L.recv_off[0], L.recv_off[1], L.recv_off[2], L.recv_off[3]);
+  d["edge_len"] = py::make_tuple(L.edge_len[0], L.edge_len[1], L.edge_len[2], L.edge_len[3]);
+  d["elem"] = L.elem;
+  d["bytes"] = L.bytes;
+  d["state_bytes"] = sizeof(PcgState);
+  d["red_a_off"] = offsetof(PcgState, red_a);
+  d["red_b_off"] = offsetof(PcgState, red_b);
+  return d;
+}
+
+// Raw-pointer ops on caller-owned buffers (torch tensors of shape (nx+2, pitch)).
+class OpContext {
+ public:
+  OpContext(const ProblemSpec& spec, int Px, int Py, int rank, int64_t pitch, int device)
+      : spec_(spec), device_(device) {
+    spec_.validate();
+    HIP_CHECK(hipSetDevice(device));
+    sd_ = decompose_2d(spec.M, spec.N, ProcGrid{Px, Py}, rank);
+    PMX_CHECK(pitch >= sd_.ny + 2, "pitch " << pitch << " < ny+2 = " << sd_.ny + 2);
+    geom_ = make_dev_geom(spec_, sd_, pitch);
+    tables_ = upload_tables(spec_, &buf_);
+    HIP_CHECK(hipMalloc(&partials_, 4096 * sizeof(double)));
+  }
+  ~OpContext() {
+    (void)hipSetDevice(device_);
+    if (buf_) (void)hipFree(buf_);
+    if (partials_) (void)hipFree(partials_);
+  }
+  py::dict subdomain() const { return sd_dict(sd_); }
+  void assemble(uintptr_t a, uintptr_t b, uintptr_t B, uintptr_t s) {
+    HIP_CHECK(hipSetDevice(device_));
+    launch_assemble(geom_, tables_, (double*)a, (double*)b, (double*)B, geom_.pitch, as_stream(s));
+  }
+  void apply_a(uintptr_t p, uintptr_t Ap, bool fp32, bool exact, uintptr_t s) {
+    HIP_CHECK(hipSetDevice(device_));
+    if (fp32) launch_apply_a<float>(geom_, tables_, (const float*)p, (float*)Ap, exact, as_stream(s));
+    else launch_apply_a<double>(geom_, tables_, (const double*)p, (double*)Ap, exact, as_stream(s));
+  }
+  void precond(uintptr_t r, uintptr_t z, bool fp32, bool exact, uintptr_t s) {
+    HIP_CHECK(hipSetDevice(device_));
+    if (fp32) launch_precond<float>(geom_, tables_, (const float*)r, (float*)z, exact, as_stream(s));
+    else launch_precond<double>(geom_, tables_, (const double*)r, (double*)z, exact, as_stream(s));
+  }
+  double dot(uintptr_t x, uintptr_t y, bool fp32, uintptr_t s) {
+    HIP_CHECK(hipSetDevice(device_));
+    const hipStream_t st = as_stream(s);
+    const int nb = fp32 ? launch_dot_partials<float>(geom_, (const float*)x, (const float*)y, partials_, 4096, st)
+                        : launch_dot_partials<double>(geom_, (const double*)x, (const double*)y, partials_, 4096, st);
+    std::vector<double> h(nb);
+    HIP_CHECK(hipMemcpyAsync(h.data(), partials_, nb * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    double sum = 0.0;
+    for (double v : h) sum += v;
+    return sum;
+  }
+
+ private:
+  ProblemSpec spec_;
+  int device_;
+  Subdomain sd_;
+  DevGeom geom_{};
+  DevTables tables_{};
+  double* buf_ = nullptr;
+  double* partials_ = nullptr;
+};
+
+GpuOptions make_options(int device, int block, int tile_rows, const std::string& dtype, bool exact,
+                        int graph_batch, bool check) {
+  GpuOptions o;
+  o.device = device;
+  o.block = block;
+  o.tile_rows = tile_rows;
+  PMX_CHECK(dtype == "fp64" || dtype == "fp32", "dtype must be fp64 or fp32, got " << dtype);
+  o.dtype = dtype == "fp64" ? DType::kFp64 : DType::kFp32;
+  o.exact = exact;
+  o.graph_batch = graph_batch;
+  o.check = check;
+  return o;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_pmx, m) {
+  m.doc() = "pmx: MI355X-native fictitious-domain Poisson PCG (native core)";
+  py::register_exception<pmx::Error>(m, "PmxError", PyExc_RuntimeError);
+
+  py::enum_<Norm>(m, "Norm").value("weighted", Norm::kWeighted).value("unweighted", Norm::kUnweighted);
+  py::enum_<Split>(m, "Split")
+      .value("reference", Split::kReference).value("auto", Split::kAuto)
+      .value("rows", Split::kRows).value("cols", Split::kCols);
+
+  py::class_<ProblemSpec>(m, "ProblemSpec")
+      .def(py::init<>())
+      .def_readwrite("M", &ProblemSpec::M).def_readwrite("N", &ProblemSpec::N)
+      .def_readwrite("A1", &ProblemSpec::A1).def_readwrite("B1", &ProblemSpec::B1)
+      .def_readwrite("A2", &ProblemSpec::A2).def_readwrite("B2", &ProblemSpec::B2)
+      .def_readwrite("ax", &ProblemSpec::ax).def_readwrite("by", &ProblemSpec::by)
+      .def_readwrite("F", &ProblemSpec::F).def_readwrite("delta", &ProblemSpec::delta)
+      .def_readwrite("max_iter", &ProblemSpec::max_iter).def_readwrite("norm", &ProblemSpec::norm)
+      .def("effective_max_iter", &ProblemSpec::effective_max_iter)
+      .def("validate", &ProblemSpec::validate);
+
+  m.def("grid_info", [](const ProblemSpec& s) {
+    const GridInfo g(s);
+    py::dict d;
+    d["h1"] = g.h1; d["h2"] = g.h2; d["eps"] = g.eps; d["inv_eps"] = g.inv_eps; d["h1h2"] = g.h1h2;
+    return d;
+  });
+  m.def("face_tables", [](const ProblemSpec& s) {
+    const GridInfo g(s);
+    const geo::FaceTables t(s, g);
+    py::dict d;
+    auto arr = [](const std::vector<double>& v) { return to_numpy(v, {py::ssize_t(v.size())}); };
+    d["rv"] = arr(t.rv); d["xlo"] = arr(t.xlo); d["xhi"] = arr(t.xhi); d["x"] = arr(t.x);
+    d["rh"] = arr(t.rh); d["ylo"] = arr(t.ylo); d["yhi"] = arr(t.yhi); d["y"] = arr(t.y);
+    return d;
+  });
+
+  // ---- decomposition ----
+  m.def("choose_process_grid", [](int size) {
+    const ProcGrid g = choose_process_grid(size);
+    return py::make_tuple(g.Px, g.Py);
+  });
+  m.def("make_process_grid", [](int size, int M, int N, Split split) {
+    const ProcGrid g = make_process_grid(size, M, N, split);
+    return py::make_tuple(g.Px, g.Py);
+  });
+  m.def("decompose_2d", [](int M, int N, int Px, int Py, int rank) {
+    return sd_dict(decompose_2d(M, N, ProcGrid{Px, Py}, rank));
+  });
+
+  // ---- CPU oracle ----
+  m.def("cpu_solve", [](const ProblemSpec& s, int threads, bool keep) {
+          SolveResult r;
+          { py::gil_scoped_release nogil; r = cpu_solve(s, threads, keep); }
+          return result_dict(r, s, keep);
+        }, py::arg("spec"), py::arg("threads") = 1, py::arg("keep_solution") = true);
+  m.def("cpu_solve_decomposed", [](const ProblemSpec& s, int nranks, Split split, int threads, bool keep) {
+          SolveResult r;
+          { py::gil_scoped_release nogil; r = cpu_solve_decomposed(s, nranks, split, threads, keep); }
+          return result_dict(r, s, keep);
+        }, py::arg("spec"), py::arg("nranks"), py::arg("split") = Split::kReference,
+        py::arg("threads") = 1, py::arg("keep_solution") = true);
+  m.def("cpu_assemble", [](const ProblemSpec& s) {
+    std::vector<double> a, b, B;
+    cpu_assemble(s, a, b, B);
+    return py::make_tuple(to_numpy(a, {s.M + 2, s.N + 2}), to_numpy(b, {s.M + 2, s.N + 2}),
+                          to_numpy(B, {s.M + 1, s.N + 1}));
+  });
+
+  // ---- GPU ----
+  m.def("device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) { (void)hipGetLastError(); return 0; }
+    return n;
+  });
+  m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+  m.def("comm_layout", [](int M, int N, int Px, int Py, int rank, const std::string& dtype) {
+    const Subdomain sd = decompose_2d(M, N, ProcGrid{Px, Py}, rank);
+    return layout_dict(GpuSubdomainSolver::comm_layout(sd, dtype == "fp32" ? DType::kFp32 : DType::kFp64));
+  });
+  m.def("max_square_grid", [](double bytes_per_gpu, int gpus, const std::string& dtype, double reserve) {
+    return max_square_grid(bytes_per_gpu, gpus, dtype == "fp32" ? DType::kFp32 : DType::kFp64, reserve);
+  }, py::arg("bytes_per_gpu"), py::arg("gpus"), py::arg("dtype") = "fp64", py::arg("reserve") = 0.1);
+
+  py::class_<OpContext>(m, "OpContext")
+      .def(py::init<const ProblemSpec&, int, int, int, int64_t, int>(), py::arg("spec"),
+           py::arg("Px"), py::arg("Py"), py::arg("rank"), py::arg("pitch"), py::arg("device") = 0)
+      .def("subdomain", &OpContext::subdomain)
+      .def("assemble", &OpContext::assemble)
+      .def("apply_a", &OpContext::apply_a)
+      .def("precond", &OpContext::precond)
+      .def("dot", &OpContext::dot);
+
+  // Single subdomain solver on caller-chosen streams/arena (Python-orchestrated comm path).
+  py::class_<GpuSubdomainSolver>(m, "SubdomainSolver")
+      .def(py::init([](const ProblemSpec& s, int Px, int Py, int rank, int device, int block,
+                       int tile_rows, const std::string& dtype, bool exact, uintptr_t arena, bool check) {
+             const Subdomain sd = decompose_2d(s.M, s.N, ProcGrid{Px, Py}, rank);
+             return std::make_unique<GpuSubdomainSolver>(
+                 s, sd, make_options(device, block, tile_rows, dtype, exact, 0, check), arena);
+           }),
+           py::arg("spec"), py::arg("Px") = 1, py::arg("Py") = 1, py::arg("rank") = 0,
+           py::arg("device") = 0, py::arg("block") = 256, py::arg("tile_rows") = 64,
+           py::arg("dtype") = "fp64", py::arg("exact") = false, py::arg("arena") = 0,
+           py::arg("check") = false)
+      .def("enqueue_init", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_init(as_stream(s)); })
+      .def("enqueue_phase_a", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_phase_a(as_stream(s)); })
+      .def("enqueue_phase_b", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_phase_b(as_stream(s)); })
+      .def("read_state", [](GpuSubdomainSolver& g, uintptr_t s) { return state_dict(g.read_state(as_stream(s))); })
+      .def("download_w", [](GpuSubdomainSolver& g, uintptr_t s) {
+        return to_numpy(g.download_w(as_stream(s)), {g.sd().nx, g.sd().ny});
+      })
+      .def("download_field", [](GpuSubdomainSolver& g, int which, uintptr_t s) {
+        return to_numpy(g.download_field(which, as_stream(s)), {g.sd().nx + 2, g.sd().ny + 2});
+      })
+      .def("layout", [](GpuSubdomainSolver& g) { return layout_dict(g.layout()); })
+      .def("subdomain", [](GpuSubdomainSolver& g) { return sd_dict(g.sd()); })
+      .def_property_readonly("arena_ptr", &GpuSubdomainSolver::arena_ptr)
+      .def_property_readonly("device_bytes", &GpuSubdomainSolver::device_bytes)
+      .def_property_readonly("ntiles", [](GpuSubdomainSolver& g) { return g.tiles().ntiles(); });
+
+  py::class_<Session>(m, "Session")
+      .def(py::init([](const ProblemSpec& s, int world, const std::string& comm, Split split,
+                       int device, int block, int tile_rows, const std::string& dtype, bool exact,
+                       int graph_batch, bool check, py::object uid, std::vector<int> ranks,
+                       std::vector<int> devices, bool rccl_graph) {
+             SessionConfig c;
+             c.spec = s;
+             c.opt = make_options(device, block, tile_rows, dtype, exact, graph_batch, check);
+             c.split = split;
+             c.world = world;
+             if (comm == "self") c.comm = CommKind::kSelf;
+             else if (comm == "local") c.comm = CommKind::kLocal;
+             else if (comm == "rccl") c.comm = CommKind::kRccl;
+             else PMX_CHECK(false, "unknown comm " << comm);
+             if (!uid.is_none()) c.rccl_uid = uid.cast<std::string>();
+             c.ranks = ranks;
+             c.devices = devices;
+             c.rccl_graph = rccl_graph;
+             py::gil_scoped_release nogil;
+             return std::make_unique<Session>(c);
+           }),
+           py::arg("spec"), py::arg("world") = 1, py::arg("comm") = "self",
+           py::arg("split") = Split::kReference, py::arg("device") = 0, py::arg("block") = 256,
+           py::arg("tile_rows") = 64, py::arg("dtype") = "fp64", py::arg("exact") = false,
+           py::arg("graph_batch") = 32, py::arg("check") = false, py::arg("uid") = py::none(),
+           py::arg("ranks") = std::vector<int>{}, py::arg("devices") = std::vector<int>{},
+           py::arg("rccl_graph") = false)
+      .def("init", [](Session& s) { py::gil_scoped_release g; s.init(); })
+      .def("step", [](Session& s, int64_t n) { py::gil_scoped_release g; s.step(n); })
+      .def("synchronize", [](Session& s) { py::gil_scoped_release g; s.synchronize(); })
+      .def("solve", [](Session& s, int poll) {
+             RunStats r;
+             { py::gil_scoped_release g; r = s.solve(poll); }
+             return stats_dict(r);
+           }, py::arg("poll_batches") = 1)
+      .def("profile", [](Session& s, int64_t n) {
+             RunStats r;
+             { py::gil_scoped_release g; r = s.profile(n); }
+             return stats_dict(r);
+           })
+      .def("state", [](Session& s, int i) { return state_dict(s.state(i)); }, py::arg("i") = 0)
+      .def("gather_local_w", [](Session& s) {
+             const auto& sp = s.solver(0).spec();
+             return to_numpy(s.gather_local_w(), {sp.M + 1, sp.N + 1});
+           })
+      .def("subdomain", [](Session& s, int i) { return sd_dict(s.solver(i).sd()); }, py::arg("i") = 0)
+      .def_property_readonly("num_local", &Session::num_local)
+      .def_property_readonly("comm_name", &Session::comm_name)
+      .def_property_readonly("device_bytes", &Session::device_bytes)
+      .def_property_readonly("grid", [](Session& s) { return py::make_tuple(s.grid().Px, s.grid().Py); })
+      .def_property_readonly("ntiles", [](Session& s) { return s.solver(0).tiles().ntiles(); });
+}

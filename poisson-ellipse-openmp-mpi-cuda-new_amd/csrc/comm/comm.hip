@@ -1,0 +1,172 @@
+// Communication backends for the GPU PCG (§5.8).
+//
+// Reference: host-staged halos (cudaMemcpy D2H -> blocking MPI_Sendrecv -> H2D, re-allocated
+// pageable buffers every call: stage4-mpi+cuda/poisson_mpi_cuda_f.cu:331-500) and three 8-byte
+// MPI_Allreduce per iteration (:843,872,893,926).
+//
+// Here:
+//  * RcclComm  — RCCL over xGMI straight from device buffers: ncclSend/ncclRecv pairs inside one
+//                ncclGroup for the 4 halo sides (edges packed by k_pcg_b), and two in-place
+//                ncclAllReduce per iteration (1 double, then (sum dw^2, (z,r)) packed into one
+//                16-byte all-reduce).  Graph-capturable.
+//  * LocalComm — P subdomains in one process on one device: halos are D2D copies, the
+//                all-reduce is a deterministic rank-ordered sum kernel.  The fake cluster used to
+//                test multi-rank logic on a 1-GPU box.
+//  * SelfComm  — P = 1.
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <sstream>
+
+#include "pmx/common.hpp"
+#include "pmx/gpu_solver.hpp"
+
+#define RCCL_CHECK(expr)                                                                \
+  do {                                                                                  \
+    ncclResult_t pmx_r_ = (expr);                                                       \
+    if (pmx_r_ != ncclSuccess)                                                          \
+      ::pmx::fail(__FILE__, __LINE__, std::string(#expr " -> ") + ncclGetErrorString(pmx_r_)); \
+  } while (0)
+
+namespace pmx {
+
+namespace {
+
+class SelfComm final : public Comm {
+ public:
+  void allreduce(std::vector<GpuSubdomainSolver*>&, int, std::vector<hipStream_t>&) override {}
+  void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>&) override {
+    for (auto* s : local) PMX_CHECK(s->geom().nb == 0, "SelfComm used with a decomposed grid");
+  }
+  std::string name() const override { return "self"; }
+  int world_size() const override { return 1; }
+};
+
+class LocalComm final : public Comm {
+ public:
+  explicit LocalComm(std::vector<GpuSubdomainSolver*>& local) : n_(int(local.size())) {
+    const int dev = local[0]->device();
+    for (size_t i = 0; i < local.size(); ++i) {
+      PMX_CHECK(local[i]->device() == dev, "LocalComm needs every subdomain on one device");
+      PMX_CHECK(local[i]->sd().rank == int(i), "LocalComm needs local[i].rank == i");
+    }
+    HIP_CHECK(hipSetDevice(dev));
+    std::vector<double*> a, b;
+    for (auto* s : local) { a.push_back(s->red_a_dev()); b.push_back(s->red_b_dev()); }
+    HIP_CHECK(hipMalloc(&ptrs_, 2 * n_ * sizeof(double*)));
+    HIP_CHECK(hipMemcpy(ptrs_, a.data(), n_ * sizeof(double*), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(ptrs_ + n_, b.data(), n_ * sizeof(double*), hipMemcpyHostToDevice));
+  }
+  ~LocalComm() override { if (ptrs_) (void)hipFree(ptrs_); }
+
+  void allreduce(std::vector<GpuSubdomainSolver*>&, int which,
+                 std::vector<hipStream_t>& streams) override {
+    if (n_ == 1) return;
+    launch_local_allreduce(ptrs_ + (which ? n_ : 0), n_, which ? 2 : 1, streams[0]);
+  }
+  void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>& streams) override {
+    for (auto* s : local) {
+      const Subdomain& sd = s->sd();
+      const int nb[4] = {sd.nb_xlo, sd.nb_xhi, sd.nb_ylo, sd.nb_yhi};
+      const CommLayout& L = s->layout();
+      for (int side = 0; side < 4; ++side) {
+        if (nb[side] < 0) continue;
+        GpuSubdomainSolver* o = local[nb[side]];
+        HIP_CHECK(hipMemcpyAsync(s->recv_dev(side), o->send_dev(side ^ 1),
+                                 size_t(L.edge_len[side]) * L.elem, hipMemcpyDeviceToDevice,
+                                 streams[0]));
+      }
+    }
+  }
+  std::string name() const override { return "local"; }
+  int world_size() const override { return n_; }
+
+ private:
+  int n_;
+  double** ptrs_ = nullptr;
+};
+
+class RcclComm final : public Comm {
+ public:
+  RcclComm(const std::string& uid, int nranks, const std::vector<int>& ranks,
+           const std::vector<int>& devices, bool capturable)
+      : nranks_(nranks), capturable_(capturable) {
+    PMX_CHECK(uid.size() == sizeof(ncclUniqueId), "bad ncclUniqueId size " << uid.size());
+    PMX_CHECK(ranks.size() == devices.size() && !ranks.empty(), "ranks/devices mismatch");
+    ncclUniqueId id;
+    std::memcpy(&id, uid.data(), sizeof(id));
+    comms_.resize(ranks.size());
+    if (ranks.size() == 1) {
+      HIP_CHECK(hipSetDevice(devices[0]));
+      RCCL_CHECK(ncclCommInitRank(&comms_[0], nranks, id, ranks[0]));
+    } else {
+      RCCL_CHECK(ncclGroupStart());
+      for (size_t i = 0; i < ranks.size(); ++i) {
+        HIP_CHECK(hipSetDevice(devices[i]));
+        RCCL_CHECK(ncclCommInitRank(&comms_[i], nranks, id, ranks[i]));
+      }
+      RCCL_CHECK(ncclGroupEnd());
+    }
+  }
+  ~RcclComm() override {
+    for (auto c : comms_) (void)ncclCommDestroy(c);
+  }
+
+  void allreduce(std::vector<GpuSubdomainSolver*>& local, int which,
+                 std::vector<hipStream_t>& streams) override {
+    RCCL_CHECK(ncclGroupStart());
+    for (size_t i = 0; i < local.size(); ++i) {
+      double* buf = which ? local[i]->red_b_dev() : local[i]->red_a_dev();
+      RCCL_CHECK(ncclAllReduce(buf, buf, which ? 2 : 1, ncclFloat64, ncclSum, comms_[i], streams[i]));
+    }
+    RCCL_CHECK(ncclGroupEnd());
+  }
+
+  void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>& streams) override {
+    RCCL_CHECK(ncclGroupStart());
+    for (size_t i = 0; i < local.size(); ++i) {
+      GpuSubdomainSolver* s = local[i];
+      const Subdomain& sd = s->sd();
+      const int nb[4] = {sd.nb_xlo, sd.nb_xhi, sd.nb_ylo, sd.nb_yhi};
+      const CommLayout& L = s->layout();
+      const ncclDataType_t t = L.elem == 8 ? ncclFloat64 : ncclFloat32;
+      for (int side = 0; side < 4; ++side) {
+        if (nb[side] < 0) continue;
+        RCCL_CHECK(ncclSend(s->send_dev(side), L.edge_len[side], t, nb[side], comms_[i], streams[i]));
+        RCCL_CHECK(ncclRecv(s->recv_dev(side), L.edge_len[side], t, nb[side], comms_[i], streams[i]));
+      }
+    }
+    RCCL_CHECK(ncclGroupEnd());
+  }
+
+  bool graph_capturable() const override { return capturable_; }
+  std::string name() const override { return "rccl"; }
+  int world_size() const override { return nranks_; }
+
+ private:
+  int nranks_;
+  bool capturable_;
+  std::vector<ncclComm_t> comms_;
+};
+
+}  // namespace
+
+std::unique_ptr<Comm> make_self_comm() { return std::make_unique<SelfComm>(); }
+
+std::unique_ptr<Comm> make_local_comm(std::vector<GpuSubdomainSolver*>& local) {
+  return std::make_unique<LocalComm>(local);
+}
+
+std::unique_ptr<Comm> make_rccl_comm(const std::string& unique_id, int nranks,
+                                     const std::vector<int>& ranks, const std::vector<int>& devices,
+                                     bool capturable) {
+  return std::make_unique<RcclComm>(unique_id, nranks, ranks, devices, capturable);
+}
+
+std::string rccl_unique_id() {
+  ncclUniqueId id;
+  RCCL_CHECK(ncclGetUniqueId(&id));
+  return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+}  // namespace pmx

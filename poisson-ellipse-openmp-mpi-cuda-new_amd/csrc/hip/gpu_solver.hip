@@ -1,0 +1,408 @@
+// GPU PCG orchestration.  See pmx/gpu_solver.hpp.
+//
+// Reference call stack being replaced (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:688-983): CPU
+// assembly + 3 H2D copies, 8 cudaMallocs, and per iteration 8 launches each followed by
+// cudaDeviceSynchronize, 3x256-KiB partial D2H copies with host summation, host-staged halos.
+// Here per iteration: 4 launches (2 streaming + 2 single-block reductions), zero host syncs,
+// replayed from a hipGraph in batches.
+#include <chrono>
+#include <cstring>
+
+#include "pmx/common.hpp"
+#include "pmx/gpu_solver.hpp"
+
+namespace pmx {
+
+namespace {
+size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+}  // namespace
+
+DevGeom make_dev_geom(const ProblemSpec& spec, const Subdomain& sd, int64_t pitch) {
+  const GridInfo g(spec);
+  DevGeom G{};
+  G.nx = sd.nx;
+  G.ny = sd.ny;
+  G.pitch = pitch;
+  G.gi0 = sd.gi0();
+  G.gj0 = sd.gj0();
+  G.M = spec.M;
+  G.N = spec.N;
+  G.nb = (sd.nb_xlo >= 0 ? kNbXlo : 0) | (sd.nb_xhi >= 0 ? kNbXhi : 0) |
+         (sd.nb_ylo >= 0 ? kNbYlo : 0) | (sd.nb_yhi >= 0 ? kNbYhi : 0);
+  G.ref_ellipse = spec.reference_ellipse() ? 1 : 0;
+  G.h1 = g.h1; G.h2 = g.h2; G.eps = g.eps; G.inv_eps = g.inv_eps; G.h1h2 = g.h1h2;
+  G.cx = 1.0 / (g.h1 * g.h1);
+  G.cy = 1.0 / (g.h2 * g.h2);
+  G.ax = spec.ax; G.by = spec.by; G.F = spec.F;
+  return G;
+}
+
+DevTables upload_tables(const ProblemSpec& spec, double** owner) {
+  const GridInfo g(spec);
+  const geo::FaceTables ft(spec, g);
+  const size_t nxT = spec.M + 2, nyT = spec.N + 2;
+  HIP_CHECK(hipMalloc(owner, (4 * nxT + 4 * nyT) * sizeof(double)));
+  std::vector<double> host(4 * nxT + 4 * nyT);
+  double* h = host.data();
+  std::memcpy(h + 0 * nxT, ft.rv.data(), nxT * 8);
+  std::memcpy(h + 1 * nxT, ft.xlo.data(), nxT * 8);
+  std::memcpy(h + 2 * nxT, ft.xhi.data(), nxT * 8);
+  std::memcpy(h + 3 * nxT, ft.x.data(), nxT * 8);
+  double* hy = h + 4 * nxT;
+  std::memcpy(hy + 0 * nyT, ft.rh.data(), nyT * 8);
+  std::memcpy(hy + 1 * nyT, ft.ylo.data(), nyT * 8);
+  std::memcpy(hy + 2 * nyT, ft.yhi.data(), nyT * 8);
+  std::memcpy(hy + 3 * nyT, ft.y.data(), nyT * 8);
+  HIP_CHECK(hipMemcpy(*owner, host.data(), host.size() * 8, hipMemcpyHostToDevice));
+  const double* d = *owner;
+  const double* dy = d + 4 * nxT;
+  return DevTables{d, d + nxT, d + 2 * nxT, d + 3 * nxT, dy, dy + nyT, dy + 2 * nyT, dy + 3 * nyT};
+}
+
+CommLayout GpuSubdomainSolver::comm_layout(const Subdomain& sd, DType dtype) {
+  CommLayout L;
+  L.elem = dtype == DType::kFp64 ? 8 : 4;
+  size_t off = 0;
+  L.state_off = 0;
+  off = round_up(sizeof(PcgState), 256);
+  for (int s = 0; s < 4; ++s) {
+    L.edge_len[s] = s < 2 ? sd.ny : sd.nx;
+    L.send_off[s] = off;
+    off = round_up(off + L.edge_len[s] * L.elem, 256);
+  }
+  for (int s = 0; s < 4; ++s) {
+    L.recv_off[s] = off;
+    off = round_up(off + L.edge_len[s] * L.elem, 256);
+  }
+  L.bytes = off;
+  return L;
+}
+
+GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain& sd,
+                                       const GpuOptions& opt, uintptr_t external_arena)
+    : spec_(spec), sd_(sd), opt_(opt), g_(spec) {
+  spec.validate();
+  PMX_CHECK(sd.nx >= 1 && sd.ny >= 1, "empty subdomain");
+  HIP_CHECK(hipSetDevice(opt.device));
+  elem_ = opt.dtype == DType::kFp64 ? 8 : 4;
+  const size_t align_elems = 256 / elem_;
+
+  geom_ = make_dev_geom(spec, sd, int64_t(round_up(size_t(sd.ny + 2), align_elems)));
+  const DevGeom& G = geom_;
+
+  // fields: element (li, lj) at base[li*pitch + lj]; base = alloc + (align-1) so that every
+  // interior row starts 256-B aligned (lj = 1)
+  field_off_ = align_elems - 1;
+  field_bytes_ = round_up((field_off_ + size_t(sd.nx + 2) * G.pitch) * elem_, 256);
+  HIP_CHECK(hipMalloc(&fields_, 4 * field_bytes_));
+
+  // 1D face tables
+  tables_ = upload_tables(spec, &tables_buf_);
+
+  tiles_ = make_tiles(G, opt.block, opt.tile_rows);
+  HIP_CHECK(hipMalloc(&partials_, size_t(tiles_.ntiles()) * 2 * sizeof(double)));
+
+  layout_ = comm_layout(sd, opt.dtype);
+  if (external_arena) {
+    arena_ = reinterpret_cast<char*>(external_arena);
+    own_arena_ = false;
+    PMX_CHECK(external_arena % 256 == 0, "external comm arena must be 256-B aligned");
+  } else {
+    HIP_CHECK(hipMalloc(&arena_, layout_.bytes));
+    own_arena_ = true;
+  }
+  HIP_CHECK(hipMemset(arena_, 0, layout_.bytes));
+  state_ = reinterpret_cast<PcgState*>(arena_ + layout_.state_off);
+  HIP_CHECK(hipHostMalloc(&host_state_, 2 * sizeof(PcgState), hipHostMallocDefault));
+}
+
+GpuSubdomainSolver::~GpuSubdomainSolver() {
+  (void)hipSetDevice(opt_.device);
+  (void)hipDeviceSynchronize();
+  if (fields_) (void)hipFree(fields_);
+  if (tables_buf_) (void)hipFree(tables_buf_);
+  if (partials_) (void)hipFree(partials_);
+  if (own_arena_ && arena_) (void)hipFree(arena_);
+  if (host_state_) (void)hipHostFree(host_state_);
+}
+
+size_t GpuSubdomainSolver::device_bytes() const {
+  return 4 * field_bytes_ + (4 * (spec_.M + 2) + 4 * (spec_.N + 2)) * sizeof(double) +
+         size_t(tiles_.ntiles()) * 2 * sizeof(double) + (own_arena_ ? layout_.bytes : 0);
+}
+
+void* GpuSubdomainSolver::field_base(int which) const {
+  PMX_CHECK(which >= 0 && which < 4, "field index");
+  return fields_ + which * field_bytes_ + field_off_ * elem_;
+}
+
+template <typename T>
+HaloBufs<T> GpuSubdomainSolver::halo() const {
+  HaloBufs<T> H;
+  for (int s = 0; s < 4; ++s) {
+    H.send[s] = reinterpret_cast<T*>(arena_ + layout_.send_off[s]);
+    H.recv[s] = reinterpret_cast<T*>(arena_ + layout_.recv_off[s]);
+  }
+  return H;
+}
+
+void GpuSubdomainSolver::after_launch(hipStream_t s) const {
+  if (opt_.check) {
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(s));
+  }
+}
+
+template <typename T>
+void GpuSubdomainSolver::init_impl(hipStream_t s) {
+  HIP_CHECK(hipMemsetAsync(fields_, 0, 4 * field_bytes_, s));
+  HIP_CHECK(hipMemsetAsync(arena_, 0, layout_.bytes, s));
+  PcgState& st = host_state_[1];  // template (never rewritten while a copy is in flight)
+  std::memset(&st, 0, sizeof(st));
+  st.delta = spec_.delta;
+  st.it = 1;
+  st.max_iter = spec_.effective_max_iter();
+  st.norm = int(spec_.norm);
+  HIP_CHECK(hipMemcpyAsync(state_, &st, sizeof(PcgState), hipMemcpyHostToDevice, s));
+  T* w = static_cast<T*>(field_base(0));
+  T* r = static_cast<T*>(field_base(1));
+  launch_init<T>(geom_, tables_, w, r, halo<T>(), partials_, tiles_, s);
+  after_launch(s);
+  launch_reduce(partials_, tiles_.ntiles(), 2, 0.0, g_.h1h2, state_->red_b, state_, 0, s);
+  after_launch(s);
+}
+
+template <typename T>
+void GpuSubdomainSolver::phase_a_impl(hipStream_t s) {
+  launch_pcg_a<T>(geom_, tables_, static_cast<const T*>(field_base(1)),
+                  static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(),
+                  partials_, state_, tiles_, opt_.exact, s);
+  after_launch(s);
+  launch_reduce(partials_, tiles_.ntiles(), 1, g_.h1h2, 0.0, state_->red_a, state_, kSkipIfDone, s);
+  after_launch(s);
+}
+
+template <typename T>
+void GpuSubdomainSolver::phase_b_impl(hipStream_t s) {
+  launch_pcg_b<T>(geom_, tables_, static_cast<T*>(field_base(0)), static_cast<T*>(field_base(1)),
+                  static_cast<const T*>(field_base(2)), static_cast<const T*>(field_base(3)),
+                  halo<T>(), partials_, state_, tiles_, opt_.exact, s);
+  after_launch(s);
+  const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
+  launch_reduce(partials_, tiles_.ntiles(), 2, wdiff, g_.h1h2, state_->red_b, state_,
+                kSkipIfDone | kBumpIter, s);
+  after_launch(s);
+}
+
+void GpuSubdomainSolver::enqueue_init(hipStream_t s) {
+  HIP_CHECK(hipSetDevice(opt_.device));
+  if (opt_.dtype == DType::kFp64) init_impl<double>(s); else init_impl<float>(s);
+}
+void GpuSubdomainSolver::enqueue_phase_a(hipStream_t s) {
+  if (opt_.dtype == DType::kFp64) phase_a_impl<double>(s); else phase_a_impl<float>(s);
+}
+void GpuSubdomainSolver::enqueue_phase_b(hipStream_t s) {
+  if (opt_.dtype == DType::kFp64) phase_b_impl<double>(s); else phase_b_impl<float>(s);
+}
+
+PcgState GpuSubdomainSolver::read_state(hipStream_t s) const {
+  HIP_CHECK(hipSetDevice(opt_.device));
+  HIP_CHECK(hipMemcpyAsync(&host_state_[0], state_, sizeof(PcgState), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  return host_state_[0];
+}
+
+std::vector<double> GpuSubdomainSolver::download_field(int which, hipStream_t s) const {
+  HIP_CHECK(hipSetDevice(opt_.device));
+  const size_t n = size_t(sd_.nx + 2) * geom_.pitch;
+  std::vector<char> raw(n * elem_);
+  HIP_CHECK(hipMemcpyAsync(raw.data(), field_base(which), raw.size(), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  std::vector<double> out(size_t(sd_.nx + 2) * (sd_.ny + 2));
+  for (int li = 0; li <= sd_.nx + 1; ++li)
+    for (int lj = 0; lj <= sd_.ny + 1; ++lj) {
+      const size_t src = size_t(li) * geom_.pitch + lj;
+      out[size_t(li) * (sd_.ny + 2) + lj] =
+          elem_ == 8 ? reinterpret_cast<const double*>(raw.data())[src]
+                     : double(reinterpret_cast<const float*>(raw.data())[src]);
+    }
+  return out;
+}
+
+std::vector<double> GpuSubdomainSolver::download_w(hipStream_t s) const {
+  const std::vector<double> f = download_field(0, s);
+  std::vector<double> out(size_t(sd_.nx) * sd_.ny);
+  for (int li = 1; li <= sd_.nx; ++li)
+    for (int lj = 1; lj <= sd_.ny; ++lj)
+      out[size_t(li - 1) * sd_.ny + (lj - 1)] = f[size_t(li) * (sd_.ny + 2) + lj];
+  return out;
+}
+
+// ---------------------------------------------------------------------------
+// PcgDriver
+// ---------------------------------------------------------------------------
+PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int graph_batch)
+    : local_(std::move(local)), comm_(comm), graph_batch_(graph_batch) {
+  PMX_CHECK(!local_.empty(), "no local subdomains");
+  bool same_device = true;
+  for (auto* s : local_) same_device &= s->device() == local_[0]->device();
+  const size_t nstreams = same_device ? 1 : local_.size();
+  for (size_t i = 0; i < nstreams; ++i) {
+    HIP_CHECK(hipSetDevice(local_[i]->device()));
+    hipStream_t st;
+    HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    streams_.push_back(st);
+  }
+  if (same_device) streams_.resize(local_.size(), streams_[0]);
+}
+
+PcgDriver::~PcgDriver() {
+  for (auto e : execs_) (void)hipGraphExecDestroy(e);
+  for (auto g : graphs_) (void)hipGraphDestroy(g);
+  hipStream_t last = nullptr;
+  for (auto s : streams_) {
+    if (s != last) (void)hipStreamDestroy(s);
+    last = s;
+  }
+}
+
+void PcgDriver::synchronize() {
+  hipStream_t last = nullptr;
+  for (size_t i = 0; i < streams_.size(); ++i) {
+    if (streams_[i] == last) continue;
+    HIP_CHECK(hipSetDevice(local_[i]->device()));
+    HIP_CHECK(hipStreamSynchronize(streams_[i]));
+    last = streams_[i];
+  }
+}
+
+void PcgDriver::init() {
+  for (size_t i = 0; i < local_.size(); ++i) local_[i]->enqueue_init(streams_[i]);
+  comm_->allreduce(local_, 1, streams_);
+  comm_->halo(local_, streams_);
+  synchronize();
+}
+
+void PcgDriver::enqueue_one_iteration() {
+  for (size_t i = 0; i < local_.size(); ++i) {
+    HIP_CHECK(hipSetDevice(local_[i]->device()));
+    local_[i]->enqueue_phase_a(streams_[i]);
+  }
+  comm_->allreduce(local_, 0, streams_);
+  for (size_t i = 0; i < local_.size(); ++i) {
+    HIP_CHECK(hipSetDevice(local_[i]->device()));
+    local_[i]->enqueue_phase_b(streams_[i]);
+  }
+  comm_->allreduce(local_, 1, streams_);
+  comm_->halo(local_, streams_);
+}
+
+void PcgDriver::build_graph() {
+  graph_ok_ = false;
+  bool single_stream = true;
+  for (auto s : streams_) single_stream &= s == streams_[0];
+  if (graph_batch_ <= 0 || !single_stream || !comm_->graph_capturable()) return;
+  for (auto* s : local_)
+    if (s->options().check) return;
+  HIP_CHECK(hipSetDevice(local_[0]->device()));
+  hipGraph_t g = nullptr;
+  if (hipStreamBeginCapture(streams_[0], hipStreamCaptureModeThreadLocal) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
+  for (int k = 0; k < graph_batch_; ++k) enqueue_one_iteration();
+  if (hipStreamEndCapture(streams_[0], &g) != hipSuccess || !g) {
+    (void)hipGetLastError();
+    return;
+  }
+  hipGraphExec_t e = nullptr;
+  if (hipGraphInstantiate(&e, g, nullptr, nullptr, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipGraphDestroy(g);
+    return;
+  }
+  graphs_.push_back(g);
+  execs_.push_back(e);
+  graph_ok_ = true;
+}
+
+void PcgDriver::enqueue_iterations(int64_t n) {
+  if (graph_batch_ > 0 && execs_.empty()) build_graph();
+  int64_t done = 0;
+  if (graph_ok_) {
+    for (; done + graph_batch_ <= n; done += graph_batch_)
+      HIP_CHECK(hipGraphLaunch(execs_[0], streams_[0]));
+  }
+  for (; done < n; ++done) enqueue_one_iteration();
+}
+
+PcgState PcgDriver::state(int idx) {
+  return local_[idx]->read_state(streams_[idx]);
+}
+
+RunStats PcgDriver::solve(int poll_batches) {
+  RunStats st;
+  const double t0 = now_s();
+  init();
+  const double t1 = now_s();
+  st.init_seconds = t1 - t0;
+  const int64_t batch = std::max(1, graph_batch_ > 0 ? graph_batch_ : 16) * std::max(1, poll_batches);
+  const int64_t max_iter = local_[0]->spec().effective_max_iter();
+  PcgState s{};
+  while (true) {
+    enqueue_iterations(batch);
+    st.launched += batch;
+    s = state(0);
+    if (s.done) break;
+    PMX_CHECK(st.launched <= max_iter + 2 * batch, "device stop flag never raised");
+  }
+  synchronize();
+  st.solve_seconds = now_s() - t1;
+  st.iters = s.iters;
+  st.status = Status(s.status);
+  st.diff = s.diff;
+  st.nan = s.nan_flag != 0;
+  return st;
+}
+
+RunStats PcgDriver::profile_phases(int64_t n) {
+  RunStats st;
+  HIP_CHECK(hipSetDevice(local_[0]->device()));
+  hipStream_t s0 = streams_[0];
+  const int kEv = 5;
+  std::vector<hipEvent_t> ev(size_t(n) * kEv);
+  for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+  for (int64_t k = 0; k < n; ++k) {
+    hipEvent_t* e = &ev[size_t(k) * kEv];
+    HIP_CHECK(hipEventRecord(e[0], s0));
+    for (size_t i = 0; i < local_.size(); ++i) local_[i]->enqueue_phase_a(streams_[i]);
+    HIP_CHECK(hipEventRecord(e[1], s0));
+    comm_->allreduce(local_, 0, streams_);
+    HIP_CHECK(hipEventRecord(e[2], s0));
+    for (size_t i = 0; i < local_.size(); ++i) local_[i]->enqueue_phase_b(streams_[i]);
+    HIP_CHECK(hipEventRecord(e[3], s0));
+    comm_->allreduce(local_, 1, streams_);
+    comm_->halo(local_, streams_);
+    HIP_CHECK(hipEventRecord(e[4], s0));
+  }
+  synchronize();
+  auto ms = [](hipEvent_t a, hipEvent_t b) {
+    float v = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&v, a, b));
+    return double(v) * 1e-3;
+  };
+  for (int64_t k = 0; k < n; ++k) {
+    hipEvent_t* e = &ev[size_t(k) * kEv];
+    st.t_kernel_a += ms(e[0], e[1]);
+    st.t_comm += ms(e[1], e[2]) + ms(e[3], e[4]);
+    st.t_kernel_b += ms(e[2], e[3]);
+  }
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  st.launched = n;
+  return st;
+}
+
+}  // namespace pmx

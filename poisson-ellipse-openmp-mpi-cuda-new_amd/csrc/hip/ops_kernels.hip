@@ -1,0 +1,120 @@
+// Unfused device ops: assembly, operator A, preconditioner, dot partials.
+//
+// They mirror the reference's one-op-per-kernel structure (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:
+// apply_A_kernel :507-536, apply_Dinv_kernel :541-562, dot_kernel :574-598) but with the
+// CDNA-friendly mapping: threadIdx.x runs along the contiguous axis lj (the reference maps it to
+// the strided li axis, :514-515), and coefficients come from the 1D face tables.  Used by the
+// unit tests (each op vs a PyTorch fp64 reference) and by the solver's `naive` kernel mode.
+#include "pcg_device.hpp"
+#include "pmx/common.hpp"
+#include "pmx/kernels.hpp"
+
+namespace pmx {
+
+using namespace dev;
+
+__global__ void __launch_bounds__(256)
+k_assemble(DevGeom G, DevTables Tb, double* a, double* b, double* B, int64_t pab) {
+  const int lj = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int li = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (li > G.nx + 1 || lj > G.ny + 1) return;
+  const int gi = G.gi0 + li, gj = G.gj0 + lj;
+  a[li * pab + lj] = coef_a(Tb, G, gi, gj);
+  b[li * pab + lj] = coef_b(Tb, G, gi, gj);
+  const bool interior = li >= 1 && li <= G.nx && lj >= 1 && lj <= G.ny;
+  B[li * pab + lj] =
+      interior && geo::inside(Tb.x[gi], Tb.y[gj], G.ax, G.by, G.ref_ellipse != 0) ? G.F : 0.0;
+}
+
+template <typename T, bool EXACT>
+__global__ void __launch_bounds__(256)
+k_apply_a(DevGeom G, DevTables Tb, const T* __restrict__ p, T* __restrict__ Ap) {
+  const int lj = 1 + blockIdx.x * 64 + (threadIdx.x & 63);
+  const int li = 1 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (li > G.nx || lj > G.ny) return;
+  const int gi = G.gi0 + li, gj = G.gj0 + lj;
+  const int64_t c = li * G.pitch + lj;
+  const double a0 = coef_a(Tb, G, gi, gj), a1 = coef_a(Tb, G, gi + 1, gj);
+  const double b0 = coef_b(Tb, G, gi, gj), b1 = coef_b(Tb, G, gi, gj + 1);
+  Ap[c] = static_cast<T>(apply_a<EXACT>(double(p[c]), double(p[c - G.pitch]),
+                                        double(p[c + G.pitch]), double(p[c - 1]),
+                                        double(p[c + 1]), a0, a1, b0, b1, G));
+}
+
+template <typename T, bool EXACT>
+__global__ void __launch_bounds__(256)
+k_precond(DevGeom G, DevTables Tb, const T* __restrict__ r, T* __restrict__ z) {
+  const int lj = 1 + blockIdx.x * 64 + (threadIdx.x & 63);
+  const int li = 1 + blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (li > G.nx || lj > G.ny) return;
+  const int gi = G.gi0 + li, gj = G.gj0 + lj;
+  const int64_t c = li * G.pitch + lj;
+  const double a0 = coef_a(Tb, G, gi, gj), a1 = coef_a(Tb, G, gi + 1, gj);
+  const double b0 = coef_b(Tb, G, gi, gj), b1 = coef_b(Tb, G, gi, gj + 1);
+  const double D = diag<EXACT>(a0, a1, b0, b1, G);
+  z[c] = static_cast<T>((D != 0.0) ? double(r[c]) / D : 0.0);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+k_dot_partials(DevGeom G, const T* __restrict__ x, const T* __restrict__ y, double* partials) {
+  __shared__ double lds[2 * 256 / kWave];
+  double s = 0.0, unused = 0.0;
+  const int64_t n = int64_t(G.nx) * G.ny;
+  for (int64_t k = int64_t(blockIdx.x) * 256 + threadIdx.x; k < n; k += int64_t(gridDim.x) * 256) {
+    const int li = int(k / G.ny) + 1, lj = int(k % G.ny) + 1;
+    const int64_t c = li * G.pitch + lj;
+    s += double(x[c]) * double(y[c]);
+  }
+  block_sum2<256>(s, unused, lds);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+void launch_assemble(const DevGeom& G, const DevTables& Tb, double* a, double* b, double* B,
+                     int64_t pab, hipStream_t s) {
+  dim3 grid((G.ny + 2 + 63) / 64, (G.nx + 2 + 3) / 4);
+  hipLaunchKernelGGL(k_assemble, grid, dim3(256), 0, s, G, Tb, a, b, B, pab);
+  HIP_CHECK(hipGetLastError());
+}
+
+template <typename T>
+void launch_apply_a(const DevGeom& G, const DevTables& Tb, const T* p, T* Ap, bool exact,
+                    hipStream_t s) {
+  dim3 grid((G.ny + 63) / 64, (G.nx + 3) / 4);
+  if (exact) hipLaunchKernelGGL((k_apply_a<T, true>), grid, dim3(256), 0, s, G, Tb, p, Ap);
+  else hipLaunchKernelGGL((k_apply_a<T, false>), grid, dim3(256), 0, s, G, Tb, p, Ap);
+  HIP_CHECK(hipGetLastError());
+}
+
+template <typename T>
+void launch_precond(const DevGeom& G, const DevTables& Tb, const T* r, T* z, bool exact,
+                    hipStream_t s) {
+  dim3 grid((G.ny + 63) / 64, (G.nx + 3) / 4);
+  if (exact) hipLaunchKernelGGL((k_precond<T, true>), grid, dim3(256), 0, s, G, Tb, r, z);
+  else hipLaunchKernelGGL((k_precond<T, false>), grid, dim3(256), 0, s, G, Tb, r, z);
+  HIP_CHECK(hipGetLastError());
+}
+
+template <typename T>
+int launch_dot_partials(const DevGeom& G, const T* x, const T* y, double* partials, int max_blocks,
+                        hipStream_t s) {
+  const int64_t n = int64_t(G.nx) * G.ny;
+  int blocks = int(std::min<int64_t>(max_blocks, (n + 255) / 256));
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL((k_dot_partials<T>), dim3(blocks), dim3(256), 0, s, G, x, y, partials);
+  HIP_CHECK(hipGetLastError());
+  return blocks;
+}
+
+#define PMX_INST(T)                                                                          \
+  template void launch_apply_a<T>(const DevGeom&, const DevTables&, const T*, T*, bool,     \
+                                  hipStream_t);                                              \
+  template void launch_precond<T>(const DevGeom&, const DevTables&, const T*, T*, bool,     \
+                                  hipStream_t);                                              \
+  template int launch_dot_partials<T>(const DevGeom&, const T*, const T*, double*, int,     \
+                                      hipStream_t);
+PMX_INST(double)
+PMX_INST(float)
+#undef PMX_INST
+
+}  // namespace pmx

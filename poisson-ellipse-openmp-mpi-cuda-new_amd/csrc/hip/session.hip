@@ -1,0 +1,77 @@
+// Session: decomposition + solvers + comm + driver.  See pmx/session.hpp.
+#include "pmx/session.hpp"
+
+#include <cmath>
+
+#include "pmx/common.hpp"
+
+namespace pmx {
+
+Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
+  cfg_.spec.validate();
+  PMX_CHECK(cfg_.world >= 1, "world size must be >= 1");
+  pg_ = make_process_grid(cfg_.world, cfg_.spec.M, cfg_.spec.N, cfg_.split);
+  if (cfg_.ranks.empty()) {
+    if (cfg_.comm == CommKind::kRccl) {
+      PMX_CHECK(false, "RCCL sessions must list the ranks they own");
+    }
+    for (int r = 0; r < cfg_.world; ++r) cfg_.ranks.push_back(r);
+  }
+  if (cfg_.devices.empty()) cfg_.devices.assign(cfg_.ranks.size(), cfg_.opt.device);
+  PMX_CHECK(cfg_.devices.size() == cfg_.ranks.size(), "one device per owned rank");
+  if (cfg_.comm == CommKind::kSelf)
+    PMX_CHECK(cfg_.world == 1, "self comm needs world == 1 (use local or rccl)");
+  if (cfg_.comm == CommKind::kLocal)
+    PMX_CHECK(int(cfg_.ranks.size()) == cfg_.world, "local comm owns every rank");
+
+  std::vector<GpuSubdomainSolver*> raw;
+  for (size_t i = 0; i < cfg_.ranks.size(); ++i) {
+    GpuOptions o = cfg_.opt;
+    o.device = cfg_.devices[i];
+    const Subdomain sd = decompose_2d(cfg_.spec.M, cfg_.spec.N, pg_, cfg_.ranks[i]);
+    solvers_.push_back(std::make_unique<GpuSubdomainSolver>(cfg_.spec, sd, o));
+    raw.push_back(solvers_.back().get());
+  }
+  switch (cfg_.comm) {
+    case CommKind::kSelf: comm_ = make_self_comm(); break;
+    case CommKind::kLocal: comm_ = make_local_comm(raw); break;
+    case CommKind::kRccl:
+      comm_ = make_rccl_comm(cfg_.rccl_uid, cfg_.world, cfg_.ranks, cfg_.devices, cfg_.rccl_graph);
+      break;
+  }
+  driver_ = std::make_unique<PcgDriver>(raw, comm_.get(), cfg_.opt.graph_batch);
+}
+
+Session::~Session() {
+  driver_.reset();
+  comm_.reset();
+  solvers_.clear();
+}
+
+size_t Session::device_bytes() const {
+  size_t b = 0;
+  for (auto& s : solvers_) b += s->device_bytes();
+  return b;
+}
+
+std::vector<double> Session::gather_local_w() {
+  const int M = cfg_.spec.M, N = cfg_.spec.N;
+  std::vector<double> g(size_t(M + 1) * (N + 1), 0.0);
+  for (size_t i = 0; i < solvers_.size(); ++i) {
+    auto& s = *solvers_[i];
+    const Subdomain& sd = s.sd();
+    const std::vector<double> w = s.download_w(driver_->streams()[i]);
+    for (int li = 1; li <= sd.nx; ++li)
+      for (int lj = 1; lj <= sd.ny; ++lj)
+        g[size_t(sd.gi0() + li) * (N + 1) + sd.gj0() + lj] = w[size_t(li - 1) * sd.ny + lj - 1];
+  }
+  return g;
+}
+
+int64_t max_square_grid(double bytes_per_gpu, int gpus, DType dtype, double reserve_fraction) {
+  const double bpp = 4.0 * (dtype == DType::kFp64 ? 8.0 : 4.0) * 1.01;  // +pitch padding
+  const double pts = bytes_per_gpu * (1.0 - reserve_fraction) * gpus / bpp;
+  return int64_t(std::floor(std::sqrt(pts)));
+}
+
+}  // namespace pmx

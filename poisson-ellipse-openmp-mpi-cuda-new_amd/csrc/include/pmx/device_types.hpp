@@ -1,0 +1,61 @@
+// Plain-old-data structs shared by host orchestration and HIP kernels.
+#pragma once
+
+#include <cstdint>
+
+namespace pmx {
+
+// Device pointers to the 1D face tables of pmx/geometry.hpp, indexed by GLOBAL node index.
+struct DevTables {
+  const double* rv;   // vertical-face clip root at x_i - h1/2   (M+2)
+  const double* xlo;  // x_i - h1/2                               (M+2)
+  const double* xhi;  // x_i + h1/2                               (M+2)
+  const double* x;    // x_i                                      (M+2)
+  const double* rh;   // horizontal-face clip root at y_j - h2/2  (N+2)
+  const double* ylo;  // y_j - h2/2                               (N+2)
+  const double* yhi;  // y_j + h2/2                               (N+2)
+  const double* y;    // y_j                                      (N+2)
+};
+
+enum NbBits : int { kNbXlo = 1, kNbXhi = 2, kNbYlo = 4, kNbYhi = 8 };
+
+// One subdomain's geometry as seen by a kernel.  Local node (li, lj), li = 0..nx+1,
+// lj = 0..ny+1, lives at field[li * pitch + lj]; global index gi = gi0 + li.
+struct DevGeom {
+  int nx, ny;
+  int64_t pitch;
+  int gi0, gj0;
+  int M, N;
+  int nb;  // NbBits: neighbour exists on that side (else Dirichlet ghost)
+  int ref_ellipse;
+  double h1, h2, eps, inv_eps, h1h2;
+  double cx, cy;  // 1/h1^2, 1/h2^2
+  double ax, by, F;
+};
+
+// Device-resident PCG scalars.  The host never reads these inside the loop; it
+// polls `done` once per graph batch (SURVEY §7.1 "graphs + predication").
+struct alignas(64) PcgState {
+  double red_a[2];   // [0] = (Ap,p) (weighted).  All-reduce buffer A.
+  double red_b[2];   // [0] = sum dw^2 (weighted per norm), [1] = (z,r).  All-reduce buffer B.
+  double zr[2];      // zr_m stored at slot m & 1
+  double diff;       // last ||w^{k+1} - w^k||
+  double delta;      // tolerance
+  long long it;      // iteration currently executing (1-based)
+  long long max_iter;
+  long long iters;   // final iteration count (valid when done)
+  int done;
+  int status;        // pmx::Status
+  int norm;          // pmx::Norm
+  int nan_flag;      // set when a reduction produced NaN/Inf (failure detection)
+};
+
+// Pointers for the halo ("ghost") exchange of r.  Side order: 0 x-lo, 1 x-hi, 2 y-lo, 3 y-hi.
+// send[s]/recv[s] hold edge_len(s) values (ny for x sides, nx for y sides).
+template <typename T>
+struct HaloBufs {
+  T* send[4];
+  T* recv[4];
+};
+
+}  // namespace pmx

@@ -1,0 +1,185 @@
+// GPU PCG: per-subdomain device state + the host orchestrator
+// (components C9, X1-X4, P3/P4/P6 of SURVEY §2; replaces gradient_solver_mpi,
+// stage4-mpi+cuda/poisson_mpi_cuda_f.cu:688-983).
+//
+// * GpuSubdomainSolver owns one subdomain's fields on one device: w, r and a ping-pong pair
+//   p0/p1 (4 arrays, 32 B/pt in fp64), the 1D face tables, the block-partials scratch and a
+//   "comm arena" holding the PcgState scalars (the all-reduce buffers) and the packed
+//   send/recv halo buffers.  The arena may be supplied externally (e.g. a torch tensor) so a
+//   Python-side communicator can operate on it.
+// * PcgDriver steps a set of local subdomains through the PCG iteration with a Comm backend,
+//   optionally replaying hipGraph-captured batches of iterations.  The host never waits per
+//   iteration: the stop test runs on the device and later launches become no-ops.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "pmx/decomp.hpp"
+#include "pmx/device_types.hpp"
+#include "pmx/geometry.hpp"
+#include "pmx/kernels.hpp"
+#include "pmx/spec.hpp"
+
+namespace pmx {
+
+enum class DType : int { kFp64 = 0, kFp32 = 1 };
+
+// Kernel-side view of a subdomain whose fields use row pitch `pitch` (elements).
+DevGeom make_dev_geom(const ProblemSpec& spec, const Subdomain& sd, int64_t pitch);
+// Upload the 1D face tables (pmx/geometry.hpp) to the current device; *owner receives the
+// allocation (caller frees).
+DevTables upload_tables(const ProblemSpec& spec, double** owner);
+
+struct GpuOptions {
+  int device = 0;
+  int block = 256;        // tile width (threads per workgroup)
+  int tile_rows = 64;     // tile height (marching length)
+  DType dtype = DType::kFp64;
+  bool exact = false;     // reference arithmetic order inside the fused kernels
+  int graph_batch = 32;   // iterations per captured hipGraph (0 = eager launches)
+  bool check = false;     // PMX_CHECK mode: synchronise + error-check after every launch
+};
+
+struct CommLayout {
+  size_t state_off = 0;          // PcgState
+  size_t send_off[4] = {0, 0, 0, 0};
+  size_t recv_off[4] = {0, 0, 0, 0};
+  int edge_len[4] = {0, 0, 0, 0};
+  size_t elem = 8;               // bytes per halo element
+  size_t bytes = 0;              // total arena size
+};
+
+class GpuSubdomainSolver {
+ public:
+  GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain& sd, const GpuOptions& opt,
+                     uintptr_t external_arena = 0);
+  ~GpuSubdomainSolver();
+  GpuSubdomainSolver(const GpuSubdomainSolver&) = delete;
+  GpuSubdomainSolver& operator=(const GpuSubdomainSolver&) = delete;
+
+  static CommLayout comm_layout(const Subdomain& sd, DType dtype);
+
+  void enqueue_init(hipStream_t s);     // r=B, w=0, p=0, state reset, red_b <- (0, zr_0)
+  void enqueue_phase_a(hipStream_t s);  // k_pcg_a + reduce -> red_a
+  void enqueue_phase_b(hipStream_t s);  // k_pcg_b + reduce -> red_b, it += 1
+
+  PcgState read_state(hipStream_t s) const;  // synchronous D2H of the scalars
+  PcgState* state_dev() const { return state_; }
+  double* red_a_dev() const { return state_->red_a; }
+  double* red_b_dev() const { return state_->red_b; }
+  void* send_dev(int side) const { return arena_ + layout_.send_off[side]; }
+  void* recv_dev(int side) const { return arena_ + layout_.recv_off[side]; }
+  const CommLayout& layout() const { return layout_; }
+  uintptr_t arena_ptr() const { return reinterpret_cast<uintptr_t>(arena_); }
+
+  // local interior of w (nx x ny, row-major) as fp64 on the host
+  std::vector<double> download_w(hipStream_t s) const;
+  // any local field (0 w, 1 r, 2 p0, 3 p1) including ghosts: (nx+2) x (ny+2)
+  std::vector<double> download_field(int which, hipStream_t s) const;
+
+  const Subdomain& sd() const { return sd_; }
+  const ProblemSpec& spec() const { return spec_; }
+  const GpuOptions& options() const { return opt_; }
+  const DevGeom& geom() const { return geom_; }
+  const DevTables& tables() const { return tables_; }
+  const TileCfg& tiles() const { return tiles_; }
+  int device() const { return opt_.device; }
+  size_t field_bytes() const { return field_bytes_; }
+  void* field_base(int which) const;  // pointer to local (0,0)
+  size_t device_bytes() const;        // total device memory owned
+
+ private:
+  template <typename T> void init_impl(hipStream_t s);
+  template <typename T> void phase_a_impl(hipStream_t s);
+  template <typename T> void phase_b_impl(hipStream_t s);
+  template <typename T> HaloBufs<T> halo() const;
+  void after_launch(hipStream_t s) const;
+
+  ProblemSpec spec_;
+  Subdomain sd_;
+  GpuOptions opt_;
+  GridInfo g_;
+  DevGeom geom_{};
+  DevTables tables_{};
+  TileCfg tiles_{};
+  CommLayout layout_{};
+  size_t elem_ = 8, field_bytes_ = 0, field_off_ = 0;
+  char* fields_ = nullptr;  // 4 fields
+  double* tables_buf_ = nullptr;
+  double* partials_ = nullptr;
+  char* arena_ = nullptr;
+  bool own_arena_ = true;
+  PcgState* state_ = nullptr;
+  PcgState* host_state_ = nullptr;  // pinned
+};
+
+// ---------------------------------------------------------------------------
+// Communication backends (RcclComm / LocalComm / SelfComm)
+// ---------------------------------------------------------------------------
+class Comm {
+ public:
+  virtual ~Comm() = default;
+  // in-place sum of red_a (which=0, 1 double) or red_b (which=1, 2 doubles) over all ranks
+  virtual void allreduce(std::vector<GpuSubdomainSolver*>& local, int which,
+                         std::vector<hipStream_t>& streams) = 0;
+  // send[s] of every rank -> recv[opposite side] of its neighbour
+  virtual void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>& streams) = 0;
+  virtual bool graph_capturable() const { return true; }
+  virtual std::string name() const = 0;
+  virtual int world_size() const = 0;
+};
+
+std::unique_ptr<Comm> make_self_comm();
+std::unique_ptr<Comm> make_local_comm(std::vector<GpuSubdomainSolver*>& local);
+// RCCL: one communicator per local solver.  `unique_id` is the 128-byte ncclUniqueId,
+// `ranks` the global ranks of the local solvers, `nranks` the world size.
+std::unique_ptr<Comm> make_rccl_comm(const std::string& unique_id, int nranks,
+                                     const std::vector<int>& ranks, const std::vector<int>& devices,
+                                     bool capturable);
+std::string rccl_unique_id();
+
+struct RunStats {
+  int64_t iters = 0;
+  Status status = Status::kRunning;
+  double diff = 0.0;
+  double init_seconds = 0.0;
+  double solve_seconds = 0.0;
+  int64_t launched = 0;    // iterations enqueued (>= iters; the rest were device no-ops)
+  bool nan = false;
+  // reference-style phase buckets (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980), seconds;
+  // only filled by profile_phases()
+  double t_kernel_a = 0, t_kernel_b = 0, t_reduce = 0, t_comm = 0, t_poll = 0;
+};
+
+class PcgDriver {
+ public:
+  PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int graph_batch);
+  ~PcgDriver();
+
+  void init();                       // enqueue init on all ranks, all-reduce, halo; sync
+  void enqueue_iterations(int64_t n);  // no host sync (graph replays when possible)
+  void synchronize();
+  RunStats solve(int poll_batches = 1);  // init + iterate until the device says done
+  RunStats profile_phases(int64_t n);    // eager iterations with events around each phase
+  PcgState state(int idx = 0);
+  std::vector<hipStream_t>& streams() { return streams_; }
+
+ private:
+  void enqueue_one_iteration();
+  void build_graph();
+
+  std::vector<GpuSubdomainSolver*> local_;
+  Comm* comm_;
+  int graph_batch_;
+  std::vector<hipStream_t> streams_;
+  bool graph_ok_ = false;
+  std::vector<hipGraph_t> graphs_;
+  std::vector<hipGraphExec_t> execs_;
+};
+
+}  // namespace pmx

@@ -1,0 +1,59 @@
+// A solve session: decomposition + per-subdomain GPU solvers + comm backend + driver.
+// Shared by the C++ CLI (apps/pmx.cpp) and the Python bindings.
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "pmx/gpu_solver.hpp"
+
+namespace pmx {
+
+enum class CommKind : int { kSelf = 0, kLocal = 1, kRccl = 2 };
+
+struct SessionConfig {
+  ProblemSpec spec;
+  GpuOptions opt;
+  Split split = Split::kReference;
+  CommKind comm = CommKind::kSelf;
+  int world = 1;                 // total ranks (subdomains)
+  std::vector<int> ranks;        // ranks owned by this process (default: all for self/local)
+  std::vector<int> devices;      // device per owned rank (default: opt.device)
+  std::string rccl_uid;          // for kRccl
+  bool rccl_graph = false;       // capture RCCL calls into the hipGraph
+};
+
+class Session {
+ public:
+  explicit Session(const SessionConfig& cfg);
+  ~Session();
+
+  void init() { driver_->init(); }
+  void step(int64_t n) { driver_->enqueue_iterations(n); }
+  void synchronize() { driver_->synchronize(); }
+  RunStats solve(int poll_batches = 1) { return driver_->solve(poll_batches); }
+  RunStats profile(int64_t n) { return driver_->profile_phases(n); }
+  PcgState state(int i = 0) { return driver_->state(i); }
+
+  const ProcGrid& grid() const { return pg_; }
+  int num_local() const { return int(solvers_.size()); }
+  GpuSubdomainSolver& solver(int i) { return *solvers_.at(size_t(i)); }
+  const std::string comm_name() const { return comm_->name(); }
+  size_t device_bytes() const;
+  // global (M+1) x (N+1) solution filled with the subdomains owned by this process
+  std::vector<double> gather_local_w();
+
+ private:
+  SessionConfig cfg_;
+  ProcGrid pg_;
+  std::vector<std::unique_ptr<GpuSubdomainSolver>> solvers_;
+  std::unique_ptr<Comm> comm_;
+  std::unique_ptr<PcgDriver> driver_;
+};
+
+// Largest square grid whose fields fit into `bytes_per_gpu` on `gpus` devices (SURVEY §5.7:
+// subgrids sized against 288 GB HBM per MI355X).  fp64: 4 fields x 8 B/pt; fp32: 4 x 4 B/pt.
+int64_t max_square_grid(double bytes_per_gpu, int gpus, DType dtype, double reserve_fraction = 0.1);
+
+}  // namespace pmx

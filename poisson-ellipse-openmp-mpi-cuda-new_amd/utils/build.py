@@ -1,0 +1,139 @@
+"""Native build driver: compiles the C++/HIP core for gfx950 in-tree.
+
+Products (all inside the package directory, so they travel with the repo snapshot):
+  * ``_pmx.<EXT_SUFFIX>``  -- Python extension (pybind11), HIP kernels + RCCL + CPU oracle
+  * ``bin/pmx``            -- standalone C++ CLI (stage0..stage4-compatible output)
+  * ``bin/pmx_mpi``        -- optional MPI CPU backend (stage 2/3 parity), when mpicxx exists
+
+No torch.utils.cpp_extension/JIT cache: the objects are plain hipcc/g++ outputs, rebuilt
+incrementally by mtime (any header change rebuilds everything).
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent.parent
+CSRC = PKG_DIR / "csrc"
+BUILD_DIR = PKG_DIR / "build"
+BIN_DIR = PKG_DIR / "bin"
+EXT_NAME = "_pmx" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so")
+EXT_PATH = PKG_DIR / EXT_NAME
+
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+HIPCC = os.environ.get("HIPCC", str(ROCM / "bin" / "hipcc"))
+ARCH = os.environ.get("PMX_ARCH", "gfx950")
+
+HIP_SOURCES = [
+    "hip/pcg_kernels.hip",
+    "hip/ops_kernels.hip",
+    "hip/gpu_solver.hip",
+    "hip/session.hip",
+    "comm/comm.hip",
+]
+CPU_SOURCES = ["cpu/cpu_pcg.cpp"]
+BIND_SOURCES = ["bindings/module.cpp"]
+
+COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC / 'include'}", "-Wall", "-Wno-unused-result"]
+HIP_FLAGS = [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+CPU_FLAGS = ["-fopenmp", "-ffp-contract=off"]
+
+
+def _headers():
+    return list((CSRC / "include").rglob("*.hpp")) + list((CSRC / "hip").glob("*.hpp"))
+
+
+def _stale(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print("+", " ".join(str(c) for c in cmd), flush=True)
+    p = subprocess.run([str(c) for c in cmd], capture_output=True, text=True)
+    if p.returncode != 0:
+        raise RuntimeError(f"build step failed ({p.returncode}): {' '.join(map(str, cmd))}\n{p.stdout}\n{p.stderr}")
+    return p
+
+
+def _compile(src: str, kind: str, verbose: bool, force: bool) -> Path:
+    srcp = CSRC / src
+    obj = BUILD_DIR / (src.replace("/", "_") + ".o")
+    deps = [srcp] + _headers()
+    if not force and not _stale(obj, deps):
+        return obj
+    obj.parent.mkdir(parents=True, exist_ok=True)
+    if kind == "hip":
+        cmd = [HIPCC, *HIP_FLAGS, *COMMON_FLAGS, "-c", srcp, "-o", obj]
+    elif kind == "bind":
+        import pybind11
+
+        py_inc = sysconfig.get_paths()["include"]
+        cmd = [HIPCC, *COMMON_FLAGS, "-D__HIP_PLATFORM_AMD__", f"-I{pybind11.get_include()}", f"-I{py_inc}",
+               "-fvisibility=hidden", "-c", srcp, "-o", obj]
+    else:
+        cmd = ["g++", *COMMON_FLAGS, *CPU_FLAGS, "-c", srcp, "-o", obj]
+    _run(cmd, verbose)
+    return obj
+
+
+def build(verbose: bool = False, force: bool = False, jobs: int | None = None, apps: bool = True) -> Path:
+    """Compile every native source for gfx950 and link the extension (and CLI apps)."""
+    BUILD_DIR.mkdir(exist_ok=True)
+    jobs = jobs or min(8, os.cpu_count() or 4)
+    todo = [(s, "hip") for s in HIP_SOURCES] + [(s, "cpu") for s in CPU_SOURCES] + \
+           [(s, "bind") for s in BIND_SOURCES]
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda a: _compile(a[0], a[1], verbose, force), todo))
+    core_objs = objs[: len(HIP_SOURCES) + len(CPU_SOURCES)]
+    link_libs = [f"-L{ROCM / 'lib'}", "-lrccl", "-lamdhip64", "-lgomp", f"-Wl,-rpath,{ROCM / 'lib'}"]
+    if force or _stale(EXT_PATH, objs):
+        _run([HIPCC, "-shared", "-fPIC", *objs, "-o", EXT_PATH, *link_libs], verbose)
+    if apps:
+        _build_apps(core_objs, link_libs, verbose, force)
+    return EXT_PATH
+
+
+def _build_apps(core_objs, link_libs, verbose, force):
+    BIN_DIR.mkdir(exist_ok=True)
+    lib = BUILD_DIR / "libpmx.a"
+    if force or _stale(lib, core_objs):
+        if lib.exists():
+            lib.unlink()
+        _run(["ar", "rcs", lib, *core_objs], verbose)
+    app_src = CSRC / "apps" / "pmx.cpp"
+    exe = BIN_DIR / "pmx"
+    if app_src.exists() and (force or _stale(exe, [app_src, lib] + _headers())):
+        _run([HIPCC, *COMMON_FLAGS, "-D__HIP_PLATFORM_AMD__", app_src, lib, "-o", exe, *link_libs], verbose)
+    mpi_src = CSRC / "apps" / "pmx_mpi.cpp"
+    mpicxx = shutil.which("mpicxx") or ("/opt/conda/bin/mpicxx" if Path("/opt/conda/bin/mpicxx").exists() else None)
+    exe_mpi = BIN_DIR / "pmx_mpi"
+    if mpi_src.exists() and mpicxx and (force or _stale(exe_mpi, [mpi_src, CSRC / "cpu" / "cpu_pcg.cpp"] + _headers())):
+        try:
+            _run([mpicxx, "-O3", "-std=c++17", "-fopenmp", "-ffp-contract=off", f"-I{CSRC / 'include'}", mpi_src,
+                  CSRC / "cpu" / "cpu_pcg.cpp", "-o", exe_mpi], verbose)
+        except RuntimeError as e:  # MPI is optional (stage-2/3 parity only)
+            print(f"[pmx build] skipping pmx_mpi: {e}", file=sys.stderr)
+
+
+def extension_built() -> bool:
+    return EXT_PATH.exists()
+
+
+if __name__ == "__main__":
+    import argparse
+
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--no-apps", action="store_true")
+    a = ap.parse_args()
+    print(build(verbose=a.verbose, force=a.force, apps=not a.no_apps))

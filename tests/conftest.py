@@ -1,0 +1,39 @@
+import importlib
+import os
+import socket
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG_NAME = "poisson-ellipse-openmp-mpi-cuda-new_amd"
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+    config.addinivalue_line("markers", "slow: long-running (large grids)")
+
+
+@pytest.fixture(scope="session")
+def pkg():
+    m = importlib.import_module(PKG_NAME)
+    m.load_native()  # builds the extension in-tree if it is missing
+    return m
+
+
+@pytest.fixture(scope="session")
+def native(pkg):
+    return pkg.load_native()
+
+
+def sub(name):
+    return importlib.import_module(PKG_NAME + "." + name)
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p

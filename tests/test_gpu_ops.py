@@ -1,0 +1,69 @@
+"""HIP ops vs plain-PyTorch fp64 references of the same op (ops/reference.py)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import sub
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev(pkg):
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    return torch.device("cuda", 0)
+
+
+@pytest.mark.parametrize("M,N,P,rank", [(40, 40, 1, 0), (400, 600, 1, 0), (257, 130, 4, 3), (64, 1000, 2, 1)])
+def test_assemble_bitwise(pkg, native, dev, M, N, P, rank):
+    p = pkg.PoissonEllipse(M=M, N=N)
+    Px, Py = sub("parallel.decomp").choose_process_grid(P)
+    ops = pkg.ops.DeviceOps(p, Px, Py, rank) if hasattr(pkg, "ops") else sub("ops").DeviceOps(p, Px, Py, rank)
+    a, b, B = ops.assemble()
+    sd = ops.sd
+    ra, rb, rB = sub("ops.reference").assemble(p, sd)
+    assert torch.equal(a.cpu(), ra) and torch.equal(b.cpu(), rb)
+    assert torch.equal(B[1:-1, 1:-1].cpu(), rB[1:-1, 1:-1])
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-13), (torch.float32, 3e-6)])
+@pytest.mark.parametrize("exact", [True, False])
+def test_apply_A_and_precond(pkg, dev, dtype, tol, exact):
+    p = pkg.PoissonEllipse(M=300, N=211)
+    ops = sub("ops").DeviceOps(p)
+    R = sub("ops.reference")
+    a, b, _ = R.assemble(p, ops.sd)
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(ops.shape, generator=g, dtype=torch.float64)
+    x[0, :] = x[-1, :] = 0
+    x[:, 0] = x[:, -1] = 0
+    xd = x.to(dev, dtype)
+    Ap = ops.apply_A(xd, exact=exact).cpu().double()[1:-1, 1:-1]
+    ref = R.apply_A(xd.cpu().double(), a, b, p.h1, p.h2)
+    scale = ref.abs().max()
+    assert (Ap - ref).abs().max() / scale < tol
+    if exact and dtype == torch.float64:
+        assert torch.equal(Ap, ref)  # same arithmetic order, no FP contraction -> bitwise
+    z = ops.precond(xd, exact=exact).cpu().double()[1:-1, 1:-1]
+    zr = R.precond(xd.cpu().double(), a, b, p.h1, p.h2)
+    assert ((z - zr).abs() / zr.abs().clamp_min(1e-300)).max() < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_dot(pkg, dev, dtype):
+    p = pkg.PoissonEllipse(M=513, N=771)
+    ops = sub("ops").DeviceOps(p)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(ops.shape, generator=g, dtype=torch.float64)
+    y = torch.randn(ops.shape, generator=g, dtype=torch.float64)
+    xd, yd = x.to(dev, dtype), y.to(dev, dtype)
+    got = ops.dot(xd, yd)
+    ref = (xd.cpu().double()[1:-1, 1:-1] * yd.cpu().double()[1:-1, 1:-1]).sum().item()
+    assert abs(got - ref) <= 1e-10 * (x.abs() * y.abs()).sum().item()
+
+
+def test_ops_reject_bad_shapes(pkg, dev):
+    p = pkg.PoissonEllipse(M=20, N=20)
+    ops = sub("ops").DeviceOps(p)
+    with pytest.raises(ValueError):
+        ops.apply_A(torch.zeros(5, 5, device=dev, dtype=torch.float64))

@@ -1,0 +1,122 @@
+"""Fused HIP PCG: goldens, CPU-oracle agreement, fake-cluster decomposition, precision modes."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import sub
+
+pytestmark = pytest.mark.gpu
+
+WEIGHTED = {(10, 10): 15, (20, 20): 26, (40, 40): 50, (400, 600): 546, (800, 1200): 989}
+UNWEIGHTED = {(10, 10): 17, (20, 20): 31, (40, 40): 61, (400, 600): 801}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu(pkg):
+    assert torch.cuda.is_available() and pkg.load_native().device_count() > 0, "no HIP device"
+
+
+@pytest.mark.parametrize("grid,iters", sorted(WEIGHTED.items()))
+@pytest.mark.parametrize("exact", [False, True])
+def test_gpu_weighted_goldens(pkg, grid, iters, exact):
+    r = pkg.solve(pkg.PoissonEllipse(M=grid[0], N=grid[1]), "hip", exact=exact)
+    assert r.status == "converged" and r.iters == iters, (r.iters, r.status)
+
+
+@pytest.mark.parametrize("grid,iters", sorted(UNWEIGHTED.items()))
+def test_gpu_unweighted_goldens(pkg, grid, iters):
+    r = pkg.solve(pkg.stage_problem("stage0", *grid), "hip")
+    assert r.iters == iters
+
+
+def test_gpu_accuracy_800x1200(pkg):
+    p = pkg.PoissonEllipse(M=800, N=1200)
+    r = pkg.solve(p, "hip")
+    e = p.error_norms(r.w)
+    assert abs(e["max_w"] - 0.0997230615) < 1e-9
+    assert abs(e["l2_error"] - 1.9157e-4) < 1e-7
+
+
+def test_gpu_matches_cpu_solution(pkg):
+    p = pkg.PoissonEllipse(M=123, N=301)
+    ref = pkg.solve(p, "omp", threads=4)
+    for exact in (False, True):
+        r = pkg.solve(p, "hip", exact=exact)
+        assert r.iters == ref.iters
+        assert np.abs(r.w - ref.w).max() < 1e-10
+
+
+@pytest.mark.parametrize("ranks", [2, 3, 4, 7, 8])
+def test_local_comm_decomposition(pkg, ranks):
+    p = pkg.PoissonEllipse(M=200, N=160)
+    ref = pkg.solve(p, "hip", ranks=1)
+    r = pkg.solve(p, "hip", ranks=ranks)
+    assert r.extra["comm"] == "local"
+    assert r.iters == ref.iters
+    assert np.abs(r.w - ref.w).max() < 1e-11
+
+
+@pytest.mark.parametrize("split", ["auto", "rows", "cols"])
+def test_local_comm_splits_and_tiles(pkg, split):
+    p = pkg.PoissonEllipse(M=300, N=700)
+    ref = pkg.solve(p, "cpu")
+    r = pkg.solve(p, "hip", ranks=6, split=split, tile_rows=17, block=128)
+    assert r.iters == ref.iters
+    assert np.abs(r.w - ref.w).max() < 1e-10
+
+
+@pytest.mark.parametrize("block,rows", [(128, 1), (256, 64), (512, 256), (256, 7)])
+def test_tile_shapes(pkg, block, rows):
+    p = pkg.PoissonEllipse(M=211, N=1031)
+    ref = pkg.solve(p, "hip")
+    r = pkg.solve(p, "hip", block=block, tile_rows=rows)
+    assert r.iters == ref.iters
+    assert np.abs(r.w - ref.w).max() < 1e-12
+
+
+def test_graph_vs_eager(pkg):
+    p = pkg.PoissonEllipse(M=400, N=600)
+    a = pkg.solve(p, "hip", graph_batch=0)
+    b = pkg.solve(p, "hip", graph_batch=16)
+    assert a.iters == b.iters == 546
+    assert np.array_equal(a.w, b.w)
+
+
+def test_fp32_mixed(pkg):
+    p = pkg.PoissonEllipse(M=800, N=1200)
+    r = pkg.solve(p, "hip", dtype="fp32")
+    e = p.error_norms(r.w)
+    assert r.status in ("converged", "max_iter")
+    assert e["l2_error"] < 3e-4  # fp64: 1.9157e-4
+
+
+def test_check_mode_and_max_iter(pkg):
+    p = pkg.PoissonEllipse(M=100, N=100, max_iter=9)
+    r = pkg.solve(p, "hip", check=True)
+    assert r.iters == 9 and r.status == "max_iter"
+
+
+def test_subdomain_solver_torch_arena(pkg, native):
+    """The torch-comm path (world=1): native kernels on torch's stream, scalars in a torch arena."""
+    launch = sub("parallel.launch")
+    ds = sub("parallel.dist_solver")
+    p = pkg.PoissonEllipse(M=400, N=600)
+    s = ds.DistGpuPCG(p, launch.DistInfo(), comm="torch")
+    r = s.solve()
+    assert r.iters == 546 and r.status == "converged"
+    ref = pkg.solve(p, "hip")
+    assert np.abs(r.w - ref.w).max() < 1e-12
+
+
+def test_bench_session_steps(pkg):
+    """step()/state() contract used by bench.py: `it` advances by exactly the steps launched."""
+    p = pkg.PoissonEllipse(M=1024, N=1024)
+    s = pkg.models.make_session(p)
+    s.init()
+    s.step(5)
+    s.synchronize()
+    st0 = s.state()
+    s.step(70)
+    s.synchronize()
+    st1 = s.state()
+    assert not st1["done"] and st1["it"] - st0["it"] == 70
