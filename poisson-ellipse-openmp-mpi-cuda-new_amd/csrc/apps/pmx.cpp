@@ -1,0 +1,238 @@
+// pmx — command-line front end (component X6/X7 of SURVEY §2.6, CLI of §5.6).
+//
+// Backward compatible with the reference programs: `pmx M N` mirrors stages 2-4
+// (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:996-1000), defaults reproduce the reference problem
+// (ellipse x^2+4y^2<1, delta=1e-6, max_iter=(M-1)(N-1), weighted norm).  The superset:
+//
+//   pmx [M N] [--ax 1.0 --by 0.5] [--box -1,1,-0.6,0.6] [--f 1.0] [--delta 1e-6] [--max-iter K]
+//       [--backend cpu|omp|hip] [--threads T] [--ranks P] [--gpus G] [--comm self|local|rccl]
+//       [--split reference|auto|rows|cols] [--dtype fp64|fp32] [--norm weighted|unweighted]
+//       [--exact] [--graph-batch 32] [--tile-rows 64] [--block 256] [--device D]
+//       [--dump sol.txt] [--dump-stride s] [--json] [--banner stage0..stage4]
+//       [--profile-phases N] [--check]
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <iomanip>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "pmx/common.hpp"
+#include "pmx/cpu_pcg.hpp"
+#include "pmx/report.hpp"
+#include "pmx/session.hpp"
+
+using namespace pmx;
+
+namespace {
+
+struct Cli {
+  ProblemSpec spec;
+  std::string backend = "auto", comm = "auto", banner = "auto", dump, split = "reference";
+  int threads = 1, ranks = 1, gpus = 0, dump_stride = 1, device = 0;
+  int64_t profile = 0;
+  bool json = false;
+  GpuOptions opt;
+};
+
+[[noreturn]] void usage(const char* msg) {
+  if (msg) std::cerr << "pmx: " << msg << "\n";
+  std::cerr << "usage: pmx [M N] [--ax A] [--by B] [--box a1,b1,a2,b2] [--f F] [--delta D] [--max-iter K]\n"
+               "           [--backend cpu|omp|hip] [--threads T] [--ranks P] [--gpus G]\n"
+               "           [--comm self|local|rccl] [--split reference|auto|rows|cols]\n"
+               "           [--dtype fp64|fp32] [--norm weighted|unweighted] [--exact]\n"
+               "           [--graph-batch N] [--tile-rows R] [--block B] [--device D]\n"
+               "           [--dump FILE] [--dump-stride S] [--json] [--banner stage0..stage4]\n"
+               "           [--profile-phases N] [--check]\n";
+  std::exit(msg ? 2 : 0);
+}
+
+Split parse_split(const std::string& s) {
+  if (s == "reference") return Split::kReference;
+  if (s == "auto") return Split::kAuto;
+  if (s == "rows") return Split::kRows;
+  if (s == "cols") return Split::kCols;
+  usage("bad --split");
+}
+
+Cli parse(int argc, char** argv) {
+  Cli c;
+  std::vector<std::string> pos;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto val = [&]() -> std::string {
+      if (i + 1 >= argc) usage(("missing value for " + a).c_str());
+      return argv[++i];
+    };
+    if (a == "-h" || a == "--help") usage(nullptr);
+    else if (a == "--ax") c.spec.ax = std::atof(val().c_str());
+    else if (a == "--by") c.spec.by = std::atof(val().c_str());
+    else if (a == "--f") c.spec.F = std::atof(val().c_str());
+    else if (a == "--delta") c.spec.delta = std::atof(val().c_str());
+    else if (a == "--max-iter") c.spec.max_iter = std::atoll(val().c_str());
+    else if (a == "--box") {
+      const std::string v = val();
+      if (std::sscanf(v.c_str(), "%lf,%lf,%lf,%lf", &c.spec.A1, &c.spec.B1, &c.spec.A2, &c.spec.B2) != 4)
+        usage("--box needs a1,b1,a2,b2");
+    } else if (a == "--backend") c.backend = val();
+    else if (a == "--threads") c.threads = std::atoi(val().c_str());
+    else if (a == "--ranks") c.ranks = std::atoi(val().c_str());
+    else if (a == "--gpus") c.gpus = std::atoi(val().c_str());
+    else if (a == "--comm") c.comm = val();
+    else if (a == "--split") c.split = val();
+    else if (a == "--dtype") {
+      const std::string v = val();
+      if (v != "fp64" && v != "fp32") usage("--dtype fp64|fp32");
+      c.opt.dtype = v == "fp64" ? DType::kFp64 : DType::kFp32;
+    } else if (a == "--norm") {
+      const std::string v = val();
+      if (v != "weighted" && v != "unweighted") usage("--norm weighted|unweighted");
+      c.spec.norm = v == "weighted" ? Norm::kWeighted : Norm::kUnweighted;
+    } else if (a == "--exact") c.opt.exact = true;
+    else if (a == "--graph-batch") c.opt.graph_batch = std::atoi(val().c_str());
+    else if (a == "--tile-rows") c.opt.tile_rows = std::atoi(val().c_str());
+    else if (a == "--block") c.opt.block = std::atoi(val().c_str());
+    else if (a == "--device") c.device = std::atoi(val().c_str());
+    else if (a == "--dump") c.dump = val();
+    else if (a == "--dump-stride") c.dump_stride = std::atoi(val().c_str());
+    else if (a == "--json") c.json = true;
+    else if (a == "--banner") c.banner = val();
+    else if (a == "--profile-phases") c.profile = std::atoll(val().c_str());
+    else if (a == "--check") c.opt.check = true;
+    else if (!a.empty() && a[0] == '-') usage(("unknown option " + a).c_str());
+    else pos.push_back(a);
+  }
+  if (pos.size() == 2) {
+    c.spec.M = std::atoi(pos[0].c_str());
+    c.spec.N = std::atoi(pos[1].c_str());
+  } else if (!pos.empty()) {
+    usage("expected positional M N");
+  }
+  if (c.backend == "auto") {
+    int n = 0;
+    c.backend = (hipGetDeviceCount(&n) == hipSuccess && n > 0) ? "hip" : (c.threads > 1 ? "omp" : "cpu");
+    (void)hipGetLastError();
+  }
+  if (c.banner == "auto") {
+    if (c.backend == "hip") c.banner = "stage4";
+    else if (c.ranks > 1) c.banner = c.threads > 1 ? "stage3" : "stage2";
+    else c.banner = c.spec.norm == Norm::kUnweighted ? "stage0" : "stage1";
+  }
+  c.opt.device = c.device;
+  return c;
+}
+
+double now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int run_cpu(Cli& c, double t_prog) {
+  const ProblemSpec& s = c.spec;
+  const bool stage0 = c.banner == "stage0";
+  if (c.banner == "stage1")
+    std::cout << "--- (Variant 9: Ellipse x^2 + 4y^2 < 1, OpenMP Test) ---\nGrid: M=" << s.M << ", N=" << s.N
+              << "\n--------------------------------------------------------\n";
+  if (c.banner == "stage2")
+    std::cout << "Pure MPI 2D run with " << c.ranks << " processes; M=" << s.M << ", N=" << s.N << std::endl;
+  if (c.banner == "stage3")
+    std::cout << "MPI/OpenMP run with " << c.ranks << " MPI processes; M=" << s.M << ", N=" << s.N << std::endl;
+  const int threads = c.backend == "cpu" ? 1 : c.threads;
+  SolveResult r = c.ranks > 1 ? cpu_solve_decomposed(s, c.ranks, parse_split(c.split), threads, true)
+                              : cpu_solve(s, threads, true);
+  if (r.status == Status::kConverged) print_converged(r.iters, s.delta, stage0);
+  if (c.banner == "stage1") {
+    std::cout << "Threads = " << std::setw(2) << threads << " | Time = " << std::fixed << std::setprecision(3)
+              << r.seconds << " s\n--------------------------------------------------------\n";
+  } else {
+    std::cout << "M=" << s.M << ", N=" << s.N << " | Iter=" << r.iters << " | Time=" << std::fixed
+              << std::setprecision(stage0 ? 4 : 6) << r.seconds << " s\n";
+  }
+  const ErrorNorms e = error_norms(s, r.w);
+  if (!c.dump.empty()) write_ascii(c.dump, s, r.w, c.dump_stride, r.iters);
+  if (c.json) {
+    JsonLine j;
+    j.ks("backend", c.backend).kv("M", s.M).kv("N", s.N).kv("ranks", c.ranks).kv("threads", threads)
+        .kv("iters", r.iters).ks("status", status_name(r.status)).kv("seconds", r.seconds)
+        .kv("mlups", double(s.M - 1) * (s.N - 1) * r.iters / r.seconds / 1e6).kv("l2_error", e.l2)
+        .kv("max_error", e.max_err).kv("max_w", e.max_w).kv("total_seconds", now() - t_prog);
+    std::cout << j.str() << std::endl;
+  }
+  return 0;
+}
+
+int run_hip(Cli& c, double t_prog) {
+  SessionConfig cfg;
+  cfg.spec = c.spec;
+  cfg.opt = c.opt;
+  cfg.split = parse_split(c.split);
+  const int gpus = std::max(1, c.gpus);
+  if (c.gpus > 1) {
+    cfg.world = gpus;
+    cfg.comm = CommKind::kRccl;
+    for (int r = 0; r < gpus; ++r) { cfg.ranks.push_back(r); cfg.devices.push_back(c.device + r); }
+    cfg.rccl_uid = rccl_unique_id();
+  } else {
+    cfg.world = c.ranks;
+    cfg.comm = c.ranks > 1 ? CommKind::kLocal : CommKind::kSelf;
+  }
+  if (c.comm == "rccl" && c.gpus <= 1) PMX_CHECK(false, "--comm rccl needs --gpus > 1");
+  const ProblemSpec& s = c.spec;
+  std::cout << "MPI + CUDA 2D run with " << cfg.world << " processes; M=" << s.M << ", N=" << s.N << std::endl;
+  const double t_before = now();
+  Session sess(cfg);
+  RunStats st = sess.solve();
+  const double t_after = now();
+  if (st.status == Status::kConverged) print_converged(st.iters, s.delta, false);
+  RunStats ph;
+  if (c.profile > 0) {
+    sess.init();
+    ph = sess.profile(c.profile);
+    const double scale = double(st.iters) / double(c.profile);
+    std::cout << "   GPU compute time (Ap + D^{-1}r, max over ranks) ~ " << (ph.t_kernel_a + ph.t_kernel_b) * scale << " s\n"
+              << "   Host<->Device copy time (max over ranks)        ~ " << 0.0 << " s\n"
+              << "   MPI halo exchange time (max over ranks)         ~ " << ph.t_comm * scale << " s\n"
+              << "   Preconditioner CPU part time (max over ranks)   ~ " << 0.0 << " s\n"
+              << "   Dot products time (max over ranks)              ~ " << 0.0 << " s\n";
+  }
+  std::cout << "M=" << s.M << ", N=" << s.N << " | Iter=" << st.iters << " | Total Time=" << std::fixed
+            << std::setprecision(6) << (t_after - t_prog) << " s\n"
+            << "   Init time (program)      ~ " << (t_before - t_prog) + st.init_seconds << " s\n"
+            << "   Solver time (MPI+CUDA)   ~ " << st.solve_seconds << " s\n"
+            << "   Finalization time        ~ " << 0.0 << " s\n";
+  std::vector<double> w;
+  if (!c.dump.empty() || c.json) w = sess.gather_local_w();
+  if (!c.dump.empty()) write_ascii(c.dump, s, w, c.dump_stride, st.iters);
+  if (c.json) {
+    const ErrorNorms e = error_norms(s, w);
+    JsonLine j;
+    j.ks("backend", "hip").kv("M", s.M).kv("N", s.N).kv("ranks", cfg.world).ks("comm", sess.comm_name())
+        .ks("dtype", c.opt.dtype == DType::kFp64 ? "fp64" : "fp32").kv("iters", st.iters)
+        .ks("status", status_name(st.status)).kv("solve_seconds", st.solve_seconds)
+        .kv("init_seconds", st.init_seconds)
+        .kv("mlups", double(s.M - 1) * (s.N - 1) * st.iters / st.solve_seconds / 1e6)
+        .kv("us_per_iter", st.solve_seconds / std::max<int64_t>(1, st.iters) * 1e6)
+        .kv("l2_error", e.l2).kv("max_error", e.max_err).kv("max_w", e.max_w)
+        .kv("device_bytes", sess.device_bytes()).kv("total_seconds", now() - t_prog);
+    if (c.profile > 0)
+      j.kv("phase_kernel_a_s", ph.t_kernel_a).kv("phase_kernel_b_s", ph.t_kernel_b).kv("phase_comm_s", ph.t_comm);
+    std::cout << j.str() << std::endl;
+  }
+  return st.nan ? 3 : 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const double t_prog = now();
+  try {
+    Cli c = parse(argc, argv);
+    c.spec.validate();
+    if (c.backend == "cpu" || c.backend == "omp") return run_cpu(c, t_prog);
+    if (c.backend == "hip") return run_hip(c, t_prog);
+    usage("unknown --backend");
+  } catch (const std::exception& e) {
+    std::cerr << e.what() << std::endl;
+    return 1;
+  }
+}
