@@ -37,8 +37,12 @@ def parse():
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
     ap.add_argument("--comm", default="native", choices=["native", "torch"])
     ap.add_argument("--split", default="reference", choices=["reference", "auto", "rows", "cols"])
-    ap.add_argument("--block", type=int, default=256)
-    ap.add_argument("--tile-rows", type=int, default=64)
+    ap.add_argument("--kernel", default="wave", choices=["wave", "lds"],
+                    help="wave: wave-tile kernels with DPP lane shifts; lds: workgroup tiles + LDS row ring")
+    ap.add_argument("--block", type=int, default=256, help="lds kernels: tile width")
+    ap.add_argument("--vec", type=int, default=2, help="wave kernels: columns per lane")
+    ap.add_argument("--waves", type=int, default=4, help="wave kernels: wave tiles per workgroup")
+    ap.add_argument("--tile-rows", type=int, default=0, help="tile height (0 = auto)")
     ap.add_argument("--graph-batch", type=int, default=32)
     ap.add_argument("--exact", action="store_true", help="reference arithmetic order in the fused kernels")
     ap.add_argument("--tol-solve", dest="tol_solve", action="store_true", default=True)
@@ -68,8 +72,8 @@ def main():
     torch.cuda.set_device(info.local_rank)
 
     problem = pmx.PoissonEllipse(M=args.M, N=args.N)
-    kw = dict(split=args.split, dtype=args.dtype, block=args.block, tile_rows=args.tile_rows, exact=args.exact,
-              graph_batch=args.graph_batch)
+    kw = dict(split=args.split, dtype=args.dtype, kernel=args.kernel, block=args.block, vec=args.vec,
+              waves=args.waves, tile_rows=args.tile_rows, exact=args.exact, graph_batch=args.graph_batch)
     comm_used = args.comm
     if world == 1:
         models = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.models")
@@ -172,7 +176,8 @@ def main():
                 "parallelism": f"domain{world}" if world > 1 else "single",
                 "grid": [args.M, args.N],
                 "comm": comm_used,
-                "tile": [args.tile_rows, args.block],
+                "kernel": args.kernel,
+                "tile": dict(rows=args.tile_rows, block=args.block, vec=args.vec, waves=args.waves),
                 "graph_batch": args.graph_batch,
                 "exact": args.exact,
             },

@@ -1,0 +1,120 @@
+// Memory-system ceiling study for the PCG access pattern on MI355X.
+//
+// Measures, on fp64 arrays of N x N (pitch N+32):
+//   copy      : 1 read + 1 write, contiguous grid-stride, 16 B/lane
+//   stream5   : 3 reads + 2 writes (the k_pcg_b traffic), contiguous grid-stride, 16 B/lane
+//   march5    : the same 5 streams, but each 256-thread block marches `rows` rows of a
+//               512-column strip (the tile-marching order of the fused kernels)
+//   rowband5  : 5 streams, one block per (row, 512-col chunk), rows assigned so that each XCD
+//               works on its own contiguous band of rows (T1-style XCD-aware mapping)
+// Usage: membw [N] [rows]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                  \
+  do {                                                                         \
+    hipError_t e = (x);                                                        \
+    if (e != hipSuccess) {                                                     \
+      printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__);          \
+      exit(1);                                                                 \
+    }                                                                          \
+  } while (0)
+
+__global__ void __launch_bounds__(256) k_copy(const double2* a, double2* b, size_t n2) {
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n2; i += size_t(gridDim.x) * 256) b[i] = a[i];
+}
+
+__global__ void __launch_bounds__(256)
+k_stream5(const double2* p, double2* w, double2* r, size_t n2, double al) {
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n2; i += size_t(gridDim.x) * 256) {
+    double2 pv = p[i], wv = w[i], rv = r[i];
+    wv.x += al * pv.x; wv.y += al * pv.y;
+    rv.x -= al * pv.y; rv.y -= al * pv.x;
+    w[i] = wv; r[i] = rv;
+  }
+}
+
+// tile = rows x 512 columns, 256 threads x 2 columns, marching down
+__global__ void __launch_bounds__(256)
+k_march5(const double* p, double* w, double* r, int n, int pitch, int rows, int tiles_j, double al) {
+  const int ti = blockIdx.x / tiles_j, tj = blockIdx.x % tiles_j;
+  const int j = tj * 512 + 2 * threadIdx.x;
+  const int i0 = ti * rows;
+  for (int i = i0; i < i0 + rows && i < n; ++i) {
+    const size_t c = size_t(i) * pitch + j;
+    double2 pv = *(const double2*)(p + c), wv = *(double2*)(w + c), rv = *(double2*)(r + c);
+    wv.x += al * pv.x; wv.y += al * pv.y;
+    rv.x -= al * pv.y; rv.y -= al * pv.x;
+    *(double2*)(w + c) = wv;
+    *(double2*)(r + c) = rv;
+  }
+}
+
+// one block per (row, 512-col chunk); block b -> XCD b%8 gets rows [xcd*n/8, (xcd+1)*n/8)
+__global__ void __launch_bounds__(256)
+k_rowband5(const double* p, double* w, double* r, int n, int pitch, int chunks, double al, int xcd_aware) {
+  int b = blockIdx.x;
+  const int nb = gridDim.x;
+  if (xcd_aware) {
+    const int per = nb / 8;  // nb multiple of 8
+    b = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  }
+  const int i = b / chunks, jc = b % chunks;
+  if (i >= n) return;
+  const int j = jc * 512 + 2 * threadIdx.x;
+  const size_t c = size_t(i) * pitch + j;
+  double2 pv = *(const double2*)(p + c), wv = *(double2*)(w + c), rv = *(double2*)(r + c);
+  wv.x += al * pv.x; wv.y += al * pv.y;
+  rv.x -= al * pv.y; rv.y -= al * pv.x;
+  *(double2*)(w + c) = wv;
+  *(double2*)(r + c) = rv;
+}
+
+int main(int argc, char** argv) {
+  const int n = argc > 1 ? atoi(argv[1]) : 16384;
+  const int rows = argc > 2 ? atoi(argv[2]) : 64;
+  const int pitch = n + 32;
+  const size_t elems = size_t(n) * pitch;
+  const size_t bytes = elems * 8;
+  double *p, *w, *r;
+  CK(hipMalloc(&p, bytes));
+  CK(hipMalloc(&w, bytes));
+  CK(hipMalloc(&r, bytes));
+  CK(hipMemset(p, 0, bytes));
+  CK(hipMemset(w, 0, bytes));
+  CK(hipMemset(r, 0, bytes));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  auto timeit = [&](const char* name, double gb, auto launch) {
+    for (int w_ = 0; w_ < 3; ++w_) launch();
+    CK(hipDeviceSynchronize());
+    const int reps = 10;
+    CK(hipEventRecord(e0));
+    for (int k = 0; k < reps; ++k) launch();
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= reps;
+    printf("{\"kernel\": \"%s\", \"n\": %d, \"ms\": %.4f, \"TBps\": %.3f}\n", name, n, ms, gb / ms * 1e-3);
+  };
+  const size_t n2 = elems / 2;
+  const double gb_copy = 2.0 * bytes / 1e9, gb5 = 5.0 * bytes / 1e9;
+  timeit("copy", gb_copy, [&] { hipLaunchKernelGGL(k_copy, dim3(8192), dim3(256), 0, 0, (const double2*)p, (double2*)w, n2); });
+  timeit("stream5", gb5, [&] { hipLaunchKernelGGL(k_stream5, dim3(8192), dim3(256), 0, 0, (const double2*)p, (double2*)w, (double2*)r, n2, 0.5); });
+  const int tiles_j = n / 512;
+  for (int rw : {rows, 16, 4, 1}) {
+    const int tiles_i = (n + rw - 1) / rw;
+    char name[64];
+    snprintf(name, sizeof name, "march5_rows%d", rw);
+    timeit(name, gb5, [&] { hipLaunchKernelGGL(k_march5, dim3(tiles_i * tiles_j), dim3(256), 0, 0, p, w, r, n, pitch, rw, tiles_j, 0.5); });
+  }
+  const int chunks = n / 512;
+  timeit("rowband5_rowmajor", gb5, [&] { hipLaunchKernelGGL(k_rowband5, dim3(n * chunks), dim3(256), 0, 0, p, w, r, n, pitch, chunks, 0.5, 0); });
+  timeit("rowband5_xcd", gb5, [&] { hipLaunchKernelGGL(k_rowband5, dim3(n * chunks), dim3(256), 0, 0, p, w, r, n, pitch, chunks, 0.5, 1); });
+  return 0;
+}

@@ -7,7 +7,8 @@
 //   pmx [M N] [--ax 1.0 --by 0.5] [--box -1,1,-0.6,0.6] [--f 1.0] [--delta 1e-6] [--max-iter K]
 //       [--backend cpu|omp|hip] [--threads T] [--ranks P] [--gpus G] [--comm self|local|rccl]
 //       [--split reference|auto|rows|cols] [--dtype fp64|fp32] [--norm weighted|unweighted]
-//       [--exact] [--graph-batch 32] [--tile-rows 64] [--block 256] [--device D]
+//       [--exact] [--graph-batch 32] [--tile-rows 0] [--kernel wave|lds] [--vec 2] [--waves 4]
+//       [--block 256] [--device D]
 //       [--dump sol.txt] [--dump-stride s] [--json] [--banner stage0..stage4]
 //       [--profile-phases N] [--check]
 #include <chrono>
@@ -42,7 +43,8 @@ struct Cli {
                "           [--backend cpu|omp|hip] [--threads T] [--ranks P] [--gpus G]\n"
                "           [--comm self|local|rccl] [--split reference|auto|rows|cols]\n"
                "           [--dtype fp64|fp32] [--norm weighted|unweighted] [--exact]\n"
-               "           [--graph-batch N] [--tile-rows R] [--block B] [--device D]\n"
+               "           [--graph-batch N] [--tile-rows R] [--kernel wave|lds] [--vec V]\n"
+               "           [--waves W] [--block B] [--device D]\n"
                "           [--dump FILE] [--dump-stride S] [--json] [--banner stage0..stage4]\n"
                "           [--profile-phases N] [--check]\n";
   std::exit(msg ? 2 : 0);
@@ -93,6 +95,13 @@ Cli parse(int argc, char** argv) {
     else if (a == "--graph-batch") c.opt.graph_batch = std::atoi(val().c_str());
     else if (a == "--tile-rows") c.opt.tile_rows = std::atoi(val().c_str());
     else if (a == "--block") c.opt.block = std::atoi(val().c_str());
+    else if (a == "--vec") c.opt.vec = std::atoi(val().c_str());
+    else if (a == "--waves") c.opt.waves = std::atoi(val().c_str());
+    else if (a == "--kernel") {
+      const std::string v = val();
+      if (v != "wave" && v != "lds") usage("--kernel wave|lds");
+      c.opt.kernel = v == "lds" ? 0 : 1;
+    }
     else if (a == "--device") c.device = std::atoi(val().c_str());
     else if (a == "--dump") c.dump = val();
     else if (a == "--dump-stride") c.dump_stride = std::atoi(val().c_str());

@@ -149,10 +149,14 @@ class OpContext {
   double* partials_ = nullptr;
 };
 
-GpuOptions make_options(int device, int block, int tile_rows, const std::string& dtype, bool exact,
-                        int graph_batch, bool check) {
+GpuOptions make_options(int device, const std::string& kernel, int block, int vec, int waves,
+                        int tile_rows, const std::string& dtype, bool exact, int graph_batch, bool check) {
   GpuOptions o;
   o.device = device;
+  PMX_CHECK(kernel == "lds" || kernel == "wave", "kernel must be lds or wave, got " << kernel);
+  o.kernel = kernel == "lds" ? 0 : 1;
+  o.vec = vec;
+  o.waves = waves;
   o.block = block;
   o.tile_rows = tile_rows;
   PMX_CHECK(dtype == "fp64" || dtype == "fp32", "dtype must be fp64 or fp32, got " << dtype);
@@ -259,14 +263,17 @@ PYBIND11_MODULE(_pmx, m) {
 
   // Single subdomain solver on caller-chosen streams/arena (Python-orchestrated comm path).
   py::class_<GpuSubdomainSolver>(m, "SubdomainSolver")
-      .def(py::init([](const ProblemSpec& s, int Px, int Py, int rank, int device, int block,
-                       int tile_rows, const std::string& dtype, bool exact, uintptr_t arena, bool check) {
+      .def(py::init([](const ProblemSpec& s, int Px, int Py, int rank, int device,
+                       const std::string& kernel, int block, int vec, int waves, int tile_rows,
+                       const std::string& dtype, bool exact, uintptr_t arena, bool check) {
              const Subdomain sd = decompose_2d(s.M, s.N, ProcGrid{Px, Py}, rank);
              return std::make_unique<GpuSubdomainSolver>(
-                 s, sd, make_options(device, block, tile_rows, dtype, exact, 0, check), arena);
+                 s, sd, make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact, 0, check),
+                 arena);
            }),
            py::arg("spec"), py::arg("Px") = 1, py::arg("Py") = 1, py::arg("rank") = 0,
-           py::arg("device") = 0, py::arg("block") = 256, py::arg("tile_rows") = 64,
+           py::arg("device") = 0, py::arg("kernel") = "wave", py::arg("block") = 256,
+           py::arg("vec") = 2, py::arg("waves") = 4, py::arg("tile_rows") = 0,
            py::arg("dtype") = "fp64", py::arg("exact") = false, py::arg("arena") = 0,
            py::arg("check") = false)
       .def("enqueue_init", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_init(as_stream(s)); })
@@ -287,12 +294,14 @@ PYBIND11_MODULE(_pmx, m) {
 
   py::class_<Session>(m, "Session")
       .def(py::init([](const ProblemSpec& s, int world, const std::string& comm, Split split,
-                       int device, int block, int tile_rows, const std::string& dtype, bool exact,
-                       int graph_batch, bool check, py::object uid, std::vector<int> ranks,
-                       std::vector<int> devices, bool rccl_graph) {
+                       int device, const std::string& kernel, int block, int vec, int waves,
+                       int tile_rows, const std::string& dtype, bool exact, int graph_batch,
+                       bool check, py::object uid, std::vector<int> ranks, std::vector<int> devices,
+                       bool rccl_graph) {
              SessionConfig c;
              c.spec = s;
-             c.opt = make_options(device, block, tile_rows, dtype, exact, graph_batch, check);
+             c.opt = make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact,
+                                  graph_batch, check);
              c.split = split;
              c.world = world;
              if (comm == "self") c.comm = CommKind::kSelf;
@@ -307,8 +316,9 @@ PYBIND11_MODULE(_pmx, m) {
              return std::make_unique<Session>(c);
            }),
            py::arg("spec"), py::arg("world") = 1, py::arg("comm") = "self",
-           py::arg("split") = Split::kReference, py::arg("device") = 0, py::arg("block") = 256,
-           py::arg("tile_rows") = 64, py::arg("dtype") = "fp64", py::arg("exact") = false,
+           py::arg("split") = Split::kReference, py::arg("device") = 0, py::arg("kernel") = "wave",
+           py::arg("block") = 256, py::arg("vec") = 2, py::arg("waves") = 4,
+           py::arg("tile_rows") = 0, py::arg("dtype") = "fp64", py::arg("exact") = false,
            py::arg("graph_batch") = 32, py::arg("check") = false, py::arg("uid") = py::none(),
            py::arg("ranks") = std::vector<int>{}, py::arg("devices") = std::vector<int>{},
            py::arg("rccl_graph") = false)
@@ -335,5 +345,12 @@ PYBIND11_MODULE(_pmx, m) {
       .def_property_readonly("comm_name", &Session::comm_name)
       .def_property_readonly("device_bytes", &Session::device_bytes)
       .def_property_readonly("grid", [](Session& s) { return py::make_tuple(s.grid().Px, s.grid().Py); })
-      .def_property_readonly("ntiles", [](Session& s) { return s.solver(0).tiles().ntiles(); });
+      .def_property_readonly("ntiles", [](Session& s) { return s.solver(0).tiles().ntiles(); })
+      .def_property_readonly("tile", [](Session& s) {
+        const TileCfg& t = s.solver(0).tiles();
+        py::dict d;
+        d["kind"] = t.kind == 0 ? "lds" : "wave"; d["block"] = t.block; d["rows"] = t.rows;
+        d["vec"] = t.vec; d["waves"] = t.waves; d["tiles_i"] = t.tiles_i; d["tiles_j"] = t.tiles_j;
+        return d;
+      });
 }

@@ -102,8 +102,12 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
   // 1D face tables
   tables_ = upload_tables(spec, &tables_buf_);
 
-  tiles_ = make_tiles(G, opt.block, opt.tile_rows);
-  HIP_CHECK(hipMalloc(&partials_, size_t(tiles_.ntiles()) * 2 * sizeof(double)));
+  PMX_CHECK(opt.kernel == 0 || opt.kernel == 1, "kernel must be 0 (lds) or 1 (wave/dpp)");
+  tiles_ = opt.kernel == 0 ? make_tiles(G, opt.block, opt.tile_rows)
+                           : make_wave_tiles(G, opt.vec, opt.waves, opt.tile_rows);
+  init_tiles_ = make_tiles(G, 256, 0);
+  const size_t npart = size_t(std::max(tiles_.ntiles(), init_tiles_.ntiles()));
+  HIP_CHECK(hipMalloc(&partials_, npart * 2 * sizeof(double)));
 
   layout_ = comm_layout(sd, opt.dtype);
   if (external_arena) {
@@ -131,7 +135,8 @@ GpuSubdomainSolver::~GpuSubdomainSolver() {
 
 size_t GpuSubdomainSolver::device_bytes() const {
   return 4 * field_bytes_ + (4 * (spec_.M + 2) + 4 * (spec_.N + 2)) * sizeof(double) +
-         size_t(tiles_.ntiles()) * 2 * sizeof(double) + (own_arena_ ? layout_.bytes : 0);
+         size_t(std::max(tiles_.ntiles(), init_tiles_.ntiles())) * 2 * sizeof(double) +
+         (own_arena_ ? layout_.bytes : 0);
 }
 
 void* GpuSubdomainSolver::field_base(int which) const {
@@ -169,17 +174,22 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
   HIP_CHECK(hipMemcpyAsync(state_, &st, sizeof(PcgState), hipMemcpyHostToDevice, s));
   T* w = static_cast<T*>(field_base(0));
   T* r = static_cast<T*>(field_base(1));
-  launch_init<T>(geom_, tables_, w, r, halo<T>(), partials_, tiles_, s);
+  launch_init<T>(geom_, tables_, w, r, halo<T>(), partials_, init_tiles_, s);
   after_launch(s);
-  launch_reduce(partials_, tiles_.ntiles(), 2, 0.0, g_.h1h2, state_->red_b, state_, 0, s);
+  launch_reduce(partials_, init_tiles_.ntiles(), 2, 0.0, g_.h1h2, state_->red_b, state_, 0, s);
   after_launch(s);
 }
 
 template <typename T>
 void GpuSubdomainSolver::phase_a_impl(hipStream_t s) {
-  launch_pcg_a<T>(geom_, tables_, static_cast<const T*>(field_base(1)),
-                  static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(),
-                  partials_, state_, tiles_, opt_.exact, s);
+  if (tiles_.kind == 1)
+    launch_pcg_a_wave<T>(geom_, tables_, static_cast<const T*>(field_base(1)),
+                         static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(),
+                         partials_, state_, tiles_, opt_.exact, s);
+  else
+    launch_pcg_a<T>(geom_, tables_, static_cast<const T*>(field_base(1)),
+                    static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(),
+                    partials_, state_, tiles_, opt_.exact, s);
   after_launch(s);
   launch_reduce(partials_, tiles_.ntiles(), 1, g_.h1h2, 0.0, state_->red_a, state_, kSkipIfDone, s);
   after_launch(s);
@@ -187,9 +197,15 @@ void GpuSubdomainSolver::phase_a_impl(hipStream_t s) {
 
 template <typename T>
 void GpuSubdomainSolver::phase_b_impl(hipStream_t s) {
-  launch_pcg_b<T>(geom_, tables_, static_cast<T*>(field_base(0)), static_cast<T*>(field_base(1)),
-                  static_cast<const T*>(field_base(2)), static_cast<const T*>(field_base(3)),
-                  halo<T>(), partials_, state_, tiles_, opt_.exact, s);
+  if (tiles_.kind == 1)
+    launch_pcg_b_wave<T>(geom_, tables_, static_cast<T*>(field_base(0)),
+                         static_cast<T*>(field_base(1)), static_cast<const T*>(field_base(2)),
+                         static_cast<const T*>(field_base(3)), halo<T>(), partials_, state_, tiles_,
+                         opt_.exact, s);
+  else
+    launch_pcg_b<T>(geom_, tables_, static_cast<T*>(field_base(0)), static_cast<T*>(field_base(1)),
+                    static_cast<const T*>(field_base(2)), static_cast<const T*>(field_base(3)),
+                    halo<T>(), partials_, state_, tiles_, opt_.exact, s);
   after_launch(s);
   const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
   launch_reduce(partials_, tiles_.ntiles(), 2, wdiff, g_.h1h2, state_->red_b, state_,

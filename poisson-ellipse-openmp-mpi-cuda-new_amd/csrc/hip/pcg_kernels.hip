@@ -25,12 +25,19 @@ constexpr int kMaxRows = 256;
 
 TileCfg make_tiles(const DevGeom& G, int block, int rows) {
   PMX_CHECK(block == 256 || block == 128 || block == 512, "unsupported block " << block);
-  PMX_CHECK(rows >= 1 && rows <= kMaxRows, "tile rows must be in [1, " << kMaxRows << "]");
+  PMX_CHECK(rows >= 0 && rows <= kMaxRows, "tile rows must be in [0, " << kMaxRows << "] (0 = auto)");
   TileCfg t;
   t.block = block;
+  t.tiles_j = (G.ny + block - 1) / block;
+  if (rows == 0) {
+    // auto: enough workgroups to fill 256 CUs x 8 resident blocks, but marching tiles no
+    // taller than 64 rows (the tile-height sweep in profiles/ shows 32-64 as the plateau)
+    constexpr int64_t kTargetBlocks = 2048;
+    const int64_t want = (int64_t(G.nx) * t.tiles_j + kTargetBlocks - 1) / kTargetBlocks;
+    rows = int(std::min<int64_t>(64, std::max<int64_t>(2, want)));
+  }
   t.rows = rows;
   t.tiles_i = (G.nx + rows - 1) / rows;
-  t.tiles_j = (G.ny + block - 1) / block;
   return t;
 }
 
@@ -144,31 +151,44 @@ k_pcg_a(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, HaloBufs
   }
   __syncthreads();
 
-  // (2) march down the rows
+  // (2) march down the rows.  Row i+1's loads (r, p^{k-1}, row tables) are issued before row
+  // i is computed, so every wave keeps two rows of HBM traffic in flight across the barrier.
   const int tid = threadIdx.x;
   const int j = t.j0 + tid;
   const bool valid = j <= t.jend;
   const int gj = G.gj0 + (valid ? j : t.jend);
   const ColConst cc = load_col(Tb, gj);
   const int rpos = t.jend - t.j0 + 2;  // LDS ring index of the right halo column
+  const int ilast = t.iend + 1;
+  auto fetch = [&](int i, double& rv, double& po) {
+    rv = 0.0;
+    po = 0.0;
+    const int gi = G.gi0 + i;
+    if (valid && i <= ilast && gi > 0 && gi < G.M) {
+      rv = (i == 0) ? double(H.recv[0][j - 1])
+                    : (i == G.nx + 1) ? double(H.recv[1][j - 1]) : double(r[int64_t(i) * P + j]);
+      if (!first) po = double(pold[int64_t(i) * P + j]);
+    }
+  };
   double pm2 = 0.0, pm1 = 0.0;         // p^k at rows i-2, i-1
   double qa0 = 0.0, qa1 = 0.0, qb0 = 0.0, qb1 = 0.0;  // coefficients of row i-1
   double acc = 0.0;
-  for (int i = t.i0 - 1; i <= t.iend + 1; ++i) {
+  double rv_c, po_c;
+  fetch(t.i0 - 1, rv_c, po_c);
+  RowConst rc = load_row(Tb, G.gi0 + t.i0 - 1);
+  for (int i = t.i0 - 1; i <= ilast; ++i) {
+    double rv_n, po_n;
+    fetch(i + 1, rv_n, po_n);
+    const RowConst rc_n = load_row(Tb, G.gi0 + min(i + 1, ilast));
     const int gi = G.gi0 + i;
-    const RowConst rc = load_row(Tb, gi);
     const double a0 = face_a(cc, rc.rv0, G), a1 = face_a(cc, rc.rv1, G);
     const double b0 = face_b(rc, cc.rh0, G), b1 = face_b(rc, cc.rh1, G);
     double pc = 0.0;
     const int slot = (i - t.i0 + 1) % 3;
     if (valid) {
       if (gi > 0 && gi < G.M) {
-        double rv;
-        if (i == 0) rv = H.recv[0][j - 1];
-        else if (i == G.nx + 1) rv = H.recv[1][j - 1];
-        else rv = r[int64_t(i) * P + j];
-        const double z = rv / diag<EXACT>(a0, a1, b0, b1, G);
-        pc = first ? z : z + beta * double(pold[int64_t(i) * P + j]);
+        const double z = rv_c / diag<EXACT>(a0, a1, b0, b1, G);
+        pc = first ? z : z + beta * po_c;
         const bool own = i >= t.i0 && i <= t.iend;
         const bool ghost = (i == 0 && (G.nb & kNbXlo)) || (i == G.nx + 1 && (G.nb & kNbXhi));
         if (own || ghost) pnew[int64_t(i) * P + j] = static_cast<T>(pc);
@@ -189,6 +209,7 @@ k_pcg_a(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, HaloBufs
     }
     pm2 = pm1; pm1 = pc;
     qa0 = a0; qa1 = a1; qb0 = b0; qb1 = b1;
+    rv_c = rv_n; po_c = po_n; rc = rc_n;
   }
   double unused = 0.0;
   block_sum2<BLOCK>(acc, unused, lds);
@@ -223,22 +244,32 @@ k_pcg_b(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, const T* 
   const int j = t.j0 + threadIdx.x;
   double dacc = 0.0, zacc = 0.0;
   if (j <= t.jend) {
+    // software-pipelined march: row i+1's five loads are in flight while row i is computed
     const int64_t P = G.pitch;
     const int gj = G.gj0 + j;
     const ColConst cc = load_col(Tb, gj);
     double pm = double(pn[int64_t(t.i0 - 1) * P + j]);
-    double pc = double(pn[int64_t(t.i0) * P + j]);
-    double acur = face_a(cc, Tb.rv[G.gi0 + t.i0], G);
+    int64_t c = int64_t(t.i0) * P + j;
+    double pc = double(pn[c]);
+    double pp = double(pn[c + P]), pjm = double(pn[c - 1]), pjp = double(pn[c + 1]);
+    double wo = double(w[c]), ro = double(r[c]);
+    RowConst rc = load_row(Tb, G.gi0 + t.i0);
+    double acur = face_a(cc, rc.rv0, G);
     for (int i = t.i0; i <= t.iend; ++i) {
-      const int64_t c = int64_t(i) * P + j;
-      const double pp = double(pn[c + P]);
-      const double pjm = double(pn[c - 1]), pjp = double(pn[c + 1]);
-      const int gi = G.gi0 + i;
-      const RowConst rc = load_row(Tb, gi);
+      const int64_t cn = c + P;
+      const bool more = i < t.iend;
+      double pp_n = 0.0, pjm_n = 0.0, pjp_n = 0.0, wo_n = 0.0, ro_n = 0.0;
+      if (more) {
+        pp_n = double(pn[cn + P]);
+        pjm_n = double(pn[cn - 1]);
+        pjp_n = double(pn[cn + 1]);
+        wo_n = double(w[cn]);
+        ro_n = double(r[cn]);
+      }
+      const RowConst rc_n = load_row(Tb, G.gi0 + (more ? i + 1 : i));
       const double a0 = acur, a1 = face_a(cc, rc.rv1, G);
       const double b0 = face_b(rc, cc.rh0, G), b1 = face_b(rc, cc.rh1, G);
       const double Ap = apply_a<EXACT>(pc, pm, pp, pjm, pjp, a0, a1, b0, b1, G);
-      const double wo = double(w[c]), ro = double(r[c]);
       const T ws = static_cast<T>(wo + alpha * pc);
       const T rs = static_cast<T>(ro - alpha * Ap);
       const double dw = double(ws) - wo;
@@ -253,6 +284,8 @@ k_pcg_b(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, const T* 
       if (j == 1 && (G.nb & kNbYlo)) H.send[2][i - 1] = rs;
       if (j == G.ny && (G.nb & kNbYhi)) H.send[3][i - 1] = rs;
       pm = pc; pc = pp; acur = a1;
+      pp = pp_n; pjm = pjm_n; pjp = pjp_n; wo = wo_n; ro = ro_n; rc = rc_n;
+      c = cn;
     }
   }
   block_sum2<BLOCK>(dacc, zacc, lds);
@@ -265,21 +298,32 @@ k_pcg_b(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, const T* 
 // ---------------------------------------------------------------------------
 // deterministic single-block finish of block partials
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256)
-k_reduce(const double* __restrict__ part, int n, int nq, double w0, double w1, double* out,
-         PcgState* S, int mode) {
-  __shared__ double lds[2 * 256 / kWave];
+template <int NQ>
+__global__ void __launch_bounds__(1024)
+k_reduce(const double* __restrict__ part, int n, double w0, double w1, double* out, PcgState* S,
+         int mode) {
+  __shared__ double lds[2 * 1024 / kWave];
   if ((mode & kSkipIfDone) && S->done) return;
-  double s0 = 0.0, s1 = 0.0;
-  for (int i = threadIdx.x; i < n; i += 256) {
-    s0 += part[int64_t(i) * nq];
-    if (nq == 2) s1 += part[int64_t(i) * nq + 1];
+  double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
+  int i = threadIdx.x;
+  for (; i + 3 * 1024 < n; i += 4 * 1024) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      s0[u] += part[int64_t(i + u * 1024) * NQ];
+      if (NQ == 2) s1[u] += part[int64_t(i + u * 1024) * NQ + 1];
+    }
   }
-  block_sum2<256>(s0, s1, lds);
+  for (; i < n; i += 1024) {
+    s0[0] += part[int64_t(i) * NQ];
+    if (NQ == 2) s1[0] += part[int64_t(i) * NQ + 1];
+  }
+  double a = (s0[0] + s0[1]) + (s0[2] + s0[3]);
+  double b = (s1[0] + s1[1]) + (s1[2] + s1[3]);
+  block_sum2<1024>(a, b, lds);
   if (threadIdx.x == 0) {
-    out[0] = s0 * w0;
-    if (nq == 2) out[1] = s1 * w1;
-    if (!(s0 == s0) || !(s1 == s1) || isinf(s0) || isinf(s1)) S->nan_flag = 1;
+    out[0] = a * w0;
+    if (NQ == 2) out[1] = b * w1;
+    if (!(a == a) || !(b == b) || isinf(a) || isinf(b)) S->nan_flag = 1;
     if (mode & kBumpIter) S->it += 1;
   }
 }
@@ -347,7 +391,8 @@ void launch_pcg_b(const DevGeom& G, const DevTables& Tb, T* w, T* r, const T* p0
 void launch_reduce(const double* partials, int n, int nq, double w0, double w1, double* out,
                    PcgState* S, int mode, hipStream_t s) {
   PMX_CHECK(nq == 1 || nq == 2, "nq must be 1 or 2");
-  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(256), 0, s, partials, n, nq, w0, w1, out, S, mode);
+  if (nq == 1) hipLaunchKernelGGL(k_reduce<1>, dim3(1), dim3(1024), 0, s, partials, n, w0, w1, out, S, mode);
+  else hipLaunchKernelGGL(k_reduce<2>, dim3(1), dim3(1024), 0, s, partials, n, w0, w1, out, S, mode);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -37,8 +37,11 @@ DevTables upload_tables(const ProblemSpec& spec, double** owner);
 
 struct GpuOptions {
   int device = 0;
-  int block = 256;        // tile width (threads per workgroup)
-  int tile_rows = 64;     // tile height (marching length)
+  int kernel = 1;         // 0: LDS-ring workgroup tiles, 1: wave tiles with DPP lane shifts
+  int block = 256;        // kernel 0: tile width (threads per workgroup)
+  int vec = 2;            // kernel 1: columns per lane (2 x fp64 = 16-B accesses)
+  int waves = 4;          // kernel 1: wave tiles per workgroup
+  int tile_rows = 0;      // tile height (marching length), 0 = auto-size for occupancy
   DType dtype = DType::kFp64;
   bool exact = false;     // reference arithmetic order inside the fused kernels
   int graph_batch = 32;   // iterations per captured hipGraph (0 = eager launches)
@@ -107,6 +110,7 @@ class GpuSubdomainSolver {
   DevGeom geom_{};
   DevTables tables_{};
   TileCfg tiles_{};
+  TileCfg init_tiles_{};
   CommLayout layout_{};
   size_t elem_ = 8, field_bytes_ = 0, field_off_ = 0;
   char* fields_ = nullptr;  // 4 fields

@@ -17,13 +17,18 @@
 namespace pmx {
 
 struct TileCfg {
-  int block = 256;    // columns per tile = threads per block (multiple of 64)
-  int rows = 64;      // rows per tile (marching length)
+  int kind = 0;       // 0: workgroup tile + LDS row ring (pcg_kernels.hip)
+                      // 1: wave tile + DPP lane shifts (pcg_kernels_dpp.hip)
+  int block = 256;    // columns per tile (kind 0: = threads per block; kind 1: = 64*vec)
+  int rows = 0;       // rows per tile (marching length); 0 = auto
+  int vec = 1;        // kind 1: columns per lane
+  int waves = 1;      // kind 1: independent wave tiles per workgroup
   int tiles_i = 0, tiles_j = 0;
   int ntiles() const { return tiles_i * tiles_j; }
 };
 
 TileCfg make_tiles(const DevGeom& G, int block, int rows);
+TileCfg make_wave_tiles(const DevGeom& G, int vec, int waves, int rows);
 
 enum ReduceMode : int { kSkipIfDone = 1, kBumpIter = 2 };
 
@@ -39,6 +44,15 @@ template <typename T>
 void launch_pcg_b(const DevGeom& G, const DevTables& Tb, T* w, T* r, const T* p0, const T* p1,
                   HaloBufs<T> H, double* partials, PcgState* S, const TileCfg& tc, bool exact,
                   hipStream_t s);
+
+template <typename T>
+void launch_pcg_a_wave(const DevGeom& G, const DevTables& Tb, const T* r, T* p0, T* p1,
+                       HaloBufs<T> H, double* partials, PcgState* S, const TileCfg& tc, bool exact,
+                       hipStream_t s);
+template <typename T>
+void launch_pcg_b_wave(const DevGeom& G, const DevTables& Tb, T* w, T* r, const T* p0,
+                       const T* p1, HaloBufs<T> H, double* partials, PcgState* S,
+                       const TileCfg& tc, bool exact, hipStream_t s);
 
 void launch_reduce(const double* partials, int n, int nq, double w0, double w1, double* out,
                    PcgState* S, int mode, hipStream_t s);

@@ -31,8 +31,8 @@ from .launch import DistInfo
 
 class DistGpuPCG:
     def __init__(self, problem, info: DistInfo, comm: str = "native", split: str = "reference",
-                 dtype: str = "fp64", block: int = 256, tile_rows: int = 64, exact: bool = False,
-                 graph_batch: int = 32, rccl_graph: bool = False):
+                 dtype: str = "fp64", kernel: str = "wave", block: int = 256, vec: int = 2, waves: int = 4,
+                 tile_rows: int = 0, exact: bool = False, graph_batch: int = 32, rccl_graph: bool = False):
         self.problem = problem
         self.info = info
         self.comm_kind = comm
@@ -48,7 +48,8 @@ class DistGpuPCG:
                 dist.broadcast_object_list(uid, src=0)
             self.session = self.n.Session(self.spec, world=info.world, comm="rccl",
                                           split=getattr(self.n.Split, split), device=self.device,
-                                          block=block, tile_rows=tile_rows, dtype=dtype, exact=exact,
+                                          kernel=kernel, block=block, vec=vec, waves=waves,
+                                          tile_rows=tile_rows, dtype=dtype, exact=exact,
                                           graph_batch=graph_batch if rccl_graph else 0, uid=uid[0],
                                           ranks=[info.rank], devices=[self.device], rccl_graph=rccl_graph)
             self.sd = self.session.subdomain(0)
@@ -59,8 +60,8 @@ class DistGpuPCG:
             pad = (-base) % 256
             self.arena_view = self.arena[pad:pad + lay["bytes"]]
             self.solver = self.n.SubdomainSolver(self.spec, self.Px, self.Py, info.rank, device=self.device,
-                                                 block=block, tile_rows=tile_rows, dtype=dtype, exact=exact,
-                                                 arena=base + pad)
+                                                 kernel=kernel, block=block, vec=vec, waves=waves,
+                                                 tile_rows=tile_rows, dtype=dtype, exact=exact, arena=base + pad)
             self.sd = self.solver.subdomain()
             tdt = torch.float64 if dtype == "fp64" else torch.float32
             el = lay["elem"]

@@ -31,6 +31,7 @@ ARCH = os.environ.get("PMX_ARCH", "gfx950")
 
 HIP_SOURCES = [
     "hip/pcg_kernels.hip",
+    "hip/pcg_kernels_dpp.hip",
     "hip/ops_kernels.hip",
     "hip/gpu_solver.hip",
     "hip/session.hip",
@@ -42,6 +43,8 @@ BIND_SOURCES = ["bindings/module.cpp"]
 COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC / 'include'}", "-Wall", "-Wno-unused-result"]
 HIP_FLAGS = [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
 CPU_FLAGS = ["-fopenmp", "-ffp-contract=off"]
+# host-only translation units that use the HIP runtime API (bindings, CLI): plain g++
+HOST_HIP_FLAGS = ["-D__HIP_PLATFORM_AMD__", "-DPMX_WITH_HIP", f"-I{ROCM / 'include'}"]
 
 
 def _headers():
@@ -77,7 +80,7 @@ def _compile(src: str, kind: str, verbose: bool, force: bool) -> Path:
         import pybind11
 
         py_inc = sysconfig.get_paths()["include"]
-        cmd = [HIPCC, *COMMON_FLAGS, "-D__HIP_PLATFORM_AMD__", f"-I{pybind11.get_include()}", f"-I{py_inc}",
+        cmd = ["g++", *COMMON_FLAGS, *HOST_HIP_FLAGS, f"-I{pybind11.get_include()}", f"-I{py_inc}",
                "-fvisibility=hidden", "-c", srcp, "-o", obj]
     else:
         cmd = ["g++", *COMMON_FLAGS, *CPU_FLAGS, "-c", srcp, "-o", obj]
@@ -112,7 +115,9 @@ def _build_apps(core_objs, link_libs, verbose, force):
     app_src = CSRC / "apps" / "pmx.cpp"
     exe = BIN_DIR / "pmx"
     if app_src.exists() and (force or _stale(exe, [app_src, lib] + _headers())):
-        _run([HIPCC, *COMMON_FLAGS, "-D__HIP_PLATFORM_AMD__", app_src, lib, "-o", exe, *link_libs], verbose)
+        app_obj = BUILD_DIR / "apps_pmx.o"
+        _run(["g++", *COMMON_FLAGS, *HOST_HIP_FLAGS, "-c", app_src, "-o", app_obj], verbose)
+        _run([HIPCC, app_obj, lib, "-o", exe, *link_libs], verbose)
     mpi_src = CSRC / "apps" / "pmx_mpi.cpp"
     mpicxx = shutil.which("mpicxx") or ("/opt/conda/bin/mpicxx" if Path("/opt/conda/bin/mpicxx").exists() else None)
     exe_mpi = BIN_DIR / "pmx_mpi"

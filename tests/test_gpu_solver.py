@@ -60,18 +60,46 @@ def test_local_comm_decomposition(pkg, ranks):
 def test_local_comm_splits_and_tiles(pkg, split):
     p = pkg.PoissonEllipse(M=300, N=700)
     ref = pkg.solve(p, "cpu")
-    r = pkg.solve(p, "hip", ranks=6, split=split, tile_rows=17, block=128)
+    r = pkg.solve(p, "hip", ranks=6, split=split, tile_rows=17, kernel="lds", block=128)
     assert r.iters == ref.iters
     assert np.abs(r.w - ref.w).max() < 1e-10
 
 
 @pytest.mark.parametrize("block,rows", [(128, 1), (256, 64), (512, 256), (256, 7)])
-def test_tile_shapes(pkg, block, rows):
+def test_lds_tile_shapes(pkg, block, rows):
     p = pkg.PoissonEllipse(M=211, N=1031)
     ref = pkg.solve(p, "hip")
-    r = pkg.solve(p, "hip", block=block, tile_rows=rows)
+    r = pkg.solve(p, "hip", kernel="lds", block=block, tile_rows=rows)
     assert r.iters == ref.iters
     assert np.abs(r.w - ref.w).max() < 1e-12
+
+
+@pytest.mark.parametrize("vec,waves,rows", [(1, 4, 1), (2, 4, 64), (2, 1, 5), (2, 8, 33), (1, 4, 0), (2, 4, 0)])
+@pytest.mark.parametrize("grid", [(211, 1031), (97, 130), (300, 257)])
+def test_wave_tile_shapes(pkg, vec, waves, rows, grid):
+    """Wave-tile kernels on full and partial tiles (odd widths leave half-filled lanes)."""
+    p = pkg.PoissonEllipse(M=grid[0], N=grid[1])
+    ref = pkg.solve(p, "hip", kernel="lds")
+    r = pkg.solve(p, "hip", kernel="wave", vec=vec, waves=waves, tile_rows=rows)
+    assert r.iters == ref.iters
+    assert np.abs(r.w - ref.w).max() < 1e-12
+
+
+def test_wave_fp32_vec4(pkg):
+    p = pkg.PoissonEllipse(M=400, N=600)
+    a = pkg.solve(p, "hip", kernel="lds", dtype="fp32")
+    b = pkg.solve(p, "hip", kernel="wave", vec=4, dtype="fp32")
+    assert abs(a.iters - b.iters) <= 3
+    assert np.abs(a.w - b.w).max() < 1e-5
+
+
+@pytest.mark.parametrize("ranks", [2, 4, 7])
+def test_wave_kernels_decomposed(pkg, ranks):
+    p = pkg.PoissonEllipse(M=260, N=390)
+    ref = pkg.solve(p, "hip", kernel="lds")
+    r = pkg.solve(p, "hip", kernel="wave", ranks=ranks)
+    assert r.iters == ref.iters
+    assert np.abs(r.w - ref.w).max() < 1e-11
 
 
 def test_graph_vs_eager(pkg):
