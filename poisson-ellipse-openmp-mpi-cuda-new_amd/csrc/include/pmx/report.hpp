@@ -84,7 +84,7 @@ inline void print_converged(int64_t k, double delta, bool stage0) {
 struct JsonLine {
   std::ostringstream os;
   bool first = true;
-  JsonLine() { os << '{'; }
+  JsonLine() { os << std::setprecision(10) << '{'; }
   template <typename V>
   JsonLine& kv(const std::string& k, const V& v) {
     os << (first ? "" : ", ") << '"' << k << "\": " << v;

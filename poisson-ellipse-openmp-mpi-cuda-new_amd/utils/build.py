@@ -119,14 +119,37 @@ def _build_apps(core_objs, link_libs, verbose, force):
         _run(["g++", *COMMON_FLAGS, *HOST_HIP_FLAGS, "-c", app_src, "-o", app_obj], verbose)
         _run([HIPCC, app_obj, lib, "-o", exe, *link_libs], verbose)
     mpi_src = CSRC / "apps" / "pmx_mpi.cpp"
-    mpicxx = shutil.which("mpicxx") or ("/opt/conda/bin/mpicxx" if Path("/opt/conda/bin/mpicxx").exists() else None)
     exe_mpi = BIN_DIR / "pmx_mpi"
-    if mpi_src.exists() and mpicxx and (force or _stale(exe_mpi, [mpi_src, CSRC / "cpu" / "cpu_pcg.cpp"] + _headers())):
+    mpi = _mpi_flags()
+    if mpi_src.exists() and mpi and (force or _stale(exe_mpi, [mpi_src, CSRC / "cpu" / "cpu_pcg.cpp"] + _headers())):
         try:
-            _run([mpicxx, "-O3", "-std=c++17", "-fopenmp", "-ffp-contract=off", f"-I{CSRC / 'include'}", mpi_src,
-                  CSRC / "cpu" / "cpu_pcg.cpp", "-o", exe_mpi], verbose)
+            _run(["g++", "-O3", "-std=c++17", "-fopenmp", "-ffp-contract=off", f"-I{CSRC / 'include'}", *mpi[0],
+                  mpi_src, CSRC / "cpu" / "cpu_pcg.cpp", "-o", exe_mpi, *mpi[1]], verbose)
         except RuntimeError as e:  # MPI is optional (stage-2/3 parity only)
             print(f"[pmx build] skipping pmx_mpi: {e}", file=sys.stderr)
+
+
+def _mpi_flags():
+    """(cflags, ldflags) of an MPI installation, using the host g++ (the conda mpicxx wrapper
+    points at a cross compiler that is not installed).  The MPI runtime libraries are reached
+    through symlinks in bin/mpilib so that the executable's RUNPATH does not expose the MPI
+    prefix's (older) libstdc++.  None when no MPI is found."""
+    for root in [os.environ.get("MPI_HOME"), "/opt/conda", "/usr/lib/x86_64-linux-gnu/openmpi", "/usr"]:
+        if not root:
+            continue
+        inc, lib = Path(root) / "include", Path(root) / "lib"
+        so = sorted(lib.glob("libmpi.so.[0-9]*"))
+        if not ((inc / "mpi.h").exists() and so):
+            continue
+        priv = BIN_DIR / "mpilib"
+        priv.mkdir(parents=True, exist_ok=True)
+        for pattern in ("libmpi.so.[0-9]*", "libgfortran.so.[0-9]*", "libquadmath.so.[0-9]*"):
+            for f in lib.glob(pattern):
+                link = priv / f.name
+                if not link.exists():
+                    link.symlink_to(f)
+        return [f"-I{inc}"], [str(so[0]), "-Wl,-rpath,$ORIGIN/mpilib"]
+    return None
 
 
 def extension_built() -> bool:

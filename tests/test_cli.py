@@ -1,0 +1,98 @@
+"""C++ front ends: `pmx` (reference-compatible stdout, ASCII dump, JSON) and `pmx_mpi` (stage 2/3)."""
+import json
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+BIN = os.path.join(ROOT, "poisson-ellipse-openmp-mpi-cuda-new_amd", "bin")
+
+
+def run(args, **kw):
+    p = subprocess.run(args, capture_output=True, text=True, timeout=300, **kw)
+    assert p.returncode == 0, p.stderr
+    return p.stdout
+
+
+@pytest.fixture(scope="module")
+def pmx_bin(pkg):
+    exe = os.path.join(BIN, "pmx")
+    if not os.path.exists(exe):
+        import importlib
+
+        importlib.import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.utils.build").build()
+    return exe
+
+
+def test_stage0_format(pmx_bin):
+    out = run([pmx_bin, "40", "40", "--backend", "cpu", "--norm", "unweighted", "--banner", "stage0"])
+    lines = out.strip().splitlines()
+    assert lines[0] == "Converged after 61 iterations (||w(k+1)-w(k)|| < δ)."
+    assert lines[1].startswith("M=40, N=40 | Iter=61 | Time=")
+
+
+def test_stage2_format(pmx_bin):
+    out = run([pmx_bin, "40", "40", "--backend", "cpu", "--ranks", "4"])
+    lines = out.strip().splitlines()
+    assert lines[0] == "Pure MPI 2D run with 4 processes; M=40, N=40"
+    assert lines[1] == "Converged after 50 iterations (||w(k+1)-w(k)|| < 1e-06)."
+    assert lines[2].startswith("M=40, N=40 | Iter=50 | Time=")
+
+
+def test_stage1_and_stage3_format(pmx_bin):
+    out = run([pmx_bin, "40", "40", "--backend", "omp", "--threads", "2", "--banner", "stage1"])
+    assert "--- (Variant 9: Ellipse x^2 + 4y^2 < 1, OpenMP Test) ---" in out and "Threads =  2 | Time =" in out
+    out = run([pmx_bin, "40", "40", "--backend", "omp", "--threads", "2", "--ranks", "2"])
+    assert out.startswith("MPI/OpenMP run with 2 MPI processes; M=40, N=40")
+
+
+def test_json_and_ascii_dump(pmx_bin, tmp_path, pkg):
+    f = tmp_path / "sol.txt"
+    out = run([pmx_bin, "120", "90", "--backend", "omp", "--threads", "2", "--json", "--dump", str(f)])
+    js = json.loads(out.strip().splitlines()[-1])
+    p = pkg.PoissonEllipse(M=120, N=90)
+    ref = pkg.solve(p, "cpu")
+    assert js["iters"] == ref.iters
+    assert abs(js["l2_error"] - p.error_norms(ref.w)["l2_error"]) < 1e-9
+    rows = [l for l in f.read_text().splitlines() if l and not l.startswith("#")]
+    data = np.array([[float(v) for v in l.split()] for l in rows])
+    assert data.shape == ((p.M + 1) * (p.N + 1), 5)
+    w = data[:, 2].reshape(p.M + 1, p.N + 1)
+    assert np.abs(w - ref.w).max() < 1e-9
+    assert np.allclose(data[:, 4], data[:, 2] - data[:, 3])
+    assert "L2_error_in_D" in f.read_text().splitlines()[-1]
+
+
+def test_cli_overrides(pmx_bin):
+    out = run([pmx_bin, "60", "60", "--backend", "cpu", "--ax", "0.8", "--by", "0.4", "--delta", "1e-5",
+               "--max-iter", "500", "--json"])
+    js = json.loads(out.strip().splitlines()[-1])
+    assert js["status"] == "converged" and js["iters"] < 500
+
+
+def test_cli_rejects_bad_args(pmx_bin):
+    p = subprocess.run([pmx_bin, "40"], capture_output=True, text=True)
+    assert p.returncode == 2 and "usage" in p.stderr
+
+
+def _mpiexec():
+    for c in (shutil.which("mpiexec"), "/opt/conda/bin/mpiexec"):
+        if c and os.path.exists(c):
+            return c
+    return None
+
+
+@pytest.mark.skipif(_mpiexec() is None, reason="no MPI launcher")
+@pytest.mark.parametrize("np_,threads", [(2, 1), (3, 1), (4, 2)])
+def test_pmx_mpi(pmx_bin, np_, threads):
+    exe = os.path.join(BIN, "pmx_mpi")
+    if not os.path.exists(exe):
+        pytest.skip("pmx_mpi not built (no MPI found at build time)")
+    out = run([_mpiexec(), "-n", str(np_), exe, "400", "600", "--threads", str(threads), "--json"])
+    js = json.loads(out.strip().splitlines()[-1])
+    assert js["iters"] == 546 and js["ranks"] == np_
+    assert abs(js["l2_error"] - 3.0607e-4) < 1e-7
