@@ -53,6 +53,33 @@ k_march5(const double* p, double* w, double* r, int n, int pitch, int rows, int 
   }
 }
 
+// wave tiles: each wave marches `rows` rows of a (64*VEC)-column strip; layout 0 = row-major
+// (pitch), layout 1 = panel-major (each strip's rows contiguous: one sequential stream per wave)
+template <int VEC>
+__global__ void __launch_bounds__(256)
+k_wavemarch5(const double* p, double* w, double* r, int n, int pitch, int rows, int tiles_j,
+             int layout, double al) {
+  constexpr int W = 64 * VEC;
+  const int wid = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63;
+  const int ti = wid / tiles_j, tj = wid % tiles_j;
+  const int i0 = ti * rows;
+  if (i0 >= n) return;
+  for (int i = i0; i < i0 + rows && i < n; ++i) {
+    size_t c;
+    if (layout == 0) c = size_t(i) * pitch + tj * W + lane * VEC;
+    else c = (size_t(tj) * n + i) * W + lane * VEC;
+#pragma unroll
+    for (int u = 0; u < VEC; u += 2) {
+      double2 pv = *(const double2*)(p + c + u), wv = *(double2*)(w + c + u), rv = *(double2*)(r + c + u);
+      wv.x += al * pv.x; wv.y += al * pv.y;
+      rv.x -= al * pv.y; rv.y -= al * pv.x;
+      *(double2*)(w + c + u) = wv;
+      *(double2*)(r + c + u) = rv;
+    }
+  }
+}
+
 // one block per (row, 512-col chunk); block b -> XCD b%8 gets rows [xcd*n/8, (xcd+1)*n/8)
 __global__ void __launch_bounds__(256)
 k_rowband5(const double* p, double* w, double* r, int n, int pitch, int chunks, double al, int xcd_aware) {
@@ -100,7 +127,7 @@ int main(int argc, char** argv) {
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     ms /= reps;
-    printf("{\"kernel\": \"%s\", \"n\": %d, \"ms\": %.4f, \"TBps\": %.3f}\n", name, n, ms, gb / ms * 1e-3);
+    printf("{\"kernel\": \"%s\", \"n\": %d, \"ms\": %.4f, \"TBps\": %.3f}\n", name, n, ms, gb / ms);
   };
   const size_t n2 = elems / 2;
   const double gb_copy = 2.0 * bytes / 1e9, gb5 = 5.0 * bytes / 1e9;
@@ -112,6 +139,22 @@ int main(int argc, char** argv) {
     char name[64];
     snprintf(name, sizeof name, "march5_rows%d", rw);
     timeit(name, gb5, [&] { hipLaunchKernelGGL(k_march5, dim3(tiles_i * tiles_j), dim3(256), 0, 0, p, w, r, n, pitch, rw, tiles_j, 0.5); });
+  }
+  for (int layout : {0, 1}) {
+    for (int rw : {64, 16}) {
+      {
+        const int tj = n / 128, waves = tj * ((n + rw - 1) / rw);
+        char name[96];
+        snprintf(name, sizeof name, "wavemarch5_v2_rows%d_%s", rw, layout ? "panel" : "rowmajor");
+        timeit(name, gb5, [&] { hipLaunchKernelGGL((k_wavemarch5<2>), dim3((waves + 3) / 4), dim3(256), 0, 0, p, w, r, n, pitch, rw, tj, layout, 0.5); });
+      }
+      {
+        const int tj = n / 512, waves = tj * ((n + rw - 1) / rw);
+        char name[96];
+        snprintf(name, sizeof name, "wavemarch5_v8_rows%d_%s", rw, layout ? "panel" : "rowmajor");
+        timeit(name, gb5, [&] { hipLaunchKernelGGL((k_wavemarch5<8>), dim3((waves + 3) / 4), dim3(256), 0, 0, p, w, r, n, pitch, rw, tj, layout, 0.5); });
+      }
+    }
   }
   const int chunks = n / 512;
   timeit("rowband5_rowmajor", gb5, [&] { hipLaunchKernelGGL(k_rowband5, dim3(n * chunks), dim3(256), 0, 0, p, w, r, n, pitch, chunks, 0.5, 0); });

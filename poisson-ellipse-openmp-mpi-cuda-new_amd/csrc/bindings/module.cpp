@@ -336,6 +336,12 @@ PYBIND11_MODULE(_pmx, m) {
              return stats_dict(r);
            })
       .def("state", [](Session& s, int i) { return state_dict(s.state(i)); }, py::arg("i") = 0)
+      .def("bench_kernel", [](Session& s, int which, int abl, int reps) {
+             py::gil_scoped_release g;
+             s.synchronize();
+             return s.solver(0).bench_kernel(which, abl, reps, nullptr);
+           }, py::arg("which"), py::arg("abl") = 0, py::arg("reps") = 20,
+           "time k_pcg_a (0) / k_pcg_b (1) alone; invalidates the solver state")
       .def("gather_local_w", [](Session& s) {
              const auto& sp = s.solver(0).spec();
              return to_numpy(s.gather_local_w(), {sp.M + 1, sp.N + 1});

@@ -36,6 +36,8 @@ DevGeom make_dev_geom(const ProblemSpec& spec, const Subdomain& sd, int64_t pitc
   G.h1 = g.h1; G.h2 = g.h2; G.eps = g.eps; G.inv_eps = g.inv_eps; G.h1h2 = g.h1h2;
   G.cx = 1.0 / (g.h1 * g.h1);
   G.cy = 1.0 / (g.h2 * g.h2);
+  G.dinv_in = 1.0 / ((1.0 + 1.0) * G.cx + (1.0 + 1.0) * G.cy);
+  G.dinv_out = 1.0 / ((g.inv_eps + g.inv_eps) * G.cx + (g.inv_eps + g.inv_eps) * G.cy);
   G.ax = spec.ax; G.by = spec.by; G.F = spec.F;
   return G;
 }
@@ -44,8 +46,9 @@ DevTables upload_tables(const ProblemSpec& spec, double** owner) {
   const GridInfo g(spec);
   const geo::FaceTables ft(spec, g);
   const size_t nxT = spec.M + 2, nyT = spec.N + 2;
-  HIP_CHECK(hipMalloc(owner, (4 * nxT + 4 * nyT) * sizeof(double)));
-  std::vector<double> host(4 * nxT + 4 * nyT);
+  const size_t ndbl = 4 * nxT + 4 * nyT, nint = 8 * nxT;
+  HIP_CHECK(hipMalloc(owner, ndbl * sizeof(double) + nint * sizeof(int)));
+  std::vector<double> host(ndbl);
   double* h = host.data();
   std::memcpy(h + 0 * nxT, ft.rv.data(), nxT * 8);
   std::memcpy(h + 1 * nxT, ft.xlo.data(), nxT * 8);
@@ -56,10 +59,18 @@ DevTables upload_tables(const ProblemSpec& spec, double** owner) {
   std::memcpy(hy + 1 * nyT, ft.ylo.data(), nyT * 8);
   std::memcpy(hy + 2 * nyT, ft.yhi.data(), nyT * 8);
   std::memcpy(hy + 3 * nyT, ft.y.data(), nyT * 8);
-  HIP_CHECK(hipMemcpy(*owner, host.data(), host.size() * 8, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(*owner, host.data(), ndbl * 8, hipMemcpyHostToDevice));
   const double* d = *owner;
   const double* dy = d + 4 * nxT;
-  return DevTables{d, d + nxT, d + 2 * nxT, d + 3 * nxT, dy, dy + nyT, dy + 2 * nyT, dy + 3 * nyT};
+  int* cls = reinterpret_cast<int*>(*owner + ndbl);
+  DevTables T{d, d + nxT, d + 2 * nxT, d + 3 * nxT, dy, dy + nyT, dy + 2 * nyT, dy + 3 * nyT,
+              cls, cls + 4 * nxT};
+  // classify every row on the device with the exact coefficient formulas
+  Subdomain whole;
+  whole.M = spec.M; whole.N = spec.N; whole.nx = spec.M - 1; whole.ny = spec.N - 1;
+  launch_classify(make_dev_geom(spec, whole, spec.N + 2), T, cls, cls + 4 * nxT, nullptr);
+  HIP_CHECK(hipDeviceSynchronize());
+  return T;
 }
 
 CommLayout GpuSubdomainSolver::comm_layout(const Subdomain& sd, DType dtype) {
@@ -90,7 +101,8 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
   elem_ = opt.dtype == DType::kFp64 ? 8 : 4;
   const size_t align_elems = 256 / elem_;
 
-  geom_ = make_dev_geom(spec, sd, int64_t(round_up(size_t(sd.ny + 2), align_elems)));
+  // +8 columns of padding: vector loads of VEC <= 4 columns starting at <= ny+1 stay in the row
+  geom_ = make_dev_geom(spec, sd, int64_t(round_up(size_t(sd.ny + 2 + 8), align_elems)));
   const DevGeom& G = geom_;
 
   // fields: element (li, lj) at base[li*pitch + lj]; base = alloc + (align-1) so that every
@@ -105,6 +117,7 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
   PMX_CHECK(opt.kernel == 0 || opt.kernel == 1, "kernel must be 0 (lds) or 1 (wave/dpp)");
   tiles_ = opt.kernel == 0 ? make_tiles(G, opt.block, opt.tile_rows)
                            : make_wave_tiles(G, opt.vec, opt.waves, opt.tile_rows);
+
   init_tiles_ = make_tiles(G, 256, 0);
   const size_t npart = size_t(std::max(tiles_.ntiles(), init_tiles_.ntiles()));
   HIP_CHECK(hipMalloc(&partials_, npart * 2 * sizeof(double)));
@@ -182,6 +195,14 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
 
 template <typename T>
 void GpuSubdomainSolver::phase_a_impl(hipStream_t s) {
+  phase_a_kernel_only<T>(s);
+  after_launch(s);
+  launch_reduce(partials_, tiles_.ntiles(), 1, g_.h1h2, 0.0, state_->red_a, state_, kSkipIfDone, s);
+  after_launch(s);
+}
+
+template <typename T>
+void GpuSubdomainSolver::phase_a_kernel_only(hipStream_t s) {
   if (tiles_.kind == 1)
     launch_pcg_a_wave<T>(geom_, tables_, static_cast<const T*>(field_base(1)),
                          static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(),
@@ -190,13 +211,20 @@ void GpuSubdomainSolver::phase_a_impl(hipStream_t s) {
     launch_pcg_a<T>(geom_, tables_, static_cast<const T*>(field_base(1)),
                     static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(),
                     partials_, state_, tiles_, opt_.exact, s);
-  after_launch(s);
-  launch_reduce(partials_, tiles_.ntiles(), 1, g_.h1h2, 0.0, state_->red_a, state_, kSkipIfDone, s);
-  after_launch(s);
 }
 
 template <typename T>
 void GpuSubdomainSolver::phase_b_impl(hipStream_t s) {
+  phase_b_kernel_only<T>(s);
+  after_launch(s);
+  const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
+  launch_reduce(partials_, tiles_.ntiles(), 2, wdiff, g_.h1h2, state_->red_b, state_,
+                kSkipIfDone | kBumpIter, s);
+  after_launch(s);
+}
+
+template <typename T>
+void GpuSubdomainSolver::phase_b_kernel_only(hipStream_t s) {
   if (tiles_.kind == 1)
     launch_pcg_b_wave<T>(geom_, tables_, static_cast<T*>(field_base(0)),
                          static_cast<T*>(field_base(1)), static_cast<const T*>(field_base(2)),
@@ -206,11 +234,6 @@ void GpuSubdomainSolver::phase_b_impl(hipStream_t s) {
     launch_pcg_b<T>(geom_, tables_, static_cast<T*>(field_base(0)), static_cast<T*>(field_base(1)),
                     static_cast<const T*>(field_base(2)), static_cast<const T*>(field_base(3)),
                     halo<T>(), partials_, state_, tiles_, opt_.exact, s);
-  after_launch(s);
-  const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
-  launch_reduce(partials_, tiles_.ntiles(), 2, wdiff, g_.h1h2, state_->red_b, state_,
-                kSkipIfDone | kBumpIter, s);
-  after_launch(s);
 }
 
 void GpuSubdomainSolver::enqueue_init(hipStream_t s) {
@@ -222,6 +245,55 @@ void GpuSubdomainSolver::enqueue_phase_a(hipStream_t s) {
 }
 void GpuSubdomainSolver::enqueue_phase_b(hipStream_t s) {
   if (opt_.dtype == DType::kFp64) phase_b_impl<double>(s); else phase_b_impl<float>(s);
+}
+
+double GpuSubdomainSolver::bench_kernel(int which, int abl, int reps, hipStream_t s) {
+  HIP_CHECK(hipSetDevice(opt_.device));
+  PcgState& st = host_state_[1];
+  std::memset(&st, 0, sizeof(st));
+  st.delta = 0.0;
+  st.it = 2;  // a mid-solve iteration: beta path, p^{k-1} read
+  st.max_iter = int64_t(1) << 40;
+  st.norm = int(spec_.norm);
+  st.red_a[0] = 1.0;
+  st.red_b[0] = 1.0;
+  st.red_b[1] = 1e-3;
+  st.zr[0] = st.zr[1] = 1e-3;
+  const TileCfg saved = tiles_;
+  tiles_.abl = abl;
+  auto launch = [&]() {
+    HIP_CHECK(hipMemcpyAsync(state_, &st, sizeof(PcgState), hipMemcpyHostToDevice, s));
+    if (which == 0) {
+      if (opt_.dtype == DType::kFp64) phase_a_kernel_only<double>(s); else phase_a_kernel_only<float>(s);
+    } else {
+      if (opt_.dtype == DType::kFp64) phase_b_kernel_only<double>(s); else phase_b_kernel_only<float>(s);
+    }
+  };
+  launch();
+  launch();
+  HIP_CHECK(hipStreamSynchronize(s));
+  hipEvent_t e0, e1;
+  HIP_CHECK(hipEventCreate(&e0));
+  HIP_CHECK(hipEventCreate(&e1));
+  float total = 0.f;
+  for (int k = 0; k < reps; ++k) {
+    HIP_CHECK(hipMemcpyAsync(state_, &st, sizeof(PcgState), hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipEventRecord(e0, s));
+    if (which == 0) {
+      if (opt_.dtype == DType::kFp64) phase_a_kernel_only<double>(s); else phase_a_kernel_only<float>(s);
+    } else {
+      if (opt_.dtype == DType::kFp64) phase_b_kernel_only<double>(s); else phase_b_kernel_only<float>(s);
+    }
+    HIP_CHECK(hipEventRecord(e1, s));
+    HIP_CHECK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    total += ms;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  tiles_ = saved;
+  return double(total) / reps;
 }
 
 PcgState GpuSubdomainSolver::read_state(hipStream_t s) const {

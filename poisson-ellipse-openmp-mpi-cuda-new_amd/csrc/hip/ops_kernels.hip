@@ -5,6 +5,8 @@
 // CDNA-friendly mapping: threadIdx.x runs along the contiguous axis lj (the reference maps it to
 // the strided li axis, :514-515), and coefficients come from the 1D face tables.  Used by the
 // unit tests (each op vs a PyTorch fp64 reference) and by the solver's `naive` kernel mode.
+#include <climits>
+
 #include "pcg_device.hpp"
 #include "pmx/common.hpp"
 #include "pmx/kernels.hpp"
@@ -68,6 +70,48 @@ k_dot_partials(DevGeom G, const T* __restrict__ x, const T* __restrict__ y, doub
   }
   block_sum2<256>(s, unused, lds);
   if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+// one workgroup per global row gi: out range (first/last j whose coefficient is not 1/eps) and
+// in range (first/last j equal to 1, kept only if every j between is exactly 1)
+__global__ void __launch_bounds__(256)
+k_classify(DevGeom G, DevTables Tb, int* acls, int* bcls) {
+  // acc: a out lo/hi, a in lo/hi, b out lo/hi, b in lo/hi, #a==1, #b==1
+  __shared__ int acc[10];
+  const int gi = blockIdx.x;
+  int ao_lo = INT_MAX, ao_hi = INT_MIN, ai_lo = INT_MAX, ai_hi = INT_MIN;
+  int bo_lo = INT_MAX, bo_hi = INT_MIN, bi_lo = INT_MAX, bi_hi = INT_MIN;
+  int na1 = 0, nb1 = 0;
+  if (threadIdx.x < 10)
+    acc[threadIdx.x] = threadIdx.x >= 8 ? 0 : (threadIdx.x % 2 == 0 ? INT_MAX : INT_MIN);
+  __syncthreads();
+  for (int j = threadIdx.x; j <= G.N + 1; j += 256) {
+    const double a = coef_a(Tb, G, gi, j);
+    const double b = coef_b(Tb, G, gi, j);
+    if (a != G.inv_eps) { ao_lo = min(ao_lo, j); ao_hi = max(ao_hi, j); }
+    if (a == 1.0) { ai_lo = min(ai_lo, j); ai_hi = max(ai_hi, j); ++na1; }
+    if (b != G.inv_eps) { bo_lo = min(bo_lo, j); bo_hi = max(bo_hi, j); }
+    if (b == 1.0) { bi_lo = min(bi_lo, j); bi_hi = max(bi_hi, j); ++nb1; }
+  }
+  atomicMin(&acc[0], ao_lo); atomicMax(&acc[1], ao_hi);
+  atomicMin(&acc[2], ai_lo); atomicMax(&acc[3], ai_hi);
+  atomicMin(&acc[4], bo_lo); atomicMax(&acc[5], bo_hi);
+  atomicMin(&acc[6], bi_lo); atomicMax(&acc[7], bi_hi);
+  atomicAdd(&acc[8], na1); atomicAdd(&acc[9], nb1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int* A = acls + 4 * gi;
+    int* B = bcls + 4 * gi;
+    const bool a_contig = acc[8] > 0 && acc[8] == acc[3] - acc[2] + 1;
+    const bool b_contig = acc[9] > 0 && acc[9] == acc[7] - acc[6] + 1;
+    A[0] = acc[0]; A[1] = a_contig ? acc[2] : 1; A[2] = a_contig ? acc[3] : 0; A[3] = acc[1];
+    B[0] = acc[4]; B[1] = b_contig ? acc[6] : 1; B[2] = b_contig ? acc[7] : 0; B[3] = acc[5];
+  }
+}
+
+void launch_classify(const DevGeom& G, const DevTables& Tb, int* acls, int* bcls, hipStream_t s) {
+  hipLaunchKernelGGL(k_classify, dim3(G.M + 2), dim3(256), 0, s, G, Tb, acls, bcls);
+  HIP_CHECK(hipGetLastError());
 }
 
 void launch_assemble(const DevGeom& G, const DevTables& Tb, double* a, double* b, double* B,

@@ -22,24 +22,67 @@ __device__ __forceinline__ double coef_b(const DevTables& T, const DevGeom& G, i
 }
 
 // Row/column-split evaluation used in the marching kernels: the column terms
-// (ylo, yhi, rh) live in registers for the whole tile, the row terms are uniform.
+// (ylo, yhi, rh) live in registers for the whole tile, the row terms (clip roots, face ends and
+// the per-row coefficient classes of DevTables::acls/bcls) are wave-uniform scalar loads.
 struct ColConst {
   double ylo, yhi, rh0, rh1;  // rh0 = rh[gj], rh1 = rh[gj+1]
+  int gj;
 };
 struct RowConst {
   double rv0, rv1, xlo, xhi;  // rv0 = rv[gi], rv1 = rv[gi+1]
+  int ca0[4], ca1[4], cb[4];  // classes of a(gi, .), a(gi+1, .), b(gi, .)
 };
 __device__ __forceinline__ ColConst load_col(const DevTables& T, int gj) {
-  return ColConst{T.ylo[gj], T.yhi[gj], T.rh[gj], T.rh[gj + 1]};
+  return ColConst{T.ylo[gj], T.yhi[gj], T.rh[gj], T.rh[gj + 1], gj};
 }
 __device__ __forceinline__ RowConst load_row(const DevTables& T, int gi) {
-  return RowConst{T.rv[gi], T.rv[gi + 1], T.xlo[gi], T.xhi[gi]};
+  RowConst r;
+  r.rv0 = T.rv[gi];
+  r.rv1 = T.rv[gi + 1];
+  r.xlo = T.xlo[gi];
+  r.xhi = T.xhi[gi];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    r.ca0[q] = T.acls[4 * gi + q];
+    r.ca1[q] = T.acls[4 * (gi + 1) + q];
+    r.cb[q] = T.bcls[4 * gi + q];
+  }
+  return r;
 }
+// exact evaluation (bit-identical to the reference formula)
 __device__ __forceinline__ double face_a(const ColConst& c, double rv, const DevGeom& G) {
   return geo::face_coef(geo::clip_len(c.ylo, c.yhi, rv), G.h2, G.eps, G.inv_eps);
 }
 __device__ __forceinline__ double face_b(const RowConst& r, double rh, const DevGeom& G) {
   return geo::face_coef(geo::clip_len(r.xlo, r.xhi, rh), G.h1, G.eps, G.inv_eps);
+}
+// class -> 1/eps, 1 or "cut" (exact formula).  The classes were produced by k_classify from the
+// exact formula, so the fast values are bit-identical; the cut branch is rare (faces crossed by
+// the ellipse) and skipped by whole waves away from the boundary.
+__device__ __forceinline__ bool cls_fast(int j, const int* c, double inv_eps, double& v) {
+  if (j < c[0] || j > c[3]) { v = inv_eps; return true; }
+  if (j >= c[1] && j <= c[2]) { v = 1.0; return true; }
+  return false;
+}
+__device__ __forceinline__ double face_a0c(const ColConst& cc, const RowConst& rc, const DevGeom& G) {
+  double v;
+  if (!cls_fast(cc.gj, rc.ca0, G.inv_eps, v)) v = face_a(cc, rc.rv0, G);
+  return v;
+}
+__device__ __forceinline__ double face_a1c(const ColConst& cc, const RowConst& rc, const DevGeom& G) {
+  double v;
+  if (!cls_fast(cc.gj, rc.ca1, G.inv_eps, v)) v = face_a(cc, rc.rv1, G);
+  return v;
+}
+__device__ __forceinline__ double face_b0c(const ColConst& cc, const RowConst& rc, const DevGeom& G) {
+  double v;
+  if (!cls_fast(cc.gj, rc.cb, G.inv_eps, v)) v = face_b(rc, cc.rh0, G);
+  return v;
+}
+__device__ __forceinline__ double face_b1c(const ColConst& cc, const RowConst& rc, const DevGeom& G) {
+  double v;
+  if (!cls_fast(cc.gj + 1, rc.cb, G.inv_eps, v)) v = face_b(rc, cc.rh1, G);
+  return v;
 }
 
 // Diagonal D_ij (stage0/Withoutopenmp1.cpp:98).  EXACT reproduces the reference's
@@ -52,6 +95,37 @@ __device__ __forceinline__ double diag(double a0, double a1, double b0, double b
   } else {
     return (a1 + a0) * G.cx + (b1 + b0) * G.cy;
   }
+}
+
+// z = r / D for a row of known uniform class (1 inside / 2 outside), else the general path.
+template <bool EXACT>
+__device__ __forceinline__ double zdiv_u(int ucls, double r, double a0, double a1, double b0,
+                                         double b1, const DevGeom& G);
+
+// z = r / D.  Fast mode: the two common stencils (all faces inside / all outside D) use a
+// precomputed 1/D; only cut stencils divide.
+template <bool EXACT>
+__device__ __forceinline__ double zdiv(double r, double a0, double a1, double b0, double b1,
+                                       const DevGeom& G) {
+  if constexpr (EXACT) {
+    return r / diag<true>(a0, a1, b0, b1, G);
+  } else {
+    const bool in = (a0 == 1.0) & (a1 == 1.0) & (b0 == 1.0) & (b1 == 1.0);
+    const bool out = (a0 == G.inv_eps) & (a1 == G.inv_eps) & (b0 == G.inv_eps) & (b1 == G.inv_eps);
+    if (in) return r * G.dinv_in;
+    if (out) return r * G.dinv_out;
+    return r / diag<false>(a0, a1, b0, b1, G);
+  }
+}
+
+template <bool EXACT>
+__device__ __forceinline__ double zdiv_u(int ucls, double r, double a0, double a1, double b0,
+                                         double b1, const DevGeom& G) {
+  if constexpr (!EXACT) {
+    if (ucls == 1) return r * G.dinv_in;
+    if (ucls == 2) return r * G.dinv_out;
+  }
+  return zdiv<EXACT>(r, a0, a1, b0, b1, G);
 }
 
 // (A p)_ij from the 5-point values (stage0/Withoutopenmp1.cpp:83-85).
@@ -96,11 +170,33 @@ __device__ __forceinline__ void block_sum2(double& v0, double& v1, double* lds /
   }
 }
 
+// Bijective XCD-aware remap (cdna_hip_programming.md §5.5 T1): hardware dispatch deals workgroup b
+// to XCD b % 8, so hand each XCD a contiguous range of logical tiles.  Neighbouring tiles share
+// halo cache lines and rows; keeping them on one XCD turns those re-reads into L2 hits.  Speed
+// only: any placement gives the same result.
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+  const int q = nb / 8, r = nb % 8;
+  const int xcd = b % 8, idx = b / 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}
+
+// Wave-uniform row class of a tile: 1 = every face of every column in [jlo, jhi] lies inside D
+// (all coefficients exactly 1), 2 = all outside (all exactly 1/eps), 0 = cut faces present.
+__device__ __forceinline__ int row_class(const RowConst& rc, int jlo, int jhi) {
+  const bool in = jlo >= rc.ca0[1] && jhi <= rc.ca0[2] && jlo >= rc.ca1[1] && jhi <= rc.ca1[2] &&
+                  jlo >= rc.cb[1] && jhi + 1 <= rc.cb[2];
+  if (in) return 1;
+  auto out = [&](const int* c, int hi) { return jlo > c[3] || hi < c[0]; };
+  if (out(rc.ca0, jhi) && out(rc.ca1, jhi) && (jlo > rc.cb[3] || jhi + 1 < rc.cb[0])) return 2;
+  return 0;
+}
+
 // Linear tile id -> (ti, tj).  Tiles are TI rows x BLOCK columns.
 struct Tile {
   int i0, iend, j0, jend, id;
 };
 __device__ __forceinline__ Tile tile_of(int id, int tiles_j, int TI, int BLOCK, const DevGeom& G) {
+  id = xcd_remap(id, int(gridDim.x));
   Tile t;
   t.id = id;
   const int ti = id / tiles_j, tj = id - ti * tiles_j;

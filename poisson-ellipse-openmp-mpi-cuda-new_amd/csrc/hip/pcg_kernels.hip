@@ -142,7 +142,7 @@ k_pcg_a(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, HaloBufs
       else rv = r[int64_t(ii) * P + jj];
       const double a0 = coef_a(Tb, G, gi, gj), a1 = coef_a(Tb, G, gi + 1, gj);
       const double b0 = coef_b(Tb, G, gi, gj), b1 = coef_b(Tb, G, gi, gj + 1);
-      const double z = rv / diag<EXACT>(a0, a1, b0, b1, G);
+      const double z = zdiv<EXACT>(rv, a0, a1, b0, b1, G);
       v = first ? z : z + beta * double(pold[int64_t(ii) * P + jj]);
       if ((jj == 0 && (G.nb & kNbYlo)) || (jj == G.ny + 1 && (G.nb & kNbYhi)))
         pnew[int64_t(ii) * P + jj] = static_cast<T>(v);
@@ -181,13 +181,13 @@ k_pcg_a(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, HaloBufs
     fetch(i + 1, rv_n, po_n);
     const RowConst rc_n = load_row(Tb, G.gi0 + min(i + 1, ilast));
     const int gi = G.gi0 + i;
-    const double a0 = face_a(cc, rc.rv0, G), a1 = face_a(cc, rc.rv1, G);
-    const double b0 = face_b(rc, cc.rh0, G), b1 = face_b(rc, cc.rh1, G);
+    const double a0 = face_a0c(cc, rc, G), a1 = face_a1c(cc, rc, G);
+    const double b0 = face_b0c(cc, rc, G), b1 = face_b1c(cc, rc, G);
     double pc = 0.0;
     const int slot = (i - t.i0 + 1) % 3;
     if (valid) {
       if (gi > 0 && gi < G.M) {
-        const double z = rv_c / diag<EXACT>(a0, a1, b0, b1, G);
+        const double z = zdiv<EXACT>(rv_c, a0, a1, b0, b1, G);
         pc = first ? z : z + beta * po_c;
         const bool own = i >= t.i0 && i <= t.iend;
         const bool ghost = (i == 0 && (G.nb & kNbXlo)) || (i == G.nx + 1 && (G.nb & kNbXhi));
@@ -254,7 +254,7 @@ k_pcg_b(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, const T* 
     double pp = double(pn[c + P]), pjm = double(pn[c - 1]), pjp = double(pn[c + 1]);
     double wo = double(w[c]), ro = double(r[c]);
     RowConst rc = load_row(Tb, G.gi0 + t.i0);
-    double acur = face_a(cc, rc.rv0, G);
+    double acur = face_a0c(cc, rc, G);
     for (int i = t.i0; i <= t.iend; ++i) {
       const int64_t cn = c + P;
       const bool more = i < t.iend;
@@ -267,15 +267,15 @@ k_pcg_b(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, const T* 
         ro_n = double(r[cn]);
       }
       const RowConst rc_n = load_row(Tb, G.gi0 + (more ? i + 1 : i));
-      const double a0 = acur, a1 = face_a(cc, rc.rv1, G);
-      const double b0 = face_b(rc, cc.rh0, G), b1 = face_b(rc, cc.rh1, G);
+      const double a0 = acur, a1 = face_a1c(cc, rc, G);
+      const double b0 = face_b0c(cc, rc, G), b1 = face_b1c(cc, rc, G);
       const double Ap = apply_a<EXACT>(pc, pm, pp, pjm, pjp, a0, a1, b0, b1, G);
       const T ws = static_cast<T>(wo + alpha * pc);
       const T rs = static_cast<T>(ro - alpha * Ap);
       const double dw = double(ws) - wo;
       dacc += dw * dw;
       const double rq = double(rs);
-      const double z = rq / diag<EXACT>(a0, a1, b0, b1, G);
+      const double z = zdiv<EXACT>(rq, a0, a1, b0, b1, G);
       zacc += z * rq;
       w[c] = ws;
       r[c] = rs;

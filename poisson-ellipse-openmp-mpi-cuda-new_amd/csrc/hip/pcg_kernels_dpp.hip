@@ -11,6 +11,7 @@
 //    broadcast per row with v_readlane;
 //  * rows are software-pipelined one row ahead (all loads of row i+1 issue before row i is used).
 #include <cmath>
+#include <type_traits>
 
 #include "pcg_device.hpp"
 #include "pmx/common.hpp"
@@ -23,7 +24,7 @@ using namespace dev;
 
 namespace {
 
-constexpr int kMaxWaveRows = 64;  // halo values for one tile live one-per-lane
+constexpr int kMaxWaveRows = 256;
 
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const long long b = __double_as_longlong(v);
@@ -78,9 +79,13 @@ struct WaveTile {
 };
 
 __device__ __forceinline__ WaveTile wave_tile(int waves, int tiles_j, int ntiles, int TI, int W,
-                                              const DevGeom& G) {
+                                              const DevGeom& G, int abl) {
   WaveTile t;
-  t.id = blockIdx.x * waves + (threadIdx.x >> 6);
+  // readfirstlane makes the wave index provably wave-uniform: without it the compiler treats the
+  // whole march as a divergent loop (row tables become per-lane vector loads, loop-carried
+  // values get copied through VGPRs every row)
+  t.id = ((abl & kAblNoXcd) ? int(blockIdx.x) : xcd_remap(blockIdx.x, gridDim.x)) * waves +
+         __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   t.live = t.id < ntiles;
   const int ti = t.id / tiles_j, tj = t.id - ti * tiles_j;
   t.i0 = 1 + ti * TI;
@@ -125,91 +130,71 @@ __device__ __forceinline__ bool prologue_a(PcgState* S, long long& k, bool& firs
 
 // ---------------------------------------------------------------------------
 // k_pcg_a (wave-tile): p^k = D^-1 r + beta p^{k-1};  partial (A p^k, p^k)
+//
+// Memory-pipeline rules (each one fixed a measured stall, see profiles/):
+//  * every global load is unconditional and branch-free (addresses clamped, results masked where
+//    used): a load inside a divergent branch forces an `s_waitcnt vmcnt(0)` at the join;
+//  * prefetched registers are never copied: the row loop is unrolled by the ring size and every
+//    ring slot is a compile-time index, because copying a register with an outstanding load makes
+//    the wave wait for that load, which serialised the whole march (vmcnt(0) every row).
 // ---------------------------------------------------------------------------
+template <typename T, int VEC>
+struct RowA {
+  double rv[VEC], po[VEC];  // r and p^{k-1} of the lane's columns
+  double hrv, hpo;          // the same for this lane's halo column
+};
+
 template <typename T, int VEC, int WAVES, bool EXACT>
 __global__ void __launch_bounds__(64 * WAVES)
 k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, HaloBufs<T> H,
-             double* __restrict__ partials, PcgState* S, int TI, int tiles_j, int ntiles) {
+             double* __restrict__ partials, PcgState* S, int TI, int tiles_j, int ntiles, int abl) {
   constexpr int W = 64 * VEC;
   long long k;
   bool first;
   double beta;
   if (!prologue_a(S, k, first, beta)) return;
-  const WaveTile t = wave_tile(WAVES, tiles_j, ntiles, TI, W, G);
+  const WaveTile t = wave_tile(WAVES, tiles_j, ntiles, TI, W, G, abl);
   if (!t.live) return;
   T* pnew = (k & 1) ? p1 : p0;
   const T* pold = (k & 1) ? p0 : p1;
   const int64_t P = G.pitch;
   const int lane = threadIdx.x & 63;
 
-  // (1) halo columns j0-1 (hl) and jend+1 (hr): lane l holds row i0+l
-  double hl = 0.0, hr = 0.0;
-  {
-    const int ii = t.i0 + lane;
-    if (ii <= t.iend) {
-#pragma unroll
-      for (int side = 0; side < 2; ++side) {
-        const int jj = side ? t.jend + 1 : t.j0 - 1;
-        const int gi = G.gi0 + ii, gj = G.gj0 + jj;
-        double v = 0.0;
-        if (!dirichlet(G, gi, gj)) {
-          double rv;
-          if (jj == 0) rv = double(H.recv[2][ii - 1]);
-          else if (jj == G.ny + 1) rv = double(H.recv[3][ii - 1]);
-          else rv = double(r[int64_t(ii) * P + jj]);
-          const double a0 = coef_a(Tb, G, gi, gj), a1 = coef_a(Tb, G, gi + 1, gj);
-          const double b0 = coef_b(Tb, G, gi, gj), b1 = coef_b(Tb, G, gi, gj + 1);
-          const double z = rv / diag<EXACT>(a0, a1, b0, b1, G);
-          v = first ? z : z + beta * double(pold[int64_t(ii) * P + jj]);
-          if ((jj == 0 && (G.nb & kNbYlo)) || (jj == G.ny + 1 && (G.nb & kNbYhi)))
-            pnew[int64_t(ii) * P + jj] = static_cast<T>(v);
-          v = double(static_cast<T>(v));
-        }
-        if (side) hr = v; else hl = v;
-      }
-    }
-  }
-
-  // (2) march.  Lane columns jl..jl+VEC-1.
   const int jl = t.j0 + lane * VEC;
+  // clamp for loads: the largest column start with jl's alignment whose VEC columns stay inside
+  // the row (the field pitch is padded by >= VEC columns)
+  const int jlc = min(jl, 1 + ((G.ny - 1) / VEC) * VEC);
   bool valid[VEC];
   ColConst cc[VEC];
-  double rhn = 0.0;  // rh[gj+VEC] for the last column's b(i, j+1)
 #pragma unroll
   for (int u = 0; u < VEC; ++u) {
     valid[u] = jl + u <= t.jend;
     cc[u] = load_col(Tb, G.gj0 + min(jl + u, t.jend));
   }
-  const bool lane_any = valid[0];
   const bool lane_full = valid[VEC - 1];
+  // halo column of this lane: j0-1 for even lanes, jend+1 for odd lanes (computed every row by
+  // all lanes, broadcast with v_readlane; the neighbouring tile loads those lines too -> L2 hits)
+  const int jh = (lane & 1) ? t.jend + 1 : t.j0 - 1;
+  const int gjh = G.gj0 + jh;
+  const bool h_dir = gjh <= 0 || gjh >= G.N || (abl & (kAblHalo | kAblHaloLoads));
+  const ColConst ch = load_col(Tb, h_dir ? G.gj0 + t.j0 : gjh);
+  const bool h_store = lane < 2 && ((jh == 0 && (G.nb & kNbYlo)) || (jh == G.ny + 1 && (G.nb & kNbYhi)));
   const int ilast = t.iend + 1;
 
-  auto fetch = [&](int i, double (&rv)[VEC], double (&po)[VEC]) {
-#pragma unroll
-    for (int u = 0; u < VEC; ++u) { rv[u] = 0.0; po[u] = 0.0; }
-    const int gi = G.gi0 + i;
-    if (!lane_any || i > ilast || gi <= 0 || gi >= G.M) return;
-    if (i == 0 || i == G.nx + 1) {
-      const T* src = H.recv[i == 0 ? 0 : 1];
-#pragma unroll
-      for (int u = 0; u < VEC; ++u)
-        if (valid[u]) rv[u] = double(src[jl + u - 1]);
-    } else if (lane_full) {
-      vload<T, VEC>(r + int64_t(i) * P + jl, rv);
-    } else {
-#pragma unroll
-      for (int u = 0; u < VEC; ++u)
-        if (valid[u]) rv[u] = double(r[int64_t(i) * P + jl + u]);
-    }
-    if (!first) {
-      if (lane_full) {
-        vload<T, VEC>(pold + int64_t(i) * P + jl, po);
-      } else {
-#pragma unroll
-        for (int u = 0; u < VEC; ++u)
-          if (valid[u]) po[u] = double(pold[int64_t(i) * P + jl + u]);
-      }
-    }
+  // branch-free row fetch (addresses always valid; rows outside [0, nx+1] never requested)
+  auto fetch = [&](int i, RowA<T, VEC>& b) {
+    const int ic = min(i, G.nx + 1);
+    const T* rrow = (ic == 0) ? (H.recv[0] - 1) : (ic == G.nx + 1) ? (H.recv[1] - 1) : (r + int64_t(ic) * P);
+    if (!(G.nb & kNbXlo) && ic == 0) rrow = r + P;           // Dirichlet ghost row: any valid row
+    if (!(G.nb & kNbXhi) && ic == G.nx + 1) rrow = r + P;
+    vload<T, VEC>(rrow + jlc, b.rv);
+    vload<T, VEC>(pold + int64_t(ic) * P + jlc, b.po);
+    const int ih = min(max(ic, 1), G.nx);
+    const T* hp = (jh == 0 && (G.nb & kNbYlo)) ? (H.recv[2] + ih - 1)
+                : (jh == G.ny + 1 && (G.nb & kNbYhi)) ? (H.recv[3] + ih - 1)
+                : (r + int64_t(ih) * P + min(max(jh, 1), G.ny));
+    b.hrv = double(*hp);
+    b.hpo = double(pold[int64_t(ih) * P + min(max(jh, 0), G.ny + 1)]);
   };
 
   double pm2[VEC], pm1[VEC], qa0[VEC], qa1[VEC], qb0[VEC], qb1[VEC];
@@ -217,30 +202,52 @@ k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, Hal
   for (int u = 0; u < VEC; ++u) { pm2[u] = pm1[u] = qa0[u] = qa1[u] = qb0[u] = qb1[u] = 0.0; }
   double hl_m1 = 0.0, hr_m1 = 0.0;  // halo values of row i-1
   double acc = 0.0;
-  double rv_c[VEC], po_c[VEC];
-  fetch(t.i0 - 1, rv_c, po_c);
+  RowA<T, VEC> buf[2];
+  fetch(t.i0 - 1, buf[0]);
   RowConst rc = load_row(Tb, G.gi0 + t.i0 - 1);
-  for (int i = t.i0 - 1; i <= ilast; ++i) {
-    double rv_n[VEC], po_n[VEC];
-    fetch(i + 1, rv_n, po_n);
+
+  auto step = [&](int i, const RowA<T, VEC>& cur, RowA<T, VEC>& nxt) {
+    fetch(min(i + 1, ilast), nxt);  // unconditional: a branch around loads forces vmcnt(0)
     const RowConst rc_n = load_row(Tb, G.gi0 + min(i + 1, ilast));
     const int gi = G.gi0 + i;
     const bool own_row = i >= t.i0 && i <= t.iend;
-    const double hl_i = own_row ? readlane_f64(hl, i - t.i0) : 0.0;
-    const double hr_i = own_row ? readlane_f64(hr, i - t.i0) : 0.0;
-    double a0[VEC], a1[VEC], b0[VEC], b1[VEC], pc[VEC];
     const bool live_row = gi > 0 && gi < G.M;
+    const int ucls = (EXACT || (abl & kAblCoef)) ? 0 : row_class(rc, G.gj0 + t.j0 - 1, G.gj0 + t.jend + 1);
+    const double uval = ucls == 1 ? 1.0 : G.inv_eps;
+    // halo column values of this row
+    double hv = 0.0;
+    if (own_row && live_row) {
+      double ha0 = uval, ha1 = uval, hb0 = uval, hb1 = uval;
+      if (ucls == 0) {
+        ha0 = face_a0c(ch, rc, G); ha1 = face_a1c(ch, rc, G);
+        hb0 = face_b0c(ch, rc, G); hb1 = face_b1c(ch, rc, G);
+      }
+      const double z = zdiv_u<EXACT>(ucls, cur.hrv, ha0, ha1, hb0, hb1, G);
+      hv = first ? z : z + beta * cur.hpo;
+      if (h_dir) hv = 0.0;
+      if (h_store && !h_dir) pnew[int64_t(i) * P + jh] = static_cast<T>(hv);
+      hv = double(static_cast<T>(hv));
+    }
+    const double hl_i = readlane_f64(hv, 0);
+    const double hr_i = readlane_f64(hv, 1);
+    double a0[VEC], a1[VEC], b0[VEC], b1[VEC], pc[VEC];
     T st[VEC];
 #pragma unroll
     for (int u = 0; u < VEC; ++u) {
-      a0[u] = face_a(cc[u], rc.rv0, G);
-      a1[u] = face_a(cc[u], rc.rv1, G);
-      b0[u] = face_b(rc, cc[u].rh0, G);
-      b1[u] = face_b(rc, cc[u].rh1, G);
+      if (abl & kAblCoef) {
+        a0[u] = a1[u] = b0[u] = b1[u] = 1.0;
+      } else if (ucls != 0) {
+        a0[u] = a1[u] = b0[u] = b1[u] = uval;
+      } else {
+        a0[u] = face_a0c(cc[u], rc, G);
+        a1[u] = face_a1c(cc[u], rc, G);
+        b0[u] = face_b0c(cc[u], rc, G);
+        b1[u] = face_b1c(cc[u], rc, G);
+      }
       double v = 0.0;
       if (valid[u] && live_row) {
-        const double z = rv_c[u] / diag<EXACT>(a0[u], a1[u], b0[u], b1[u], G);
-        v = first ? z : z + beta * po_c[u];
+        const double z = zdiv_u<EXACT>(ucls, cur.rv[u], a0[u], a1[u], b0[u], b1[u], G);
+        v = first ? z : z + beta * cur.po[u];
       }
       st[u] = static_cast<T>(v);
       v = double(st[u]);
@@ -249,7 +256,8 @@ k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, Hal
       if (jl + u == t.jend + 1) v = hr_i;
       pc[u] = v;
     }
-    if (live_row && (own_row || (i == 0 && (G.nb & kNbXlo)) || (i == G.nx + 1 && (G.nb & kNbXhi)))) {
+    if (!(abl & kAblStore) &&
+        live_row && (own_row || (i == 0 && (G.nb & kNbXlo)) || (i == G.nx + 1 && (G.nb & kNbXhi)))) {
       if (lane_full) {
         vstore<T, VEC>(pnew + int64_t(i) * P + jl, st);
       } else {
@@ -259,7 +267,7 @@ k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, Hal
       }
     }
     // A p^k for row i-1 (pm1), neighbours: rows i-2 (pm2), i (pc); columns by DPP
-    if (i - 1 >= t.i0) {
+    if (i - 1 >= t.i0 && !(abl & kAblAp)) {
       const double left = dpp_shift_f64<kWaveShr1>(pm1[VEC - 1], hl_m1);
       const double right = dpp_shift_f64<kWaveShl1>(pm1[0], hr_m1);
 #pragma unroll
@@ -274,24 +282,30 @@ k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, Hal
     for (int u = 0; u < VEC; ++u) {
       pm2[u] = pm1[u]; pm1[u] = pc[u];
       qa0[u] = a0[u]; qa1[u] = a1[u]; qb0[u] = b0[u]; qb1[u] = b1[u];
-      rv_c[u] = rv_n[u]; po_c[u] = po_n[u];
     }
     hl_m1 = hl_i; hr_m1 = hr_i;
     rc = rc_n;
+  };
+  // unrolled by the ring size: buf[0]/buf[1] are never copied
+  for (int i = t.i0 - 1; i <= ilast; i += 2) {
+    step(i, buf[0], buf[1]);
+    if (i + 1 > ilast) break;
+    step(i + 1, buf[1], buf[0]);
   }
-  (void)rhn;
   acc = wave_sum(acc);
   if (lane == 0) partials[t.id] = acc;
 }
 
 // ---------------------------------------------------------------------------
 // k_pcg_b (wave-tile): alpha, A p^k, w/r update, sum dw^2, (z, r), halo pack
+// Ring of 4 p rows (i-1, i, i+1 in use, i+2 in flight) and 2 w/r rows; the loop is unrolled by 4
+// so every ring slot is a compile-time register set (see k_pcg_a_wave).
 // ---------------------------------------------------------------------------
 template <typename T, int VEC, int WAVES, bool EXACT>
 __global__ void __launch_bounds__(64 * WAVES)
 k_pcg_b_wave(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, const T* p0,
              const T* p1, HaloBufs<T> H, double* __restrict__ partials, PcgState* S, int TI,
-             int tiles_j, int ntiles) {
+             int tiles_j, int ntiles, int abl) {
   constexpr int W = 64 * VEC;
   if (S->done) return;
   const long long k = S->it;
@@ -307,7 +321,7 @@ k_pcg_b_wave(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
     return;
   }
   const double alpha = S->zr[(k - 1) & 1] / denom;
-  const WaveTile t = wave_tile(WAVES, tiles_j, ntiles, TI, W, G);
+  const WaveTile t = wave_tile(WAVES, tiles_j, ntiles, TI, W, G, abl);
   if (!t.live) return;
   const T* __restrict__ pn = (k & 1) ? p1 : p0;
   const int64_t P = G.pitch;
@@ -322,87 +336,79 @@ k_pcg_b_wave(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
   }
   const bool lane_any = valid[0];
   const bool lane_full = valid[VEC - 1];
-  // columns that exist in memory (<= ny+1): the partial tile's right halo column is a real load
-  bool mem[VEC];
-#pragma unroll
-  for (int u = 0; u < VEC; ++u) mem[u] = jl + u <= t.jend + 1;
-  const bool lane_mem_full = mem[VEC - 1];
+  // p columns exist up to ny+1 (ghost); w/r loads stay within the interior.  The pitch is padded
+  // by >= VEC columns, so a VEC-wide load starting at <= ny+1 stays inside the row.
+  const int jlp = min(jl, 1 + (G.ny / VEC) * VEC);
+  const int jlw = min(jl, 1 + ((G.ny - 1) / VEC) * VEC);
   const int jr = t.jend + 1;
+  const bool edges = !(abl & (kAblHalo | kAblHaloLoads));
 
-  auto load_p = [&](int i, double (&out)[VEC]) {
-#pragma unroll
-    for (int u = 0; u < VEC; ++u) out[u] = 0.0;
-    if (lane_mem_full) {
-      vload<T, VEC>(pn + int64_t(i) * P + jl, out);
-    } else {
-#pragma unroll
-      for (int u = 0; u < VEC; ++u)
-        if (mem[u]) out[u] = double(pn[int64_t(i) * P + jl + u]);
-    }
+  double pr[4][VEC];        // p rows ring
+  double wr[2][VEC], rr[2][VEC];
+  double er[2][2];          // [slot][left/right edge]
+  auto load_p = [&](int i, double (&out)[VEC]) { vload<T, VEC>(pn + int64_t(i) * P + jlp, out); };
+  auto load_wr = [&](int i, double (&wo)[VEC], double (&ro)[VEC], double (&e)[2]) {
+    vload<T, VEC>(w + int64_t(i) * P + jlw, wo);
+    vload<T, VEC>(r + int64_t(i) * P + jlw, ro);
+    e[0] = double(pn[int64_t(i) * P + t.j0 - 1]);
+    e[1] = double(pn[int64_t(i) * P + jr]);
   };
-  auto load_f = [&](const T* f, int i, double (&out)[VEC]) {
-#pragma unroll
-    for (int u = 0; u < VEC; ++u) out[u] = 0.0;
-    if (lane_full) {
-      vload<T, VEC>(f + int64_t(i) * P + jl, out);
-    } else {
-#pragma unroll
-      for (int u = 0; u < VEC; ++u)
-        if (valid[u]) out[u] = double(f[int64_t(i) * P + jl + u]);
-    }
-  };
-
-  double pm[VEC], pc[VEC], pp[VEC], wo[VEC], ro[VEC];
-  load_p(t.i0 - 1, pm);
-  load_p(t.i0, pc);
-  load_p(t.i0 + 1, pp);
-  load_f(w, t.i0, wo);
-  load_f(r, t.i0, ro);
-  double el = double(pn[int64_t(t.i0) * P + t.j0 - 1]);  // left edge (column j0-1)
-  double er = double(pn[int64_t(t.i0) * P + jr]);        // right edge (column jend+1)
+  load_p(t.i0 - 1, pr[3]);
+  load_p(t.i0, pr[0]);
+  load_p(t.i0 + 1, pr[1]);
+  load_wr(t.i0, wr[0], rr[0], er[0]);
   RowConst rc = load_row(Tb, G.gi0 + t.i0);
   double acur[VEC];
 #pragma unroll
-  for (int u = 0; u < VEC; ++u) acur[u] = face_a(cc[u], rc.rv0, G);
+  for (int u = 0; u < VEC; ++u) acur[u] = face_a0c(cc[u], rc, G);
   double dacc = 0.0, zacc = 0.0;
-  for (int i = t.i0; i <= t.iend; ++i) {
+
+  // S = slot of row i in the p ring; row i's w/r live in slot S & 1
+  auto step = [&](auto SC, int i) {
+    constexpr int S0 = decltype(SC)::value;
+    constexpr int SM = (S0 + 3) & 3, SP = (S0 + 1) & 3, SN = (S0 + 2) & 3, WC = S0 & 1, WN = WC ^ 1;
     const bool more = i < t.iend;
-    double pp_n[VEC], wo_n[VEC], ro_n[VEC];
-    double el_n = 0.0, er_n = 0.0;
-    if (more) {
-      load_p(i + 2, pp_n);
-      load_f(w, i + 1, wo_n);
-      load_f(r, i + 1, ro_n);
-      el_n = double(pn[int64_t(i + 1) * P + t.j0 - 1]);
-      er_n = double(pn[int64_t(i + 1) * P + jr]);
-    } else {
-#pragma unroll
-      for (int u = 0; u < VEC; ++u) pp_n[u] = wo_n[u] = ro_n[u] = 0.0;
-    }
+    // unconditional (rows clamped at the tile end): a branch around loads forces vmcnt(0)
+    load_p(min(i + 2, t.iend + 1), pr[SN]);
+    load_wr(min(i + 1, t.iend), wr[WN], rr[WN], er[WN]);
     const RowConst rc_n = load_row(Tb, G.gi0 + (more ? i + 1 : i));
-    const double left = dpp_shift_f64<kWaveShr1>(pc[VEC - 1], el);
-    const double right = dpp_shift_f64<kWaveShl1>(pc[0], er);
+    const int ucls = (EXACT || (abl & kAblCoef)) ? 0 : row_class(rc, G.gj0 + t.j0, G.gj0 + t.jend);
+    const double uval = ucls == 1 ? 1.0 : G.inv_eps;
+    const double left = dpp_shift_f64<kWaveShr1>(pr[S0][VEC - 1], edges ? er[WC][0] : 0.0);
+    const double right = dpp_shift_f64<kWaveShl1>(pr[S0][0], edges ? er[WC][1] : 0.0);
     T ws[VEC], rs[VEC];
 #pragma unroll
     for (int u = 0; u < VEC; ++u) {
-      const double pjm = u == 0 ? left : pc[u - 1];
-      const double pjp = u == VEC - 1 ? right : pc[u + 1];
-      const double a0 = acur[u], a1 = face_a(cc[u], rc.rv1, G);
-      const double b0 = face_b(rc, cc[u].rh0, G), b1 = face_b(rc, cc[u].rh1, G);
-      const double Ap = apply_a<EXACT>(pc[u], pm[u], pp[u], pjm, pjp, a0, a1, b0, b1, G);
-      ws[u] = static_cast<T>(wo[u] + alpha * pc[u]);
-      rs[u] = static_cast<T>(ro[u] - alpha * Ap);
+      const double pjm = u == 0 ? left : pr[S0][u - 1];
+      const double pjp = u == VEC - 1 ? right : pr[S0][u + 1];
+      double a0, a1, b0, b1;
+      if (abl & kAblCoef) {
+        a0 = a1 = b0 = b1 = 1.0;
+      } else if (ucls != 0) {
+        a0 = a1 = b0 = b1 = uval;
+      } else {
+        a0 = acur[u];
+        a1 = face_a1c(cc[u], rc, G);
+        b0 = face_b0c(cc[u], rc, G);
+        b1 = face_b1c(cc[u], rc, G);
+      }
+      const double pc = pr[S0][u];
+      const double Ap = apply_a<EXACT>(pc, pr[SM][u], pr[SP][u], pjm, pjp, a0, a1, b0, b1, G);
+      const double wo = wr[WC][u], ro = rr[WC][u];
+      ws[u] = static_cast<T>(wo + alpha * pc);
+      rs[u] = static_cast<T>(ro - alpha * Ap);
       if (valid[u]) {
-        const double dw = double(ws[u]) - wo[u];
+        const double dw = double(ws[u]) - wo;
         dacc += dw * dw;
         const double rq = double(rs[u]);
-        const double z = rq / diag<EXACT>(a0, a1, b0, b1, G);
+        const double z = zdiv_u<EXACT>(ucls, rq, a0, a1, b0, b1, G);
         zacc += z * rq;
       }
       acur[u] = a1;
     }
     const int64_t c = int64_t(i) * P + jl;
-    if (lane_full) {
+    if (abl & kAblStore) {
+    } else if (lane_full) {
       vstore<T, VEC>(w + c, ws);
       vstore<T, VEC>(r + c, rs);
     } else {
@@ -424,11 +430,16 @@ k_pcg_b_wave(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
       for (int u = 0; u < VEC; ++u)
         if (jl + u == G.ny && (G.nb & kNbYhi)) H.send[3][i - 1] = rs[u];
     }
-#pragma unroll
-    for (int u = 0; u < VEC; ++u) {
-      pm[u] = pc[u]; pc[u] = pp[u]; pp[u] = pp_n[u]; wo[u] = wo_n[u]; ro[u] = ro_n[u];
-    }
-    el = el_n; er = er_n; rc = rc_n;
+    rc = rc_n;
+  };
+  for (int i = t.i0; i <= t.iend; i += 4) {
+    step(std::integral_constant<int, 0>{}, i);
+    if (i + 1 > t.iend) break;
+    step(std::integral_constant<int, 1>{}, i + 1);
+    if (i + 2 > t.iend) break;
+    step(std::integral_constant<int, 2>{}, i + 2);
+    if (i + 3 > t.iend) break;
+    step(std::integral_constant<int, 3>{}, i + 3);
   }
   dacc = wave_sum(dacc);
   zacc = wave_sum(zacc);
@@ -444,7 +455,7 @@ k_pcg_b_wave(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
 TileCfg make_wave_tiles(const DevGeom& G, int vec, int waves, int rows) {
   PMX_CHECK(vec == 1 || vec == 2 || vec == 4, "vec must be 1, 2 or 4");
   PMX_CHECK(waves >= 1 && waves <= 16, "waves per block must be in [1,16]");
-  PMX_CHECK(rows >= 0 && rows <= kMaxWaveRows, "wave tile rows must be in [0, 64] (0 = auto)");
+  PMX_CHECK(rows >= 0 && rows <= kMaxWaveRows, "wave tile rows must be in [0, 256] (0 = auto)");
   TileCfg t;
   t.kind = 1;
   t.vec = vec;
@@ -484,10 +495,10 @@ void launch_pcg_a_wave(const DevGeom& G, const DevTables& Tb, const T* r, T* p0,
                        hipStream_t s) {
   if (exact)
     PMX_WAVE_DISPATCH(tc, true, k_pcg_a_wave, G, Tb, r, p0, p1, H, partials, S, tc.rows,
-                      tc.tiles_j, tc.ntiles());
+                      tc.tiles_j, tc.ntiles(), tc.abl);
   else
     PMX_WAVE_DISPATCH(tc, false, k_pcg_a_wave, G, Tb, r, p0, p1, H, partials, S, tc.rows,
-                      tc.tiles_j, tc.ntiles());
+                      tc.tiles_j, tc.ntiles(), tc.abl);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -497,10 +508,10 @@ void launch_pcg_b_wave(const DevGeom& G, const DevTables& Tb, T* w, T* r, const 
                        const TileCfg& tc, bool exact, hipStream_t s) {
   if (exact)
     PMX_WAVE_DISPATCH(tc, true, k_pcg_b_wave, G, Tb, w, r, p0, p1, H, partials, S, tc.rows,
-                      tc.tiles_j, tc.ntiles());
+                      tc.tiles_j, tc.ntiles(), tc.abl);
   else
     PMX_WAVE_DISPATCH(tc, false, k_pcg_b_wave, G, Tb, w, r, p0, p1, H, partials, S, tc.rows,
-                      tc.tiles_j, tc.ntiles());
+                      tc.tiles_j, tc.ntiles(), tc.abl);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -15,6 +15,12 @@ struct DevTables {
   const double* ylo;  // y_j - h2/2                               (N+2)
   const double* yhi;  // y_j + h2/2                               (N+2)
   const double* y;    // y_j                                      (N+2)
+  // Per-row coefficient classes (4 ints per GLOBAL row gi = 0..M+1), built on the device by
+  // k_classify from the exact formulas: for j < c[0] or j > c[3] the coefficient is exactly
+  // 1/eps (face outside D), for c[1] <= j <= c[2] exactly 1 (face inside D), otherwise the face
+  // is cut by the ellipse and the exact formula is evaluated.  acls: a(gi, j), bcls: b(gi, j).
+  const int* acls;
+  const int* bcls;
 };
 
 enum NbBits : int { kNbXlo = 1, kNbXhi = 2, kNbYlo = 4, kNbYhi = 8 };
@@ -30,6 +36,7 @@ struct DevGeom {
   int ref_ellipse;
   double h1, h2, eps, inv_eps, h1h2;
   double cx, cy;  // 1/h1^2, 1/h2^2
+  double dinv_in, dinv_out;  // 1/D for all-inside / all-outside stencils (fast mode)
   double ax, by, F;
 };
 

@@ -72,6 +72,10 @@ class GpuSubdomainSolver {
   void enqueue_phase_b(hipStream_t s);  // k_pcg_b + reduce -> red_b, it += 1
 
   PcgState read_state(hipStream_t s) const;  // synchronous D2H of the scalars
+  // Kernel isolation benchmark: pins the scalar state to a mid-solve iteration and launches
+  // k_pcg_a (which=0) or k_pcg_b (which=1) alone `reps` times; returns ms per launch.  Leaves
+  // the solver state invalid (call enqueue_init afterwards).
+  double bench_kernel(int which, int abl, int reps, hipStream_t s);
   PcgState* state_dev() const { return state_; }
   double* red_a_dev() const { return state_->red_a; }
   double* red_b_dev() const { return state_->red_b; }
@@ -100,6 +104,8 @@ class GpuSubdomainSolver {
   template <typename T> void init_impl(hipStream_t s);
   template <typename T> void phase_a_impl(hipStream_t s);
   template <typename T> void phase_b_impl(hipStream_t s);
+  template <typename T> void phase_a_kernel_only(hipStream_t s);
+  template <typename T> void phase_b_kernel_only(hipStream_t s);
   template <typename T> HaloBufs<T> halo() const;
   void after_launch(hipStream_t s) const;
 

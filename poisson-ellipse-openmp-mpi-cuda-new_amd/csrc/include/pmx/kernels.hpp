@@ -23,6 +23,7 @@ struct TileCfg {
   int rows = 0;       // rows per tile (marching length); 0 = auto
   int vec = 1;        // kind 1: columns per lane
   int waves = 1;      // kind 1: independent wave tiles per workgroup
+  int abl = 0;        // kernel-isolation ablation bits (kAbl*), 0 in production
   int tiles_i = 0, tiles_j = 0;
   int ntiles() const { return tiles_i * tiles_j; }
 };
@@ -31,6 +32,15 @@ TileCfg make_tiles(const DevGeom& G, int block, int rows);
 TileCfg make_wave_tiles(const DevGeom& G, int vec, int waves, int rows);
 
 enum ReduceMode : int { kSkipIfDone = 1, kBumpIter = 2 };
+
+// Ablation bits for the kernel-isolation benchmark (GpuSubdomainSolver::bench_kernel): each
+// switches off one part of the wave-tile kernels so its cost can be measured.  Results are
+// numerically meaningless with any bit set.
+enum AblBits : int {
+  kAblHalo = 1, kAblAp = 2, kAblCoef = 4, kAblStore = 8,
+  kAblHaloLoads = 16,  // skip the halo-column loads (k_pcg_a) / edge loads (k_pcg_b)
+  kAblNoXcd = 64,      // identity workgroup -> tile mapping instead of the XCD-aware remap
+};
 
 template <typename T>
 void launch_init(const DevGeom& G, const DevTables& Tb, T* w, T* r, HaloBufs<T> H,
@@ -60,6 +70,9 @@ void launch_reduce(const double* partials, int n, int nq, double w0, double w1, 
 // Deterministic in-process "all-reduce" across P subdomains on one device (LocalComm):
 // out_k[q] = sum_r in_r[q] for every k, summed in rank order.
 void launch_local_allreduce(double* const* bufs, int nranks, int nq, hipStream_t s);
+
+// Per-row coefficient classes (see DevTables::acls); rows gi = 0..M+1, columns j = 0..N+1.
+void launch_classify(const DevGeom& Gglobal, const DevTables& Tb, int* acls, int* bcls, hipStream_t s);
 
 // ---- unfused ops (tests, naive solver mode, bit-equality checks) ----
 // All fields are local arrays with ghost ring: element (li,lj) at f[li*pitch+lj].

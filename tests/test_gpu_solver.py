@@ -74,7 +74,7 @@ def test_lds_tile_shapes(pkg, block, rows):
     assert np.abs(r.w - ref.w).max() < 1e-12
 
 
-@pytest.mark.parametrize("vec,waves,rows", [(1, 4, 1), (2, 4, 64), (2, 1, 5), (2, 8, 33), (1, 4, 0), (2, 4, 0)])
+@pytest.mark.parametrize("vec,waves,rows", [(1, 4, 1), (2, 4, 64), (2, 1, 5), (2, 8, 33), (1, 4, 0), (2, 4, 0), (4, 4, 0), (4, 1, 7)])
 @pytest.mark.parametrize("grid", [(211, 1031), (97, 130), (300, 257)])
 def test_wave_tile_shapes(pkg, vec, waves, rows, grid):
     """Wave-tile kernels on full and partial tiles (odd widths leave half-filled lanes)."""
