@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--waves", type=int, default=4, help="wave kernels: wave tiles per workgroup")
     ap.add_argument("--tile-rows", type=int, default=0, help="tile height (0 = auto)")
     ap.add_argument("--graph-batch", type=int, default=32)
+    ap.add_argument("--overlap", default="on", choices=["on", "off"],
+                    help="ghost exchange on a second HIP stream, overlapped with the w/r update kernel")
     ap.add_argument("--exact", action="store_true", help="reference arithmetic order in the fused kernels")
     ap.add_argument("--tol-solve", dest="tol_solve", action="store_true", default=True)
     ap.add_argument("--no-tol-solve", dest="tol_solve", action="store_false")
@@ -73,7 +75,8 @@ def main():
 
     problem = pmx.PoissonEllipse(M=args.M, N=args.N)
     kw = dict(split=args.split, dtype=args.dtype, kernel=args.kernel, block=args.block, vec=args.vec,
-              waves=args.waves, tile_rows=args.tile_rows, exact=args.exact, graph_batch=args.graph_batch)
+              waves=args.waves, tile_rows=args.tile_rows, exact=args.exact, graph_batch=args.graph_batch,
+              overlap=args.overlap == "on")
     comm_used = args.comm
     if world == 1:
         models = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.models")
@@ -179,6 +182,7 @@ def main():
                 "kernel": args.kernel,
                 "tile": dict(rows=args.tile_rows, block=args.block, vec=args.vec, waves=args.waves),
                 "graph_batch": args.graph_batch,
+                "overlap": args.overlap,
                 "exact": args.exact,
             },
             "valid": valid,

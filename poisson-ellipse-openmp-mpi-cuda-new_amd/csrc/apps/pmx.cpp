@@ -10,7 +10,7 @@
 //       [--exact] [--graph-batch 32] [--tile-rows 0] [--kernel wave|lds] [--vec 2] [--waves 4]
 //       [--block 256] [--device D]
 //       [--dump sol.txt] [--dump-stride s] [--json] [--banner stage0..stage4]
-//       [--profile-phases N] [--check]
+//       [--profile-phases N] [--check] [--overlap on|off]
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -46,7 +46,7 @@ struct Cli {
                "           [--graph-batch N] [--tile-rows R] [--kernel wave|lds] [--vec V]\n"
                "           [--waves W] [--block B] [--device D]\n"
                "           [--dump FILE] [--dump-stride S] [--json] [--banner stage0..stage4]\n"
-               "           [--profile-phases N] [--check]\n";
+               "           [--profile-phases N] [--check] [--overlap on|off]\n";
   std::exit(msg ? 2 : 0);
 }
 
@@ -109,6 +109,11 @@ Cli parse(int argc, char** argv) {
     else if (a == "--banner") c.banner = val();
     else if (a == "--profile-phases") c.profile = std::atoll(val().c_str());
     else if (a == "--check") c.opt.check = true;
+    else if (a == "--overlap") {
+      const std::string v = val();
+      if (v != "on" && v != "off") usage("--overlap on|off");
+      c.opt.overlap = v == "on";
+    }
     else if (!a.empty() && a[0] == '-') usage(("unknown option " + a).c_str());
     else pos.push_back(a);
   }

@@ -150,7 +150,8 @@ class OpContext {
 };
 
 GpuOptions make_options(int device, const std::string& kernel, int block, int vec, int waves,
-                        int tile_rows, const std::string& dtype, bool exact, int graph_batch, bool check) {
+                        int tile_rows, const std::string& dtype, bool exact, int graph_batch, bool check,
+                        bool overlap = true) {
   GpuOptions o;
   o.device = device;
   PMX_CHECK(kernel == "lds" || kernel == "wave", "kernel must be lds or wave, got " << kernel);
@@ -164,6 +165,7 @@ GpuOptions make_options(int device, const std::string& kernel, int block, int ve
   o.exact = exact;
   o.graph_batch = graph_batch;
   o.check = check;
+  o.overlap = overlap;
   return o;
 }
 
@@ -278,7 +280,10 @@ PYBIND11_MODULE(_pmx, m) {
            py::arg("check") = false)
       .def("enqueue_init", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_init(as_stream(s)); })
       .def("enqueue_phase_a", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_phase_a(as_stream(s)); })
-      .def("enqueue_phase_b", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_phase_b(as_stream(s)); })
+      .def("enqueue_phase_b", [](GpuSubdomainSolver& g, uintptr_t s, bool pack) {
+             g.enqueue_phase_b(as_stream(s), pack);
+           }, py::arg("stream"), py::arg("pack") = true)
+      .def("enqueue_pack", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_pack(as_stream(s)); })
       .def("read_state", [](GpuSubdomainSolver& g, uintptr_t s) { return state_dict(g.read_state(as_stream(s))); })
       .def("download_w", [](GpuSubdomainSolver& g, uintptr_t s) {
         return to_numpy(g.download_w(as_stream(s)), {g.sd().nx, g.sd().ny});
@@ -297,11 +302,11 @@ PYBIND11_MODULE(_pmx, m) {
                        int device, const std::string& kernel, int block, int vec, int waves,
                        int tile_rows, const std::string& dtype, bool exact, int graph_batch,
                        bool check, py::object uid, std::vector<int> ranks, std::vector<int> devices,
-                       bool rccl_graph) {
+                       bool rccl_graph, bool overlap) {
              SessionConfig c;
              c.spec = s;
              c.opt = make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact,
-                                  graph_batch, check);
+                                  graph_batch, check, overlap);
              c.split = split;
              c.world = world;
              if (comm == "self") c.comm = CommKind::kSelf;
@@ -321,7 +326,7 @@ PYBIND11_MODULE(_pmx, m) {
            py::arg("tile_rows") = 0, py::arg("dtype") = "fp64", py::arg("exact") = false,
            py::arg("graph_batch") = 32, py::arg("check") = false, py::arg("uid") = py::none(),
            py::arg("ranks") = std::vector<int>{}, py::arg("devices") = std::vector<int>{},
-           py::arg("rccl_graph") = false)
+           py::arg("rccl_graph") = false, py::arg("overlap") = true)
       .def("init", [](Session& s) { py::gil_scoped_release g; s.init(); })
       .def("step", [](Session& s, int64_t n) { py::gil_scoped_release g; s.step(n); })
       .def("synchronize", [](Session& s) { py::gil_scoped_release g; s.synchronize(); })
@@ -349,6 +354,7 @@ PYBIND11_MODULE(_pmx, m) {
       .def("subdomain", [](Session& s, int i) { return sd_dict(s.solver(i).sd()); }, py::arg("i") = 0)
       .def_property_readonly("num_local", &Session::num_local)
       .def_property_readonly("comm_name", &Session::comm_name)
+      .def_property_readonly("overlapped", [](Session& s) { return s.overlapped(); })
       .def_property_readonly("device_bytes", &Session::device_bytes)
       .def_property_readonly("grid", [](Session& s) { return py::make_tuple(s.grid().Px, s.grid().Py); })
       .def_property_readonly("ntiles", [](Session& s) { return s.solver(0).tiles().ntiles(); })

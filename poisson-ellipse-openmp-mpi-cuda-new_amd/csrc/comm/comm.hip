@@ -6,9 +6,9 @@
 //
 // Here:
 //  * RcclComm  — RCCL over xGMI straight from device buffers: ncclSend/ncclRecv pairs inside one
-//                ncclGroup for the 4 halo sides (edges packed by k_pcg_b), and two in-place
-//                ncclAllReduce per iteration (1 double, then (sum dw^2, (z,r)) packed into one
-//                16-byte all-reduce).  Graph-capturable.
+//                ncclGroup for the 4 halo sides (edges packed by k_edge_r / k_pcg_b) on a split
+//                halo communicator, and two in-place ncclAllReduce per iteration (1 double, then
+//                (sum dw^2, (z,r)) packed into one 16-byte all-reduce).  Graph-capturable.
 //  * LocalComm — P subdomains in one process on one device: halos are D2D copies, the
 //                all-reduce is a deterministic rank-ordered sum kernel.  The fake cluster used to
 //                test multi-rank logic on a 1-GPU box.
@@ -107,8 +107,18 @@ class RcclComm final : public Comm {
       }
       RCCL_CHECK(ncclGroupEnd());
     }
+    // A second communicator (same ranks) carries the halos, so the ghost exchange on the comm
+    // stream and the all-reduce on the compute stream never queue behind each other.
+    halo_comms_.resize(comms_.size());
+    RCCL_CHECK(ncclGroupStart());
+    for (size_t i = 0; i < comms_.size(); ++i) {
+      HIP_CHECK(hipSetDevice(devices[i]));
+      RCCL_CHECK(ncclCommSplit(comms_[i], 0, ranks[i], &halo_comms_[i], nullptr));
+    }
+    RCCL_CHECK(ncclGroupEnd());
   }
   ~RcclComm() override {
+    for (auto c : halo_comms_) (void)ncclCommDestroy(c);
     for (auto c : comms_) (void)ncclCommDestroy(c);
   }
 
@@ -132,8 +142,8 @@ class RcclComm final : public Comm {
       const ncclDataType_t t = L.elem == 8 ? ncclFloat64 : ncclFloat32;
       for (int side = 0; side < 4; ++side) {
         if (nb[side] < 0) continue;
-        RCCL_CHECK(ncclSend(s->send_dev(side), L.edge_len[side], t, nb[side], comms_[i], streams[i]));
-        RCCL_CHECK(ncclRecv(s->recv_dev(side), L.edge_len[side], t, nb[side], comms_[i], streams[i]));
+        RCCL_CHECK(ncclSend(s->send_dev(side), L.edge_len[side], t, nb[side], halo_comms_[i], streams[i]));
+        RCCL_CHECK(ncclRecv(s->recv_dev(side), L.edge_len[side], t, nb[side], halo_comms_[i], streams[i]));
       }
     }
     RCCL_CHECK(ncclGroupEnd());
@@ -146,7 +156,8 @@ class RcclComm final : public Comm {
  private:
   int nranks_;
   bool capturable_;
-  std::vector<ncclComm_t> comms_;
+  std::vector<ncclComm_t> comms_;       // scalar all-reduces (compute stream)
+  std::vector<ncclComm_t> halo_comms_;  // ghost exchange (comm stream when overlapped)
 };
 
 }  // namespace

@@ -214,8 +214,8 @@ void GpuSubdomainSolver::phase_a_kernel_only(hipStream_t s) {
 }
 
 template <typename T>
-void GpuSubdomainSolver::phase_b_impl(hipStream_t s) {
-  phase_b_kernel_only<T>(s);
+void GpuSubdomainSolver::phase_b_impl(hipStream_t s, bool pack) {
+  phase_b_kernel_only<T>(s, pack);
   after_launch(s);
   const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
   launch_reduce(partials_, tiles_.ntiles(), 2, wdiff, g_.h1h2, state_->red_b, state_,
@@ -224,14 +224,17 @@ void GpuSubdomainSolver::phase_b_impl(hipStream_t s) {
 }
 
 template <typename T>
-void GpuSubdomainSolver::phase_b_kernel_only(hipStream_t s) {
+void GpuSubdomainSolver::phase_b_kernel_only(hipStream_t s, bool pack) {
+  // pcg_b reads G.nb only to pack the send buffers: clearing it skips the packing
+  DevGeom G = geom_;
+  if (!pack) G.nb = 0;
   if (tiles_.kind == 1)
-    launch_pcg_b_wave<T>(geom_, tables_, static_cast<T*>(field_base(0)),
+    launch_pcg_b_wave<T>(G, tables_, static_cast<T*>(field_base(0)),
                          static_cast<T*>(field_base(1)), static_cast<const T*>(field_base(2)),
                          static_cast<const T*>(field_base(3)), halo<T>(), partials_, state_, tiles_,
                          opt_.exact, s);
   else
-    launch_pcg_b<T>(geom_, tables_, static_cast<T*>(field_base(0)), static_cast<T*>(field_base(1)),
+    launch_pcg_b<T>(G, tables_, static_cast<T*>(field_base(0)), static_cast<T*>(field_base(1)),
                     static_cast<const T*>(field_base(2)), static_cast<const T*>(field_base(3)),
                     halo<T>(), partials_, state_, tiles_, opt_.exact, s);
 }
@@ -243,8 +246,22 @@ void GpuSubdomainSolver::enqueue_init(hipStream_t s) {
 void GpuSubdomainSolver::enqueue_phase_a(hipStream_t s) {
   if (opt_.dtype == DType::kFp64) phase_a_impl<double>(s); else phase_a_impl<float>(s);
 }
-void GpuSubdomainSolver::enqueue_phase_b(hipStream_t s) {
-  if (opt_.dtype == DType::kFp64) phase_b_impl<double>(s); else phase_b_impl<float>(s);
+void GpuSubdomainSolver::enqueue_phase_b(hipStream_t s, bool pack) {
+  if (opt_.dtype == DType::kFp64) phase_b_impl<double>(s, pack); else phase_b_impl<float>(s, pack);
+}
+
+template <typename T>
+static void pack_impl(const GpuSubdomainSolver& g, HaloBufs<T> H, hipStream_t s) {
+  launch_edge_r<T>(g.geom(), g.tables(), static_cast<const T*>(g.field_base(1)),
+                   static_cast<const T*>(g.field_base(2)), static_cast<const T*>(g.field_base(3)), H,
+                   g.state_dev(), g.options().exact, s);
+}
+
+void GpuSubdomainSolver::enqueue_pack(hipStream_t s) {
+  if (geom_.nb == 0) return;
+  if (opt_.dtype == DType::kFp64) pack_impl<double>(*this, halo<double>(), s);
+  else pack_impl<float>(*this, halo<float>(), s);
+  after_launch(s);
 }
 
 double GpuSubdomainSolver::bench_kernel(int which, int abl, int reps, hipStream_t s) {
@@ -345,16 +362,37 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
     streams_.push_back(st);
   }
   if (same_device) streams_.resize(local_.size(), streams_[0]);
+  bool any_nb = false;
+  for (auto* s : local_) any_nb |= s->geom().nb != 0;
+  overlap_ = any_nb && local_[0]->options().overlap;
+  if (overlap_) {
+    for (size_t i = 0; i < nstreams; ++i) {
+      HIP_CHECK(hipSetDevice(local_[i]->device()));
+      hipStream_t st;
+      HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      comm_streams_.push_back(st);
+      hipEvent_t e0, e1;
+      HIP_CHECK(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+      ev_packed_.push_back(e0);
+      ev_halo_.push_back(e1);
+    }
+    if (same_device) comm_streams_.resize(local_.size(), comm_streams_[0]);
+  }
 }
 
 PcgDriver::~PcgDriver() {
   for (auto e : execs_) (void)hipGraphExecDestroy(e);
   for (auto g : graphs_) (void)hipGraphDestroy(g);
-  hipStream_t last = nullptr;
-  for (auto s : streams_) {
-    if (s != last) (void)hipStreamDestroy(s);
-    last = s;
+  for (auto* v : {&streams_, &comm_streams_}) {
+    hipStream_t last = nullptr;
+    for (auto s : *v) {
+      if (s != last) (void)hipStreamDestroy(s);
+      last = s;
+    }
   }
+  for (auto e : ev_packed_) (void)hipEventDestroy(e);
+  for (auto e : ev_halo_) (void)hipEventDestroy(e);
 }
 
 void PcgDriver::synchronize() {
@@ -380,12 +418,46 @@ void PcgDriver::enqueue_one_iteration() {
     local_[i]->enqueue_phase_a(streams_[i]);
   }
   comm_->allreduce(local_, 0, streams_);
+  if (!overlap_) {
+    for (size_t i = 0; i < local_.size(); ++i) {
+      HIP_CHECK(hipSetDevice(local_[i]->device()));
+      local_[i]->enqueue_phase_b(streams_[i]);
+    }
+    comm_->allreduce(local_, 1, streams_);
+    comm_->halo(local_, streams_);
+    return;
+  }
+  // Overlapped: compute stream  [edge r -> send bufs] -> pcg_b -> reduce -> all-reduce(b) -> join
+  //             comm stream           `-> halo send/recv ------------------------------'
+  // The next pcg_a is the only reader of the recv buffers and the next edge kernel the next
+  // writer of the send buffers; both come after the join.
   for (size_t i = 0; i < local_.size(); ++i) {
     HIP_CHECK(hipSetDevice(local_[i]->device()));
-    local_[i]->enqueue_phase_b(streams_[i]);
+    local_[i]->enqueue_pack(streams_[i]);
+  }
+  for_each_stream([&](size_t i, size_t u) {
+    HIP_CHECK(hipEventRecord(ev_packed_[u], streams_[i]));
+    HIP_CHECK(hipStreamWaitEvent(comm_streams_[i], ev_packed_[u], 0));
+  });
+  comm_->halo(local_, comm_streams_);
+  for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipEventRecord(ev_halo_[u], comm_streams_[i])); });
+  for (size_t i = 0; i < local_.size(); ++i) {
+    HIP_CHECK(hipSetDevice(local_[i]->device()));
+    local_[i]->enqueue_phase_b(streams_[i], /*pack=*/false);
   }
   comm_->allreduce(local_, 1, streams_);
-  comm_->halo(local_, streams_);
+  for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipStreamWaitEvent(streams_[i], ev_halo_[u], 0)); });
+}
+
+template <typename F>
+void PcgDriver::for_each_stream(F&& f) {
+  // (index of the first solver using a stream, index of that unique stream)
+  size_t u = 0;
+  for (size_t i = 0; i < streams_.size(); ++i) {
+    if (i > 0 && streams_[i] == streams_[i - 1]) continue;
+    HIP_CHECK(hipSetDevice(local_[i]->device()));
+    f(i, u++);
+  }
 }
 
 void PcgDriver::build_graph() {

@@ -139,7 +139,33 @@ __device__ __forceinline__ double apply_a(double pc, double pim, double pip, dou
     const double Ay = -1.0 / G.h2 * (b1 * (pjp - pc) / G.h2 - b0 * (pc - pjm) / G.h2);
     return Ax + Ay;
   } else {
-    return G.cx * (a1 * (pc - pip) + a0 * (pc - pim)) + G.cy * (b1 * (pc - pjp) + b0 * (pc - pjm));
+    // explicit FMAs: every kernel that evaluates A p (pcg_a, pcg_b, edge_r) gets bit-identical
+    // values whatever the compiler's contraction choices in the surrounding code
+    const double x = __builtin_fma(a1, pc - pip, a0 * (pc - pim));
+    const double y = __builtin_fma(b1, pc - pjp, b0 * (pc - pjm));
+    return __builtin_fma(G.cx, x, G.cy * y);
+  }
+}
+
+// w + alpha p and r - alpha A p.  EXACT: the reference's separate multiply and add
+// (stage0/Withoutopenmp1.cpp:135-143); fast: one explicit FMA each, so the r values packed for the
+// halo by k_edge_r equal those k_pcg_b stores.
+template <bool EXACT>
+__device__ __forceinline__ double upd_w(double wo, double alpha, double p) {
+  if constexpr (EXACT) {
+    PMX_NO_CONTRACT
+    return wo + alpha * p;
+  } else {
+    return __builtin_fma(alpha, p, wo);
+  }
+}
+template <bool EXACT>
+__device__ __forceinline__ double upd_r(double ro, double alpha, double Ap) {
+  if constexpr (EXACT) {
+    PMX_NO_CONTRACT
+    return ro - alpha * Ap;
+  } else {
+    return __builtin_fma(-alpha, Ap, ro);
   }
 }
 

@@ -270,8 +270,8 @@ k_pcg_b(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, const T* 
       const double a0 = acur, a1 = face_a1c(cc, rc, G);
       const double b0 = face_b0c(cc, rc, G), b1 = face_b1c(cc, rc, G);
       const double Ap = apply_a<EXACT>(pc, pm, pp, pjm, pjp, a0, a1, b0, b1, G);
-      const T ws = static_cast<T>(wo + alpha * pc);
-      const T rs = static_cast<T>(ro - alpha * Ap);
+      const T ws = static_cast<T>(upd_w<EXACT>(wo, alpha, pc));
+      const T rs = static_cast<T>(upd_r<EXACT>(ro, alpha, Ap));
       const double dw = double(ws) - wo;
       dacc += dw * dw;
       const double rq = double(rs);
@@ -293,6 +293,44 @@ k_pcg_b(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, const T* 
     partials[2 * t.id] = dacc;
     partials[2 * t.id + 1] = zacc;
   }
+}
+
+// ---------------------------------------------------------------------------
+// k_edge_r: the r update of k_pcg_b restricted to the edge lines that feed a neighbour (one
+// thread per edge node).  Same inputs, coefficient values and expression as k_pcg_b, so the
+// packed values equal the r that k_pcg_b stores.  It reads p, r and the scalars only, so it
+// is enqueued right before k_pcg_b and the halo send waits on it alone.
+// ---------------------------------------------------------------------------
+template <typename T, bool EXACT>
+__global__ void __launch_bounds__(256)
+k_edge_r(DevGeom G, DevTables Tb, const T* __restrict__ r, const T* p0, const T* p1, HaloBufs<T> H,
+         const PcgState* S) {
+  if (S->done) return;
+  const long long k = S->it;
+  const double denom = S->red_a[0];
+  const bool bd = S->norm == int(Norm::kWeighted) ? fabs(denom) < 1e-15 : denom < 1e-15;
+  if (bd || !(denom == denom)) return;  // k_pcg_b records the breakdown
+  const double alpha = S->zr[(k - 1) & 1] / denom;
+  const T* pn = (k & 1) ? p1 : p0;
+  int idx = blockIdx.x * 256 + threadIdx.x;
+  int side = 0;
+  for (; side < 4; ++side) {
+    const int len = side < 2 ? G.ny : G.nx;
+    if (idx < len) break;
+    idx -= len;
+  }
+  if (side == 4 || !(G.nb & (1 << side))) return;  // kNbXlo..kNbYhi == 1 << side
+  const int i = side == 0 ? 1 : side == 1 ? G.nx : idx + 1;
+  const int j = side < 2 ? idx + 1 : side == 2 ? 1 : G.ny;
+  const int gi = G.gi0 + i, gj = G.gj0 + j;
+  const int64_t P = G.pitch, c = int64_t(i) * P + j;
+  const double a0 = coef_a(Tb, G, gi, gj), a1 = coef_a(Tb, G, gi + 1, gj);
+  const double b0 = coef_b(Tb, G, gi, gj), b1 = coef_b(Tb, G, gi, gj + 1);
+  const double pc = double(pn[c]);
+  const double Ap = apply_a<EXACT>(pc, double(pn[c - P]), double(pn[c + P]), double(pn[c - 1]),
+                                   double(pn[c + 1]), a0, a1, b0, b1, G);
+  const double ro = double(r[c]);
+  H.send[side][idx] = static_cast<T>(upd_r<EXACT>(ro, alpha, Ap));
 }
 
 // ---------------------------------------------------------------------------
@@ -388,6 +426,16 @@ void launch_pcg_b(const DevGeom& G, const DevTables& Tb, T* w, T* r, const T* p0
   HIP_CHECK(hipGetLastError());
 }
 
+template <typename T>
+void launch_edge_r(const DevGeom& G, const DevTables& Tb, const T* r, const T* p0, const T* p1,
+                   HaloBufs<T> H, const PcgState* S, bool exact, hipStream_t s) {
+  const int n = 2 * G.nx + 2 * G.ny;
+  const dim3 grid((n + 255) / 256);
+  if (exact) hipLaunchKernelGGL((k_edge_r<T, true>), grid, dim3(256), 0, s, G, Tb, r, p0, p1, H, S);
+  else hipLaunchKernelGGL((k_edge_r<T, false>), grid, dim3(256), 0, s, G, Tb, r, p0, p1, H, S);
+  HIP_CHECK(hipGetLastError());
+}
+
 void launch_reduce(const double* partials, int n, int nq, double w0, double w1, double* out,
                    PcgState* S, int mode, hipStream_t s) {
   PMX_CHECK(nq == 1 || nq == 2, "nq must be 1 or 2");
@@ -408,7 +456,9 @@ void launch_local_allreduce(double* const* bufs, int nranks, int nq, hipStream_t
                                 double*, PcgState*, const TileCfg&, bool, hipStream_t);          \
   template void launch_pcg_b<T>(const DevGeom&, const DevTables&, T*, T*, const T*, const T*,    \
                                 HaloBufs<T>, double*, PcgState*, const TileCfg&, bool,           \
-                                hipStream_t);
+                                hipStream_t);                                                    \
+  template void launch_edge_r<T>(const DevGeom&, const DevTables&, const T*, const T*, const T*, \
+                                 HaloBufs<T>, const PcgState*, bool, hipStream_t);
 PMX_INST(double)
 PMX_INST(float)
 #undef PMX_INST

@@ -395,8 +395,8 @@ k_pcg_b_wave(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
       const double pc = pr[S0][u];
       const double Ap = apply_a<EXACT>(pc, pr[SM][u], pr[SP][u], pjm, pjp, a0, a1, b0, b1, G);
       const double wo = wr[WC][u], ro = rr[WC][u];
-      ws[u] = static_cast<T>(wo + alpha * pc);
-      rs[u] = static_cast<T>(ro - alpha * Ap);
+      ws[u] = static_cast<T>(upd_w<EXACT>(wo, alpha, pc));
+      rs[u] = static_cast<T>(upd_r<EXACT>(ro, alpha, Ap));
       if (valid[u]) {
         const double dw = double(ws[u]) - wo;
         dacc += dw * dw;

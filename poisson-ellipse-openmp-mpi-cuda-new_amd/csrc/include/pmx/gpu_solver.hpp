@@ -46,6 +46,7 @@ struct GpuOptions {
   bool exact = false;     // reference arithmetic order inside the fused kernels
   int graph_batch = 32;   // iterations per captured hipGraph (0 = eager launches)
   bool check = false;     // PMX_CHECK mode: synchronise + error-check after every launch
+  bool overlap = true;    // halo exchange on a comm stream, overlapped with pcg_b
 };
 
 struct CommLayout {
@@ -69,7 +70,9 @@ class GpuSubdomainSolver {
 
   void enqueue_init(hipStream_t s);     // r=B, w=0, p=0, state reset, red_b <- (0, zr_0)
   void enqueue_phase_a(hipStream_t s);  // k_pcg_a + reduce -> red_a
-  void enqueue_phase_b(hipStream_t s);  // k_pcg_b + reduce -> red_b, it += 1
+  // k_pcg_b + reduce -> red_b, it += 1.  pack=false: the edges were packed by enqueue_pack.
+  void enqueue_phase_b(hipStream_t s, bool pack = true);
+  void enqueue_pack(hipStream_t s);     // k_edge_r: r^{k+1} edges -> send buffers
 
   PcgState read_state(hipStream_t s) const;  // synchronous D2H of the scalars
   // Kernel isolation benchmark: pins the scalar state to a mid-solve iteration and launches
@@ -103,9 +106,9 @@ class GpuSubdomainSolver {
  private:
   template <typename T> void init_impl(hipStream_t s);
   template <typename T> void phase_a_impl(hipStream_t s);
-  template <typename T> void phase_b_impl(hipStream_t s);
+  template <typename T> void phase_b_impl(hipStream_t s, bool pack);
   template <typename T> void phase_a_kernel_only(hipStream_t s);
-  template <typename T> void phase_b_kernel_only(hipStream_t s);
+  template <typename T> void phase_b_kernel_only(hipStream_t s, bool pack = true);
   template <typename T> HaloBufs<T> halo() const;
   void after_launch(hipStream_t s) const;
 
@@ -178,15 +181,21 @@ class PcgDriver {
   RunStats profile_phases(int64_t n);    // eager iterations with events around each phase
   PcgState state(int idx = 0);
   std::vector<hipStream_t>& streams() { return streams_; }
+  bool overlapped() const { return overlap_; }
 
  private:
   void enqueue_one_iteration();
   void build_graph();
+  template <typename F> void for_each_stream(F&& f);
 
   std::vector<GpuSubdomainSolver*> local_;
   Comm* comm_;
   int graph_batch_;
   std::vector<hipStream_t> streams_;
+  // halo/compute overlap: one comm stream per compute stream, fork/join events per iteration
+  bool overlap_ = false;
+  std::vector<hipStream_t> comm_streams_;
+  std::vector<hipEvent_t> ev_packed_, ev_halo_;
   bool graph_ok_ = false;
   std::vector<hipGraph_t> graphs_;
   std::vector<hipGraphExec_t> execs_;

@@ -64,6 +64,13 @@ void launch_pcg_b_wave(const DevGeom& G, const DevTables& Tb, T* w, T* r, const 
                        const T* p1, HaloBufs<T> H, double* partials, PcgState* S,
                        const TileCfg& tc, bool exact, hipStream_t s);
 
+// Halo/compute overlap: r^{k+1} on the subdomain edges that have a neighbour,
+// written to the send buffers only, with exactly the arithmetic of pcg_b.  Runs first so the
+// ghost exchange on the comm stream overlaps pcg_b, which then skips its own packing.
+template <typename T>
+void launch_edge_r(const DevGeom& G, const DevTables& Tb, const T* r, const T* p0, const T* p1,
+                   HaloBufs<T> H, const PcgState* S, bool exact, hipStream_t s);
+
 void launch_reduce(const double* partials, int n, int nq, double w0, double w1, double* out,
                    PcgState* S, int mode, hipStream_t s);
 

@@ -40,6 +40,7 @@ class Session {
   int num_local() const { return int(solvers_.size()); }
   GpuSubdomainSolver& solver(int i) { return *solvers_.at(size_t(i)); }
   const std::string comm_name() const { return comm_->name(); }
+  bool overlapped() const { return driver_->overlapped(); }
   size_t device_bytes() const;
   // global (M+1) x (N+1) solution filled with the subdomains owned by this process
   std::vector<double> gather_local_w();

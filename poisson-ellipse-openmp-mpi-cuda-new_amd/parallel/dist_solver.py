@@ -32,7 +32,8 @@ from .launch import DistInfo
 class DistGpuPCG:
     def __init__(self, problem, info: DistInfo, comm: str = "native", split: str = "reference",
                  dtype: str = "fp64", kernel: str = "wave", block: int = 256, vec: int = 2, waves: int = 4,
-                 tile_rows: int = 0, exact: bool = False, graph_batch: int = 32, rccl_graph: bool = False):
+                 tile_rows: int = 0, exact: bool = False, graph_batch: int = 32, rccl_graph: bool = False,
+                 overlap: bool = True):
         self.problem = problem
         self.info = info
         self.comm_kind = comm
@@ -51,7 +52,8 @@ class DistGpuPCG:
                                           kernel=kernel, block=block, vec=vec, waves=waves,
                                           tile_rows=tile_rows, dtype=dtype, exact=exact,
                                           graph_batch=graph_batch if rccl_graph else 0, uid=uid[0],
-                                          ranks=[info.rank], devices=[self.device], rccl_graph=rccl_graph)
+                                          ranks=[info.rank], devices=[self.device], rccl_graph=rccl_graph,
+                                          overlap=overlap)
             self.sd = self.session.subdomain(0)
         elif comm == "torch":
             lay = self.n.comm_layout(problem.M, problem.N, self.Px, self.Py, info.rank, dtype)

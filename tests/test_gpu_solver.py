@@ -74,7 +74,7 @@ def test_lds_tile_shapes(pkg, block, rows):
     assert np.abs(r.w - ref.w).max() < 1e-12
 
 
-@pytest.mark.parametrize("vec,waves,rows", [(1, 4, 1), (2, 4, 64), (2, 1, 5), (2, 8, 33), (1, 4, 0), (2, 4, 0), (4, 4, 0), (4, 1, 7)])
+@pytest.mark.parametrize("vec,waves,rows", [(1, 4, 1), (2, 4, 64), (2, 1, 5), (2, 8, 33), (1, 4, 0), (2, 4, 0), (4, 4, 0), (4, 4, 7)])
 @pytest.mark.parametrize("grid", [(211, 1031), (97, 130), (300, 257)])
 def test_wave_tile_shapes(pkg, vec, waves, rows, grid):
     """Wave-tile kernels on full and partial tiles (odd widths leave half-filled lanes)."""
@@ -108,6 +108,36 @@ def test_graph_vs_eager(pkg):
     b = pkg.solve(p, "hip", graph_batch=16)
     assert a.iters == b.iters == 546
     assert np.array_equal(a.w, b.w)
+
+
+@pytest.mark.parametrize("kernel", ["wave", "lds"])
+@pytest.mark.parametrize("ranks,split", [(2, "reference"), (4, "reference"), (7, "auto"), (3, "cols")])
+def test_overlap_matches_serial_halo(pkg, kernel, ranks, split):
+    """Halo on a second stream (edges packed by k_edge_r) is bit-identical to the in-order path."""
+    p = pkg.PoissonEllipse(M=260, N=390)
+    a = pkg.solve(p, "hip", kernel=kernel, ranks=ranks, split=split, overlap=False)
+    b = pkg.solve(p, "hip", kernel=kernel, ranks=ranks, split=split, overlap=True)
+    assert a.iters == b.iters
+    assert np.array_equal(a.w, b.w)
+
+
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+def test_overlap_graph_vs_eager(pkg, dtype):
+    p = pkg.PoissonEllipse(M=400, N=600)
+    a = pkg.solve(p, "hip", ranks=4, overlap=True, graph_batch=0, dtype=dtype)
+    b = pkg.solve(p, "hip", ranks=4, overlap=True, graph_batch=16, dtype=dtype)
+    assert a.iters == b.iters
+    assert np.array_equal(a.w, b.w)
+    if dtype == "fp64":
+        assert a.iters == 546
+
+
+def test_session_reports_overlap(pkg):
+    p = pkg.PoissonEllipse(M=100, N=120)
+    models = sub("models")
+    assert models.make_session(p, ranks=2, overlap=True).overlapped
+    assert not models.make_session(p, ranks=2, overlap=False).overlapped
+    assert not models.make_session(p, ranks=1, overlap=True).overlapped  # no neighbours
 
 
 def test_fp32_mixed(pkg):
