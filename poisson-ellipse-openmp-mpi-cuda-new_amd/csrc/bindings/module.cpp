@@ -245,6 +245,10 @@ PYBIND11_MODULE(_pmx, m) {
     if (hipGetDeviceCount(&n) != hipSuccess) { (void)hipGetLastError(); return 0; }
     return n;
   });
+  m.def("mfma_wave_sums", [](uintptr_t x, uintptr_t out, int nwaves, bool fp32, uintptr_t stream) {
+    if (fp32) launch_wave_sums<float>(reinterpret_cast<const float*>(x), reinterpret_cast<float*>(out), nwaves, as_stream(stream));
+    else launch_wave_sums<double>(reinterpret_cast<const double*>(x), reinterpret_cast<double*>(out), nwaves, as_stream(stream));
+  }, py::arg("x"), py::arg("out"), py::arg("nwaves"), py::arg("fp32") = false, py::arg("stream") = 0);
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("comm_layout", [](int M, int N, int Px, int Py, int rank, const std::string& dtype) {
     const Subdomain sd = decompose_2d(M, N, ProcGrid{Px, Py}, rank);

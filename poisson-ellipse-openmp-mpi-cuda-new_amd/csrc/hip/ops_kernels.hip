@@ -72,6 +72,31 @@ k_dot_partials(DevGeom G, const T* __restrict__ x, const T* __restrict__ y, doub
   if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
 
+// MFMA wave reductions (pcg_device.hpp) on arbitrary data, for the unit tests: per wave64 of x,
+// out[3w] = sum x, out[3w+1] = sum x (packed pair), out[3w+2] = sum x^2 (packed pair)
+template <typename T>
+__global__ void __launch_bounds__(256) k_wave_sums(const T* __restrict__ x, T* __restrict__ out, int nw) {
+  const int w = blockIdx.x * 4 + int(threadIdx.x >> 6);
+  if (w >= nw) return;  // wave-uniform: EXEC stays full for the MFMAs
+  const T v = x[int64_t(w) * 64 + (threadIdx.x & 63)];
+  const T s = wave_sum_mfma(v);
+  T a = v, b = v * v;
+  wave_sum2_mfma(a, b);
+  if ((threadIdx.x & 63) == 0) {
+    out[3 * w] = s;
+    out[3 * w + 1] = a;
+    out[3 * w + 2] = b;
+  }
+}
+
+template <typename T>
+void launch_wave_sums(const T* x, T* out, int nw, hipStream_t s) {
+  hipLaunchKernelGGL((k_wave_sums<T>), dim3((nw + 3) / 4), dim3(256), 0, s, x, out, nw);
+  HIP_CHECK(hipGetLastError());
+}
+template void launch_wave_sums<double>(const double*, double*, int, hipStream_t);
+template void launch_wave_sums<float>(const float*, float*, int, hipStream_t);
+
 // one workgroup per global row gi: out range (first/last j whose coefficient is not 1/eps) and
 // in range (first/last j equal to 1, kept only if every j between is exactly 1)
 __global__ void __launch_bounds__(256)

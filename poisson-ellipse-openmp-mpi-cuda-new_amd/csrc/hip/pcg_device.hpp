@@ -173,18 +173,75 @@ __device__ __forceinline__ bool dirichlet(const DevGeom& G, int gi, int gj) {
   return gi <= 0 || gi >= G.M || gj <= 0 || gj >= G.N;
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int off = kWave / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
-  return v;
+// ---- wave64 reductions on the matrix cores --------------------------------------------------
+// v_mfma_*_16x16x4 with B = ones computes D[i][j] = sum_k A[i][k], where lane l supplies
+// A[l % 16][l / 16]: one MFMA folds the 64 lanes into 16 row sums (lanes i, i+16, i+32, i+48).
+// Lane l receives 4 of those rows (a set fixed by l / 16 that partitions the 16 rows; f64 and f32
+// interleave them differently, see wave_sum2_mfma), so after
+// adding its 4 outputs every lane of group g = l / 16 holds the same group sum S_g, and a second
+// MFMA with A[.][g] = S_g sums the 4 groups.  No LDS and no cross-lane permutes; deterministic.
+// Requires a full EXEC mask (all callers reduce after their wave-uniform control flow).
+typedef double v4f64 __attribute__((ext_vector_type(4)));
+typedef float v4f32 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4f64 mfma_rowsum(double a) {
+  const v4f64 z = {0.0, 0.0, 0.0, 0.0};
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, 1.0, z, 0, 0, 0);
 }
+__device__ __forceinline__ v4f32 mfma_rowsum(float a) {
+  const v4f32 z = {0.f, 0.f, 0.f, 0.f};
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, 1.0f, z, 0, 0, 0);
+}
+
+__device__ __forceinline__ double readlane_t(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane(int(b), lane);
+  const int hi = __builtin_amdgcn_readlane(int(b >> 32), lane);
+  return __longlong_as_double((long long)(unsigned)lo | ((long long)hi << 32));
+}
+__device__ __forceinline__ float readlane_t(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// sum over the wave, returned in every lane
+template <typename T>
+__device__ __forceinline__ T wave_sum_mfma(T v) {
+  auto d = mfma_rowsum(v);
+  const T g = (d[0] + d[1]) + (d[2] + d[3]);
+  d = mfma_rowsum(g);
+  return d[0];
+}
+
+// Packed pair: two first-stage MFMAs, then ONE second-stage MFMA whose rows 0-7 carry the group
+// sums of v0 and rows 8-15 those of v1.  Lanes 0-31 end with sum(v0), lanes 32-63 with sum(v1);
+// both are returned wave-uniform.
+template <typename T>
+__device__ __forceinline__ void wave_sum2_mfma(T& v0, T& v1) {
+  const auto d0 = mfma_rowsum(v0);
+  const auto d1 = mfma_rowsum(v1);
+  const T g0 = (d0[0] + d0[1]) + (d0[2] + d0[3]);
+  const T g1 = (d1[0] + d1[1]) + (d1[2] + d1[3]);
+  const int lane = __lane_id();
+  const auto e = mfma_rowsum((lane & 15) < 8 ? g0 : g1);
+  // D[i][j] = sum_k A[i][k]: rows 0-7 hold sum(v0), rows 8-15 sum(v1).  Output rows of lane l,
+  // register r (measured on gfx950, bench/probe/mfma_layout.hip): f64 row l/16 + 4r, f32 row
+  // 4(l/16) + r.  So f64 reads lane 0 registers 0 / 2 and f32 lanes 0 / 32 of register 0.
+  if constexpr (sizeof(T) == 8) {
+    v0 = readlane_t(e[0], 0);
+    v1 = readlane_t(e[2], 0);
+  } else {
+    v0 = readlane_t(e[0], 0);
+    v1 = readlane_t(e[0], 32);
+  }
+}
+
+__device__ __forceinline__ double wave_sum(double v) { return wave_sum_mfma(v); }
 
 // Deterministic block sum of up to two values; result valid in thread 0.
 template <int BLOCK>
 __device__ __forceinline__ void block_sum2(double& v0, double& v1, double* lds /*2*BLOCK/64*/) {
   constexpr int NW = BLOCK / kWave;
-  v0 = wave_sum(v0);
-  v1 = wave_sum(v1);
+  wave_sum2_mfma(v0, v1);
   const int wid = threadIdx.x / kWave, lane = threadIdx.x % kWave;
   if (lane == 0) { lds[wid] = v0; lds[NW + wid] = v1; }
   __syncthreads();

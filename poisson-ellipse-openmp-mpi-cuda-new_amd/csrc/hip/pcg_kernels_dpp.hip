@@ -26,12 +26,6 @@ namespace {
 
 constexpr int kMaxWaveRows = 256;
 
-__device__ __forceinline__ double readlane_f64(double v, int lane) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane(int(b), lane);
-  const int hi = __builtin_amdgcn_readlane(int(b >> 32), lane);
-  return __longlong_as_double((long long)(unsigned)lo | ((long long)hi << 32));
-}
 
 // DPP wave shifts on a double: lane l receives lane l-1's (SHR) / l+1's (SHL) value; the edge lane
 // that has no source keeps `edge`.
@@ -228,8 +222,8 @@ k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, Hal
       if (h_store && !h_dir) pnew[int64_t(i) * P + jh] = static_cast<T>(hv);
       hv = double(static_cast<T>(hv));
     }
-    const double hl_i = readlane_f64(hv, 0);
-    const double hr_i = readlane_f64(hv, 1);
+    const double hl_i = readlane_t(hv, 0);
+    const double hr_i = readlane_t(hv, 1);
     double a0[VEC], a1[VEC], b0[VEC], b1[VEC], pc[VEC];
     T st[VEC];
 #pragma unroll
@@ -441,8 +435,7 @@ k_pcg_b_wave(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
     if (i + 3 > t.iend) break;
     step(std::integral_constant<int, 3>{}, i + 3);
   }
-  dacc = wave_sum(dacc);
-  zacc = wave_sum(zacc);
+  wave_sum2_mfma(dacc, zacc);
   if (lane == 0) {
     partials[2 * t.id] = dacc;
     partials[2 * t.id + 1] = zacc;

@@ -81,6 +81,10 @@ void launch_local_allreduce(double* const* bufs, int nranks, int nq, hipStream_t
 // Per-row coefficient classes (see DevTables::acls); rows gi = 0..M+1, columns j = 0..N+1.
 void launch_classify(const DevGeom& Gglobal, const DevTables& Tb, int* acls, int* bcls, hipStream_t s);
 
+// MFMA wave reductions on test data: per wave64 w, out[3w..3w+2] = (sum x, sum x, sum x^2)
+template <typename T>
+void launch_wave_sums(const T* x, T* out, int nwaves, hipStream_t s);
+
 // ---- unfused ops (tests, naive solver mode, bit-equality checks) ----
 // All fields are local arrays with ghost ring: element (li,lj) at f[li*pitch+lj].
 void launch_assemble(const DevGeom& G, const DevTables& Tb, double* a, double* b, double* B,

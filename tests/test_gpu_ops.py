@@ -67,3 +67,21 @@ def test_ops_reject_bad_shapes(pkg, dev):
     ops = sub("ops").DeviceOps(p)
     with pytest.raises(ValueError):
         ops.apply_A(torch.zeros(5, 5, device=dev, dtype=torch.float64))
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-13), (torch.float32, 2e-5)])
+def test_mfma_wave_reductions(native, dev, dtype, tol):
+    """Matrix-core wave64 sums (single and packed pair) vs torch fp64 sums per wave."""
+    nw = 1000
+    g = torch.Generator().manual_seed(1)
+    x = (torch.rand(nw * 64, generator=g, dtype=torch.float64) - 0.3).to(dtype)
+    out = torch.zeros(nw * 3, dtype=dtype, device=dev)
+    xd = x.to(dev)
+    native.mfma_wave_sums(xd.data_ptr(), out.data_ptr(), nw, dtype == torch.float32,
+                          torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    xr = x.double().view(nw, 64)
+    ref = torch.stack([xr.sum(1), xr.sum(1), (xr * xr).sum(1)], 1).flatten()
+    o = out.cpu().double()
+    scale = torch.stack([xr.abs().sum(1)] * 2 + [(xr * xr).sum(1)], 1).flatten()
+    assert ((o - ref).abs() <= tol * scale).all(), (o - ref).abs().max()

@@ -166,6 +166,21 @@ def test_subdomain_solver_torch_arena(pkg, native):
     assert np.abs(r.w - ref.w).max() < 1e-12
 
 
+@pytest.mark.parametrize("rccl_graph", [False, True])
+def test_native_rccl_world1(pkg, rccl_graph):
+    """Production multi-GPU path with one rank: ncclCommInitRank + ncclCommSplit + in-place
+    all-reduces on the solver stream (optionally captured in the hipGraph)."""
+    launch = sub("parallel.launch")
+    ds = sub("parallel.dist_solver")
+    p = pkg.PoissonEllipse(M=400, N=600)
+    s = ds.DistGpuPCG(p, launch.DistInfo(), comm="native", rccl_graph=rccl_graph)
+    r = s.solve()
+    assert r.iters == 546 and r.status == "converged"
+    assert s.session.comm_name == "rccl"
+    ref = pkg.solve(p, "hip")
+    assert np.array_equal(r.w, ref.w)
+
+
 def test_bench_session_steps(pkg):
     """step()/state() contract used by bench.py: `it` advances by exactly the steps launched."""
     p = pkg.PoissonEllipse(M=1024, N=1024)
