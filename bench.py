@@ -40,7 +40,9 @@ def parse():
     ap.add_argument("--kernel", default="wave", choices=["wave", "lds"],
                     help="wave: wave-tile kernels with DPP lane shifts; lds: workgroup tiles + LDS row ring")
     ap.add_argument("--block", type=int, default=256, help="lds kernels: tile width")
-    ap.add_argument("--vec", type=int, default=2, help="wave kernels: columns per lane")
+    ap.add_argument("--vec", type=int, default=0, help="wave kernels: columns per lane (0 = per-kernel best)")
+    ap.add_argument("--vec-b", type=int, default=0, help="pcg_b columns per lane (0 = follow --vec / auto)")
+    ap.add_argument("--tile-rows-b", type=int, default=-1, help="pcg_b tile height (-1 = --tile-rows)")
     ap.add_argument("--waves", type=int, default=4, help="wave kernels: wave tiles per workgroup")
     ap.add_argument("--tile-rows", type=int, default=0, help="tile height (0 = auto)")
     ap.add_argument("--graph-batch", type=int, default=32)
@@ -76,7 +78,7 @@ def main():
     problem = pmx.PoissonEllipse(M=args.M, N=args.N)
     kw = dict(split=args.split, dtype=args.dtype, kernel=args.kernel, block=args.block, vec=args.vec,
               waves=args.waves, tile_rows=args.tile_rows, exact=args.exact, graph_batch=args.graph_batch,
-              overlap=args.overlap == "on")
+              overlap=args.overlap == "on", vec_b=args.vec_b, tile_rows_b=args.tile_rows_b)
     comm_used = args.comm
     if world == 1:
         models = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.models")
@@ -86,6 +88,10 @@ def main():
             init = sess.init
             step = sess.step
             synchronize = sess.synchronize
+
+            @staticmethod
+            def tile():
+                return sess.tile
 
             @staticmethod
             def state():
@@ -127,6 +133,7 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    tile_desc = runner.tile() if hasattr(runner, "tile") else dict(rows=args.tile_rows, vec=args.vec)
     valid = (not st1["done"]) and (st1["it"] - st0["it"] == args.steps) and not st1["nan"]
     pts = (args.M - 1) * (args.N - 1)
     mlups = pts * args.steps / dt / 1e6
@@ -180,7 +187,7 @@ def main():
                 "grid": [args.M, args.N],
                 "comm": comm_used,
                 "kernel": args.kernel,
-                "tile": dict(rows=args.tile_rows, block=args.block, vec=args.vec, waves=args.waves),
+                "tile": tile_desc,
                 "graph_batch": args.graph_batch,
                 "overlap": args.overlap,
                 "exact": args.exact,

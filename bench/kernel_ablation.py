@@ -26,7 +26,7 @@ a = ap.parse_args()
 def parse_cfg(c):
     parts = c.split(":")
     kw = dict(kernel=parts[0])
-    keys = dict(b="block", v="vec", w="waves", r="tile_rows")
+    keys = dict(b="block", v="vec", w="waves", r="tile_rows", V="vec_b", W="waves_b", R="tile_rows_b")
     for q in parts[1:]:
         kw[keys[q[0]]] = int(q[1:])
     return kw

@@ -8,7 +8,7 @@
 //       [--backend cpu|omp|hip] [--threads T] [--ranks P] [--gpus G] [--comm self|local|rccl]
 //       [--split reference|auto|rows|cols] [--dtype fp64|fp32] [--norm weighted|unweighted]
 //       [--exact] [--graph-batch 32] [--tile-rows 0] [--kernel wave|lds] [--vec 2] [--waves 4]
-//       [--block 256] [--device D]
+//       [--block 256] [--device D] [--vec-b V] [--waves-b W] [--tile-rows-b R]
 //       [--dump sol.txt] [--dump-stride s] [--json] [--banner stage0..stage4]
 //       [--profile-phases N] [--check] [--overlap on|off]
 #include <chrono>
@@ -44,7 +44,7 @@ struct Cli {
                "           [--comm self|local|rccl] [--split reference|auto|rows|cols]\n"
                "           [--dtype fp64|fp32] [--norm weighted|unweighted] [--exact]\n"
                "           [--graph-batch N] [--tile-rows R] [--kernel wave|lds] [--vec V]\n"
-               "           [--waves W] [--block B] [--device D]\n"
+               "           [--waves W] [--block B] [--device D] [--vec-b V] [--waves-b W] [--tile-rows-b R]\n"
                "           [--dump FILE] [--dump-stride S] [--json] [--banner stage0..stage4]\n"
                "           [--profile-phases N] [--check] [--overlap on|off]\n";
   std::exit(msg ? 2 : 0);
@@ -97,6 +97,9 @@ Cli parse(int argc, char** argv) {
     else if (a == "--block") c.opt.block = std::atoi(val().c_str());
     else if (a == "--vec") c.opt.vec = std::atoi(val().c_str());
     else if (a == "--waves") c.opt.waves = std::atoi(val().c_str());
+    else if (a == "--vec-b") c.opt.vec_b = std::atoi(val().c_str());
+    else if (a == "--waves-b") c.opt.waves_b = std::atoi(val().c_str());
+    else if (a == "--tile-rows-b") c.opt.tile_rows_b = std::atoi(val().c_str());
     else if (a == "--kernel") {
       const std::string v = val();
       if (v != "wave" && v != "lds") usage("--kernel wave|lds");

@@ -151,7 +151,7 @@ class OpContext {
 
 GpuOptions make_options(int device, const std::string& kernel, int block, int vec, int waves,
                         int tile_rows, const std::string& dtype, bool exact, int graph_batch, bool check,
-                        bool overlap = true) {
+                        bool overlap = true, int vec_b = 0, int waves_b = 0, int tile_rows_b = -1) {
   GpuOptions o;
   o.device = device;
   PMX_CHECK(kernel == "lds" || kernel == "wave", "kernel must be lds or wave, got " << kernel);
@@ -166,6 +166,9 @@ GpuOptions make_options(int device, const std::string& kernel, int block, int ve
   o.graph_batch = graph_batch;
   o.check = check;
   o.overlap = overlap;
+  o.vec_b = vec_b;
+  o.waves_b = waves_b;
+  o.tile_rows_b = tile_rows_b;
   return o;
 }
 
@@ -271,17 +274,20 @@ PYBIND11_MODULE(_pmx, m) {
   py::class_<GpuSubdomainSolver>(m, "SubdomainSolver")
       .def(py::init([](const ProblemSpec& s, int Px, int Py, int rank, int device,
                        const std::string& kernel, int block, int vec, int waves, int tile_rows,
-                       const std::string& dtype, bool exact, uintptr_t arena, bool check) {
+                       const std::string& dtype, bool exact, uintptr_t arena, bool check, int vec_b,
+                       int waves_b, int tile_rows_b) {
              const Subdomain sd = decompose_2d(s.M, s.N, ProcGrid{Px, Py}, rank);
              return std::make_unique<GpuSubdomainSolver>(
-                 s, sd, make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact, 0, check),
+                 s, sd, make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact, 0, check,
+                                     true, vec_b, waves_b, tile_rows_b),
                  arena);
            }),
            py::arg("spec"), py::arg("Px") = 1, py::arg("Py") = 1, py::arg("rank") = 0,
            py::arg("device") = 0, py::arg("kernel") = "wave", py::arg("block") = 256,
-           py::arg("vec") = 2, py::arg("waves") = 4, py::arg("tile_rows") = 0,
+           py::arg("vec") = 0, py::arg("waves") = 4, py::arg("tile_rows") = 0,
            py::arg("dtype") = "fp64", py::arg("exact") = false, py::arg("arena") = 0,
-           py::arg("check") = false)
+           py::arg("check") = false, py::arg("vec_b") = 0, py::arg("waves_b") = 0,
+           py::arg("tile_rows_b") = -1)
       .def("enqueue_init", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_init(as_stream(s)); })
       .def("enqueue_phase_a", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_phase_a(as_stream(s)); })
       .def("enqueue_phase_b", [](GpuSubdomainSolver& g, uintptr_t s, bool pack) {
@@ -306,11 +312,11 @@ PYBIND11_MODULE(_pmx, m) {
                        int device, const std::string& kernel, int block, int vec, int waves,
                        int tile_rows, const std::string& dtype, bool exact, int graph_batch,
                        bool check, py::object uid, std::vector<int> ranks, std::vector<int> devices,
-                       bool rccl_graph, bool overlap) {
+                       bool rccl_graph, bool overlap, int vec_b, int waves_b, int tile_rows_b) {
              SessionConfig c;
              c.spec = s;
              c.opt = make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact,
-                                  graph_batch, check, overlap);
+                                  graph_batch, check, overlap, vec_b, waves_b, tile_rows_b);
              c.split = split;
              c.world = world;
              if (comm == "self") c.comm = CommKind::kSelf;
@@ -326,11 +332,12 @@ PYBIND11_MODULE(_pmx, m) {
            }),
            py::arg("spec"), py::arg("world") = 1, py::arg("comm") = "self",
            py::arg("split") = Split::kReference, py::arg("device") = 0, py::arg("kernel") = "wave",
-           py::arg("block") = 256, py::arg("vec") = 2, py::arg("waves") = 4,
+           py::arg("block") = 256, py::arg("vec") = 0, py::arg("waves") = 4,
            py::arg("tile_rows") = 0, py::arg("dtype") = "fp64", py::arg("exact") = false,
            py::arg("graph_batch") = 32, py::arg("check") = false, py::arg("uid") = py::none(),
            py::arg("ranks") = std::vector<int>{}, py::arg("devices") = std::vector<int>{},
-           py::arg("rccl_graph") = false, py::arg("overlap") = true)
+           py::arg("rccl_graph") = false, py::arg("overlap") = true, py::arg("vec_b") = 0,
+           py::arg("waves_b") = 0, py::arg("tile_rows_b") = -1)
       .def("init", [](Session& s) { py::gil_scoped_release g; s.init(); })
       .def("step", [](Session& s, int64_t n) { py::gil_scoped_release g; s.step(n); })
       .def("synchronize", [](Session& s) { py::gil_scoped_release g; s.synchronize(); })
@@ -363,10 +370,14 @@ PYBIND11_MODULE(_pmx, m) {
       .def_property_readonly("grid", [](Session& s) { return py::make_tuple(s.grid().Px, s.grid().Py); })
       .def_property_readonly("ntiles", [](Session& s) { return s.solver(0).tiles().ntiles(); })
       .def_property_readonly("tile", [](Session& s) {
-        const TileCfg& t = s.solver(0).tiles();
-        py::dict d;
-        d["kind"] = t.kind == 0 ? "lds" : "wave"; d["block"] = t.block; d["rows"] = t.rows;
-        d["vec"] = t.vec; d["waves"] = t.waves; d["tiles_i"] = t.tiles_i; d["tiles_j"] = t.tiles_j;
+        auto one = [](const TileCfg& t) {
+          py::dict d;
+          d["kind"] = t.kind == 0 ? "lds" : "wave"; d["block"] = t.block; d["rows"] = t.rows;
+          d["vec"] = t.vec; d["waves"] = t.waves; d["tiles_i"] = t.tiles_i; d["tiles_j"] = t.tiles_j;
+          return d;
+        };
+        py::dict d = one(s.solver(0).tiles());
+        d["b"] = one(s.solver(0).tiles_b());
         return d;
       });
 }

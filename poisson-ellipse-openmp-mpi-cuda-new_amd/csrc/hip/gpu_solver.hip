@@ -115,11 +115,21 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
   tables_ = upload_tables(spec, &tables_buf_);
 
   PMX_CHECK(opt.kernel == 0 || opt.kernel == 1, "kernel must be 0 (lds) or 1 (wave/dpp)");
+  // tile shapes per kernel (profiles/tile_counters_16384_fp64.md: pcg_a is fastest with 4
+  // columns/lane, pcg_b with 2 in fp64; fp32 moves 16 B with 4 columns)
+  const bool fp64 = opt.dtype == DType::kFp64;
+  const int vec_a = opt.vec ? opt.vec : (opt.waves == 4 ? 4 : 2);  // (4, 4) is instantiated
+  const int vec_b = opt.vec_b ? opt.vec_b : opt.vec ? opt.vec : (fp64 || opt.waves != 4 ? 2 : 4);
+  const int waves_b = opt.waves_b ? opt.waves_b : opt.waves;
+  const int rows_b = opt.tile_rows_b >= 0 ? opt.tile_rows_b : opt.tile_rows;
+  // auto tile heights: pcg_a plateaus at 32-48 rows, pcg_b at 16-24 (bench/tile_sweep.py, 16384^2)
   tiles_ = opt.kernel == 0 ? make_tiles(G, opt.block, opt.tile_rows)
-                           : make_wave_tiles(G, opt.vec, opt.waves, opt.tile_rows);
+                           : make_wave_tiles(G, vec_a, opt.waves, opt.tile_rows, 32);
+  tiles_b_ = opt.kernel == 0 ? make_tiles(G, opt.block, rows_b)
+                             : make_wave_tiles(G, vec_b, waves_b, rows_b, 24);
 
   init_tiles_ = make_tiles(G, 256, 0);
-  const size_t npart = size_t(std::max(tiles_.ntiles(), init_tiles_.ntiles()));
+  const size_t npart = size_t(std::max({tiles_.ntiles(), tiles_b_.ntiles(), init_tiles_.ntiles()}));
   HIP_CHECK(hipMalloc(&partials_, npart * 2 * sizeof(double)));
 
   layout_ = comm_layout(sd, opt.dtype);
@@ -148,7 +158,7 @@ GpuSubdomainSolver::~GpuSubdomainSolver() {
 
 size_t GpuSubdomainSolver::device_bytes() const {
   return 4 * field_bytes_ + (4 * (spec_.M + 2) + 4 * (spec_.N + 2)) * sizeof(double) +
-         size_t(std::max(tiles_.ntiles(), init_tiles_.ntiles())) * 2 * sizeof(double) +
+         size_t(std::max({tiles_.ntiles(), tiles_b_.ntiles(), init_tiles_.ntiles()})) * 2 * sizeof(double) +
          (own_arena_ ? layout_.bytes : 0);
 }
 
@@ -218,7 +228,7 @@ void GpuSubdomainSolver::phase_b_impl(hipStream_t s, bool pack) {
   phase_b_kernel_only<T>(s, pack);
   after_launch(s);
   const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
-  launch_reduce(partials_, tiles_.ntiles(), 2, wdiff, g_.h1h2, state_->red_b, state_,
+  launch_reduce(partials_, tiles_b_.ntiles(), 2, wdiff, g_.h1h2, state_->red_b, state_,
                 kSkipIfDone | kBumpIter, s);
   after_launch(s);
 }
@@ -228,15 +238,15 @@ void GpuSubdomainSolver::phase_b_kernel_only(hipStream_t s, bool pack) {
   // pcg_b reads G.nb only to pack the send buffers: clearing it skips the packing
   DevGeom G = geom_;
   if (!pack) G.nb = 0;
-  if (tiles_.kind == 1)
+  if (tiles_b_.kind == 1)
     launch_pcg_b_wave<T>(G, tables_, static_cast<T*>(field_base(0)),
                          static_cast<T*>(field_base(1)), static_cast<const T*>(field_base(2)),
-                         static_cast<const T*>(field_base(3)), halo<T>(), partials_, state_, tiles_,
+                         static_cast<const T*>(field_base(3)), halo<T>(), partials_, state_, tiles_b_,
                          opt_.exact, s);
   else
     launch_pcg_b<T>(G, tables_, static_cast<T*>(field_base(0)), static_cast<T*>(field_base(1)),
                     static_cast<const T*>(field_base(2)), static_cast<const T*>(field_base(3)),
-                    halo<T>(), partials_, state_, tiles_, opt_.exact, s);
+                    halo<T>(), partials_, state_, tiles_b_, opt_.exact, s);
 }
 
 void GpuSubdomainSolver::enqueue_init(hipStream_t s) {
@@ -276,8 +286,9 @@ double GpuSubdomainSolver::bench_kernel(int which, int abl, int reps, hipStream_
   st.red_b[0] = 1.0;
   st.red_b[1] = 1e-3;
   st.zr[0] = st.zr[1] = 1e-3;
-  const TileCfg saved = tiles_;
+  const TileCfg saved = tiles_, saved_b = tiles_b_;
   tiles_.abl = abl;
+  tiles_b_.abl = abl;
   auto launch = [&]() {
     HIP_CHECK(hipMemcpyAsync(state_, &st, sizeof(PcgState), hipMemcpyHostToDevice, s));
     if (which == 0) {
@@ -310,6 +321,7 @@ double GpuSubdomainSolver::bench_kernel(int which, int abl, int reps, hipStream_
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   tiles_ = saved;
+  tiles_b_ = saved_b;
   return double(total) / reps;
 }
 

@@ -445,7 +445,7 @@ k_pcg_b_wave(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-TileCfg make_wave_tiles(const DevGeom& G, int vec, int waves, int rows) {
+TileCfg make_wave_tiles(const DevGeom& G, int vec, int waves, int rows, int max_auto_rows) {
   PMX_CHECK(vec == 1 || vec == 2 || vec == 4, "vec must be 1, 2 or 4");
   PMX_CHECK(waves >= 1 && waves <= 16, "waves per block must be in [1,16]");
   PMX_CHECK(rows >= 0 && rows <= kMaxWaveRows, "wave tile rows must be in [0, 256] (0 = auto)");
@@ -458,7 +458,7 @@ TileCfg make_wave_tiles(const DevGeom& G, int vec, int waves, int rows) {
   if (rows == 0) {
     constexpr int64_t kTargetWaves = 8192;  // 256 CUs x 32 wave slots
     const int64_t want = (int64_t(G.nx) * t.tiles_j + kTargetWaves - 1) / kTargetWaves;
-    rows = int(std::min<int64_t>(64, std::max<int64_t>(2, want)));
+    rows = int(std::min<int64_t>(max_auto_rows, std::max<int64_t>(2, want)));
   }
   t.rows = rows;
   t.tiles_i = (G.nx + rows - 1) / rows;

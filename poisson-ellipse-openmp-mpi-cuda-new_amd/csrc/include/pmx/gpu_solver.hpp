@@ -39,9 +39,14 @@ struct GpuOptions {
   int device = 0;
   int kernel = 1;         // 0: LDS-ring workgroup tiles, 1: wave tiles with DPP lane shifts
   int block = 256;        // kernel 0: tile width (threads per workgroup)
-  int vec = 2;            // kernel 1: columns per lane (2 x fp64 = 16-B accesses)
+  // Tile shapes.  pcg_a and pcg_b are separate launches, so each gets its own shape; the *_b
+  // fields default to "same as pcg_a" when the pcg_a field is set explicitly.
+  int vec = 0;            // kernel 1, pcg_a: columns per lane (0 = auto: 4 = 32-B fp64 accesses)
   int waves = 4;          // kernel 1: wave tiles per workgroup
   int tile_rows = 0;      // tile height (marching length), 0 = auto-size for occupancy
+  int vec_b = 0;          // pcg_b columns per lane (0 = vec if set, else auto: 2 fp64 / 4 fp32)
+  int waves_b = 0;        // pcg_b wave tiles per workgroup (0 = waves)
+  int tile_rows_b = -1;   // pcg_b tile height (-1 = tile_rows)
   DType dtype = DType::kFp64;
   bool exact = false;     // reference arithmetic order inside the fused kernels
   int graph_batch = 32;   // iterations per captured hipGraph (0 = eager launches)
@@ -97,7 +102,8 @@ class GpuSubdomainSolver {
   const GpuOptions& options() const { return opt_; }
   const DevGeom& geom() const { return geom_; }
   const DevTables& tables() const { return tables_; }
-  const TileCfg& tiles() const { return tiles_; }
+  const TileCfg& tiles() const { return tiles_; }      // pcg_a
+  const TileCfg& tiles_b() const { return tiles_b_; }  // pcg_b
   int device() const { return opt_.device; }
   size_t field_bytes() const { return field_bytes_; }
   void* field_base(int which) const;  // pointer to local (0,0)
@@ -118,7 +124,8 @@ class GpuSubdomainSolver {
   GridInfo g_;
   DevGeom geom_{};
   DevTables tables_{};
-  TileCfg tiles_{};
+  TileCfg tiles_{};    // pcg_a
+  TileCfg tiles_b_{};  // pcg_b
   TileCfg init_tiles_{};
   CommLayout layout_{};
   size_t elem_ = 8, field_bytes_ = 0, field_off_ = 0;

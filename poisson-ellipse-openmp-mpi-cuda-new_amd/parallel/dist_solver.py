@@ -31,9 +31,9 @@ from .launch import DistInfo
 
 class DistGpuPCG:
     def __init__(self, problem, info: DistInfo, comm: str = "native", split: str = "reference",
-                 dtype: str = "fp64", kernel: str = "wave", block: int = 256, vec: int = 2, waves: int = 4,
+                 dtype: str = "fp64", kernel: str = "wave", block: int = 256, vec: int = 0, waves: int = 4,
                  tile_rows: int = 0, exact: bool = False, graph_batch: int = 32, rccl_graph: bool = False,
-                 overlap: bool = True):
+                 overlap: bool = True, vec_b: int = 0, waves_b: int = 0, tile_rows_b: int = -1):
         self.problem = problem
         self.info = info
         self.comm_kind = comm
@@ -53,7 +53,7 @@ class DistGpuPCG:
                                           tile_rows=tile_rows, dtype=dtype, exact=exact,
                                           graph_batch=graph_batch if rccl_graph else 0, uid=uid[0],
                                           ranks=[info.rank], devices=[self.device], rccl_graph=rccl_graph,
-                                          overlap=overlap)
+                                          overlap=overlap, vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b)
             self.sd = self.session.subdomain(0)
         elif comm == "torch":
             lay = self.n.comm_layout(problem.M, problem.N, self.Px, self.Py, info.rank, dtype)
@@ -63,7 +63,8 @@ class DistGpuPCG:
             self.arena_view = self.arena[pad:pad + lay["bytes"]]
             self.solver = self.n.SubdomainSolver(self.spec, self.Px, self.Py, info.rank, device=self.device,
                                                  kernel=kernel, block=block, vec=vec, waves=waves,
-                                                 tile_rows=tile_rows, dtype=dtype, exact=exact, arena=base + pad)
+                                                 tile_rows=tile_rows, dtype=dtype, exact=exact, arena=base + pad,
+                                                 vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b)
             self.sd = self.solver.subdomain()
             tdt = torch.float64 if dtype == "fp64" else torch.float32
             el = lay["elem"]
@@ -76,6 +77,11 @@ class DistGpuPCG:
             self.tcomm = TorchComm() if info.world > 1 else None
         else:
             raise ValueError(f"unknown comm {comm!r}")
+
+    def tile(self) -> dict:
+        if self.comm_kind == "native":
+            return self.session.tile
+        return dict(ntiles=self.solver.ntiles)
 
     # ---- torch-comm path ----
     def _stream(self) -> int:
