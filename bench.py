@@ -34,7 +34,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--M", type=int, default=16384)
     ap.add_argument("--N", type=int, default=16384)
-    ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
+    ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32", "mixed"],
+                    help="mixed = fp32: fp32 storage, fp64 arithmetic and reductions")
     ap.add_argument("--comm", default="native", choices=["native", "torch"])
     ap.add_argument("--split", default="reference", choices=["reference", "auto", "rows", "cols"])
     ap.add_argument("--kernel", default="wave", choices=["wave", "lds"],

@@ -6,7 +6,7 @@
 //
 //   pmx [M N] [--ax 1.0 --by 0.5] [--box -1,1,-0.6,0.6] [--f 1.0] [--delta 1e-6] [--max-iter K]
 //       [--backend cpu|omp|hip] [--threads T] [--ranks P] [--gpus G] [--comm self|local|rccl]
-//       [--split reference|auto|rows|cols] [--dtype fp64|fp32] [--norm weighted|unweighted]
+//       [--split reference|auto|rows|cols] [--dtype fp64|fp32|mixed] [--norm weighted|unweighted]
 //       [--exact] [--graph-batch 32] [--tile-rows 0] [--kernel wave|lds] [--vec 2] [--waves 4]
 //       [--block 256] [--device D] [--vec-b V] [--waves-b W] [--tile-rows-b R]
 //       [--dump sol.txt] [--dump-stride s] [--json] [--banner stage0..stage4]
@@ -42,7 +42,7 @@ struct Cli {
   std::cerr << "usage: pmx [M N] [--ax A] [--by B] [--box a1,b1,a2,b2] [--f F] [--delta D] [--max-iter K]\n"
                "           [--backend cpu|omp|hip] [--threads T] [--ranks P] [--gpus G]\n"
                "           [--comm self|local|rccl] [--split reference|auto|rows|cols]\n"
-               "           [--dtype fp64|fp32] [--norm weighted|unweighted] [--exact]\n"
+               "           [--dtype fp64|fp32|mixed] [--norm weighted|unweighted] [--exact]\n"
                "           [--graph-batch N] [--tile-rows R] [--kernel wave|lds] [--vec V]\n"
                "           [--waves W] [--block B] [--device D] [--vec-b V] [--waves-b W] [--tile-rows-b R]\n"
                "           [--dump FILE] [--dump-stride S] [--json] [--banner stage0..stage4]\n"
@@ -85,7 +85,9 @@ Cli parse(int argc, char** argv) {
     else if (a == "--split") c.split = val();
     else if (a == "--dtype") {
       const std::string v = val();
-      if (v != "fp64" && v != "fp32") usage("--dtype fp64|fp32");
+      // mixed == fp32: fields stored in fp32, every stencil/update evaluated in fp64 registers,
+      // all reductions and PCG scalars in fp64
+      if (v != "fp64" && v != "fp32" && v != "mixed") usage("--dtype fp64|fp32|mixed");
       c.opt.dtype = v == "fp64" ? DType::kFp64 : DType::kFp32;
     } else if (a == "--norm") {
       const std::string v = val();
@@ -201,24 +203,26 @@ int run_hip(Cli& c, double t_prog) {
   RunStats st = sess.solve();
   const double t_after = now();
   if (st.status == Status::kConverged) print_converged(st.iters, s.delta, false);
+  std::vector<double> w;  // gathered before profiling, which restarts the solver
+  if (!c.dump.empty() || c.json) w = sess.gather_local_w();
   RunStats ph;
   if (c.profile > 0) {
     sess.init();
     ph = sess.profile(c.profile);
     const double scale = double(st.iters) / double(c.profile);
+    // the reference's 5 buckets (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:970-979), scaled from the
+    // profiled iterations to the whole solve; copy and precond are 0 by construction here
     std::cout << "   GPU compute time (Ap + D^{-1}r, max over ranks) ~ " << (ph.t_kernel_a + ph.t_kernel_b) * scale << " s\n"
               << "   Host<->Device copy time (max over ranks)        ~ " << 0.0 << " s\n"
               << "   MPI halo exchange time (max over ranks)         ~ " << ph.t_comm * scale << " s\n"
               << "   Preconditioner CPU part time (max over ranks)   ~ " << 0.0 << " s\n"
-              << "   Dot products time (max over ranks)              ~ " << 0.0 << " s\n";
+              << "   Dot products time (max over ranks)              ~ " << ph.t_reduce * scale << " s\n";
   }
   std::cout << "M=" << s.M << ", N=" << s.N << " | Iter=" << st.iters << " | Total Time=" << std::fixed
             << std::setprecision(6) << (t_after - t_prog) << " s\n"
             << "   Init time (program)      ~ " << (t_before - t_prog) + st.init_seconds << " s\n"
             << "   Solver time (MPI+CUDA)   ~ " << st.solve_seconds << " s\n"
             << "   Finalization time        ~ " << 0.0 << " s\n";
-  std::vector<double> w;
-  if (!c.dump.empty() || c.json) w = sess.gather_local_w();
   if (!c.dump.empty()) write_ascii(c.dump, s, w, c.dump_stride, st.iters);
   if (c.json) {
     const ErrorNorms e = error_norms(s, w);
@@ -232,7 +236,9 @@ int run_hip(Cli& c, double t_prog) {
         .kv("l2_error", e.l2).kv("max_error", e.max_err).kv("max_w", e.max_w)
         .kv("device_bytes", sess.device_bytes()).kv("total_seconds", now() - t_prog);
     if (c.profile > 0)
-      j.kv("phase_kernel_a_s", ph.t_kernel_a).kv("phase_kernel_b_s", ph.t_kernel_b).kv("phase_comm_s", ph.t_comm);
+      j.kv("profiled_iters", c.profile).kv("phase_kernel_a_s", ph.t_kernel_a)
+          .kv("phase_kernel_b_s", ph.t_kernel_b).kv("phase_reduce_s", ph.t_reduce)
+          .kv("phase_allreduce_s", ph.t_allreduce).kv("phase_halo_s", ph.t_halo);
     std::cout << j.str() << std::endl;
   }
   return st.nan ? 3 : 0;

@@ -76,6 +76,9 @@ py::dict stats_dict(const RunStats& r) {
   d["t_kernel_a"] = r.t_kernel_a;
   d["t_kernel_b"] = r.t_kernel_b;
   d["t_comm"] = r.t_comm;
+  d["t_reduce"] = r.t_reduce;
+  d["t_allreduce"] = r.t_allreduce;
+  d["t_halo"] = r.t_halo;
   return d;
 }
 
@@ -160,7 +163,8 @@ GpuOptions make_options(int device, const std::string& kernel, int block, int ve
   o.waves = waves;
   o.block = block;
   o.tile_rows = tile_rows;
-  PMX_CHECK(dtype == "fp64" || dtype == "fp32", "dtype must be fp64 or fp32, got " << dtype);
+  PMX_CHECK(dtype == "fp64" || dtype == "fp32" || dtype == "mixed",
+            "dtype must be fp64, fp32 or mixed (= fp32 storage, fp64 arithmetic), got " << dtype);
   o.dtype = dtype == "fp64" ? DType::kFp64 : DType::kFp32;
   o.exact = exact;
   o.graph_batch = graph_batch;
@@ -255,10 +259,10 @@ PYBIND11_MODULE(_pmx, m) {
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   m.def("comm_layout", [](int M, int N, int Px, int Py, int rank, const std::string& dtype) {
     const Subdomain sd = decompose_2d(M, N, ProcGrid{Px, Py}, rank);
-    return layout_dict(GpuSubdomainSolver::comm_layout(sd, dtype == "fp32" ? DType::kFp32 : DType::kFp64));
+    return layout_dict(GpuSubdomainSolver::comm_layout(sd, dtype == "fp64" ? DType::kFp64 : DType::kFp32));
   });
   m.def("max_square_grid", [](double bytes_per_gpu, int gpus, const std::string& dtype, double reserve) {
-    return max_square_grid(bytes_per_gpu, gpus, dtype == "fp32" ? DType::kFp32 : DType::kFp64, reserve);
+    return max_square_grid(bytes_per_gpu, gpus, dtype == "fp64" ? DType::kFp64 : DType::kFp32, reserve);
   }, py::arg("bytes_per_gpu"), py::arg("gpus"), py::arg("dtype") = "fp64", py::arg("reserve") = 0.1);
 
   py::class_<OpContext>(m, "OpContext")

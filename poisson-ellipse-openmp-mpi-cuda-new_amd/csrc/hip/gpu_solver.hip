@@ -205,10 +205,8 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
 
 template <typename T>
 void GpuSubdomainSolver::phase_a_impl(hipStream_t s) {
-  phase_a_kernel_only<T>(s);
-  after_launch(s);
-  launch_reduce(partials_, tiles_.ntiles(), 1, g_.h1h2, 0.0, state_->red_a, state_, kSkipIfDone, s);
-  after_launch(s);
+  enqueue_kernel_a(s);
+  enqueue_reduce_a(s);
 }
 
 template <typename T>
@@ -225,12 +223,8 @@ void GpuSubdomainSolver::phase_a_kernel_only(hipStream_t s) {
 
 template <typename T>
 void GpuSubdomainSolver::phase_b_impl(hipStream_t s, bool pack) {
-  phase_b_kernel_only<T>(s, pack);
-  after_launch(s);
-  const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
-  launch_reduce(partials_, tiles_b_.ntiles(), 2, wdiff, g_.h1h2, state_->red_b, state_,
-                kSkipIfDone | kBumpIter, s);
-  after_launch(s);
+  enqueue_kernel_b(s, pack);
+  enqueue_reduce_b(s);
 }
 
 template <typename T>
@@ -258,6 +252,25 @@ void GpuSubdomainSolver::enqueue_phase_a(hipStream_t s) {
 }
 void GpuSubdomainSolver::enqueue_phase_b(hipStream_t s, bool pack) {
   if (opt_.dtype == DType::kFp64) phase_b_impl<double>(s, pack); else phase_b_impl<float>(s, pack);
+}
+void GpuSubdomainSolver::enqueue_kernel_a(hipStream_t s) {
+  if (opt_.dtype == DType::kFp64) phase_a_kernel_only<double>(s); else phase_a_kernel_only<float>(s);
+  after_launch(s);
+}
+void GpuSubdomainSolver::enqueue_reduce_a(hipStream_t s) {
+  launch_reduce(partials_, tiles_.ntiles(), 1, g_.h1h2, 0.0, state_->red_a, state_, kSkipIfDone, s);
+  after_launch(s);
+}
+void GpuSubdomainSolver::enqueue_kernel_b(hipStream_t s, bool pack) {
+  if (opt_.dtype == DType::kFp64) phase_b_kernel_only<double>(s, pack);
+  else phase_b_kernel_only<float>(s, pack);
+  after_launch(s);
+}
+void GpuSubdomainSolver::enqueue_reduce_b(hipStream_t s) {
+  const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
+  launch_reduce(partials_, tiles_b_.ntiles(), 2, wdiff, g_.h1h2, state_->red_b, state_,
+                kSkipIfDone | kBumpIter, s);
+  after_launch(s);
 }
 
 template <typename T>
@@ -541,37 +554,57 @@ RunStats PcgDriver::solve(int poll_batches) {
 }
 
 RunStats PcgDriver::profile_phases(int64_t n) {
+  // Eager iterations with an event after every step, all on the compute stream(s) (no overlap, so
+  // each step's time is its own).  Events on the first device's stream; on a multi-device
+  // driver the other streams are joined by the collectives.
   RunStats st;
   HIP_CHECK(hipSetDevice(local_[0]->device()));
   hipStream_t s0 = streams_[0];
-  const int kEv = 5;
-  std::vector<hipEvent_t> ev(size_t(n) * kEv);
+  constexpr int kEv = 8;
+  std::vector<hipEvent_t> ev(size_t(n) * kEv + 1);
   for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+  auto each = [&](auto&& f) {
+    for (size_t i = 0; i < local_.size(); ++i) {
+      HIP_CHECK(hipSetDevice(local_[i]->device()));
+      f(local_[i], streams_[i]);
+    }
+    HIP_CHECK(hipSetDevice(local_[0]->device()));
+  };
+  HIP_CHECK(hipEventRecord(ev[0], s0));
   for (int64_t k = 0; k < n; ++k) {
-    hipEvent_t* e = &ev[size_t(k) * kEv];
+    hipEvent_t* e = &ev[size_t(k) * kEv + 1];
+    each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_kernel_a(s); });
     HIP_CHECK(hipEventRecord(e[0], s0));
-    for (size_t i = 0; i < local_.size(); ++i) local_[i]->enqueue_phase_a(streams_[i]);
+    each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_reduce_a(s); });
     HIP_CHECK(hipEventRecord(e[1], s0));
     comm_->allreduce(local_, 0, streams_);
     HIP_CHECK(hipEventRecord(e[2], s0));
-    for (size_t i = 0; i < local_.size(); ++i) local_[i]->enqueue_phase_b(streams_[i]);
+    each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_kernel_b(s, true); });
     HIP_CHECK(hipEventRecord(e[3], s0));
-    comm_->allreduce(local_, 1, streams_);
-    comm_->halo(local_, streams_);
+    each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_reduce_b(s); });
     HIP_CHECK(hipEventRecord(e[4], s0));
+    comm_->allreduce(local_, 1, streams_);
+    HIP_CHECK(hipEventRecord(e[5], s0));
+    comm_->halo(local_, streams_);
+    HIP_CHECK(hipEventRecord(e[6], s0));
+    HIP_CHECK(hipEventRecord(e[7], s0));
   }
   synchronize();
-  auto ms = [](hipEvent_t a, hipEvent_t b) {
+  auto sec = [](hipEvent_t a, hipEvent_t b) {
     float v = 0.f;
     HIP_CHECK(hipEventElapsedTime(&v, a, b));
     return double(v) * 1e-3;
   };
   for (int64_t k = 0; k < n; ++k) {
-    hipEvent_t* e = &ev[size_t(k) * kEv];
-    st.t_kernel_a += ms(e[0], e[1]);
-    st.t_comm += ms(e[1], e[2]) + ms(e[3], e[4]);
-    st.t_kernel_b += ms(e[2], e[3]);
+    hipEvent_t* e = &ev[size_t(k) * kEv + 1];
+    hipEvent_t start = k == 0 ? ev[0] : ev[size_t(k - 1) * kEv + 1 + 7];
+    st.t_kernel_a += sec(start, e[0]);
+    st.t_reduce += sec(e[0], e[1]) + sec(e[3], e[4]);
+    st.t_allreduce += sec(e[1], e[2]) + sec(e[4], e[5]);
+    st.t_kernel_b += sec(e[2], e[3]);
+    st.t_halo += sec(e[5], e[6]);
   }
+  st.t_comm = st.t_allreduce + st.t_halo;
   for (auto& e : ev) (void)hipEventDestroy(e);
   st.launched = n;
   return st;

@@ -75,6 +75,11 @@ class GpuSubdomainSolver {
 
   void enqueue_init(hipStream_t s);     // r=B, w=0, p=0, state reset, red_b <- (0, zr_0)
   void enqueue_phase_a(hipStream_t s);  // k_pcg_a + reduce -> red_a
+  // the two halves of each phase, for per-step timing (PcgDriver::profile_phases)
+  void enqueue_kernel_a(hipStream_t s);
+  void enqueue_reduce_a(hipStream_t s);
+  void enqueue_kernel_b(hipStream_t s, bool pack);
+  void enqueue_reduce_b(hipStream_t s);
   // k_pcg_b + reduce -> red_b, it += 1.  pack=false: the edges were packed by enqueue_pack.
   void enqueue_phase_b(hipStream_t s, bool pack = true);
   void enqueue_pack(hipStream_t s);     // k_edge_r: r^{k+1} edges -> send buffers
@@ -171,9 +176,11 @@ struct RunStats {
   double solve_seconds = 0.0;
   int64_t launched = 0;    // iterations enqueued (>= iters; the rest were device no-ops)
   bool nan = false;
-  // reference-style phase buckets (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980), seconds;
-  // only filled by profile_phases()
-  double t_kernel_a = 0, t_kernel_b = 0, t_reduce = 0, t_comm = 0, t_poll = 0;
+  // per-step times (seconds, summed over the profiled iterations; only profile_phases() fills
+  // them).  Mapped onto the reference's 5 buckets (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980)
+  // by the CLI: compute = kernel_a + kernel_b, comm = allreduce + halo (incl. edge pack),
+  // dot = reduce; copy and precond are 0 by construction (no H2D/D2H in the loop, D^-1 fused).
+  double t_kernel_a = 0, t_kernel_b = 0, t_reduce = 0, t_allreduce = 0, t_halo = 0, t_comm = 0;
 };
 
 class PcgDriver {
