@@ -10,7 +10,8 @@
 //       [--exact] [--graph-batch 32] [--tile-rows 0] [--kernel wave|lds] [--vec 2] [--waves 4]
 //       [--block 256] [--device D] [--vec-b V] [--waves-b W] [--tile-rows-b R]
 //       [--dump sol.txt] [--dump-stride s] [--json] [--banner stage0..stage4]
-//       [--profile-phases N] [--check] [--overlap on|off]
+//       [--profile-phases N] [--check] [--overlap on|off] [--poison-halos]
+//       [--checkpoint FILE [--checkpoint-every K]] [--resume FILE]
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -31,6 +32,8 @@ namespace {
 struct Cli {
   ProblemSpec spec;
   std::string backend = "auto", comm = "auto", banner = "auto", dump, split = "reference";
+  std::string checkpoint, resume;
+  int64_t checkpoint_every = 0;
   int threads = 1, ranks = 1, gpus = 0, dump_stride = 1, device = 0;
   int64_t profile = 0;
   bool json = false;
@@ -46,7 +49,8 @@ struct Cli {
                "           [--graph-batch N] [--tile-rows R] [--kernel wave|lds] [--vec V]\n"
                "           [--waves W] [--block B] [--device D] [--vec-b V] [--waves-b W] [--tile-rows-b R]\n"
                "           [--dump FILE] [--dump-stride S] [--json] [--banner stage0..stage4]\n"
-               "           [--profile-phases N] [--check] [--overlap on|off]\n";
+               "           [--profile-phases N] [--check] [--overlap on|off] [--poison-halos]\n"
+               "           [--checkpoint FILE [--checkpoint-every K]] [--resume FILE]\n";
   std::exit(msg ? 2 : 0);
 }
 
@@ -114,6 +118,10 @@ Cli parse(int argc, char** argv) {
     else if (a == "--banner") c.banner = val();
     else if (a == "--profile-phases") c.profile = std::atoll(val().c_str());
     else if (a == "--check") c.opt.check = true;
+    else if (a == "--poison-halos") c.opt.poison_halos = true;
+    else if (a == "--checkpoint") c.checkpoint = val();
+    else if (a == "--checkpoint-every") c.checkpoint_every = std::atoll(val().c_str());
+    else if (a == "--resume") c.resume = val();
     else if (a == "--overlap") {
       const std::string v = val();
       if (v != "on" && v != "off") usage("--overlap on|off");
@@ -200,7 +208,15 @@ int run_hip(Cli& c, double t_prog) {
   std::cout << "MPI + CUDA 2D run with " << cfg.world << " processes; M=" << s.M << ", N=" << s.N << std::endl;
   const double t_before = now();
   Session sess(cfg);
-  RunStats st = sess.solve();
+  RunStats st;
+  if (!c.resume.empty() || !c.checkpoint.empty()) {
+    // periodic checkpoints go to --checkpoint (default: the --resume file)
+    const std::string out = c.checkpoint.empty() ? c.resume : c.checkpoint;
+    st = sess.solve_checkpointed(out, c.checkpoint_every, c.resume);
+  } else {
+    st = sess.solve();
+  }
+  if (!c.checkpoint.empty()) sess.save_checkpoint(c.checkpoint);  // final state
   const double t_after = now();
   if (st.status == Status::kConverged) print_converged(st.iters, s.delta, false);
   std::vector<double> w;  // gathered before profiling, which restarts the solver

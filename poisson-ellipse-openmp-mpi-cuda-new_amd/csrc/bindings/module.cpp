@@ -154,7 +154,8 @@ class OpContext {
 
 GpuOptions make_options(int device, const std::string& kernel, int block, int vec, int waves,
                         int tile_rows, const std::string& dtype, bool exact, int graph_batch, bool check,
-                        bool overlap = true, int vec_b = 0, int waves_b = 0, int tile_rows_b = -1) {
+                        bool overlap = true, int vec_b = 0, int waves_b = 0, int tile_rows_b = -1,
+                        bool poison_halos = false) {
   GpuOptions o;
   o.device = device;
   PMX_CHECK(kernel == "lds" || kernel == "wave", "kernel must be lds or wave, got " << kernel);
@@ -173,6 +174,7 @@ GpuOptions make_options(int device, const std::string& kernel, int block, int ve
   o.vec_b = vec_b;
   o.waves_b = waves_b;
   o.tile_rows_b = tile_rows_b;
+  o.poison_halos = poison_halos;
   return o;
 }
 
@@ -298,6 +300,7 @@ PYBIND11_MODULE(_pmx, m) {
              g.enqueue_phase_b(as_stream(s), pack);
            }, py::arg("stream"), py::arg("pack") = true)
       .def("enqueue_pack", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_pack(as_stream(s)); })
+      .def("enqueue_poison_recv", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_poison_recv(as_stream(s)); })
       .def("read_state", [](GpuSubdomainSolver& g, uintptr_t s) { return state_dict(g.read_state(as_stream(s))); })
       .def("download_w", [](GpuSubdomainSolver& g, uintptr_t s) {
         return to_numpy(g.download_w(as_stream(s)), {g.sd().nx, g.sd().ny});
@@ -316,11 +319,12 @@ PYBIND11_MODULE(_pmx, m) {
                        int device, const std::string& kernel, int block, int vec, int waves,
                        int tile_rows, const std::string& dtype, bool exact, int graph_batch,
                        bool check, py::object uid, std::vector<int> ranks, std::vector<int> devices,
-                       bool rccl_graph, bool overlap, int vec_b, int waves_b, int tile_rows_b) {
+                       bool rccl_graph, bool overlap, int vec_b, int waves_b, int tile_rows_b,
+                       bool poison_halos) {
              SessionConfig c;
              c.spec = s;
              c.opt = make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact,
-                                  graph_batch, check, overlap, vec_b, waves_b, tile_rows_b);
+                                  graph_batch, check, overlap, vec_b, waves_b, tile_rows_b, poison_halos);
              c.split = split;
              c.world = world;
              if (comm == "self") c.comm = CommKind::kSelf;
@@ -341,7 +345,7 @@ PYBIND11_MODULE(_pmx, m) {
            py::arg("graph_batch") = 32, py::arg("check") = false, py::arg("uid") = py::none(),
            py::arg("ranks") = std::vector<int>{}, py::arg("devices") = std::vector<int>{},
            py::arg("rccl_graph") = false, py::arg("overlap") = true, py::arg("vec_b") = 0,
-           py::arg("waves_b") = 0, py::arg("tile_rows_b") = -1)
+           py::arg("waves_b") = 0, py::arg("tile_rows_b") = -1, py::arg("poison_halos") = false)
       .def("init", [](Session& s) { py::gil_scoped_release g; s.init(); })
       .def("step", [](Session& s, int64_t n) { py::gil_scoped_release g; s.step(n); })
       .def("synchronize", [](Session& s) { py::gil_scoped_release g; s.synchronize(); })
@@ -350,6 +354,21 @@ PYBIND11_MODULE(_pmx, m) {
              { py::gil_scoped_release g; r = s.solve(poll); }
              return stats_dict(r);
            }, py::arg("poll_batches") = 1)
+      .def("solve_checkpointed", [](Session& s, const std::string& path, int64_t every, bool resume,
+                                    int poll) {
+             RunStats r;
+             { py::gil_scoped_release g; r = s.solve_checkpointed(path, every, resume ? path : "", poll); }
+             return stats_dict(r);
+           }, py::arg("path"), py::arg("every") = 0, py::arg("resume") = false,
+           py::arg("poll_batches") = 1)
+      .def("save_checkpoint", [](Session& s, const std::string& path) {
+             py::gil_scoped_release g;
+             s.save_checkpoint(path);
+           })
+      .def("load_checkpoint", [](Session& s, const std::string& path) {
+             py::gil_scoped_release g;
+             s.load_checkpoint(path);
+           })
       .def("profile", [](Session& s, int64_t n) {
              RunStats r;
              { py::gil_scoped_release g; r = s.profile(n); }
@@ -370,6 +389,7 @@ PYBIND11_MODULE(_pmx, m) {
       .def_property_readonly("num_local", &Session::num_local)
       .def_property_readonly("comm_name", &Session::comm_name)
       .def_property_readonly("overlapped", [](Session& s) { return s.overlapped(); })
+      .def_property_readonly("poisoned", [](Session& s) { return s.poisoned(); })
       .def_property_readonly("device_bytes", &Session::device_bytes)
       .def_property_readonly("grid", [](Session& s) { return py::make_tuple(s.grid().Px, s.grid().Py); })
       .def_property_readonly("ntiles", [](Session& s) { return s.solver(0).tiles().ntiles(); })

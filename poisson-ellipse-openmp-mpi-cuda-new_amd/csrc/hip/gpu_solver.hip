@@ -6,10 +6,14 @@
 // Here per iteration: 4 launches (2 streaming + 2 single-block reductions), zero host syncs,
 // replayed from a hipGraph in batches.
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <istream>
+#include <ostream>
 
 #include "pmx/common.hpp"
 #include "pmx/gpu_solver.hpp"
+#include "pmx/trace.hpp"
 
 namespace pmx {
 
@@ -280,6 +284,65 @@ static void pack_impl(const GpuSubdomainSolver& g, HaloBufs<T> H, hipStream_t s)
                    g.state_dev(), g.options().exact, s);
 }
 
+void GpuSubdomainSolver::enqueue_poison_recv(hipStream_t s) {
+  const size_t off = layout_.recv_off[0];
+  HIP_CHECK(hipMemsetAsync(arena_ + off, 0xFF, layout_.bytes - off, s));  // all-ones = NaN
+}
+
+namespace {
+struct CkptHeader {
+  char magic[8];
+  int32_t version, M, N, gi0, gj0, rank, elem, norm;
+  int64_t nx, ny, pitch, field_bytes, arena_bytes, max_iter;
+  double delta;
+};
+constexpr char kCkptMagic[8] = {'P', 'M', 'X', 'C', 'K', 'P', 'T', '1'};
+}  // namespace
+
+void GpuSubdomainSolver::save_checkpoint(std::ostream& os, hipStream_t s) const {
+  HIP_CHECK(hipSetDevice(opt_.device));
+  HIP_CHECK(hipStreamSynchronize(s));
+  CkptHeader h{};
+  std::memcpy(h.magic, kCkptMagic, 8);
+  h.version = 1; h.M = spec_.M; h.N = spec_.N; h.gi0 = sd_.gi0(); h.gj0 = sd_.gj0();
+  h.rank = sd_.rank; h.elem = int32_t(elem_); h.norm = int32_t(spec_.norm);
+  h.nx = sd_.nx; h.ny = sd_.ny; h.pitch = geom_.pitch; h.field_bytes = int64_t(field_bytes_);
+  h.arena_bytes = int64_t(layout_.bytes); h.max_iter = spec_.effective_max_iter(); h.delta = spec_.delta;
+  os.write(reinterpret_cast<const char*>(&h), sizeof(h));
+  std::vector<char> buf(std::max(4 * field_bytes_, layout_.bytes));
+  HIP_CHECK(hipMemcpy(buf.data(), fields_, 4 * field_bytes_, hipMemcpyDeviceToHost));
+  os.write(buf.data(), std::streamsize(4 * field_bytes_));
+  HIP_CHECK(hipMemcpy(buf.data(), arena_, layout_.bytes, hipMemcpyDeviceToHost));
+  os.write(buf.data(), std::streamsize(layout_.bytes));
+  PMX_CHECK(os.good(), "checkpoint write failed");
+}
+
+void GpuSubdomainSolver::load_checkpoint(std::istream& is, hipStream_t s) {
+  HIP_CHECK(hipSetDevice(opt_.device));
+  CkptHeader h{};
+  is.read(reinterpret_cast<char*>(&h), sizeof(h));
+  PMX_CHECK(is.good() && std::memcmp(h.magic, kCkptMagic, 8) == 0 && h.version == 1,
+            "not a pmx checkpoint (v1)");
+  PMX_CHECK(h.M == spec_.M && h.N == spec_.N && h.gi0 == sd_.gi0() && h.gj0 == sd_.gj0() &&
+                h.nx == sd_.nx && h.ny == sd_.ny && h.rank == sd_.rank,
+            "checkpoint is for a different grid/decomposition (M=" << h.M << " N=" << h.N << " rank "
+                                                                  << h.rank << ")");
+  PMX_CHECK(h.elem == int32_t(elem_) && h.pitch == geom_.pitch &&
+                h.field_bytes == int64_t(field_bytes_) && h.arena_bytes == int64_t(layout_.bytes),
+            "checkpoint precision/layout differs from this solver");
+  PMX_CHECK(h.norm == int32_t(spec_.norm) && h.delta == spec_.delta &&
+                h.max_iter == spec_.effective_max_iter(),
+            "checkpoint was written with a different stop rule (norm/delta/max_iter)");
+  std::vector<char> buf(std::max(4 * field_bytes_, layout_.bytes));
+  is.read(buf.data(), std::streamsize(4 * field_bytes_));
+  PMX_CHECK(is.good(), "truncated checkpoint (fields)");
+  HIP_CHECK(hipStreamSynchronize(s));
+  HIP_CHECK(hipMemcpy(fields_, buf.data(), 4 * field_bytes_, hipMemcpyHostToDevice));
+  is.read(buf.data(), std::streamsize(layout_.bytes));
+  PMX_CHECK(is.good(), "truncated checkpoint (scalars/halos)");
+  HIP_CHECK(hipMemcpy(arena_, buf.data(), layout_.bytes, hipMemcpyHostToDevice));
+}
+
 void GpuSubdomainSolver::enqueue_pack(hipStream_t s) {
   if (geom_.nb == 0) return;
   if (opt_.dtype == DType::kFp64) pack_impl<double>(*this, halo<double>(), s);
@@ -384,17 +447,21 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
     HIP_CHECK(hipSetDevice(local_[i]->device()));
     hipStream_t st;
     HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    roctxNameHipStream("pmx:compute", st);
     streams_.push_back(st);
   }
   if (same_device) streams_.resize(local_.size(), streams_[0]);
   bool any_nb = false;
   for (auto* s : local_) any_nb |= s->geom().nb != 0;
   overlap_ = any_nb && local_[0]->options().overlap;
+  const char* env = std::getenv("PMX_POISON_HALOS");
+  poison_ = any_nb && (local_[0]->options().poison_halos || (env && env[0] == '1'));
   if (overlap_) {
     for (size_t i = 0; i < nstreams; ++i) {
       HIP_CHECK(hipSetDevice(local_[i]->device()));
       hipStream_t st;
       HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      roctxNameHipStream("pmx:comm", st);
       comm_streams_.push_back(st);
       hipEvent_t e0, e1;
       HIP_CHECK(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
@@ -431,10 +498,20 @@ void PcgDriver::synchronize() {
 }
 
 void PcgDriver::init() {
+  TraceRange tr("pmx:init");
   for (size_t i = 0; i < local_.size(); ++i) local_[i]->enqueue_init(streams_[i]);
   comm_->allreduce(local_, 1, streams_);
+  poison(streams_);
   comm_->halo(local_, streams_);
   synchronize();
+}
+
+void PcgDriver::poison(std::vector<hipStream_t>& streams) {
+  if (!poison_) return;
+  for (size_t i = 0; i < local_.size(); ++i) {
+    HIP_CHECK(hipSetDevice(local_[i]->device()));
+    local_[i]->enqueue_poison_recv(streams[i]);
+  }
 }
 
 void PcgDriver::enqueue_one_iteration() {
@@ -449,6 +526,7 @@ void PcgDriver::enqueue_one_iteration() {
       local_[i]->enqueue_phase_b(streams_[i]);
     }
     comm_->allreduce(local_, 1, streams_);
+    poison(streams_);
     comm_->halo(local_, streams_);
     return;
   }
@@ -464,6 +542,7 @@ void PcgDriver::enqueue_one_iteration() {
     HIP_CHECK(hipEventRecord(ev_packed_[u], streams_[i]));
     HIP_CHECK(hipStreamWaitEvent(comm_streams_[i], ev_packed_[u], 0));
   });
+  poison(comm_streams_);
   comm_->halo(local_, comm_streams_);
   for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipEventRecord(ev_halo_[u], comm_streams_[i])); });
   for (size_t i = 0; i < local_.size(); ++i) {
@@ -486,6 +565,7 @@ void PcgDriver::for_each_stream(F&& f) {
 }
 
 void PcgDriver::build_graph() {
+  TraceRange tr("pmx:build_graph");
   graph_ok_ = false;
   bool single_stream = true;
   for (auto s : streams_) single_stream &= s == streams_[0];
@@ -515,6 +595,7 @@ void PcgDriver::build_graph() {
 }
 
 void PcgDriver::enqueue_iterations(int64_t n) {
+  TraceRange tr("pmx:enqueue_iterations");
   if (graph_batch_ > 0 && execs_.empty()) build_graph();
   int64_t done = 0;
   if (graph_ok_) {
@@ -525,24 +606,35 @@ void PcgDriver::enqueue_iterations(int64_t n) {
 }
 
 PcgState PcgDriver::state(int idx) {
+  TraceRange tr("pmx:poll_state");
   return local_[idx]->read_state(streams_[idx]);
 }
 
-RunStats PcgDriver::solve(int poll_batches) {
+RunStats PcgDriver::solve(int poll_batches, bool do_init, int64_t ckpt_every,
+                          const std::function<void(const PcgState&)>& on_checkpoint) {
+  TraceRange tr("pmx:solve");
   RunStats st;
   const double t0 = now_s();
-  init();
+  if (do_init) init();
   const double t1 = now_s();
   st.init_seconds = t1 - t0;
   const int64_t batch = std::max(1, graph_batch_ > 0 ? graph_batch_ : 16) * std::max(1, poll_batches);
   const int64_t max_iter = local_[0]->spec().effective_max_iter();
-  PcgState s{};
-  while (true) {
+  PcgState s = state(0);
+  int64_t last_ckpt = s.it;
+  const int64_t budget = max_iter - s.it + 1 + 2 * batch;
+  while (!s.done) {
     enqueue_iterations(batch);
     st.launched += batch;
     s = state(0);
     if (s.done) break;
-    PMX_CHECK(st.launched <= max_iter + 2 * batch, "device stop flag never raised");
+    PMX_CHECK(st.launched <= budget, "device stop flag never raised");
+    if (ckpt_every > 0 && on_checkpoint && s.it - last_ckpt >= ckpt_every) {
+      synchronize();
+      TraceRange trc("pmx:checkpoint");
+      on_checkpoint(s);
+      last_ckpt = s.it;
+    }
   }
   synchronize();
   st.solve_seconds = now_s() - t1;
@@ -554,6 +646,7 @@ RunStats PcgDriver::solve(int poll_batches) {
 }
 
 RunStats PcgDriver::profile_phases(int64_t n) {
+  TraceRange tr("pmx:profile_phases");
   // Eager iterations with an event after every step, all on the compute stream(s) (no overlap, so
   // each step's time is its own).  Events on the first device's stream; on a multi-device
   // driver the other streams are joined by the collectives.

@@ -2,6 +2,8 @@
 #include "pmx/session.hpp"
 
 #include <cmath>
+#include <cstdio>
+#include <fstream>
 
 #include "pmx/common.hpp"
 
@@ -66,6 +68,43 @@ std::vector<double> Session::gather_local_w() {
         g[size_t(sd.gi0() + li) * (N + 1) + sd.gj0() + lj] = w[size_t(li - 1) * sd.ny + lj - 1];
   }
   return g;
+}
+
+std::string Session::checkpoint_file(const std::string& path, int rank) const {
+  return cfg_.world == 1 ? path : path + ".rank" + std::to_string(rank);
+}
+
+void Session::save_checkpoint(const std::string& path) {
+  driver_->synchronize();
+  for (size_t i = 0; i < solvers_.size(); ++i) {
+    const std::string f = checkpoint_file(path, solvers_[i]->sd().rank);
+    const std::string tmp = f + ".tmp";
+    {
+      std::ofstream os(tmp, std::ios::binary | std::ios::trunc);
+      PMX_CHECK(os.good(), "cannot open checkpoint file " << tmp);
+      solvers_[i]->save_checkpoint(os, driver_->streams()[i]);
+    }
+    PMX_CHECK(std::rename(tmp.c_str(), f.c_str()) == 0, "cannot rename " << tmp << " -> " << f);
+  }
+}
+
+void Session::load_checkpoint(const std::string& path) {
+  driver_->synchronize();
+  for (size_t i = 0; i < solvers_.size(); ++i) {
+    const std::string f = checkpoint_file(path, solvers_[i]->sd().rank);
+    std::ifstream is(f, std::ios::binary);
+    PMX_CHECK(is.good(), "cannot open checkpoint file " << f);
+    solvers_[i]->load_checkpoint(is, driver_->streams()[i]);
+  }
+}
+
+RunStats Session::solve_checkpointed(const std::string& save_path, int64_t every,
+                                     const std::string& resume_path, int poll_batches) {
+  const bool resume = !resume_path.empty();
+  if (resume) load_checkpoint(resume_path);
+  std::function<void(const PcgState&)> cb;
+  if (every > 0 && !save_path.empty()) cb = [&](const PcgState&) { save_checkpoint(save_path); };
+  return driver_->solve(poll_batches, !resume, every, cb);
 }
 
 int64_t max_square_grid(double bytes_per_gpu, int gpus, DType dtype, double reserve_fraction) {

@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
+#include <iosfwd>
 #include <memory>
 #include <string>
 #include <vector>
@@ -52,6 +54,10 @@ struct GpuOptions {
   int graph_batch = 32;   // iterations per captured hipGraph (0 = eager launches)
   bool check = false;     // PMX_CHECK mode: synchronise + error-check after every launch
   bool overlap = true;    // halo exchange on a comm stream, overlapped with pcg_b
+  // Debug: fill the ghost receive buffers with NaN before every exchange, so a
+  // ghost value that the exchange failed to deliver poisons the reductions and raises the
+  // device NaN flag.  Also enabled by the environment variable PMX_POISON_HALOS=1.
+  bool poison_halos = false;
 };
 
 struct CommLayout {
@@ -83,6 +89,12 @@ class GpuSubdomainSolver {
   // k_pcg_b + reduce -> red_b, it += 1.  pack=false: the edges were packed by enqueue_pack.
   void enqueue_phase_b(hipStream_t s, bool pack = true);
   void enqueue_pack(hipStream_t s);     // k_edge_r: r^{k+1} edges -> send buffers
+  void enqueue_poison_recv(hipStream_t s);  // recv buffers <- NaN (poison_halos debug mode)
+
+  // Checkpoint: the 4 fields with ghosts, the PCG scalars and the halo buffers,
+  // i.e. everything the next iteration reads.  Synchronous; written at batch boundaries.
+  void save_checkpoint(std::ostream& os, hipStream_t s) const;
+  void load_checkpoint(std::istream& is, hipStream_t s);
 
   PcgState read_state(hipStream_t s) const;  // synchronous D2H of the scalars
   // Kernel isolation benchmark: pins the scalar state to a mid-solve iteration and launches
@@ -191,16 +203,22 @@ class PcgDriver {
   void init();                       // enqueue init on all ranks, all-reduce, halo; sync
   void enqueue_iterations(int64_t n);  // no host sync (graph replays when possible)
   void synchronize();
-  RunStats solve(int poll_batches = 1);  // init + iterate until the device says done
+  // init (or continue from the current device state when do_init is false, e.g. after a
+  // checkpoint load) + iterate until the device says done; on_checkpoint is called every
+  // ckpt_every iterations (at batch granularity) with the device idle
+  RunStats solve(int poll_batches = 1, bool do_init = true, int64_t ckpt_every = 0,
+                 const std::function<void(const PcgState&)>& on_checkpoint = {});
   RunStats profile_phases(int64_t n);    // eager iterations with events around each phase
   PcgState state(int idx = 0);
   std::vector<hipStream_t>& streams() { return streams_; }
   bool overlapped() const { return overlap_; }
+  bool poisoned() const { return poison_; }
 
  private:
   void enqueue_one_iteration();
   void build_graph();
   template <typename F> void for_each_stream(F&& f);
+  void poison(std::vector<hipStream_t>& streams);
 
   std::vector<GpuSubdomainSolver*> local_;
   Comm* comm_;
@@ -208,6 +226,7 @@ class PcgDriver {
   std::vector<hipStream_t> streams_;
   // halo/compute overlap: one comm stream per compute stream, fork/join events per iteration
   bool overlap_ = false;
+  bool poison_ = false;
   std::vector<hipStream_t> comm_streams_;
   std::vector<hipEvent_t> ev_packed_, ev_halo_;
   bool graph_ok_ = false;

@@ -33,6 +33,14 @@ class Session {
   void step(int64_t n) { driver_->enqueue_iterations(n); }
   void synchronize() { driver_->synchronize(); }
   RunStats solve(int poll_batches = 1) { return driver_->solve(poll_batches); }
+  // solve with periodic checkpoints to `save_path` (every `every` iterations; none if empty or
+  // every == 0), optionally continuing from `resume_path` instead of starting from w = 0
+  RunStats solve_checkpointed(const std::string& save_path, int64_t every,
+                              const std::string& resume_path, int poll_batches = 1);
+  // One file per owned subdomain: `path` when world == 1, else `path.rank<r>`.
+  void save_checkpoint(const std::string& path);
+  void load_checkpoint(const std::string& path);
+  std::string checkpoint_file(const std::string& path, int rank) const;
   RunStats profile(int64_t n) { return driver_->profile_phases(n); }
   PcgState state(int i = 0) { return driver_->state(i); }
 
@@ -41,6 +49,7 @@ class Session {
   GpuSubdomainSolver& solver(int i) { return *solvers_.at(size_t(i)); }
   const std::string comm_name() const { return comm_->name(); }
   bool overlapped() const { return driver_->overlapped(); }
+  bool poisoned() const { return driver_->poisoned(); }
   size_t device_bytes() const;
   // global (M+1) x (N+1) solution filled with the subdomains owned by this process
   std::vector<double> gather_local_w();

@@ -79,7 +79,8 @@ def solve_cpu_decomposed(problem: PoissonEllipse, ranks: int = 4, split: str = "
 def make_session(problem: PoissonEllipse, ranks: int = 1, split: str = "reference", device: int = 0,
                  dtype: str = "fp64", kernel: str = "wave", block: int = 256, vec: int = 0, waves: int = 4,
                  tile_rows: int = 0, exact: bool = False, graph_batch: int = 32, check: bool = False,
-                 overlap: bool = True, vec_b: int = 0, waves_b: int = 0, tile_rows_b: int = -1):
+                 overlap: bool = True, vec_b: int = 0, waves_b: int = 0, tile_rows_b: int = -1,
+                 poison_halos: bool = False):
     """Native GPU session with `ranks` subdomains on one device (LocalComm when ranks > 1).
 
     overlap: ghost exchange on a second stream concurrent with pcg_b (only matters for ranks > 1).
@@ -91,7 +92,8 @@ def make_session(problem: PoissonEllipse, ranks: int = 1, split: str = "referenc
     return n.Session(problem.to_native(), world=int(ranks), comm="self" if ranks == 1 else "local",
                      split=getattr(n.Split, split), device=device, kernel=kernel, block=block, vec=vec,
                      waves=waves, tile_rows=tile_rows, dtype=dtype, exact=exact, graph_batch=graph_batch,
-                     check=check, overlap=overlap, vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b)
+                     check=check, overlap=overlap, vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b,
+                     poison_halos=poison_halos)
 
 
 def solve_hip(problem: PoissonEllipse, ranks: int = 1, keep_solution: bool = True, poll_batches: int = 1,

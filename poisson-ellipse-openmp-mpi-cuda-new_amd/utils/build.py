@@ -97,7 +97,8 @@ def build(verbose: bool = False, force: bool = False, jobs: int | None = None, a
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda a: _compile(a[0], a[1], verbose, force), todo))
     core_objs = objs[: len(HIP_SOURCES) + len(CPU_SOURCES)]
-    link_libs = [f"-L{ROCM / 'lib'}", "-lrccl", "-lamdhip64", "-lgomp", f"-Wl,-rpath,{ROCM / 'lib'}"]
+    link_libs = [f"-L{ROCM / 'lib'}", "-lrccl", "-lrocprofiler-sdk-roctx", "-lamdhip64", "-lgomp",
+                 f"-Wl,-rpath,{ROCM / 'lib'}"]
     if force or _stale(EXT_PATH, objs):
         _run([HIPCC, "-shared", "-fPIC", *objs, "-o", EXT_PATH, *link_libs], verbose)
     if apps:
