@@ -130,6 +130,30 @@ def _build_apps(core_objs, link_libs, verbose, force):
             print(f"[pmx build] skipping pmx_mpi: {e}", file=sys.stderr)
 
 
+def build_sanitized(verbose: bool = False, force: bool = False) -> Path:
+    """bin/pmx_asan: the CLI with AddressSanitizer + UBSan on the HOST code.
+
+    The CPU oracle and the CLI are recompiled with -fsanitize=address,undefined; the HIP objects
+    are linked unchanged (their device code is never instrumented: GPU sanitizers are not used on
+    this pool).  Meant for `--backend cpu|omp` runs, e.g. in tests/test_sanitizers.py."""
+    build(verbose=verbose, apps=True)
+    san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"]
+    exe = BIN_DIR / "pmx_asan"
+    srcs = [CSRC / "apps" / "pmx.cpp", CSRC / "cpu" / "cpu_pcg.cpp"]
+    hip_objs = [BUILD_DIR / (s.replace("/", "_") + ".o") for s in HIP_SOURCES]
+    if not (force or _stale(exe, srcs + hip_objs + _headers())):
+        return exe
+    objs = []
+    for src, extra in ((srcs[0], HOST_HIP_FLAGS), (srcs[1], CPU_FLAGS)):
+        obj = BUILD_DIR / ("asan_" + src.name + ".o")
+        _run(["g++", "-O1", "-g", "-std=c++17", f"-I{CSRC / 'include'}", *extra, *san, "-c", src, "-o", obj],
+             verbose)
+        objs.append(obj)
+    _run(["g++", *san, *objs, *hip_objs, "-o", exe, "-fopenmp", f"-L{ROCM / 'lib'}", "-lrccl",
+          "-lrocprofiler-sdk-roctx", "-lamdhip64", f"-Wl,-rpath,{ROCM / 'lib'}"], verbose)
+    return exe
+
+
 def _mpi_flags():
     """(cflags, ldflags) of an MPI installation, using the host g++ (the conda mpicxx wrapper
     points at a cross compiler that is not installed).  The MPI runtime libraries are reached
@@ -164,5 +188,8 @@ if __name__ == "__main__":
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("--no-apps", action="store_true")
+    ap.add_argument("--asan", action="store_true", help="also build bin/pmx_asan (host ASan+UBSan)")
     a = ap.parse_args()
     print(build(verbose=a.verbose, force=a.force, apps=not a.no_apps))
+    if a.asan:
+        print(build_sanitized(verbose=a.verbose, force=a.force))
