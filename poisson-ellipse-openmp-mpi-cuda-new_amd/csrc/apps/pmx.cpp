@@ -12,6 +12,7 @@
 //       [--dump sol.txt] [--dump-stride s] [--json] [--banner stage0..stage4]
 //       [--profile-phases N] [--check] [--overlap on|off] [--poison-halos]
 //       [--checkpoint FILE [--checkpoint-every K]] [--resume FILE]
+//       [--sweep-grids 10x10,20x20,40x40] [--sweep-threads 2,4,8,16]
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -34,6 +35,10 @@ struct Cli {
   std::string backend = "auto", comm = "auto", banner = "auto", dump, split = "reference";
   std::string checkpoint, resume;
   int64_t checkpoint_every = 0;
+  // benchmark sweeps (the reference's hard-coded drivers): grids for any backend,
+  // OpenMP thread counts for cpu/omp (stage0/Withoutopenmp1.cpp:177, stage1-openmp/*:214)
+  std::vector<std::pair<int, int>> sweep_grids;
+  std::vector<int> sweep_threads;
   int threads = 1, ranks = 1, gpus = 0, dump_stride = 1, device = 0;
   int64_t profile = 0;
   bool json = false;
@@ -50,7 +55,8 @@ struct Cli {
                "           [--waves W] [--block B] [--device D] [--vec-b V] [--waves-b W] [--tile-rows-b R]\n"
                "           [--dump FILE] [--dump-stride S] [--json] [--banner stage0..stage4]\n"
                "           [--profile-phases N] [--check] [--overlap on|off] [--poison-halos]\n"
-               "           [--checkpoint FILE [--checkpoint-every K]] [--resume FILE]\n";
+               "           [--checkpoint FILE [--checkpoint-every K]] [--resume FILE]\n"
+               "           [--sweep-grids MxN,MxN,...] [--sweep-threads T,T,...]\n";
   std::exit(msg ? 2 : 0);
 }
 
@@ -119,6 +125,20 @@ Cli parse(int argc, char** argv) {
     else if (a == "--profile-phases") c.profile = std::atoll(val().c_str());
     else if (a == "--check") c.opt.check = true;
     else if (a == "--poison-halos") c.opt.poison_halos = true;
+    else if (a == "--sweep-grids") {
+      std::string v = val() + ",";
+      for (size_t p = 0, q; (q = v.find(',', p)) != std::string::npos; p = q + 1) {
+        const std::string g = v.substr(p, q - p);
+        const size_t x = g.find('x');
+        if (g.empty()) continue;
+        if (x == std::string::npos) usage("--sweep-grids MxN,MxN,...");
+        c.sweep_grids.emplace_back(std::atoi(g.substr(0, x).c_str()), std::atoi(g.substr(x + 1).c_str()));
+      }
+    } else if (a == "--sweep-threads") {
+      std::string v = val() + ",";
+      for (size_t p = 0, q; (q = v.find(',', p)) != std::string::npos; p = q + 1)
+        if (q > p) c.sweep_threads.push_back(std::atoi(v.substr(p, q - p).c_str()));
+    }
     else if (a == "--checkpoint") c.checkpoint = val();
     else if (a == "--checkpoint-every") c.checkpoint_every = std::atoll(val().c_str());
     else if (a == "--resume") c.resume = val();
@@ -154,23 +174,24 @@ double now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-int run_cpu(Cli& c, double t_prog) {
+int run_cpu(Cli& c, double t_prog, bool header = true, bool footer = true) {
   const ProblemSpec& s = c.spec;
   const bool stage0 = c.banner == "stage0";
-  if (c.banner == "stage1")
+  if (c.banner == "stage1" && header)
     std::cout << "--- (Variant 9: Ellipse x^2 + 4y^2 < 1, OpenMP Test) ---\nGrid: M=" << s.M << ", N=" << s.N
               << "\n--------------------------------------------------------\n";
-  if (c.banner == "stage2")
+  if (c.banner == "stage2" && header)
     std::cout << "Pure MPI 2D run with " << c.ranks << " processes; M=" << s.M << ", N=" << s.N << std::endl;
-  if (c.banner == "stage3")
+  if (c.banner == "stage3" && header)
     std::cout << "MPI/OpenMP run with " << c.ranks << " MPI processes; M=" << s.M << ", N=" << s.N << std::endl;
   const int threads = c.backend == "cpu" ? 1 : c.threads;
   SolveResult r = c.ranks > 1 ? cpu_solve_decomposed(s, c.ranks, parse_split(c.split), threads, true)
                               : cpu_solve(s, threads, true);
-  if (r.status == Status::kConverged) print_converged(r.iters, s.delta, stage0);
+  if (r.status == Status::kConverged) print_converged(r.iters, s.delta, stage0 || c.banner == "stage1");
   if (c.banner == "stage1") {
     std::cout << "Threads = " << std::setw(2) << threads << " | Time = " << std::fixed << std::setprecision(3)
-              << r.seconds << " s\n--------------------------------------------------------\n";
+              << r.seconds << " s\n";
+    if (footer) std::cout << "--------------------------------------------------------\n";
   } else {
     std::cout << "M=" << s.M << ", N=" << s.N << " | Iter=" << r.iters << " | Time=" << std::fixed
               << std::setprecision(stage0 ? 4 : 6) << r.seconds << " s\n";
@@ -267,9 +288,27 @@ int main(int argc, char** argv) {
   try {
     Cli c = parse(argc, argv);
     c.spec.validate();
-    if (c.backend == "cpu" || c.backend == "omp") return run_cpu(c, t_prog);
-    if (c.backend == "hip") return run_hip(c, t_prog);
-    usage("unknown --backend");
+    if (c.backend != "cpu" && c.backend != "omp" && c.backend != "hip") usage("unknown --backend");
+    if (c.sweep_grids.empty() && c.sweep_threads.empty()) {
+      return c.backend == "hip" ? run_hip(c, t_prog) : run_cpu(c, t_prog);
+    }
+    // sweep: grids outer, thread counts inner; header/footer once per grid like stage 1
+    if (c.sweep_grids.empty()) c.sweep_grids.emplace_back(c.spec.M, c.spec.N);
+    if (c.sweep_threads.empty()) c.sweep_threads.push_back(c.threads);
+    int rc = 0;
+    for (const auto& g : c.sweep_grids) {
+      for (size_t k = 0; k < c.sweep_threads.size(); ++k) {
+        Cli r = c;
+        r.spec.M = g.first;
+        r.spec.N = g.second;
+        r.spec.validate();
+        r.threads = c.sweep_threads[k];
+        if (r.backend == "cpu" && r.threads > 1) r.backend = "omp";
+        rc |= r.backend == "hip" ? run_hip(r, now())
+                                 : run_cpu(r, now(), k == 0, k + 1 == c.sweep_threads.size());
+      }
+    }
+    return rc;
   } catch (const std::exception& e) {
     std::cerr << e.what() << std::endl;
     return 1;

@@ -2,7 +2,7 @@
 // one-line JSON summaries (components X3, X7 of SURVEY §2.6 and §5.5/§5.6).
 //
 // Reference formats kept byte-compatible:
-//   stage 0 : "Converged after k iterations (||w(k+1)-w(k)|| < δ)."      stage0/Withoutopenmp1.cpp:157-158
+//   stage 0/1: "Converged after k iterations (||w(k+1)-w(k)|| < δ)."     stage0/Withoutopenmp1.cpp:157-158
 //             "M=40, N=40 | Iter=61 | Time=0.0034 s"                     stage0/Withoutopenmp1.cpp:189-192
 //   stage 1 : banner + "Threads =  4 | Time = 0.123 s"                  stage1-openmp/Withopenmp1.cpp:208-224
 //   stage 2 : "Pure MPI 2D run with P processes; M=.., N=.."            stage2-mpi/poisson_mpi_decomp.cpp:476-477
@@ -74,11 +74,16 @@ inline void write_ascii(const std::string& path, const ProblemSpec& s, const std
   f << "# L2_error_in_D=" << e.l2 << " max_error_in_D=" << e.max_err << " max_w=" << e.max_w << '\n';
 }
 
-inline void print_converged(int64_t k, double delta, bool stage0) {
-  if (stage0)
+// symbolic: stages 0/1 print the literal "δ" (stage0/Withoutopenmp1.cpp:157-158,
+// stage1-openmp/Withopenmp1.cpp:192); stages 2-4 print the value with default stream formatting
+inline void print_converged(int64_t k, double delta, bool symbolic) {
+  if (symbolic) {
     std::cout << "Converged after " << k << " iterations (||w(k+1)-w(k)|| < δ)." << std::endl;
-  else
-    std::cout << "Converged after " << k << " iterations (||w(k+1)-w(k)|| < " << delta << ").\n";
+  } else {
+    std::ostringstream d;  // independent of any std::fixed left on std::cout
+    d << delta;
+    std::cout << "Converged after " << k << " iterations (||w(k+1)-w(k)|| < " << d.str() << ").\n";
+  }
 }
 
 struct JsonLine {

@@ -50,6 +50,25 @@ def test_stage1_and_stage3_format(pmx_bin):
     assert out.startswith("MPI/OpenMP run with 2 MPI processes; M=40, N=40")
 
 
+def test_stage1_thread_sweep_format(pmx_bin):
+    """stage1-openmp/Withopenmp2.cpp:204-228: banner once, one line per thread count, footer once."""
+    out = run([pmx_bin, "40", "40", "--backend", "omp", "--sweep-threads", "1,2,4"]).splitlines()
+    dash = "-" * 56
+    assert out[:3] == ["--- (Variant 9: Ellipse x^2 + 4y^2 < 1, OpenMP Test) ---", "Grid: M=40, N=40", dash]
+    conv = "Converged after 50 iterations (||w(k+1)-w(k)|| < δ)."
+    assert out[3::2][:3] == [conv] * 3
+    assert [l[:13] for l in out[4:9:2]] == ["Threads =  1 ", "Threads =  2 ", "Threads =  4 "]
+    assert out[-1] == dash and out.count(dash) == 2
+
+
+def test_stage0_grid_sweep_format(pmx_bin):
+    """stage0/Withoutopenmp1.cpp:176-196: grids 10x10, 20x20, 40x40 (unweighted norm)."""
+    out = run([pmx_bin, "--backend", "cpu", "--norm", "unweighted", "--sweep-grids", "10x10,20x20,40x40"])
+    res = [l for l in out.splitlines() if l.startswith("M=")]
+    assert [l.split(" | ")[:2] for l in res] == [["M=10, N=10", "Iter=17"], ["M=20, N=20", "Iter=31"],
+                                                 ["M=40, N=40", "Iter=61"]]
+
+
 def test_json_and_ascii_dump(pmx_bin, tmp_path, pkg):
     f = tmp_path / "sol.txt"
     out = run([pmx_bin, "120", "90", "--backend", "omp", "--threads", "2", "--json", "--dump", str(f)])
