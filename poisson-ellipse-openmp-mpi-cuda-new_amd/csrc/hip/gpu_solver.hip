@@ -134,7 +134,9 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
 
   init_tiles_ = make_tiles(G, 256, 0);
   const size_t npart = size_t(std::max({tiles_.ntiles(), tiles_b_.ntiles(), init_tiles_.ntiles()}));
-  HIP_CHECK(hipMalloc(&partials_, npart * 2 * sizeof(double)));
+  HIP_CHECK(hipMalloc(&partials_, (npart * 2 + kReduceWsDoubles) * sizeof(double)));
+  reduce_ws_ = partials_ + npart * 2;
+  HIP_CHECK(hipMemset(reduce_ws_, 0, kReduceWsDoubles * sizeof(double)));
 
   layout_ = comm_layout(sd, opt.dtype);
   if (external_arena) {
@@ -162,7 +164,7 @@ GpuSubdomainSolver::~GpuSubdomainSolver() {
 
 size_t GpuSubdomainSolver::device_bytes() const {
   return 4 * field_bytes_ + (4 * (spec_.M + 2) + 4 * (spec_.N + 2)) * sizeof(double) +
-         size_t(std::max({tiles_.ntiles(), tiles_b_.ntiles(), init_tiles_.ntiles()})) * 2 * sizeof(double) +
+         (size_t(std::max({tiles_.ntiles(), tiles_b_.ntiles(), init_tiles_.ntiles()})) * 2 + kReduceWsDoubles) * sizeof(double) +
          (own_arena_ ? layout_.bytes : 0);
 }
 
@@ -203,7 +205,7 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
   T* r = static_cast<T*>(field_base(1));
   launch_init<T>(geom_, tables_, w, r, halo<T>(), partials_, init_tiles_, s);
   after_launch(s);
-  launch_reduce(partials_, init_tiles_.ntiles(), 2, 0.0, g_.h1h2, state_->red_b, state_, 0, s);
+  launch_reduce(partials_, init_tiles_.ntiles(), 2, 0.0, g_.h1h2, state_->red_b, state_, 0, reduce_ws_, s);
   after_launch(s);
 }
 
@@ -262,7 +264,8 @@ void GpuSubdomainSolver::enqueue_kernel_a(hipStream_t s) {
   after_launch(s);
 }
 void GpuSubdomainSolver::enqueue_reduce_a(hipStream_t s) {
-  launch_reduce(partials_, tiles_.ntiles(), 1, g_.h1h2, 0.0, state_->red_a, state_, kSkipIfDone, s);
+  launch_reduce(partials_, tiles_.ntiles(), 1, g_.h1h2, 0.0, state_->red_a, state_, kSkipIfDone,
+                reduce_ws_, s);
   after_launch(s);
 }
 void GpuSubdomainSolver::enqueue_kernel_b(hipStream_t s, bool pack) {
@@ -273,7 +276,7 @@ void GpuSubdomainSolver::enqueue_kernel_b(hipStream_t s, bool pack) {
 void GpuSubdomainSolver::enqueue_reduce_b(hipStream_t s) {
   const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
   launch_reduce(partials_, tiles_b_.ntiles(), 2, wdiff, g_.h1h2, state_->red_b, state_,
-                kSkipIfDone | kBumpIter, s);
+                kSkipIfDone | kBumpIter, reduce_ws_, s);
   after_launch(s);
 }
 

@@ -10,6 +10,7 @@
 // contiguous axis, so every wave64 load/store is one coalesced 512-B (fp64) segment) and
 // marches down the rows.  The i-neighbours of the stencil live in registers, the j-neighbours
 // of the freshly computed p row in a 3-slot LDS ring (one barrier per row).
+#include <algorithm>
 #include <cmath>
 
 #include "pcg_device.hpp"
@@ -334,35 +335,58 @@ k_edge_r(DevGeom G, DevTables Tb, const T* __restrict__ r, const T* p0, const T*
 }
 
 // ---------------------------------------------------------------------------
-// deterministic single-block finish of block partials
+// Deterministic multi-block finish of the block partials.  Block c sums the fixed chunk
+// [c*n/nb, (c+1)*n/nb) and stores it; the last block to finish (atomic ticket) adds the nb chunk
+// sums in chunk order on the matrix cores.  Same bits on every run and every nb-invariant
+// launch; ~64 CUs stream the partials instead of one (the pcg_b partials of a 16384^2 tile
+// grid are 1.4 MB: 26 us on a single workgroup).
 // ---------------------------------------------------------------------------
 template <int NQ>
-__global__ void __launch_bounds__(1024)
+__global__ void __launch_bounds__(256)
 k_reduce(const double* __restrict__ part, int n, double w0, double w1, double* out, PcgState* S,
-         int mode) {
-  __shared__ double lds[2 * 1024 / kWave];
+         int mode, double* chunk, unsigned* ticket) {
+  __shared__ double lds[2 * 256 / kWave];
+  __shared__ int last;
   if ((mode & kSkipIfDone) && S->done) return;
+  const int nb = int(gridDim.x);
+  const int lo = int(int64_t(n) * blockIdx.x / nb);
+  const int hi = int(int64_t(n) * (blockIdx.x + 1) / nb);
   double s0[4] = {0, 0, 0, 0}, s1[4] = {0, 0, 0, 0};
-  int i = threadIdx.x;
-  for (; i + 3 * 1024 < n; i += 4 * 1024) {
+  int i = lo + int(threadIdx.x);
+  for (; i + 3 * 256 < hi; i += 4 * 256) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      s0[u] += part[int64_t(i + u * 1024) * NQ];
-      if (NQ == 2) s1[u] += part[int64_t(i + u * 1024) * NQ + 1];
+      s0[u] += part[int64_t(i + u * 256) * NQ];
+      if (NQ == 2) s1[u] += part[int64_t(i + u * 256) * NQ + 1];
     }
   }
-  for (; i < n; i += 1024) {
+  for (; i < hi; i += 256) {
     s0[0] += part[int64_t(i) * NQ];
     if (NQ == 2) s1[0] += part[int64_t(i) * NQ + 1];
   }
   double a = (s0[0] + s0[1]) + (s0[2] + s0[3]);
   double b = (s1[0] + s1[1]) + (s1[2] + s1[3]);
-  block_sum2<1024>(a, b, lds);
+  block_sum2<256>(a, b, lds);
   if (threadIdx.x == 0) {
-    out[0] = a * w0;
-    if (NQ == 2) out[1] = b * w1;
-    if (!(a == a) || !(b == b) || isinf(a) || isinf(b)) S->nan_flag = 1;
+    chunk[2 * blockIdx.x] = a;
+    chunk[2 * blockIdx.x + 1] = b;
+    __threadfence();
+    last = atomicAdd(ticket, 1u) == unsigned(nb - 1);
+  }
+  __syncthreads();
+  if (!last || threadIdx.x >= kWave) return;  // wave 0 of the last block finishes (full EXEC)
+  __threadfence();
+  const volatile double* c = chunk;
+  const int l = int(threadIdx.x);
+  double ta = l < nb ? c[2 * l] : 0.0;
+  double tb = l < nb ? c[2 * l + 1] : 0.0;
+  wave_sum2_mfma(ta, tb);
+  if (l == 0) {
+    out[0] = ta * w0;
+    if (NQ == 2) out[1] = tb * w1;
+    if (!(ta == ta) || !(tb == tb) || isinf(ta) || isinf(tb)) S->nan_flag = 1;
     if (mode & kBumpIter) S->it += 1;
+    *ticket = 0u;  // re-arm for the next launch (stream order makes this visible to it)
   }
 }
 
@@ -437,10 +461,15 @@ void launch_edge_r(const DevGeom& G, const DevTables& Tb, const T* r, const T* p
 }
 
 void launch_reduce(const double* partials, int n, int nq, double w0, double w1, double* out,
-                   PcgState* S, int mode, hipStream_t s) {
+                   PcgState* S, int mode, double* ws, hipStream_t s) {
   PMX_CHECK(nq == 1 || nq == 2, "nq must be 1 or 2");
-  if (nq == 1) hipLaunchKernelGGL(k_reduce<1>, dim3(1), dim3(1024), 0, s, partials, n, w0, w1, out, S, mode);
-  else hipLaunchKernelGGL(k_reduce<2>, dim3(1), dim3(1024), 0, s, partials, n, w0, w1, out, S, mode);
+  const int nb = std::max(1, std::min(kReduceMaxBlocks, n / 2048));
+  double* chunk = ws;
+  unsigned* ticket = reinterpret_cast<unsigned*>(ws + 2 * kReduceMaxBlocks);
+  if (nq == 1)
+    hipLaunchKernelGGL(k_reduce<1>, dim3(nb), dim3(256), 0, s, partials, n, w0, w1, out, S, mode, chunk, ticket);
+  else
+    hipLaunchKernelGGL(k_reduce<2>, dim3(nb), dim3(256), 0, s, partials, n, w0, w1, out, S, mode, chunk, ticket);
   HIP_CHECK(hipGetLastError());
 }
 

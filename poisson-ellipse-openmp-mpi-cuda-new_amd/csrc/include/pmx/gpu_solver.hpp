@@ -149,6 +149,7 @@ class GpuSubdomainSolver {
   char* fields_ = nullptr;  // 4 fields
   double* tables_buf_ = nullptr;
   double* partials_ = nullptr;
+  double* reduce_ws_ = nullptr;  // k_reduce chunk sums + ticket (inside the partials allocation)
   char* arena_ = nullptr;
   bool own_arena_ = true;
   PcgState* state_ = nullptr;

@@ -72,8 +72,14 @@ template <typename T>
 void launch_edge_r(const DevGeom& G, const DevTables& Tb, const T* r, const T* p0, const T* p1,
                    HaloBufs<T> H, const PcgState* S, bool exact, hipStream_t s);
 
+// Deterministic reduction of n block partials (nq interleaved values each) into out[0..nq),
+// scaled by w0/w1.  `ws` is a per-solver workspace of kReduceWsDoubles doubles whose ticket
+// word starts zeroed; the kernel re-arms it.  One workspace per stream (launches on a workspace
+// must be stream-ordered).
+constexpr int kReduceMaxBlocks = 64;
+constexpr int kReduceWsDoubles = 2 * kReduceMaxBlocks + 2;
 void launch_reduce(const double* partials, int n, int nq, double w0, double w1, double* out,
-                   PcgState* S, int mode, hipStream_t s);
+                   PcgState* S, int mode, double* ws, hipStream_t s);
 
 // Deterministic in-process "all-reduce" across P subdomains on one device (LocalComm):
 // out_k[q] = sum_r in_r[q] for every k, summed in rank order.
