@@ -32,6 +32,15 @@ constexpr int kMaxWaveRows = 256;
 constexpr int kWaveShl1 = 0x130;
 constexpr int kWaveShr1 = 0x138;
 template <int CTRL>
+__device__ __forceinline__ float dpp_shift(float v, float edge) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(edge), __float_as_int(v), CTRL, 0xf,
+                                                    0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_shift_f64(double v, double edge);
+template <int CTRL>
+__device__ __forceinline__ double dpp_shift(double v, double edge) { return dpp_shift_f64<CTRL>(v, edge); }
+template <int CTRL>
 __device__ __forceinline__ double dpp_shift_f64(double v, double edge) {
   const long long b = __double_as_longlong(v);
   const long long e = __double_as_longlong(edge);
@@ -47,6 +56,17 @@ template <> struct VecT<double, 4> { using type = double4; };
 template <> struct VecT<float, 1> { using type = float; };
 template <> struct VecT<float, 2> { using type = float2; };
 template <> struct VecT<float, 4> { using type = float4; };
+
+// Loads keep the storage type: prefetch rings hold raw T (half the VGPRs in fp32 storage mode)
+// and values are widened to fp64 where they are used.
+template <typename T, int VEC>
+__device__ __forceinline__ void vload_raw(const T* p, T (&out)[VEC]) {
+  using V = typename VecT<T, VEC>::type;
+  const V v = *reinterpret_cast<const V*>(p);
+  const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+  for (int u = 0; u < VEC; ++u) out[u] = e[u];
+}
 
 template <typename T, int VEC>
 __device__ __forceinline__ void vload(const T* p, double (&out)[VEC]) {
@@ -134,8 +154,8 @@ __device__ __forceinline__ bool prologue_a(PcgState* S, long long& k, bool& firs
 // ---------------------------------------------------------------------------
 template <typename T, int VEC>
 struct RowA {
-  double rv[VEC], po[VEC];  // r and p^{k-1} of the lane's columns
-  double hrv, hpo;          // the same for this lane's halo column
+  T rv[VEC], po[VEC];  // r and p^{k-1} of the lane's columns (storage precision)
+  T hrv, hpo;          // the same for this lane's halo column
 };
 
 template <typename T, int VEC, int WAVES, bool EXACT>
@@ -181,14 +201,14 @@ k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, Hal
     const T* rrow = (ic == 0) ? (H.recv[0] - 1) : (ic == G.nx + 1) ? (H.recv[1] - 1) : (r + int64_t(ic) * P);
     if (!(G.nb & kNbXlo) && ic == 0) rrow = r + P;           // Dirichlet ghost row: any valid row
     if (!(G.nb & kNbXhi) && ic == G.nx + 1) rrow = r + P;
-    vload<T, VEC>(rrow + jlc, b.rv);
-    vload<T, VEC>(pold + int64_t(ic) * P + jlc, b.po);
+    vload_raw<T, VEC>(rrow + jlc, b.rv);
+    vload_raw<T, VEC>(pold + int64_t(ic) * P + jlc, b.po);
     const int ih = min(max(ic, 1), G.nx);
     const T* hp = (jh == 0 && (G.nb & kNbYlo)) ? (H.recv[2] + ih - 1)
                 : (jh == G.ny + 1 && (G.nb & kNbYhi)) ? (H.recv[3] + ih - 1)
                 : (r + int64_t(ih) * P + min(max(jh, 1), G.ny));
-    b.hrv = double(*hp);
-    b.hpo = double(pold[int64_t(ih) * P + min(max(jh, 0), G.ny + 1)]);
+    b.hrv = *hp;
+    b.hpo = pold[int64_t(ih) * P + min(max(jh, 0), G.ny + 1)];
   };
 
   double pm2[VEC], pm1[VEC], qa0[VEC], qa1[VEC], qb0[VEC], qb1[VEC];
@@ -216,8 +236,8 @@ k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, Hal
         ha0 = face_a0c(ch, rc, G); ha1 = face_a1c(ch, rc, G);
         hb0 = face_b0c(ch, rc, G); hb1 = face_b1c(ch, rc, G);
       }
-      const double z = zdiv_u<EXACT>(ucls, cur.hrv, ha0, ha1, hb0, hb1, G);
-      hv = first ? z : z + beta * cur.hpo;
+      const double z = zdiv_u<EXACT>(ucls, double(cur.hrv), ha0, ha1, hb0, hb1, G);
+      hv = first ? z : z + beta * double(cur.hpo);
       if (h_dir) hv = 0.0;
       if (h_store && !h_dir) pnew[int64_t(i) * P + jh] = static_cast<T>(hv);
       hv = double(static_cast<T>(hv));
@@ -240,8 +260,8 @@ k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, Hal
       }
       double v = 0.0;
       if (valid[u] && live_row) {
-        const double z = zdiv_u<EXACT>(ucls, cur.rv[u], a0[u], a1[u], b0[u], b1[u], G);
-        v = first ? z : z + beta * cur.po[u];
+        const double z = zdiv_u<EXACT>(ucls, double(cur.rv[u]), a0[u], a1[u], b0[u], b1[u], G);
+        v = first ? z : z + beta * double(cur.po[u]);
       }
       st[u] = static_cast<T>(v);
       v = double(st[u]);
@@ -337,15 +357,15 @@ k_pcg_b_wave(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
   const int jr = t.jend + 1;
   const bool edges = !(abl & (kAblHalo | kAblHaloLoads));
 
-  double pr[4][VEC];        // p rows ring
-  double wr[2][VEC], rr[2][VEC];
-  double er[2][2];          // [slot][left/right edge]
-  auto load_p = [&](int i, double (&out)[VEC]) { vload<T, VEC>(pn + int64_t(i) * P + jlp, out); };
-  auto load_wr = [&](int i, double (&wo)[VEC], double (&ro)[VEC], double (&e)[2]) {
-    vload<T, VEC>(w + int64_t(i) * P + jlw, wo);
-    vload<T, VEC>(r + int64_t(i) * P + jlw, ro);
-    e[0] = double(pn[int64_t(i) * P + t.j0 - 1]);
-    e[1] = double(pn[int64_t(i) * P + jr]);
+  T pr[4][VEC];             // p rows ring (storage precision)
+  T wr[2][VEC], rr[2][VEC];
+  T er[2][2];               // [slot][left/right edge]
+  auto load_p = [&](int i, T (&out)[VEC]) { vload_raw<T, VEC>(pn + int64_t(i) * P + jlp, out); };
+  auto load_wr = [&](int i, T (&wo)[VEC], T (&ro)[VEC], T (&e)[2]) {
+    vload_raw<T, VEC>(w + int64_t(i) * P + jlw, wo);
+    vload_raw<T, VEC>(r + int64_t(i) * P + jlw, ro);
+    e[0] = pn[int64_t(i) * P + t.j0 - 1];
+    e[1] = pn[int64_t(i) * P + jr];
   };
   load_p(t.i0 - 1, pr[3]);
   load_p(t.i0, pr[0]);
@@ -368,13 +388,13 @@ k_pcg_b_wave(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
     const RowConst rc_n = load_row(Tb, G.gi0 + (more ? i + 1 : i));
     const int ucls = (EXACT || (abl & kAblCoef)) ? 0 : row_class(rc, G.gj0 + t.j0, G.gj0 + t.jend);
     const double uval = ucls == 1 ? 1.0 : G.inv_eps;
-    const double left = dpp_shift_f64<kWaveShr1>(pr[S0][VEC - 1], edges ? er[WC][0] : 0.0);
-    const double right = dpp_shift_f64<kWaveShl1>(pr[S0][0], edges ? er[WC][1] : 0.0);
+    const double left = double(dpp_shift<kWaveShr1>(pr[S0][VEC - 1], edges ? er[WC][0] : T(0)));
+    const double right = double(dpp_shift<kWaveShl1>(pr[S0][0], edges ? er[WC][1] : T(0)));
     T ws[VEC], rs[VEC];
 #pragma unroll
     for (int u = 0; u < VEC; ++u) {
-      const double pjm = u == 0 ? left : pr[S0][u - 1];
-      const double pjp = u == VEC - 1 ? right : pr[S0][u + 1];
+      const double pjm = u == 0 ? left : double(pr[S0][u - 1]);
+      const double pjp = u == VEC - 1 ? right : double(pr[S0][u + 1]);
       double a0, a1, b0, b1;
       if (abl & kAblCoef) {
         a0 = a1 = b0 = b1 = 1.0;
@@ -386,9 +406,10 @@ k_pcg_b_wave(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
         b0 = face_b0c(cc[u], rc, G);
         b1 = face_b1c(cc[u], rc, G);
       }
-      const double pc = pr[S0][u];
-      const double Ap = apply_a<EXACT>(pc, pr[SM][u], pr[SP][u], pjm, pjp, a0, a1, b0, b1, G);
-      const double wo = wr[WC][u], ro = rr[WC][u];
+      const double pc = double(pr[S0][u]);
+      const double Ap = apply_a<EXACT>(pc, double(pr[SM][u]), double(pr[SP][u]), pjm, pjp, a0, a1, b0,
+                                       b1, G);
+      const double wo = double(wr[WC][u]), ro = double(rr[WC][u]);
       ws[u] = static_cast<T>(upd_w<EXACT>(wo, alpha, pc));
       rs[u] = static_cast<T>(upd_r<EXACT>(ro, alpha, Ap));
       if (valid[u]) {
