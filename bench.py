@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--no-tol-solve", dest="tol_solve", action="store_false")
     ap.add_argument("--tol-time-cap", type=float, default=300.0, help="seconds allowed for the tol solve")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--cpu-dry-run", action="store_true",
+                    help="test the launch/timing/reporting flow on CPU (gloo, plain-PyTorch PCG); "
+                         "prints a JSON line marked data=cpu-dry-run, not a measurement")
     return ap.parse_args()
 
 
@@ -68,20 +71,32 @@ def main():
     from importlib import import_module
 
     launch = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.parallel.launch")
-    info = launch.init_distributed()
+    dry = args.cpu_dry_run
+    info = launch.init_distributed(device_type="cpu" if dry else None)
     world = info.world
     if world != args.gpus:
         print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
-    if not torch.cuda.is_available():
-        raise SystemExit("bench.py needs an MI355X (no HIP device visible)")
-    torch.cuda.set_device(info.local_rank)
+    if not dry:
+        if not torch.cuda.is_available():
+            raise SystemExit("bench.py needs an MI355X (no HIP device visible)")
+        torch.cuda.set_device(info.local_rank)
+
+    def device_sync():
+        if not dry:
+            torch.cuda.synchronize()
 
     problem = pmx.PoissonEllipse(M=args.M, N=args.N)
     kw = dict(split=args.split, dtype=args.dtype, kernel=args.kernel, block=args.block, vec=args.vec,
               waves=args.waves, tile_rows=args.tile_rows, exact=args.exact, graph_batch=args.graph_batch,
               overlap=args.overlap == "on", vec_b=args.vec_b, tile_rows_b=args.tile_rows_b)
     comm_used = args.comm
-    if world == 1:
+    if dry:
+        tp = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.models.torch_pcg")
+        comm = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.parallel.comm")
+        runner = tp.TorchPCG(problem, comm=comm.TorchComm() if world > 1 else None, split=args.split)
+        runner.tile = lambda: dict(kind="torch-cpu")
+        comm_used = "gloo" if world > 1 else "self"
+    elif world == 1:
         models = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.models")
         sess = models.make_session(problem, ranks=1, device=info.local_rank, **kw)
 
@@ -121,17 +136,17 @@ def main():
     runner.synchronize()
     st0 = runner.state()
     barrier()
-    torch.cuda.synchronize()
+    device_sync()
     t0 = time.perf_counter()
     runner.step(args.steps)
     runner.synchronize()
-    torch.cuda.synchronize()
+    device_sync()
     barrier()
     t1 = time.perf_counter()
     dt = t1 - t0
     st1 = runner.state()
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device="cpu" if dry else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     tile_desc = runner.tile() if hasattr(runner, "tile") else dict(rows=args.tile_rows, vec=args.vec)
@@ -144,7 +159,7 @@ def main():
     if args.tol_solve:
         runner.init()
         barrier()
-        torch.cuda.synchronize()
+        device_sync()
         ts = time.perf_counter()
         launched, batch = 0, max(args.graph_batch, 32)
         max_iter = problem.effective_max_iter()
@@ -179,7 +194,8 @@ def main():
             "scaling": "strong",
             "vs_baseline": round(mlups / BASELINE_MLUPS, 2),
             "dtype": args.dtype,
-            "data": "synthetic (reference problem: F=1 in ellipse x^2+4y^2<1, zero initial guess)",
+            "data": "cpu-dry-run (plain-PyTorch PCG on CPU: flow test, not a measurement)" if dry else
+                    "synthetic (reference problem: F=1 in ellipse x^2+4y^2<1, zero initial guess)",
             "config": {
                 "model": f"fictitious-domain Poisson ellipse, Jacobi-PCG, {args.M}x{args.N}",
                 "global_batch": 1,

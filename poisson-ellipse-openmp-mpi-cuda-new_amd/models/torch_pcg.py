@@ -41,29 +41,41 @@ class TorchPCG:
         t = x.reshape(1).to(torch.float64)
         return float(self.comm.allreduce_(t).item())
 
-    def solve(self, keep_solution: bool = True) -> Result:
+    # ---- stepwise interface (same contract as the native Session: init / step / state) ----
+    def init(self):
+        P = self.p
+        h1, h2 = P.h1, P.h2
+        self.w = torch.zeros(self.B.shape, dtype=self.dtype, device=self.device)
+        self.r = self.B.clone()
+        self.pv = torch.zeros_like(self.w)
+        z = R.precond(self.r, self.a, self.b, h1, h2)
+        self.pv[1:-1, 1:-1] = z
+        self.zr_old = self._allsum(R.dot(z, self.r[1:-1, 1:-1], h1, h2))
+        self.k = 1
+        self.done = False
+        self.status, self.iters, self.diff = "max_iter", 0, float("nan")
+
+    def step(self, n: int = 1):
+        """Run up to n iterations (no-ops once the stop rule fired, like the device flag)."""
         P = self.p
         h1, h2 = P.h1, P.h2
         weighted = P.norm == "weighted"
-        a, b = self.a, self.b
-        shape = self.B.shape
-        w = torch.zeros(shape, dtype=self.dtype, device=self.device)
-        r = self.B.clone()
-        p = torch.zeros_like(w)
-        t0 = time.perf_counter()
-        z = R.precond(r, a, b, h1, h2)
-        p[1:-1, 1:-1] = z
-        zr_old = self._allsum(R.dot(z, r[1:-1, 1:-1], h1, h2))
-        status, iters, diff = "max_iter", 0, float("nan")
-        for k in range(1, P.effective_max_iter() + 1):
-            iters = k
+        a, b, w, r, p = self.a, self.b, self.w, self.r, self.pv
+        for _ in range(n):
+            if self.done:
+                return
+            if self.k > P.effective_max_iter():
+                self.done, self.status = True, "max_iter"
+                return
+            k = self.k
+            self.iters = k
             self._exchange(p)
             Ap = R.apply_A(p, a, b, h1, h2)
             denom = self._allsum(R.dot(Ap, p[1:-1, 1:-1], h1, h2))
             if (abs(denom) < 1e-15) if weighted else (denom < 1e-15):
-                status = "breakdown"
-                break
-            alpha = zr_old / denom
+                self.done, self.status = True, "breakdown"
+                return
+            alpha = self.zr_old / denom
             w_old = w[1:-1, 1:-1].clone()
             w[1:-1, 1:-1] += alpha * p[1:-1, 1:-1]
             r[1:-1, 1:-1] -= alpha * Ap
@@ -71,17 +83,33 @@ class TorchPCG:
             zr_new = self._allsum(R.dot(z, r[1:-1, 1:-1], h1, h2))
             dw = w[1:-1, 1:-1] - w_old
             dsum = self._allsum((dw * dw).sum(dtype=torch.float64))
-            diff = math.sqrt(dsum * h1 * h2) if weighted else math.sqrt(dsum)
-            if diff < P.delta:
-                status = "converged"
-                break
-            beta = zr_new / zr_old
-            zr_old = zr_new
+            self.diff = math.sqrt(dsum * h1 * h2) if weighted else math.sqrt(dsum)
+            self.k = k + 1
+            if self.diff < P.delta:
+                self.done, self.status = True, "converged"
+                return
+            beta = zr_new / self.zr_old
+            self.zr_old = zr_new
             p[1:-1, 1:-1] = z + beta * p[1:-1, 1:-1]
+
+    def state(self) -> dict:
+        return dict(it=self.k, done=self.done, iters=self.iters, status=self.status, diff=self.diff, nan=False)
+
+    def synchronize(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def solve(self, keep_solution: bool = True) -> Result:
+        P = self.p
+        t0 = time.perf_counter()
+        self.init()
+        while not self.done:
+            self.step(64)
         seconds = time.perf_counter() - t0
+        iters, status, diff = self.iters, self.status, self.diff
         wl = None
         if keep_solution:
-            wl = w[1:-1, 1:-1].to(torch.float64).cpu().numpy()
+            wl = self.w[1:-1, 1:-1].to(torch.float64).cpu().numpy()
         res = Result(iters, status, diff, seconds, None, backend="torch", ranks=self.comm.world)
         res.extra["local_w"] = wl
         res.extra["subdomain"] = self.sd
