@@ -11,6 +11,8 @@ incrementally by mtime (any header change rebuilds everything).
 from __future__ import annotations
 
 import concurrent.futures as cf
+import contextlib
+import fcntl
 import os
 import shutil
 import subprocess
@@ -88,8 +90,25 @@ def _compile(src: str, kind: str, verbose: bool, force: bool) -> Path:
     return obj
 
 
+@contextlib.contextmanager
+def _build_lock():
+    """Serialise concurrent builds (pytest-xdist workers, parallel shells) on one lock file."""
+    BUILD_DIR.mkdir(exist_ok=True)
+    with open(BUILD_DIR / ".lock", "w") as fh:
+        fcntl.flock(fh, fcntl.LOCK_EX)
+        try:
+            yield
+        finally:
+            fcntl.flock(fh, fcntl.LOCK_UN)
+
+
 def build(verbose: bool = False, force: bool = False, jobs: int | None = None, apps: bool = True) -> Path:
     """Compile every native source for gfx950 and link the extension (and CLI apps)."""
+    with _build_lock():
+        return _build(verbose, force, jobs, apps)
+
+
+def _build(verbose: bool, force: bool, jobs: int | None, apps: bool) -> Path:
     BUILD_DIR.mkdir(exist_ok=True)
     jobs = jobs or min(8, os.cpu_count() or 4)
     todo = [(s, "hip") for s in HIP_SOURCES] + [(s, "cpu") for s in CPU_SOURCES] + \
@@ -137,6 +156,11 @@ def build_sanitized(verbose: bool = False, force: bool = False) -> Path:
     are linked unchanged (their device code is never instrumented: GPU sanitizers are not used on
     this pool).  Meant for `--backend cpu|omp` runs, e.g. in tests/test_sanitizers.py."""
     build(verbose=verbose, apps=True)
+    with _build_lock():
+        return _build_sanitized(verbose, force)
+
+
+def _build_sanitized(verbose: bool, force: bool) -> Path:
     san = ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"]
     exe = BIN_DIR / "pmx_asan"
     srcs = [CSRC / "apps" / "pmx.cpp", CSRC / "cpu" / "cpu_pcg.cpp"]
