@@ -211,10 +211,18 @@ k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, Hal
     b.hpo = pold[int64_t(ih) * P + min(max(jh, 0), G.ny + 1)];
   };
 
-  double pm2[VEC], pm1[VEC], qa0[VEC], qa1[VEC], qb0[VEC], qb1[VEC];
+  // Row history for A p.  EXACT keeps the reference formula, so it carries rows i-1 and i-2 of
+  // p and row i-1's four coefficients.  The fast path starts A p of row i as soon as p^k of row i
+  // exists (every term except the one with row i+1) and finishes it one row later with
+  // a1(i) = a0(i+1): it carries one partial per column instead of five rows of history, which
+  // keeps the VEC=4 kernel's VGPRs inside one wave's budget.
+  constexpr int NH = EXACT ? VEC : 1;
+  double pm1[VEC], part[VEC], pm2[NH], qa0[NH], qa1[NH], qb0[NH], qb1[NH];
 #pragma unroll
-  for (int u = 0; u < VEC; ++u) { pm2[u] = pm1[u] = qa0[u] = qa1[u] = qb0[u] = qb1[u] = 0.0; }
-  double hl_m1 = 0.0, hr_m1 = 0.0;  // halo values of row i-1
+  for (int u = 0; u < VEC; ++u) pm1[u] = part[u] = 0.0;
+#pragma unroll
+  for (int u = 0; u < NH; ++u) pm2[u] = qa0[u] = qa1[u] = qb0[u] = qb1[u] = 0.0;
+  double hl_m1 = 0.0, hr_m1 = 0.0;  // halo values of row i-1 (EXACT path)
   double acc = 0.0;
   RowA<T, VEC> buf[2];
   fetch(t.i0 - 1, buf[0]);
@@ -280,24 +288,47 @@ k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, Hal
           if (valid[u]) pnew[int64_t(i) * P + jl + u] = st[u];
       }
     }
-    // A p^k for row i-1 (pm1), neighbours: rows i-2 (pm2), i (pc); columns by DPP
-    if (i - 1 >= t.i0 && !(abl & kAblAp)) {
-      const double left = dpp_shift_f64<kWaveShr1>(pm1[VEC - 1], hl_m1);
-      const double right = dpp_shift_f64<kWaveShl1>(pm1[0], hr_m1);
+    if constexpr (EXACT) {
+      // A p^k for row i-1 (pm1), neighbours: rows i-2 (pm2), i (pc); columns by DPP
+      if (i - 1 >= t.i0 && !(abl & kAblAp)) {
+        const double left = dpp_shift_f64<kWaveShr1>(pm1[VEC - 1], hl_m1);
+        const double right = dpp_shift_f64<kWaveShl1>(pm1[0], hr_m1);
 #pragma unroll
-      for (int u = 0; u < VEC; ++u) {
-        const double pjm = u == 0 ? left : pm1[u - 1];
-        const double pjp = u == VEC - 1 ? right : pm1[u + 1];
-        if (valid[u])
-          acc += apply_a<EXACT>(pm1[u], pm2[u], pc[u], pjm, pjp, qa0[u], qa1[u], qb0[u], qb1[u], G) * pm1[u];
+        for (int u = 0; u < VEC; ++u) {
+          const double pjm = u == 0 ? left : pm1[u - 1];
+          const double pjp = u == VEC - 1 ? right : pm1[u + 1];
+          if (valid[u])
+            acc += apply_a<true>(pm1[u], pm2[u], pc[u], pjm, pjp, qa0[u], qa1[u], qb0[u], qb1[u], G) * pm1[u];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < NH; ++u) {
+        pm2[u] = pm1[u];
+        qa0[u] = a0[u]; qa1[u] = a1[u]; qb0[u] = b0[u]; qb1[u] = b1[u];
+      }
+      hl_m1 = hl_i; hr_m1 = hr_i;
+    } else if (!(abl & kAblAp)) {
+      // finish row i-1: + cx a1(i-1) (p(i-1) - p(i)), with a1(i-1) = a0(i)
+      if (i - 1 >= t.i0) {
+#pragma unroll
+        for (int u = 0; u < VEC; ++u)
+          if (valid[u]) acc += __builtin_fma(G.cx * a0[u], pm1[u] - pc[u], part[u]) * pm1[u];
+      }
+      // start row i: every term but the one with row i+1
+      if (own_row) {
+        const double left = dpp_shift_f64<kWaveShr1>(pc[VEC - 1], hl_i);
+        const double right = dpp_shift_f64<kWaveShl1>(pc[0], hr_i);
+#pragma unroll
+        for (int u = 0; u < VEC; ++u) {
+          const double pjm = u == 0 ? left : pc[u - 1];
+          const double pjp = u == VEC - 1 ? right : pc[u + 1];
+          const double y = __builtin_fma(b1[u], pc[u] - pjp, b0[u] * (pc[u] - pjm));
+          part[u] = __builtin_fma(G.cx * a0[u], pc[u] - pm1[u], G.cy * y);
+        }
       }
     }
 #pragma unroll
-    for (int u = 0; u < VEC; ++u) {
-      pm2[u] = pm1[u]; pm1[u] = pc[u];
-      qa0[u] = a0[u]; qa1[u] = a1[u]; qb0[u] = b0[u]; qb1[u] = b1[u];
-    }
-    hl_m1 = hl_i; hr_m1 = hr_i;
+    for (int u = 0; u < VEC; ++u) pm1[u] = pc[u];
     rc = rc_n;
   };
   // unrolled by the ring size: buf[0]/buf[1] are never copied
