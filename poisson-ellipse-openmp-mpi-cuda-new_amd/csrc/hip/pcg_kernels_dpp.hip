@@ -152,6 +152,22 @@ __device__ __forceinline__ bool prologue_a(PcgState* S, long long& k, bool& firs
 //    ring slot is a compile-time index, because copying a register with an outstanding load makes
 //    the wave wait for that load, which serialised the whole march (vmcnt(0) every row).
 // ---------------------------------------------------------------------------
+// Column constants of a wave tile, parked in LDS: the face ends / clip roots of each lane's
+// columns are read only on rows cut by the ellipse, so holding them in VGPRs (9 per column) cost
+// occupancy on every row.  Lane-private slots (no barrier); LDS reads count on lgkmcnt and never
+// wait for the row prefetch (vmcnt).
+template <int VEC>
+struct ColLds {
+  // slots [0, 64*VEC): lane l's columns at l*VEC + u; slot 64*VEC + l: lane l's halo column
+  double ylo[64 * VEC + 64], yhi[64 * VEC + 64], rh0[64 * VEC + 64], rh1[64 * VEC + 64];
+  __device__ void put(int slot, const ColConst& c) {
+    ylo[slot] = c.ylo; yhi[slot] = c.yhi; rh0[slot] = c.rh0; rh1[slot] = c.rh1;
+  }
+  __device__ ColConst get(int slot, int gj) const {
+    return ColConst{ylo[slot], yhi[slot], rh0[slot], rh1[slot], gj};
+  }
+};
+
 template <typename T, int VEC>
 struct RowA {
   T rv[VEC], po[VEC];  // r and p^{k-1} of the lane's columns (storage precision)
@@ -159,10 +175,11 @@ struct RowA {
 };
 
 template <typename T, int VEC, int WAVES, bool EXACT>
-__global__ void __launch_bounds__(64 * WAVES)
+__global__ void __launch_bounds__(64 * WAVES, (VEC == 4 && WAVES == 4 && !EXACT) ? 3 : 1)
 k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, HaloBufs<T> H,
              double* __restrict__ partials, PcgState* S, int TI, int tiles_j, int ntiles, int abl) {
   constexpr int W = 64 * VEC;
+  __shared__ ColLds<VEC> col_lds[WAVES];
   long long k;
   bool first;
   double beta;
@@ -178,12 +195,14 @@ k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, Hal
   // clamp for loads: the largest column start with jl's alignment whose VEC columns stay inside
   // the row (the field pitch is padded by >= VEC columns)
   const int jlc = min(jl, 1 + ((G.ny - 1) / VEC) * VEC);
+  ColLds<VEC>& L = col_lds[threadIdx.x >> 6];
   bool valid[VEC];
-  ColConst cc[VEC];
+  int gjc[VEC];
 #pragma unroll
   for (int u = 0; u < VEC; ++u) {
     valid[u] = jl + u <= t.jend;
-    cc[u] = load_col(Tb, G.gj0 + min(jl + u, t.jend));
+    gjc[u] = G.gj0 + min(jl + u, t.jend);
+    L.put(lane * VEC + u, load_col(Tb, gjc[u]));
   }
   const bool lane_full = valid[VEC - 1];
   // halo column of this lane: j0-1 for even lanes, jend+1 for odd lanes (computed every row by
@@ -191,7 +210,8 @@ k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, Hal
   const int jh = (lane & 1) ? t.jend + 1 : t.j0 - 1;
   const int gjh = G.gj0 + jh;
   const bool h_dir = gjh <= 0 || gjh >= G.N || (abl & (kAblHalo | kAblHaloLoads));
-  const ColConst ch = load_col(Tb, h_dir ? G.gj0 + t.j0 : gjh);
+  const int gjh_c = h_dir ? G.gj0 + t.j0 : gjh;
+  L.put(W + lane, load_col(Tb, gjh_c));
   const bool h_store = lane < 2 && ((jh == 0 && (G.nb & kNbYlo)) || (jh == G.ny + 1 && (G.nb & kNbYhi)));
   const int ilast = t.iend + 1;
 
@@ -241,6 +261,7 @@ k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, Hal
     if (own_row && live_row) {
       double ha0 = uval, ha1 = uval, hb0 = uval, hb1 = uval;
       if (ucls == 0) {
+        const ColConst ch = L.get(W + lane, gjh_c);
         ha0 = face_a0c(ch, rc, G); ha1 = face_a1c(ch, rc, G);
         hb0 = face_b0c(ch, rc, G); hb1 = face_b1c(ch, rc, G);
       }
@@ -261,10 +282,11 @@ k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, Hal
       } else if (ucls != 0) {
         a0[u] = a1[u] = b0[u] = b1[u] = uval;
       } else {
-        a0[u] = face_a0c(cc[u], rc, G);
-        a1[u] = face_a1c(cc[u], rc, G);
-        b0[u] = face_b0c(cc[u], rc, G);
-        b1[u] = face_b1c(cc[u], rc, G);
+        const ColConst c = L.get(lane * VEC + u, gjc[u]);
+        a0[u] = face_a0c(c, rc, G);
+        a1[u] = face_a1c(c, rc, G);
+        b0[u] = face_b0c(c, rc, G);
+        b1[u] = face_b1c(c, rc, G);
       }
       double v = 0.0;
       if (valid[u] && live_row) {
