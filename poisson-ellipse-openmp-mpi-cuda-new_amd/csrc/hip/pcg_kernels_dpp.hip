@@ -158,7 +158,7 @@ __device__ __forceinline__ bool prologue_a(PcgState* S, long long& k, bool& firs
 // wait for the row prefetch (vmcnt).
 template <int VEC>
 struct ColLds {
-  // slots [0, 64*VEC): lane l's columns at l*VEC + u; slot 64*VEC + l: lane l's halo column
+  // slot u*64 + l: lane l's column u (lane-contiguous: conflict-free); 64*VEC + l: lane l's halo column
   double ylo[64 * VEC + 64], yhi[64 * VEC + 64], rh0[64 * VEC + 64], rh1[64 * VEC + 64];
   __device__ void put(int slot, const ColConst& c) {
     ylo[slot] = c.ylo; yhi[slot] = c.yhi; rh0[slot] = c.rh0; rh1[slot] = c.rh1;
@@ -202,7 +202,7 @@ k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, Hal
   for (int u = 0; u < VEC; ++u) {
     valid[u] = jl + u <= t.jend;
     gjc[u] = G.gj0 + min(jl + u, t.jend);
-    L.put(lane * VEC + u, load_col(Tb, gjc[u]));
+    L.put(u * 64 + lane, load_col(Tb, gjc[u]));
   }
   const bool lane_full = valid[VEC - 1];
   // halo column of this lane: j0-1 for even lanes, jend+1 for odd lanes (computed every row by
@@ -282,7 +282,7 @@ k_pcg_a_wave(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, Hal
       } else if (ucls != 0) {
         a0[u] = a1[u] = b0[u] = b1[u] = uval;
       } else {
-        const ColConst c = L.get(lane * VEC + u, gjc[u]);
+        const ColConst c = L.get(u * 64 + lane, gjc[u]);
         a0[u] = face_a0c(c, rc, G);
         a1[u] = face_a1c(c, rc, G);
         b0[u] = face_b0c(c, rc, G);
