@@ -168,10 +168,15 @@ def main():
             runner.step(batch)
             launched += batch
             st = runner.state()
-            if st["done"] or launched > max_iter + batch:
-                break
-            if time.perf_counter() - ts > args.tol_time_cap:
-                capped = True
+            stop = 2 if (st["done"] or launched > max_iter + batch) else 0
+            if not stop and time.perf_counter() - ts > args.tol_time_cap:
+                stop = 1
+            if world > 1:  # one decision for all ranks: a rank that stops alone would hang the rest
+                flag = torch.tensor([stop], dtype=torch.int32, device="cpu" if dry else "cuda")
+                dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+                stop = int(flag.item())
+            if stop:
+                capped = stop == 1
                 break
         runner.synchronize()
         barrier()
