@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU iteration: gpu tests, end-to-end tile sweep, short 1-GPU bench with defaults
+# GPU check: the gpu test-suite, an end-to-end tile sweep (configs in $1) and a short 1-GPU bench
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 mkdir -p gpurun_out
 export PMX_NO_AUTOBUILD=1
