@@ -126,11 +126,11 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
   const int vec_b = opt.vec_b ? opt.vec_b : opt.vec ? opt.vec : (fp64 || opt.waves != 4 ? 2 : 4);
   const int waves_b = opt.waves_b ? opt.waves_b : opt.waves;
   const int rows_b = opt.tile_rows_b >= 0 ? opt.tile_rows_b : opt.tile_rows;
-  // auto tile heights: pcg_a plateaus at 32-48 rows, pcg_b at 16-24 (bench/tile_sweep.py, 16384^2)
+  // auto tile heights (caps and tile-count targets from bench/tile_sweep.py, see make_wave_tiles)
   tiles_ = opt.kernel == 0 ? make_tiles(G, opt.block, opt.tile_rows)
-                           : make_wave_tiles(G, vec_a, opt.waves, opt.tile_rows, 32);
+                           : make_wave_tiles(G, vec_a, opt.waves, opt.tile_rows, 32, 22000);
   tiles_b_ = opt.kernel == 0 ? make_tiles(G, opt.block, rows_b)
-                             : make_wave_tiles(G, vec_b, waves_b, rows_b, 24);
+                             : make_wave_tiles(G, vec_b, waves_b, rows_b, 24, 66000);
 
   init_tiles_ = make_tiles(G, 256, 0);
   const size_t npart = size_t(std::max({tiles_.ntiles(), tiles_b_.ntiles(), init_tiles_.ntiles()}));

@@ -519,7 +519,8 @@ k_pcg_b_wave(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
-TileCfg make_wave_tiles(const DevGeom& G, int vec, int waves, int rows, int max_auto_rows) {
+TileCfg make_wave_tiles(const DevGeom& G, int vec, int waves, int rows, int max_auto_rows,
+                        int target_tiles) {
   PMX_CHECK(vec == 1 || vec == 2 || vec == 4, "vec must be 1, 2 or 4");
   PMX_CHECK(waves >= 1 && waves <= 16, "waves per block must be in [1,16]");
   PMX_CHECK(rows >= 0 && rows <= kMaxWaveRows, "wave tile rows must be in [0, 256] (0 = auto)");
@@ -530,9 +531,15 @@ TileCfg make_wave_tiles(const DevGeom& G, int vec, int waves, int rows, int max_
   t.block = 64 * vec;  // columns per tile
   t.tiles_j = (G.ny + t.block - 1) / t.block;
   if (rows == 0) {
-    constexpr int64_t kTargetWaves = 8192;  // 256 CUs x 32 wave slots
-    const int64_t want = (int64_t(G.nx) * t.tiles_j + kTargetWaves - 1) / kTargetWaves;
-    rows = int(std::min<int64_t>(max_auto_rows, std::max<int64_t>(2, want)));
+    // Auto height (bench/tile_sweep.py at the per-rank shapes of 1/2/4/8 GPUs: 16384^2,
+    // 16384x8192, 8192^2, 8192x4096): about `target_tiles` tiles per launch (pcg_a 22K = ~7
+    // rounds of its 3072 wave slots, pcg_b 66K) balances the halo re-reads of short tiles against
+    // the tail of tall ones; never shorter than 12 rows while that still leaves >= 6K tiles;
+    // small grids go down to 2.
+    const int64_t cells = int64_t(G.nx) * t.tiles_j;  // tile-rows x tile-columns at 1 row/tile
+    const int64_t want = (cells + target_tiles / 2) / target_tiles;
+    const int64_t floor_rows = std::min<int64_t>(12, std::max<int64_t>(2, cells / 6144));
+    rows = int(std::min<int64_t>(max_auto_rows, std::max(want, floor_rows)));
   }
   t.rows = rows;
   t.tiles_i = (G.nx + rows - 1) / rows;

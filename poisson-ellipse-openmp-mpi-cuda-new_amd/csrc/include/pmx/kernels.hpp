@@ -29,8 +29,9 @@ struct TileCfg {
 };
 
 TileCfg make_tiles(const DevGeom& G, int block, int rows);
-// rows = 0: auto, enough tiles to fill the GPU but no taller than max_auto_rows
-TileCfg make_wave_tiles(const DevGeom& G, int vec, int waves, int rows, int max_auto_rows = 64);
+// rows = 0: auto, about target_tiles tiles but no taller than max_auto_rows
+TileCfg make_wave_tiles(const DevGeom& G, int vec, int waves, int rows, int max_auto_rows = 32,
+                        int target_tiles = 22000);
 
 enum ReduceMode : int { kSkipIfDone = 1, kBumpIter = 2 };
 
