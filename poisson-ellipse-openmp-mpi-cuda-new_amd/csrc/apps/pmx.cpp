@@ -12,12 +12,14 @@
 //       [--dump sol.txt] [--dump-stride s] [--json] [--banner stage0..stage4]
 //       [--profile-phases N] [--check] [--overlap on|off] [--poison-halos]
 //       [--checkpoint FILE [--checkpoint-every K]] [--resume FILE]
-//       [--sweep-grids 10x10,20x20,40x40] [--sweep-threads 2,4,8,16]
+//       [--sweep-grids 10x10,20x20,40x40] [--sweep-threads 2,4,8,16] [--plan]
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <iomanip>
 #include <iostream>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -41,7 +43,7 @@ struct Cli {
   std::vector<int> sweep_threads;
   int threads = 1, ranks = 1, gpus = 0, dump_stride = 1, device = 0;
   int64_t profile = 0;
-  bool json = false;
+  bool json = false, plan = false;
   GpuOptions opt;
 };
 
@@ -56,7 +58,7 @@ struct Cli {
                "           [--dump FILE] [--dump-stride S] [--json] [--banner stage0..stage4]\n"
                "           [--profile-phases N] [--check] [--overlap on|off] [--poison-halos]\n"
                "           [--checkpoint FILE [--checkpoint-every K]] [--resume FILE]\n"
-               "           [--sweep-grids MxN,MxN,...] [--sweep-threads T,T,...]\n";
+               "           [--sweep-grids MxN,MxN,...] [--sweep-threads T,T,...] [--plan]\n";
   std::exit(msg ? 2 : 0);
 }
 
@@ -125,6 +127,7 @@ Cli parse(int argc, char** argv) {
     else if (a == "--profile-phases") c.profile = std::atoll(val().c_str());
     else if (a == "--check") c.opt.check = true;
     else if (a == "--poison-halos") c.opt.poison_halos = true;
+    else if (a == "--plan") c.plan = true;
     else if (a == "--sweep-grids") {
       std::string v = val() + ",";
       for (size_t p = 0, q; (q = v.find(',', p)) != std::string::npos; p = q + 1) {
@@ -209,6 +212,45 @@ int run_cpu(Cli& c, double t_prog, bool header = true, bool footer = true) {
   return 0;
 }
 
+// --plan: decomposition and device-memory plan for the requested run, no solve (SURVEY §5.7:
+// subgrids sized against the HBM of each MI355X)
+int run_plan(const Cli& c) {
+  const ProblemSpec& s = c.spec;
+  const int ranks = std::max({1, c.gpus, c.ranks});
+  const ProcGrid pg = make_process_grid(ranks, s.M, s.N, parse_split(c.split));
+  double dev_bytes = 288e9;  // MI355X HBM3E when no device is visible
+  std::string dev_src = "assumed 288 GB (no device visible)";
+  int n = 0;
+  if (hipGetDeviceCount(&n) == hipSuccess && n > 0) {
+    size_t fb = 0, tb = 0;
+    if (hipSetDevice(c.device) == hipSuccess && hipMemGetInfo(&fb, &tb) == hipSuccess) {
+      dev_bytes = double(tb);
+      std::ostringstream o;
+      o << "device " << c.device << ": " << tb / 1e9 << " GB total, " << fb / 1e9 << " GB free";
+      dev_src = o.str();
+    }
+  }
+  (void)hipGetLastError();
+  const int gpus = std::max(1, c.gpus);
+  std::cout << "plan: M=" << s.M << ", N=" << s.N << ", " << ranks << " subdomain(s) as " << pg.Px << " x "
+            << pg.Py << ", dtype " << (c.opt.dtype == DType::kFp64 ? "fp64" : "fp32") << "\n"
+            << "memory: " << dev_src << "\n";
+  size_t worst = 0;
+  for (int r = 0; r < ranks; ++r) {
+    const Subdomain sd = decompose_2d(s.M, s.N, pg, r);
+    const size_t b = GpuSubdomainSolver::estimate_device_bytes(s, sd, c.opt.dtype);
+    worst = std::max(worst, b);
+    std::cout << "  rank " << r << ": " << sd.nx << " x " << sd.ny << " nodes, ~" << b / 1e9 << " GB\n";
+  }
+  // subdomains on one device add up (LocalComm); one per device otherwise
+  const size_t per_device = c.gpus > 1 ? worst : worst * size_t(ranks);
+  std::cout << "per device: ~" << per_device / 1e9 << " GB -> "
+            << (double(per_device) <= dev_bytes ? "fits" : "DOES NOT FIT") << "\n"
+            << "largest square grid on " << gpus << " such device(s): ~"
+            << max_square_grid(dev_bytes, gpus, c.opt.dtype) << "^2\n";
+  return double(per_device) <= dev_bytes ? 0 : 4;
+}
+
 int run_hip(Cli& c, double t_prog) {
   SessionConfig cfg;
   cfg.spec = c.spec;
@@ -289,6 +331,7 @@ int main(int argc, char** argv) {
     Cli c = parse(argc, argv);
     c.spec.validate();
     if (c.backend != "cpu" && c.backend != "omp" && c.backend != "hip") usage("unknown --backend");
+    if (c.plan) return run_plan(c);
     if (c.sweep_grids.empty() && c.sweep_threads.empty()) {
       return c.backend == "hip" ? run_hip(c, t_prog) : run_cpu(c, t_prog);
     }

@@ -13,6 +13,7 @@
 
 #include "pmx/common.hpp"
 #include "pmx/gpu_solver.hpp"
+#include "pmx/session.hpp"
 #include "pmx/trace.hpp"
 
 namespace pmx {
@@ -113,6 +114,17 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
   // interior row starts 256-B aligned (lj = 1)
   field_off_ = align_elems - 1;
   field_bytes_ = round_up((field_off_ + size_t(sd.nx + 2) * G.pitch) * elem_, 256);
+  {  // fail with a sizing message instead of a bare hipErrorOutOfMemory
+    size_t free_b = 0, total_b = 0;
+    HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+    const size_t need = estimate_device_bytes(spec, sd, opt.dtype);
+    PMX_CHECK(need <= free_b,
+              "subdomain " << sd.nx << "x" << sd.ny << " needs " << need / 1e9 << " GB on device "
+                           << opt.device << " but only " << free_b / 1e9 << " of " << total_b / 1e9
+                           << " GB are free; the largest square grid for this precision on one such "
+                              "device is ~"
+                           << max_square_grid(double(total_b), 1, opt.dtype) << "^2 (pmx --plan)");
+  }
   HIP_CHECK(hipMalloc(&fields_, 4 * field_bytes_));
 
   // 1D face tables
@@ -160,6 +172,17 @@ GpuSubdomainSolver::~GpuSubdomainSolver() {
   if (partials_) (void)hipFree(partials_);
   if (own_arena_ && arena_) (void)hipFree(arena_);
   if (host_state_) (void)hipHostFree(host_state_);
+}
+
+size_t GpuSubdomainSolver::estimate_device_bytes(const ProblemSpec& spec, const Subdomain& sd,
+                                                 DType dtype) {
+  const size_t elem = dtype == DType::kFp64 ? 8 : 4, align = 256 / elem;
+  const size_t pitch = round_up(size_t(sd.ny + 2 + 8), align);
+  const size_t field = round_up((align - 1 + size_t(sd.nx + 2) * pitch) * elem, 256);
+  const size_t tables = (4 * size_t(spec.M + 2) + 4 * size_t(spec.N + 2)) * 8 + 8 * size_t(spec.M + 2) * 4;
+  // partials: at most one per 2 rows x 64 columns tile (the smallest auto tile), 2 doubles each
+  const size_t partials = (size_t(sd.nx + 1) / 2 + 1) * (size_t(sd.ny) / 64 + 1) * 16;
+  return 4 * field + tables + partials + comm_layout(sd, dtype).bytes + (1u << 20);
 }
 
 size_t GpuSubdomainSolver::device_bytes() const {

@@ -78,6 +78,9 @@ class GpuSubdomainSolver {
   GpuSubdomainSolver& operator=(const GpuSubdomainSolver&) = delete;
 
   static CommLayout comm_layout(const Subdomain& sd, DType dtype);
+  // Upper bound of the device memory a solver for `sd` allocates (fields, tables, partials,
+  // comm arena).  Checked against hipMemGetInfo before allocating; used by `pmx --plan`.
+  static size_t estimate_device_bytes(const ProblemSpec& spec, const Subdomain& sd, DType dtype);
 
   void enqueue_init(hipStream_t s);     // r=B, w=0, p=0, state reset, red_b <- (0, zr_0)
   void enqueue_phase_a(hipStream_t s);  // k_pcg_a + reduce -> red_a

@@ -69,6 +69,17 @@ def test_stage0_grid_sweep_format(pmx_bin):
                                                  ["M=40, N=40", "Iter=61"]]
 
 
+def test_plan_memory_sizing(pmx_bin):
+    """--plan: decomposition + per-rank device bytes against 288 GB/GPU (no solve, no GPU needed)."""
+    out = run([pmx_bin, "16384", "16384", "--gpus", "8", "--plan"])
+    assert "8 subdomain(s) as 2 x 4" in out and "-> fits" in out
+    ranks = [l for l in out.splitlines() if l.strip().startswith("rank ")]
+    assert len(ranks) == 8 and "8192 x 4096 nodes" in ranks[0]
+    big = subprocess.run([pmx_bin, "200000", "200000", "--plan"], capture_output=True, text=True, timeout=60)
+    if "no device visible" in big.stdout:  # 288 GB assumed: 200000^2 fp64 needs ~1.3 TB
+        assert big.returncode == 4 and "DOES NOT FIT" in big.stdout
+
+
 def test_json_and_ascii_dump(pmx_bin, tmp_path, pkg):
     f = tmp_path / "sol.txt"
     out = run([pmx_bin, "120", "90", "--backend", "omp", "--threads", "2", "--json", "--dump", str(f)])
