@@ -150,6 +150,16 @@ class RcclComm final : public Comm {
   }
 
   bool graph_capturable() const override { return capturable_; }
+  void check_health() override {
+    for (auto* v : {&comms_, &halo_comms_})
+      for (auto c : *v) {
+        ncclResult_t async = ncclSuccess;
+        RCCL_CHECK(ncclCommGetAsyncError(c, &async));
+        if (async != ncclSuccess && async != ncclInProgress)
+          ::pmx::fail(__FILE__, __LINE__,
+                      std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
+      }
+  }
   std::string name() const override { return "rccl"; }
   int world_size() const override { return nranks_; }
 

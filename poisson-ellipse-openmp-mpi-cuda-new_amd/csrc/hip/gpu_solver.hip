@@ -633,6 +633,7 @@ void PcgDriver::enqueue_iterations(int64_t n) {
 
 PcgState PcgDriver::state(int idx) {
   TraceRange tr("pmx:poll_state");
+  comm_->check_health();
   return local_[idx]->read_state(streams_[idx]);
 }
 

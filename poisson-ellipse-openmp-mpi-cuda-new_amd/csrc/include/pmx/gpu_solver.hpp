@@ -171,6 +171,9 @@ class Comm {
   // send[s] of every rank -> recv[opposite side] of its neighbour
   virtual void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>& streams) = 0;
   virtual bool graph_capturable() const { return true; }
+  // Failure detection: called by the driver at every host poll (once per batch);
+  // throws if the communicator reported an asynchronous error (RCCL: ncclCommGetAsyncError).
+  virtual void check_health() {}
   virtual std::string name() const = 0;
   virtual int world_size() const = 0;
 };
