@@ -34,6 +34,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--M", type=int, default=16384)
     ap.add_argument("--N", type=int, default=16384)
+    ap.add_argument("--breakdown-tol", type=float, default=1e-15,
+                    help="CG guard on (Ap,p) (reference: 1e-15; grids beyond ~100000^2 need a smaller value)")
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32", "mixed"],
                     help="mixed = fp32: fp32 storage, fp64 arithmetic and reductions")
     ap.add_argument("--comm", default="native", choices=["native", "torch"])
@@ -85,7 +87,7 @@ def main():
         if not dry:
             torch.cuda.synchronize()
 
-    problem = pmx.PoissonEllipse(M=args.M, N=args.N)
+    problem = pmx.PoissonEllipse(M=args.M, N=args.N, breakdown_tol=args.breakdown_tol)
     kw = dict(split=args.split, dtype=args.dtype, kernel=args.kernel, block=args.block, vec=args.vec,
               waves=args.waves, tile_rows=args.tile_rows, exact=args.exact, graph_batch=args.graph_batch,
               overlap=args.overlap == "on", vec_b=args.vec_b, tile_rows_b=args.tile_rows_b)

@@ -5,6 +5,7 @@
 // (ellipse x^2+4y^2<1, delta=1e-6, max_iter=(M-1)(N-1), weighted norm).  The superset:
 //
 //   pmx [M N] [--ax 1.0 --by 0.5] [--box -1,1,-0.6,0.6] [--f 1.0] [--delta 1e-6] [--max-iter K]
+//       [--breakdown-tol 1e-15]
 //       [--backend cpu|omp|hip] [--threads T] [--ranks P] [--gpus G] [--comm self|local|rccl]
 //       [--split reference|auto|rows|cols] [--dtype fp64|fp32|mixed] [--norm weighted|unweighted]
 //       [--exact] [--graph-batch 32] [--tile-rows 0] [--kernel wave|lds] [--vec 2] [--waves 4]
@@ -50,6 +51,7 @@ struct Cli {
 [[noreturn]] void usage(const char* msg) {
   if (msg) std::cerr << "pmx: " << msg << "\n";
   std::cerr << "usage: pmx [M N] [--ax A] [--by B] [--box a1,b1,a2,b2] [--f F] [--delta D] [--max-iter K]\n"
+               "           [--breakdown-tol T]\n"
                "           [--backend cpu|omp|hip] [--threads T] [--ranks P] [--gpus G]\n"
                "           [--comm self|local|rccl] [--split reference|auto|rows|cols]\n"
                "           [--dtype fp64|fp32|mixed] [--norm weighted|unweighted] [--exact]\n"
@@ -84,6 +86,7 @@ Cli parse(int argc, char** argv) {
     else if (a == "--by") c.spec.by = std::atof(val().c_str());
     else if (a == "--f") c.spec.F = std::atof(val().c_str());
     else if (a == "--delta") c.spec.delta = std::atof(val().c_str());
+    else if (a == "--breakdown-tol") c.spec.breakdown_tol = std::atof(val().c_str());
     else if (a == "--max-iter") c.spec.max_iter = std::atoll(val().c_str());
     else if (a == "--box") {
       const std::string v = val();

@@ -45,6 +45,7 @@ int main(int argc, char** argv) {
       split = v == "auto" ? Split::kAuto : v == "rows" ? Split::kRows : v == "cols" ? Split::kCols : Split::kReference;
     } else if (a == "--delta") spec.delta = std::atof(val().c_str());
     else if (a == "--max-iter") spec.max_iter = std::atoll(val().c_str());
+    else if (a == "--breakdown-tol") spec.breakdown_tol = std::atof(val().c_str());
     else pos.push_back(a);
   }
   if (pos.size() >= 2) {

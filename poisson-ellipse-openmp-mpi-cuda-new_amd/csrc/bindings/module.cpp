@@ -196,6 +196,7 @@ PYBIND11_MODULE(_pmx, m) {
       .def_readwrite("A2", &ProblemSpec::A2).def_readwrite("B2", &ProblemSpec::B2)
       .def_readwrite("ax", &ProblemSpec::ax).def_readwrite("by", &ProblemSpec::by)
       .def_readwrite("F", &ProblemSpec::F).def_readwrite("delta", &ProblemSpec::delta)
+      .def_readwrite("breakdown_tol", &ProblemSpec::breakdown_tol)
       .def_readwrite("max_iter", &ProblemSpec::max_iter).def_readwrite("norm", &ProblemSpec::norm)
       .def("effective_max_iter", &ProblemSpec::effective_max_iter)
       .def("validate", &ProblemSpec::validate);

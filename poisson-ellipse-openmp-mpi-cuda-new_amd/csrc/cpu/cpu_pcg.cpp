@@ -33,7 +33,7 @@ inline double norm_of(double sum_sq, const ProblemSpec& s, const GridInfo& g) {
 
 inline bool breakdown(double denom, const ProblemSpec& s) {
   // stage0/Withoutopenmp1.cpp:128 vs stage2-mpi/poisson_mpi_decomp.cpp:413
-  return s.norm == Norm::kWeighted ? std::fabs(denom) < 1e-15 : denom < 1e-15;
+  return s.norm == Norm::kWeighted ? std::fabs(denom) < s.breakdown_tol : denom < s.breakdown_tol;
 }
 
 }  // namespace

@@ -220,6 +220,7 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
   PcgState& st = host_state_[1];  // template (never rewritten while a copy is in flight)
   std::memset(&st, 0, sizeof(st));
   st.delta = spec_.delta;
+  st.bd_tol = spec_.breakdown_tol;
   st.it = 1;
   st.max_iter = spec_.effective_max_iter();
   st.norm = int(spec_.norm);

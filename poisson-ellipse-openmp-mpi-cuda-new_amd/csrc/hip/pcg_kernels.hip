@@ -228,8 +228,8 @@ k_pcg_b(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, const T* 
   if (S->done) return;
   const long long k = S->it;
   const double denom = S->red_a[0];
-  // breakdown guard: |denom| < 1e-15 (stages 2-4) or denom < 1e-15 (stage 0)
-  const bool bd = S->norm == int(Norm::kWeighted) ? fabs(denom) < 1e-15 : denom < 1e-15;
+  // breakdown guard: |denom| < tol (stages 2-4) or denom < tol (stage 0), tol = 1e-15 by default
+  const bool bd = S->norm == int(Norm::kWeighted) ? fabs(denom) < S->bd_tol : denom < S->bd_tol;
   if (bd || !(denom == denom)) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       S->iters = k;
@@ -309,7 +309,7 @@ k_edge_r(DevGeom G, DevTables Tb, const T* __restrict__ r, const T* p0, const T*
   if (S->done) return;
   const long long k = S->it;
   const double denom = S->red_a[0];
-  const bool bd = S->norm == int(Norm::kWeighted) ? fabs(denom) < 1e-15 : denom < 1e-15;
+  const bool bd = S->norm == int(Norm::kWeighted) ? fabs(denom) < S->bd_tol : denom < S->bd_tol;
   if (bd || !(denom == denom)) return;  // k_pcg_b records the breakdown
   const double alpha = S->zr[(k - 1) & 1] / denom;
   const T* pn = (k & 1) ? p1 : p0;

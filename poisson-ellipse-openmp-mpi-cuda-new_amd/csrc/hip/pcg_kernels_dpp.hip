@@ -377,7 +377,7 @@ k_pcg_b_wave(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
   if (S->done) return;
   const long long k = S->it;
   const double denom = S->red_a[0];
-  const bool bd = S->norm == int(Norm::kWeighted) ? fabs(denom) < 1e-15 : denom < 1e-15;
+  const bool bd = S->norm == int(Norm::kWeighted) ? fabs(denom) < S->bd_tol : denom < S->bd_tol;
   if (bd || !(denom == denom)) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       S->iters = k;

@@ -48,6 +48,7 @@ struct alignas(64) PcgState {
   double zr[2];      // zr_m stored at slot m & 1
   double diff;       // last ||w^{k+1} - w^k||
   double delta;      // tolerance
+  double bd_tol;     // breakdown guard on (A p, p)
   long long it;      // iteration currently executing (1-based)
   long long max_iter;
   long long iters;   // final iteration count (valid when done)

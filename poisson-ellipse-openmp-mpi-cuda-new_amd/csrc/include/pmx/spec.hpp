@@ -15,8 +15,8 @@
 namespace pmx {
 
 // Stop-rule / breakdown-guard semantics of the reference stages.
-//  kWeighted  : sqrt(h1*h2*sum dw^2) < delta, |denom| < 1e-15  (stages 1-4)
-//  kUnweighted: sqrt(sum dw^2) < delta,        denom  < 1e-15  (stage 0)
+//  kWeighted  : sqrt(h1*h2*sum dw^2) < delta, |denom| < breakdown_tol (1e-15)  (stages 1-4)
+//  kUnweighted: sqrt(sum dw^2) < delta,        denom  < breakdown_tol (1e-15)  (stage 0)
 enum class Norm : int { kWeighted = 0, kUnweighted = 1 };
 
 enum class Status : int { kRunning = 0, kConverged = 1, kBreakdown = 2, kMaxIter = 3 };
@@ -40,6 +40,11 @@ struct ProblemSpec {
   double delta = 1e-6;                // stop tolerance (stage0/Withoutopenmp1.cpp:178)
   int64_t max_iter = -1;              // <0 -> (M-1)(N-1) (stage0/Withoutopenmp1.cpp:182)
   Norm norm = Norm::kWeighted;
+  // CG breakdown guard on (A p, p): |denom| < tol (weighted) / denom < tol (unweighted), 1e-15 in
+  // every reference stage (stage0/Withoutopenmp1.cpp:130, stage4-mpi+cuda/...:876).  The value is
+  // absolute and (A p, p) shrinks like h^3 for this problem, so grids beyond ~100000^2 trip it at
+  // the first iteration; lower it (e.g. 0) there.
+  double breakdown_tol = 1e-15;
 
   int64_t effective_max_iter() const {
     return max_iter >= 0 ? max_iter : int64_t(M - 1) * int64_t(N - 1);
@@ -54,6 +59,7 @@ struct ProblemSpec {
     PMX_CHECK(B1 > A1 && B2 > A2, "empty box");
     PMX_CHECK(ax > 0 && by > 0, "ellipse semi-axes must be positive");
     PMX_CHECK(delta > 0, "delta must be positive");
+    PMX_CHECK(breakdown_tol >= 0, "breakdown tolerance must be >= 0");
   }
 };
 

@@ -30,6 +30,7 @@ class PoissonEllipse:
     delta: float = 1e-6      # stage0/Withoutopenmp1.cpp:178
     max_iter: Optional[int] = None   # None -> (M-1)(N-1)  (stage0/Withoutopenmp1.cpp:182)
     norm: str = "weighted"   # "weighted" (stages 1-4) | "unweighted" (stage 0)
+    breakdown_tol: float = 1e-15     # CG guard on (Ap,p) (stage0/Withoutopenmp1.cpp:130); see spec.hpp
 
     def __post_init__(self):
         if self.norm not in ("weighted", "unweighted"):
@@ -63,7 +64,7 @@ class PoissonEllipse:
     def to_native(self):
         n = _native()
         s = n.ProblemSpec()
-        for f in ("M", "N", "A1", "B1", "A2", "B2", "ax", "by", "F", "delta"):
+        for f in ("M", "N", "A1", "B1", "A2", "B2", "ax", "by", "F", "delta", "breakdown_tol"):
             setattr(s, f, getattr(self, f))
         s.max_iter = -1 if self.max_iter is None else int(self.max_iter)
         s.norm = n.Norm.weighted if self.norm == "weighted" else n.Norm.unweighted

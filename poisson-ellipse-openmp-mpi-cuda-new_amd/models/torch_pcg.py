@@ -72,7 +72,8 @@ class TorchPCG:
             self._exchange(p)
             Ap = R.apply_A(p, a, b, h1, h2)
             denom = self._allsum(R.dot(Ap, p[1:-1, 1:-1], h1, h2))
-            if (abs(denom) < 1e-15) if weighted else (denom < 1e-15):
+            tol = P.breakdown_tol
+            if (abs(denom) < tol) if weighted else (denom < tol):
                 self.done, self.status = True, "breakdown"
                 return
             alpha = self.zr_old / denom

@@ -74,3 +74,11 @@ def test_max_iter_and_breakdown_status(pkg):
     p = pkg.PoissonEllipse(M=40, N=40, max_iter=7)
     r = pkg.solve(p, "cpu")
     assert r.iters == 7 and r.status == "max_iter"
+
+
+def test_breakdown_tolerance_parameter(pkg):
+    """The (Ap,p) guard is the reference's absolute 1e-15 by default and configurable."""
+    p = pkg.PoissonEllipse(M=40, N=40, breakdown_tol=1e3)
+    r = pkg.solve(p, "cpu")
+    assert r.status == "breakdown" and r.iters == 1
+    assert pkg.solve(pkg.PoissonEllipse(M=40, N=40, breakdown_tol=0.0), "cpu").iters == 50

@@ -193,3 +193,10 @@ def test_bench_session_steps(pkg):
     s.synchronize()
     st1 = s.state()
     assert not st1["done"] and st1["it"] - st0["it"] == 70
+
+
+@pytest.mark.parametrize("kernel", ["wave", "lds"])
+def test_breakdown_tolerance_parameter_gpu(pkg, kernel):
+    r = pkg.solve(pkg.PoissonEllipse(M=40, N=40, breakdown_tol=1e3), "hip", kernel=kernel)
+    assert r.status == "breakdown" and r.iters == 1
+    assert pkg.solve(pkg.PoissonEllipse(M=40, N=40, breakdown_tol=0.0), "hip", kernel=kernel).iters == 50
