@@ -138,6 +138,11 @@ def _build_apps(core_objs, link_libs, verbose, force):
         app_obj = BUILD_DIR / "apps_pmx.o"
         _run(["g++", *COMMON_FLAGS, *HOST_HIP_FLAGS, "-c", app_src, "-o", app_obj], verbose)
         _run([HIPCC, app_obj, lib, "-o", exe, *link_libs], verbose)
+    unit_src = CSRC / "tests" / "unit_tests.cpp"
+    exe_unit = BIN_DIR / "pmx_unit_tests"
+    if unit_src.exists() and (force or _stale(exe_unit, [unit_src, CSRC / "cpu" / "cpu_pcg.cpp"] + _headers())):
+        _run(["g++", "-O2", "-std=c++17", "-fopenmp", "-ffp-contract=off", "-Wall", f"-I{CSRC / 'include'}",
+              unit_src, CSRC / "cpu" / "cpu_pcg.cpp", "-o", exe_unit], verbose)
     mpi_src = CSRC / "apps" / "pmx_mpi.cpp"
     exe_mpi = BIN_DIR / "pmx_mpi"
     mpi = _mpi_flags()
