@@ -45,7 +45,9 @@ def parse():
     ap.add_argument("--block", type=int, default=256, help="lds kernels: tile width")
     ap.add_argument("--vec", type=int, default=0, help="wave kernels: columns per lane (0 = per-kernel best)")
     ap.add_argument("--vec-b", type=int, default=0, help="pcg_b columns per lane (0 = follow --vec / auto)")
-    ap.add_argument("--tile-rows-b", type=int, default=-1, help="pcg_b tile height (-1 = --tile-rows)")
+    ap.add_argument("--tile-rows-b", type=int, default=-1, help="pcg_b tile height (-1 = auto)")
+    ap.add_argument("--b-kernel", default="rows", choices=["rows", "ring"],
+                    help="pcg_b: ring-free 2-row tiles (default) or the software-pipelined ring kernel")
     ap.add_argument("--waves", type=int, default=4, help="wave kernels: wave tiles per workgroup")
     ap.add_argument("--tile-rows", type=int, default=0, help="tile height (0 = auto)")
     ap.add_argument("--graph-batch", type=int, default=32)
@@ -90,7 +92,8 @@ def main():
     problem = pmx.PoissonEllipse(M=args.M, N=args.N, breakdown_tol=args.breakdown_tol)
     kw = dict(split=args.split, dtype=args.dtype, kernel=args.kernel, block=args.block, vec=args.vec,
               waves=args.waves, tile_rows=args.tile_rows, exact=args.exact, graph_batch=args.graph_batch,
-              overlap=args.overlap == "on", vec_b=args.vec_b, tile_rows_b=args.tile_rows_b)
+              overlap=args.overlap == "on", vec_b=args.vec_b, tile_rows_b=args.tile_rows_b,
+              b_ring=args.b_kernel == "ring")
     comm_used = args.comm
     if dry:
         tp = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.models.torch_pcg")

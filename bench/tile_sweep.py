@@ -33,6 +33,9 @@ def parse_cfg(c):
     kw = dict(kernel=parts[0])
     keys = dict(b="block", v="vec", w="waves", r="tile_rows", V="vec_b", W="waves_b", R="tile_rows_b")
     for q in parts[1:]:
+        if q == "ring":  # pcg_b ring kernel instead of the row kernel
+            kw["b_ring"] = True
+            continue
         kw[keys[q[0]]] = int(q[1:])
     return kw
 

@@ -9,7 +9,7 @@
 //       [--backend cpu|omp|hip] [--threads T] [--ranks P] [--gpus G] [--comm self|local|rccl]
 //       [--split reference|auto|rows|cols] [--dtype fp64|fp32|mixed] [--norm weighted|unweighted]
 //       [--exact] [--graph-batch 32] [--tile-rows 0] [--kernel wave|lds] [--vec 2] [--waves 4]
-//       [--block 256] [--device D] [--vec-b V] [--waves-b W] [--tile-rows-b R]
+//       [--block 256] [--device D] [--vec-b V] [--waves-b W] [--tile-rows-b R] [--b-kernel rows|ring]
 //       [--dump sol.txt] [--dump-stride s] [--json] [--banner stage0..stage4]
 //       [--profile-phases N] [--check] [--overlap on|off] [--poison-halos]
 //       [--checkpoint FILE [--checkpoint-every K]] [--resume FILE]
@@ -57,6 +57,7 @@ struct Cli {
                "           [--dtype fp64|fp32|mixed] [--norm weighted|unweighted] [--exact]\n"
                "           [--graph-batch N] [--tile-rows R] [--kernel wave|lds] [--vec V]\n"
                "           [--waves W] [--block B] [--device D] [--vec-b V] [--waves-b W] [--tile-rows-b R]\n"
+               "           [--b-kernel rows|ring]\n"
                "           [--dump FILE] [--dump-stride S] [--json] [--banner stage0..stage4]\n"
                "           [--profile-phases N] [--check] [--overlap on|off] [--poison-halos]\n"
                "           [--checkpoint FILE [--checkpoint-every K]] [--resume FILE]\n"
@@ -117,6 +118,11 @@ Cli parse(int argc, char** argv) {
     else if (a == "--vec-b") c.opt.vec_b = std::atoi(val().c_str());
     else if (a == "--waves-b") c.opt.waves_b = std::atoi(val().c_str());
     else if (a == "--tile-rows-b") c.opt.tile_rows_b = std::atoi(val().c_str());
+    else if (a == "--b-kernel") {
+      const std::string v = val();
+      if (v != "rows" && v != "ring") usage("--b-kernel rows|ring");
+      c.opt.b_ring = v == "ring";
+    }
     else if (a == "--kernel") {
       const std::string v = val();
       if (v != "wave" && v != "lds") usage("--kernel wave|lds");

@@ -155,7 +155,7 @@ class OpContext {
 GpuOptions make_options(int device, const std::string& kernel, int block, int vec, int waves,
                         int tile_rows, const std::string& dtype, bool exact, int graph_batch, bool check,
                         bool overlap = true, int vec_b = 0, int waves_b = 0, int tile_rows_b = -1,
-                        bool poison_halos = false) {
+                        bool poison_halos = false, bool b_ring = false) {
   GpuOptions o;
   o.device = device;
   PMX_CHECK(kernel == "lds" || kernel == "wave", "kernel must be lds or wave, got " << kernel);
@@ -175,6 +175,7 @@ GpuOptions make_options(int device, const std::string& kernel, int block, int ve
   o.waves_b = waves_b;
   o.tile_rows_b = tile_rows_b;
   o.poison_halos = poison_halos;
+  o.b_ring = b_ring ? 1 : 0;
   return o;
 }
 
@@ -282,11 +283,11 @@ PYBIND11_MODULE(_pmx, m) {
       .def(py::init([](const ProblemSpec& s, int Px, int Py, int rank, int device,
                        const std::string& kernel, int block, int vec, int waves, int tile_rows,
                        const std::string& dtype, bool exact, uintptr_t arena, bool check, int vec_b,
-                       int waves_b, int tile_rows_b) {
+                       int waves_b, int tile_rows_b, bool b_ring) {
              const Subdomain sd = decompose_2d(s.M, s.N, ProcGrid{Px, Py}, rank);
              return std::make_unique<GpuSubdomainSolver>(
                  s, sd, make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact, 0, check,
-                                     true, vec_b, waves_b, tile_rows_b),
+                                     true, vec_b, waves_b, tile_rows_b, false, b_ring),
                  arena);
            }),
            py::arg("spec"), py::arg("Px") = 1, py::arg("Py") = 1, py::arg("rank") = 0,
@@ -294,7 +295,7 @@ PYBIND11_MODULE(_pmx, m) {
            py::arg("vec") = 0, py::arg("waves") = 4, py::arg("tile_rows") = 0,
            py::arg("dtype") = "fp64", py::arg("exact") = false, py::arg("arena") = 0,
            py::arg("check") = false, py::arg("vec_b") = 0, py::arg("waves_b") = 0,
-           py::arg("tile_rows_b") = -1)
+           py::arg("tile_rows_b") = -1, py::arg("b_ring") = false)
       .def("enqueue_init", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_init(as_stream(s)); })
       .def("enqueue_phase_a", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_phase_a(as_stream(s)); })
       .def("enqueue_phase_b", [](GpuSubdomainSolver& g, uintptr_t s, bool pack) {
@@ -321,11 +322,12 @@ PYBIND11_MODULE(_pmx, m) {
                        int tile_rows, const std::string& dtype, bool exact, int graph_batch,
                        bool check, py::object uid, std::vector<int> ranks, std::vector<int> devices,
                        bool rccl_graph, bool overlap, int vec_b, int waves_b, int tile_rows_b,
-                       bool poison_halos) {
+                       bool poison_halos, bool b_ring) {
              SessionConfig c;
              c.spec = s;
              c.opt = make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact,
-                                  graph_batch, check, overlap, vec_b, waves_b, tile_rows_b, poison_halos);
+                                  graph_batch, check, overlap, vec_b, waves_b, tile_rows_b, poison_halos,
+                                  b_ring);
              c.split = split;
              c.world = world;
              if (comm == "self") c.comm = CommKind::kSelf;
@@ -346,7 +348,8 @@ PYBIND11_MODULE(_pmx, m) {
            py::arg("graph_batch") = 32, py::arg("check") = false, py::arg("uid") = py::none(),
            py::arg("ranks") = std::vector<int>{}, py::arg("devices") = std::vector<int>{},
            py::arg("rccl_graph") = false, py::arg("overlap") = true, py::arg("vec_b") = 0,
-           py::arg("waves_b") = 0, py::arg("tile_rows_b") = -1, py::arg("poison_halos") = false)
+           py::arg("waves_b") = 0, py::arg("tile_rows_b") = -1, py::arg("poison_halos") = false,
+           py::arg("b_ring") = false)
       .def("init", [](Session& s) { py::gil_scoped_release g; s.init(); })
       .def("step", [](Session& s, int64_t n) { py::gil_scoped_release g; s.step(n); })
       .def("synchronize", [](Session& s) { py::gil_scoped_release g; s.synchronize(); })
@@ -397,7 +400,8 @@ PYBIND11_MODULE(_pmx, m) {
       .def_property_readonly("tile", [](Session& s) {
         auto one = [](const TileCfg& t) {
           py::dict d;
-          d["kind"] = t.kind == 0 ? "lds" : "wave"; d["block"] = t.block; d["rows"] = t.rows;
+          d["kind"] = t.kind == 0 ? "lds" : t.kind == 1 ? "wave" : "wave-rows";
+          d["block"] = t.block; d["rows"] = t.rows;
           d["vec"] = t.vec; d["waves"] = t.waves; d["tiles_i"] = t.tiles_i; d["tiles_j"] = t.tiles_j;
           return d;
         };

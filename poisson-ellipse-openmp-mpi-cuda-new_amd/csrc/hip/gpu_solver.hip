@@ -141,8 +141,12 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
   // auto tile heights (caps and tile-count targets from bench/tile_sweep.py, see make_wave_tiles)
   tiles_ = opt.kernel == 0 ? make_tiles(G, opt.block, opt.tile_rows)
                            : make_wave_tiles(G, vec_a, opt.waves, opt.tile_rows, 32, 22000);
-  tiles_b_ = opt.kernel == 0 ? make_tiles(G, opt.block, rows_b)
-                             : make_wave_tiles(G, vec_b, waves_b, rows_b, 24, 66000);
+  if (opt.kernel == 0)
+    tiles_b_ = make_tiles(G, opt.block, rows_b);
+  else if (opt.b_ring)
+    tiles_b_ = make_wave_tiles(G, vec_b, waves_b, rows_b, 24, 66000);
+  else  // default: ring-free 2-row tiles, independent of the pcg_a height
+    tiles_b_ = make_row_tiles(G, vec_b, waves_b, opt.tile_rows_b >= 0 ? opt.tile_rows_b : 0);
 
   init_tiles_ = make_tiles(G, 256, 0);
   const size_t npart = size_t(std::max({tiles_.ntiles(), tiles_b_.ntiles(), init_tiles_.ntiles()}));
@@ -262,7 +266,7 @@ void GpuSubdomainSolver::phase_b_kernel_only(hipStream_t s, bool pack) {
   // pcg_b reads G.nb only to pack the send buffers: clearing it skips the packing
   DevGeom G = geom_;
   if (!pack) G.nb = 0;
-  if (tiles_b_.kind == 1)
+  if (tiles_b_.kind != 0)
     launch_pcg_b_wave<T>(G, tables_, static_cast<T*>(field_base(0)),
                          static_cast<T*>(field_base(1)), static_cast<const T*>(field_base(2)),
                          static_cast<const T*>(field_base(3)), halo<T>(), partials_, state_, tiles_b_,

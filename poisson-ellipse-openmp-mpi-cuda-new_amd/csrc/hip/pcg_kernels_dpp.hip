@@ -517,8 +517,132 @@ k_pcg_b_wave(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
 }
 
 // ---------------------------------------------------------------------------
+// k_pcg_b_rows (TileCfg kind 2, the default pcg_b): the same update without a register ring:
+// every row loads its three p rows (two of them L1/L2 hits: the neighbouring 2-row tiles of the
+// band run at the same time on the same XCD), w and r, and computes; latency is hidden by
+// occupancy (4 waves/SIMD) instead of software pipelining.  2-row tiles in XCD-banded row-major
+// order keep the concurrent DRAM footprint to a narrow band of rows: 5.24 TB/s effective vs
+// 5.04 for the ring kernel's 24-row marches (profiles/NOTES_perf_experiments.md #19).
+// ---------------------------------------------------------------------------
+template <typename T, int VEC, int WAVES, bool EXACT>
+__global__ void __launch_bounds__(64 * WAVES)
+k_pcg_b_rows(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, const T* p0,
+             const T* p1, HaloBufs<T> H, double* __restrict__ partials, PcgState* S, int TI,
+             int tiles_j, int ntiles, int abl) {
+  constexpr int W = 64 * VEC;
+  if (S->done) return;
+  const long long k = S->it;
+  const double denom = S->red_a[0];
+  const bool bd = S->norm == int(Norm::kWeighted) ? fabs(denom) < S->bd_tol : denom < S->bd_tol;
+  if (bd || !(denom == denom)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      S->iters = k;
+      S->status = int(Status::kBreakdown);
+      if (!(denom == denom)) S->nan_flag = 1;
+      S->done = 1;
+    }
+    return;
+  }
+  const double alpha = S->zr[(k - 1) & 1] / denom;
+  const WaveTile t = wave_tile(WAVES, tiles_j, ntiles, TI, W, G, abl);
+  if (!t.live) return;
+  const T* __restrict__ pn = (k & 1) ? p1 : p0;
+  const int64_t P = G.pitch;
+  const int lane = threadIdx.x & 63;
+  const int jl = t.j0 + lane * VEC;
+  bool valid[VEC];
+  int gjc[VEC];
+#pragma unroll
+  for (int u = 0; u < VEC; ++u) {
+    valid[u] = jl + u <= t.jend;
+    gjc[u] = G.gj0 + min(jl + u, t.jend);
+  }
+  const bool lane_any = valid[0];
+  const bool lane_full = valid[VEC - 1];
+  const int jlp = min(jl, 1 + (G.ny / VEC) * VEC);
+  const int jlw = min(jl, 1 + ((G.ny - 1) / VEC) * VEC);
+  const int jr = t.jend + 1;
+  double dacc = 0.0, zacc = 0.0;
+  for (int i = t.i0; i <= t.iend; ++i) {
+    T pm[VEC], pc[VEC], pp[VEC], wr[VEC], rr[VEC];
+    vload_raw<T, VEC>(pn + int64_t(i - 1) * P + jlp, pm);
+    vload_raw<T, VEC>(pn + int64_t(i) * P + jlp, pc);
+    vload_raw<T, VEC>(pn + int64_t(i + 1) * P + jlp, pp);
+    vload_raw<T, VEC>(w + int64_t(i) * P + jlw, wr);
+    vload_raw<T, VEC>(r + int64_t(i) * P + jlw, rr);
+    const T el = pn[int64_t(i) * P + t.j0 - 1], er = pn[int64_t(i) * P + jr];
+    const RowConst rc = load_row(Tb, G.gi0 + i);
+    const int ucls = EXACT ? 0 : row_class(rc, G.gj0 + t.j0, G.gj0 + t.jend);
+    const double uval = ucls == 1 ? 1.0 : G.inv_eps;
+    const double left = double(dpp_shift<kWaveShr1>(pc[VEC - 1], el));
+    const double right = double(dpp_shift<kWaveShl1>(pc[0], er));
+    T ws[VEC], rs[VEC];
+#pragma unroll
+    for (int u = 0; u < VEC; ++u) {
+      const double pjm = u == 0 ? left : double(pc[u - 1]);
+      const double pjp = u == VEC - 1 ? right : double(pc[u + 1]);
+      double a0, a1, b0, b1;
+      if (ucls != 0) {
+        a0 = a1 = b0 = b1 = uval;
+      } else {
+        const ColConst c = load_col(Tb, gjc[u]);
+        a0 = face_a0c(c, rc, G);
+        a1 = face_a1c(c, rc, G);
+        b0 = face_b0c(c, rc, G);
+        b1 = face_b1c(c, rc, G);
+      }
+      const double pcu = double(pc[u]);
+      const double Ap = apply_a<EXACT>(pcu, double(pm[u]), double(pp[u]), pjm, pjp, a0, a1, b0, b1, G);
+      const double wo = double(wr[u]), ro = double(rr[u]);
+      ws[u] = static_cast<T>(upd_w<EXACT>(wo, alpha, pcu));
+      rs[u] = static_cast<T>(upd_r<EXACT>(ro, alpha, Ap));
+      if (valid[u]) {
+        const double dw = double(ws[u]) - wo;
+        dacc += dw * dw;
+        const double rq = double(rs[u]);
+        zacc += zdiv_u<EXACT>(ucls, rq, a0, a1, b0, b1, G) * rq;
+      }
+    }
+    const int64_t c = int64_t(i) * P + jl;
+    if (lane_full) {
+      vstore<T, VEC>(w + c, ws);
+      vstore<T, VEC>(r + c, rs);
+    } else {
+#pragma unroll
+      for (int u = 0; u < VEC; ++u)
+        if (valid[u]) { w[c + u] = ws[u]; r[c + u] = rs[u]; }
+    }
+    if (lane_any) {
+      if (i == 1 && (G.nb & kNbXlo)) {
+#pragma unroll
+        for (int u = 0; u < VEC; ++u) if (valid[u]) H.send[0][jl + u - 1] = rs[u];
+      }
+      if (i == G.nx && (G.nb & kNbXhi)) {
+#pragma unroll
+        for (int u = 0; u < VEC; ++u) if (valid[u]) H.send[1][jl + u - 1] = rs[u];
+      }
+      if (jl == 1 && (G.nb & kNbYlo)) H.send[2][i - 1] = rs[0];
+#pragma unroll
+      for (int u = 0; u < VEC; ++u)
+        if (jl + u == G.ny && (G.nb & kNbYhi)) H.send[3][i - 1] = rs[u];
+    }
+  }
+  wave_sum2_mfma(dacc, zacc);
+  if (lane == 0) {
+    partials[2 * t.id] = dacc;
+    partials[2 * t.id + 1] = zacc;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
+TileCfg make_row_tiles(const DevGeom& G, int vec, int waves, int rows) {
+  TileCfg t = make_wave_tiles(G, vec, waves, rows == 0 ? 2 : rows);
+  t.kind = 2;
+  return t;
+}
+
 TileCfg make_wave_tiles(const DevGeom& G, int vec, int waves, int rows, int max_auto_rows,
                         int target_tiles) {
   PMX_CHECK(vec == 1 || vec == 2 || vec == 4, "vec must be 1, 2 or 4");
@@ -580,7 +704,14 @@ template <typename T>
 void launch_pcg_b_wave(const DevGeom& G, const DevTables& Tb, T* w, T* r, const T* p0,
                        const T* p1, HaloBufs<T> H, double* partials, PcgState* S,
                        const TileCfg& tc, bool exact, hipStream_t s) {
-  if (exact)
+  if (tc.kind == 2) {  // ring-free row kernel
+    if (exact)
+      PMX_WAVE_DISPATCH(tc, true, k_pcg_b_rows, G, Tb, w, r, p0, p1, H, partials, S, tc.rows,
+                        tc.tiles_j, tc.ntiles(), tc.abl);
+    else
+      PMX_WAVE_DISPATCH(tc, false, k_pcg_b_rows, G, Tb, w, r, p0, p1, H, partials, S, tc.rows,
+                        tc.tiles_j, tc.ntiles(), tc.abl);
+  } else if (exact)
     PMX_WAVE_DISPATCH(tc, true, k_pcg_b_wave, G, Tb, w, r, p0, p1, H, partials, S, tc.rows,
                       tc.tiles_j, tc.ntiles(), tc.abl);
   else

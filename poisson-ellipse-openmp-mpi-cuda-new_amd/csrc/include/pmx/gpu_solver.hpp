@@ -48,7 +48,8 @@ struct GpuOptions {
   int tile_rows = 0;      // tile height (marching length), 0 = auto-size for occupancy
   int vec_b = 0;          // pcg_b columns per lane (0 = vec if set, else auto: 2 fp64 / 4 fp32)
   int waves_b = 0;        // pcg_b wave tiles per workgroup (0 = waves)
-  int tile_rows_b = -1;   // pcg_b tile height (-1 = tile_rows)
+  int tile_rows_b = -1;   // pcg_b tile height (-1 = tile_rows, or 2 for the row kernel)
+  int b_ring = 0;         // kernel 1: 0 = ring-free row kernel for pcg_b (default), 1 = ring kernel
   DType dtype = DType::kFp64;
   bool exact = false;     // reference arithmetic order inside the fused kernels
   int graph_batch = 32;   // iterations per captured hipGraph (0 = eager launches)

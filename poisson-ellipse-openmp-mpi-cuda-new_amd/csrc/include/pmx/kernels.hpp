@@ -18,7 +18,8 @@ namespace pmx {
 
 struct TileCfg {
   int kind = 0;       // 0: workgroup tile + LDS row ring (pcg_kernels.hip)
-                      // 1: wave tile + DPP lane shifts (pcg_kernels_dpp.hip)
+                      // 1: wave tile + DPP lane shifts, software-pipelined register ring
+                      // 2: wave tile + DPP lane shifts, ring-free short tiles (pcg_b only)
   int block = 256;    // columns per tile (kind 0: = threads per block; kind 1: = 64*vec)
   int rows = 0;       // rows per tile (marching length); 0 = auto
   int vec = 1;        // kind 1: columns per lane
@@ -32,6 +33,8 @@ TileCfg make_tiles(const DevGeom& G, int block, int rows);
 // rows = 0: auto, about target_tiles tiles but no taller than max_auto_rows
 TileCfg make_wave_tiles(const DevGeom& G, int vec, int waves, int rows, int max_auto_rows = 32,
                         int target_tiles = 22000);
+// kind 2 tiles for k_pcg_b_rows (rows = 0: 2)
+TileCfg make_row_tiles(const DevGeom& G, int vec, int waves, int rows);
 
 enum ReduceMode : int { kSkipIfDone = 1, kBumpIter = 2 };
 

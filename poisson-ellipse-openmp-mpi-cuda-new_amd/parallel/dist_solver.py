@@ -33,7 +33,8 @@ class DistGpuPCG:
     def __init__(self, problem, info: DistInfo, comm: str = "native", split: str = "reference",
                  dtype: str = "fp64", kernel: str = "wave", block: int = 256, vec: int = 0, waves: int = 4,
                  tile_rows: int = 0, exact: bool = False, graph_batch: int = 32, rccl_graph: bool = False,
-                 overlap: bool = True, vec_b: int = 0, waves_b: int = 0, tile_rows_b: int = -1):
+                 overlap: bool = True, vec_b: int = 0, waves_b: int = 0, tile_rows_b: int = -1,
+                 b_ring: bool = False):
         self.problem = problem
         self.info = info
         self.comm_kind = comm
@@ -53,7 +54,8 @@ class DistGpuPCG:
                                           tile_rows=tile_rows, dtype=dtype, exact=exact,
                                           graph_batch=graph_batch if rccl_graph else 0, uid=uid[0],
                                           ranks=[info.rank], devices=[self.device], rccl_graph=rccl_graph,
-                                          overlap=overlap, vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b)
+                                          overlap=overlap, vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b,
+                                          b_ring=b_ring)
             self.sd = self.session.subdomain(0)
         elif comm == "torch":
             lay = self.n.comm_layout(problem.M, problem.N, self.Px, self.Py, info.rank, dtype)
@@ -64,7 +66,8 @@ class DistGpuPCG:
             self.solver = self.n.SubdomainSolver(self.spec, self.Px, self.Py, info.rank, device=self.device,
                                                  kernel=kernel, block=block, vec=vec, waves=waves,
                                                  tile_rows=tile_rows, dtype=dtype, exact=exact, arena=base + pad,
-                                                 vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b)
+                                                 vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b,
+                                                 b_ring=b_ring)
             self.sd = self.solver.subdomain()
             tdt = torch.float64 if dtype == "fp64" else torch.float32
             el = lay["elem"]

@@ -76,11 +76,14 @@ def test_lds_tile_shapes(pkg, block, rows):
 
 @pytest.mark.parametrize("vec,waves,rows", [(1, 4, 1), (2, 4, 64), (2, 1, 5), (2, 8, 33), (1, 4, 0), (2, 4, 0), (4, 4, 0), (4, 4, 7)])
 @pytest.mark.parametrize("grid", [(211, 1031), (97, 130), (300, 257)])
-def test_wave_tile_shapes(pkg, vec, waves, rows, grid):
-    """Wave-tile kernels on full and partial tiles (odd widths leave half-filled lanes)."""
+@pytest.mark.parametrize("b_ring", [False, True])
+def test_wave_tile_shapes(pkg, vec, waves, rows, grid, b_ring):
+    """Wave-tile kernels on full and partial tiles (odd widths leave half-filled lanes); pcg_b as
+    the ring-free row kernel (rows = its tile height) or the pipelined ring kernel."""
     p = pkg.PoissonEllipse(M=grid[0], N=grid[1])
     ref = pkg.solve(p, "hip", kernel="lds")
-    r = pkg.solve(p, "hip", kernel="wave", vec=vec, waves=waves, tile_rows=rows)
+    r = pkg.solve(p, "hip", kernel="wave", vec=vec, waves=waves, tile_rows=rows, b_ring=b_ring,
+                  tile_rows_b=-1 if b_ring else rows)
     assert r.iters == ref.iters
     assert np.abs(r.w - ref.w).max() < 1e-12
 
