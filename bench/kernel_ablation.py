@@ -43,7 +43,7 @@ for rnd in range(a.rounds):
     for cfg in a.configs.split(","):
         s = models.make_session(p, **parse_cfg(cfg))
         s.init()
-        for which in (0, 1):
+        for which in (0, 1, 2):
             for abl in abls:
                 if cfg.startswith("lds") and abl:
                     continue
@@ -52,6 +52,9 @@ for rnd in range(a.rounds):
         del s
 for (cfg, which, abl), v in res.items():
     ms = statistics.median(v)
-    gb = field_gb * (3 if which == 0 else 5)
-    print(json.dumps(dict(cfg=cfg, kernel="pcg_a" if which == 0 else "pcg_b", abl=abl, ms=round(ms, 4),
+    # pcg_a: r, p^{k-1} in, p^k out; pcg_b even (paired w step): p, w, r in, w, r out; pcg_b odd
+    # (w step deferred): p, r in, r out
+    gb = field_gb * (3, 5, 3)[which]
+    name = ("pcg_a", "pcg_b_even", "pcg_b_odd")[which]
+    print(json.dumps(dict(cfg=cfg, kernel=name, abl=abl, ms=round(ms, 4),
                           tbps=round(gb / ms, 3))))

@@ -61,6 +61,7 @@ py::dict state_dict(const PcgState& st) {
   d["done"] = bool(st.done);
   d["status"] = std::string(status_name(Status(st.status)));
   d["nan"] = bool(st.nan_flag);
+  d["w_pend"] = st.w_pend;
   return d;
 }
 

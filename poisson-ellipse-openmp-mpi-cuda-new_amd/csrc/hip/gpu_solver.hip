@@ -6,6 +6,7 @@
 // Here per iteration: 4 launches (2 streaming + 2 single-block reductions), zero host syncs,
 // replayed from a hipGraph in batches.
 #include <chrono>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <istream>
@@ -386,13 +387,16 @@ double GpuSubdomainSolver::bench_kernel(int which, int abl, int reps, hipStream_
   PcgState& st = host_state_[1];
   std::memset(&st, 0, sizeof(st));
   st.delta = 0.0;
-  st.it = 2;  // a mid-solve iteration: beta path, p^{k-1} read
+  // a mid-solve iteration: beta path, p^{k-1} read.  which = 2: pcg_b on an odd iteration (w
+  // step deferred, see k_pcg_b_rows); which = 1 is the even (paired w update) one
+  st.it = which == 2 ? 3 : 2;
   st.max_iter = int64_t(1) << 40;
   st.norm = int(spec_.norm);
   st.red_a[0] = 1.0;
   st.red_b[0] = 1.0;
   st.red_b[1] = 1e-3;
   st.zr[0] = st.zr[1] = 1e-3;
+  st.alpha[0] = st.alpha[1] = 1.0;
   const TileCfg saved = tiles_, saved_b = tiles_b_;
   tiles_.abl = abl;
   tiles_b_.abl = abl;
@@ -458,10 +462,26 @@ std::vector<double> GpuSubdomainSolver::download_field(int which, hipStream_t s)
 
 std::vector<double> GpuSubdomainSolver::download_w(hipStream_t s) const {
   const std::vector<double> f = download_field(0, s);
+  // Paired w updates (k_pcg_b_rows): an odd iteration leaves w^{k+1} = w^k + alpha_k p^k pending
+  // in device memory; apply it here, rounded to the storage type like a device update.
+  const PcgState st = read_state(s);
+  std::vector<double> pk;
+  double a = 0.0;
+  if (st.w_pend > 0) {
+    pk = download_field((st.w_pend & 1) ? 3 : 2, s);
+    a = st.alpha[st.w_pend & 1];
+  }
   std::vector<double> out(size_t(sd_.nx) * sd_.ny);
   for (int li = 1; li <= sd_.nx; ++li)
-    for (int lj = 1; lj <= sd_.ny; ++lj)
-      out[size_t(li - 1) * sd_.ny + (lj - 1)] = f[size_t(li) * (sd_.ny + 2) + lj];
+    for (int lj = 1; lj <= sd_.ny; ++lj) {
+      const size_t src = size_t(li) * (sd_.ny + 2) + lj;
+      double v = f[src];
+      if (!pk.empty()) {
+        v = std::fma(a, pk[src], v);
+        if (elem_ == 4) v = double(float(v));
+      }
+      out[size_t(li - 1) * sd_.ny + (lj - 1)] = v;
+    }
   return out;
 }
 

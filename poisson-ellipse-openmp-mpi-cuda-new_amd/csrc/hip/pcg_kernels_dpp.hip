@@ -523,30 +523,29 @@ k_pcg_b_wave(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
 // occupancy (4 waves/SIMD) instead of software pipelining.  2-row tiles in XCD-banded row-major
 // order keep the concurrent DRAM footprint to a narrow band of rows: 5.24 TB/s effective vs
 // 5.04 for the ring kernel's 24-row marches (profiles/NOTES_perf_experiments.md #19).
+//
+// Paired w updates (fast mode).  w is not part of the CG recurrence (r is updated recursively),
+// so its update can be deferred: an odd iteration k leaves alpha_k p^k pending (PcgState::w_pend)
+// and does not touch w, the next (even) iteration applies both steps in one read-modify-write:
+//   w^{k+1} = w^{k-1} + alpha_{k-1} p^{k-1} + alpha_k p^k.
+// p^{k-1} is not re-read: k_pcg_a formed p^k = z^{k-1} + beta_k p^{k-1}, and this kernel already
+// holds r^{k-1} (its input r), so p^{k-1} = (p^k - z^{k-1}) / beta_k and
+//   w^{k+1} = w^{k-1} + c1 p^k - c2 z^{k-1},  c2 = alpha_{k-1} / beta_k,  c1 = alpha_k + c2.
+// The recovery's rounding error is eps |p^k| / beta_k; for |beta_k| < kRecoverMinBeta the kernel
+// reads p^{k-1} from the other ping-pong buffer instead (still intact: k_pcg_a(k) only read it).
+// Traffic per iteration pair: 40 + 24 B/pt instead of 2 x 40 (the iteration is 64 -> 56 B/pt).
+// ||w^{k+1} - w^k|| is computed as ||alpha_k p^k|| (the same quantity without the rounding of w).
+// Readers of w materialise a pending step (GpuSubdomainSolver::download_w).
 // ---------------------------------------------------------------------------
-template <typename T, int VEC, int WAVES, bool EXACT>
-__global__ void __launch_bounds__(64 * WAVES)
-k_pcg_b_rows(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, const T* p0,
-             const T* p1, HaloBufs<T> H, double* __restrict__ partials, PcgState* S, int TI,
-             int tiles_j, int ntiles, int abl) {
-  constexpr int W = 64 * VEC;
-  if (S->done) return;
-  const long long k = S->it;
-  const double denom = S->red_a[0];
-  const bool bd = S->norm == int(Norm::kWeighted) ? fabs(denom) < S->bd_tol : denom < S->bd_tol;
-  if (bd || !(denom == denom)) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      S->iters = k;
-      S->status = int(Status::kBreakdown);
-      if (!(denom == denom)) S->nan_flag = 1;
-      S->done = 1;
-    }
-    return;
-  }
-  const double alpha = S->zr[(k - 1) & 1] / denom;
-  const WaveTile t = wave_tile(WAVES, tiles_j, ntiles, TI, W, G, abl);
-  if (!t.live) return;
-  const T* __restrict__ pn = (k & 1) ? p1 : p0;
+enum BwMode : int { kBwEvery = 0, kBwPend = 1, kBwRecover = 2, kBwLoad = 3 };
+constexpr double kRecoverMinBeta = 1e-3;
+
+template <typename T, int VEC, bool EXACT, int MODE>
+__device__ __forceinline__ void pcg_b_rows_march(const DevGeom& G, const DevTables& Tb, T* __restrict__ w,
+                                                 T* __restrict__ r, const T* __restrict__ pn,
+                                                 const T* __restrict__ pprev, const HaloBufs<T>& H,
+                                                 const WaveTile& t, double alpha, double c1, double c2,
+                                                 double& dacc, double& zacc) {
   const int64_t P = G.pitch;
   const int lane = threadIdx.x & 63;
   const int jl = t.j0 + lane * VEC;
@@ -562,13 +561,14 @@ k_pcg_b_rows(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
   const int jlp = min(jl, 1 + (G.ny / VEC) * VEC);
   const int jlw = min(jl, 1 + ((G.ny - 1) / VEC) * VEC);
   const int jr = t.jend + 1;
-  double dacc = 0.0, zacc = 0.0;
+  constexpr bool kReadW = MODE != kBwPend;
   for (int i = t.i0; i <= t.iend; ++i) {
-    T pm[VEC], pc[VEC], pp[VEC], wr[VEC], rr[VEC];
+    T pm[VEC], pc[VEC], pp[VEC], wr[VEC], rr[VEC], pv[VEC];
     vload_raw<T, VEC>(pn + int64_t(i - 1) * P + jlp, pm);
     vload_raw<T, VEC>(pn + int64_t(i) * P + jlp, pc);
     vload_raw<T, VEC>(pn + int64_t(i + 1) * P + jlp, pp);
-    vload_raw<T, VEC>(w + int64_t(i) * P + jlw, wr);
+    if constexpr (kReadW) vload_raw<T, VEC>(w + int64_t(i) * P + jlw, wr);
+    if constexpr (MODE == kBwLoad) vload_raw<T, VEC>(pprev + int64_t(i) * P + jlw, pv);
     vload_raw<T, VEC>(r + int64_t(i) * P + jlw, rr);
     const T el = pn[int64_t(i) * P + t.j0 - 1], er = pn[int64_t(i) * P + jr];
     const RowConst rc = load_row(Tb, G.gi0 + i);
@@ -593,11 +593,23 @@ k_pcg_b_rows(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
       }
       const double pcu = double(pc[u]);
       const double Ap = apply_a<EXACT>(pcu, double(pm[u]), double(pp[u]), pjm, pjp, a0, a1, b0, b1, G);
-      const double wo = double(wr[u]), ro = double(rr[u]);
-      ws[u] = static_cast<T>(upd_w<EXACT>(wo, alpha, pcu));
+      const double ro = double(rr[u]);
+      double dw;
+      if constexpr (MODE == kBwEvery) {
+        const double wo = double(wr[u]);
+        ws[u] = static_cast<T>(upd_w<EXACT>(wo, alpha, pcu));
+        dw = double(ws[u]) - wo;
+      } else {
+        dw = alpha * pcu;
+        if constexpr (MODE == kBwRecover) {
+          const double zo = zdiv_u<EXACT>(ucls, ro, a0, a1, b0, b1, G);  // z^{k-1}, as in k_pcg_a
+          ws[u] = static_cast<T>(__builtin_fma(c1, pcu, __builtin_fma(-c2, zo, double(wr[u]))));
+        } else if constexpr (MODE == kBwLoad) {
+          ws[u] = static_cast<T>(__builtin_fma(alpha, pcu, __builtin_fma(c2, double(pv[u]), double(wr[u]))));
+        }
+      }
       rs[u] = static_cast<T>(upd_r<EXACT>(ro, alpha, Ap));
       if (valid[u]) {
-        const double dw = double(ws[u]) - wo;
         dacc += dw * dw;
         const double rq = double(rs[u]);
         zacc += zdiv_u<EXACT>(ucls, rq, a0, a1, b0, b1, G) * rq;
@@ -605,12 +617,15 @@ k_pcg_b_rows(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
     }
     const int64_t c = int64_t(i) * P + jl;
     if (lane_full) {
-      vstore<T, VEC>(w + c, ws);
+      if constexpr (kReadW) vstore<T, VEC>(w + c, ws);
       vstore<T, VEC>(r + c, rs);
     } else {
 #pragma unroll
       for (int u = 0; u < VEC; ++u)
-        if (valid[u]) { w[c + u] = ws[u]; r[c + u] = rs[u]; }
+        if (valid[u]) {
+          if constexpr (kReadW) w[c + u] = ws[u];
+          r[c + u] = rs[u];
+        }
     }
     if (lane_any) {
       if (i == 1 && (G.nb & kNbXlo)) {
@@ -627,8 +642,57 @@ k_pcg_b_rows(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
         if (jl + u == G.ny && (G.nb & kNbYhi)) H.send[3][i - 1] = rs[u];
     }
   }
+}
+
+template <typename T, int VEC, int WAVES, bool EXACT>
+__global__ void __launch_bounds__(64 * WAVES)
+k_pcg_b_rows(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, const T* p0,
+             const T* p1, HaloBufs<T> H, double* __restrict__ partials, PcgState* S, int TI,
+             int tiles_j, int ntiles, int abl) {
+  constexpr int W = 64 * VEC;
+  if (S->done) return;
+  const long long k = S->it;
+  const double denom = S->red_a[0];
+  const bool bd = S->norm == int(Norm::kWeighted) ? fabs(denom) < S->bd_tol : denom < S->bd_tol;
+  if (bd || !(denom == denom)) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      S->iters = k;
+      S->status = int(Status::kBreakdown);
+      if (!(denom == denom)) S->nan_flag = 1;
+      S->done = 1;
+    }
+    return;
+  }
+  const double alpha = S->zr[(k - 1) & 1] / denom;
+  // pairing: odd k defers its w step, even k applies two (slot k & 1 of alpha is written here and
+  // slot (k - 1) & 1 only read, so no block can see a half-written value)
+  const bool odd = k & 1;
+  const double alpha_prev = S->alpha[(k - 1) & 1];
+  const double beta = S->zr[(k - 1) & 1] / S->zr[k & 1];  // beta_k of k_pcg_a(k)
+  const bool recover = !odd && fabs(beta) >= kRecoverMinBeta;
+  if (!EXACT && blockIdx.x == 0 && threadIdx.x == 0) {
+    S->alpha[k & 1] = alpha;
+    S->w_pend = odd ? k : 0;
+  }
+  const WaveTile t = wave_tile(WAVES, tiles_j, ntiles, TI, W, G, abl);
+  if (!t.live) return;
+  const T* __restrict__ pn = (k & 1) ? p1 : p0;
+  const T* __restrict__ pprev = (k & 1) ? p0 : p1;
+  double dacc = 0.0, zacc = 0.0;
+  if constexpr (EXACT) {
+    pcg_b_rows_march<T, VEC, EXACT, kBwEvery>(G, Tb, w, r, pn, pprev, H, t, alpha, 0.0, 0.0, dacc, zacc);
+  } else if (odd) {
+    pcg_b_rows_march<T, VEC, EXACT, kBwPend>(G, Tb, w, r, pn, pprev, H, t, alpha, 0.0, 0.0, dacc, zacc);
+  } else if (recover) {
+    const double c2 = alpha_prev / beta;
+    pcg_b_rows_march<T, VEC, EXACT, kBwRecover>(G, Tb, w, r, pn, pprev, H, t, alpha, alpha + c2, c2,
+                                                 dacc, zacc);
+  } else {
+    pcg_b_rows_march<T, VEC, EXACT, kBwLoad>(G, Tb, w, r, pn, pprev, H, t, alpha, alpha, alpha_prev,
+                                              dacc, zacc);
+  }
   wave_sum2_mfma(dacc, zacc);
-  if (lane == 0) {
+  if ((threadIdx.x & 63) == 0) {
     partials[2 * t.id] = dacc;
     partials[2 * t.id + 1] = zacc;
   }

@@ -56,6 +56,10 @@ struct alignas(64) PcgState {
   int status;        // pmx::Status
   int norm;          // pmx::Norm
   int nan_flag;      // set when a reduction produced NaN/Inf (failure detection)
+  // Paired w updates (fast row kernel): odd iterations leave w^{k+1} = w^k + alpha_k p^k pending
+  // and the next (even) iteration applies both steps in one read-modify-write of w.
+  double alpha[2];   // alpha_k at slot k & 1
+  long long w_pend;  // k whose alpha_k p^k is not yet in w (0 = w is current); p^k is in p[k & 1]
 };
 
 // Pointers for the halo ("ghost") exchange of r.  Side order: 0 x-lo, 1 x-hi, 2 y-lo, 3 y-hi.
