@@ -57,7 +57,7 @@ struct Cli {
                "           [--dtype fp64|fp32|mixed] [--norm weighted|unweighted] [--exact]\n"
                "           [--graph-batch N] [--tile-rows R] [--kernel wave|lds] [--vec V]\n"
                "           [--waves W] [--block B] [--device D] [--vec-b V] [--waves-b W] [--tile-rows-b R]\n"
-               "           [--b-kernel rows|ring]\n"
+               "           [--b-kernel rows|ring] [--pair-w 0|1|2]\n"
                "           [--dump FILE] [--dump-stride S] [--json] [--banner stage0..stage4]\n"
                "           [--profile-phases N] [--check] [--overlap on|off] [--poison-halos]\n"
                "           [--checkpoint FILE [--checkpoint-every K]] [--resume FILE]\n"
@@ -123,6 +123,7 @@ Cli parse(int argc, char** argv) {
       if (v != "rows" && v != "ring") usage("--b-kernel rows|ring");
       c.opt.b_ring = v == "ring";
     }
+    else if (a == "--pair-w") c.opt.pair_w = std::atoi(val().c_str());
     else if (a == "--kernel") {
       const std::string v = val();
       if (v != "wave" && v != "lds") usage("--kernel wave|lds");

@@ -401,13 +401,14 @@ PYBIND11_MODULE(_pmx, m) {
       .def_property_readonly("tile", [](Session& s) {
         auto one = [](const TileCfg& t) {
           py::dict d;
-          d["kind"] = t.kind == 0 ? "lds" : t.kind == 1 ? "wave" : "wave-rows";
+          d["kind"] = t.kind == 0 ? "lds" : t.kind == 1 ? "wave" : t.kind == 2 ? "wave-rows" : "pcg1";
           d["block"] = t.block; d["rows"] = t.rows;
           d["vec"] = t.vec; d["waves"] = t.waves; d["tiles_i"] = t.tiles_i; d["tiles_j"] = t.tiles_j;
           return d;
         };
         py::dict d = one(s.solver(0).tiles());
-        d["b"] = one(s.solver(0).tiles_b());
+        if (!s.solver(0).single_pass()) d["b"] = one(s.solver(0).tiles_b());
+        d["algo"] = s.solver(0).single_pass() ? "pcg1" : "pcg2";
         return d;
       });
 }

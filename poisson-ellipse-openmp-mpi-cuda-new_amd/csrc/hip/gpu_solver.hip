@@ -105,6 +105,12 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
   PMX_CHECK(sd.nx >= 1 && sd.ny >= 1, "empty subdomain");
   HIP_CHECK(hipSetDevice(opt.device));
   elem_ = opt.dtype == DType::kFp64 ? 8 : 4;
+  if (const char* pw = std::getenv("PMX_PAIR_W"); pw && pw[0]) opt_.pair_w = std::atoi(pw);
+  PMX_CHECK(opt_.pair_w >= 0 && opt_.pair_w <= 2, "pair_w must be 0, 1 or 2");
+  if (const char* a = std::getenv("PMX_ALGO"); a && a[0]) opt_.algo = std::atoi(a);
+  if (const char* a = std::getenv("PMX_PCG1_VEC"); a && a[0]) opt_.vec1 = std::atoi(a);
+  if (const char* a = std::getenv("PMX_PCG1_ROWS"); a && a[0]) opt_.rows1 = std::atoi(a);
+  if (const char* a = std::getenv("PMX_PCG1_WAVES"); a && a[0]) opt_.waves1 = std::atoi(a);
   const size_t align_elems = 256 / elem_;
 
   // +8 columns of padding: vector loads of VEC <= 4 columns starting at <= ny+1 stay in the row
@@ -148,11 +154,24 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
     tiles_b_ = make_wave_tiles(G, vec_b, waves_b, rows_b, 24, 66000);
   else  // default: ring-free 2-row tiles, independent of the pcg_a height
     tiles_b_ = make_row_tiles(G, vec_b, waves_b, opt.tile_rows_b >= 0 ? opt.tile_rows_b : 0);
+  tiles_b_.pair_w = tiles_b_.kind == 2 && !opt.exact && opt_.pair_w != 0;
+
+  // single-pass iteration where it applies (see GpuOptions::algo)
+  PMX_CHECK(opt_.algo == -1 || opt_.algo == 1 || opt_.algo == 2, "algo must be -1, 1 or 2");
+  const bool pcg1_ok = G.nb == 0 && !opt.exact && opt.kernel == 1;
+  PMX_CHECK(opt_.algo != 1 || pcg1_ok,
+            "pcg1 needs the wave kernels, the fast arithmetic and a subdomain without neighbours");
+  pcg1_ = opt_.algo == 1 || (opt_.algo == -1 && pcg1_ok);
+  if (pcg1_) {
+    tiles1_ = make_pcg1_tiles(G, opt_.vec1, opt_.waves1, opt_.rows1);
+    HIP_CHECK(hipMalloc(&r2_, field_bytes_));
+  }
 
   init_tiles_ = make_tiles(G, 256, 0);
-  const size_t npart = size_t(std::max({tiles_.ntiles(), tiles_b_.ntiles(), init_tiles_.ntiles()}));
-  HIP_CHECK(hipMalloc(&partials_, (npart * 2 + kReduceWsDoubles) * sizeof(double)));
-  reduce_ws_ = partials_ + npart * 2;
+  const size_t npart = size_t(std::max({tiles_.ntiles(), tiles_b_.ntiles(), init_tiles_.ntiles(),
+                                        pcg1_ ? tiles1_.ntiles() : 0}));
+  HIP_CHECK(hipMalloc(&partials_, (npart * 5 + kReduceWsDoubles) * sizeof(double)));
+  reduce_ws_ = partials_ + npart * 5;
   HIP_CHECK(hipMemset(reduce_ws_, 0, kReduceWsDoubles * sizeof(double)));
 
   layout_ = comm_layout(sd, opt.dtype);
@@ -173,6 +192,7 @@ GpuSubdomainSolver::~GpuSubdomainSolver() {
   (void)hipSetDevice(opt_.device);
   (void)hipDeviceSynchronize();
   if (fields_) (void)hipFree(fields_);
+  if (r2_) (void)hipFree(r2_);
   if (tables_buf_) (void)hipFree(tables_buf_);
   if (partials_) (void)hipFree(partials_);
   if (own_arena_ && arena_) (void)hipFree(arena_);
@@ -186,13 +206,13 @@ size_t GpuSubdomainSolver::estimate_device_bytes(const ProblemSpec& spec, const 
   const size_t field = round_up((align - 1 + size_t(sd.nx + 2) * pitch) * elem, 256);
   const size_t tables = (4 * size_t(spec.M + 2) + 4 * size_t(spec.N + 2)) * 8 + 8 * size_t(spec.M + 2) * 4;
   // partials: at most one per 2 rows x 64 columns tile (the smallest auto tile), 2 doubles each
-  const size_t partials = (size_t(sd.nx + 1) / 2 + 1) * (size_t(sd.ny) / 64 + 1) * 16;
+  const size_t partials = (size_t(sd.nx + 1) / 2 + 1) * (size_t(sd.ny) / 64 + 1) * 40;
   return 4 * field + tables + partials + comm_layout(sd, dtype).bytes + (1u << 20);
 }
 
 size_t GpuSubdomainSolver::device_bytes() const {
   return 4 * field_bytes_ + (4 * (spec_.M + 2) + 4 * (spec_.N + 2)) * sizeof(double) +
-         (size_t(std::max({tiles_.ntiles(), tiles_b_.ntiles(), init_tiles_.ntiles()})) * 2 + kReduceWsDoubles) * sizeof(double) +
+         (size_t(std::max({tiles_.ntiles(), tiles_b_.ntiles(), init_tiles_.ntiles(), tiles1_.ntiles()})) * 5 + kReduceWsDoubles) * sizeof(double) +
          (own_arena_ ? layout_.bytes : 0);
 }
 
@@ -221,14 +241,17 @@ void GpuSubdomainSolver::after_launch(hipStream_t s) const {
 template <typename T>
 void GpuSubdomainSolver::init_impl(hipStream_t s) {
   HIP_CHECK(hipMemsetAsync(fields_, 0, 4 * field_bytes_, s));
+  if (r2_) HIP_CHECK(hipMemsetAsync(r2_, 0, field_bytes_, s));
   HIP_CHECK(hipMemsetAsync(arena_, 0, layout_.bytes, s));
   PcgState& st = host_state_[1];  // template (never rewritten while a copy is in flight)
   std::memset(&st, 0, sizeof(st));
   st.delta = spec_.delta;
   st.bd_tol = spec_.breakdown_tol;
-  st.it = 1;
+  st.it = pcg1_ ? 0 : 1;  // pcg1: sweep 0 below forms (z^0, r^0) and (A z^0, z^0)
   st.max_iter = spec_.effective_max_iter();
   st.norm = int(spec_.norm);
+  st.pair_w = opt_.pair_w ? 1 : 0;
+  st.pair_min_beta = opt_.pair_w == 2 ? HUGE_VAL : 1e-3;
   HIP_CHECK(hipMemcpyAsync(state_, &st, sizeof(PcgState), hipMemcpyHostToDevice, s));
   T* w = static_cast<T*>(field_base(0));
   T* r = static_cast<T*>(field_base(1));
@@ -236,6 +259,11 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
   after_launch(s);
   launch_reduce(partials_, init_tiles_.ntiles(), 2, 0.0, g_.h1h2, state_->red_b, state_, 0, reduce_ws_, s);
   after_launch(s);
+  if (pcg1_) {
+    phase_a_kernel_only<T>(s);
+    after_launch(s);
+    enqueue_reduce_a(s);  // it 0 -> 1
+  }
 }
 
 template <typename T>
@@ -246,7 +274,11 @@ void GpuSubdomainSolver::phase_a_impl(hipStream_t s) {
 
 template <typename T>
 void GpuSubdomainSolver::phase_a_kernel_only(hipStream_t s) {
-  if (tiles_.kind == 1)
+  if (pcg1_)
+    launch_pcg1<T>(geom_, tables_, static_cast<T*>(field_base(0)), static_cast<T*>(field_base(1)),
+                   reinterpret_cast<T*>(r2_ + field_off_ * elem_), static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), partials_, state_,
+                   tiles1_, s);
+  else if (tiles_.kind == 1)
     launch_pcg_a_wave<T>(geom_, tables_, static_cast<const T*>(field_base(1)),
                          static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(),
                          partials_, state_, tiles_, opt_.exact, s);
@@ -264,6 +296,7 @@ void GpuSubdomainSolver::phase_b_impl(hipStream_t s, bool pack) {
 
 template <typename T>
 void GpuSubdomainSolver::phase_b_kernel_only(hipStream_t s, bool pack) {
+  if (pcg1_) return;  // the single sweep ran in phase a
   // pcg_b reads G.nb only to pack the send buffers: clearing it skips the packing
   DevGeom G = geom_;
   if (!pack) G.nb = 0;
@@ -293,6 +326,14 @@ void GpuSubdomainSolver::enqueue_kernel_a(hipStream_t s) {
   after_launch(s);
 }
 void GpuSubdomainSolver::enqueue_reduce_a(hipStream_t s) {
+  if (pcg1_) {
+    const double h = g_.h1h2, wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
+    const double wts[5] = {h, h, h, h, wdiff};
+    launch_reduce_n(partials_, tiles1_.ntiles(), 5, wts, state_->red_c, state_, kSkipIfDone | kBumpIter,
+                    reduce_ws_, s);
+    after_launch(s);
+    return;
+  }
   launch_reduce(partials_, tiles_.ntiles(), 1, g_.h1h2, 0.0, state_->red_a, state_, kSkipIfDone,
                 reduce_ws_, s);
   after_launch(s);
@@ -303,6 +344,7 @@ void GpuSubdomainSolver::enqueue_kernel_b(hipStream_t s, bool pack) {
   after_launch(s);
 }
 void GpuSubdomainSolver::enqueue_reduce_b(hipStream_t s) {
+  if (pcg1_) return;
   const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
   launch_reduce(partials_, tiles_b_.ntiles(), 2, wdiff, g_.h1h2, state_->red_b, state_,
                 kSkipIfDone | kBumpIter, reduce_ws_, s);
@@ -336,7 +378,8 @@ void GpuSubdomainSolver::save_checkpoint(std::ostream& os, hipStream_t s) const 
   HIP_CHECK(hipStreamSynchronize(s));
   CkptHeader h{};
   std::memcpy(h.magic, kCkptMagic, 8);
-  h.version = 1; h.M = spec_.M; h.N = spec_.N; h.gi0 = sd_.gi0(); h.gj0 = sd_.gj0();
+  h.version = pcg1_ ? 2 : 1;  // v2: pcg1 state, r2 appended
+  h.M = spec_.M; h.N = spec_.N; h.gi0 = sd_.gi0(); h.gj0 = sd_.gj0();
   h.rank = sd_.rank; h.elem = int32_t(elem_); h.norm = int32_t(spec_.norm);
   h.nx = sd_.nx; h.ny = sd_.ny; h.pitch = geom_.pitch; h.field_bytes = int64_t(field_bytes_);
   h.arena_bytes = int64_t(layout_.bytes); h.max_iter = spec_.effective_max_iter(); h.delta = spec_.delta;
@@ -346,6 +389,10 @@ void GpuSubdomainSolver::save_checkpoint(std::ostream& os, hipStream_t s) const 
   os.write(buf.data(), std::streamsize(4 * field_bytes_));
   HIP_CHECK(hipMemcpy(buf.data(), arena_, layout_.bytes, hipMemcpyDeviceToHost));
   os.write(buf.data(), std::streamsize(layout_.bytes));
+  if (pcg1_) {
+    HIP_CHECK(hipMemcpy(buf.data(), r2_, field_bytes_, hipMemcpyDeviceToHost));
+    os.write(buf.data(), std::streamsize(field_bytes_));
+  }
   PMX_CHECK(os.good(), "checkpoint write failed");
 }
 
@@ -353,8 +400,9 @@ void GpuSubdomainSolver::load_checkpoint(std::istream& is, hipStream_t s) {
   HIP_CHECK(hipSetDevice(opt_.device));
   CkptHeader h{};
   is.read(reinterpret_cast<char*>(&h), sizeof(h));
-  PMX_CHECK(is.good() && std::memcmp(h.magic, kCkptMagic, 8) == 0 && h.version == 1,
-            "not a pmx checkpoint (v1)");
+  PMX_CHECK(is.good() && std::memcmp(h.magic, kCkptMagic, 8) == 0 &&
+                h.version == (pcg1_ ? 2 : 1),
+            "not a pmx checkpoint of this iteration algorithm (v1 pcg2, v2 pcg1)");
   PMX_CHECK(h.M == spec_.M && h.N == spec_.N && h.gi0 == sd_.gi0() && h.gj0 == sd_.gj0() &&
                 h.nx == sd_.nx && h.ny == sd_.ny && h.rank == sd_.rank,
             "checkpoint is for a different grid/decomposition (M=" << h.M << " N=" << h.N << " rank "
@@ -373,10 +421,15 @@ void GpuSubdomainSolver::load_checkpoint(std::istream& is, hipStream_t s) {
   is.read(buf.data(), std::streamsize(layout_.bytes));
   PMX_CHECK(is.good(), "truncated checkpoint (scalars/halos)");
   HIP_CHECK(hipMemcpy(arena_, buf.data(), layout_.bytes, hipMemcpyHostToDevice));
+  if (pcg1_) {
+    is.read(buf.data(), std::streamsize(field_bytes_));
+    PMX_CHECK(is.good(), "truncated checkpoint (pcg1 r2)");
+    HIP_CHECK(hipMemcpy(r2_, buf.data(), field_bytes_, hipMemcpyHostToDevice));
+  }
 }
 
 void GpuSubdomainSolver::enqueue_pack(hipStream_t s) {
-  if (geom_.nb == 0) return;
+  if (geom_.nb == 0 || pcg1_) return;
   if (opt_.dtype == DType::kFp64) pack_impl<double>(*this, halo<double>(), s);
   else pack_impl<float>(*this, halo<float>(), s);
   after_launch(s);
@@ -397,12 +450,16 @@ double GpuSubdomainSolver::bench_kernel(int which, int abl, int reps, hipStream_
   st.red_b[1] = 1e-3;
   st.zr[0] = st.zr[1] = 1e-3;
   st.alpha[0] = st.alpha[1] = 1.0;
+  st.red_c[0] = 1e-3;
+  st.red_c[1] = st.red_c[3] = st.red_c[4] = 1.0;
+  st.pair_w = opt_.pair_w ? 1 : 0;
+  st.pair_min_beta = opt_.pair_w == 2 ? HUGE_VAL : 1e-3;
   const TileCfg saved = tiles_, saved_b = tiles_b_;
   tiles_.abl = abl;
   tiles_b_.abl = abl;
   auto launch = [&]() {
     HIP_CHECK(hipMemcpyAsync(state_, &st, sizeof(PcgState), hipMemcpyHostToDevice, s));
-    if (which == 0) {
+    if (which == 0 || pcg1_) {
       if (opt_.dtype == DType::kFp64) phase_a_kernel_only<double>(s); else phase_a_kernel_only<float>(s);
     } else {
       if (opt_.dtype == DType::kFp64) phase_b_kernel_only<double>(s); else phase_b_kernel_only<float>(s);
@@ -418,7 +475,7 @@ double GpuSubdomainSolver::bench_kernel(int which, int abl, int reps, hipStream_
   for (int k = 0; k < reps; ++k) {
     HIP_CHECK(hipMemcpyAsync(state_, &st, sizeof(PcgState), hipMemcpyHostToDevice, s));
     HIP_CHECK(hipEventRecord(e0, s));
-    if (which == 0) {
+    if (which == 0 || pcg1_) {
       if (opt_.dtype == DType::kFp64) phase_a_kernel_only<double>(s); else phase_a_kernel_only<float>(s);
     } else {
       if (opt_.dtype == DType::kFp64) phase_b_kernel_only<double>(s); else phase_b_kernel_only<float>(s);

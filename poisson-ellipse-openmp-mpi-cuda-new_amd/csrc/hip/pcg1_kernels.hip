@@ -1,0 +1,433 @@
+// Single-pass PCG iteration ("pcg1"): ONE streaming kernel and ONE 5-value reduction per
+// iteration, instead of pcg_a + pcg_b with two reductions (pcg_kernels_dpp.hip).
+//
+// The reference iteration (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:847-943; stage0/
+// Withoutopenmp1.cpp:124-169) needs the global (A p^k, p^k) before it can update r, which is
+// what forces two sweeps.  pcg1 gets that denominator from the previous sweep instead:
+//   p^k = z^{k-1} + beta_k p^{k-1}
+//   (A p^k, p^k) = (A z, z) + 2 beta_k (A z, p^{k-1}) + beta_k^2 (A p^{k-1}, p^{k-1}),  z = z^{k-1}
+// so sweep k-1 also accumulates (A z^{k-1}, z^{k-1}) and (A z^{k-1}, p^{k-1}) next to (z, r) and
+// (A p, p).  Sweep k then has alpha_k before it starts and does everything in one pass:
+//   p^k = z + beta p;  A p^k (explicit 5-point stencil, not a recurrence);  r^k = r - alpha A p^k;
+//   z^k = D^-1 r^k;  A z^k;  partials (z^k, r^k), (A z^k, z^k), (A z^k, p^k), (A p^k, p^k), |p^k|^2.
+// r is updated with an explicitly computed A p^k exactly as in the reference, only alpha's
+// denominator is formed differently.  Measured in fp64 on the reference grids the
+// expanded denominator differs from the direct one by <= 1.4e-15 relative and every iteration
+// count is unchanged (15/26/50/546/989/1858), see profiles/NOTES_perf_experiments.md.
+//
+// Mapping (CDNA4): one wave64 marches a tile of TI rows x (64*VEC - 4) owned columns with a
+// 3-stage row pipeline (A: p^k of row m, B: A p^k / r^k / z^k of row m-1, C: A z^k of row m-2).
+// The dependency radius is 2 (A z^k needs z^k of the neighbours, which needs A p^k there), so a
+// tile loads 2 extra columns on each side (overlapped tiles: the edge lanes compute values that
+// only feed their neighbours, DPP lane shifts supply j +- 1) and marches 2 extra rows above and
+// below.  Loads are 2-column chunks (16 B in fp64), aligned because tiles start at even offsets.
+// w uses the paired update of k_pcg_b_rows_paired: odd iterations skip w, even ones apply
+// alpha_{k-1} p^{k-1} + alpha_k p^k, and p^{k-1} is the p_old this kernel reads anyway.
+// HBM traffic: r, p read + written (32 B) + w every other iteration (8 B) = 40 B/pt/iteration
+// (pcg_a + pcg_b: 56), one deterministic reduction and one all-reduce per iteration (pcg2: two).
+#include <cmath>
+
+#include "pcg_device.hpp"
+#include "pmx/common.hpp"
+#include "pmx/kernels.hpp"
+#include "pmx/spec.hpp"
+
+namespace pmx {
+
+using namespace dev;
+
+namespace {
+
+constexpr int kNq = 5;  // rho, (Az,z), (Az,p), (Ap,p), |p|^2
+
+// VEC columns from c0 (c0 - 1 even, so every 2-column chunk is 2-element aligned); chunks are
+// clamped to start <= cmax (cmax - 1 even, cmax + 1 inside the padded row).
+template <typename T, int VEC>
+__device__ __forceinline__ void load_cols(const T* row, int c0, int cmax, T (&out)[VEC]) {
+#pragma unroll
+  for (int q = 0; q < VEC / 2; ++q) {
+    T v[2];
+    vload_raw<T, 2>(row + min(c0 + 2 * q, cmax), v);
+    out[2 * q] = v[0];
+    out[2 * q + 1] = v[1];
+  }
+}
+
+template <typename T, int VEC>
+__device__ __forceinline__ void store_cols(T* row, int c0, const T (&in)[VEC], bool all,
+                                           const bool (&own)[VEC]) {
+  if (all) {
+#pragma unroll
+    for (int q = 0; q < VEC / 2; ++q) {
+      const T v[2] = {in[2 * q], in[2 * q + 1]};
+      vstore<T, 2>(row + c0 + 2 * q, v);
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < VEC; ++u)
+      if (own[u]) row[c0 + u] = in[u];
+  }
+}
+
+// One row of the tile: its scalar face constants and wave-uniform coefficient class.  The
+// per-column coefficients are rebuilt where they are used (class fast path, or the exact formula
+// on rows the ellipse cuts) instead of being carried through the pipeline in VGPRs.
+struct RowCo {
+  RowConst rc;
+  int ucls;
+  double uval;
+};
+
+__device__ __forceinline__ RowCo row_co(const DevTables& Tb, const DevGeom& G, int gi, int gjlo, int gjhi) {
+  RowCo c;
+  c.rc = load_row(Tb, gi);
+  c.ucls = row_class(c.rc, gjlo, gjhi);
+  c.uval = c.ucls == 1 ? 1.0 : G.inv_eps;
+  return c;
+}
+
+__device__ __forceinline__ void coef(const RowCo& c, const DevTables& Tb, const DevGeom& G, int gj,
+                                     double& a0, double& a1, double& b0, double& b1) {
+  if (c.ucls != 0) {
+    a0 = a1 = b0 = b1 = c.uval;
+  } else {
+    const ColConst cc = load_col(Tb, gj);
+    a0 = face_a0c(cc, c.rc, G);
+    a1 = face_a1c(cc, c.rc, G);
+    b0 = face_b0c(cc, c.rc, G);
+    b1 = face_b1c(cc, c.rc, G);
+  }
+}
+
+template <typename T, int VEC>
+struct Pcg1Row {
+  T r[VEC], p[VEC], w[VEC];
+};
+
+template <typename T, int VEC, bool EVEN>
+__device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb, T* __restrict__ w,
+                                           const T* __restrict__ rold, T* __restrict__ rnew,
+                                           const T* __restrict__ pold,
+                                           T* __restrict__ pnew, int i0, int i1, int j0, int j1,
+                                           double alpha, double beta, double alpha_prev,
+                                           double (&acc)[kNq]) {
+  const int64_t P = G.pitch;
+  const int lane = threadIdx.x & 63;
+  const int c0 = j0 - 2 + lane * VEC;
+  const int cmax = 1 + (G.ny / 2) * 2;
+  bool colin[VEC], own[VEC];
+  int gj[VEC];
+#pragma unroll
+  for (int u = 0; u < VEC; ++u) {
+    const int c = c0 + u;
+    colin[u] = c >= 1 && c <= G.ny;
+    own[u] = c >= j0 && c <= j1;
+    gj[u] = G.gj0 + min(max(c, 0), G.ny + 1);
+  }
+  const bool own_all = own[0] && own[VEC - 1];
+  bool own_any = false;
+#pragma unroll
+  for (int u = 0; u < VEC; ++u) own_any |= own[u];
+  const int gjlo = G.gj0 + max(j0 - 2, 0), gjhi = G.gj0 + min(j0 - 2 + 64 * VEC - 1, G.ny + 1);
+
+  auto fetch = [&](int m, Pcg1Row<T, VEC>& b) {
+    const int mc = min(max(m, 0), G.nx + 1);
+    load_cols<T, VEC>(rold + int64_t(mc) * P, c0, cmax, b.r);
+    load_cols<T, VEC>(pold + int64_t(mc) * P, c0, cmax, b.p);
+    if constexpr (EVEN) {  // w of the row stage B handles next step
+      const int wc = min(max(m - 1, 0), G.nx + 1);
+      load_cols<T, VEC>(w + int64_t(wc) * P, c0, cmax, b.w);
+    }
+  };
+
+  // pipeline registers
+  double Pm2[VEC], Pm1[VEC], Zm3[VEC], Zm2[VEC], ro1[VEC], po1[VEC];
+#pragma unroll
+  for (int u = 0; u < VEC; ++u) Pm2[u] = Pm1[u] = Zm3[u] = Zm2[u] = ro1[u] = po1[u] = 0.0;
+  RowCo cB = row_co(Tb, G, G.gi0 + min(max(i0 - 3, 0), G.nx + 1), gjlo, gjhi);  // rows m-1, m-2
+  RowCo cC = cB;
+
+  auto step = [&](int m, const Pcg1Row<T, VEC>& cur, Pcg1Row<T, VEC>& nxt) {
+    fetch(m + 1, nxt);  // unconditional (clamped): a branch around loads forces vmcnt(0)
+    // ---- stage A: p^k of row m
+    const bool rowA = m >= 1 && m <= G.nx;
+    const RowCo cA = row_co(Tb, G, G.gi0 + min(max(m, 0), G.nx + 1), gjlo, gjhi);
+    double Pm[VEC], rom[VEC], pom[VEC];
+#pragma unroll
+    for (int u = 0; u < VEC; ++u) {
+      const bool in = rowA && colin[u];
+      rom[u] = in ? double(cur.r[u]) : 0.0;
+      pom[u] = in ? double(cur.p[u]) : 0.0;
+      double a0, a1, b0, b1;
+      coef(cA, Tb, G, gj[u], a0, a1, b0, b1);
+      const double z = zdiv_u<false>(cA.ucls, rom[u], a0, a1, b0, b1, G);
+      const double v = __builtin_fma(beta, pom[u], z);
+      Pm[u] = in ? double(static_cast<T>(v)) : 0.0;  // the stored (rounded) p^k is the one used
+    }
+    // ---- stage B: A p^k, r^k, z^k of row m-1 (j neighbours by DPP; edge lanes get 0, their
+    // results only feed columns that are not owned)
+    const int mb = m - 1;
+    const bool rowB = mb >= 1 && mb <= G.nx;
+    const bool ownB = mb >= i0 && mb <= i1;
+    double Zm1[VEC];
+    T rs[VEC], ps[VEC], ws[VEC];
+    {
+      const double left = dpp_shift_f64<kWaveShr1>(Pm1[VEC - 1], 0.0);
+      const double right = dpp_shift_f64<kWaveShl1>(Pm1[0], 0.0);
+#pragma unroll
+      for (int u = 0; u < VEC; ++u) {
+        double a0, a1, b0, b1;
+        coef(cB, Tb, G, gj[u], a0, a1, b0, b1);
+        const double xjm = u == 0 ? left : Pm1[u - 1];
+        const double xjp = u == VEC - 1 ? right : Pm1[u + 1];
+        const double Ap = apply_a<false>(Pm1[u], Pm2[u], Pm[u], xjm, xjp, a0, a1, b0, b1, G);
+        const bool in = rowB && colin[u];
+        const double rn = double(static_cast<T>(upd_r<false>(ro1[u], alpha, Ap)));
+        rs[u] = static_cast<T>(in ? rn : 0.0);
+        const double zn = zdiv_u<false>(cB.ucls, rn, a0, a1, b0, b1, G);
+        Zm1[u] = in ? zn : 0.0;
+        ps[u] = static_cast<T>(Pm1[u]);
+        if constexpr (EVEN)
+          ws[u] = static_cast<T>(__builtin_fma(alpha, Pm1[u], __builtin_fma(alpha_prev, po1[u], double(cur.w[u]))));
+        if (ownB && own[u]) {
+          acc[0] += Zm1[u] * rn;
+          acc[3] += Ap * Pm1[u];
+          acc[4] += Pm1[u] * Pm1[u];
+        }
+      }
+    }
+    if (ownB && own_any) {
+      const int64_t o = int64_t(mb) * P;
+      store_cols<T, VEC>(rnew + o, c0, rs, own_all, own);
+      store_cols<T, VEC>(pnew + o, c0, ps, own_all, own);
+      if constexpr (EVEN) store_cols<T, VEC>(w + o, c0, ws, own_all, own);
+    }
+    // ---- stage C: A z^k of row m-2
+    const int mcr = m - 2;
+    if (mcr >= i0 && mcr <= i1) {
+      const double left = dpp_shift_f64<kWaveShr1>(Zm2[VEC - 1], 0.0);
+      const double right = dpp_shift_f64<kWaveShl1>(Zm2[0], 0.0);
+#pragma unroll
+      for (int u = 0; u < VEC; ++u) {
+        double a0, a1, b0, b1;
+        coef(cC, Tb, G, gj[u], a0, a1, b0, b1);
+        const double xjm = u == 0 ? left : Zm2[u - 1];
+        const double xjp = u == VEC - 1 ? right : Zm2[u + 1];
+        const double Az = apply_a<false>(Zm2[u], Zm3[u], Zm1[u], xjm, xjp, a0, a1, b0, b1, G);
+        if (own[u]) {
+          acc[1] += Az * Zm2[u];
+          acc[2] += Az * Pm2[u];
+        }
+      }
+    }
+    // ---- shift the pipeline
+#pragma unroll
+    for (int u = 0; u < VEC; ++u) {
+      Pm2[u] = Pm1[u]; Pm1[u] = Pm[u];
+      Zm3[u] = Zm2[u]; Zm2[u] = Zm1[u];
+      ro1[u] = rom[u]; po1[u] = pom[u];
+    }
+    cC = cB;
+    cB = cA;
+  };
+
+  Pcg1Row<T, VEC> buf[2];
+  const int mfirst = i0 - 2, mlast = i1 + 2;
+  fetch(mfirst, buf[0]);
+  // unrolled by the prefetch ring size: buf[0] / buf[1] are never copied
+  for (int m = mfirst; m <= mlast; m += 2) {
+    step(m, buf[0], buf[1]);
+    if (m + 1 > mlast) break;
+    step(m + 1, buf[1], buf[0]);
+  }
+}
+
+template <typename T, int VEC, int WAVES>
+__global__ void __launch_bounds__(64 * WAVES)
+k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
+       double* __restrict__ partials, PcgState* S, int TI, int tiles_j, int ntiles) {
+  constexpr int WO = 64 * VEC - 4;  // owned columns per tile
+  if (S->done) return;
+  const long long k = S->it;  // 0 = the init sweep (alpha = beta = 0: sums of r^0, z^0 only)
+  double alpha = 0.0, beta = 0.0, alpha_prev = 0.0;
+  if (k > 0) {
+    const double rho = S->red_c[0];  // rho_{k-1} = (z^{k-1}, r^{k-1})
+    double diff = 0.0;
+    if (k >= 2) {
+      // stop test of iteration k-1: ||w^k - w^{k-1}|| = |alpha_{k-1}| ||p^{k-1}||
+      diff = fabs(S->alpha[(k - 1) & 1]) * sqrt(S->red_c[4]);
+      const bool bad = !(diff == diff) || !(rho == rho);
+      if (bad || diff < S->delta || k > S->max_iter) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+          S->diff = diff;
+          S->iters = k - 1;
+          S->status = bad ? int(Status::kBreakdown)
+                          : (diff < S->delta ? int(Status::kConverged) : int(Status::kMaxIter));
+          if (bad) S->nan_flag = 1;
+          S->done = 1;
+        }
+        return;
+      }
+      beta = rho / S->zr[k & 1];  // rho_{k-2} sits in slot k & 1
+    }
+    const double denom = S->red_c[1] + beta * (2.0 * S->red_c[2] + beta * S->red_c[3]);
+    const bool bd = S->norm == int(Norm::kWeighted) ? fabs(denom) < S->bd_tol : denom < S->bd_tol;
+    if (bd || !(denom == denom)) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (k >= 2) S->diff = diff;
+        S->iters = k;
+        S->status = int(Status::kBreakdown);
+        if (!(denom == denom)) S->nan_flag = 1;
+        S->done = 1;
+      }
+      return;
+    }
+    alpha = rho / denom;
+    alpha_prev = S->alpha[(k - 1) & 1];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      S->zr[(k - 1) & 1] = rho;  // slot of k-1 (read as rho_{k-2} by the next sweep)
+      S->alpha[k & 1] = alpha;
+      if (k >= 2) S->diff = diff;
+      S->w_pend = (k & 1) ? k : 0;
+    }
+  }
+  const int id = xcd_remap(blockIdx.x, gridDim.x) * WAVES + __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  if (id >= ntiles) return;
+  const int ti = id / tiles_j, tj = id - ti * tiles_j;
+  const int i0 = 1 + ti * TI, i1 = min(i0 + TI - 1, G.nx);
+  const int j0 = 1 + tj * WO, j1 = min(j0 + WO - 1, G.ny);
+  T* pnew = (k & 1) ? p1 : p0;
+  const T* pold = (k & 1) ? p0 : p1;
+  const T* rold = (k & 1) ? r2 : r;
+  T* rnew = (k & 1) ? r : r2;
+  double acc[kNq] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  if (k > 0 && !(k & 1))
+    pcg1_march<T, VEC, true>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, alpha_prev, acc);
+  else
+    pcg1_march<T, VEC, false>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, alpha_prev, acc);
+  wave_sum2_mfma(acc[0], acc[1]);
+  wave_sum2_mfma(acc[2], acc[3]);
+  acc[4] = wave_sum_mfma(acc[4]);
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int q = 0; q < kNq; ++q) partials[int64_t(kNq) * id + q] = acc[q];
+  }
+}
+
+// Deterministic reduction of n partial vectors of NQ values (fixed chunk order, MFMA wave sums),
+// multi-block with a ticketed last-block finish like k_reduce (pcg_kernels.hip).
+struct ReduceWeights {
+  double w[8];
+};
+
+template <int NQ>
+__global__ void __launch_bounds__(256)
+k_reduce_n(const double* __restrict__ part, int n, ReduceWeights wt, double* out, PcgState* S,
+           int mode, double* chunk, unsigned* ticket) {
+  __shared__ double lds[NQ][256 / kWave];
+  __shared__ int last;
+  if ((mode & kSkipIfDone) && S->done) return;
+  const int nb = int(gridDim.x);
+  const int lo = int(int64_t(n) * blockIdx.x / nb);
+  const int hi = int(int64_t(n) * (blockIdx.x + 1) / nb);
+  double s[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) s[q] = 0.0;
+  for (int i = lo + int(threadIdx.x); i < hi; i += 256) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) s[q] += part[int64_t(i) * NQ + q];
+  }
+  const int wid = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    s[q] = wave_sum_mfma(s[q]);
+    if (lane == 0) lds[q][wid] = s[q];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) chunk[NQ * blockIdx.x + q] = (lds[q][0] + lds[q][1]) + (lds[q][2] + lds[q][3]);
+    __threadfence();
+    last = atomicAdd(ticket, 1u) == unsigned(nb - 1);
+  }
+  __syncthreads();
+  if (!last || threadIdx.x >= kWave) return;  // wave 0 of the last block finishes (full EXEC)
+  __threadfence();
+  const volatile double* c = chunk;
+  const int l = int(threadIdx.x);
+  double t[NQ];
+  bool bad = false;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    t[q] = wave_sum_mfma(l < nb ? c[NQ * l + q] : 0.0);
+    bad |= !(t[q] == t[q]) || isinf(t[q]);
+  }
+  if (l == 0) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) out[q] = t[q] * wt.w[q];
+    if (bad) S->nan_flag = 1;
+    if (mode & kBumpIter) S->it += 1;
+    *ticket = 0u;  // re-arm for the next launch (stream order makes this visible to it)
+  }
+}
+
+}  // namespace
+
+TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows) {
+  PMX_CHECK(vec == 2 || vec == 4, "pcg1: vec must be 2 or 4");
+  PMX_CHECK(waves == 1 || waves == 2 || waves == 4, "pcg1: waves must be 1, 2 or 4");
+  TileCfg t;
+  t.kind = 3;
+  t.vec = vec;
+  t.waves = waves;
+  t.block = 64 * vec - 4;  // owned columns per tile
+  t.tiles_j = (G.ny + t.block - 1) / t.block;
+  if (rows <= 0) {
+    // tall tiles keep the 4 extra marched rows cheap; shorter only when the grid is small
+    // (>= ~8K tiles keep 3 waves/SIMD busy for a few rounds)
+    rows = 64;
+    while (rows > 8 && int64_t((G.nx + rows - 1) / rows) * t.tiles_j < 8192) rows /= 2;
+  }
+  PMX_CHECK(rows >= 1 && rows <= 4096, "pcg1: tile rows must be in [1, 4096]");
+  t.rows = rows;
+  t.tiles_i = (G.nx + rows - 1) / rows;
+  return t;
+}
+
+template <typename T>
+void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1,
+                 double* partials, PcgState* S, const TileCfg& tc, hipStream_t s) {
+  PMX_CHECK(tc.kind == 3, "launch_pcg1 needs make_pcg1_tiles");
+  PMX_CHECK(G.nb == 0, "pcg1 runs on a subdomain without neighbours (use pcg2 for decompositions)");
+  const int nb = (tc.ntiles() + tc.waves - 1) / tc.waves;
+  const int bs = 64 * tc.waves;
+#define PMX_PCG1(V, WV) \
+  hipLaunchKernelGGL((k_pcg1<T, V, WV>), dim3(nb), dim3(bs), 0, s, G, Tb, w, r, r2, p0, p1, partials, S, tc.rows, tc.tiles_j, tc.ntiles())
+  if (tc.vec == 2 && tc.waves == 4) PMX_PCG1(2, 4);
+  else if (tc.vec == 2 && tc.waves == 2) PMX_PCG1(2, 2);
+  else if (tc.vec == 2 && tc.waves == 1) PMX_PCG1(2, 1);
+  else if (tc.vec == 4 && tc.waves == 4) PMX_PCG1(4, 4);
+  else if (tc.vec == 4 && tc.waves == 2) PMX_PCG1(4, 2);
+  else PMX_PCG1(4, 1);
+#undef PMX_PCG1
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_reduce_n(const double* partials, int n, int nq, const double* weights, double* out,
+                     PcgState* S, int mode, double* ws, hipStream_t s) {
+  PMX_CHECK(nq == kNq, "launch_reduce_n: nq must be " << kNq);
+  const int nb = std::max(1, std::min(kReduceMaxBlocks, n / 2048));
+  double* chunk = ws + kReduceNOffset;
+  unsigned* ticket = reinterpret_cast<unsigned*>(chunk + 8 * kReduceMaxBlocks);
+  ReduceWeights wt{};
+  for (int q = 0; q < nq; ++q) wt.w[q] = weights[q];
+  hipLaunchKernelGGL(k_reduce_n<kNq>, dim3(nb), dim3(256), 0, s, partials, n, wt, out, S, mode, chunk, ticket);
+  HIP_CHECK(hipGetLastError());
+}
+
+template void launch_pcg1<double>(const DevGeom&, const DevTables&, double*, double*, double*, double*,
+                                  double*, double*, PcgState*, const TileCfg&, hipStream_t);
+template void launch_pcg1<float>(const DevGeom&, const DevTables&, float*, float*, float*, float*, float*,
+                                 double*, PcgState*, const TileCfg&, hipStream_t);
+
+}  // namespace pmx

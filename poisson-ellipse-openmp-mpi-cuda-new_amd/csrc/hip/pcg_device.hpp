@@ -290,5 +290,66 @@ __device__ __forceinline__ Tile tile_of(int id, int tiles_j, int TI, int BLOCK, 
   return t;
 }
 
+// ---- wave-tile helpers (pcg_kernels_dpp.hip, pcg1_kernels.hip) -------------------------------
+// DPP wave shifts on a double: lane l receives lane l-1's (SHR) / l+1's (SHL) value; the edge lane
+// that has no source keeps `edge`.
+constexpr int kWaveShl1 = 0x130;
+constexpr int kWaveShr1 = 0x138;
+template <int CTRL>
+__device__ __forceinline__ float dpp_shift(float v, float edge) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(edge), __float_as_int(v), CTRL, 0xf,
+                                                    0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_shift_f64(double v, double edge);
+template <int CTRL>
+__device__ __forceinline__ double dpp_shift(double v, double edge) { return dpp_shift_f64<CTRL>(v, edge); }
+template <int CTRL>
+__device__ __forceinline__ double dpp_shift_f64(double v, double edge) {
+  const long long b = __double_as_longlong(v);
+  const long long e = __double_as_longlong(edge);
+  const int lo = __builtin_amdgcn_update_dpp(int(e), int(b), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(int(e >> 32), int(b >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double((long long)(unsigned)lo | ((long long)hi << 32));
+}
+
+template <typename T, int VEC> struct VecT;
+template <> struct VecT<double, 1> { using type = double; };
+template <> struct VecT<double, 2> { using type = double2; };
+template <> struct VecT<double, 4> { using type = double4; };
+template <> struct VecT<float, 1> { using type = float; };
+template <> struct VecT<float, 2> { using type = float2; };
+template <> struct VecT<float, 4> { using type = float4; };
+
+// Loads keep the storage type: prefetch rings hold raw T (half the VGPRs in fp32 storage mode)
+// and values are widened to fp64 where they are used.
+template <typename T, int VEC>
+__device__ __forceinline__ void vload_raw(const T* p, T (&out)[VEC]) {
+  using V = typename VecT<T, VEC>::type;
+  const V v = *reinterpret_cast<const V*>(p);
+  const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+  for (int u = 0; u < VEC; ++u) out[u] = e[u];
+}
+
+template <typename T, int VEC>
+__device__ __forceinline__ void vload(const T* p, double (&out)[VEC]) {
+  using V = typename VecT<T, VEC>::type;
+  const V v = *reinterpret_cast<const V*>(p);
+  const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+  for (int u = 0; u < VEC; ++u) out[u] = double(e[u]);
+}
+
+template <typename T, int VEC>
+__device__ __forceinline__ void vstore(T* p, const T (&in)[VEC]) {
+  using V = typename VecT<T, VEC>::type;
+  V v;
+  T* e = reinterpret_cast<T*>(&v);
+#pragma unroll
+  for (int u = 0; u < VEC; ++u) e[u] = in[u];
+  *reinterpret_cast<V*>(p) = v;
+}
+
 }  // namespace dev
 }  // namespace pmx

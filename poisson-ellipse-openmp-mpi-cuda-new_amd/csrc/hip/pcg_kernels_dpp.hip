@@ -27,66 +27,6 @@ namespace {
 constexpr int kMaxWaveRows = 256;
 
 
-// DPP wave shifts on a double: lane l receives lane l-1's (SHR) / l+1's (SHL) value; the edge lane
-// that has no source keeps `edge`.
-constexpr int kWaveShl1 = 0x130;
-constexpr int kWaveShr1 = 0x138;
-template <int CTRL>
-__device__ __forceinline__ float dpp_shift(float v, float edge) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(edge), __float_as_int(v), CTRL, 0xf,
-                                                    0xf, false));
-}
-template <int CTRL>
-__device__ __forceinline__ double dpp_shift_f64(double v, double edge);
-template <int CTRL>
-__device__ __forceinline__ double dpp_shift(double v, double edge) { return dpp_shift_f64<CTRL>(v, edge); }
-template <int CTRL>
-__device__ __forceinline__ double dpp_shift_f64(double v, double edge) {
-  const long long b = __double_as_longlong(v);
-  const long long e = __double_as_longlong(edge);
-  const int lo = __builtin_amdgcn_update_dpp(int(e), int(b), CTRL, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(int(e >> 32), int(b >> 32), CTRL, 0xf, 0xf, false);
-  return __longlong_as_double((long long)(unsigned)lo | ((long long)hi << 32));
-}
-
-template <typename T, int VEC> struct VecT;
-template <> struct VecT<double, 1> { using type = double; };
-template <> struct VecT<double, 2> { using type = double2; };
-template <> struct VecT<double, 4> { using type = double4; };
-template <> struct VecT<float, 1> { using type = float; };
-template <> struct VecT<float, 2> { using type = float2; };
-template <> struct VecT<float, 4> { using type = float4; };
-
-// Loads keep the storage type: prefetch rings hold raw T (half the VGPRs in fp32 storage mode)
-// and values are widened to fp64 where they are used.
-template <typename T, int VEC>
-__device__ __forceinline__ void vload_raw(const T* p, T (&out)[VEC]) {
-  using V = typename VecT<T, VEC>::type;
-  const V v = *reinterpret_cast<const V*>(p);
-  const T* e = reinterpret_cast<const T*>(&v);
-#pragma unroll
-  for (int u = 0; u < VEC; ++u) out[u] = e[u];
-}
-
-template <typename T, int VEC>
-__device__ __forceinline__ void vload(const T* p, double (&out)[VEC]) {
-  using V = typename VecT<T, VEC>::type;
-  const V v = *reinterpret_cast<const V*>(p);
-  const T* e = reinterpret_cast<const T*>(&v);
-#pragma unroll
-  for (int u = 0; u < VEC; ++u) out[u] = double(e[u]);
-}
-
-template <typename T, int VEC>
-__device__ __forceinline__ void vstore(T* p, const T (&in)[VEC]) {
-  using V = typename VecT<T, VEC>::type;
-  V v;
-  T* e = reinterpret_cast<T*>(&v);
-#pragma unroll
-  for (int u = 0; u < VEC; ++u) e[u] = in[u];
-  *reinterpret_cast<V*>(p) = v;
-}
-
 struct WaveTile {
   int i0, iend, j0, jend, id;
   bool live;
@@ -531,14 +471,14 @@ k_pcg_b_wave(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
 // p^{k-1} is not re-read: k_pcg_a formed p^k = z^{k-1} + beta_k p^{k-1}, and this kernel already
 // holds r^{k-1} (its input r), so p^{k-1} = (p^k - z^{k-1}) / beta_k and
 //   w^{k+1} = w^{k-1} + c1 p^k - c2 z^{k-1},  c2 = alpha_{k-1} / beta_k,  c1 = alpha_k + c2.
-// The recovery's rounding error is eps |p^k| / beta_k; for |beta_k| < kRecoverMinBeta the kernel
-// reads p^{k-1} from the other ping-pong buffer instead (still intact: k_pcg_a(k) only read it).
+// The recovery's rounding error is eps |p^k| / beta_k; for |beta_k| < S->pair_min_beta (1e-3) the
+// kernel reads p^{k-1} from the other ping-pong buffer instead (still intact: k_pcg_a(k) only
+// read it).  GpuOptions::pair_w = 0 launches the unpaired kernel (w updated every iteration).
 // Traffic per iteration pair: 40 + 24 B/pt instead of 2 x 40 (the iteration is 64 -> 56 B/pt).
 // ||w^{k+1} - w^k|| is computed as ||alpha_k p^k|| (the same quantity without the rounding of w).
 // Readers of w materialise a pending step (GpuSubdomainSolver::download_w).
 // ---------------------------------------------------------------------------
 enum BwMode : int { kBwEvery = 0, kBwPend = 1, kBwRecover = 2, kBwLoad = 3 };
-constexpr double kRecoverMinBeta = 1e-3;
 
 template <typename T, int VEC, bool EXACT, int MODE>
 __device__ __forceinline__ void pcg_b_rows_march(const DevGeom& G, const DevTables& Tb, T* __restrict__ w,
@@ -644,11 +584,11 @@ __device__ __forceinline__ void pcg_b_rows_march(const DevGeom& G, const DevTabl
   }
 }
 
-template <typename T, int VEC, int WAVES, bool EXACT>
-__global__ void __launch_bounds__(64 * WAVES)
-k_pcg_b_rows(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, const T* p0,
-             const T* p1, HaloBufs<T> H, double* __restrict__ partials, PcgState* S, int TI,
-             int tiles_j, int ntiles, int abl) {
+template <typename T, int VEC, int WAVES, bool EXACT, bool PAIRW>
+__device__ __forceinline__ void pcg_b_rows_body(const DevGeom& G, const DevTables& Tb, T* __restrict__ w,
+                                                T* __restrict__ r, const T* p0, const T* p1,
+                                                const HaloBufs<T>& H, double* __restrict__ partials,
+                                                PcgState* S, int TI, int tiles_j, int ntiles, int abl) {
   constexpr int W = 64 * VEC;
   if (S->done) return;
   const long long k = S->it;
@@ -667,10 +607,14 @@ k_pcg_b_rows(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
   // pairing: odd k defers its w step, even k applies two (slot k & 1 of alpha is written here and
   // slot (k - 1) & 1 only read, so no block can see a half-written value)
   const bool odd = k & 1;
-  const double alpha_prev = S->alpha[(k - 1) & 1];
-  const double beta = S->zr[(k - 1) & 1] / S->zr[k & 1];  // beta_k of k_pcg_a(k)
-  const bool recover = !odd && fabs(beta) >= kRecoverMinBeta;
-  if (!EXACT && blockIdx.x == 0 && threadIdx.x == 0) {
+  double alpha_prev = 0.0, beta = 0.0;
+  bool recover = false;
+  if constexpr (PAIRW) {
+    alpha_prev = S->alpha[(k - 1) & 1];
+    beta = S->zr[(k - 1) & 1] / S->zr[k & 1];  // beta_k of k_pcg_a(k)
+    recover = !odd && fabs(beta) >= S->pair_min_beta;
+  }
+  if (PAIRW && blockIdx.x == 0 && threadIdx.x == 0) {
     S->alpha[k & 1] = alpha;
     S->w_pend = odd ? k : 0;
   }
@@ -679,7 +623,7 @@ k_pcg_b_rows(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
   const T* __restrict__ pn = (k & 1) ? p1 : p0;
   const T* __restrict__ pprev = (k & 1) ? p0 : p1;
   double dacc = 0.0, zacc = 0.0;
-  if constexpr (EXACT) {
+  if constexpr (!PAIRW) {
     pcg_b_rows_march<T, VEC, EXACT, kBwEvery>(G, Tb, w, r, pn, pprev, H, t, alpha, 0.0, 0.0, dacc, zacc);
   } else if (odd) {
     pcg_b_rows_march<T, VEC, EXACT, kBwPend>(G, Tb, w, r, pn, pprev, H, t, alpha, 0.0, 0.0, dacc, zacc);
@@ -696,6 +640,25 @@ k_pcg_b_rows(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, cons
     partials[2 * t.id] = dacc;
     partials[2 * t.id + 1] = zacc;
   }
+}
+
+template <typename T, int VEC, int WAVES, bool EXACT>
+__global__ void __launch_bounds__(64 * WAVES)
+k_pcg_b_rows(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, const T* p0,
+             const T* p1, HaloBufs<T> H, double* __restrict__ partials, PcgState* S, int TI,
+             int tiles_j, int ntiles, int abl) {
+  pcg_b_rows_body<T, VEC, WAVES, EXACT, false>(G, Tb, w, r, p0, p1, H, partials, S, TI, tiles_j,
+                                               ntiles, abl);
+}
+
+template <typename T, int VEC, int WAVES, bool EXACT>
+__global__ void __launch_bounds__(64 * WAVES)
+k_pcg_b_rows_paired(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, const T* p0,
+                    const T* p1, HaloBufs<T> H, double* __restrict__ partials, PcgState* S, int TI,
+                    int tiles_j, int ntiles, int abl) {
+  static_assert(!EXACT, "exact mode keeps the reference's per-iteration w update");
+  pcg_b_rows_body<T, VEC, WAVES, false, true>(G, Tb, w, r, p0, p1, H, partials, S, TI, tiles_j,
+                                              ntiles, abl);
 }
 
 // ---------------------------------------------------------------------------
@@ -771,6 +734,9 @@ void launch_pcg_b_wave(const DevGeom& G, const DevTables& Tb, T* w, T* r, const 
   if (tc.kind == 2) {  // ring-free row kernel
     if (exact)
       PMX_WAVE_DISPATCH(tc, true, k_pcg_b_rows, G, Tb, w, r, p0, p1, H, partials, S, tc.rows,
+                        tc.tiles_j, tc.ntiles(), tc.abl);
+    else if (tc.pair_w)
+      PMX_WAVE_DISPATCH(tc, false, k_pcg_b_rows_paired, G, Tb, w, r, p0, p1, H, partials, S, tc.rows,
                         tc.tiles_j, tc.ntiles(), tc.abl);
     else
       PMX_WAVE_DISPATCH(tc, false, k_pcg_b_rows, G, Tb, w, r, p0, p1, H, partials, S, tc.rows,

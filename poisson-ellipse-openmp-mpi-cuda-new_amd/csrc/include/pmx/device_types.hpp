@@ -60,6 +60,11 @@ struct alignas(64) PcgState {
   // and the next (even) iteration applies both steps in one read-modify-write of w.
   double alpha[2];   // alpha_k at slot k & 1
   long long w_pend;  // k whose alpha_k p^k is not yet in w (0 = w is current); p^k is in p[k & 1]
+  double pair_min_beta;  // |beta_k| below which p^{k-1} is re-read instead of recovered
+  int pair_w;            // 0: w updated every iteration, 1: paired updates (GpuOptions::pair_w)
+  // Single-pass iteration (pcg1_kernels.hip): all-reduce buffer C = (z,r), (Az,z), (Az,p),
+  // (Ap,p) (weighted) and |p|^2 (weighted per norm) of the last sweep.
+  double red_c[5];
 };
 
 // Pointers for the halo ("ghost") exchange of r.  Side order: 0 x-lo, 1 x-hi, 2 y-lo, 3 y-hi.

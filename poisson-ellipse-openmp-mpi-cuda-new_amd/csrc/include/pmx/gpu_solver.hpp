@@ -59,6 +59,16 @@ struct GpuOptions {
   // ghost value that the exchange failed to deliver poisons the reductions and raises the
   // device NaN flag.  Also enabled by the environment variable PMX_POISON_HALOS=1.
   bool poison_halos = false;
+  // Paired w updates in the pcg_b row kernel (pcg_kernels_dpp.hip): 1 = on (default), 0 = w
+  // updated every iteration, 2 = paired but always re-reading p^{k-1} (no recovery; test and
+  // ablation).  The environment variable PMX_PAIR_W=0|1|2 overrides it.
+  int pair_w = 1;
+  // Iteration algorithm: 2 = pcg2 (k_pcg_a + k_pcg_b, two reductions), 1 = pcg1 (single-pass
+  // k_pcg1, one reduction; subdomains without neighbours), -1 = auto (pcg1 where it applies:
+  // wave kernels, not exact, no neighbours).  PMX_ALGO=1|2 overrides.  Default pcg2: pcg1 is
+  // experimental (its convergence test is not yet validated on the GPU).
+  int algo = 2;
+  int vec1 = 2, waves1 = 4, rows1 = 0;  // pcg1 tile shape (rows1 = 0: auto)
 };
 
 struct CommLayout {
@@ -123,7 +133,8 @@ class GpuSubdomainSolver {
   const GpuOptions& options() const { return opt_; }
   const DevGeom& geom() const { return geom_; }
   const DevTables& tables() const { return tables_; }
-  const TileCfg& tiles() const { return tiles_; }      // pcg_a
+  const TileCfg& tiles() const { return pcg1_ ? tiles1_ : tiles_; }  // pcg_a (or pcg1)
+  bool single_pass() const { return pcg1_; }
   const TileCfg& tiles_b() const { return tiles_b_; }  // pcg_b
   int device() const { return opt_.device; }
   size_t field_bytes() const { return field_bytes_; }
@@ -147,10 +158,13 @@ class GpuSubdomainSolver {
   DevTables tables_{};
   TileCfg tiles_{};    // pcg_a
   TileCfg tiles_b_{};  // pcg_b
+  TileCfg tiles1_{};   // pcg1
+  bool pcg1_ = false;
   TileCfg init_tiles_{};
   CommLayout layout_{};
   size_t elem_ = 8, field_bytes_ = 0, field_off_ = 0;
   char* fields_ = nullptr;  // 4 fields
+  char* r2_ = nullptr;      // pcg1 only: the second r buffer (r is double-buffered there)
   double* tables_buf_ = nullptr;
   double* partials_ = nullptr;
   double* reduce_ws_ = nullptr;  // k_reduce chunk sums + ticket (inside the partials allocation)

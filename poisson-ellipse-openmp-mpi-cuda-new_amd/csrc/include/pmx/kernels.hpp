@@ -20,11 +20,13 @@ struct TileCfg {
   int kind = 0;       // 0: workgroup tile + LDS row ring (pcg_kernels.hip)
                       // 1: wave tile + DPP lane shifts, software-pipelined register ring
                       // 2: wave tile + DPP lane shifts, ring-free short tiles (pcg_b only)
+                      // 3: single-pass pcg1 tiles (overlapped by 2 columns, 3-stage row pipeline)
   int block = 256;    // columns per tile (kind 0: = threads per block; kind 1: = 64*vec)
   int rows = 0;       // rows per tile (marching length); 0 = auto
   int vec = 1;        // kind 1: columns per lane
   int waves = 1;      // kind 1: independent wave tiles per workgroup
   int abl = 0;        // kernel-isolation ablation bits (kAbl*), 0 in production
+  int pair_w = 0;     // kind 2: paired w updates (k_pcg_b_rows_paired, pcg_kernels_dpp.hip)
   int tiles_i = 0, tiles_j = 0;
   int ntiles() const { return tiles_i * tiles_j; }
 };
@@ -35,6 +37,8 @@ TileCfg make_wave_tiles(const DevGeom& G, int vec, int waves, int rows, int max_
                         int target_tiles = 22000);
 // kind 2 tiles for k_pcg_b_rows (rows = 0: 2)
 TileCfg make_row_tiles(const DevGeom& G, int vec, int waves, int rows);
+// kind 3 tiles for k_pcg1: 64*vec - 4 owned columns, rows = 0: auto
+TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows);
 
 enum ReduceMode : int { kSkipIfDone = 1, kBumpIter = 2 };
 
@@ -69,6 +73,14 @@ void launch_pcg_b_wave(const DevGeom& G, const DevTables& Tb, T* w, T* r, const 
                        const T* p1, HaloBufs<T> H, double* partials, PcgState* S,
                        const TileCfg& tc, bool exact, hipStream_t s);
 
+// Single-pass PCG iteration (pcg1_kernels.hip): p^k, A p^k, w, r^k, z^k, A z^k in one sweep,
+// 5 partials per tile (rho, (Az,z), (Az,p), (Ap,p), |p|^2).  S->it == 0 is the init sweep.
+// Subdomains without neighbours only (G.nb == 0).  r is double-buffered (overlapped tiles read
+// neighbour rows/columns of r^{k-1} while others write r^k): sweep k reads (k & 1 ? r2 : r).
+template <typename T>
+void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1,
+                 double* partials, PcgState* S, const TileCfg& tc, hipStream_t s);
+
 // Halo/compute overlap: r^{k+1} on the subdomain edges that have a neighbour,
 // written to the send buffers only, with exactly the arithmetic of pcg_b.  Runs first so the
 // ghost exchange on the comm stream overlaps pcg_b, which then skips its own packing.
@@ -81,9 +93,14 @@ void launch_edge_r(const DevGeom& G, const DevTables& Tb, const T* r, const T* p
 // word starts zeroed; the kernel re-arms it.  One workspace per stream (launches on a workspace
 // must be stream-ordered).
 constexpr int kReduceMaxBlocks = 64;
-constexpr int kReduceWsDoubles = 2 * kReduceMaxBlocks + 2;
+// k_reduce: chunk sums [0, 2*64) + ticket; k_reduce_n: its own chunk sums + ticket after that
+constexpr int kReduceNOffset = 2 * kReduceMaxBlocks + 2;
+constexpr int kReduceWsDoubles = kReduceNOffset + 8 * kReduceMaxBlocks + 2;
 void launch_reduce(const double* partials, int n, int nq, double w0, double w1, double* out,
                    PcgState* S, int mode, double* ws, hipStream_t s);
+// the same for nq = 5 interleaved values (k_pcg1 partials), out[q] = sum_q * weights[q]
+void launch_reduce_n(const double* partials, int n, int nq, const double* weights, double* out,
+                     PcgState* S, int mode, double* ws, hipStream_t s);
 
 // Deterministic in-process "all-reduce" across P subdomains on one device (LocalComm):
 // out_k[q] = sum_r in_r[q] for every k, summed in rank order.

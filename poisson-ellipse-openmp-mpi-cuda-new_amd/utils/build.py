@@ -34,6 +34,7 @@ ARCH = os.environ.get("PMX_ARCH", "gfx950")
 HIP_SOURCES = [
     "hip/pcg_kernels.hip",
     "hip/pcg_kernels_dpp.hip",
+    "hip/pcg1_kernels.hip",
     "hip/ops_kernels.hip",
     "hip/gpu_solver.hip",
     "hip/session.hip",

@@ -73,3 +73,23 @@ def test_poisoned_halo_without_exchange_raises_nan_flag(pkg, native):
     s0.enqueue_phase_a(0)
     st = s0.read_state(0)
     assert st["nan"]
+
+
+def test_resume_with_pending_w_step_is_bitwise(pkg, tmp_path):
+    """A checkpoint taken after an odd iteration holds a deferred w step (paired w updates); the
+    resumed solve must apply it exactly like the uninterrupted one."""
+    models = sub("models")
+    p = pkg.PoissonEllipse(M=400, N=600)
+    path = str(tmp_path / "ck.bin")
+    ref = models.make_session(p)
+    rr = ref.solve_checkpointed(str(tmp_path / "unused.bin"), every=0)
+    a = models.make_session(p, graph_batch=0)
+    a.init()
+    a.step(7)
+    a.synchronize()
+    assert a.state()["w_pend"] == 7
+    a.save_checkpoint(path)
+    b = models.make_session(p)
+    rb = b.solve_checkpointed(path, every=0, resume=True)
+    assert rb["iters"] == rr["iters"] == 546
+    assert np.array_equal(b.gather_local_w(), ref.gather_local_w())

@@ -203,3 +203,41 @@ def test_breakdown_tolerance_parameter_gpu(pkg, kernel):
     r = pkg.solve(pkg.PoissonEllipse(M=40, N=40, breakdown_tol=1e3), "hip", kernel=kernel)
     assert r.status == "breakdown" and r.iters == 1
     assert pkg.solve(pkg.PoissonEllipse(M=40, N=40, breakdown_tol=0.0), "hip", kernel=kernel).iters == 50
+
+
+@pytest.mark.parametrize("grid,iters", [((400, 600), 546), ((800, 1200), 989), ((97, 130), None)])
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+def test_paired_w_modes(pkg, monkeypatch, grid, iters, dtype):
+    """Paired w updates (k_pcg_b_rows): odd iterations defer alpha_k p^k, even ones apply two steps
+    with p^{k-1} recovered (mode 1) or re-read (mode 2).  Both match w updated every iteration
+    (mode 0) -- stops on even (546) and odd (989) iterations included."""
+    p = pkg.PoissonEllipse(M=grid[0], N=grid[1])
+    res = {}
+    for mode in (0, 1, 2):
+        monkeypatch.setenv("PMX_PAIR_W", str(mode))
+        res[mode] = pkg.solve(p, "hip", dtype=dtype)
+    tol = 1e-12 if dtype == "fp64" else 2e-6
+    for mode in (1, 2):
+        if dtype == "fp64":
+            assert res[mode].iters == res[0].iters
+        assert np.abs(res[mode].w - res[0].w).max() < tol
+    if iters is not None and dtype == "fp64":
+        assert res[1].iters == iters
+
+
+@pytest.mark.parametrize("steps", [7, 8])
+def test_paired_w_midrun_materialised(pkg, monkeypatch, steps):
+    """w read after an odd number of iterations includes the deferred step."""
+    p = pkg.PoissonEllipse(M=300, N=200)
+    models = sub("models")
+    out = {}
+    for mode in (0, 1):
+        monkeypatch.setenv("PMX_PAIR_W", str(mode))
+        s = models.make_session(p, ranks=2, graph_batch=0)
+        s.init()
+        s.step(steps)
+        s.synchronize()
+        st = s.state()
+        assert st["w_pend"] == (steps if (mode == 1 and steps % 2) else 0)
+        out[mode] = s.gather_local_w()
+    assert np.abs(out[1] - out[0]).max() < 1e-14
