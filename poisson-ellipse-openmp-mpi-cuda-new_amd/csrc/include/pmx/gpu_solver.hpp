@@ -65,10 +65,13 @@ struct GpuOptions {
   int pair_w = 1;
   // Iteration algorithm: 2 = pcg2 (k_pcg_a + k_pcg_b, two reductions), 1 = pcg1 (single-pass
   // k_pcg1, one reduction; subdomains without neighbours), -1 = auto (pcg1 where it applies:
-  // wave kernels, not exact, no neighbours).  PMX_ALGO=1|2 overrides.  Default pcg2: pcg1 is
-  // experimental (its convergence test is not yet validated on the GPU).
-  int algo = 2;
-  int vec1 = 2, waves1 = 4, rows1 = 0;  // pcg1 tile shape (rows1 = 0: auto)
+  // wave kernels, not exact, no neighbours).  PMX_ALGO=-1|1|2 overrides.  Default auto: pcg1
+  // matches the reference iteration counts and pcg2's solution on the GPU (tests/test_gpu_pcg1.py)
+  // and is 5-11% faster on one GPU (profiles/NOTES_perf_experiments.md #22).
+  int algo = -1;
+  // pcg1 tile shape (rows1 = 0: auto).  VEC=2 x 2 waves/workgroup won the 16384^2 sweep
+  // (bench/gpu_pcg1_sweep.sh; VEC=4 needs 256 VGPRs and is 35% slower).
+  int vec1 = 2, waves1 = 2, rows1 = 0;
 };
 
 struct CommLayout {
