@@ -243,7 +243,10 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
 }
 
 template <typename T, int VEC, int WAVES>
-__global__ void __launch_bounds__(64 * WAVES)
+#ifndef PMX_PCG1_MIN_WAVES
+#define PMX_PCG1_MIN_WAVES 1
+#endif
+__global__ void __launch_bounds__(64 * WAVES, PMX_PCG1_MIN_WAVES)
 k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
        double* __restrict__ partials, PcgState* S, int TI, int tiles_j, int ntiles) {
   constexpr int WO = 64 * VEC - 4;  // owned columns per tile

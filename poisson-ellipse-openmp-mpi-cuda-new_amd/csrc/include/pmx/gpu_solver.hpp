@@ -69,9 +69,9 @@ struct GpuOptions {
   // matches the reference iteration counts and pcg2's solution on the GPU (tests/test_gpu_pcg1.py)
   // and is 5-11% faster on one GPU (profiles/NOTES_perf_experiments.md #22).
   int algo = -1;
-  // pcg1 tile shape (rows1 = 0: auto).  VEC=2 x 2 waves/workgroup won the 16384^2 sweep
+  // pcg1 tile shape (rows1 = 0: auto).  VEC=2 x 1 wave/workgroup won the 16384^2 sweeps
   // (bench/gpu_pcg1_sweep.sh; VEC=4 needs 256 VGPRs and is 35% slower).
-  int vec1 = 2, waves1 = 2, rows1 = 0;
+  int vec1 = 2, waves1 = 1, rows1 = 0;
 };
 
 struct CommLayout {
