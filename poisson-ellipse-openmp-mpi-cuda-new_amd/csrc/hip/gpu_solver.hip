@@ -161,7 +161,9 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
   const bool pcg1_ok = G.nb == 0 && !opt.exact && opt.kernel == 1;
   PMX_CHECK(opt_.algo != 1 || pcg1_ok,
             "pcg1 needs the wave kernels, the fast arithmetic and a subdomain without neighbours");
-  pcg1_ = opt_.algo == 1 || (opt_.algo == -1 && pcg1_ok);
+  // auto picks pcg1 in fp64 only: with fp32 storage the stream halves and pcg1's second stencil
+  // makes it compute-bound (32768^2 fp32: pcg1 8.99 ms vs pcg2 7.69 ms per iteration)
+  pcg1_ = opt_.algo == 1 || (opt_.algo == -1 && pcg1_ok && opt.dtype == DType::kFp64);
   if (pcg1_) {
     tiles1_ = make_pcg1_tiles(G, opt_.vec1, opt_.waves1, opt_.rows1);
     HIP_CHECK(hipMalloc(&r2_, field_bytes_));

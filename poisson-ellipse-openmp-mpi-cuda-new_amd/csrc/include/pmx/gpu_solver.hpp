@@ -65,7 +65,7 @@ struct GpuOptions {
   int pair_w = 1;
   // Iteration algorithm: 2 = pcg2 (k_pcg_a + k_pcg_b, two reductions), 1 = pcg1 (single-pass
   // k_pcg1, one reduction; subdomains without neighbours), -1 = auto (pcg1 where it applies:
-  // wave kernels, not exact, no neighbours).  PMX_ALGO=-1|1|2 overrides.  Default auto: pcg1
+  // wave kernels, not exact, no neighbours, fp64 storage).  PMX_ALGO=-1|1|2 overrides.  Default auto: pcg1
   // matches the reference iteration counts and pcg2's solution on the GPU (tests/test_gpu_pcg1.py)
   // and is 5-11% faster on one GPU (profiles/NOTES_perf_experiments.md #22).
   int algo = -1;

@@ -45,3 +45,16 @@ def test_pcg1_matches_cpu_oracle(pkg, monkeypatch):
     ref = pkg.solve(p, "cpu")
     assert one.iters == ref.iters
     assert np.abs(one.w - ref.w).max() < 1e-10
+
+
+@pytest.mark.parametrize("ranks,kw,algo", [
+    (1, {}, "pcg1"),                  # fp64, one subdomain: single pass
+    (1, {"dtype": "fp32"}, "pcg2"),   # fp32 storage: pcg2 is faster (NOTES #26)
+    (1, {"exact": True}, "pcg2"),     # reference arithmetic order
+    (2, {}, "pcg2"),                  # subdomains with neighbours
+])
+def test_auto_algorithm_selection(pkg, monkeypatch, ranks, kw, algo):
+    monkeypatch.delenv("PMX_ALGO", raising=False)
+    from conftest import sub
+    s = sub("models").make_session(pkg.PoissonEllipse(M=200, N=300), ranks=ranks, **kw)
+    assert s.tile["algo"] == algo
