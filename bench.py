@@ -9,8 +9,13 @@ MLUPS = (M-1)(N-1) * steps / time / 1e6, whole-job aggregate.  The grid is fixed
 x^2 + 4y^2 < 1, zero initial guess (there is no dataset).
 
     python bench.py --gpus 1 --steps 200 --warmup 20
+    python bench.py --gpus 8                  # spawns 8 ranks itself (one per GPU)
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29500 bench.py --gpus 8 --steps 200 --warmup 20
+
+Without a launcher (no WORLD_SIZE in the environment) and --gpus N > 1, this process starts the N
+ranks itself -- before anything touches the GPU -- and exits with their status.  A run whose rank
+count differs from --gpus fails; it never measures fewer GPUs than it reports.
 
 After the timed region a full solve to ||w^{k+1}-w^k|| < 1e-6 reports iters-to-tol and the
 accuracy against the analytic solution (disable with --no-tol-solve).
@@ -61,11 +66,59 @@ def parse():
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="test the launch/timing/reporting flow on CPU (gloo, plain-PyTorch PCG); "
                          "prints a JSON line marked data=cpu-dry-run, not a measurement")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal: all ranks on GPU 0, native kernels, gloo comm staged through host "
+                         "memory (valid=false: not a multi-GPU measurement)")
+    ap.add_argument("--rccl-graph", default="on", choices=["on", "off"],
+                    help="multi-rank native path: capture the RCCL calls into the hipGraph batches")
+    ap.add_argument("--profile-phases", type=int, default=0,
+                    help="after the run: N eager iterations timed per phase, MAX over ranks, printed as "
+                         "the reference's stage-4 buckets on stderr and added to the JSON line")
     return ap.parse_args()
+
+
+def spawn_ranks(n: int) -> int:
+    """Start n ranks of this script (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set) and return their
+    status.  Runs before any GPU call in this process; a failing rank stops the others."""
+    import signal
+    import socket
+    import subprocess
+
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PMX_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc, failed_at = 0, None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad and failed_at is None:
+            rc, failed_at = bad[0], time.time()
+            print(f"[bench] a rank exited with status {rc}; stopping the others", file=sys.stderr, flush=True)
+            for p in procs:
+                if p.poll() is None:
+                    p.send_signal(signal.SIGTERM)
+        if all(c is not None for c in codes):
+            break
+        if failed_at is not None and time.time() - failed_at > 20:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        time.sleep(0.2)
+    return rc or max(p.returncode for p in procs)
 
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     import importlib
 
     import torch
@@ -75,15 +128,21 @@ def main():
     from importlib import import_module
 
     launch = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.parallel.launch")
+    ds = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.parallel.dist_solver")
     dry = args.cpu_dry_run
-    info = launch.init_distributed(device_type="cpu" if dry else None)
+    share = args.share_gpu and not dry
+    info = launch.init_distributed(device_type="cpu" if (dry or share) else None)
     world = info.world
     if world != args.gpus:
-        print(f"[bench] warning: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+        raise SystemExit(f"[bench] --gpus {args.gpus} but {world} rank(s) came up (WORLD_SIZE); refusing to "
+                         "report a different GPU count")
+    device = 0 if share else info.local_rank
     if not dry:
         if not torch.cuda.is_available():
             raise SystemExit("bench.py needs an MI355X (no HIP device visible)")
-        torch.cuda.set_device(info.local_rank)
+        if not share and torch.cuda.device_count() < world:
+            raise SystemExit(f"[bench] {world} ranks need {world} visible GPUs, found {torch.cuda.device_count()}")
+        torch.cuda.set_device(device)
 
     def device_sync():
         if not dry:
@@ -118,18 +177,28 @@ def main():
             def state():
                 return sess.state(0)
 
+            @staticmethod
+            def profile(n):
+                sess.init()
+                ph = sess.profile(int(n))
+                return {"compute": ph["t_kernel_a"] + ph["t_kernel_b"], "copy": 0.0, "comm": ph["t_comm"],
+                        "precond": 0.0, "dot": ph["t_reduce"]}
+
         runner = Runner()
         comm_used = "self"
     else:
-        ds = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.parallel.dist_solver")
-        try:
-            runner = ds.DistGpuPCG(problem, info, comm=args.comm, rccl_graph=False, **kw)
-        except Exception as e:  # native RCCL bootstrap failed -> portable torch.distributed path
-            if args.comm != "native":
-                raise
-            print(f"[bench] native RCCL comm failed ({e}); falling back to torch.distributed", file=sys.stderr)
-            runner = ds.DistGpuPCG(problem, info, comm="torch", **kw)
-            comm_used = "torch"
+        if share:
+            runner = ds.DistGpuPCG(problem, info, comm="torch", device=0, **kw)
+            comm_used = "gloo-host-staged"
+        else:
+            try:  # setup and RCCL init are agreed collectively: every rank raises, or none does
+                runner = ds.DistGpuPCG(problem, info, comm=args.comm, rccl_graph=args.rccl_graph == "on", **kw)
+            except RuntimeError as e:  # native RCCL bootstrap failed -> portable torch.distributed path
+                if args.comm != "native":
+                    raise
+                print(f"[bench] native RCCL comm failed ({e}); falling back to torch.distributed", file=sys.stderr)
+                runner = ds.DistGpuPCG(problem, info, comm="torch", **kw)
+                comm_used = "torch"
 
     def barrier():
         if world > 1:
@@ -151,7 +220,7 @@ def main():
     dt = t1 - t0
     st1 = runner.state()
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cpu" if dry else "cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device="cpu" if (dry or share) else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     tile_desc = runner.tile() if hasattr(runner, "tile") else dict(rows=args.tile_rows, vec=args.vec)
@@ -177,7 +246,7 @@ def main():
             if not stop and time.perf_counter() - ts > args.tol_time_cap:
                 stop = 1
             if world > 1:  # one decision for all ranks: a rank that stops alone would hang the rest
-                flag = torch.tensor([stop], dtype=torch.int32, device="cpu" if dry else "cuda")
+                flag = torch.tensor([stop], dtype=torch.int32, device="cpu" if (dry or share) else "cuda")
                 dist.all_reduce(flag, op=dist.ReduceOp.MAX)
                 stop = int(flag.item())
             if stop:
@@ -190,6 +259,14 @@ def main():
                    tol_final_diff=st["diff"], tol_solve_seconds=round(tsolve, 4),
                    tol_solve_mlups=round(pts * (st["iters"] if st["done"] else st["it"]) / tsolve / 1e6, 1),
                    tol_time_capped=capped)
+
+    phases = {}
+    if args.profile_phases > 0 and not dry and hasattr(runner, "profile"):
+        ph = runner.profile(args.profile_phases)
+        phases = {"phase_seconds_per_iter_max_over_ranks": {k: v / args.profile_phases for k, v in ph.items()}}
+        if info.rank == 0:
+            print(f"[bench] {args.profile_phases} profiled iterations (MAX over {world} ranks):\n"
+                  + ds.phase_table(ph), file=sys.stderr, flush=True)
 
     if info.rank == 0:
         out = {
@@ -205,7 +282,8 @@ def main():
             "vs_baseline": round(mlups / BASELINE_MLUPS, 2),
             "dtype": args.dtype,
             "data": "cpu-dry-run (plain-PyTorch PCG on CPU: flow test, not a measurement)" if dry else
-                    "synthetic (reference problem: F=1 in ellipse x^2+4y^2<1, zero initial guess)",
+                    ("share-gpu rehearsal (all ranks on one GPU, gloo host-staged comm: not a measurement)"
+                     if share else "synthetic (reference problem: F=1 in ellipse x^2+4y^2<1, zero initial guess)"),
             "config": {
                 "model": f"fictitious-domain Poisson ellipse, Jacobi-PCG, {args.M}x{args.N}",
                 "global_batch": 1,
@@ -219,9 +297,10 @@ def main():
                 "overlap": args.overlap,
                 "exact": args.exact,
             },
-            "valid": valid,
+            "valid": valid and not share,
             "baseline_mlups": BASELINE_MLUPS,
             **tol,
+            **phases,
         }
         line = json.dumps(out)
         print(line, flush=True)

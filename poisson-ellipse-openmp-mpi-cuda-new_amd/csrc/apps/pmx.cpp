@@ -245,10 +245,13 @@ int run_plan(const Cli& c) {
   std::cout << "plan: M=" << s.M << ", N=" << s.N << ", " << ranks << " subdomain(s) as " << pg.Px << " x "
             << pg.Py << ", dtype " << (c.opt.dtype == DType::kFp64 ? "fp64" : "fp32") << "\n"
             << "memory: " << dev_src << "\n";
+  const int subs_per_device = c.gpus > 1 ? 1 : ranks;  // LocalComm: every subdomain on one device
+  const bool single_pass = choose_single_pass(s, pg, resolve_options(c.opt), dev_bytes, subs_per_device);
+  std::cout << "iteration: " << (single_pass ? "pcg1 (single pass, 5 fields)" : "pcg2 (two sweeps, 4 fields)") << "\n";
   size_t worst = 0;
   for (int r = 0; r < ranks; ++r) {
     const Subdomain sd = decompose_2d(s.M, s.N, pg, r);
-    const size_t b = GpuSubdomainSolver::estimate_device_bytes(s, sd, c.opt.dtype);
+    const size_t b = GpuSubdomainSolver::estimate_device_bytes(s, sd, c.opt.dtype, single_pass);
     worst = std::max(worst, b);
     std::cout << "  rank " << r << ": " << sd.nx << " x " << sd.ny << " nodes, ~" << b / 1e9 << " GB\n";
   }

@@ -85,15 +85,28 @@ py::dict stats_dict(const RunStats& r) {
 
 py::dict layout_dict(const CommLayout& L) {
   py::dict d;
+  py::list so, ro, el, pe;
+  for (int s = 0; s < kHaloSlots; ++s) {
+    so.append(L.send_off[s]);
+    ro.append(L.recv_off[s]);
+    el.append(L.edge_len[s]);
+    pe.append(L.peer[s]);
+  }
   d["state_off"] = L.state_off;
-  d["send_off"] = py::make_tuple(L.send_off[0], L.send_off[1], L.send_off[2], L.send_off[3]);
-  d["recv_off"] = py::make_tuple(L.recv_off[0], L.recv_off[1], L.recv_off[2], L.recv_off[3]);
-  d["edge_len"] = py::make_tuple(L.edge_len[0], L.edge_len[1], L.edge_len[2], L.edge_len[3]);
+  d["send_off"] = py::tuple(so);
+  d["recv_off"] = py::tuple(ro);
+  d["edge_len"] = py::tuple(el);
+  d["peer"] = py::tuple(pe);  // rank across each slot (-1: none); slot s pairs with opposite_slot(s)
+  d["opposite"] = py::make_tuple(opposite_slot(0), opposite_slot(1), opposite_slot(2), opposite_slot(3),
+                                 opposite_slot(4), opposite_slot(5), opposite_slot(6), opposite_slot(7));
   d["elem"] = L.elem;
   d["bytes"] = L.bytes;
+  d["single_pass"] = L.single_pass;
+  d["algo"] = L.single_pass ? "pcg1" : "pcg2";
   d["state_bytes"] = sizeof(PcgState);
   d["red_a_off"] = offsetof(PcgState, red_a);
   d["red_b_off"] = offsetof(PcgState, red_b);
+  d["red_c_off"] = offsetof(PcgState, red_c);
   return d;
 }
 
@@ -156,8 +169,9 @@ class OpContext {
 GpuOptions make_options(int device, const std::string& kernel, int block, int vec, int waves,
                         int tile_rows, const std::string& dtype, bool exact, int graph_batch, bool check,
                         bool overlap = true, int vec_b = 0, int waves_b = 0, int tile_rows_b = -1,
-                        bool poison_halos = false, bool b_ring = false) {
+                        bool poison_halos = false, bool b_ring = false, int algo = -1) {
   GpuOptions o;
+  o.algo = algo;
   o.device = device;
   PMX_CHECK(kernel == "lds" || kernel == "wave", "kernel must be lds or wave, got " << kernel);
   o.kernel = kernel == "lds" ? 0 : 1;
@@ -262,10 +276,27 @@ PYBIND11_MODULE(_pmx, m) {
     else launch_wave_sums<double>(reinterpret_cast<const double*>(x), reinterpret_cast<double*>(out), nwaves, as_stream(stream));
   }, py::arg("x"), py::arg("out"), py::arg("nwaves"), py::arg("fp32") = false, py::arg("stream") = 0);
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
-  m.def("comm_layout", [](int M, int N, int Px, int Py, int rank, const std::string& dtype) {
-    const Subdomain sd = decompose_2d(M, N, ProcGrid{Px, Py}, rank);
-    return layout_dict(GpuSubdomainSolver::comm_layout(sd, dtype == "fp64" ? DType::kFp64 : DType::kFp32));
-  });
+  // Arena layout for a Python-orchestrated solver (DistGpuPCG comm="torch").  The iteration
+  // algorithm is resolved exactly as the solver will (options + environment + device size), so
+  // pass the returned "algo" on to SubdomainSolver(algo=...).
+  m.def("comm_layout", [](const ProblemSpec& s, int Px, int Py, int rank, const std::string& dtype,
+                          const std::string& kernel, bool exact, int device, int algo) {
+          GpuOptions o = make_options(device, kernel, 256, 0, 4, 0, dtype, exact, 0, false);
+          o.algo = algo;
+          o = resolve_options(o);
+          double total = 0.0;
+          if (o.algo == -1) {
+            HIP_CHECK(hipSetDevice(device));
+            size_t fb = 0, tb = 0;
+            HIP_CHECK(hipMemGetInfo(&fb, &tb));
+            total = double(tb);
+          }
+          const ProcGrid g{Px, Py};
+          const bool sp = choose_single_pass(s, g, o, total, 1);
+          const Subdomain sd = decompose_2d(s.M, s.N, g, rank);
+          return layout_dict(GpuSubdomainSolver::comm_layout(sd, o.dtype, sp));
+        }, py::arg("spec"), py::arg("Px"), py::arg("Py"), py::arg("rank"), py::arg("dtype") = "fp64",
+        py::arg("kernel") = "wave", py::arg("exact") = false, py::arg("device") = 0, py::arg("algo") = -1);
   m.def("max_square_grid", [](double bytes_per_gpu, int gpus, const std::string& dtype, double reserve) {
     return max_square_grid(bytes_per_gpu, gpus, dtype == "fp64" ? DType::kFp64 : DType::kFp32, reserve);
   }, py::arg("bytes_per_gpu"), py::arg("gpus"), py::arg("dtype") = "fp64", py::arg("reserve") = 0.1);
@@ -284,11 +315,11 @@ PYBIND11_MODULE(_pmx, m) {
       .def(py::init([](const ProblemSpec& s, int Px, int Py, int rank, int device,
                        const std::string& kernel, int block, int vec, int waves, int tile_rows,
                        const std::string& dtype, bool exact, uintptr_t arena, bool check, int vec_b,
-                       int waves_b, int tile_rows_b, bool b_ring) {
+                       int waves_b, int tile_rows_b, bool b_ring, int algo) {
              const Subdomain sd = decompose_2d(s.M, s.N, ProcGrid{Px, Py}, rank);
              return std::make_unique<GpuSubdomainSolver>(
                  s, sd, make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact, 0, check,
-                                     true, vec_b, waves_b, tile_rows_b, false, b_ring),
+                                     true, vec_b, waves_b, tile_rows_b, false, b_ring, algo),
                  arena);
            }),
            py::arg("spec"), py::arg("Px") = 1, py::arg("Py") = 1, py::arg("rank") = 0,
@@ -296,8 +327,11 @@ PYBIND11_MODULE(_pmx, m) {
            py::arg("vec") = 0, py::arg("waves") = 4, py::arg("tile_rows") = 0,
            py::arg("dtype") = "fp64", py::arg("exact") = false, py::arg("arena") = 0,
            py::arg("check") = false, py::arg("vec_b") = 0, py::arg("waves_b") = 0,
-           py::arg("tile_rows_b") = -1, py::arg("b_ring") = false)
+           py::arg("tile_rows_b") = -1, py::arg("b_ring") = false, py::arg("algo") = -1)
       .def("enqueue_init", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_init(as_stream(s)); })
+      .def("enqueue_halo_pack", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_halo_pack(as_stream(s)); })
+      .def("enqueue_halo_unpack", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_halo_unpack(as_stream(s)); })
+      .def_property_readonly("single_pass", &GpuSubdomainSolver::single_pass)
       .def("enqueue_phase_a", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_phase_a(as_stream(s)); })
       .def("enqueue_phase_b", [](GpuSubdomainSolver& g, uintptr_t s, bool pack) {
              g.enqueue_phase_b(as_stream(s), pack);
@@ -323,12 +357,13 @@ PYBIND11_MODULE(_pmx, m) {
                        int tile_rows, const std::string& dtype, bool exact, int graph_batch,
                        bool check, py::object uid, std::vector<int> ranks, std::vector<int> devices,
                        bool rccl_graph, bool overlap, int vec_b, int waves_b, int tile_rows_b,
-                       bool poison_halos, bool b_ring) {
+                       bool poison_halos, bool b_ring, int algo, bool defer_connect) {
              SessionConfig c;
              c.spec = s;
              c.opt = make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact,
                                   graph_batch, check, overlap, vec_b, waves_b, tile_rows_b, poison_halos,
-                                  b_ring);
+                                  b_ring, algo);
+             c.defer_connect = defer_connect;
              c.split = split;
              c.world = world;
              if (comm == "self") c.comm = CommKind::kSelf;
@@ -350,7 +385,15 @@ PYBIND11_MODULE(_pmx, m) {
            py::arg("ranks") = std::vector<int>{}, py::arg("devices") = std::vector<int>{},
            py::arg("rccl_graph") = false, py::arg("overlap") = true, py::arg("vec_b") = 0,
            py::arg("waves_b") = 0, py::arg("tile_rows_b") = -1, py::arg("poison_halos") = false,
-           py::arg("b_ring") = false)
+           py::arg("b_ring") = false, py::arg("algo") = -1, py::arg("defer_connect") = false)
+      .def("connect", [](Session& s) { py::gil_scoped_release g; s.connect(); },
+           "create the communicator and driver (sessions built with defer_connect=True)")
+      .def_property_readonly("connected", &Session::connected)
+      .def("local_w", [](Session& s, int i) {
+             std::vector<double> w;
+             { py::gil_scoped_release g; w = s.local_w(i); }
+             return to_numpy(w, {s.solver(i).sd().nx, s.solver(i).sd().ny});
+           }, py::arg("i") = 0)
       .def("init", [](Session& s) { py::gil_scoped_release g; s.init(); })
       .def("step", [](Session& s, int64_t n) { py::gil_scoped_release g; s.step(n); })
       .def("synchronize", [](Session& s) { py::gil_scoped_release g; s.synchronize(); })

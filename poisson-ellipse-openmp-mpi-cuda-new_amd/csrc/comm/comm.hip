@@ -6,9 +6,11 @@
 //
 // Here:
 //  * RcclComm  — RCCL over xGMI straight from device buffers: ncclSend/ncclRecv pairs inside one
-//                ncclGroup for the 4 halo sides (edges packed by k_edge_r / k_pcg_b) on a split
-//                halo communicator, and two in-place ncclAllReduce per iteration (1 double, then
-//                (sum dw^2, (z,r)) packed into one 16-byte all-reduce).  Graph-capturable.
+//                ncclGroup for the active halo slots on a split halo communicator, and in-place
+//                ncclAllReduce of the PCG scalars.  Single-pass iteration: ONE 40-byte all-reduce
+//                (red_c) and up to 8 peers (4 sides with 2 lines of r and p, 4 corners).
+//                Two-sweep iteration: 2 all-reduces (1 double, then (sum dw^2, (z,r))) and the 4
+//                sides with one line of r (packed by k_edge_r / k_pcg_b).  Graph-capturable.
 //  * LocalComm — P subdomains in one process on one device: halos are D2D copies, the
 //                all-reduce is a deterministic rank-ordered sum kernel.  The fake cluster used to
 //                test multi-rank logic on a 1-GPU box.
@@ -51,29 +53,28 @@ class LocalComm final : public Comm {
       PMX_CHECK(local[i]->sd().rank == int(i), "LocalComm needs local[i].rank == i");
     }
     HIP_CHECK(hipSetDevice(dev));
-    std::vector<double*> a, b;
-    for (auto* s : local) { a.push_back(s->red_a_dev()); b.push_back(s->red_b_dev()); }
-    HIP_CHECK(hipMalloc(&ptrs_, 2 * n_ * sizeof(double*)));
-    HIP_CHECK(hipMemcpy(ptrs_, a.data(), n_ * sizeof(double*), hipMemcpyHostToDevice));
-    HIP_CHECK(hipMemcpy(ptrs_ + n_, b.data(), n_ * sizeof(double*), hipMemcpyHostToDevice));
+    // device table of the all-reduce buffers: [which][rank] for red_a, red_b, red_c
+    std::vector<double*> p;
+    for (int which = 0; which < 3; ++which)
+      for (auto* s : local) p.push_back(s->reduce_buf(which));
+    HIP_CHECK(hipMalloc(&ptrs_, p.size() * sizeof(double*)));
+    HIP_CHECK(hipMemcpy(ptrs_, p.data(), p.size() * sizeof(double*), hipMemcpyHostToDevice));
   }
   ~LocalComm() override { if (ptrs_) (void)hipFree(ptrs_); }
 
   void allreduce(std::vector<GpuSubdomainSolver*>&, int which,
                  std::vector<hipStream_t>& streams) override {
     if (n_ == 1) return;
-    launch_local_allreduce(ptrs_ + (which ? n_ : 0), n_, which ? 2 : 1, streams[0]);
+    launch_local_allreduce(ptrs_ + which * n_, n_, GpuSubdomainSolver::reduce_len(which), streams[0]);
   }
   void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>& streams) override {
     for (auto* s : local) {
-      const Subdomain& sd = s->sd();
-      const int nb[4] = {sd.nb_xlo, sd.nb_xhi, sd.nb_ylo, sd.nb_yhi};
       const CommLayout& L = s->layout();
-      for (int side = 0; side < 4; ++side) {
-        if (nb[side] < 0) continue;
-        GpuSubdomainSolver* o = local[nb[side]];
-        HIP_CHECK(hipMemcpyAsync(s->recv_dev(side), o->send_dev(side ^ 1),
-                                 size_t(L.edge_len[side]) * L.elem, hipMemcpyDeviceToDevice,
+      for (int slot = 0; slot < kHaloSlots; ++slot) {
+        if (!L.active(slot)) continue;
+        GpuSubdomainSolver* o = local[L.peer[slot]];
+        HIP_CHECK(hipMemcpyAsync(s->recv_dev(slot), o->send_dev(opposite_slot(slot)),
+                                 size_t(L.edge_len[slot]) * L.elem, hipMemcpyDeviceToDevice,
                                  streams[0]));
       }
     }
@@ -126,8 +127,9 @@ class RcclComm final : public Comm {
                  std::vector<hipStream_t>& streams) override {
     RCCL_CHECK(ncclGroupStart());
     for (size_t i = 0; i < local.size(); ++i) {
-      double* buf = which ? local[i]->red_b_dev() : local[i]->red_a_dev();
-      RCCL_CHECK(ncclAllReduce(buf, buf, which ? 2 : 1, ncclFloat64, ncclSum, comms_[i], streams[i]));
+      double* buf = local[i]->reduce_buf(which);
+      RCCL_CHECK(ncclAllReduce(buf, buf, GpuSubdomainSolver::reduce_len(which), ncclFloat64, ncclSum,
+                               comms_[i], streams[i]));
     }
     RCCL_CHECK(ncclGroupEnd());
   }
@@ -136,14 +138,12 @@ class RcclComm final : public Comm {
     RCCL_CHECK(ncclGroupStart());
     for (size_t i = 0; i < local.size(); ++i) {
       GpuSubdomainSolver* s = local[i];
-      const Subdomain& sd = s->sd();
-      const int nb[4] = {sd.nb_xlo, sd.nb_xhi, sd.nb_ylo, sd.nb_yhi};
       const CommLayout& L = s->layout();
       const ncclDataType_t t = L.elem == 8 ? ncclFloat64 : ncclFloat32;
-      for (int side = 0; side < 4; ++side) {
-        if (nb[side] < 0) continue;
-        RCCL_CHECK(ncclSend(s->send_dev(side), L.edge_len[side], t, nb[side], halo_comms_[i], streams[i]));
-        RCCL_CHECK(ncclRecv(s->recv_dev(side), L.edge_len[side], t, nb[side], halo_comms_[i], streams[i]));
+      for (int slot = 0; slot < kHaloSlots; ++slot) {
+        if (!L.active(slot)) continue;
+        RCCL_CHECK(ncclSend(s->send_dev(slot), L.edge_len[slot], t, L.peer[slot], halo_comms_[i], streams[i]));
+        RCCL_CHECK(ncclRecv(s->recv_dev(slot), L.edge_len[slot], t, L.peer[slot], halo_comms_[i], streams[i]));
       }
     }
     RCCL_CHECK(ncclGroupEnd());

@@ -36,8 +36,8 @@ DevGeom make_dev_geom(const ProblemSpec& spec, const Subdomain& sd, int64_t pitc
   G.gj0 = sd.gj0();
   G.M = spec.M;
   G.N = spec.N;
-  G.nb = (sd.nb_xlo >= 0 ? kNbXlo : 0) | (sd.nb_xhi >= 0 ? kNbXhi : 0) |
-         (sd.nb_ylo >= 0 ? kNbYlo : 0) | (sd.nb_yhi >= 0 ? kNbYhi : 0);
+  G.nb = 0;  // slot s <-> bit 1 << s (kNbXlo .. kNbXhiYhi)
+  for (int s = 0; s < kHaloSlots; ++s) G.nb |= sd.peer(s) >= 0 ? 1 << s : 0;
   G.ref_ellipse = spec.reference_ellipse() ? 1 : 0;
   G.h1 = g.h1; G.h2 = g.h2; G.eps = g.eps; G.inv_eps = g.inv_eps; G.h1h2 = g.h1h2;
   G.cx = 1.0 / (g.h1 * g.h1);
@@ -79,18 +79,63 @@ DevTables upload_tables(const ProblemSpec& spec, double** owner) {
   return T;
 }
 
-CommLayout GpuSubdomainSolver::comm_layout(const Subdomain& sd, DType dtype) {
+GpuOptions resolve_options(const GpuOptions& in) {
+  if (in.resolved) return in;
+  GpuOptions o = in;
+  auto env_int = [](const char* name, int& v) {
+    if (const char* e = std::getenv(name); e && e[0]) v = std::atoi(e);
+  };
+  env_int("PMX_PAIR_W", o.pair_w);
+  env_int("PMX_ALGO", o.algo);
+  env_int("PMX_PCG1_VEC", o.vec1);
+  env_int("PMX_PCG1_ROWS", o.rows1);
+  env_int("PMX_PCG1_WAVES", o.waves1);
+  PMX_CHECK(o.pair_w >= 0 && o.pair_w <= 2, "pair_w must be 0, 1 or 2");
+  PMX_CHECK(o.algo == -1 || o.algo == 1 || o.algo == 2, "algo must be -1, 1 or 2");
+  o.resolved = true;
+  return o;
+}
+
+bool choose_single_pass(const ProblemSpec& spec, const ProcGrid& grid, const GpuOptions& o,
+                        double device_total_bytes, int subdomains_per_device) {
+  PMX_CHECK(o.resolved, "choose_single_pass needs resolve_options()");
+  if (o.algo == 2) return false;
+  // the radius-2 halo takes two owned lines from every neighbour: each block needs >= 2 x 2
+  const bool thick = grid.size() == 1 || ((spec.M - 1) / grid.Px >= 2 && (spec.N - 1) / grid.Py >= 2);
+  const bool ok = !o.exact && o.kernel == 1 && thick;
+  PMX_CHECK(o.algo != 1 || ok,
+            "pcg1 needs the wave kernels, the fast arithmetic and subdomains of at least 2 x 2 nodes");
+  if (o.algo == 1) return true;
+  // auto: fp64 only -- with fp32 storage the stream halves and pcg1's second stencil makes it
+  // compute-bound (32768^2 fp32: pcg1 8.99 ms vs pcg2 7.69 ms per iteration)
+  if (!ok || o.dtype != DType::kFp64) return false;
+  if (device_total_bytes > 0) {  // the 5th field must fit (rank 0 holds the largest block)
+    const Subdomain sd0 = decompose_2d(spec.M, spec.N, grid, 0);
+    const double need = double(GpuSubdomainSolver::estimate_device_bytes(spec, sd0, o.dtype, true)) *
+                        std::max(1, subdomains_per_device);
+    if (need > 0.95 * device_total_bytes) return false;
+  }
+  return true;
+}
+
+CommLayout GpuSubdomainSolver::comm_layout(const Subdomain& sd, DType dtype, bool single_pass) {
   CommLayout L;
   L.elem = dtype == DType::kFp64 ? 8 : 4;
+  L.single_pass = single_pass;
   size_t off = 0;
   L.state_off = 0;
   off = round_up(sizeof(PcgState), 256);
-  for (int s = 0; s < 4; ++s) {
-    L.edge_len[s] = s < 2 ? sd.ny : sd.nx;
+  for (int s = 0; s < kHaloSlots; ++s) {
+    L.peer[s] = sd.peer(s);
+    // pcg2: one line of r per side; pcg1: 2 lines x (r, p) per side, one (r, p) per corner
+    const int line = s < 2 ? sd.ny : sd.nx;
+    L.edge_len[s] = single_pass ? (s < 4 ? 4 * line : 2) : (s < 4 ? line : 0);
+  }
+  for (int s = 0; s < kHaloSlots; ++s) {
     L.send_off[s] = off;
     off = round_up(off + L.edge_len[s] * L.elem, 256);
   }
-  for (int s = 0; s < 4; ++s) {
+  for (int s = 0; s < kHaloSlots; ++s) {
     L.recv_off[s] = off;
     off = round_up(off + L.edge_len[s] * L.elem, 256);
   }
@@ -100,34 +145,48 @@ CommLayout GpuSubdomainSolver::comm_layout(const Subdomain& sd, DType dtype) {
 
 GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain& sd,
                                        const GpuOptions& opt, uintptr_t external_arena)
-    : spec_(spec), sd_(sd), opt_(opt), g_(spec) {
+    : spec_(spec), sd_(sd), opt_(resolve_options(opt)), g_(spec) {
   spec.validate();
   PMX_CHECK(sd.nx >= 1 && sd.ny >= 1, "empty subdomain");
-  HIP_CHECK(hipSetDevice(opt.device));
-  elem_ = opt.dtype == DType::kFp64 ? 8 : 4;
-  if (const char* pw = std::getenv("PMX_PAIR_W"); pw && pw[0]) opt_.pair_w = std::atoi(pw);
-  PMX_CHECK(opt_.pair_w >= 0 && opt_.pair_w <= 2, "pair_w must be 0, 1 or 2");
-  if (const char* a = std::getenv("PMX_ALGO"); a && a[0]) opt_.algo = std::atoi(a);
-  if (const char* a = std::getenv("PMX_PCG1_VEC"); a && a[0]) opt_.vec1 = std::atoi(a);
-  if (const char* a = std::getenv("PMX_PCG1_ROWS"); a && a[0]) opt_.rows1 = std::atoi(a);
-  if (const char* a = std::getenv("PMX_PCG1_WAVES"); a && a[0]) opt_.waves1 = std::atoi(a);
-  const size_t align_elems = 256 / elem_;
+  HIP_CHECK(hipSetDevice(opt_.device));
+  try {
+    construct(external_arena);
+  } catch (...) {
+    release();  // the destructor does not run for a throwing constructor
+    throw;
+  }
+}
 
-  // +8 columns of padding: vector loads of VEC <= 4 columns starting at <= ny+1 stay in the row
+void GpuSubdomainSolver::construct(uintptr_t external_arena) {
+  const GpuOptions& opt = opt_;
+  const ProblemSpec& spec = spec_;
+  const Subdomain& sd = sd_;
+  elem_ = opt.dtype == DType::kFp64 ? 8 : 4;
+  const size_t align_elems = 256 / elem_;
+  size_t free_b = 0, total_b = 0;
+  HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+
+  // iteration algorithm (see GpuOptions::algo); a Session resolves it once for all its solvers
+  if (opt_.algo == -1) opt_.algo = choose_single_pass(spec, sd.grid, opt_, double(total_b), 1) ? 1 : 2;
+  pcg1_ = opt_.algo == 1;
+  PMX_CHECK(!pcg1_ || (!opt.exact && opt.kernel == 1 && (sd.grid.size() == 1 || (sd.nx >= 2 && sd.ny >= 2))),
+            "pcg1 needs the wave kernels, the fast arithmetic and a subdomain of at least 2 x 2 nodes");
+
+  // +8 columns of padding: vector loads of VEC <= 4 columns starting at <= ny+3 stay in the row,
+  // and the last padding element of a row is column -1 of the next one
   geom_ = make_dev_geom(spec, sd, int64_t(round_up(size_t(sd.ny + 2 + 8), align_elems)));
   const DevGeom& G = geom_;
 
-  // fields: element (li, lj) at base[li*pitch + lj]; base = alloc + (align-1) so that every
-  // interior row starts 256-B aligned (lj = 1)
-  field_off_ = align_elems - 1;
-  field_bytes_ = round_up((field_off_ + size_t(sd.nx + 2) * G.pitch) * elem_, 256);
+  // fields: element (li, lj), li = -1 .. nx+2, at base[li*pitch + lj]; base = alloc + pitch +
+  // (align-1) so that every interior row starts 256-B aligned (lj = 1)
+  field_off_ = size_t(G.pitch) + align_elems - 1;
+  field_bytes_ = round_up((align_elems - 1 + size_t(sd.nx + 4) * G.pitch) * elem_, 256);
   {  // fail with a sizing message instead of a bare hipErrorOutOfMemory
-    size_t free_b = 0, total_b = 0;
-    HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-    const size_t need = estimate_device_bytes(spec, sd, opt.dtype);
+    const size_t need = estimate_device_bytes(spec, sd, opt.dtype, pcg1_);
     PMX_CHECK(need <= free_b,
-              "subdomain " << sd.nx << "x" << sd.ny << " needs " << need / 1e9 << " GB on device "
-                           << opt.device << " but only " << free_b / 1e9 << " of " << total_b / 1e9
+              "subdomain " << sd.nx << "x" << sd.ny << " (" << (pcg1_ ? "pcg1, 5" : "pcg2, 4")
+                           << " fields) needs " << need / 1e9 << " GB on device " << opt.device
+                           << " but only " << free_b / 1e9 << " of " << total_b / 1e9
                            << " GB are free; the largest square grid for this precision on one such "
                               "device is ~"
                            << max_square_grid(double(total_b), 1, opt.dtype) << "^2 (pmx --plan)");
@@ -156,14 +215,6 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
     tiles_b_ = make_row_tiles(G, vec_b, waves_b, opt.tile_rows_b >= 0 ? opt.tile_rows_b : 0);
   tiles_b_.pair_w = tiles_b_.kind == 2 && !opt.exact && opt_.pair_w != 0;
 
-  // single-pass iteration where it applies (see GpuOptions::algo)
-  PMX_CHECK(opt_.algo == -1 || opt_.algo == 1 || opt_.algo == 2, "algo must be -1, 1 or 2");
-  const bool pcg1_ok = G.nb == 0 && !opt.exact && opt.kernel == 1;
-  PMX_CHECK(opt_.algo != 1 || pcg1_ok,
-            "pcg1 needs the wave kernels, the fast arithmetic and a subdomain without neighbours");
-  // auto picks pcg1 in fp64 only: with fp32 storage the stream halves and pcg1's second stencil
-  // makes it compute-bound (32768^2 fp32: pcg1 8.99 ms vs pcg2 7.69 ms per iteration)
-  pcg1_ = opt_.algo == 1 || (opt_.algo == -1 && pcg1_ok && opt.dtype == DType::kFp64);
   if (pcg1_) {
     tiles1_ = make_pcg1_tiles(G, opt_.vec1, opt_.waves1, opt_.rows1);
     HIP_CHECK(hipMalloc(&r2_, field_bytes_));
@@ -172,11 +223,12 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
   init_tiles_ = make_tiles(G, 256, 0);
   const size_t npart = size_t(std::max({tiles_.ntiles(), tiles_b_.ntiles(), init_tiles_.ntiles(),
                                         pcg1_ ? tiles1_.ntiles() : 0}));
+  npart_ = npart;
   HIP_CHECK(hipMalloc(&partials_, (npart * 5 + kReduceWsDoubles) * sizeof(double)));
   reduce_ws_ = partials_ + npart * 5;
   HIP_CHECK(hipMemset(reduce_ws_, 0, kReduceWsDoubles * sizeof(double)));
 
-  layout_ = comm_layout(sd, opt.dtype);
+  layout_ = comm_layout(sd, opt.dtype, pcg1_);
   if (external_arena) {
     arena_ = reinterpret_cast<char*>(external_arena);
     own_arena_ = false;
@@ -190,7 +242,7 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
   HIP_CHECK(hipHostMalloc(&host_state_, 2 * sizeof(PcgState), hipHostMallocDefault));
 }
 
-GpuSubdomainSolver::~GpuSubdomainSolver() {
+void GpuSubdomainSolver::release() noexcept {
   (void)hipSetDevice(opt_.device);
   (void)hipDeviceSynchronize();
   if (fields_) (void)hipFree(fields_);
@@ -199,22 +251,30 @@ GpuSubdomainSolver::~GpuSubdomainSolver() {
   if (partials_) (void)hipFree(partials_);
   if (own_arena_ && arena_) (void)hipFree(arena_);
   if (host_state_) (void)hipHostFree(host_state_);
+  fields_ = r2_ = nullptr;
+  arena_ = nullptr;
+  tables_buf_ = partials_ = nullptr;
+  host_state_ = nullptr;
 }
 
+GpuSubdomainSolver::~GpuSubdomainSolver() { release(); }
+
 size_t GpuSubdomainSolver::estimate_device_bytes(const ProblemSpec& spec, const Subdomain& sd,
-                                                 DType dtype) {
+                                                 DType dtype, bool single_pass) {
   const size_t elem = dtype == DType::kFp64 ? 8 : 4, align = 256 / elem;
   const size_t pitch = round_up(size_t(sd.ny + 2 + 8), align);
-  const size_t field = round_up((align - 1 + size_t(sd.nx + 2) * pitch) * elem, 256);
+  const size_t field = round_up((align - 1 + size_t(sd.nx + 4) * pitch) * elem, 256);
   const size_t tables = (4 * size_t(spec.M + 2) + 4 * size_t(spec.N + 2)) * 8 + 8 * size_t(spec.M + 2) * 4;
-  // partials: at most one per 2 rows x 64 columns tile (the smallest auto tile), 2 doubles each
+  // partials: at most one per 2 rows x 64 columns tile (the smallest auto tile), 5 doubles each
   const size_t partials = (size_t(sd.nx + 1) / 2 + 1) * (size_t(sd.ny) / 64 + 1) * 40;
-  return 4 * field + tables + partials + comm_layout(sd, dtype).bytes + (1u << 20);
+  return (single_pass ? 5 : 4) * field + tables + partials + comm_layout(sd, dtype, single_pass).bytes +
+         (1u << 20);
 }
 
 size_t GpuSubdomainSolver::device_bytes() const {
-  return 4 * field_bytes_ + (4 * (spec_.M + 2) + 4 * (spec_.N + 2)) * sizeof(double) +
-         (size_t(std::max({tiles_.ntiles(), tiles_b_.ntiles(), init_tiles_.ntiles(), tiles1_.ntiles()})) * 5 + kReduceWsDoubles) * sizeof(double) +
+  const size_t tables = (4 * size_t(spec_.M + 2) + 4 * size_t(spec_.N + 2)) * sizeof(double) +
+                        8 * size_t(spec_.M + 2) * sizeof(int);
+  return (r2_ ? 5 : 4) * field_bytes_ + tables + (npart_ * 5 + kReduceWsDoubles) * sizeof(double) +
          (own_arena_ ? layout_.bytes : 0);
 }
 
@@ -226,7 +286,7 @@ void* GpuSubdomainSolver::field_base(int which) const {
 template <typename T>
 HaloBufs<T> GpuSubdomainSolver::halo() const {
   HaloBufs<T> H;
-  for (int s = 0; s < 4; ++s) {
+  for (int s = 0; s < kHaloSlots; ++s) {
     H.send[s] = reinterpret_cast<T*>(arena_ + layout_.send_off[s]);
     H.recv[s] = reinterpret_cast<T*>(arena_ + layout_.recv_off[s]);
   }
@@ -249,7 +309,8 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
   std::memset(&st, 0, sizeof(st));
   st.delta = spec_.delta;
   st.bd_tol = spec_.breakdown_tol;
-  st.it = pcg1_ ? 0 : 1;  // pcg1: sweep 0 below forms (z^0, r^0) and (A z^0, z^0)
+  st.it = pcg1_ ? 0 : 1;  // pcg1: sweep 0 (enqueued by the driver) forms (z^0, r^0), (A z^0, z^0)
+  st.halo_k = 0;          // pcg1: the first ghost exchange fills sweep 0's inputs
   st.max_iter = spec_.effective_max_iter();
   st.norm = int(spec_.norm);
   st.pair_w = opt_.pair_w ? 1 : 0;
@@ -257,15 +318,31 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
   HIP_CHECK(hipMemcpyAsync(state_, &st, sizeof(PcgState), hipMemcpyHostToDevice, s));
   T* w = static_cast<T*>(field_base(0));
   T* r = static_cast<T*>(field_base(1));
-  launch_init<T>(geom_, tables_, w, r, halo<T>(), partials_, init_tiles_, s);
+  // k_init packs r^0 into the two-sweep send buffers; pcg1 packs its own radius-2 halo
+  DevGeom G = geom_;
+  if (pcg1_) G.nb = 0;
+  launch_init<T>(G, tables_, w, r, halo<T>(), partials_, init_tiles_, s);
   after_launch(s);
   launch_reduce(partials_, init_tiles_.ntiles(), 2, 0.0, g_.h1h2, state_->red_b, state_, 0, reduce_ws_, s);
   after_launch(s);
-  if (pcg1_) {
-    phase_a_kernel_only<T>(s);
-    after_launch(s);
-    enqueue_reduce_a(s);  // it 0 -> 1
-  }
+}
+
+template <typename T>
+void GpuSubdomainSolver::halo_impl(hipStream_t s, bool unpack) {
+  launch_pcg1_halo<T>(geom_, static_cast<T*>(field_base(1)), reinterpret_cast<T*>(r2_ + field_off_ * elem_),
+                      static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(), state_,
+                      unpack, s);
+  after_launch(s);
+}
+
+void GpuSubdomainSolver::enqueue_halo_pack(hipStream_t s) {
+  if (!pcg1_ || geom_.nb == 0) return;
+  if (opt_.dtype == DType::kFp64) halo_impl<double>(s, false); else halo_impl<float>(s, false);
+}
+
+void GpuSubdomainSolver::enqueue_halo_unpack(hipStream_t s) {
+  if (!pcg1_ || geom_.nb == 0) return;
+  if (opt_.dtype == DType::kFp64) halo_impl<double>(s, true); else halo_impl<float>(s, true);
 }
 
 template <typename T>
@@ -380,7 +457,7 @@ void GpuSubdomainSolver::save_checkpoint(std::ostream& os, hipStream_t s) const 
   HIP_CHECK(hipStreamSynchronize(s));
   CkptHeader h{};
   std::memcpy(h.magic, kCkptMagic, 8);
-  h.version = pcg1_ ? 2 : 1;  // v2: pcg1 state, r2 appended
+  h.version = pcg1_ ? 4 : 3;  // v3: fields with 2 ghost rows; v4: + pcg1 state, r2 appended
   h.M = spec_.M; h.N = spec_.N; h.gi0 = sd_.gi0(); h.gj0 = sd_.gj0();
   h.rank = sd_.rank; h.elem = int32_t(elem_); h.norm = int32_t(spec_.norm);
   h.nx = sd_.nx; h.ny = sd_.ny; h.pitch = geom_.pitch; h.field_bytes = int64_t(field_bytes_);
@@ -403,8 +480,8 @@ void GpuSubdomainSolver::load_checkpoint(std::istream& is, hipStream_t s) {
   CkptHeader h{};
   is.read(reinterpret_cast<char*>(&h), sizeof(h));
   PMX_CHECK(is.good() && std::memcmp(h.magic, kCkptMagic, 8) == 0 &&
-                h.version == (pcg1_ ? 2 : 1),
-            "not a pmx checkpoint of this iteration algorithm (v1 pcg2, v2 pcg1)");
+                h.version == (pcg1_ ? 4 : 3),
+            "not a pmx checkpoint of this iteration algorithm and layout (v3 pcg2, v4 pcg1)");
   PMX_CHECK(h.M == spec_.M && h.N == spec_.N && h.gi0 == sd_.gi0() && h.gj0 == sd_.gj0() &&
                 h.nx == sd_.nx && h.ny == sd_.ny && h.rank == sd_.rank,
             "checkpoint is for a different grid/decomposition (M=" << h.M << " N=" << h.N << " rank "
@@ -563,6 +640,10 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
   if (same_device) streams_.resize(local_.size(), streams_[0]);
   bool any_nb = false;
   for (auto* s : local_) any_nb |= s->geom().nb != 0;
+  any_nb_ = any_nb;
+  single_pass_ = local_[0]->single_pass();
+  for (auto* s : local_)
+    PMX_CHECK(s->single_pass() == single_pass_, "local subdomains disagree on the iteration algorithm");
   overlap_ = any_nb && local_[0]->options().overlap;
   const char* env = std::getenv("PMX_POISON_HALOS");
   poison_ = any_nb && (local_[0]->options().poison_halos || (env && env[0] == '1'));
@@ -610,9 +691,21 @@ void PcgDriver::synchronize() {
 void PcgDriver::init() {
   TraceRange tr("pmx:init");
   for (size_t i = 0; i < local_.size(); ++i) local_[i]->enqueue_init(streams_[i]);
-  comm_->allreduce(local_, 1, streams_);
-  poison(streams_);
-  comm_->halo(local_, streams_);
+  if (single_pass_) {
+    // ghosts of r^0 -> sweep 0 ((z^0, r^0), (A z^0, z^0); it 0 -> 1) -> all-reduce -> ghosts of
+    // sweep 0's outputs, which sweep 1 reads
+    if (any_nb_) halo_exchange_pcg1(streams_);
+    for (size_t i = 0; i < local_.size(); ++i) {
+      HIP_CHECK(hipSetDevice(local_[i]->device()));
+      local_[i]->enqueue_phase_a(streams_[i]);
+    }
+    comm_->allreduce(local_, 2, streams_);
+    if (any_nb_) halo_exchange_pcg1(streams_);
+  } else {
+    comm_->allreduce(local_, 1, streams_);
+    poison(streams_);
+    comm_->halo(local_, streams_);
+  }
   synchronize();
 }
 
@@ -624,7 +717,53 @@ void PcgDriver::poison(std::vector<hipStream_t>& streams) {
   }
 }
 
+void PcgDriver::halo_exchange_pcg1(std::vector<hipStream_t>& streams) {
+  for (size_t i = 0; i < local_.size(); ++i) {
+    HIP_CHECK(hipSetDevice(local_[i]->device()));
+    local_[i]->enqueue_halo_pack(streams[i]);
+  }
+  poison(streams);
+  comm_->halo(local_, streams);
+  for (size_t i = 0; i < local_.size(); ++i) {
+    HIP_CHECK(hipSetDevice(local_[i]->device()));
+    local_[i]->enqueue_halo_unpack(streams[i]);
+  }
+}
+
 void PcgDriver::enqueue_one_iteration() {
+  if (single_pass_) {
+    // Single pass.  Every tile of sweep k+1 needs alpha_{k+1}, i.e. the all-reduced sums of
+    // sweep k, so no part of the next sweep can start before the all-reduce; what CAN run
+    // concurrently is the ghost exchange, which only needs sweep k's outputs:
+    //   compute stream  sweep k -> reduce_n -> all-reduce(red_c, 5 doubles) -> join -> sweep k+1
+    //   comm stream             `-> pack -> send/recv (8 slots) -> unpack ---'
+    if (!any_nb_ || !overlap_) {
+      for (size_t i = 0; i < local_.size(); ++i) {
+        HIP_CHECK(hipSetDevice(local_[i]->device()));
+        local_[i]->enqueue_phase_a(streams_[i]);
+      }
+      comm_->allreduce(local_, 2, streams_);  // no-op for SelfComm
+      if (any_nb_) halo_exchange_pcg1(streams_);
+      return;
+    }
+    for (size_t i = 0; i < local_.size(); ++i) {
+      HIP_CHECK(hipSetDevice(local_[i]->device()));
+      local_[i]->enqueue_kernel_a(streams_[i]);
+    }
+    for_each_stream([&](size_t i, size_t u) {
+      HIP_CHECK(hipEventRecord(ev_packed_[u], streams_[i]));
+      HIP_CHECK(hipStreamWaitEvent(comm_streams_[i], ev_packed_[u], 0));
+    });
+    halo_exchange_pcg1(comm_streams_);
+    for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipEventRecord(ev_halo_[u], comm_streams_[i])); });
+    for (size_t i = 0; i < local_.size(); ++i) {
+      HIP_CHECK(hipSetDevice(local_[i]->device()));
+      local_[i]->enqueue_reduce_a(streams_[i]);
+    }
+    comm_->allreduce(local_, 2, streams_);
+    for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipStreamWaitEvent(streams_[i], ev_halo_[u], 0)); });
+    return;
+  }
   for (size_t i = 0; i < local_.size(); ++i) {
     HIP_CHECK(hipSetDevice(local_[i]->device()));
     local_[i]->enqueue_phase_a(streams_[i]);
@@ -760,11 +899,13 @@ RunStats PcgDriver::profile_phases(int64_t n) {
   TraceRange tr("pmx:profile_phases");
   // Eager iterations with an event after every step, all on the compute stream(s) (no overlap, so
   // each step's time is its own).  Events on the first device's stream; on a multi-device
-  // driver the other streams are joined by the collectives.
+  // driver the other streams are joined by the collectives.  Single pass: kernel_a = the sweep,
+  // kernel_b = 0, reduce = the 5-value reduction, allreduce = red_c, halo = pack + exchange +
+  // unpack.
   RunStats st;
   HIP_CHECK(hipSetDevice(local_[0]->device()));
   hipStream_t s0 = streams_[0];
-  constexpr int kEv = 8;
+  constexpr int kEv = 7;
   std::vector<hipEvent_t> ev(size_t(n) * kEv + 1);
   for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
   auto each = [&](auto&& f) {
@@ -781,17 +922,24 @@ RunStats PcgDriver::profile_phases(int64_t n) {
     HIP_CHECK(hipEventRecord(e[0], s0));
     each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_reduce_a(s); });
     HIP_CHECK(hipEventRecord(e[1], s0));
-    comm_->allreduce(local_, 0, streams_);
+    comm_->allreduce(local_, single_pass_ ? 2 : 0, streams_);
     HIP_CHECK(hipEventRecord(e[2], s0));
-    each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_kernel_b(s, true); });
+    if (!single_pass_) each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_kernel_b(s, true); });
     HIP_CHECK(hipEventRecord(e[3], s0));
-    each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_reduce_b(s); });
-    HIP_CHECK(hipEventRecord(e[4], s0));
-    comm_->allreduce(local_, 1, streams_);
+    if (!single_pass_) {
+      each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_reduce_b(s); });
+      HIP_CHECK(hipEventRecord(e[4], s0));
+      comm_->allreduce(local_, 1, streams_);
+    } else {
+      HIP_CHECK(hipEventRecord(e[4], s0));
+    }
     HIP_CHECK(hipEventRecord(e[5], s0));
-    comm_->halo(local_, streams_);
+    if (single_pass_) {
+      if (any_nb_) halo_exchange_pcg1(streams_);
+    } else {
+      comm_->halo(local_, streams_);
+    }
     HIP_CHECK(hipEventRecord(e[6], s0));
-    HIP_CHECK(hipEventRecord(e[7], s0));
   }
   synchronize();
   auto sec = [](hipEvent_t a, hipEvent_t b) {
@@ -801,7 +949,7 @@ RunStats PcgDriver::profile_phases(int64_t n) {
   };
   for (int64_t k = 0; k < n; ++k) {
     hipEvent_t* e = &ev[size_t(k) * kEv + 1];
-    hipEvent_t start = k == 0 ? ev[0] : ev[size_t(k - 1) * kEv + 1 + 7];
+    hipEvent_t start = k == 0 ? ev[0] : ev[size_t(k - 1) * kEv + 1 + 6];
     st.t_kernel_a += sec(start, e[0]);
     st.t_reduce += sec(e[0], e[1]) + sec(e[3], e[4]);
     st.t_allreduce += sec(e[1], e[2]) + sec(e[4], e[5]);

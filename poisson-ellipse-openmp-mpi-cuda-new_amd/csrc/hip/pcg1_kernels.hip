@@ -25,6 +25,15 @@
 // alpha_{k-1} p^{k-1} + alpha_k p^k, and p^{k-1} is the p_old this kernel reads anyway.
 // HBM traffic: r, p read + written (32 B) + w every other iteration (8 B) = 40 B/pt/iteration
 // (pcg_a + pcg_b: 56), one deterministic reduction and one all-reduce per iteration (pcg2: two).
+//
+// Decomposed grids: the radius-2 dependency needs r^{k-1} and p^{k-1} on the owned block grown by
+// a diamond of radius 2 -- two ghost lines per side plus ONE corner value per diagonal neighbour
+// ((0,0), (0,ny+1), (nx+1,0), (nx+1,ny+1)).  Fields carry 2 ghost rows above/below and 2 ghost
+// columns left/right (column -1 sits in the previous row's padding); k_pcg1_halo packs/unpacks
+// them (8 slots: 4 sides, 4 corners) and the sweep reads ghosts like interior values, deciding
+// "interior vs Dirichlet" on global indices.  Values outside the diamond (e.g. (-1, 0)) are never
+// exchanged: they only feed columns/rows that are not owned, which are neither stored nor summed.
+#include <algorithm>
 #include <cmath>
 
 #include "pcg_device.hpp"
@@ -114,28 +123,32 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   const int64_t P = G.pitch;
   const int lane = threadIdx.x & 63;
   const int c0 = j0 - 2 + lane * VEC;
-  const int cmax = 1 + (G.ny / 2) * 2;
+  const int cmax = G.ny + 1 + (G.ny & 1);  // last odd column <= ny + 2 (second ghost column)
+  // Interior / Dirichlet is decided on GLOBAL indices: the ghost rows/columns of a decomposed
+  // subdomain hold its neighbours' values (k_pcg1_halo), those on the domain boundary are 0.
   bool colin[VEC], own[VEC];
   int gj[VEC];
 #pragma unroll
   for (int u = 0; u < VEC; ++u) {
-    const int c = c0 + u;
-    colin[u] = c >= 1 && c <= G.ny;
+    const int c = c0 + u, g = G.gj0 + c;
+    colin[u] = g >= 1 && g <= G.N - 1;
     own[u] = c >= j0 && c <= j1;
-    gj[u] = G.gj0 + min(max(c, 0), G.ny + 1);
+    gj[u] = min(max(g, 0), G.N);
   }
   const bool own_all = own[0] && own[VEC - 1];
   bool own_any = false;
 #pragma unroll
   for (int u = 0; u < VEC; ++u) own_any |= own[u];
-  const int gjlo = G.gj0 + max(j0 - 2, 0), gjhi = G.gj0 + min(j0 - 2 + 64 * VEC - 1, G.ny + 1);
+  const int gjlo = max(G.gj0 + j0 - 2, 0), gjhi = min(G.gj0 + j0 - 2 + 64 * VEC - 1, G.N);
+  auto grow = [&](int m) { return min(max(G.gi0 + m, 0), G.M); };  // table row of local row m
+  auto interior_row = [&](int m) { return G.gi0 + m >= 1 && G.gi0 + m <= G.M - 1; };
 
   auto fetch = [&](int m, Pcg1Row<T, VEC>& b) {
-    const int mc = min(max(m, 0), G.nx + 1);
+    const int mc = min(max(m, -1), G.nx + 2);  // rows -1 .. nx+2 exist (2 ghost layers)
     load_cols<T, VEC>(rold + int64_t(mc) * P, c0, cmax, b.r);
     load_cols<T, VEC>(pold + int64_t(mc) * P, c0, cmax, b.p);
     if constexpr (EVEN) {  // w of the row stage B handles next step
-      const int wc = min(max(m - 1, 0), G.nx + 1);
+      const int wc = min(max(m - 1, -1), G.nx + 2);
       load_cols<T, VEC>(w + int64_t(wc) * P, c0, cmax, b.w);
     }
   };
@@ -144,14 +157,14 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   double Pm2[VEC], Pm1[VEC], Zm3[VEC], Zm2[VEC], ro1[VEC], po1[VEC];
 #pragma unroll
   for (int u = 0; u < VEC; ++u) Pm2[u] = Pm1[u] = Zm3[u] = Zm2[u] = ro1[u] = po1[u] = 0.0;
-  RowCo cB = row_co(Tb, G, G.gi0 + min(max(i0 - 3, 0), G.nx + 1), gjlo, gjhi);  // rows m-1, m-2
+  RowCo cB = row_co(Tb, G, grow(i0 - 3), gjlo, gjhi);  // rows m-1, m-2
   RowCo cC = cB;
 
   auto step = [&](int m, const Pcg1Row<T, VEC>& cur, Pcg1Row<T, VEC>& nxt) {
     fetch(m + 1, nxt);  // unconditional (clamped): a branch around loads forces vmcnt(0)
     // ---- stage A: p^k of row m
-    const bool rowA = m >= 1 && m <= G.nx;
-    const RowCo cA = row_co(Tb, G, G.gi0 + min(max(m, 0), G.nx + 1), gjlo, gjhi);
+    const bool rowA = interior_row(m);
+    const RowCo cA = row_co(Tb, G, grow(m), gjlo, gjhi);
     double Pm[VEC], rom[VEC], pom[VEC];
 #pragma unroll
     for (int u = 0; u < VEC; ++u) {
@@ -167,7 +180,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     // ---- stage B: A p^k, r^k, z^k of row m-1 (j neighbours by DPP; edge lanes get 0, their
     // results only feed columns that are not owned)
     const int mb = m - 1;
-    const bool rowB = mb >= 1 && mb <= G.nx;
+    const bool rowB = interior_row(mb);
     const bool ownB = mb >= i0 && mb <= i1;
     double Zm1[VEC];
     T rs[VEC], ps[VEC], ws[VEC];
@@ -294,6 +307,7 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
       S->w_pend = (k & 1) ? k : 0;
     }
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) S->halo_k = k + 1;  // the next exchange fills sweep k+1's inputs
   const int id = xcd_remap(blockIdx.x, gridDim.x) * WAVES + __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   if (id >= ntiles) return;
   const int ti = id / tiles_j, tj = id - ti * tiles_j;
@@ -315,6 +329,48 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
 #pragma unroll
     for (int q = 0; q < kNq; ++q) partials[int64_t(kNq) * id + q] = acc[q];
   }
+}
+
+// Radius-2 ghost exchange of the single-pass iteration (see the header): pack (unpack = 0) copies
+// the owned edge lines of the buffers the NEXT sweep reads -- sweep S->halo_k reads
+// r^{k-1} = (k & 1 ? r2 : r) and p^{k-1} = (k & 1 ? p0 : p1) -- into the send slots; unpack copies
+// the receive slots into the ghost cells of the same buffers.  Slot layout: sides
+// [field][line][pos] (field 0 = r, 1 = p; line q = ghost row/column -1+q on the receiving side,
+// ordered by increasing index), corners [field].  Grid: (ceil(max(nx, ny) / 256), 8 slots,
+// 4 = (field, line)).  Tiny and stream-ordered; launched by the driver between two sweeps.
+template <typename T>
+__global__ void __launch_bounds__(256)
+k_pcg1_halo(DevGeom G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, const PcgState* S, int unpack) {
+  const int slot = blockIdx.y;
+  if (!((G.nb >> slot) & 1)) return;
+  const int f = blockIdx.z >> 1, q = blockIdx.z & 1;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int nx = G.nx, ny = G.ny;
+  int li, lj, idx;
+  if (slot < 2) {          // x sides: rows
+    if (t >= ny) return;
+    li = slot == 0 ? (unpack ? -1 + q : 1 + q) : (unpack ? nx + 1 + q : nx - 1 + q);
+    lj = 1 + t;
+    idx = (f * 2 + q) * ny + t;
+  } else if (slot < 4) {   // y sides: columns
+    if (t >= nx) return;
+    li = 1 + t;
+    lj = slot == 2 ? (unpack ? -1 + q : 1 + q) : (unpack ? ny + 1 + q : ny - 1 + q);
+    idx = (f * 2 + q) * nx + t;
+  } else {                 // corners: one value per field
+    if (t != 0 || q != 0) return;
+    const bool xhi = slot >= 6, yhi = slot == 5 || slot == 7;
+    li = xhi ? (unpack ? nx + 1 : nx) : (unpack ? 0 : 1);
+    lj = yhi ? (unpack ? ny + 1 : ny) : (unpack ? 0 : 1);
+    idx = f;
+  }
+  const long long kk = S->halo_k;
+  T* fld = f == 0 ? ((kk & 1) ? r2 : r) : ((kk & 1) ? p0 : p1);
+  const int64_t o = int64_t(li) * G.pitch + lj;
+  if (unpack)
+    fld[o] = H.recv[slot][idx];
+  else
+    H.send[slot][idx] = fld[o];
 }
 
 // Deterministic reduction of n partial vectors of NQ values (fixed chunk order, MFMA wave sums),
@@ -401,7 +457,7 @@ template <typename T>
 void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1,
                  double* partials, PcgState* S, const TileCfg& tc, hipStream_t s) {
   PMX_CHECK(tc.kind == 3, "launch_pcg1 needs make_pcg1_tiles");
-  PMX_CHECK(G.nb == 0, "pcg1 runs on a subdomain without neighbours (use pcg2 for decompositions)");
+  PMX_CHECK(G.nb == 0 || (G.nx >= 2 && G.ny >= 2), "pcg1 on a decomposed grid needs subdomains >= 2 x 2");
   const int nb = (tc.ntiles() + tc.waves - 1) / tc.waves;
   const int bs = 64 * tc.waves;
 #define PMX_PCG1(V, WV) \
@@ -413,6 +469,16 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
   else if (tc.vec == 4 && tc.waves == 2) PMX_PCG1(4, 2);
   else PMX_PCG1(4, 1);
 #undef PMX_PCG1
+  HIP_CHECK(hipGetLastError());
+}
+
+template <typename T>
+void launch_pcg1_halo(const DevGeom& G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, const PcgState* S,
+                      bool unpack, hipStream_t s) {
+  if (G.nb == 0) return;
+  const int len = std::max(G.nx, G.ny);
+  hipLaunchKernelGGL(k_pcg1_halo<T>, dim3((len + 255) / 256, kHaloSlots, 4), dim3(256), 0, s, G, r, r2,
+                     p0, p1, H, S, unpack ? 1 : 0);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -430,6 +496,10 @@ void launch_reduce_n(const double* partials, int n, int nq, const double* weight
 
 template void launch_pcg1<double>(const DevGeom&, const DevTables&, double*, double*, double*, double*,
                                   double*, double*, PcgState*, const TileCfg&, hipStream_t);
+template void launch_pcg1_halo<double>(const DevGeom&, double*, double*, double*, double*, HaloBufs<double>,
+                                        const PcgState*, bool, hipStream_t);
+template void launch_pcg1_halo<float>(const DevGeom&, float*, float*, float*, float*, HaloBufs<float>,
+                                       const PcgState*, bool, hipStream_t);
 template void launch_pcg1<float>(const DevGeom&, const DevTables&, float*, float*, float*, float*, float*,
                                  double*, PcgState*, const TileCfg&, hipStream_t);
 

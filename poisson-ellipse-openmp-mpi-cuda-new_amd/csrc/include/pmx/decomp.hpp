@@ -64,6 +64,13 @@ struct Subdomain {
   // global index of local (li, lj): gi = i_start - 1 + li  (li = 0 .. nx+1)
   int gi0() const { return i_start - 1; }
   int gj0() const { return j_start - 1; }
+  // rank across halo slot s (pmx/device_types.hpp kHaloSlots: 4 sides, then 4 corners), or -1
+  int peer(int s) const {
+    static constexpr int dx[8] = {-1, 1, 0, 0, -1, -1, 1, 1};
+    static constexpr int dy[8] = {0, 0, -1, 1, -1, 1, -1, 1};
+    const int qx = px + dx[s], qy = py + dy[s];
+    return (qx >= 0 && qx < grid.Px && qy >= 0 && qy < grid.Py) ? qy * grid.Px + qx : -1;
+  }
   double aspect() const {
     return nx > 0 && ny > 0 ? double(std::max(nx, ny)) / double(std::min(nx, ny)) : 0.0;
   }

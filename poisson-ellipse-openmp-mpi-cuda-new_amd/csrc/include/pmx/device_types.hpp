@@ -23,16 +23,27 @@ struct DevTables {
   const int* bcls;
 };
 
-enum NbBits : int { kNbXlo = 1, kNbXhi = 2, kNbYlo = 4, kNbYhi = 8 };
+// Neighbour bits: the 4 sides, then the 4 diagonal neighbours (only the single-pass iteration,
+// whose stencil radius is 2, needs the corner values of the diagonal ranks).
+enum NbBits : int {
+  kNbXlo = 1, kNbXhi = 2, kNbYlo = 4, kNbYhi = 8,
+  kNbXloYlo = 16, kNbXloYhi = 32, kNbXhiYlo = 64, kNbXhiYhi = 128,
+};
+// Halo slots: 0 x-lo, 1 x-hi, 2 y-lo, 3 y-hi, 4 (x-lo, y-lo), 5 (x-lo, y-hi), 6 (x-hi, y-lo),
+// 7 (x-hi, y-hi).  Slot s of a rank talks to the rank whose slot opposite_slot(s) faces back.
+constexpr int kHaloSlots = 8;
+inline constexpr int opposite_slot(int s) { return s < 4 ? (s ^ 1) : 11 - s; }
 
-// One subdomain's geometry as seen by a kernel.  Local node (li, lj), li = 0..nx+1,
-// lj = 0..ny+1, lives at field[li * pitch + lj]; global index gi = gi0 + li.
+// One subdomain's geometry as seen by a kernel.  Local node (li, lj), li = -1..nx+2,
+// lj = -1..ny+2, lives at field[li * pitch + lj]; global index gi = gi0 + li.  Rows -1 and nx+2
+// and columns -1 and ny+2 are the second ghost layer of the single-pass iteration (column -1 of
+// row li is the last padding element of row li-1, pitch >= ny + 10).
 struct DevGeom {
   int nx, ny;
   int64_t pitch;
   int gi0, gj0;
   int M, N;
-  int nb;  // NbBits: neighbour exists on that side (else Dirichlet ghost)
+  int nb;  // NbBits: neighbour exists on that side / corner (else Dirichlet ghost)
   int ref_ellipse;
   double h1, h2, eps, inv_eps, h1h2;
   double cx, cy;  // 1/h1^2, 1/h2^2
@@ -65,14 +76,19 @@ struct alignas(64) PcgState {
   // Single-pass iteration (pcg1_kernels.hip): all-reduce buffer C = (z,r), (Az,z), (Az,p),
   // (Ap,p) (weighted) and |p|^2 (weighted per norm) of the last sweep.
   double red_c[5];
+  // Single-pass halo: index of the sweep whose input buffers (r^{k-1}, p^{k-1}) the next ghost
+  // exchange fills.  Written by sweep k (= k + 1) and by init (= 0); read by k_pcg1_halo, which
+  // runs on the comm stream between the sweeps, so it never races with the writer.
+  long long halo_k;
 };
 
-// Pointers for the halo ("ghost") exchange of r.  Side order: 0 x-lo, 1 x-hi, 2 y-lo, 3 y-hi.
-// send[s]/recv[s] hold edge_len(s) values (ny for x sides, nx for y sides).
+// Pointers for the halo ("ghost") exchange, one per slot (see kHaloSlots).  Two-sweep iteration:
+// slots 0-3 hold one line of r (ny values for x sides, nx for y sides).  Single-pass iteration:
+// two lines of r and of p per side (4 ny / 4 nx values) and one (r, p) pair per corner.
 template <typename T>
 struct HaloBufs {
-  T* send[4];
-  T* recv[4];
+  T* send[kHaloSlots];
+  T* recv[kHaloSlots];
 };
 
 }  // namespace pmx

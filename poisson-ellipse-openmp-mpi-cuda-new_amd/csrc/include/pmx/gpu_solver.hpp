@@ -63,24 +63,41 @@ struct GpuOptions {
   // updated every iteration, 2 = paired but always re-reading p^{k-1} (no recovery; test and
   // ablation).  The environment variable PMX_PAIR_W=0|1|2 overrides it.
   int pair_w = 1;
-  // Iteration algorithm: 2 = pcg2 (k_pcg_a + k_pcg_b, two reductions), 1 = pcg1 (single-pass
-  // k_pcg1, one reduction; subdomains without neighbours), -1 = auto (pcg1 where it applies:
-  // wave kernels, not exact, no neighbours, fp64 storage).  PMX_ALGO=-1|1|2 overrides.  Default auto: pcg1
-  // matches the reference iteration counts and pcg2's solution on the GPU (tests/test_gpu_pcg1.py)
-  // and is 5-11% faster on one GPU (profiles/NOTES_perf_experiments.md #22).
+  // Iteration algorithm: 2 = pcg2 (k_pcg_a + k_pcg_b, two reductions, radius-1 halo), 1 = pcg1
+  // (single-pass k_pcg1, one 5-value reduction, radius-2 halo with corners), -1 = auto (pcg1
+  // where it applies: wave kernels, not exact, fp64 storage, every subdomain >= 2 x 2 and the 5th
+  // field fits into the device).  The choice depends only on global data (problem, process grid,
+  // options, device size), so every rank of a distributed run makes the same one.
+  // PMX_ALGO=-1|1|2 overrides.  pcg1 matches the reference iteration counts and pcg2's solution
+  // (tests/test_gpu_pcg1.py) and moves 40 instead of 56 B/pt per iteration.
   int algo = -1;
   // pcg1 tile shape (rows1 = 0: auto).  VEC=2 x 1 wave/workgroup won the 16384^2 sweeps
   // (bench/gpu_pcg1_sweep.sh; VEC=4 needs 256 VGPRs and is 35% slower).
   int vec1 = 2, waves1 = 1, rows1 = 0;
+  bool resolved = false;  // environment overrides already applied (resolve_options)
 };
 
+// Environment overrides (PMX_ALGO, PMX_PAIR_W, PMX_PCG1_*) applied to a copy of `opt`.
+GpuOptions resolve_options(const GpuOptions& opt);
+// Single-pass (pcg1) or two-sweep (pcg2) iteration for this problem/process grid/options.  A pure
+// function of global data (see GpuOptions::algo); `device_total_bytes` = 0 skips the size test.
+// `subdomains_per_device` subdomains share one device (LocalComm: all of them).
+bool choose_single_pass(const ProblemSpec& spec, const ProcGrid& grid, const GpuOptions& resolved,
+                        double device_total_bytes, int subdomains_per_device);
+
+// The comm arena: PcgState (the all-reduce buffers) and one send + one receive buffer per halo
+// slot (pmx/device_types.hpp kHaloSlots), all sends first, then all receives.
 struct CommLayout {
   size_t state_off = 0;          // PcgState
-  size_t send_off[4] = {0, 0, 0, 0};
-  size_t recv_off[4] = {0, 0, 0, 0};
-  int edge_len[4] = {0, 0, 0, 0};
+  size_t send_off[kHaloSlots] = {};
+  size_t recv_off[kHaloSlots] = {};
+  int edge_len[kHaloSlots] = {};  // elements per message (0: slot unused by this algorithm)
+  int peer[kHaloSlots] = {-1, -1, -1, -1, -1, -1, -1, -1};  // rank across the slot, -1 = none
   size_t elem = 8;               // bytes per halo element
   size_t bytes = 0;              // total arena size
+  bool single_pass = false;
+  // slot s carries a message in this layout
+  bool active(int s) const { return peer[s] >= 0 && edge_len[s] > 0; }
 };
 
 class GpuSubdomainSolver {
@@ -91,12 +108,16 @@ class GpuSubdomainSolver {
   GpuSubdomainSolver(const GpuSubdomainSolver&) = delete;
   GpuSubdomainSolver& operator=(const GpuSubdomainSolver&) = delete;
 
-  static CommLayout comm_layout(const Subdomain& sd, DType dtype);
-  // Upper bound of the device memory a solver for `sd` allocates (fields, tables, partials,
-  // comm arena).  Checked against hipMemGetInfo before allocating; used by `pmx --plan`.
-  static size_t estimate_device_bytes(const ProblemSpec& spec, const Subdomain& sd, DType dtype);
+  static CommLayout comm_layout(const Subdomain& sd, DType dtype, bool single_pass);
+  // Upper bound of the device memory a solver for `sd` allocates (fields -- 4, or 5 for the
+  // single-pass iteration -- tables, partials, comm arena).  Checked against hipMemGetInfo before
+  // allocating; used by `pmx --plan` and the pcg1/pcg2 choice.
+  static size_t estimate_device_bytes(const ProblemSpec& spec, const Subdomain& sd, DType dtype,
+                                      bool single_pass);
 
-  void enqueue_init(hipStream_t s);     // r=B, w=0, p=0, state reset, red_b <- (0, zr_0)
+  // r=B, w=0, p=0, state reset, red_b <- (0, zr_0).  Single-pass: the driver then runs the ghost
+  // exchange of r^0 (decomposed grids), sweep 0 (enqueue_phase_a) and the all-reduce of red_c.
+  void enqueue_init(hipStream_t s);
   void enqueue_phase_a(hipStream_t s);  // k_pcg_a + reduce -> red_a
   // the two halves of each phase, for per-step timing (PcgDriver::profile_phases)
   void enqueue_kernel_a(hipStream_t s);
@@ -105,7 +126,11 @@ class GpuSubdomainSolver {
   void enqueue_reduce_b(hipStream_t s);
   // k_pcg_b + reduce -> red_b, it += 1.  pack=false: the edges were packed by enqueue_pack.
   void enqueue_phase_b(hipStream_t s, bool pack = true);
-  void enqueue_pack(hipStream_t s);     // k_edge_r: r^{k+1} edges -> send buffers
+  void enqueue_pack(hipStream_t s);     // pcg2, k_edge_r: r^{k+1} edges -> send buffers
+  // pcg1: radius-2 edges (2 lines of r and p per side, corner values) of the buffers the next
+  // sweep reads -> send buffers / receive buffers -> ghost cells of those buffers
+  void enqueue_halo_pack(hipStream_t s);
+  void enqueue_halo_unpack(hipStream_t s);
   void enqueue_poison_recv(hipStream_t s);  // recv buffers <- NaN (poison_halos debug mode)
 
   // Checkpoint: the 4 fields with ghosts, the PCG scalars and the halo buffers,
@@ -121,6 +146,10 @@ class GpuSubdomainSolver {
   PcgState* state_dev() const { return state_; }
   double* red_a_dev() const { return state_->red_a; }
   double* red_b_dev() const { return state_->red_b; }
+  double* red_c_dev() const { return state_->red_c; }
+  // all-reduce buffer `which` (0: red_a, 1 value; 1: red_b, 2; 2: red_c, 5) and its length
+  double* reduce_buf(int which) const { return which == 0 ? red_a_dev() : which == 1 ? red_b_dev() : red_c_dev(); }
+  static int reduce_len(int which) { return which == 0 ? 1 : which == 1 ? 2 : 5; }
   void* send_dev(int side) const { return arena_ + layout_.send_off[side]; }
   void* recv_dev(int side) const { return arena_ + layout_.recv_off[side]; }
   const CommLayout& layout() const { return layout_; }
@@ -151,7 +180,10 @@ class GpuSubdomainSolver {
   template <typename T> void phase_a_kernel_only(hipStream_t s);
   template <typename T> void phase_b_kernel_only(hipStream_t s, bool pack = true);
   template <typename T> HaloBufs<T> halo() const;
+  template <typename T> void halo_impl(hipStream_t s, bool unpack);
   void after_launch(hipStream_t s) const;
+  void construct(uintptr_t external_arena);
+  void release() noexcept;  // frees every allocation (destructor, failed constructor)
 
   ProblemSpec spec_;
   Subdomain sd_;
@@ -166,10 +198,11 @@ class GpuSubdomainSolver {
   TileCfg init_tiles_{};
   CommLayout layout_{};
   size_t elem_ = 8, field_bytes_ = 0, field_off_ = 0;
-  char* fields_ = nullptr;  // 4 fields
+  char* fields_ = nullptr;  // 4 fields, rows -1 .. nx+2
   char* r2_ = nullptr;      // pcg1 only: the second r buffer (r is double-buffered there)
   double* tables_buf_ = nullptr;
   double* partials_ = nullptr;
+  size_t npart_ = 0;
   double* reduce_ws_ = nullptr;  // k_reduce chunk sums + ticket (inside the partials allocation)
   char* arena_ = nullptr;
   bool own_arena_ = true;
@@ -222,6 +255,10 @@ struct RunStats {
 
 class PcgDriver {
  public:
+  // All local solvers must run the same iteration algorithm (checked).  The single-pass
+  // iteration runs: sweep -> 5-value reduction -> ONE all-reduce (red_c); on decomposed grids the
+  // radius-2 ghost exchange (pack -> send/recv -> unpack) runs on the comm stream, overlapped with
+  // the reduction and the all-reduce, and the next sweep waits for it.
   PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int graph_batch);
   ~PcgDriver();
 
@@ -241,6 +278,7 @@ class PcgDriver {
 
  private:
   void enqueue_one_iteration();
+  void halo_exchange_pcg1(std::vector<hipStream_t>& streams);  // pack -> comm -> unpack
   void build_graph();
   template <typename F> void for_each_stream(F&& f);
   void poison(std::vector<hipStream_t>& streams);
@@ -252,6 +290,8 @@ class PcgDriver {
   // halo/compute overlap: one comm stream per compute stream, fork/join events per iteration
   bool overlap_ = false;
   bool poison_ = false;
+  bool single_pass_ = false;
+  bool any_nb_ = false;
   std::vector<hipStream_t> comm_streams_;
   std::vector<hipEvent_t> ev_packed_, ev_halo_;
   bool graph_ok_ = false;

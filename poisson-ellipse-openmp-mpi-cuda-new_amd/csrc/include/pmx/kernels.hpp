@@ -75,11 +75,18 @@ void launch_pcg_b_wave(const DevGeom& G, const DevTables& Tb, T* w, T* r, const 
 
 // Single-pass PCG iteration (pcg1_kernels.hip): p^k, A p^k, w, r^k, z^k, A z^k in one sweep,
 // 5 partials per tile (rho, (Az,z), (Az,p), (Ap,p), |p|^2).  S->it == 0 is the init sweep.
-// Subdomains without neighbours only (G.nb == 0).  r is double-buffered (overlapped tiles read
-// neighbour rows/columns of r^{k-1} while others write r^k): sweep k reads (k & 1 ? r2 : r).
+// r is double-buffered (overlapped tiles read neighbour rows/columns of r^{k-1} while others
+// write r^k): sweep k reads (k & 1 ? r2 : r).  Decomposed grids read the radius-2 ghosts that
+// launch_pcg1_halo unpacked into the fields.
 template <typename T>
 void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1,
                  double* partials, PcgState* S, const TileCfg& tc, hipStream_t s);
+
+// pcg1 ghost exchange: pack (unpack=false) the radius-2 edges of the buffers the next sweep reads
+// (selected on the device by S->halo_k) into H.send, or unpack H.recv into their ghost cells.
+template <typename T>
+void launch_pcg1_halo(const DevGeom& G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, const PcgState* S,
+                      bool unpack, hipStream_t s);
 
 // Halo/compute overlap: r^{k+1} on the subdomain edges that have a neighbour,
 // written to the send buffers only, with exactly the arithmetic of pcg_b.  Runs first so the

@@ -52,28 +52,47 @@ class SingleComm:
 
 
 class TorchComm:
-    def __init__(self, group=None):
+    """torch.distributed collectives.  ``stage_host`` (default: on for a gloo group) copies device
+    tensors through host memory around each call -- gloo has no device P2P -- which is how several
+    ranks that share ONE GPU exercise the native multi-rank solver (RCCL refuses two ranks on one
+    device)."""
+
+    def __init__(self, group=None, stage_host: bool | None = None):
         if not dist.is_initialized():
             raise RuntimeError("torch.distributed is not initialised (see parallel.launch.init_distributed)")
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        self.backend = dist.get_backend(group)
+        self.stage_host = (self.backend == "gloo") if stage_host is None else stage_host
+
+    def _host(self, t: torch.Tensor) -> torch.Tensor:
+        return t.cpu() if (self.stage_host and t.device.type != "cpu") else t
 
     def allreduce_(self, t: torch.Tensor) -> torch.Tensor:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        h = self._host(t)
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+        if h is not t:
+            t.copy_(h)
         return t
 
     def exchange(self, sends, recvs, nbs) -> None:
-        """sends[s] -> neighbour nbs[s] (it lands in that rank's recvs[s^1]); recvs[s] <- nbs[s]."""
-        ops = []
+        """sends[s] -> rank nbs[s] (it lands in that rank's recvs[opposite(s)]); recvs[s] <- nbs[s].
+        Any number of slots (4 sides for pcg2 / TorchPCG, 4 sides + 4 corners for pcg1)."""
+        ops, back = [], []
         for s, nb in enumerate(nbs):
-            if nb < 0:
+            if nb < 0 or sends[s] is None or sends[s].numel() == 0:
                 continue
-            ops.append(dist.P2POp(dist.isend, sends[s], nb, self.group))
-            ops.append(dist.P2POp(dist.irecv, recvs[s], nb, self.group))
+            snd, rcv = self._host(sends[s]), self._host(recvs[s])
+            if rcv is not recvs[s]:
+                back.append((recvs[s], rcv))
+            ops.append(dist.P2POp(dist.isend, snd, nb, self.group))
+            ops.append(dist.P2POp(dist.irecv, rcv, nb, self.group))
         if ops:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
+        for dev, host in back:
+            dev.copy_(host)
 
     def barrier(self):
         dist.barrier(group=self.group)

@@ -60,3 +60,20 @@ def subdomain(M: int, N: int, Px: int, Py: int, rank: int) -> dict:
                 nb_xlo=rank - 1 if px > 0 else -1, nb_xhi=rank + 1 if px < Px - 1 else -1,
                 nb_ylo=rank - Px if py > 0 else -1, nb_yhi=rank + Px if py < Py - 1 else -1,
                 aspect=max(nx, ny) / min(nx, ny))
+
+
+# halo slots (csrc/include/pmx/device_types.hpp kHaloSlots): 4 sides, then 4 corners
+SLOT_OFFSETS = ((-1, 0), (1, 0), (0, -1), (0, 1), (-1, -1), (-1, 1), (1, -1), (1, 1))
+
+
+def opposite_slot(s: int) -> int:
+    return s ^ 1 if s < 4 else 11 - s
+
+
+def peers(sd: dict) -> list[int]:
+    """Rank across each of the 8 halo slots (-1 = none); mirror of Subdomain::peer."""
+    out = []
+    for dx, dy in SLOT_OFFSETS:
+        qx, qy = sd["px"] + dx, sd["py"] + dy
+        out.append(qy * sd["Px"] + qx if 0 <= qx < sd["Px"] and 0 <= qy < sd["Py"] else -1)
+    return out

@@ -4,18 +4,28 @@ Two communicators, same fused HIP kernels:
 
 * ``comm="native"`` -- the production path.  Rank 0 creates an ncclUniqueId, it is broadcast
   over torch.distributed, and every rank builds its own RCCL communicator inside the native
-  Session (csrc/comm/comm.hip).  Halos (ncclSend/ncclRecv in one group) and the two scalar
-  all-reduces per iteration are issued from C++ on the solver's stream, optionally captured in a
-  hipGraph together with the kernels.
+  Session (csrc/comm/comm.hip).  Halos (ncclSend/ncclRecv in one group) and the scalar
+  all-reduce(s) are issued from C++ on the solver's streams and captured in the hipGraph
+  together with the kernels (``rccl_graph=True``, the default).
 * ``comm="torch"`` -- the portable path.  The native SubdomainSolver runs its kernels on torch's
   current stream and keeps its scalars/halo buffers in a torch-allocated arena; the all-reduces
-  and the ghost exchange go through torch.distributed (ProcessGroupNCCL = RCCL).
+  and the ghost exchange go through torch.distributed: ProcessGroupNCCL (= RCCL) on GPUs, or
+  gloo with the buffers staged through host memory -- which lets 2..16 processes share ONE GPU
+  and run the real native multi-rank iteration (RCCL refuses two ranks on one device).
+
+Lifecycle hardening (reference: MPI_Init/MPI_Finalize, stage4-mpi+cuda/poisson_mpi_cuda_f.cu:
+987-1037): the native path builds every rank's solver first, agrees collectively that all ranks
+succeeded, and only then enters the blocking RCCL initialisation, under a watchdog that ends the
+process if the initialisation hangs (the launcher then stops the other ranks).
 
 Replaces the reference's MPI+CUDA driver (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:688-983,986-1039):
 no host staging, no per-iteration host synchronisation, explicit rank->device binding.
 """
 from __future__ import annotations
 
+import os
+import sys
+import threading
 import time
 
 import numpy as np
@@ -25,20 +35,72 @@ import torch.distributed as dist
 from ..models.solvers import Result
 from ..utils.native import load as _native
 from .comm import TorchComm
-from .decomp import process_grid
+from .decomp import process_grid, subdomain
 from .launch import DistInfo
+
+# stage-4 Table 2 buckets (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980)
+PHASE_BUCKETS = ("compute", "copy", "comm", "precond", "dot")
+PHASE_LABELS = {
+    "compute": "GPU compute time (Ap + D^{-1}r, max over ranks)",
+    "copy": "Host<->Device copy time (max over ranks)       ",
+    "comm": "MPI halo exchange time (max over ranks)        ",
+    "precond": "Preconditioner CPU part time (max over ranks)  ",
+    "dot": "Dot products time (max over ranks)             ",
+}
+
+
+def _comm_device(info: DistInfo, device: int):
+    """Device for torch.distributed tensors: the GPU for nccl, host memory for gloo."""
+    return torch.device("cuda", device) if info.backend == "nccl" else torch.device("cpu")
+
+
+def agree(info: DistInfo, ok: bool, what: str, device: int = 0) -> None:
+    """Collective success check: raises on EVERY rank if any rank reports failure."""
+    if info.world > 1:
+        t = torch.tensor([0 if ok else 1], dtype=torch.int32, device=_comm_device(info, device))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        bad = int(t.item())
+    else:
+        bad = 0 if ok else 1
+    if bad:
+        raise RuntimeError(f"{what} failed on at least one rank (rank {info.rank}: {'ok' if ok else 'failed'})")
+
+
+class _Watchdog:
+    """Ends the process if a blocking collective setup does not finish in time: a rank stuck in
+    ncclCommInitRank cannot be interrupted, and a dead rank is what lets the launcher (torchrun or
+    bench.py's spawner) stop the others instead of hanging the job."""
+
+    def __init__(self, seconds: float, what: str):
+        self.what = what
+        self.timer = threading.Timer(seconds, self._fire) if seconds > 0 else None
+
+    def _fire(self):
+        print(f"[pmx] {self.what} did not finish in time; aborting this rank", file=sys.stderr, flush=True)
+        os._exit(86)
+
+    def __enter__(self):
+        if self.timer:
+            self.timer.daemon = True
+            self.timer.start()
+        return self
+
+    def __exit__(self, *exc):
+        if self.timer:
+            self.timer.cancel()
+        return False
 
 
 class DistGpuPCG:
     def __init__(self, problem, info: DistInfo, comm: str = "native", split: str = "reference",
                  dtype: str = "fp64", kernel: str = "wave", block: int = 256, vec: int = 0, waves: int = 4,
-                 tile_rows: int = 0, exact: bool = False, graph_batch: int = 32, rccl_graph: bool = False,
+                 tile_rows: int = 0, exact: bool = False, graph_batch: int = 32, rccl_graph: bool = True,
                  overlap: bool = True, vec_b: int = 0, waves_b: int = 0, tile_rows_b: int = -1,
-                 b_ring: bool = False):
+                 b_ring: bool = False, algo: int = -1, init_timeout: float = 300.0, device: int | None = None):
         self.problem = problem
         self.info = info
         self.comm_kind = comm
-        self.device = info.local_rank
+        self.device = info.local_rank if device is None else device
         self.n = _native()
         self.spec = problem.to_native()
         self.Px, self.Py = process_grid(info.world, problem.M, problem.N, split)
@@ -48,17 +110,32 @@ class DistGpuPCG:
             uid = [self.n.rccl_unique_id() if info.rank == 0 else None]
             if info.world > 1:
                 dist.broadcast_object_list(uid, src=0)
-            self.session = self.n.Session(self.spec, world=info.world, comm="rccl",
-                                          split=getattr(self.n.Split, split), device=self.device,
-                                          kernel=kernel, block=block, vec=vec, waves=waves,
-                                          tile_rows=tile_rows, dtype=dtype, exact=exact,
-                                          graph_batch=graph_batch if rccl_graph else 0, uid=uid[0],
-                                          ranks=[info.rank], devices=[self.device], rccl_graph=rccl_graph,
-                                          overlap=overlap, vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b,
-                                          b_ring=b_ring)
+            self.session, err = None, None
+            try:
+                self.session = self.n.Session(
+                    self.spec, world=info.world, comm="rccl", split=getattr(self.n.Split, split),
+                    device=self.device, kernel=kernel, block=block, vec=vec, waves=waves, tile_rows=tile_rows,
+                    dtype=dtype, exact=exact, graph_batch=graph_batch if rccl_graph else 0, uid=uid[0],
+                    ranks=[info.rank], devices=[self.device], rccl_graph=rccl_graph, overlap=overlap,
+                    vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b, b_ring=b_ring, algo=algo,
+                    defer_connect=True)
+            except Exception as e:  # sizing / allocation: reported collectively below
+                err = e
+            agree(info, err is None, f"native solver setup ({err})" if err else "native solver setup",
+                  self.device)
+            with _Watchdog(init_timeout, "RCCL communicator initialisation"):
+                try:
+                    self.session.connect()
+                    err = None
+                except Exception as e:
+                    err = e
+                agree(info, err is None, f"RCCL communicator initialisation ({err})", self.device)
             self.sd = self.session.subdomain(0)
+            self.single_pass = self.session.tile["algo"] == "pcg1"
         elif comm == "torch":
-            lay = self.n.comm_layout(problem.M, problem.N, self.Px, self.Py, info.rank, dtype)
+            lay = self.n.comm_layout(self.spec, self.Px, self.Py, info.rank, dtype=dtype, kernel=kernel,
+                                     exact=exact, device=self.device, algo=algo)
+            self.single_pass = bool(lay["single_pass"])
             self.arena = torch.zeros(lay["bytes"] + 256, dtype=torch.uint8, device=f"cuda:{self.device}")
             base = self.arena.data_ptr()
             pad = (-base) % 256
@@ -67,16 +144,21 @@ class DistGpuPCG:
                                                  kernel=kernel, block=block, vec=vec, waves=waves,
                                                  tile_rows=tile_rows, dtype=dtype, exact=exact, arena=base + pad,
                                                  vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b,
-                                                 b_ring=b_ring)
+                                                 b_ring=b_ring, algo=1 if self.single_pass else 2)
+            assert self.solver.single_pass == self.single_pass
             self.sd = self.solver.subdomain()
             tdt = torch.float64 if dtype == "fp64" else torch.float32
             el = lay["elem"]
             so = lay["state_off"]
-            self.red_a = self.arena_view[so + lay["red_a_off"]: so + lay["red_a_off"] + 8].view(torch.float64)
-            self.red_b = self.arena_view[so + lay["red_b_off"]: so + lay["red_b_off"] + 16].view(torch.float64)
+
+            def scal(off, n):
+                return self.arena_view[so + off: so + off + 8 * n].view(torch.float64)
+
+            self.red_a, self.red_b, self.red_c = scal(lay["red_a_off"], 1), scal(lay["red_b_off"], 2), \
+                scal(lay["red_c_off"], 5)
             self.sends = [self.arena_view[o:o + n * el].view(tdt) for o, n in zip(lay["send_off"], lay["edge_len"])]
             self.recvs = [self.arena_view[o:o + n * el].view(tdt) for o, n in zip(lay["recv_off"], lay["edge_len"])]
-            self.nbs = [self.sd[k] for k in ("nb_xlo", "nb_xhi", "nb_ylo", "nb_yhi")]
+            self.peers = [p if n > 0 else -1 for p, n in zip(lay["peer"], lay["edge_len"])]
             self.tcomm = TorchComm() if info.world > 1 else None
         else:
             raise ValueError(f"unknown comm {comm!r}")
@@ -84,24 +166,42 @@ class DistGpuPCG:
     def tile(self) -> dict:
         if self.comm_kind == "native":
             return self.session.tile
-        return dict(ntiles=self.solver.ntiles)
+        return dict(ntiles=self.solver.ntiles, algo="pcg1" if self.single_pass else "pcg2")
 
     # ---- torch-comm path ----
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.device).cuda_stream
 
-    def _comm_b(self):
+    def _allreduce(self, t):
+        if self.tcomm is not None:
+            self.tcomm.allreduce_(t)
+
+    def _exchange(self):
+        if self.tcomm is not None:
+            self.tcomm.exchange(self.sends, self.recvs, self.peers)
+
+    def _halo1(self, s):
+        """pcg1 radius-2 ghosts: pack -> torch.distributed P2P -> unpack (all on torch's stream)."""
         if self.tcomm is None:
             return
-        self.tcomm.allreduce_(self.red_b)
-        self.tcomm.exchange(self.sends, self.recvs, self.nbs)
+        self.solver.enqueue_halo_pack(s)
+        self._exchange()
+        self.solver.enqueue_halo_unpack(s)
 
     def init(self):
         if self.comm_kind == "native":
             self.session.init()
             return
-        self.solver.enqueue_init(self._stream())
-        self._comm_b()
+        s = self._stream()
+        self.solver.enqueue_init(s)
+        if self.single_pass:  # same order as PcgDriver::init
+            self._halo1(s)
+            self.solver.enqueue_phase_a(s)
+            self._allreduce(self.red_c)
+            self._halo1(s)
+        else:
+            self._allreduce(self.red_b)
+            self._exchange()
         torch.cuda.synchronize(self.device)
 
     def step(self, n: int):
@@ -111,10 +211,14 @@ class DistGpuPCG:
         s = self._stream()
         for _ in range(n):
             self.solver.enqueue_phase_a(s)
-            if self.tcomm is not None:
-                self.tcomm.allreduce_(self.red_a)
-            self.solver.enqueue_phase_b(s)
-            self._comm_b()
+            if self.single_pass:
+                self._allreduce(self.red_c)
+                self._halo1(s)
+            else:
+                self._allreduce(self.red_a)
+                self.solver.enqueue_phase_b(s)
+                self._allreduce(self.red_b)
+                self._exchange()
 
     def synchronize(self):
         if self.comm_kind == "native":
@@ -127,11 +231,22 @@ class DistGpuPCG:
         return self.solver.read_state(self._stream())
 
     def local_w(self) -> np.ndarray:
+        """This rank's interior block of w (nx x ny, fp64)."""
         if self.comm_kind == "native":
-            g = self.session.gather_local_w()
-            sd = self.sd
-            return g[sd["i_start"]:sd["i_end"] + 1, sd["j_start"]:sd["j_end"] + 1].copy()
+            return self.session.local_w(0)
         return self.solver.download_w(self._stream())
+
+    def profile(self, n: int) -> dict:
+        """Per-phase times of n eager iterations (native path), reduced with MAX over ranks and
+        mapped onto the reference's 5 stage-4 buckets (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:
+        956-980).  Restarts the solver (init) first; values are seconds for the n iterations."""
+        if self.comm_kind != "native":
+            raise NotImplementedError("phase profiling runs on the native communicator")
+        self.session.init()
+        ph = self.session.profile(int(n))
+        vals = {"compute": ph["t_kernel_a"] + ph["t_kernel_b"], "copy": 0.0, "comm": ph["t_comm"],
+                "precond": 0.0, "dot": ph["t_reduce"]}
+        return reduce_max(vals, self.info, self.device)
 
     def solve(self, gather: bool = True, batch: int | None = None) -> Result:
         batch = batch or max(self.graph_batch, 16)
@@ -151,22 +266,49 @@ class DistGpuPCG:
         self.synchronize()
         t2 = time.perf_counter()
         res = Result(st["iters"], st["status"], st["diff"], t2 - t1, None, backend=f"hip-{self.comm_kind}",
-                     ranks=self.info.world, init_seconds=t1 - t0, extra=dict(launched=launched, nan=st["nan"]))
+                     ranks=self.info.world, init_seconds=t1 - t0,
+                     extra=dict(launched=launched, nan=st["nan"], algo=self.tile().get("algo")))
         if gather:
-            res.w = gather_solution(self.problem, self.sd, self.local_w(), self.info)
+            res.w = gather_solution(self.problem, self.sd, self.local_w(), self.info, self.device)
         return res
 
 
-def gather_solution(problem, sd: dict, local: np.ndarray, info: DistInfo):
-    """Assemble the global (M+1)x(N+1) solution on rank 0 (None elsewhere)."""
-    pieces = [(sd, local)]
+def reduce_max(vals: dict, info: DistInfo, device: int = 0) -> dict:
+    """MAX over ranks of a dict of floats (MPI_Reduce(MAX), stage4-mpi+cuda/poisson_mpi_cuda_f.cu:963-967)."""
+    keys = list(vals)
     if info.world > 1:
-        out = [None] * info.world if info.rank == 0 else None
-        dist.gather_object((sd, local), out, dst=0)
-        pieces = out
-    if info.rank != 0:
-        return None
-    g = np.zeros((problem.M + 1, problem.N + 1))
-    for s, w in pieces:
-        g[s["i_start"]:s["i_end"] + 1, s["j_start"]:s["j_end"] + 1] = w
-    return g
+        t = torch.tensor([float(vals[k]) for k in keys], dtype=torch.float64, device=_comm_device(info, device))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return {k: float(v) for k, v in zip(keys, t.tolist())}
+    return dict(vals)
+
+
+def phase_table(buckets: dict, scale: float = 1.0) -> str:
+    """The stage-4 Table 2 lines (reference stdout, stage4-mpi+cuda/poisson_mpi_cuda_f.cu:970-979)."""
+    return "\n".join(f"   {PHASE_LABELS[k]} ~ {buckets[k] * scale:.6f} s" for k in PHASE_BUCKETS)
+
+
+def gather_solution(problem, sd: dict, local: np.ndarray, info: DistInfo, device: int = 0):
+    """Assemble the global (M+1)x(N+1) solution on rank 0 (None elsewhere).
+
+    Rank by rank over point-to-point tensors (device tensors for nccl, host for gloo): rank 0 holds
+    the global array plus ONE block at a time, and nothing is pickled."""
+    if info.rank == 0:
+        g = np.zeros((problem.M + 1, problem.N + 1))
+        g[sd["i_start"]:sd["i_end"] + 1, sd["j_start"]:sd["j_end"] + 1] = local
+    if info.world == 1:
+        return g
+    cdev = _comm_device(info, device)
+    Px, Py = sd["Px"], sd["Py"]
+    if info.rank == 0:
+        for r in range(1, info.world):
+            s = subdomain(problem.M, problem.N, Px, Py, r)
+            buf = torch.empty(s["nx"] * s["ny"], dtype=torch.float64, device=cdev)
+            dist.recv(buf, src=r)
+            g[s["i_start"]:s["i_end"] + 1, s["j_start"]:s["j_end"] + 1] = \
+                buf.cpu().numpy().reshape(s["nx"], s["ny"])
+            del buf
+        return g
+    t = torch.from_numpy(np.ascontiguousarray(local, dtype=np.float64).reshape(-1)).to(cdev)
+    dist.send(t, dst=0)
+    return None

@@ -49,3 +49,38 @@ def test_bench_torchrun_dry_run(n):
     assert len(lines) == 1, p.stdout  # rank 0 only
     _check(lines[0], n, 6, 2)
     assert lines[0]["config"]["parallelism"] == f"domain{n}"
+
+
+def test_bench_spawns_its_own_ranks():
+    """Without a launcher, --gpus N starts N ranks itself (before any GPU call) and reports N."""
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--cpu-dry-run", "--M", "64", "--N", "96",
+                        "--steps", "4", "--warmup", "1"], cwd=ROOT, capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = _json_lines(p.stdout)
+    assert len(lines) == 1
+    _check(lines[0], 2, 4, 1)
+    assert lines[0]["config"]["parallelism"] == "domain2"
+
+
+def test_bench_refuses_rank_count_mismatch():
+    """A launcher that brings up fewer ranks than --gpus is an error, not a warning."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--cpu-dry-run", "--M", "32", "--N", "32",
+                        "--steps", "2", "--warmup", "1"], cwd=ROOT, capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert p.returncode != 0
+    assert "refusing" in p.stderr
+    assert not _json_lines(p.stdout)
+
+
+def test_bench_spawner_propagates_rank_failure():
+    """One failing rank fails the whole job (and the spawner stops the other rank)."""
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--cpu-dry-run", "--M", "1", "--N", "32",
+                        "--steps", "2", "--warmup", "1"], cwd=ROOT, capture_output=True, text=True, timeout=300,
+                       env=env)
+    assert p.returncode != 0

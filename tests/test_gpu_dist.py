@@ -1,0 +1,80 @@
+"""Multi-process runs of the native GPU solver on ONE GPU (the production multi-rank code path).
+
+RCCL refuses two ranks on one device, so these tests start 2..8 processes that share GPU 0 and
+exchange the PCG scalars and the ghost lines over gloo, staged through host memory
+(parallel/comm.py TorchComm(stage_host=True)).  Everything else is what an 8-GPU run executes:
+DistGpuPCG, the native SubdomainSolver with its comm arena, the pcg1 radius-2 halo pack/unpack
+kernels (8 slots incl. corners) or the pcg2 edge packing, the init/iteration order and the
+tensor gather.  Reference: stage4-mpi+cuda/poisson_mpi_cuda_f.cu:331-500 (halo), 843-943
+(iteration), 986-1011 (rank setup).
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, free_port
+
+pytestmark = pytest.mark.gpu
+WORKER = os.path.join(ROOT, "tests", "dist_worker.py")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu(pkg):
+    assert torch.cuda.is_available() and pkg.load_native().device_count() > 0, "no HIP device"
+
+
+def _run(tmp_path, world, M, N, algo=-1, split="reference", dtype="fp64"):
+    out = str(tmp_path / f"w{world}_{algo}_{split}")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), WORKER, "--M", str(M), "--N", str(N),
+           "--algo", str(algo), "--split", split, "--dtype", dtype, "--out", out]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=170, env=env)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
+    with open(out + ".json") as f:
+        meta = json.load(f)
+    return meta, np.load(out + ".npy")
+
+
+@pytest.mark.parametrize("world,split,algo,expect", [
+    (2, "reference", -1, "pcg1"),   # auto picks the single pass on decomposed fp64 grids
+    (3, "cols", 1, "pcg1"),
+    (4, "reference", 1, "pcg1"),    # 2 x 2: every rank has 2 sides + 1 corner
+    (6, "auto", 1, "pcg1"),         # 3 x 2 / 2 x 3: middle ranks have corners on both sides
+    (4, "reference", 2, "pcg2"),
+    (3, "rows", 2, "pcg2"),
+])
+def test_native_multiprocess_matches_single_rank(pkg, tmp_path, world, split, algo, expect):
+    M, N = 400, 600
+    meta, w = _run(tmp_path, world, M, N, algo, split)
+    assert meta["world"] == world and meta["algo"] == expect
+    ref = pkg.solve(pkg.PoissonEllipse(M=M, N=N), "hip", ranks=1)
+    assert meta["iters"] == ref.iters == 546 and meta["status"] == "converged"
+    assert np.abs(w - ref.w).max() < 1e-11
+
+
+def test_native_multiprocess_odd_blocks(pkg, tmp_path):
+    """Uneven block sizes (odd nx/ny, the last chunk of a row straddling the ghost column)."""
+    M, N = 211, 157
+    meta, w = _run(tmp_path, 4, M, N, 1, "reference")
+    ref = pkg.solve(pkg.PoissonEllipse(M=M, N=N), "hip", ranks=1)
+    assert meta["iters"] == ref.iters
+    assert np.abs(w - ref.w).max() < 1e-11
+
+
+def test_bench_share_gpu_rehearsal(tmp_path):
+    """bench.py --gpus 2 spawns its own ranks; --share-gpu runs them on GPU 0 (valid=false)."""
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--share-gpu", "--M", "512", "--N", "512",
+                        "--steps", "20", "--warmup", "4", "--tol-time-cap", "60"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=170)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    j = lines[0]
+    assert j["n_gpus"] == 2 and j["valid"] is False and j["tol_status"] == "converged"
+    assert j["config"]["comm"] == "gloo-host-staged" and j["config"]["tile"]["algo"] == "pcg1"

@@ -1,9 +1,12 @@
-"""Single-pass PCG iteration (pcg1, csrc/hip/pcg1_kernels.hip, opt-in with PMX_ALGO=1).
+"""Single-pass PCG iteration (pcg1, csrc/hip/pcg1_kernels.hip).
 
-pcg1 forms alpha's denominator (A p^k, p^k) from the previous sweep's partials instead of a second
-sweep; r is still updated with an explicitly computed A p^k.  These tests pin it to the default
-two-sweep iteration (pcg2) and to the reference's iteration counts
-(stage4-mpi+cuda/poisson_mpi_cuda_f.cu:847-943 convergence rule, SURVEY §4.1 goldens).
+pcg1 is the automatic choice in fp64 with the wave kernels and the fast arithmetic -- on one
+subdomain and on decomposed grids (radius-2 halo with corner exchange) alike; PMX_ALGO=1/2 forces
+one algorithm.  It forms alpha's denominator (A p^k, p^k) from the previous sweep's partials
+instead of a second sweep; r is still updated with an explicitly computed A p^k.  These tests pin
+it to the two-sweep iteration (pcg2) and to the reference's iteration counts
+(stage4-mpi+cuda/poisson_mpi_cuda_f.cu:847-943 convergence rule; SURVEY §4.1 goldens, including
+the published stage-4 grids 1600x2400 -> 1858 and 2400x3200 -> 2449).
 """
 import numpy as np
 import pytest
@@ -11,7 +14,8 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-WEIGHTED = {(10, 10): 15, (20, 20): 26, (40, 40): 50, (400, 600): 546, (800, 1200): 989}
+WEIGHTED = {(10, 10): 15, (20, 20): 26, (40, 40): 50, (400, 600): 546, (800, 1200): 989,
+            (1600, 2400): 1858, (2400, 3200): 2449}
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -51,10 +55,48 @@ def test_pcg1_matches_cpu_oracle(pkg, monkeypatch):
     (1, {}, "pcg1"),                  # fp64, one subdomain: single pass
     (1, {"dtype": "fp32"}, "pcg2"),   # fp32 storage: pcg2 is faster (NOTES #26)
     (1, {"exact": True}, "pcg2"),     # reference arithmetic order
-    (2, {}, "pcg2"),                  # subdomains with neighbours
+    (2, {}, "pcg1"),                  # decomposed: radius-2 halo
+    (8, {}, "pcg1"),
+    (2, {"dtype": "fp32"}, "pcg2"),
+    (2, {"kernel": "lds"}, "pcg2"),
 ])
 def test_auto_algorithm_selection(pkg, monkeypatch, ranks, kw, algo):
     monkeypatch.delenv("PMX_ALGO", raising=False)
     from conftest import sub
     s = sub("models").make_session(pkg.PoissonEllipse(M=200, N=300), ranks=ranks, **kw)
     assert s.tile["algo"] == algo
+
+
+def test_auto_falls_back_for_thin_subdomains(pkg, monkeypatch):
+    """Blocks of one row cannot feed a radius-2 halo: auto picks pcg2, forcing pcg1 fails."""
+    from conftest import sub
+    monkeypatch.delenv("PMX_ALGO", raising=False)
+    p = pkg.PoissonEllipse(M=4, N=300)
+    s = sub("models").make_session(p, ranks=3, split="rows")
+    assert s.tile["algo"] == "pcg2"
+    monkeypatch.setenv("PMX_ALGO", "1")
+    with pytest.raises(RuntimeError, match="2 x 2"):
+        sub("models").make_session(p, ranks=3, split="rows")
+
+
+@pytest.mark.parametrize("ranks,split", [(2, "reference"), (3, "cols"), (4, "reference"), (6, "auto"),
+                                         (7, "auto"), (8, "reference"), (9, "reference")])
+@pytest.mark.parametrize("grid", [(400, 600), (211, 157)])
+def test_pcg1_decomposed_matches_single_subdomain(pkg, monkeypatch, ranks, split, grid):
+    """LocalComm (P subdomains on one GPU): pcg1 with the radius-2 ghost exchange gives the
+    single-subdomain iteration count and solution; odd block sizes included."""
+    p = pkg.PoissonEllipse(M=grid[0], N=grid[1])
+    ref = _solve(pkg, monkeypatch, 1, p)
+    r = _solve(pkg, monkeypatch, 1, p, ranks=ranks, split=split)
+    assert r.iters == ref.iters
+    assert np.abs(r.w - ref.w).max() < 1e-11
+
+
+@pytest.mark.parametrize("graph_batch", [0, 16])
+def test_pcg1_decomposed_overlap_bitwise(pkg, monkeypatch, graph_batch):
+    """Halo on the comm stream (overlapped with reduce + all-reduce) == serial halo, bitwise."""
+    p = pkg.PoissonEllipse(M=400, N=600)
+    a = _solve(pkg, monkeypatch, 1, p, ranks=4, overlap=False, graph_batch=graph_batch)
+    b = _solve(pkg, monkeypatch, 1, p, ranks=4, overlap=True, graph_batch=graph_batch)
+    assert a.iters == b.iters == 546
+    assert np.array_equal(a.w, b.w)

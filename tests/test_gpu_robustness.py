@@ -64,12 +64,16 @@ def test_poisoned_halos_change_nothing_when_exchange_is_complete(pkg, overlap):
     assert np.array_equal(s.gather_local_w(), ref.w)
 
 
-def test_poisoned_halo_without_exchange_raises_nan_flag(pkg, native):
-    """A ghost that never arrives stays NaN and trips the device NaN flag in the reductions."""
+@pytest.mark.parametrize("algo", [1, 2])
+def test_poisoned_halo_without_exchange_raises_nan_flag(pkg, native, algo):
+    """A ghost that never arrives stays NaN and trips the device NaN flag in the reductions
+    (pcg2 reads the receive buffers directly; pcg1 unpacks them into the ghost cells)."""
     p = pkg.PoissonEllipse(M=200, N=300)
-    s0 = native.SubdomainSolver(p.to_native(), Px=1, Py=2, rank=0)
+    s0 = native.SubdomainSolver(p.to_native(), Px=1, Py=2, rank=0, algo=algo)
+    assert s0.single_pass == (algo == 1)
     s0.enqueue_init(0)
     s0.enqueue_poison_recv(0)  # ... and no exchange
+    s0.enqueue_halo_unpack(0)  # pcg1 only (no-op for pcg2)
     s0.enqueue_phase_a(0)
     st = s0.read_state(0)
     assert st["nan"]

@@ -212,6 +212,7 @@ def test_paired_w_modes(pkg, monkeypatch, grid, iters, dtype):
     with p^{k-1} recovered (mode 1) or re-read (mode 2).  Both match w updated every iteration
     (mode 0) -- stops on even (546) and odd (989) iterations included."""
     p = pkg.PoissonEllipse(M=grid[0], N=grid[1])
+    monkeypatch.setenv("PMX_ALGO", "2")  # paired-w modes belong to the two-sweep row kernel
     res = {}
     for mode in (0, 1, 2):
         monkeypatch.setenv("PMX_PAIR_W", str(mode))
@@ -230,6 +231,7 @@ def test_paired_w_midrun_materialised(pkg, monkeypatch, steps):
     """w read after an odd number of iterations includes the deferred step."""
     p = pkg.PoissonEllipse(M=300, N=200)
     models = sub("models")
+    monkeypatch.setenv("PMX_ALGO", "2")  # pcg1 always pairs (its own tests cover it)
     out = {}
     for mode in (0, 1):
         monkeypatch.setenv("PMX_PAIR_W", str(mode))
