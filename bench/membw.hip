@@ -7,7 +7,9 @@
 //               512-column strip (the tile-marching order of the fused kernels)
 //   rowband5  : 5 streams, one block per (row, 512-col chunk), rows assigned so that each XCD
 //               works on its own contiguous band of rows (T1-style XCD-aware mapping)
-// Usage: membw [N] [rows]
+// Usage: membw [N] [rows] [reps] [fill]   (reps = timed launches per kernel, default 10; fill 1 =
+// non-zero data: HBM power depends on the bit patterns, and sustained runs of >= 1 s show the
+// clock/power-limited steady state instead of the first-launch burst)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -103,6 +105,8 @@ k_rowband5(const double* p, double* w, double* r, int n, int pitch, int chunks, 
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 16384;
   const int rows = argc > 2 ? atoi(argv[2]) : 64;
+  const int reps = argc > 3 ? atoi(argv[3]) : 10;
+  const int fill = argc > 4 ? atoi(argv[4]) : 0;
   const int pitch = n + 32;
   const size_t elems = size_t(n) * pitch;
   const size_t bytes = elems * 8;
@@ -113,13 +117,20 @@ int main(int argc, char** argv) {
   CK(hipMemset(p, 0, bytes));
   CK(hipMemset(w, 0, bytes));
   CK(hipMemset(r, 0, bytes));
+  if (fill) {  // pseudo-random doubles in [0.5, 1): the +/-0.5 updates keep them finite
+    std::vector<double> h(elems);
+    unsigned long long x = 88172645463325252ull;
+    for (auto& v : h) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; v = 0.5 + double(x >> 11) * 0x1.0p-54; }
+    CK(hipMemcpy(p, h.data(), bytes, hipMemcpyHostToDevice));
+    CK(hipMemcpy(w, h.data(), bytes, hipMemcpyHostToDevice));
+    CK(hipMemcpy(r, h.data(), bytes, hipMemcpyHostToDevice));
+  }
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   auto timeit = [&](const char* name, double gb, auto launch) {
     for (int w_ = 0; w_ < 3; ++w_) launch();
     CK(hipDeviceSynchronize());
-    const int reps = 10;
     CK(hipEventRecord(e0));
     for (int k = 0; k < reps; ++k) launch();
     CK(hipEventRecord(e1));
@@ -127,7 +138,9 @@ int main(int argc, char** argv) {
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     ms /= reps;
-    printf("{\"kernel\": \"%s\", \"n\": %d, \"ms\": %.4f, \"TBps\": %.3f}\n", name, n, ms, gb / ms);
+    printf("{\"kernel\": \"%s\", \"n\": %d, \"reps\": %d, \"fill\": %d, \"ms\": %.4f, \"TBps\": %.3f}\n", name, n,
+           reps, fill, ms, gb / ms);
+    fflush(stdout);
   };
   const size_t n2 = elems / 2;
   const double gb_copy = 2.0 * bytes / 1e9, gb5 = 5.0 * bytes / 1e9;

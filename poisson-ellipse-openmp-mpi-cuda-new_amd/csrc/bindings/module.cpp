@@ -447,6 +447,7 @@ PYBIND11_MODULE(_pmx, m) {
           d["kind"] = t.kind == 0 ? "lds" : t.kind == 1 ? "wave" : t.kind == 2 ? "wave-rows" : "pcg1";
           d["block"] = t.block; d["rows"] = t.rows;
           d["vec"] = t.vec; d["waves"] = t.waves; d["tiles_i"] = t.tiles_i; d["tiles_j"] = t.tiles_j;
+          if (t.kind == 3) d["pf"] = t.pf;
           return d;
         };
         py::dict d = one(s.solver(0).tiles());

@@ -90,6 +90,7 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_PCG1_VEC", o.vec1);
   env_int("PMX_PCG1_ROWS", o.rows1);
   env_int("PMX_PCG1_WAVES", o.waves1);
+  env_int("PMX_PCG1_PF", o.pf1);
   PMX_CHECK(o.pair_w >= 0 && o.pair_w <= 2, "pair_w must be 0, 1 or 2");
   PMX_CHECK(o.algo == -1 || o.algo == 1 || o.algo == 2, "algo must be -1, 1 or 2");
   o.resolved = true;
@@ -216,7 +217,7 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   tiles_b_.pair_w = tiles_b_.kind == 2 && !opt.exact && opt_.pair_w != 0;
 
   if (pcg1_) {
-    tiles1_ = make_pcg1_tiles(G, opt_.vec1, opt_.waves1, opt_.rows1);
+    tiles1_ = make_pcg1_tiles(G, opt_.vec1, opt_.waves1, opt_.rows1, opt_.pf1);
     HIP_CHECK(hipMalloc(&r2_, field_bytes_));
   }
 

@@ -48,6 +48,7 @@ using namespace dev;
 namespace {
 
 constexpr int kNq = 5;  // rho, (Az,z), (Az,p), (Ap,p), |p|^2
+constexpr int kPcg1AutoPf = 1;
 
 // VEC columns from c0 (c0 - 1 even, so every 2-column chunk is 2-element aligned); chunks are
 // clamped to start <= cmax (cmax - 1 even, cmax + 1 inside the padded row).
@@ -78,33 +79,30 @@ __device__ __forceinline__ void store_cols(T* row, int c0, const T (&in)[VEC], b
   }
 }
 
-// One row of the tile: its scalar face constants and wave-uniform coefficient class.  The
-// per-column coefficients are rebuilt where they are used (class fast path, or the exact formula
-// on rows the ellipse cuts) instead of being carried through the pipeline in VGPRs.
+// One row of the tile: its table row and wave-uniform coefficient class.  Only these 2 scalars
+// travel down the 3-stage pipeline; the row's face constants (20 SGPRs) are re-read from the
+// tables on the rare rows the ellipse cuts, which keeps 3 live rows from spilling SGPRs.  The
+// per-column coefficients are rebuilt where they are used (class fast path, or the exact formula).
 struct RowCo {
-  RowConst rc;
+  int gi;
   int ucls;
-  double uval;
 };
 
-__device__ __forceinline__ RowCo row_co(const DevTables& Tb, const DevGeom& G, int gi, int gjlo, int gjhi) {
-  RowCo c;
-  c.rc = load_row(Tb, gi);
-  c.ucls = row_class(c.rc, gjlo, gjhi);
-  c.uval = c.ucls == 1 ? 1.0 : G.inv_eps;
-  return c;
+__device__ __forceinline__ RowCo row_co(const DevTables& Tb, int gi, int gjlo, int gjhi) {
+  return RowCo{gi, row_class(load_row(Tb, gi), gjlo, gjhi)};
 }
 
 __device__ __forceinline__ void coef(const RowCo& c, const DevTables& Tb, const DevGeom& G, int gj,
                                      double& a0, double& a1, double& b0, double& b1) {
   if (c.ucls != 0) {
-    a0 = a1 = b0 = b1 = c.uval;
+    a0 = a1 = b0 = b1 = c.ucls == 1 ? 1.0 : G.inv_eps;
   } else {
+    const RowConst rc = load_row(Tb, c.gi);
     const ColConst cc = load_col(Tb, gj);
-    a0 = face_a0c(cc, c.rc, G);
-    a1 = face_a1c(cc, c.rc, G);
-    b0 = face_b0c(cc, c.rc, G);
-    b1 = face_b1c(cc, c.rc, G);
+    a0 = face_a0c(cc, rc, G);
+    a1 = face_a1c(cc, rc, G);
+    b0 = face_b0c(cc, rc, G);
+    b1 = face_b1c(cc, rc, G);
   }
 }
 
@@ -113,7 +111,11 @@ struct Pcg1Row {
   T r[VEC], p[VEC], w[VEC];
 };
 
-template <typename T, int VEC, bool EVEN>
+// FAST: an interior tile (full width, every marched row and column strictly inside the global
+// domain, VEC = 2): no Dirichlet masks, and ownership is a fixed lane set (lanes 1..62 own both
+// their columns, lanes 0 and 63 none), so the sums accumulate unmasked and are masked once at the
+// end.  Same arithmetic as the general path, so a point's values never depend on its tile.
+template <typename T, int VEC, int PF, bool EVEN, bool FAST>
 __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb, T* __restrict__ w,
                                            const T* __restrict__ rold, T* __restrict__ rnew,
                                            const T* __restrict__ pold,
@@ -157,18 +159,21 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   double Pm2[VEC], Pm1[VEC], Zm3[VEC], Zm2[VEC], ro1[VEC], po1[VEC];
 #pragma unroll
   for (int u = 0; u < VEC; ++u) Pm2[u] = Pm1[u] = Zm3[u] = Zm2[u] = ro1[u] = po1[u] = 0.0;
-  RowCo cB = row_co(Tb, G, grow(i0 - 3), gjlo, gjhi);  // rows m-1, m-2
+  RowCo cB = row_co(Tb, grow(i0 - 3), gjlo, gjhi);  // rows m-1, m-2
   RowCo cC = cB;
 
+  const int mfirst = i0 - 2, mlast = i1 + 2;
   auto step = [&](int m, const Pcg1Row<T, VEC>& cur, Pcg1Row<T, VEC>& nxt) {
-    fetch(m + 1, nxt);  // unconditional (clamped): a branch around loads forces vmcnt(0)
+    // PF rows ahead, unconditional (a branch around loads forces vmcnt(0)); past the tile's last
+    // row re-read that row (a cache hit) instead of the next tile's rows
+    fetch(min(m + PF, mlast), nxt);
     // ---- stage A: p^k of row m
-    const bool rowA = interior_row(m);
-    const RowCo cA = row_co(Tb, G, grow(m), gjlo, gjhi);
+    const bool rowA = FAST || interior_row(m);
+    const RowCo cA = row_co(Tb, grow(m), gjlo, gjhi);
     double Pm[VEC], rom[VEC], pom[VEC];
 #pragma unroll
     for (int u = 0; u < VEC; ++u) {
-      const bool in = rowA && colin[u];
+      const bool in = FAST || (rowA && colin[u]);
       rom[u] = in ? double(cur.r[u]) : 0.0;
       pom[u] = in ? double(cur.p[u]) : 0.0;
       double a0, a1, b0, b1;
@@ -180,7 +185,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     // ---- stage B: A p^k, r^k, z^k of row m-1 (j neighbours by DPP; edge lanes get 0, their
     // results only feed columns that are not owned)
     const int mb = m - 1;
-    const bool rowB = interior_row(mb);
+    const bool rowB = FAST || interior_row(mb);
     const bool ownB = mb >= i0 && mb <= i1;
     double Zm1[VEC];
     T rs[VEC], ps[VEC], ws[VEC];
@@ -194,7 +199,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
         const double xjm = u == 0 ? left : Pm1[u - 1];
         const double xjp = u == VEC - 1 ? right : Pm1[u + 1];
         const double Ap = apply_a<false>(Pm1[u], Pm2[u], Pm[u], xjm, xjp, a0, a1, b0, b1, G);
-        const bool in = rowB && colin[u];
+        const bool in = FAST || (rowB && colin[u]);
         const double rn = double(static_cast<T>(upd_r<false>(ro1[u], alpha, Ap)));
         rs[u] = static_cast<T>(in ? rn : 0.0);
         const double zn = zdiv_u<false>(cB.ucls, rn, a0, a1, b0, b1, G);
@@ -202,18 +207,18 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
         ps[u] = static_cast<T>(Pm1[u]);
         if constexpr (EVEN)
           ws[u] = static_cast<T>(__builtin_fma(alpha, Pm1[u], __builtin_fma(alpha_prev, po1[u], double(cur.w[u]))));
-        if (ownB && own[u]) {
+        if (ownB && (FAST || own[u])) {
           acc[0] += Zm1[u] * rn;
           acc[3] += Ap * Pm1[u];
           acc[4] += Pm1[u] * Pm1[u];
         }
       }
     }
-    if (ownB && own_any) {
+    if (ownB && (FAST ? own_all : own_any)) {
       const int64_t o = int64_t(mb) * P;
-      store_cols<T, VEC>(rnew + o, c0, rs, own_all, own);
-      store_cols<T, VEC>(pnew + o, c0, ps, own_all, own);
-      if constexpr (EVEN) store_cols<T, VEC>(w + o, c0, ws, own_all, own);
+      store_cols<T, VEC>(rnew + o, c0, rs, FAST || own_all, own);
+      store_cols<T, VEC>(pnew + o, c0, ps, FAST || own_all, own);
+      if constexpr (EVEN) store_cols<T, VEC>(w + o, c0, ws, FAST || own_all, own);
     }
     // ---- stage C: A z^k of row m-2
     const int mcr = m - 2;
@@ -227,7 +232,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
         const double xjm = u == 0 ? left : Zm2[u - 1];
         const double xjp = u == VEC - 1 ? right : Zm2[u + 1];
         const double Az = apply_a<false>(Zm2[u], Zm3[u], Zm1[u], xjm, xjp, a0, a1, b0, b1, G);
-        if (own[u]) {
+        if (FAST || own[u]) {
           acc[1] += Az * Zm2[u];
           acc[2] += Az * Pm2[u];
         }
@@ -244,22 +249,35 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     cB = cA;
   };
 
-  Pcg1Row<T, VEC> buf[2];
-  const int mfirst = i0 - 2, mlast = i1 + 2;
-  fetch(mfirst, buf[0]);
-  // unrolled by the prefetch ring size: buf[0] / buf[1] are never copied
-  for (int m = mfirst; m <= mlast; m += 2) {
-    step(m, buf[0], buf[1]);
-    if (m + 1 > mlast) break;
-    step(m + 1, buf[1], buf[0]);
+  // ring of PF + 1 row buffers, unrolled by its size so no buffer is ever copied: step m reads
+  // slot q and refills the slot step m - 1 consumed
+  Pcg1Row<T, VEC> buf[PF + 1];
+#pragma unroll
+  for (int q = 0; q < PF; ++q) fetch(min(mfirst + q, mlast), buf[q]);
+  for (int m = mfirst; m <= mlast; m += PF + 1) {
+#pragma unroll
+    for (int q = 0; q <= PF; ++q) {
+      if (m + q > mlast) goto done;
+      step(m + q, buf[q], buf[(q + PF) % (PF + 1)]);
+    }
+  }
+done:
+  if constexpr (FAST) {  // lanes 0 and 63 own no column
+#pragma unroll
+    for (int q = 0; q < kNq; ++q) acc[q] = own_all ? acc[q] : 0.0;
   }
 }
 
-template <typename T, int VEC, int WAVES>
-#ifndef PMX_PCG1_MIN_WAVES
-#define PMX_PCG1_MIN_WAVES 1
-#endif
-__global__ void __launch_bounds__(64 * WAVES, PMX_PCG1_MIN_WAVES)
+// Waves per SIMD the register allocation must allow.  VEC=2, 1 wave/workgroup: 148 VGPRs at
+// PF=1 and 166 at PF=2 fit 3 waves/SIMD with no spills (the MFMA reduction then stays out of
+// AGPRs); PF >= 3 needs > 168 and runs at 2.  Other shapes: whatever the allocator picks.
+template <int VEC, int WAVES, int PF>
+constexpr int pcg1_min_waves() {
+  return VEC == 2 && WAVES == 1 ? (PF <= 2 ? 3 : 2) : 1;
+}
+
+template <typename T, int VEC, int WAVES, int PF>
+__global__ void __launch_bounds__(64 * WAVES, (pcg1_min_waves<VEC, WAVES, PF>()))
 k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
        double* __restrict__ partials, PcgState* S, int TI, int tiles_j, int ntiles) {
   constexpr int WO = 64 * VEC - 4;  // owned columns per tile
@@ -318,10 +336,19 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
   const T* rold = (k & 1) ? r2 : r;
   T* rnew = (k & 1) ? r : r2;
   double acc[kNq] = {0.0, 0.0, 0.0, 0.0, 0.0};
-  if (k > 0 && !(k & 1))
-    pcg1_march<T, VEC, true>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, alpha_prev, acc);
-  else
-    pcg1_march<T, VEC, false>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, alpha_prev, acc);
+  // interior tile: full width, and the marched rows i0-2..i1+2 / columns j0-2..j0+64*VEC-3 lie
+  // strictly inside the global domain (no Dirichlet node in reach)
+  const bool fast = VEC == 2 && j1 == j0 + WO - 1 && G.gi0 + i0 - 2 >= 1 && G.gi0 + i1 + 2 <= G.M - 1 &&
+                    G.gj0 + j0 - 2 >= 1 && G.gj0 + j0 + 64 * VEC - 3 <= G.N - 1;
+  const bool even = k > 0 && !(k & 1);
+#define PMX_MARCH(E, F) \
+  pcg1_march<T, VEC, PF, E, F>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, alpha_prev, acc)
+  if (fast) {
+    if (even) PMX_MARCH(true, true); else PMX_MARCH(false, true);
+  } else {
+    if (even) PMX_MARCH(true, false); else PMX_MARCH(false, false);
+  }
+#undef PMX_MARCH
   wave_sum2_mfma(acc[0], acc[1]);
   wave_sum2_mfma(acc[2], acc[3]);
   acc[4] = wave_sum_mfma(acc[4]);
@@ -432,14 +459,17 @@ k_reduce_n(const double* __restrict__ part, int n, ReduceWeights wt, double* out
 
 }  // namespace
 
-TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows) {
+TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf) {
   PMX_CHECK(vec == 2 || vec == 4, "pcg1: vec must be 2 or 4");
+  PMX_CHECK(pf >= 0 && pf <= 4, "pcg1: prefetch depth must be 0 (auto) or 1..4");
+  PMX_CHECK(pf <= 1 || (vec == 2 && waves == 1), "pcg1: prefetch depth > 1 needs vec 2 x 1 wave");
   PMX_CHECK(waves == 1 || waves == 2 || waves == 4, "pcg1: waves must be 1, 2 or 4");
   TileCfg t;
   t.kind = 3;
   t.vec = vec;
   t.waves = waves;
   t.block = 64 * vec - 4;  // owned columns per tile
+  t.pf = pf ? pf : (vec == 2 && waves == 1 ? kPcg1AutoPf : 1);
   t.tiles_j = (G.ny + t.block - 1) / t.block;
   if (rows <= 0) {
     // tall tiles keep the 4 extra marched rows cheap; shorter only when the grid is small
@@ -460,14 +490,19 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
   PMX_CHECK(G.nb == 0 || (G.nx >= 2 && G.ny >= 2), "pcg1 on a decomposed grid needs subdomains >= 2 x 2");
   const int nb = (tc.ntiles() + tc.waves - 1) / tc.waves;
   const int bs = 64 * tc.waves;
-#define PMX_PCG1(V, WV) \
-  hipLaunchKernelGGL((k_pcg1<T, V, WV>), dim3(nb), dim3(bs), 0, s, G, Tb, w, r, r2, p0, p1, partials, S, tc.rows, tc.tiles_j, tc.ntiles())
-  if (tc.vec == 2 && tc.waves == 4) PMX_PCG1(2, 4);
-  else if (tc.vec == 2 && tc.waves == 2) PMX_PCG1(2, 2);
-  else if (tc.vec == 2 && tc.waves == 1) PMX_PCG1(2, 1);
-  else if (tc.vec == 4 && tc.waves == 4) PMX_PCG1(4, 4);
-  else if (tc.vec == 4 && tc.waves == 2) PMX_PCG1(4, 2);
-  else PMX_PCG1(4, 1);
+#define PMX_PCG1(V, WV, PF) \
+  hipLaunchKernelGGL((k_pcg1<T, V, WV, PF>), dim3(nb), dim3(bs), 0, s, G, Tb, w, r, r2, p0, p1, partials, S, tc.rows, tc.tiles_j, tc.ntiles())
+  if (tc.vec == 2 && tc.waves == 1) {
+    if (tc.pf == 1) PMX_PCG1(2, 1, 1);
+    else if (tc.pf == 2) PMX_PCG1(2, 1, 2);
+    else if (tc.pf == 3) PMX_PCG1(2, 1, 3);
+    else PMX_PCG1(2, 1, 4);
+  }
+  else if (tc.vec == 2 && tc.waves == 4) PMX_PCG1(2, 4, 1);
+  else if (tc.vec == 2 && tc.waves == 2) PMX_PCG1(2, 2, 1);
+  else if (tc.vec == 4 && tc.waves == 4) PMX_PCG1(4, 4, 1);
+  else if (tc.vec == 4 && tc.waves == 2) PMX_PCG1(4, 2, 1);
+  else PMX_PCG1(4, 1, 1);
 #undef PMX_PCG1
   HIP_CHECK(hipGetLastError());
 }

@@ -35,17 +35,27 @@ struct RowConst {
 __device__ __forceinline__ ColConst load_col(const DevTables& T, int gj) {
   return ColConst{T.ylo[gj], T.yhi[gj], T.rh[gj], T.rh[gj + 1], gj};
 }
+// Wave-uniform loads from the read-only tables through the scalar cache: the tables are
+// never written by a kernel that reads them, but the compiler cannot prove that (they may alias
+// the fields), so without the constant address space it issues VECTOR loads -- and waiting for
+// those (vmcnt is in-order) also drains every row prefetch issued before them.
+template <typename T>
+__device__ __forceinline__ T ld_uniform(const T* p, int i) {
+  typedef const __attribute__((address_space(4))) T CT;
+  return ((CT*)p)[i];
+}
 __device__ __forceinline__ RowConst load_row(const DevTables& T, int gi) {
   RowConst r;
-  r.rv0 = T.rv[gi];
-  r.rv1 = T.rv[gi + 1];
-  r.xlo = T.xlo[gi];
-  r.xhi = T.xhi[gi];
+  gi = __builtin_amdgcn_readfirstlane(gi);
+  r.rv0 = ld_uniform(T.rv, gi);
+  r.rv1 = ld_uniform(T.rv, gi + 1);
+  r.xlo = ld_uniform(T.xlo, gi);
+  r.xhi = ld_uniform(T.xhi, gi);
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    r.ca0[q] = T.acls[4 * gi + q];
-    r.ca1[q] = T.acls[4 * (gi + 1) + q];
-    r.cb[q] = T.bcls[4 * gi + q];
+    r.ca0[q] = ld_uniform(T.acls, 4 * gi + q);
+    r.ca1[q] = ld_uniform(T.acls, 4 * (gi + 1) + q);
+    r.cb[q] = ld_uniform(T.bcls, 4 * gi + q);
   }
   return r;
 }

@@ -74,6 +74,9 @@ struct GpuOptions {
   // pcg1 tile shape (rows1 = 0: auto).  VEC=2 x 1 wave/workgroup won the 16384^2 sweeps
   // (bench/gpu_pcg1_sweep.sh; VEC=4 needs 256 VGPRs and is 35% slower).
   int vec1 = 2, waves1 = 1, rows1 = 0;
+  // pcg1 prefetch depth: rows loaded ahead of the row being computed (1..4).  The sweep is
+  // latency-bound at 2 waves/SIMD; deeper prefetch spends VGPRs that occupancy does not use.
+  int pf1 = 0;  // 0 = auto
   bool resolved = false;  // environment overrides already applied (resolve_options)
 };
 

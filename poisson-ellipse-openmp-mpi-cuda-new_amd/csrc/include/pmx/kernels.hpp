@@ -27,6 +27,7 @@ struct TileCfg {
   int waves = 1;      // kind 1: independent wave tiles per workgroup
   int abl = 0;        // kernel-isolation ablation bits (kAbl*), 0 in production
   int pair_w = 0;     // kind 2: paired w updates (k_pcg_b_rows_paired, pcg_kernels_dpp.hip)
+  int pf = 1;         // kind 3: rows prefetched ahead of the computed row
   int tiles_i = 0, tiles_j = 0;
   int ntiles() const { return tiles_i * tiles_j; }
 };
@@ -38,7 +39,7 @@ TileCfg make_wave_tiles(const DevGeom& G, int vec, int waves, int rows, int max_
 // kind 2 tiles for k_pcg_b_rows (rows = 0: 2)
 TileCfg make_row_tiles(const DevGeom& G, int vec, int waves, int rows);
 // kind 3 tiles for k_pcg1: 64*vec - 4 owned columns, rows = 0: auto
-TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows);
+TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf = 0);
 
 enum ReduceMode : int { kSkipIfDone = 1, kBumpIter = 2 };
 
