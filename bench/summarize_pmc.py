@@ -40,7 +40,7 @@ def read_pass(p):
     return out
 
 
-passes = {p: read_pass(p) for p in ("ea_rd", "ea_wr", "sq1", "sq2", "grbm")}
+passes = {p: read_pass(p) for p in ("ea_rd", "ea_wr", "sq1", "sq2", "grbm", "tlb", "tcc", "sq3")}
 wr = passes["ea_wr"]
 
 
@@ -67,6 +67,7 @@ for k in sorted(set().union(*[set(v) for v in passes.values()])):
     print(f"| write B/pt (64 B x 64B-req + 32 B x rest) | {wr_bytes / pts:.2f} |")
     print(f"| DRAM read / write requests | {stats('ea_wr', 'TCC_EA0_RDREQ_DRAM_sum'):.4g} / {stats('ea_wr', 'TCC_EA0_WRREQ_DRAM_sum'):.4g} |")
     waves = stats("sq1", "SQ_WAVES")
+    waves = waves if waves == waves else stats("sq3", "SQ_WAVES")
     for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"):
         print(f"| {c} per wave | {stats('sq1', c) / waves:.1f} |")
     for c in ("SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_INST_ANY"):
@@ -75,6 +76,22 @@ for k in sorted(set().union(*[set(v) for v in passes.values()])):
               "SQ_WAIT_ANY", "SQ_INST_LEVEL_VMEM", "SQ_IFETCH", "SQ_INSTS_VALU_FMA_F64"):
         print(f"| {c} | {stats('sq2', c):.4g} |")
     print(f"| GRBM_GUI_ACTIVE (GPU cycles) | {stats('grbm', 'GRBM_GUI_ACTIVE'):.4g} |")
+    if passes["tlb"]:
+        hit, miss = stats("tlb", "TCP_UTCL1_TRANSLATION_HIT_sum"), stats("tlb", "TCP_UTCL1_TRANSLATION_MISS_sum")
+        lat, req = stats("tlb", "TCP_TCC_READ_REQ_LATENCY_sum"), stats("tlb", "TCP_TCC_READ_REQ_sum")
+        print(f"| UTCL1 translation hit / miss | {hit:.4g} / {miss:.4g} (miss {miss / max(hit + miss, 1):.3%}) |")
+        print(f"| TCP->TCC read latency (cycles per request) | {lat / max(req, 1):.0f} |")
+    if passes["tcc"]:
+        hit, miss = stats("tcc", "TCC_HIT_sum"), stats("tcc", "TCC_MISS_sum")
+        print(f"| TCC hit / miss | {hit:.4g} / {miss:.4g} (hit {hit / max(hit + miss, 1):.1%}) |")
+        print(f"| EA read requests, 128 B of them (tcc pass) | {stats('tcc', 'TCC_EA0_RDREQ_sum'):.4g} "
+              f"({stats('tcc', 'TCC_EA0_RDREQ_128B_sum'):.4g}) |")
+    if passes["sq3"]:
+        w3 = stats("sq3", "SQ_WAVES")
+        for c in ("SQ_INSTS_SMEM", "SQ_INSTS_SALU", "SQ_INSTS_VALU", "SQ_INSTS_LDS"):
+            print(f"| {c} per wave (sq3) | {stats('sq3', c) / w3:.1f} |")
+        for c in ("SQ_WAIT_INST_ANY", "SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_VALU"):
+            print(f"| {c} (sq3) | {stats('sq3', c):.4g} |")
     print(f"| waves | {waves:.0f} |\n")
 
 f = os.path.join(a.root, "trace", "run_kernel_trace.csv")

@@ -126,3 +126,20 @@ def test_pmx_mpi(pmx_bin, np_, threads):
     js = json.loads(out.strip().splitlines()[-1])
     assert js["iters"] == 546 and js["ranks"] == np_
     assert abs(js["l2_error"] - 3.0607e-4) < 1e-7
+
+
+@pytest.mark.skipif(_mpiexec() is None, reason="no MPI launcher")
+def test_pmx_mpi_phase_max(pmx_bin):
+    """--phases: compute / halo / all-reduce buckets, MPI_MAX over ranks, printed once by rank 0
+    (reference: stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980)."""
+    exe = os.path.join(BIN, "pmx_mpi")
+    if not os.path.exists(exe):
+        pytest.skip("pmx_mpi not built (no MPI found at build time)")
+    out = run([_mpiexec(), "-n", "4", exe, "200", "300", "--phases", "--json"])
+    lines = out.strip().splitlines()
+    assert sum("max over ranks)" in l for l in lines) == 3  # rank 0 only
+    js = json.loads(lines[-1])
+    assert js["ranks"] == 4
+    total = js["t_compute_max"] + js["t_halo_max"] + js["t_allreduce_max"]
+    assert all(js[k] >= 0.0 for k in ("t_compute_max", "t_halo_max", "t_allreduce_max"))
+    assert total >= 0.9 * js["seconds"]  # maxima of a partition of every rank's time
