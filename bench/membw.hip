@@ -7,6 +7,9 @@
 //               512-column strip (the tile-marching order of the fused kernels)
 //   rowband5  : 5 streams, one block per (row, 512-col chunk), rows assigned so that each XCD
 //               works on its own contiguous band of rows (T1-style XCD-aware mapping)
+//   mix_2r2w  : the k_pcg1 odd-iteration traffic: read 2 arrays, write 2 OTHER arrays (rowband
+//               mapping, XCD-aware); mix_3r3w: the even one (+ a third array read and written
+//               in place)
 // Usage: membw [N] [rows] [reps] [fill]   (reps = timed launches per kernel, default 10; fill 1 =
 // non-zero data: HBM power depends on the bit patterns, and sustained runs of >= 1 s show the
 // clock/power-limited steady state instead of the first-launch burst)
@@ -102,6 +105,31 @@ k_rowband5(const double* p, double* w, double* r, int n, int pitch, int chunks, 
   *(double2*)(r + c) = rv;
 }
 
+struct Ptrs {
+  double* a[5];
+};
+// reads a[0..NR-1]; writes a[NR], a[NR+1] (separate arrays) and, if WIN, a[NR-1] in place
+template <int NR, bool WIN>
+__global__ void __launch_bounds__(256) k_mix(Ptrs P, int n, int pitch, int chunks) {
+  const int nb = gridDim.x, per = nb / 8;
+  const int b = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  const int i = b / chunks, jc = b % chunks;
+  if (i >= n) return;
+  const size_t c = size_t(i) * pitch + jc * 512 + 2 * threadIdx.x;
+  double2 v[NR];
+#pragma unroll
+  for (int q = 0; q < NR; ++q) v[q] = *(const double2*)(P.a[q] + c);
+  double2 o0 = v[0], o1 = v[1];
+  o0.x += 0.5 * v[1].y; o1.y -= 0.5 * v[0].x;
+  *(double2*)(P.a[NR] + c) = o0;
+  *(double2*)(P.a[NR + 1] + c) = o1;
+  if constexpr (WIN) {
+    double2 wv = v[NR - 1];
+    wv.x += 0.25 * o0.y; wv.y += 0.25 * o1.x;
+    *(double2*)(P.a[NR - 1] + c) = wv;
+  }
+}
+
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 16384;
   const int rows = argc > 2 ? atoi(argv[2]) : 64;
@@ -172,5 +200,18 @@ int main(int argc, char** argv) {
   const int chunks = n / 512;
   timeit("rowband5_rowmajor", gb5, [&] { hipLaunchKernelGGL(k_rowband5, dim3(n * chunks), dim3(256), 0, 0, p, w, r, n, pitch, chunks, 0.5, 0); });
   timeit("rowband5_xcd", gb5, [&] { hipLaunchKernelGGL(k_rowband5, dim3(n * chunks), dim3(256), 0, 0, p, w, r, n, pitch, chunks, 0.5, 1); });
+  {
+    double *c, *d;
+    CK(hipMalloc(&c, bytes));
+    CK(hipMalloc(&d, bytes));
+    CK(hipMemcpy(c, p, bytes, hipMemcpyDeviceToDevice));
+    CK(hipMemcpy(d, p, bytes, hipMemcpyDeviceToDevice));
+    const int nblk = ((n * chunks + 7) / 8) * 8;
+    Ptrs odd{{p, r, c, d, nullptr}}, even{{p, r, w, c, d}};
+    timeit("mix_2r2w", 4.0 * bytes / 1e9, [&] { hipLaunchKernelGGL((k_mix<2, false>), dim3(nblk), dim3(256), 0, 0, odd, n, pitch, chunks); });
+    timeit("mix_3r3w", 6.0 * bytes / 1e9, [&] { hipLaunchKernelGGL((k_mix<3, true>), dim3(nblk), dim3(256), 0, 0, even, n, pitch, chunks); });
+    CK(hipFree(c));
+    CK(hipFree(d));
+  }
   return 0;
 }

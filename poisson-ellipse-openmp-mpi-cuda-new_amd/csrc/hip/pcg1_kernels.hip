@@ -49,7 +49,6 @@ namespace {
 
 constexpr int kNq = 5;  // rho, (Az,z), (Az,p), (Ap,p), |p|^2
 constexpr int kPcg1AutoPf = 1;
-constexpr int kPcg1MaxRows = 56;  // + 5 marched rows of row classes fit one VGPR (64 lanes)
 
 // VEC columns from c0 (c0 - 1 even, so every 2-column chunk is 2-element aligned); chunks are
 // clamped to start <= cmax (cmax - 1 even, cmax + 1 inside the padded row).
@@ -89,6 +88,10 @@ struct RowCo {
   int ucls;
 };
 
+__device__ __forceinline__ RowCo row_co(const DevTables& Tb, int gi, int gjlo, int gjhi) {
+  return RowCo{gi, row_class(load_row(Tb, gi), gjlo, gjhi)};
+}
+
 __device__ __forceinline__ void coef(const RowCo& c, const DevTables& Tb, const DevGeom& G, int gj,
                                      double& a0, double& a1, double& b0, double& b1) {
   if (c.ucls != 0) {
@@ -112,13 +115,7 @@ struct Pcg1Row {
 // domain, VEC = 2): no Dirichlet masks, and ownership is a fixed lane set (lanes 1..62 own both
 // their columns, lanes 0 and 63 none), so the sums accumulate unmasked and are masked once at the
 // end.  Same arithmetic as the general path, so a point's values never depend on its tile.
-//
-// DOWN: march direction.  Bands of tiles alternate (even tile rows march down, odd ones up), so the
-// 2 extra rows a tile reads on each side are read by the neighbouring band at about the same time
-// -- both at the start of their marches or both at the end -- and the second read is an L2 hit
-// instead of an HBM read.  The stencils take the same neighbours either way: values never depend
-// on the direction, only the order of the partial sums does.
-template <typename T, int VEC, int PF, bool EVEN, bool FAST, bool DOWN>
+template <typename T, int VEC, int PF, bool EVEN, bool FAST>
 __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb, T* __restrict__ w,
                                            const T* __restrict__ rold, T* __restrict__ rnew,
                                            const T* __restrict__ pold,
@@ -147,21 +144,13 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   const int gjlo = max(G.gj0 + j0 - 2, 0), gjhi = min(G.gj0 + j0 - 2 + 64 * VEC - 1, G.N);
   auto grow = [&](int m) { return min(max(G.gi0 + m, 0), G.M); };  // table row of local row m
   auto interior_row = [&](int m) { return G.gi0 + m >= 1 && G.gi0 + m <= G.M - 1; };
-  // Row classes of the whole tile up front: lane q holds the class of local row i0 - 3 + q (the
-  // pipeline touches rows i0 - 3 .. i1 + 3, at most kPcg1MaxRows + 7 <= 64).  A step then reads its
-  // row's class with one v_readlane instead of a scalar-cache round trip that no other work hides.
-  const int mcls0 = i0 - 3;
-  const int cls_lane = row_class_lane(Tb, grow(min(mcls0 + lane, i1 + 3)), gjlo, gjhi);
-  auto row_co = [&](int m) { return RowCo{grow(m), __builtin_amdgcn_readlane(cls_lane, m - mcls0)}; };
 
-  constexpr int d = DOWN ? 1 : -1;  // march step: stage B handles row m - d, stage C row m - 2d
   auto fetch = [&](int m, Pcg1Row<T, VEC>& b) {
     const int mc = min(max(m, -1), G.nx + 2);  // rows -1 .. nx+2 exist (2 ghost layers)
     load_cols<T, VEC>(rold + int64_t(mc) * P, c0, cmax, b.r);
     load_cols<T, VEC>(pold + int64_t(mc) * P, c0, cmax, b.p);
-    if constexpr (EVEN) {  // w of the row stage B handles at that step; rows outside the tile
-      // store no w, so they re-read an owned row (a cache hit) instead of another HBM row
-      const int wc = min(max(m - d, i0), i1);
+    if constexpr (EVEN) {  // w of the row stage B handles next step
+      const int wc = min(max(m - 1, -1), G.nx + 2);
       load_cols<T, VEC>(w + int64_t(wc) * P, c0, cmax, b.w);
     }
   };
@@ -170,19 +159,17 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   double Pm2[VEC], Pm1[VEC], Zm3[VEC], Zm2[VEC], ro1[VEC], po1[VEC];
 #pragma unroll
   for (int u = 0; u < VEC; ++u) Pm2[u] = Pm1[u] = Zm3[u] = Zm2[u] = ro1[u] = po1[u] = 0.0;
-  const int mfirst = i0 - 2, mlast = i1 + 2;
-  const int mstart = DOWN ? mfirst : mlast, mend = DOWN ? mlast : mfirst;
-  RowCo cB = row_co(mstart - d);  // rows m - d, m - 2d
+  RowCo cB = row_co(Tb, grow(i0 - 3), gjlo, gjhi);  // rows m-1, m-2
   RowCo cC = cB;
-  auto clamp_m = [&](int m) { return DOWN ? min(m, mend) : max(m, mend); };
 
+  const int mfirst = i0 - 2, mlast = i1 + 2;
   auto step = [&](int m, const Pcg1Row<T, VEC>& cur, Pcg1Row<T, VEC>& nxt) {
     // PF rows ahead, unconditional (a branch around loads forces vmcnt(0)); past the tile's last
     // row re-read that row (a cache hit) instead of the next tile's rows
-    fetch(clamp_m(m + PF * d), nxt);
+    fetch(min(m + PF, mlast), nxt);
     // ---- stage A: p^k of row m
     const bool rowA = FAST || interior_row(m);
-    const RowCo cA = row_co(m);
+    const RowCo cA = row_co(Tb, grow(m), gjlo, gjhi);
     double Pm[VEC], rom[VEC], pom[VEC];
 #pragma unroll
     for (int u = 0; u < VEC; ++u) {
@@ -195,9 +182,9 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
       const double v = __builtin_fma(beta, pom[u], z);
       Pm[u] = in ? double(static_cast<T>(v)) : 0.0;  // the stored (rounded) p^k is the one used
     }
-    // ---- stage B: A p^k, r^k, z^k of row m - d (j neighbours by DPP; edge lanes get 0, their
-    // results only feed columns that are not owned); Pm2 / Pm are rows mb - d / mb + d
-    const int mb = m - d;
+    // ---- stage B: A p^k, r^k, z^k of row m-1 (j neighbours by DPP; edge lanes get 0, their
+    // results only feed columns that are not owned)
+    const int mb = m - 1;
     const bool rowB = FAST || interior_row(mb);
     const bool ownB = mb >= i0 && mb <= i1;
     double Zm1[VEC];
@@ -211,8 +198,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
         coef(cB, Tb, G, gj[u], a0, a1, b0, b1);
         const double xjm = u == 0 ? left : Pm1[u - 1];
         const double xjp = u == VEC - 1 ? right : Pm1[u + 1];
-        const double Ap = DOWN ? apply_a<false>(Pm1[u], Pm2[u], Pm[u], xjm, xjp, a0, a1, b0, b1, G)
-                               : apply_a<false>(Pm1[u], Pm[u], Pm2[u], xjm, xjp, a0, a1, b0, b1, G);
+        const double Ap = apply_a<false>(Pm1[u], Pm2[u], Pm[u], xjm, xjp, a0, a1, b0, b1, G);
         const bool in = FAST || (rowB && colin[u]);
         const double rn = double(static_cast<T>(upd_r<false>(ro1[u], alpha, Ap)));
         rs[u] = static_cast<T>(in ? rn : 0.0);
@@ -234,8 +220,8 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
       store_cols<T, VEC>(pnew + o, c0, ps, FAST || own_all, own);
       if constexpr (EVEN) store_cols<T, VEC>(w + o, c0, ws, FAST || own_all, own);
     }
-    // ---- stage C: A z^k of row m - 2d
-    const int mcr = m - 2 * d;
+    // ---- stage C: A z^k of row m-2
+    const int mcr = m - 2;
     if (mcr >= i0 && mcr <= i1) {
       const double left = dpp_shift_f64<kWaveShr1>(Zm2[VEC - 1], 0.0);
       const double right = dpp_shift_f64<kWaveShl1>(Zm2[0], 0.0);
@@ -245,8 +231,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
         coef(cC, Tb, G, gj[u], a0, a1, b0, b1);
         const double xjm = u == 0 ? left : Zm2[u - 1];
         const double xjp = u == VEC - 1 ? right : Zm2[u + 1];
-        const double Az = DOWN ? apply_a<false>(Zm2[u], Zm3[u], Zm1[u], xjm, xjp, a0, a1, b0, b1, G)
-                               : apply_a<false>(Zm2[u], Zm1[u], Zm3[u], xjm, xjp, a0, a1, b0, b1, G);
+        const double Az = apply_a<false>(Zm2[u], Zm3[u], Zm1[u], xjm, xjp, a0, a1, b0, b1, G);
         if (FAST || own[u]) {
           acc[1] += Az * Zm2[u];
           acc[2] += Az * Pm2[u];
@@ -268,13 +253,12 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   // slot q and refills the slot step m - 1 consumed
   Pcg1Row<T, VEC> buf[PF + 1];
 #pragma unroll
-  for (int q = 0; q < PF; ++q) fetch(clamp_m(mstart + q * d), buf[q]);
-  const int nsteps = mlast - mfirst + 1;
-  for (int t = 0; t < nsteps; t += PF + 1) {
+  for (int q = 0; q < PF; ++q) fetch(min(mfirst + q, mlast), buf[q]);
+  for (int m = mfirst; m <= mlast; m += PF + 1) {
 #pragma unroll
     for (int q = 0; q <= PF; ++q) {
-      if (t + q >= nsteps) goto done;
-      step(mstart + (t + q) * d, buf[q], buf[(q + PF) % (PF + 1)]);
+      if (m + q > mlast) goto done;
+      step(m + q, buf[q], buf[(q + PF) % (PF + 1)]);
     }
   }
 done:
@@ -357,21 +341,12 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
   const bool fast = VEC == 2 && j1 == j0 + WO - 1 && G.gi0 + i0 - 2 >= 1 && G.gi0 + i1 + 2 <= G.M - 1 &&
                     G.gj0 + j0 - 2 >= 1 && G.gj0 + j0 + 64 * VEC - 3 <= G.N - 1;
   const bool even = k > 0 && !(k & 1);
-  const bool down = !(ti & 1);  // alternate bands (see pcg1_march)
-#define PMX_MARCH(E, F, D) \
-  pcg1_march<T, VEC, PF, E, F, D>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, alpha_prev, acc)
+#define PMX_MARCH(E, F) \
+  pcg1_march<T, VEC, PF, E, F>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, alpha_prev, acc)
   if (fast) {
-    if (down) {
-      if (even) PMX_MARCH(true, true, true); else PMX_MARCH(false, true, true);
-    } else {
-      if (even) PMX_MARCH(true, true, false); else PMX_MARCH(false, true, false);
-    }
+    if (even) PMX_MARCH(true, true); else PMX_MARCH(false, true);
   } else {
-    if (down) {
-      if (even) PMX_MARCH(true, false, true); else PMX_MARCH(false, false, true);
-    } else {
-      if (even) PMX_MARCH(true, false, false); else PMX_MARCH(false, false, false);
-    }
+    if (even) PMX_MARCH(true, false); else PMX_MARCH(false, false);
   }
 #undef PMX_MARCH
   wave_sum2_mfma(acc[0], acc[1]);
@@ -500,12 +475,13 @@ TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf) 
   if (rows <= 0) {
     // tall tiles keep the 4 extra marched rows cheap; shorter only when the grid is small
     // (>= ~8K tiles keep 3 waves/SIMD busy for a few rounds)
-    // 16384^2 sweep with alternating march directions (profiles/r2/pcg1_rows_sweep.txt): 8 rows
-    // 2.226 ms, 12 2.189, 16 2.207, 24 2.236, 32 2.293, 48 2.375
+    // 16384^2 sweeps (profiles/r2/pcg1_rows_sweep.txt; same-box A/B: 12 rows 2.36 ms vs 32 rows
+    // 2.52): 8 rows 2.34 ms, 12 2.34, 16 2.39, 24 2.47, 32 2.54 -- short tiles keep fewer DRAM
+    // rows in flight and win despite the 4 extra marched rows
     rows = 12;
     while (rows > 6 && int64_t((G.nx + rows - 1) / rows) * t.tiles_j < 8192) rows /= 2;
   }
-  PMX_CHECK(rows >= 1 && rows <= kPcg1MaxRows, "pcg1: tile rows must be in [1, " << kPcg1MaxRows << "]");
+  PMX_CHECK(rows >= 1 && rows <= 4096, "pcg1: tile rows must be in [1, 4096]");
   t.rows = rows;
   t.tiles_i = (G.nx + rows - 1) / rows;
   return t;

@@ -284,20 +284,6 @@ __device__ __forceinline__ int row_class(const RowConst& rc, int jlo, int jhi) {
   return 0;
 }
 
-// The same class from per-lane (vector) loads: lane q classifies its own table row gi, so a tile
-// classifies up to 64 rows with one batch of loads in its prologue instead of one scalar load
-// round trip (and ~40 SALU instructions) per marched row.
-__device__ __forceinline__ int row_class_lane(const DevTables& T, int gi, int jlo, int jhi) {
-  RowConst rc;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    rc.ca0[q] = T.acls[4 * gi + q];
-    rc.ca1[q] = T.acls[4 * (gi + 1) + q];
-    rc.cb[q] = T.bcls[4 * gi + q];
-  }
-  return row_class(rc, jlo, jhi);
-}
-
 // Linear tile id -> (ti, tj).  Tiles are TI rows x BLOCK columns.
 struct Tile {
   int i0, iend, j0, jend, id;
