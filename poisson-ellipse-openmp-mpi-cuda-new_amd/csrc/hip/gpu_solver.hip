@@ -107,9 +107,10 @@ bool choose_single_pass(const ProblemSpec& spec, const ProcGrid& grid, const Gpu
   PMX_CHECK(o.algo != 1 || ok,
             "pcg1 needs the wave kernels, the fast arithmetic and subdomains of at least 2 x 2 nodes");
   if (o.algo == 1) return true;
-  // auto: fp64 only -- with fp32 storage the stream halves and pcg1's second stencil makes it
-  // compute-bound (32768^2 fp32: pcg1 8.99 ms vs pcg2 7.69 ms per iteration)
-  if (!ok || o.dtype != DType::kFp64) return false;
+  // auto: every storage type.  (Round 1 kept pcg2 for fp32 -- 32768^2: pcg1 8.99 ms vs pcg2 7.69 --
+  // but with the scalar-cache row tables and short tiles pcg1 wins there too: 5.20 vs 7.08 ms,
+  // 16384^2 1.41 vs 2.00 ms, profiles/r2/fp32_pcg1_sweep.txt)
+  if (!ok) return false;
   if (device_total_bytes > 0) {  // the 5th field must fit (rank 0 holds the largest block)
     const Subdomain sd0 = decompose_2d(spec.M, spec.N, grid, 0);
     const double need = double(GpuSubdomainSolver::estimate_device_bytes(spec, sd0, o.dtype, true)) *
@@ -217,7 +218,7 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   tiles_b_.pair_w = tiles_b_.kind == 2 && !opt.exact && opt_.pair_w != 0;
 
   if (pcg1_) {
-    tiles1_ = make_pcg1_tiles(G, opt_.vec1, opt_.waves1, opt_.rows1, opt_.pf1);
+    tiles1_ = make_pcg1_tiles(G, opt_.vec1, opt_.waves1, opt_.rows1, opt_.pf1, int(elem_));
     HIP_CHECK(hipMalloc(&r2_, field_bytes_));
   }
 

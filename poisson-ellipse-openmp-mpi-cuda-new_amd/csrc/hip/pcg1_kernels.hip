@@ -11,9 +11,10 @@
 //   p^k = z + beta p;  A p^k (explicit 5-point stencil, not a recurrence);  r^k = r - alpha A p^k;
 //   z^k = D^-1 r^k;  A z^k;  partials (z^k, r^k), (A z^k, z^k), (A z^k, p^k), (A p^k, p^k), |p^k|^2.
 // r is updated with an explicitly computed A p^k exactly as in the reference, only alpha's
-// denominator is formed differently.  Measured in fp64 on the reference grids the
-// expanded denominator differs from the direct one by <= 1.4e-15 relative and every iteration
-// count is unchanged (15/26/50/546/989/1858), see profiles/NOTES_perf_experiments.md.
+// denominator is formed differently.  Measured in fp64 the expanded denominator differs from the
+// direct one by <= 1.4e-15 relative, and every iteration count is unchanged: the reference grids
+// 15/26/50/546/989/1858/2449 are GPU tests (tests/test_gpu_pcg1.py), and 32768^2 takes 14,316
+// iterations with both pcg1 and pcg2 (profiles/r2/big_32768_records.md).
 //
 // Mapping (CDNA4): one wave64 marches a tile of TI rows x (64*VEC - 4) owned columns with a
 // 3-stage row pipeline (A: p^k of row m, B: A p^k / r^k / z^k of row m-1, C: A z^k of row m-2).
@@ -459,9 +460,9 @@ k_reduce_n(const double* __restrict__ part, int n, ReduceWeights wt, double* out
 
 }  // namespace
 
-TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf) {
+TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf, int elem) {
   PMX_CHECK(vec == 2 || vec == 4, "pcg1: vec must be 2 or 4");
-  PMX_CHECK(pf >= 0 && pf <= 2, "pcg1: prefetch depth must be 0 (auto), 1 or 2");
+  PMX_CHECK(pf >= 0 && pf <= 4, "pcg1: prefetch depth must be 0 (auto) or 1..4");
   PMX_CHECK(pf <= 1 || (vec == 2 && waves == 1), "pcg1: prefetch depth > 1 needs vec 2 x 1 wave");
   PMX_CHECK(waves == 1 || waves == 2 || waves == 4, "pcg1: waves must be 1, 2 or 4");
   PMX_CHECK(vec == 2 || waves == 1, "pcg1: VEC 4 runs 1 wave per workgroup");
@@ -470,7 +471,10 @@ TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf) 
   t.vec = vec;
   t.waves = waves;
   t.block = 64 * vec - 4;  // owned columns per tile
-  t.pf = pf ? pf : (vec == 2 && waves == 1 ? kPcg1AutoPf : 1);
+  // fp32 storage: half the bytes per row, so the prefetch ring is cheap and a deeper one pays
+  // (32768^2: PF 2 x 24 rows 5.06 ms vs PF 1 x 12 rows 5.20, profiles/r2/fp32_pcg1_sweep.txt)
+  const bool fp32 = elem == 4;
+  t.pf = pf ? pf : (vec == 2 && waves == 1 ? (fp32 ? 2 : kPcg1AutoPf) : 1);
   t.tiles_j = (G.ny + t.block - 1) / t.block;
   if (rows <= 0) {
     // tall tiles keep the 4 extra marched rows cheap; shorter only when the grid is small
@@ -478,7 +482,7 @@ TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf) 
     // 16384^2 sweeps (profiles/r2/pcg1_rows_sweep.txt; same-box A/B: 12 rows 2.36 ms vs 32 rows
     // 2.52): 8 rows 2.34 ms, 12 2.34, 16 2.39, 24 2.47, 32 2.54 -- short tiles keep fewer DRAM
     // rows in flight and win despite the 4 extra marched rows
-    rows = 12;
+    rows = fp32 ? 24 : 12;
     while (rows > 6 && int64_t((G.nx + rows - 1) / rows) * t.tiles_j < 8192) rows /= 2;
   }
   PMX_CHECK(rows >= 1 && rows <= 4096, "pcg1: tile rows must be in [1, 4096]");
@@ -497,10 +501,12 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
 #define PMX_PCG1(V, WV, PF) \
   hipLaunchKernelGGL((k_pcg1<T, V, WV, PF>), dim3(nb), dim3(bs), 0, s, G, Tb, w, r, r2, p0, p1, partials, S, tc.rows, tc.tiles_j, tc.ntiles())
   // instantiated shapes: the default (VEC 2, 1 wave, prefetch 1) and the ones the sweeps still
-  // compare against (prefetch 2; 2 or 4 waves per workgroup; VEC 4)
+  // compare against (prefetch 2-4; 2 or 4 waves per workgroup; VEC 4)
   if (tc.vec == 2 && tc.waves == 1) {
     if (tc.pf == 1) PMX_PCG1(2, 1, 1);
-    else PMX_PCG1(2, 1, 2);
+    else if (tc.pf == 2) PMX_PCG1(2, 1, 2);
+    else if (tc.pf == 3) PMX_PCG1(2, 1, 3);
+    else PMX_PCG1(2, 1, 4);
   }
   else if (tc.vec == 2 && tc.waves == 4) PMX_PCG1(2, 4, 1);
   else if (tc.vec == 2 && tc.waves == 2) PMX_PCG1(2, 2, 1);

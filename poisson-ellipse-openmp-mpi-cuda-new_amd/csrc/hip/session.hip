@@ -130,8 +130,8 @@ RunStats Session::solve_checkpointed(const std::string& save_path, int64_t every
 }
 
 int64_t max_square_grid(double bytes_per_gpu, int gpus, DType dtype, double reserve_fraction) {
-  // the default iteration per precision: fp64 pcg1 (5 fields), fp32 pcg2 (4 fields); +1% pitch
-  const double bpp = (dtype == DType::kFp64 ? 5.0 * 8.0 : 4.0 * 4.0) * 1.01;
+  // the default iteration (pcg1) keeps 5 fields in either precision; +1% pitch
+  const double bpp = 5.0 * (dtype == DType::kFp64 ? 8.0 : 4.0) * 1.01;
   const double pts = bytes_per_gpu * (1.0 - reserve_fraction) * gpus / bpp;
   return int64_t(std::floor(std::sqrt(pts)));
 }

@@ -39,7 +39,7 @@ TileCfg make_wave_tiles(const DevGeom& G, int vec, int waves, int rows, int max_
 // kind 2 tiles for k_pcg_b_rows (rows = 0: 2)
 TileCfg make_row_tiles(const DevGeom& G, int vec, int waves, int rows);
 // kind 3 tiles for k_pcg1: 64*vec - 4 owned columns, rows = 0: auto
-TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf = 0);
+TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf = 0, int elem = 8);
 
 enum ReduceMode : int { kSkipIfDone = 1, kBumpIter = 2 };
 

@@ -53,11 +53,11 @@ def test_pcg1_matches_cpu_oracle(pkg, monkeypatch):
 
 @pytest.mark.parametrize("ranks,kw,algo", [
     (1, {}, "pcg1"),                  # fp64, one subdomain: single pass
-    (1, {"dtype": "fp32"}, "pcg2"),   # fp32 storage: pcg2 is faster (NOTES #26)
+    (1, {"dtype": "fp32"}, "pcg1"),   # fp32 storage too (profiles/r2/fp32_pcg1_sweep.txt)
     (1, {"exact": True}, "pcg2"),     # reference arithmetic order
     (2, {}, "pcg1"),                  # decomposed: radius-2 halo
     (8, {}, "pcg1"),
-    (2, {"dtype": "fp32"}, "pcg2"),
+    (2, {"dtype": "fp32"}, "pcg1"),
     (2, {"kernel": "lds"}, "pcg2"),
 ])
 def test_auto_algorithm_selection(pkg, monkeypatch, ranks, kw, algo):
