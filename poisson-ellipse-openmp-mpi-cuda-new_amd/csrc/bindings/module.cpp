@@ -357,13 +357,14 @@ PYBIND11_MODULE(_pmx, m) {
                        int tile_rows, const std::string& dtype, bool exact, int graph_batch,
                        bool check, py::object uid, std::vector<int> ranks, std::vector<int> devices,
                        bool rccl_graph, bool overlap, int vec_b, int waves_b, int tile_rows_b,
-                       bool poison_halos, bool b_ring, int algo, bool defer_connect) {
+                       bool poison_halos, bool b_ring, int algo, bool defer_connect, int threaded) {
              SessionConfig c;
              c.spec = s;
              c.opt = make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact,
                                   graph_batch, check, overlap, vec_b, waves_b, tile_rows_b, poison_halos,
                                   b_ring, algo);
              c.defer_connect = defer_connect;
+             c.threaded = threaded;
              c.split = split;
              c.world = world;
              if (comm == "self") c.comm = CommKind::kSelf;
@@ -385,10 +386,12 @@ PYBIND11_MODULE(_pmx, m) {
            py::arg("ranks") = std::vector<int>{}, py::arg("devices") = std::vector<int>{},
            py::arg("rccl_graph") = false, py::arg("overlap") = true, py::arg("vec_b") = 0,
            py::arg("waves_b") = 0, py::arg("tile_rows_b") = -1, py::arg("poison_halos") = false,
-           py::arg("b_ring") = false, py::arg("algo") = -1, py::arg("defer_connect") = false)
+           py::arg("b_ring") = false, py::arg("algo") = -1, py::arg("defer_connect") = false,
+           py::arg("threaded") = -1)
       .def("connect", [](Session& s) { py::gil_scoped_release g; s.connect(); },
            "create the communicator and driver (sessions built with defer_connect=True)")
       .def_property_readonly("connected", &Session::connected)
+      .def_property_readonly("threaded", &Session::threaded)
       .def("local_w", [](Session& s, int i) {
              std::vector<double> w;
              { py::gil_scoped_release g; w = s.local_w(i); }

@@ -32,6 +32,11 @@
 
 namespace pmx {
 
+std::unique_ptr<Comm> Comm::rank_view(int) {
+  PMX_CHECK(false, name() << " communicator has no per-rank view (threaded drivers need RCCL)");
+  return nullptr;
+}
+
 namespace {
 
 class SelfComm final : public Comm {
@@ -85,6 +90,50 @@ class LocalComm final : public Comm {
  private:
   int n_;
   double** ptrs_ = nullptr;
+};
+
+// One local rank of an RcclComm, driven by its own host thread: its collectives need no
+// ncclGroupStart/End across local ranks (RCCL matches them per communicator, whichever thread
+// issues them); the send/recv pairs of its halo slots still form one group.
+class RcclRankView final : public Comm {
+ public:
+  RcclRankView(ncclComm_t comm, ncclComm_t halo_comm, int nranks, bool capturable)
+      : comm_(comm), halo_comm_(halo_comm), nranks_(nranks), capturable_(capturable) {}
+  void allreduce(std::vector<GpuSubdomainSolver*>& local, int which,
+                 std::vector<hipStream_t>& streams) override {
+    PMX_CHECK(local.size() == 1, "a rank view drives one subdomain");
+    double* buf = local[0]->reduce_buf(which);
+    RCCL_CHECK(ncclAllReduce(buf, buf, GpuSubdomainSolver::reduce_len(which), ncclFloat64, ncclSum, comm_,
+                             streams[0]));
+  }
+  void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>& streams) override {
+    PMX_CHECK(local.size() == 1, "a rank view drives one subdomain");
+    const CommLayout& L = local[0]->layout();
+    const ncclDataType_t t = L.elem == 8 ? ncclFloat64 : ncclFloat32;
+    RCCL_CHECK(ncclGroupStart());
+    for (int slot = 0; slot < kHaloSlots; ++slot) {
+      if (!L.active(slot)) continue;
+      RCCL_CHECK(ncclSend(local[0]->send_dev(slot), L.edge_len[slot], t, L.peer[slot], halo_comm_, streams[0]));
+      RCCL_CHECK(ncclRecv(local[0]->recv_dev(slot), L.edge_len[slot], t, L.peer[slot], halo_comm_, streams[0]));
+    }
+    RCCL_CHECK(ncclGroupEnd());
+  }
+  bool graph_capturable() const override { return capturable_; }
+  void check_health() override {
+    for (auto c : {comm_, halo_comm_}) {
+      ncclResult_t async = ncclSuccess;
+      RCCL_CHECK(ncclCommGetAsyncError(c, &async));
+      if (async != ncclSuccess && async != ncclInProgress)
+        ::pmx::fail(__FILE__, __LINE__, std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
+    }
+  }
+  std::string name() const override { return "rccl"; }
+  int world_size() const override { return nranks_; }
+
+ private:
+  ncclComm_t comm_, halo_comm_;
+  int nranks_;
+  bool capturable_;
 };
 
 class RcclComm final : public Comm {
@@ -150,6 +199,10 @@ class RcclComm final : public Comm {
   }
 
   bool graph_capturable() const override { return capturable_; }
+  std::unique_ptr<Comm> rank_view(int i) override {
+    PMX_CHECK(i >= 0 && i < int(comms_.size()), "rank view index");
+    return std::make_unique<RcclRankView>(comms_[size_t(i)], halo_comms_[size_t(i)], nranks_, capturable_);
+  }
   void check_health() override {
     for (auto* v : {&comms_, &halo_comms_})
       for (auto c : *v) {

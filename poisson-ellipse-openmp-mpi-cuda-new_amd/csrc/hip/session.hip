@@ -4,7 +4,11 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <exception>
 #include <fstream>
+#include <mutex>
+#include <set>
+#include <thread>
 
 #include "pmx/common.hpp"
 
@@ -48,7 +52,7 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
 }
 
 void Session::connect() {
-  PMX_CHECK(driver_ == nullptr, "session already connected");
+  PMX_CHECK(drivers_.empty(), "session already connected");
   std::vector<GpuSubdomainSolver*> raw;
   for (auto& s : solvers_) raw.push_back(s.get());
   switch (cfg_.comm) {
@@ -58,13 +62,122 @@ void Session::connect() {
       comm_ = make_rccl_comm(cfg_.rccl_uid, cfg_.world, cfg_.ranks, cfg_.devices, cfg_.rccl_graph);
       break;
   }
-  driver_ = std::make_unique<PcgDriver>(raw, comm_.get(), cfg_.opt.graph_batch);
+  // one host thread per GPU.  Several owned ranks on distinct devices (pmx --gpus G)
+  // get a driver each -- own streams, own graph captured by its own thread -- so no device's
+  // launches queue behind another's on one host thread.
+  const std::set<int> devs(cfg_.devices.begin(), cfg_.devices.end());
+  const bool auto_threads = cfg_.comm == CommKind::kRccl && raw.size() > 1 && devs.size() == raw.size();
+  threaded_ = cfg_.threaded == 1 || (cfg_.threaded == -1 && auto_threads);
+  PMX_CHECK(!threaded_ || cfg_.comm == CommKind::kRccl, "threaded drivers need the RCCL communicator");
+  if (!threaded_) {
+    drivers_.push_back(std::make_unique<PcgDriver>(raw, comm_.get(), cfg_.opt.graph_batch));
+    return;
+  }
+  for (size_t i = 0; i < raw.size(); ++i) {
+    views_.push_back(comm_->rank_view(int(i)));
+    HIP_CHECK(hipSetDevice(raw[i]->device()));
+    drivers_.push_back(std::make_unique<PcgDriver>(std::vector<GpuSubdomainSolver*>{raw[i]}, views_.back().get(),
+                                                   cfg_.opt.graph_batch));
+  }
 }
 
 Session::~Session() {
-  driver_.reset();
+  drivers_.clear();
+  views_.clear();
   comm_.reset();
   solvers_.clear();
+}
+
+void Session::for_drivers(const std::function<void(size_t, PcgDriver&)>& f) {
+  require_connected();
+  if (!threaded_) {
+    f(0, *drivers_[0]);
+    return;
+  }
+  std::exception_ptr err;
+  std::mutex mu;
+  std::vector<std::thread> th;
+  th.reserve(drivers_.size());
+  for (size_t i = 0; i < drivers_.size(); ++i)
+    th.emplace_back([&, i] {
+      try {
+        HIP_CHECK(hipSetDevice(solvers_[i]->device()));
+        f(i, *drivers_[i]);
+      } catch (...) {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!err) err = std::current_exception();
+      }
+    });
+  for (auto& t : th) t.join();
+  if (err) std::rethrow_exception(err);
+}
+
+hipStream_t Session::stream_of(int i) const {
+  require_connected();
+  return threaded_ ? drivers_.at(size_t(i))->streams()[0] : drivers_[0]->streams().at(size_t(i));
+}
+
+void Session::init() {
+  for_drivers([](size_t, PcgDriver& d) { d.init(); });
+}
+
+void Session::step(int64_t n) {
+  for_drivers([n](size_t, PcgDriver& d) { d.enqueue_iterations(n); });
+}
+
+void Session::synchronize() {
+  for_drivers([](size_t, PcgDriver& d) { d.synchronize(); });
+}
+
+PcgState Session::state(int i) {
+  require_connected();
+  return threaded_ ? drivers_.at(size_t(i))->state(0) : drivers_[0]->state(i);
+}
+
+RunStats Session::solve_impl(int poll_batches, bool do_init, int64_t every, const std::string& save_path) {
+  // every rank's driver iterates to the same device stop decision (the all-reduced scalars are
+  // identical everywhere); rank 0's statistics are returned
+  std::vector<RunStats> st(drivers_.size());
+  for_drivers([&](size_t i, PcgDriver& d) {
+    std::function<void(const PcgState&)> cb;
+    if (every > 0 && !save_path.empty()) {
+      cb = [&, i](const PcgState&) {
+        if (!threaded_) {
+          save_checkpoint(save_path);
+          return;
+        }
+        const std::string f = checkpoint_file(save_path, solvers_[i]->sd().rank), tmp = f + ".tmp";
+        {
+          std::ofstream os(tmp, std::ios::binary | std::ios::trunc);
+          PMX_CHECK(os.good(), "cannot open checkpoint file " << tmp);
+          solvers_[i]->save_checkpoint(os, d.streams()[0]);
+        }
+        PMX_CHECK(std::rename(tmp.c_str(), f.c_str()) == 0, "cannot rename " << tmp << " -> " << f);
+      };
+    }
+    st[i] = d.solve(poll_batches, do_init, every, cb);
+  });
+  for (const RunStats& r : st)
+    PMX_CHECK(r.iters == st[0].iters && r.status == st[0].status,
+              "ranks disagree on the stop decision (" << r.iters << " vs " << st[0].iters << " iterations)");
+  return st[0];
+}
+
+RunStats Session::solve(int poll_batches) { return solve_impl(poll_batches, true, 0, ""); }
+
+RunStats Session::profile(int64_t n) {
+  std::vector<RunStats> st(drivers_.size());
+  for_drivers([&](size_t i, PcgDriver& d) { st[i] = d.profile_phases(n); });
+  RunStats m = st[0];
+  for (const RunStats& r : st) {  // MAX over ranks, as the reference reports its buckets
+    m.t_kernel_a = std::max(m.t_kernel_a, r.t_kernel_a);
+    m.t_kernel_b = std::max(m.t_kernel_b, r.t_kernel_b);
+    m.t_reduce = std::max(m.t_reduce, r.t_reduce);
+    m.t_allreduce = std::max(m.t_allreduce, r.t_allreduce);
+    m.t_halo = std::max(m.t_halo, r.t_halo);
+    m.t_comm = std::max(m.t_comm, r.t_comm);
+  }
+  return m;
 }
 
 size_t Session::device_bytes() const {
@@ -74,8 +187,8 @@ size_t Session::device_bytes() const {
 }
 
 std::vector<double> Session::local_w(int i) {
-  drv().synchronize();
-  return solvers_.at(size_t(i))->download_w(driver_->streams()[size_t(i)]);
+  synchronize();
+  return solvers_.at(size_t(i))->download_w(stream_of(i));
 }
 
 std::vector<double> Session::gather_local_w() {
@@ -84,7 +197,7 @@ std::vector<double> Session::gather_local_w() {
   for (size_t i = 0; i < solvers_.size(); ++i) {
     auto& s = *solvers_[i];
     const Subdomain& sd = s.sd();
-    const std::vector<double> w = s.download_w(drv().streams()[i]);
+    const std::vector<double> w = s.download_w(stream_of(int(i)));
     for (int li = 1; li <= sd.nx; ++li)
       for (int lj = 1; lj <= sd.ny; ++lj)
         g[size_t(sd.gi0() + li) * (N + 1) + sd.gj0() + lj] = w[size_t(li - 1) * sd.ny + lj - 1];
@@ -97,26 +210,26 @@ std::string Session::checkpoint_file(const std::string& path, int rank) const {
 }
 
 void Session::save_checkpoint(const std::string& path) {
-  drv().synchronize();
+  synchronize();
   for (size_t i = 0; i < solvers_.size(); ++i) {
     const std::string f = checkpoint_file(path, solvers_[i]->sd().rank);
     const std::string tmp = f + ".tmp";
     {
       std::ofstream os(tmp, std::ios::binary | std::ios::trunc);
       PMX_CHECK(os.good(), "cannot open checkpoint file " << tmp);
-      solvers_[i]->save_checkpoint(os, driver_->streams()[i]);
+      solvers_[i]->save_checkpoint(os, stream_of(int(i)));
     }
     PMX_CHECK(std::rename(tmp.c_str(), f.c_str()) == 0, "cannot rename " << tmp << " -> " << f);
   }
 }
 
 void Session::load_checkpoint(const std::string& path) {
-  drv().synchronize();
+  synchronize();
   for (size_t i = 0; i < solvers_.size(); ++i) {
     const std::string f = checkpoint_file(path, solvers_[i]->sd().rank);
     std::ifstream is(f, std::ios::binary);
     PMX_CHECK(is.good(), "cannot open checkpoint file " << f);
-    solvers_[i]->load_checkpoint(is, driver_->streams()[i]);
+    solvers_[i]->load_checkpoint(is, stream_of(int(i)));
   }
 }
 
@@ -124,9 +237,7 @@ RunStats Session::solve_checkpointed(const std::string& save_path, int64_t every
                                      const std::string& resume_path, int poll_batches) {
   const bool resume = !resume_path.empty();
   if (resume) load_checkpoint(resume_path);
-  std::function<void(const PcgState&)> cb;
-  if (every > 0 && !save_path.empty()) cb = [&](const PcgState&) { save_checkpoint(save_path); };
-  return drv().solve(poll_batches, !resume, every, cb);
+  return solve_impl(poll_batches, !resume, every, save_path);
 }
 
 int64_t max_square_grid(double bytes_per_gpu, int gpus, DType dtype, double reserve_fraction) {

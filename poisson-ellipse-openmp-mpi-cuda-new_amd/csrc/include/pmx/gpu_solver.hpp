@@ -230,6 +230,9 @@ class Comm {
   virtual void check_health() {}
   virtual std::string name() const = 0;
   virtual int world_size() const = 0;
+  // A communicator for local rank i alone, for a driver thread that owns just that rank (one host
+  // thread per device).  Non-owning: valid while this communicator lives.
+  virtual std::unique_ptr<Comm> rank_view(int i);
 };
 
 std::unique_ptr<Comm> make_self_comm();

@@ -27,6 +27,10 @@ struct SessionConfig {
   // multi-process caller checks that every rank allocated its subdomain before any rank enters
   // the (blocking, collective) RCCL initialisation, so one failing rank cannot hang the others.
   bool defer_connect = false;
+  // One host thread (and one driver, graph and stream set) per owned rank: -1 = auto (RCCL with
+  // several owned ranks on distinct devices, i.e. `pmx --gpus G`), 1 = always (RCCL only; with a
+  // single rank it exercises the threaded path on one GPU), 0 = one host thread drives all ranks.
+  int threaded = -1;
 };
 
 class Session {
@@ -34,12 +38,12 @@ class Session {
   explicit Session(const SessionConfig& cfg);
   ~Session();
   void connect();  // comm + driver (called by the constructor unless cfg.defer_connect)
-  bool connected() const { return driver_ != nullptr; }
+  bool connected() const { return !drivers_.empty(); }
 
-  void init() { drv().init(); }
-  void step(int64_t n) { drv().enqueue_iterations(n); }
-  void synchronize() { drv().synchronize(); }
-  RunStats solve(int poll_batches = 1) { return drv().solve(poll_batches); }
+  void init();
+  void step(int64_t n);
+  void synchronize();
+  RunStats solve(int poll_batches = 1);
   // solve with periodic checkpoints to `save_path` (every `every` iterations; none if empty or
   // every == 0), optionally continuing from `resume_path` instead of starting from w = 0
   RunStats solve_checkpointed(const std::string& save_path, int64_t every,
@@ -48,15 +52,16 @@ class Session {
   void save_checkpoint(const std::string& path);
   void load_checkpoint(const std::string& path);
   std::string checkpoint_file(const std::string& path, int rank) const;
-  RunStats profile(int64_t n) { return drv().profile_phases(n); }
-  PcgState state(int i = 0) { return drv().state(i); }
+  RunStats profile(int64_t n);  // threaded: every bucket is the MAX over the owned ranks
+  PcgState state(int i = 0);
+  bool threaded() const { return threaded_; }  // one host thread per owned rank
 
   const ProcGrid& grid() const { return pg_; }
   int num_local() const { return int(solvers_.size()); }
   GpuSubdomainSolver& solver(int i) { return *solvers_.at(size_t(i)); }
   const std::string comm_name() const { return comm_ ? comm_->name() : "unconnected"; }
-  bool overlapped() const { return driver_ && driver_->overlapped(); }
-  bool poisoned() const { return driver_ && driver_->poisoned(); }
+  bool overlapped() const { return !drivers_.empty() && drivers_[0]->overlapped(); }
+  bool poisoned() const { return !drivers_.empty() && drivers_[0]->poisoned(); }
   size_t device_bytes() const;
   // global (M+1) x (N+1) solution filled with the subdomains owned by this process
   std::vector<double> gather_local_w();
@@ -64,15 +69,22 @@ class Session {
   std::vector<double> local_w(int i = 0);
 
  private:
-  PcgDriver& drv() const {
-    PMX_CHECK(driver_ != nullptr, "session not connected (Session::connect)");
-    return *driver_;
+  void require_connected() const {
+    PMX_CHECK(!drivers_.empty(), "session not connected (Session::connect)");
   }
+  // f(driver index, driver) for every driver: inline, or one host thread per driver (each bound
+  // to its rank's device) in threaded mode; the first exception is rethrown after all joined
+  void for_drivers(const std::function<void(size_t, PcgDriver&)>& f);
+  hipStream_t stream_of(int i) const;  // the compute stream of owned rank i
+  RunStats solve_impl(int poll_batches, bool do_init, int64_t every, const std::string& save_path);
+
   SessionConfig cfg_;
   ProcGrid pg_;
   std::vector<std::unique_ptr<GpuSubdomainSolver>> solvers_;
   std::unique_ptr<Comm> comm_;
-  std::unique_ptr<PcgDriver> driver_;
+  std::vector<std::unique_ptr<Comm>> views_;            // threaded: per-rank communicators
+  std::vector<std::unique_ptr<PcgDriver>> drivers_;     // one (all ranks) or one per rank
+  bool threaded_ = false;
 };
 
 // Largest square grid whose fields fit into `bytes_per_gpu` on `gpus` devices (SURVEY §5.7:

@@ -243,3 +243,33 @@ def test_paired_w_midrun_materialised(pkg, monkeypatch, steps):
         assert st["w_pend"] == (steps if (mode == 1 and steps % 2) else 0)
         out[mode] = s.gather_local_w()
     assert np.abs(out[1] - out[0]).max() < 1e-14
+
+
+@pytest.mark.parametrize("rccl_graph", [False, True])
+def test_threaded_rccl_session_world1(pkg, rccl_graph, tmp_path):
+    """One host thread per owned rank (the `pmx --gpus G` driver), forced on with a
+    single RCCL rank: the worker thread captures and replays its own graph, solves, profiles and
+    checkpoints; the result equals the single-thread driver's bitwise."""
+    n = pkg.load_native()
+    p = pkg.PoissonEllipse(M=400, N=600)
+    out = {}
+    for threaded in (0, 1):
+        s = n.Session(p.to_native(), world=1, comm="rccl", uid=n.rccl_unique_id(), ranks=[0], devices=[0],
+                      rccl_graph=rccl_graph, threaded=threaded)
+        assert s.threaded == bool(threaded)
+        r = s.solve(1)
+        assert r["iters"] == 546 and r["status"] == "converged"
+        out[threaded] = s.local_w(0)
+        ph = s.profile(5)
+        assert ph["t_kernel_a"] > 0.0
+        ck = str(tmp_path / f"ck{threaded}.bin")
+        r2 = s.solve_checkpointed(ck, every=100)
+        assert r2["iters"] == 546
+        s.load_checkpoint(ck)
+    assert np.array_equal(out[0], out[1])
+
+
+def test_threaded_needs_rccl(pkg):
+    n = pkg.load_native()
+    with pytest.raises(RuntimeError, match="RCCL"):
+        n.Session(pkg.PoissonEllipse(M=40, N=40).to_native(), world=2, comm="local", threaded=1)
