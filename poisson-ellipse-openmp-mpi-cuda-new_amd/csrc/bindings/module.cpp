@@ -333,6 +333,10 @@ PYBIND11_MODULE(_pmx, m) {
       .def("enqueue_halo_unpack", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_halo_unpack(as_stream(s)); })
       .def_property_readonly("single_pass", &GpuSubdomainSolver::single_pass)
       .def("enqueue_phase_a", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_phase_a(as_stream(s)); })
+      .def("enqueue_kernel_a", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_kernel_a(as_stream(s)); })
+      .def("enqueue_reduce_a", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_reduce_a(as_stream(s)); })
+      .def("enqueue_kernel_b", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_kernel_b(as_stream(s), true); })
+      .def("enqueue_reduce_b", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_reduce_b(as_stream(s)); })
       .def("enqueue_phase_b", [](GpuSubdomainSolver& g, uintptr_t s, bool pack) {
              g.enqueue_phase_b(as_stream(s), pack);
            }, py::arg("stream"), py::arg("pack") = true)

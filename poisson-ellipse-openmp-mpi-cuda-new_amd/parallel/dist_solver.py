@@ -240,13 +240,64 @@ class DistGpuPCG:
         """Per-phase times of n eager iterations (native path), reduced with MAX over ranks and
         mapped onto the reference's 5 stage-4 buckets (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:
         956-980).  Restarts the solver (init) first; values are seconds for the n iterations."""
-        if self.comm_kind != "native":
-            raise NotImplementedError("phase profiling runs on the native communicator")
-        self.session.init()
-        ph = self.session.profile(int(n))
-        vals = {"compute": ph["t_kernel_a"] + ph["t_kernel_b"], "copy": 0.0, "comm": ph["t_comm"],
-                "precond": 0.0, "dot": ph["t_reduce"]}
+        if self.comm_kind == "native":
+            self.session.init()
+            ph = self.session.profile(int(n))
+            vals = {"compute": ph["t_kernel_a"] + ph["t_kernel_b"], "copy": 0.0, "comm": ph["t_comm"],
+                    "precond": 0.0, "dot": ph["t_reduce"]}
+        else:
+            vals = self._profile_torch(int(n))
         return reduce_max(vals, self.info, self.device)
+
+    def _profile_torch(self, n: int) -> dict:
+        """Eager iterations on torch's stream with events between the steps (the torch-comm twin of
+        PcgDriver::profile_phases).  With gloo the all-reduce and the ghost exchange include their
+        device<->host staging, which lands in the comm bucket."""
+        self.init()
+        s = self._stream()
+        t = {k: 0.0 for k in PHASE_BUCKETS}
+
+        def ev():
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+
+        marks = []
+        for _ in range(n):
+            e0 = ev()
+            self.solver.enqueue_kernel_a(s)
+            e1 = ev()
+            self.solver.enqueue_reduce_a(s)
+            e2 = ev()
+            if self.single_pass:
+                self._allreduce(self.red_c)
+                e3 = ev()
+                self._halo1(s)
+                marks.append((e0, e1, e2, e3, ev(), None, None))
+            else:
+                self._allreduce(self.red_a)
+                e3 = ev()
+                self.solver.enqueue_kernel_b(s)
+                e4 = ev()
+                self.solver.enqueue_reduce_b(s)
+                e5 = ev()
+                self._allreduce(self.red_b)
+                self._exchange()
+                marks.append((e0, e1, e2, e3, e4, e5, ev()))
+        torch.cuda.synchronize(self.device)
+        ms = lambda a, b: a.elapsed_time(b) * 1e-3  # noqa: E731
+        for m in marks:
+            if self.single_pass:
+                e0, e1, e2, e3, e4 = m[:5]
+                t["compute"] += ms(e0, e1)
+                t["dot"] += ms(e1, e2)
+                t["comm"] += ms(e2, e3) + ms(e3, e4)
+            else:
+                e0, e1, e2, e3, e4, e5, e6 = m
+                t["compute"] += ms(e0, e1) + ms(e3, e4)
+                t["dot"] += ms(e1, e2) + ms(e4, e5)
+                t["comm"] += ms(e2, e3) + ms(e5, e6)
+        return t
 
     def solve(self, gather: bool = True, batch: int | None = None) -> Result:
         batch = batch or max(self.graph_batch, 16)

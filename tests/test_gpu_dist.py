@@ -70,7 +70,7 @@ def test_native_multiprocess_odd_blocks(pkg, tmp_path):
 def test_bench_share_gpu_rehearsal(tmp_path):
     """bench.py --gpus 2 spawns its own ranks; --share-gpu runs them on GPU 0 (valid=false)."""
     p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--share-gpu", "--M", "512", "--N", "512",
-                        "--steps", "20", "--warmup", "4", "--tol-time-cap", "60"],
+                        "--steps", "20", "--warmup", "4", "--tol-time-cap", "60", "--profile-phases", "8"],
                        cwd=ROOT, capture_output=True, text=True, timeout=170)
     assert p.returncode == 0, p.stderr[-4000:]
     lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
@@ -78,3 +78,7 @@ def test_bench_share_gpu_rehearsal(tmp_path):
     j = lines[0]
     assert j["n_gpus"] == 2 and j["valid"] is False and j["tol_status"] == "converged"
     assert j["config"]["comm"] == "gloo-host-staged" and j["config"]["tile"]["algo"] == "pcg1"
+    # phase buckets of the torch-comm path, MAX over the 2 ranks, table printed by rank 0 only
+    ph = j["phase_seconds_per_iter_max_over_ranks"]
+    assert set(ph) == {"compute", "copy", "comm", "precond", "dot"} and ph["compute"] > 0 and ph["comm"] > 0
+    assert p.stderr.count("max over ranks)") == 5
