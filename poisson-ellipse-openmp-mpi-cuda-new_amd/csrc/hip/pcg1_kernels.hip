@@ -420,6 +420,7 @@ k_reduce_n(const double* __restrict__ part, int n, ReduceWeights wt, double* out
   double s[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) s[q] = 0.0;
+#pragma unroll 4
   for (int i = lo + int(threadIdx.x); i < hi; i += 256) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) s[q] += part[int64_t(i) * NQ + q];
@@ -479,11 +480,12 @@ TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf, 
   if (rows <= 0) {
     // tall tiles keep the 4 extra marched rows cheap; shorter only when the grid is small
     // (>= ~8K tiles keep 3 waves/SIMD busy for a few rounds)
-    // 16384^2 sweeps (profiles/r2/pcg1_rows_sweep.txt; same-box A/B: 12 rows 2.36 ms vs 32 rows
-    // 2.52): 8 rows 2.34 ms, 12 2.34, 16 2.39, 24 2.47, 32 2.54 -- short tiles keep fewer DRAM
-    // rows in flight and win despite the 4 extra marched rows
-    rows = fp32 ? 24 : 12;
-    while (rows > 6 && int64_t((G.nx + rows - 1) / rows) * t.tiles_j < 8192) rows /= 2;
+    // fp64, interleaved same-box A/B (profiles/r2/pcg1_rows_sweep.txt): 16384^2 8 rows = 12 rows
+    // (+-0.1%), 16 rows +1.4%, 32 rows +7%; the 8-GPU per-rank shape 4096x8192: 8 rows 374 us,
+    // 12 rows 388 us (shorter tiles shrink the last, partly filled round of waves).  Short tiles
+    // keep fewer DRAM rows in flight and win despite the 4 extra marched rows.
+    rows = fp32 ? 24 : 8;
+    while (rows > 4 && int64_t((G.nx + rows - 1) / rows) * t.tiles_j < 8192) rows /= 2;
   }
   PMX_CHECK(rows >= 1 && rows <= 4096, "pcg1: tile rows must be in [1, 4096]");
   t.rows = rows;
@@ -528,7 +530,9 @@ void launch_pcg1_halo(const DevGeom& G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H
 void launch_reduce_n(const double* partials, int n, int nq, const double* weights, double* out,
                      PcgState* S, int mode, double* ws, hipStream_t s) {
   PMX_CHECK(nq == kNq, "launch_reduce_n: nq must be " << kNq);
-  const int nb = std::max(1, std::min(kReduceMaxBlocks, n / 2048));
+  // ~512 partials per block: the loads of a block are 2 rounds per thread, not a latency chain
+  // (4096x8192 fp64: 22.9K tiles, 11 -> 44 blocks)
+  const int nb = std::max(1, std::min(kReduceMaxBlocks, n / 512));
   double* chunk = ws + kReduceNOffset;
   unsigned* ticket = reinterpret_cast<unsigned*>(chunk + 8 * kReduceMaxBlocks);
   ReduceWeights wt{};
