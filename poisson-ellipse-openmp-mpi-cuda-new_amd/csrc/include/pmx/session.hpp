@@ -88,8 +88,8 @@ class Session {
 };
 
 // Largest square grid whose fields fit into `bytes_per_gpu` on `gpus` devices (SURVEY §5.7:
-// subgrids sized against 288 GB HBM per MI355X).  fp64 (single pass): 5 fields x 8 B/pt; fp32
-// (two sweeps): 4 x 4 B/pt.
+// subgrids sized against 288 GB HBM per MI355X): the default single pass keeps 5 fields, 8 B/pt
+// each in fp64 and 4 B/pt in fp32.
 int64_t max_square_grid(double bytes_per_gpu, int gpus, DType dtype, double reserve_fraction = 0.1);
 
 }  // namespace pmx

@@ -1,8 +1,8 @@
 """Single-pass PCG iteration (pcg1, csrc/hip/pcg1_kernels.hip).
 
-pcg1 is the automatic choice in fp64 with the wave kernels and the fast arithmetic -- on one
-subdomain and on decomposed grids (radius-2 halo with corner exchange) alike; PMX_ALGO=1/2 forces
-one algorithm.  It forms alpha's denominator (A p^k, p^k) from the previous sweep's partials
+pcg1 is the automatic choice with the wave kernels and the fast arithmetic, in fp64 and fp32
+storage alike, on one subdomain and on decomposed grids (radius-2 halo with corner exchange);
+PMX_ALGO=1/2 forces one algorithm.  It forms alpha's denominator (A p^k, p^k) from the previous sweep's partials
 instead of a second sweep; r is still updated with an explicitly computed A p^k.  These tests pin
 it to the two-sweep iteration (pcg2) and to the reference's iteration counts
 (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:847-943 convergence rule; SURVEY §4.1 goldens, including
