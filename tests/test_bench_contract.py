@@ -49,6 +49,8 @@ def test_bench_torchrun_dry_run(n):
     assert len(lines) == 1, p.stdout  # rank 0 only
     _check(lines[0], n, 6, 2)
     assert lines[0]["config"]["parallelism"] == f"domain{n}"
+    pg = lines[0]["config"]["process_grid"]  # default split "auto": least ghost volume
+    assert lines[0]["config"]["split"] == "auto" and pg[0] * pg[1] == n
 
 
 def test_bench_spawns_its_own_ranks():
