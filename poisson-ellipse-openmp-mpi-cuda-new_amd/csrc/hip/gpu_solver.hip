@@ -354,11 +354,11 @@ void GpuSubdomainSolver::phase_a_impl(hipStream_t s) {
 }
 
 template <typename T>
-void GpuSubdomainSolver::phase_a_kernel_only(hipStream_t s) {
+void GpuSubdomainSolver::phase_a_kernel_only(hipStream_t s, int part) {
   if (pcg1_)
     launch_pcg1<T>(geom_, tables_, static_cast<T*>(field_base(0)), static_cast<T*>(field_base(1)),
                    reinterpret_cast<T*>(r2_ + field_off_ * elem_), static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), partials_, state_,
-                   tiles1_, s);
+                   tiles1_, s, part);
   else if (tiles_.kind == 1)
     launch_pcg_a_wave<T>(geom_, tables_, static_cast<const T*>(field_base(1)),
                          static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(),
@@ -404,6 +404,11 @@ void GpuSubdomainSolver::enqueue_phase_b(hipStream_t s, bool pack) {
 }
 void GpuSubdomainSolver::enqueue_kernel_a(hipStream_t s) {
   if (opt_.dtype == DType::kFp64) phase_a_kernel_only<double>(s); else phase_a_kernel_only<float>(s);
+  after_launch(s);
+}
+void GpuSubdomainSolver::enqueue_kernel_a_part(hipStream_t s, int part) {
+  PMX_CHECK(pcg1_, "interior/frame sweeps are a pcg1 feature");
+  if (opt_.dtype == DType::kFp64) phase_a_kernel_only<double>(s, part); else phase_a_kernel_only<float>(s, part);
   after_launch(s);
 }
 void GpuSubdomainSolver::enqueue_reduce_a(hipStream_t s) {
@@ -664,20 +669,47 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
     }
     if (same_device) comm_streams_.resize(local_.size(), comm_streams_[0]);
   }
+  // Split sweep: interior tiles on the compute stream while the previous sweep's ghost exchange is
+  // in flight, frame tiles on their own stream once it has landed.  Default: on with RCCL, whose
+  // xGMI exchange is the long pole; off with LocalComm, whose device copies are cheaper than the
+  // extra launch (16384^2 as 2x2 subdomains on one GPU: 2.647 vs 2.602 ms; 2 strips: 2.416 vs
+  // 2.430).  PMX_PCG1_SPLIT=0/1 forces it.
+  const char* sp = std::getenv("PMX_PCG1_SPLIT");
+  const bool split_default = comm_->name() == "rccl";
+  split_ = overlap_ && single_pass_ && (sp && sp[0] ? sp[0] == '1' : split_default);
+  if (split_) {
+    auto ev = [](std::vector<hipEvent_t>& v) {
+      hipEvent_t e;
+      HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      v.push_back(e);
+    };
+    for (size_t i = 0; i < nstreams; ++i) {
+      HIP_CHECK(hipSetDevice(local_[i]->device()));
+      hipStream_t st;
+      HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      roctxNameHipStream("pmx:frame", st);
+      frame_streams_.push_back(st);
+      ev(ev_ar_);
+      ev(ev_fdone_);
+      ev(ev_swept_);
+      ev(ev_pk_);
+    }
+    if (same_device) frame_streams_.resize(local_.size(), frame_streams_[0]);
+  }
 }
 
 PcgDriver::~PcgDriver() {
   for (auto e : execs_) (void)hipGraphExecDestroy(e);
   for (auto g : graphs_) (void)hipGraphDestroy(g);
-  for (auto* v : {&streams_, &comm_streams_}) {
+  for (auto* v : {&streams_, &comm_streams_, &frame_streams_}) {
     hipStream_t last = nullptr;
     for (auto s : *v) {
       if (s != last) (void)hipStreamDestroy(s);
       last = s;
     }
   }
-  for (auto e : ev_packed_) (void)hipEventDestroy(e);
-  for (auto e : ev_halo_) (void)hipEventDestroy(e);
+  for (auto* v : {&ev_packed_, &ev_halo_, &ev_ar_, &ev_fdone_, &ev_swept_, &ev_pk_})
+    for (auto e : *v) (void)hipEventDestroy(e);
 }
 
 void PcgDriver::synchronize() {
@@ -732,7 +764,63 @@ void PcgDriver::halo_exchange_pcg1(std::vector<hipStream_t>& streams) {
   }
 }
 
+// Split sweep k (pcg1, decomposed, overlap on).  Streams C (compute), F (frame), H (comm):
+//   C: [all-reduce k-1] -> ev_ar -> interior tiles of sweep k ----------> wait F -> ev_swept ->
+//   F:                     wait ev_ar (+ ev_halo of k-1) -> frame tiles -'
+//   C: reduce -> all-reduce k -> wait ev_pk (the next sweep rewrites halo_k, which the pack reads)
+//   H: wait ev_swept -> pack -> ev_pk -> send/recv -> unpack -> ev_halo (joined by the next F, or
+//      by C at the end of the batch: join_halo)
+// So the ghost exchange of sweep k runs under the reduction, the all-reduce AND the interior of
+// sweep k+1; only the frame tiles (a few % of the sweep) wait for it.
+void PcgDriver::enqueue_split_iteration() {
+  for_each_stream([&](size_t i, size_t u) {
+    HIP_CHECK(hipEventRecord(ev_ar_[u], streams_[i]));
+    HIP_CHECK(hipStreamWaitEvent(frame_streams_[i], ev_ar_[u], 0));
+    if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(frame_streams_[i], ev_halo_[u], 0));
+  });
+  for (size_t i = 0; i < local_.size(); ++i) {
+    HIP_CHECK(hipSetDevice(local_[i]->device()));
+    local_[i]->enqueue_kernel_a_part(streams_[i], 1);
+    local_[i]->enqueue_kernel_a_part(frame_streams_[i], 2);
+  }
+  for_each_stream([&](size_t i, size_t u) {
+    HIP_CHECK(hipEventRecord(ev_fdone_[u], frame_streams_[i]));
+    HIP_CHECK(hipStreamWaitEvent(streams_[i], ev_fdone_[u], 0));
+    HIP_CHECK(hipEventRecord(ev_swept_[u], streams_[i]));
+    HIP_CHECK(hipStreamWaitEvent(comm_streams_[i], ev_swept_[u], 0));
+  });
+  for (size_t i = 0; i < local_.size(); ++i) {
+    HIP_CHECK(hipSetDevice(local_[i]->device()));
+    local_[i]->enqueue_halo_pack(comm_streams_[i]);
+  }
+  for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipEventRecord(ev_pk_[u], comm_streams_[i])); });
+  poison(comm_streams_);
+  comm_->halo(local_, comm_streams_);
+  for (size_t i = 0; i < local_.size(); ++i) {
+    HIP_CHECK(hipSetDevice(local_[i]->device()));
+    local_[i]->enqueue_halo_unpack(comm_streams_[i]);
+  }
+  for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipEventRecord(ev_halo_[u], comm_streams_[i])); });
+  halo_pending_ = true;
+  for (size_t i = 0; i < local_.size(); ++i) {
+    HIP_CHECK(hipSetDevice(local_[i]->device()));
+    local_[i]->enqueue_reduce_a(streams_[i]);
+  }
+  comm_->allreduce(local_, 2, streams_);
+  for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipStreamWaitEvent(streams_[i], ev_pk_[u], 0)); });
+}
+
+void PcgDriver::join_halo() {
+  if (!halo_pending_) return;
+  for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipStreamWaitEvent(streams_[i], ev_halo_[u], 0)); });
+  halo_pending_ = false;
+}
+
 void PcgDriver::enqueue_one_iteration() {
+  if (split_) {
+    enqueue_split_iteration();
+    return;
+  }
   if (single_pass_) {
     // Single pass.  Every tile of sweep k+1 needs alpha_{k+1}, i.e. the all-reduced sums of
     // sweep k, so no part of the next sweep can start before the all-reduce; what CAN run
@@ -830,6 +918,7 @@ void PcgDriver::build_graph() {
     return;
   }
   for (int k = 0; k < graph_batch_; ++k) enqueue_one_iteration();
+  join_halo();  // a captured batch is self-contained: every forked stream rejoins
   if (hipStreamEndCapture(streams_[0], &g) != hipSuccess || !g) {
     (void)hipGetLastError();
     return;
@@ -854,6 +943,7 @@ void PcgDriver::enqueue_iterations(int64_t n) {
       HIP_CHECK(hipGraphLaunch(execs_[0], streams_[0]));
   }
   for (; done < n; ++done) enqueue_one_iteration();
+  join_halo();
 }
 
 PcgState PcgDriver::state(int idx) {

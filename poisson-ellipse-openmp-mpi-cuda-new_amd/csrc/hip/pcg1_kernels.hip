@@ -277,10 +277,45 @@ constexpr int pcg1_min_waves() {
   return VEC == 2 && WAVES == 1 ? (PF <= 2 ? 3 : 2) : 1;
 }
 
+// Which tiles a launch covers (launch_pcg1's part) and where tile k of that launch sits.
+struct Pcg1Part {
+  int part;  // 0 all, 1 interior rectangle, 2 frame
+  int tiles_i, ti_lo, ti_hi, tj_lo, tj_hi;
+};
+
+// k-th tile of the part -> (ti, tj); false past the end.  The frame is enumerated as: tile rows
+// above the interior rectangle, tile rows below it, then the left and right columns beside it.
+__device__ __forceinline__ bool pcg1_tile(int k, const Pcg1Part& P, int tiles_j, int& ti, int& tj) {
+  if (P.part == 0) {
+    ti = k / tiles_j;
+    tj = k - ti * tiles_j;
+    return ti < P.tiles_i;
+  }
+  const int h = P.ti_hi - P.ti_lo;
+  if (P.part == 1) {
+    const int wj = P.tj_hi - P.tj_lo;
+    if (wj <= 0 || k >= h * wj) return false;
+    ti = P.ti_lo + k / wj;
+    tj = P.tj_lo + k % wj;
+    return true;
+  }
+  const int ntop = P.ti_lo * tiles_j;
+  if (k < ntop) { ti = k / tiles_j; tj = k % tiles_j; return true; }
+  k -= ntop;
+  const int nbot = (P.tiles_i - P.ti_hi) * tiles_j;
+  if (k < nbot) { ti = P.ti_hi + k / tiles_j; tj = k % tiles_j; return true; }
+  k -= nbot;
+  if (P.tj_lo > 0 && k < h * P.tj_lo) { ti = P.ti_lo + k / P.tj_lo; tj = k % P.tj_lo; return true; }
+  k -= h * P.tj_lo;
+  const int wr = tiles_j - P.tj_hi;
+  if (wr > 0 && k < h * wr) { ti = P.ti_lo + k / wr; tj = P.tj_hi + k % wr; return true; }
+  return false;
+}
+
 template <typename T, int VEC, int WAVES, int PF>
 __global__ void __launch_bounds__(64 * WAVES, (pcg1_min_waves<VEC, WAVES, PF>()))
 k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
-       double* __restrict__ partials, PcgState* S, int TI, int tiles_j, int ntiles) {
+       double* __restrict__ partials, PcgState* S, int TI, int tiles_j, int ntiles, Pcg1Part part) {
   constexpr int WO = 64 * VEC - 4;  // owned columns per tile
   if (S->done) return;
   const long long k = S->it;  // 0 = the init sweep (alpha = beta = 0: sums of r^0, z^0 only)
@@ -327,9 +362,12 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) S->halo_k = k + 1;  // the next exchange fills sweep k+1's inputs
-  const int id = xcd_remap(blockIdx.x, gridDim.x) * WAVES + __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
-  if (id >= ntiles) return;
-  const int ti = id / tiles_j, tj = id - ti * tiles_j;
+  int ti = 0, tj = 0;
+  if (!pcg1_tile(xcd_remap(blockIdx.x, gridDim.x) * WAVES + __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)),
+                 part, tiles_j, ti, tj))
+    return;
+  const int id = ti * tiles_j + tj;  // the tile's partials slot, whichever launch covers it
+  (void)ntiles;
   const int i0 = 1 + ti * TI, i1 = min(i0 + TI - 1, G.nx);
   const int j0 = 1 + tj * WO, j1 = min(j0 + WO - 1, G.ny);
   T* pnew = (k & 1) ? p1 : p0;
@@ -368,8 +406,10 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
 // 4 = (field, line)).  Tiny and stream-ordered; launched by the driver between two sweeps.
 template <typename T>
 __global__ void __launch_bounds__(256)
-k_pcg1_halo(DevGeom G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, const PcgState* S, int unpack) {
+k_pcg1_halo(DevGeom G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, PcgState* S, int unpack) {
   const int slot = blockIdx.y;
+  if (!unpack && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0)
+    S->halo_k_unpack = S->halo_k;  // see PcgState::halo_k_unpack
   if (!((G.nb >> slot) & 1)) return;
   const int f = blockIdx.z >> 1, q = blockIdx.z & 1;
   const int t = blockIdx.x * 256 + threadIdx.x;
@@ -392,7 +432,7 @@ k_pcg1_halo(DevGeom G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, const PcgState*
     lj = yhi ? (unpack ? ny + 1 : ny) : (unpack ? 0 : 1);
     idx = f;
   }
-  const long long kk = S->halo_k;
+  const long long kk = unpack ? S->halo_k_unpack : S->halo_k;
   T* fld = f == 0 ? ((kk & 1) ? r2 : r) : ((kk & 1) ? p0 : p1);
   const int64_t o = int64_t(li) * G.pitch + lj;
   if (unpack)
@@ -490,18 +530,33 @@ TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf, 
   PMX_CHECK(rows >= 1 && rows <= 4096, "pcg1: tile rows must be in [1, 4096]");
   t.rows = rows;
   t.tiles_i = (G.nx + rows - 1) / rows;
+  // interior rectangle: tiles whose marched rows i0-2 .. i1+2 and loaded columns j0-2 ..
+  // j0+64*vec-3 stay clear of the ghost cells of every side that has a neighbour
+  auto cdiv = [](int a, int b) { return a <= 0 ? 0 : (a + b - 1) / b; };
+  t.ti_lo = (G.nb & kNbXlo) ? (rows == 1 ? 2 : 1) : 0;
+  t.ti_hi = (G.nb & kNbXhi) ? std::max(0, cdiv(G.nx - 1, rows) - 1) : t.tiles_i;
+  t.tj_lo = (G.nb & kNbYlo) ? 1 : 0;
+  t.tj_hi = (G.nb & kNbYhi) ? cdiv(G.ny + 3 - 64 * vec, t.block) : t.tiles_j;
+  t.ti_lo = std::min(t.ti_lo, t.tiles_i);
+  t.ti_hi = std::min(std::max(t.ti_hi, t.ti_lo), t.tiles_i);
+  t.tj_lo = std::min(t.tj_lo, t.tiles_j);
+  t.tj_hi = std::min(std::max(t.tj_hi, t.tj_lo), t.tiles_j);
   return t;
 }
 
 template <typename T>
 void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1,
-                 double* partials, PcgState* S, const TileCfg& tc, hipStream_t s) {
+                 double* partials, PcgState* S, const TileCfg& tc, hipStream_t s, int part) {
   PMX_CHECK(tc.kind == 3, "launch_pcg1 needs make_pcg1_tiles");
+  PMX_CHECK(part >= 0 && part <= 2, "launch_pcg1: part must be 0, 1 or 2");
+  const Pcg1Part P{part, tc.tiles_i, tc.ti_lo, tc.ti_hi, tc.tj_lo, tc.tj_hi};
+  const int count = part == 0 ? tc.ntiles() : part == 1 ? tc.interior_tiles() : tc.ntiles() - tc.interior_tiles();
+  if (count == 0) return;
   PMX_CHECK(G.nb == 0 || (G.nx >= 2 && G.ny >= 2), "pcg1 on a decomposed grid needs subdomains >= 2 x 2");
-  const int nb = (tc.ntiles() + tc.waves - 1) / tc.waves;
+  const int nb = (count + tc.waves - 1) / tc.waves;
   const int bs = 64 * tc.waves;
 #define PMX_PCG1(V, WV, PF) \
-  hipLaunchKernelGGL((k_pcg1<T, V, WV, PF>), dim3(nb), dim3(bs), 0, s, G, Tb, w, r, r2, p0, p1, partials, S, tc.rows, tc.tiles_j, tc.ntiles())
+  hipLaunchKernelGGL((k_pcg1<T, V, WV, PF>), dim3(nb), dim3(bs), 0, s, G, Tb, w, r, r2, p0, p1, partials, S, tc.rows, tc.tiles_j, tc.ntiles(), P)
   // instantiated shapes: the default (VEC 2, 1 wave, prefetch 1) and the ones the sweeps still
   // compare against (prefetch 2-4; 2 or 4 waves per workgroup; VEC 4)
   if (tc.vec == 2 && tc.waves == 1) {
@@ -518,7 +573,7 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
 }
 
 template <typename T>
-void launch_pcg1_halo(const DevGeom& G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, const PcgState* S,
+void launch_pcg1_halo(const DevGeom& G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, PcgState* S,
                       bool unpack, hipStream_t s) {
   if (G.nb == 0) return;
   const int len = std::max(G.nx, G.ny);
@@ -542,12 +597,12 @@ void launch_reduce_n(const double* partials, int n, int nq, const double* weight
 }
 
 template void launch_pcg1<double>(const DevGeom&, const DevTables&, double*, double*, double*, double*,
-                                  double*, double*, PcgState*, const TileCfg&, hipStream_t);
+                                  double*, double*, PcgState*, const TileCfg&, hipStream_t, int);
 template void launch_pcg1_halo<double>(const DevGeom&, double*, double*, double*, double*, HaloBufs<double>,
-                                        const PcgState*, bool, hipStream_t);
+                                        PcgState*, bool, hipStream_t);
 template void launch_pcg1_halo<float>(const DevGeom&, float*, float*, float*, float*, HaloBufs<float>,
-                                       const PcgState*, bool, hipStream_t);
+                                       PcgState*, bool, hipStream_t);
 template void launch_pcg1<float>(const DevGeom&, const DevTables&, float*, float*, float*, float*, float*,
-                                 double*, PcgState*, const TileCfg&, hipStream_t);
+                                 double*, PcgState*, const TileCfg&, hipStream_t, int);
 
 }  // namespace pmx

@@ -77,9 +77,11 @@ struct alignas(64) PcgState {
   // (Ap,p) (weighted) and |p|^2 (weighted per norm) of the last sweep.
   double red_c[5];
   // Single-pass halo: index of the sweep whose input buffers (r^{k-1}, p^{k-1}) the next ghost
-  // exchange fills.  Written by sweep k (= k + 1) and by init (= 0); read by k_pcg1_halo, which
-  // runs on the comm stream between the sweeps, so it never races with the writer.
+  // exchange fills.  Written by sweep k (= k + 1) and by init (= 0); read by the pack kernel,
+  // which the next sweep waits for.  The pack copies it to halo_k_unpack for the unpack kernel,
+  // which may still run while the next sweep's interior tiles (and their halo_k write) run.
   long long halo_k;
+  long long halo_k_unpack;
 };
 
 // Pointers for the halo ("ghost") exchange, one per slot (see kHaloSlots).  Two-sweep iteration:

@@ -124,6 +124,9 @@ class GpuSubdomainSolver {
   void enqueue_phase_a(hipStream_t s);  // k_pcg_a + reduce -> red_a
   // the two halves of each phase, for per-step timing (PcgDriver::profile_phases)
   void enqueue_kernel_a(hipStream_t s);
+  // pcg1 only: the interior (part 1) or frame (part 2) tiles of the sweep, see launch_pcg1
+  void enqueue_kernel_a_part(hipStream_t s, int part);
+  bool has_interior_split() const { return pcg1_ && geom_.nb != 0; }
   void enqueue_reduce_a(hipStream_t s);
   void enqueue_kernel_b(hipStream_t s, bool pack);
   void enqueue_reduce_b(hipStream_t s);
@@ -180,7 +183,7 @@ class GpuSubdomainSolver {
   template <typename T> void init_impl(hipStream_t s);
   template <typename T> void phase_a_impl(hipStream_t s);
   template <typename T> void phase_b_impl(hipStream_t s, bool pack);
-  template <typename T> void phase_a_kernel_only(hipStream_t s);
+  template <typename T> void phase_a_kernel_only(hipStream_t s, int part = 0);
   template <typename T> void phase_b_kernel_only(hipStream_t s, bool pack = true);
   template <typename T> HaloBufs<T> halo() const;
   template <typename T> void halo_impl(hipStream_t s, bool unpack);
@@ -285,6 +288,8 @@ class PcgDriver {
  private:
   void enqueue_one_iteration();
   void halo_exchange_pcg1(std::vector<hipStream_t>& streams);  // pack -> comm -> unpack
+  void enqueue_split_iteration();  // pcg1, decomposed, overlap: interior/frame sweep split
+  void join_halo();                // compute stream waits for a pending ghost exchange
   void build_graph();
   template <typename F> void for_each_stream(F&& f);
   void poison(std::vector<hipStream_t>& streams);
@@ -300,6 +305,11 @@ class PcgDriver {
   bool any_nb_ = false;
   std::vector<hipStream_t> comm_streams_;
   std::vector<hipEvent_t> ev_packed_, ev_halo_;
+  // split sweep (pcg1 with neighbours and overlap): the frame tiles run on their own stream
+  bool split_ = false;
+  bool halo_pending_ = false;  // a ghost exchange on the comm stream not yet joined
+  std::vector<hipStream_t> frame_streams_;
+  std::vector<hipEvent_t> ev_ar_, ev_fdone_, ev_swept_, ev_pk_;
   bool graph_ok_ = false;
   std::vector<hipGraph_t> graphs_;
   std::vector<hipGraphExec_t> execs_;

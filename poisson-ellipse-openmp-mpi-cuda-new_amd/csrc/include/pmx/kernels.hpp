@@ -29,6 +29,10 @@ struct TileCfg {
   int pair_w = 0;     // kind 2: paired w updates (k_pcg_b_rows_paired, pcg_kernels_dpp.hip)
   int pf = 1;         // kind 3: rows prefetched ahead of the computed row
   int tiles_i = 0, tiles_j = 0;
+  // kind 3 on decomposed grids: the tiles [ti_lo, ti_hi) x [tj_lo, tj_hi) read no ghost cell of a
+  // side that has a neighbour ("interior"); the rest form the frame (see launch_pcg1's part)
+  int ti_lo = 0, ti_hi = 0, tj_lo = 0, tj_hi = 0;
+  int interior_tiles() const { return (ti_hi - ti_lo) * (tj_hi - tj_lo); }
   int ntiles() const { return tiles_i * tiles_j; }
 };
 
@@ -79,14 +83,17 @@ void launch_pcg_b_wave(const DevGeom& G, const DevTables& Tb, T* w, T* r, const 
 // r is double-buffered (overlapped tiles read neighbour rows/columns of r^{k-1} while others
 // write r^k): sweep k reads (k & 1 ? r2 : r).  Decomposed grids read the radius-2 ghosts that
 // launch_pcg1_halo unpacked into the fields.
+// part: 0 = every tile; 1 = the interior tiles only (they read no ghost cell, so they may run
+// while the previous sweep's ghost exchange is still in flight); 2 = the frame tiles only.
+// Parts 1 and 2 of one sweep may run concurrently on two streams: they write disjoint partials.
 template <typename T>
 void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1,
-                 double* partials, PcgState* S, const TileCfg& tc, hipStream_t s);
+                 double* partials, PcgState* S, const TileCfg& tc, hipStream_t s, int part = 0);
 
 // pcg1 ghost exchange: pack (unpack=false) the radius-2 edges of the buffers the next sweep reads
 // (selected on the device by S->halo_k) into H.send, or unpack H.recv into their ghost cells.
 template <typename T>
-void launch_pcg1_halo(const DevGeom& G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, const PcgState* S,
+void launch_pcg1_halo(const DevGeom& G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, PcgState* S,
                       bool unpack, hipStream_t s);
 
 // Halo/compute overlap: r^{k+1} on the subdomain edges that have a neighbour,
