@@ -10,7 +10,7 @@ for g in ${AB_GRIDS:-"16384x16384" "4096x8192"}; do
   for r in $(seq 1 ${ROUNDS:-3}); do
     for v in base new; do
       if [ $v = base ]; then B=$BASE; E=${AB_ENV_A:-}; else B=$NEW; E=${AB_ENV_B:-}; fi
-      env $E timeout -k 10 120 $B ${g/x/ } --max-iter ${ITERS:-2000} --json > $O/${g}_${v}_$r.log 2>&1 || { echo "FAILED $v $g"; tail -5 $O/${g}_${v}_$r.log; exit 1; }
+      env $E timeout -k 10 120 $B ${g/x/ } --max-iter ${ITERS:-2000} --json ${ABB_ARGS:-} > $O/${g}_${v}_$r.log 2>&1 || { echo "FAILED $v $g"; tail -5 $O/${g}_${v}_$r.log; exit 1; }
     done
   done
   python3 - "$O" "$g" "${ROUNDS:-3}" <<'PY'

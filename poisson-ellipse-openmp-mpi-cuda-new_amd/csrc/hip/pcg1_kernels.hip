@@ -269,12 +269,17 @@ done:
   }
 }
 
-// Waves per SIMD the register allocation must allow.  VEC=2, 1 wave/workgroup: 148 VGPRs at
-// PF=1 and 166 at PF=2 fit 3 waves/SIMD with no spills (the MFMA reduction then stays out of
-// AGPRs); PF >= 3 needs > 168 and runs at 2.  Other shapes: whatever the allocator picks.
-template <int VEC, int WAVES, int PF>
+// Waves per SIMD the register allocation must allow (VEC=2, 1 wave/workgroup):
+//  * fp64: 139 VGPRs at PF=1 and 153 at PF=2 fit 3 waves/SIMD with no spills; forcing 4 (127
+//    VGPRs, 4 spilled) is 2.65% slower (NOTES #36).  PF >= 3 runs at 2.
+//  * fp32 storage (half the prefetch registers): PF=1 fits 4 waves/SIMD with no spills (127
+//    VGPRs) -- 32768^2 4.54 vs 5.03 ms at 3 waves/SIMD with PF=2 (NOTES #37); PF=2 would spill.
+// Other shapes: whatever the allocator picks.
+template <typename T, int VEC, int WAVES, int PF>
 constexpr int pcg1_min_waves() {
-  return VEC == 2 && WAVES == 1 ? (PF <= 2 ? 3 : 2) : 1;
+  if (VEC != 2 || WAVES != 1) return 1;
+  if (sizeof(T) == 4 && PF == 1) return 4;
+  return PF <= 2 ? 3 : 2;
 }
 
 // Which tiles a launch covers (launch_pcg1's part) and where tile k of that launch sits.
@@ -313,7 +318,7 @@ __device__ __forceinline__ bool pcg1_tile(int k, const Pcg1Part& P, int tiles_j,
 }
 
 template <typename T, int VEC, int WAVES, int PF>
-__global__ void __launch_bounds__(64 * WAVES, (pcg1_min_waves<VEC, WAVES, PF>()))
+__global__ void __launch_bounds__(64 * WAVES, (pcg1_min_waves<T, VEC, WAVES, PF>()))
 k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
        double* __restrict__ partials, PcgState* S, int TI, int tiles_j, int ntiles, Pcg1Part part) {
   constexpr int WO = 64 * VEC - 4;  // owned columns per tile
@@ -512,10 +517,10 @@ TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf, 
   t.vec = vec;
   t.waves = waves;
   t.block = 64 * vec - 4;  // owned columns per tile
-  // fp32 storage: half the bytes per row, so the prefetch ring is cheap and a deeper one pays
-  // (32768^2: PF 2 x 24 rows 5.06 ms vs PF 1 x 12 rows 5.20, profiles/r2/fp32_pcg1_sweep.txt)
+  // fp32 storage: PF 1 at 4 waves/SIMD (see pcg1_min_waves) with 24-row tiles
+  // (profiles/r2/fp32_pcg1_sweep.txt)
   const bool fp32 = elem == 4;
-  t.pf = pf ? pf : (vec == 2 && waves == 1 ? (fp32 ? 2 : kPcg1AutoPf) : 1);
+  t.pf = pf ? pf : (vec == 2 && waves == 1 ? kPcg1AutoPf : 1);
   t.tiles_j = (G.ny + t.block - 1) / t.block;
   if (rows <= 0) {
     // tall tiles keep the 4 extra marched rows cheap; shorter only when the grid is small
