@@ -62,6 +62,8 @@ py::dict state_dict(const PcgState& st) {
   d["status"] = std::string(status_name(Status(st.status)));
   d["nan"] = bool(st.nan_flag);
   d["w_pend"] = st.w_pend;
+  d["w_pend_n"] = st.w_pend_n;
+  d["w_cycle"] = st.w_cycle;
   return d;
 }
 

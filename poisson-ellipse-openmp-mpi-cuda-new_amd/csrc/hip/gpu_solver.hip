@@ -91,6 +91,8 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_PCG1_ROWS", o.rows1);
   env_int("PMX_PCG1_WAVES", o.waves1);
   env_int("PMX_PCG1_PF", o.pf1);
+  env_int("PMX_PCG1_WCYCLE", o.wcycle1);
+  PMX_CHECK(o.wcycle1 == 2 || o.wcycle1 == 3, "pcg1 w cycle must be 2 or 3");
   PMX_CHECK(o.pair_w >= 0 && o.pair_w <= 2, "pair_w must be 0, 1 or 2");
   PMX_CHECK(o.algo == -1 || o.algo == 1 || o.algo == 2, "algo must be -1, 1 or 2");
   o.resolved = true;
@@ -317,6 +319,7 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
   st.norm = int(spec_.norm);
   st.pair_w = opt_.pair_w ? 1 : 0;
   st.pair_min_beta = opt_.pair_w == 2 ? HUGE_VAL : 1e-3;
+  st.w_cycle = elem_ == 8 ? opt_.wcycle1 : 2;  // fp32 k_pcg1 is built with pairs only
   HIP_CHECK(hipMemcpyAsync(state_, &st, sizeof(PcgState), hipMemcpyHostToDevice, s));
   T* w = static_cast<T*>(field_base(0));
   T* r = static_cast<T*>(field_base(1));
@@ -464,7 +467,7 @@ void GpuSubdomainSolver::save_checkpoint(std::ostream& os, hipStream_t s) const 
   HIP_CHECK(hipStreamSynchronize(s));
   CkptHeader h{};
   std::memcpy(h.magic, kCkptMagic, 8);
-  h.version = pcg1_ ? 4 : 3;  // v3: fields with 2 ghost rows; v4: + pcg1 state, r2 appended
+  h.version = pcg1_ ? 5 : 3;  // v3: fields with 2 ghost rows; v5: + pcg1 state (w cycle), r2 appended
   h.M = spec_.M; h.N = spec_.N; h.gi0 = sd_.gi0(); h.gj0 = sd_.gj0();
   h.rank = sd_.rank; h.elem = int32_t(elem_); h.norm = int32_t(spec_.norm);
   h.nx = sd_.nx; h.ny = sd_.ny; h.pitch = geom_.pitch; h.field_bytes = int64_t(field_bytes_);
@@ -487,8 +490,8 @@ void GpuSubdomainSolver::load_checkpoint(std::istream& is, hipStream_t s) {
   CkptHeader h{};
   is.read(reinterpret_cast<char*>(&h), sizeof(h));
   PMX_CHECK(is.good() && std::memcmp(h.magic, kCkptMagic, 8) == 0 &&
-                h.version == (pcg1_ ? 4 : 3),
-            "not a pmx checkpoint of this iteration algorithm and layout (v3 pcg2, v4 pcg1)");
+                h.version == (pcg1_ ? 5 : 3),
+            "not a pmx checkpoint of this iteration algorithm and layout (v3 pcg2, v5 pcg1)");
   PMX_CHECK(h.M == spec_.M && h.N == spec_.N && h.gi0 == sd_.gi0() && h.gj0 == sd_.gj0() &&
                 h.nx == sd_.nx && h.ny == sd_.ny && h.rank == sd_.rank,
             "checkpoint is for a different grid/decomposition (M=" << h.M << " N=" << h.N << " rank "
@@ -536,6 +539,8 @@ double GpuSubdomainSolver::bench_kernel(int which, int abl, int reps, hipStream_
   st.red_b[1] = 1e-3;
   st.zr[0] = st.zr[1] = 1e-3;
   st.alpha[0] = st.alpha[1] = 1.0;
+  for (int q = 0; q < 4; ++q) st.alpha1[q] = st.beta1[q] = 1.0;
+  st.w_cycle = elem_ == 8 ? opt_.wcycle1 : 2;
   st.red_c[0] = 1e-3;
   st.red_c[1] = st.red_c[3] = st.red_c[4] = 1.0;
   st.pair_w = opt_.pair_w ? 1 : 0;
@@ -607,22 +612,30 @@ std::vector<double> GpuSubdomainSolver::download_w(hipStream_t s) const {
   const std::vector<double> f = download_field(0, s);
   // Paired w updates (k_pcg_b_rows): an odd iteration leaves w^{k+1} = w^k + alpha_k p^k pending
   // in device memory; apply it here, rounded to the storage type like a device update.
+  // pcg1 (k_pcg1) leaves w_pend_n (1 or 2) steps pending, p^j in p[j & 1], alpha_j in alpha1[j & 3].
   const PcgState st = read_state(s);
-  std::vector<double> pk;
-  double a = 0.0;
-  if (st.w_pend > 0) {
-    pk = download_field((st.w_pend & 1) ? 3 : 2, s);
-    a = st.alpha[st.w_pend & 1];
+  std::vector<double> pk[2];
+  double a[2] = {0.0, 0.0};
+  int npend = 0;
+  if (pcg1_ && st.w_pend_n > 0 && st.w_pend > 0) {
+    npend = st.w_pend_n;
+    for (int q = 0; q < npend; ++q) {  // q = 0: the oldest pending step
+      const long long j = st.w_pend - (npend - 1) + q;
+      pk[q] = download_field((j & 1) ? 3 : 2, s);
+      a[q] = st.alpha1[j & 3];
+    }
+  } else if (!pcg1_ && st.w_pend > 0) {
+    npend = 1;
+    pk[0] = download_field((st.w_pend & 1) ? 3 : 2, s);
+    a[0] = st.alpha[st.w_pend & 1];
   }
   std::vector<double> out(size_t(sd_.nx) * sd_.ny);
   for (int li = 1; li <= sd_.nx; ++li)
     for (int lj = 1; lj <= sd_.ny; ++lj) {
       const size_t src = size_t(li) * (sd_.ny + 2) + lj;
       double v = f[src];
-      if (!pk.empty()) {
-        v = std::fma(a, pk[src], v);
-        if (elem_ == 4) v = double(float(v));
-      }
+      for (int q = 0; q < npend; ++q) v = std::fma(a[q], pk[q][src], v);
+      if (npend && elem_ == 4) v = double(float(v));
       out[size_t(li - 1) * sd_.ny + (lj - 1)] = v;
     }
   return out;

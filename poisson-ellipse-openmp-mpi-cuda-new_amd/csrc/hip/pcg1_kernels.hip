@@ -109,20 +109,27 @@ __device__ __forceinline__ void coef(const RowCo& c, const DevTables& Tb, const 
 
 template <typename T, int VEC>
 struct Pcg1Row {
-  T r[VEC], p[VEC], w[VEC];
+  T r[VEC], p[VEC], w[VEC], q[VEC];  // q: p^{k-2} (WM 3 only)
 };
+
+// w schedule of one sweep (template WM of pcg1_march): 0 = w untouched; 1 = pairs, w += c1 p^{k-1}
+// + alpha p^k; 2 = triples with p^{k-2} recovered, w += c2 (p^{k-1} - z^{k-2}) + c1 p^{k-1} +
+// alpha p^k (c2 = alpha_{k-2} / beta_{k-1}); 3 = triples re-reading p^{k-2}, w += c2 p^{k-2} + ...
+// (c2 = alpha_{k-2}).  See k_pcg1.
+
 
 // FAST: an interior tile (full width, every marched row and column strictly inside the global
 // domain, VEC = 2): no Dirichlet masks, and ownership is a fixed lane set (lanes 1..62 own both
 // their columns, lanes 0 and 63 none), so the sums accumulate unmasked and are masked once at the
 // end.  Same arithmetic as the general path, so a point's values never depend on its tile.
-template <typename T, int VEC, int PF, bool EVEN, bool FAST>
+template <typename T, int VEC, int PF, int WM, bool FAST>
 __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb, T* __restrict__ w,
                                            const T* __restrict__ rold, T* __restrict__ rnew,
                                            const T* __restrict__ pold,
-                                           T* __restrict__ pnew, int i0, int i1, int j0, int j1,
-                                           double alpha, double beta, double alpha_prev,
+                                           T* pnew, int i0, int i1, int j0, int j1,
+                                           double alpha, double beta, double c1, double c2,
                                            double (&acc)[kNq]) {
+  constexpr bool WUP = WM != 0;
   const int64_t P = G.pitch;
   const int lane = threadIdx.x & 63;
   const int c0 = j0 - 2 + lane * VEC;
@@ -150,16 +157,19 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     const int mc = min(max(m, -1), G.nx + 2);  // rows -1 .. nx+2 exist (2 ghost layers)
     load_cols<T, VEC>(rold + int64_t(mc) * P, c0, cmax, b.r);
     load_cols<T, VEC>(pold + int64_t(mc) * P, c0, cmax, b.p);
-    if constexpr (EVEN) {  // w of the row stage B handles next step
+    if constexpr (WUP) {  // w of the row stage B handles next step
       const int wc = min(max(m - 1, -1), G.nx + 2);
       load_cols<T, VEC>(w + int64_t(wc) * P, c0, cmax, b.w);
+      // p^{k-2} still sits in the buffer this sweep overwrites with p^k: the owner of a point
+      // reads it here, before its own store of that row (rows it does not own are never used)
+      if constexpr (WM == 3) load_cols<T, VEC>(pnew + int64_t(wc) * P, c0, cmax, b.q);
     }
   };
 
   // pipeline registers
-  double Pm2[VEC], Pm1[VEC], Zm3[VEC], Zm2[VEC], ro1[VEC], po1[VEC];
+  double Pm2[VEC], Pm1[VEC], Zm3[VEC], Zm2[VEC], ro1[VEC], po1[VEC], po2[VEC];
 #pragma unroll
-  for (int u = 0; u < VEC; ++u) Pm2[u] = Pm1[u] = Zm3[u] = Zm2[u] = ro1[u] = po1[u] = 0.0;
+  for (int u = 0; u < VEC; ++u) Pm2[u] = Pm1[u] = Zm3[u] = Zm2[u] = ro1[u] = po1[u] = po2[u] = 0.0;
   RowCo cB = row_co(Tb, grow(i0 - 3), gjlo, gjhi);  // rows m-1, m-2
   RowCo cC = cB;
 
@@ -193,6 +203,11 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     {
       const double left = dpp_shift_f64<kWaveShr1>(Pm1[VEC - 1], 0.0);
       const double right = dpp_shift_f64<kWaveShl1>(Pm1[0], 0.0);
+      double oleft = 0.0, oright = 0.0;
+      if constexpr (WM == 2) {
+        oleft = dpp_shift_f64<kWaveShr1>(po1[VEC - 1], 0.0);
+        oright = dpp_shift_f64<kWaveShl1>(po1[0], 0.0);
+      }
 #pragma unroll
       for (int u = 0; u < VEC; ++u) {
         double a0, a1, b0, b1;
@@ -206,8 +221,20 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
         const double zn = zdiv_u<false>(cB.ucls, rn, a0, a1, b0, b1, G);
         Zm1[u] = in ? zn : 0.0;
         ps[u] = static_cast<T>(Pm1[u]);
-        if constexpr (EVEN)
-          ws[u] = static_cast<T>(__builtin_fma(alpha, Pm1[u], __builtin_fma(alpha_prev, po1[u], double(cur.w[u]))));
+        if constexpr (WM == 1) {
+          ws[u] = static_cast<T>(__builtin_fma(alpha, Pm1[u], __builtin_fma(c1, po1[u], double(cur.w[u]))));
+        } else if constexpr (WM == 2) {
+          // r^{k-2} = r^{k-1} + alpha_{k-1} A p^{k-1};  p^{k-2} = (p^{k-1} - D^-1 r^{k-2}) / beta_{k-1}
+          const double xm = u == 0 ? oleft : po1[u - 1];
+          const double xp = u == VEC - 1 ? oright : po1[u + 1];
+          const double Apo = apply_a<false>(po1[u], po2[u], pom[u], xm, xp, a0, a1, b0, b1, G);
+          const double zo = zdiv_u<false>(cB.ucls, __builtin_fma(c1, Apo, ro1[u]), a0, a1, b0, b1, G);
+          const double t = __builtin_fma(c2, po1[u] - zo, double(cur.w[u]));
+          ws[u] = static_cast<T>(__builtin_fma(alpha, Pm1[u], __builtin_fma(c1, po1[u], t)));
+        } else if constexpr (WM == 3) {
+          const double t = __builtin_fma(c2, double(cur.q[u]), double(cur.w[u]));
+          ws[u] = static_cast<T>(__builtin_fma(alpha, Pm1[u], __builtin_fma(c1, po1[u], t)));
+        }
         if (ownB && (FAST || own[u])) {
           acc[0] += Zm1[u] * rn;
           acc[3] += Ap * Pm1[u];
@@ -219,7 +246,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
       const int64_t o = int64_t(mb) * P;
       store_cols<T, VEC>(rnew + o, c0, rs, FAST || own_all, own);
       store_cols<T, VEC>(pnew + o, c0, ps, FAST || own_all, own);
-      if constexpr (EVEN) store_cols<T, VEC>(w + o, c0, ws, FAST || own_all, own);
+      if constexpr (WUP) store_cols<T, VEC>(w + o, c0, ws, FAST || own_all, own);
     }
     // ---- stage C: A z^k of row m-2
     const int mcr = m - 2;
@@ -244,7 +271,9 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     for (int u = 0; u < VEC; ++u) {
       Pm2[u] = Pm1[u]; Pm1[u] = Pm[u];
       Zm3[u] = Zm2[u]; Zm2[u] = Zm1[u];
-      ro1[u] = rom[u]; po1[u] = pom[u];
+      ro1[u] = rom[u];
+      if constexpr (WM == 2) po2[u] = po1[u];
+      po1[u] = pom[u];
     }
     cC = cB;
     cB = cA;
@@ -324,13 +353,14 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
   constexpr int WO = 64 * VEC - 4;  // owned columns per tile
   if (S->done) return;
   const long long k = S->it;  // 0 = the init sweep (alpha = beta = 0: sums of r^0, z^0 only)
-  double alpha = 0.0, beta = 0.0, alpha_prev = 0.0;
+  double alpha = 0.0, beta = 0.0, c1 = 0.0, c2 = 0.0;
+  int wm = 0;
   if (k > 0) {
     const double rho = S->red_c[0];  // rho_{k-1} = (z^{k-1}, r^{k-1})
     double diff = 0.0;
     if (k >= 2) {
       // stop test of iteration k-1: ||w^k - w^{k-1}|| = |alpha_{k-1}| ||p^{k-1}||
-      diff = fabs(S->alpha[(k - 1) & 1]) * sqrt(S->red_c[4]);
+      diff = fabs(S->alpha1[(k - 1) & 3]) * sqrt(S->red_c[4]);
       const bool bad = !(diff == diff) || !(rho == rho);
       if (bad || diff < S->delta || k > S->max_iter) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -358,12 +388,34 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
       return;
     }
     alpha = rho / denom;
-    alpha_prev = S->alpha[(k - 1) & 1];
+    // w schedule.  Pairs (w_cycle 2): even sweeps add alpha_{k-1} p^{k-1} + alpha_k p^k, p^{k-1}
+    // being the p_old the sweep reads anyway.  Triples (w_cycle 3, default): sweeps k = 0 mod 3
+    // also add alpha_{k-2} p^{k-2}, recovered without reading it: sweep k-1 formed
+    // p^{k-1} = D^-1 r^{k-2} + beta_{k-1} p^{k-2} and r^{k-1} = r^{k-2} - alpha_{k-1} A p^{k-1}, so
+    // p^{k-2} = (p^{k-1} - D^-1 (r^{k-1} + alpha_{k-1} A p^{k-1})) / beta_{k-1} -- one more stencil,
+    // on the p_old this sweep already holds.  Its rounding error grows like eps / |beta_{k-1}|, so
+    // below pair_min_beta the sweep re-reads p^{k-2} from the buffer it is about to overwrite.
+    // w moves on one sweep in three: 37.3 instead of 40 B/pt per iteration.  The stop test uses
+    // |alpha| ||p||, so the schedule changes no iteration count, only w's rounding.
+    const int cyc = S->w_cycle;
+    const int ph = int(k % cyc);
+    if (ph == 0) {
+      c1 = S->alpha1[(k - 1) & 3];
+      wm = 1;
+      if (cyc == 3) {
+        const double bprev = S->beta1[(k - 1) & 3];
+        const double a2 = S->alpha1[(k - 2) & 3];
+        if (fabs(bprev) >= S->pair_min_beta) { wm = 2; c2 = a2 / bprev; }
+        else { wm = 3; c2 = a2; }
+      }
+    }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       S->zr[(k - 1) & 1] = rho;  // slot of k-1 (read as rho_{k-2} by the next sweep)
-      S->alpha[k & 1] = alpha;
+      S->alpha1[k & 3] = alpha;
+      S->beta1[k & 3] = beta;
       if (k >= 2) S->diff = diff;
-      S->w_pend = (k & 1) ? k : 0;
+      S->w_pend = ph ? k : 0;
+      S->w_pend_n = ph;
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) S->halo_k = k + 1;  // the next exchange fills sweep k+1's inputs
@@ -384,14 +436,27 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
   // strictly inside the global domain (no Dirichlet node in reach)
   const bool fast = VEC == 2 && j1 == j0 + WO - 1 && G.gi0 + i0 - 2 >= 1 && G.gi0 + i1 + 2 <= G.M - 1 &&
                     G.gj0 + j0 - 2 >= 1 && G.gj0 + j0 + 64 * VEC - 3 <= G.N - 1;
-  const bool even = k > 0 && !(k & 1);
 #define PMX_MARCH(E, F) \
-  pcg1_march<T, VEC, PF, E, F>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, alpha_prev, acc)
-  if (fast) {
-    if (even) PMX_MARCH(true, true); else PMX_MARCH(false, true);
-  } else {
-    if (even) PMX_MARCH(true, false); else PMX_MARCH(false, false);
+  pcg1_march<T, VEC, PF, E, F>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, acc)
+  // fp32 storage keeps pairs (w_cycle 2, see init): the triple paths' registers would push the
+  // 4-waves/SIMD fp32 kernel (127 VGPRs) into spills
+#define PMX_MARCH_W(F)                                     \
+  if constexpr (sizeof(T) == 4) {                          \
+    if (wm == 0) PMX_MARCH(0, F); else PMX_MARCH(1, F);    \
+  } else {                                                 \
+    switch (wm) {                                          \
+      case 0: PMX_MARCH(0, F); break;                      \
+      case 1: PMX_MARCH(1, F); break;                      \
+      case 2: PMX_MARCH(2, F); break;                      \
+      default: PMX_MARCH(3, F); break;                     \
+    }                                                      \
   }
+  if (fast) {
+    PMX_MARCH_W(true)
+  } else {
+    PMX_MARCH_W(false)
+  }
+#undef PMX_MARCH_W
 #undef PMX_MARCH
   wave_sum2_mfma(acc[0], acc[1]);
   wave_sum2_mfma(acc[2], acc[3]);

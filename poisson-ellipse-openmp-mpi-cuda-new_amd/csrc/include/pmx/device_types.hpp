@@ -82,6 +82,13 @@ struct alignas(64) PcgState {
   // which may still run while the next sweep's interior tiles (and their halo_k write) run.
   long long halo_k;
   long long halo_k_unpack;
+  // Single-pass w schedule (pcg1): w is read and written on one sweep in w_cycle (2 = pairs, 3 =
+  // triples, see k_pcg1).  alpha1/beta1 hold alpha_k / beta_k at slot k & 3; w_pend_n steps
+  // (p^{w_pend - w_pend_n + 1} .. p^{w_pend}, both still in the two p buffers) are not yet in w.
+  double alpha1[4];
+  double beta1[4];
+  int w_cycle;
+  int w_pend_n;
 };
 
 // Pointers for the halo ("ghost") exchange, one per slot (see kHaloSlots).  Two-sweep iteration:

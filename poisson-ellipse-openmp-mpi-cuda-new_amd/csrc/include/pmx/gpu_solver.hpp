@@ -77,6 +77,10 @@ struct GpuOptions {
   // pcg1 prefetch depth: rows loaded ahead of the row being computed (1..4).  The sweep is
   // latency-bound at 2 waves/SIMD; deeper prefetch spends VGPRs that occupancy does not use.
   int pf1 = 0;  // 0 = auto
+  // pcg1 w schedule: w is read and written on one sweep in wcycle1 (3 = triples, 2 = pairs).
+  // Triples recover p^{k-2} from p^{k-1} and r^{k-1} (one extra stencil), or re-read it when
+  // |beta_{k-1}| < 1e-3 or pair_w == 2.  PMX_PCG1_WCYCLE=2|3 overrides.
+  int wcycle1 = 3;
   bool resolved = false;  // environment overrides already applied (resolve_options)
 };
 

@@ -114,3 +114,58 @@ def test_pcg1_split_sweep_matches_single_subdomain(pkg, monkeypatch, ranks, spli
     r = _solve(pkg, monkeypatch, 1, p, ranks=ranks, split=split, graph_batch=graph_batch)
     assert r.iters == ref.iters == 546
     assert np.abs(r.w - ref.w).max() < 1e-11
+
+
+# ---- w schedule: pairs (PMX_PCG1_WCYCLE=2) vs triples (default in fp64), triples re-reading
+# p^{k-2} (PMX_PAIR_W=2) instead of recovering it from p^{k-1}, r^{k-1} and one more stencil.
+
+@pytest.mark.parametrize("ranks", [1, 2, 4])
+@pytest.mark.parametrize("grid", [(400, 600), (211, 157)])
+def test_pcg1_w_cycles_agree(pkg, monkeypatch, ranks, grid):
+    from conftest import sub
+    p = pkg.PoissonEllipse(M=grid[0], N=grid[1])
+    monkeypatch.setenv("PMX_ALGO", "1")
+    out = {}
+    for name, env in (("pairs", {"PMX_PCG1_WCYCLE": "2"}), ("triples", {"PMX_PCG1_WCYCLE": "3"}),
+                      ("reread", {"PMX_PCG1_WCYCLE": "3", "PMX_PAIR_W": "2"})):
+        for k in ("PMX_PCG1_WCYCLE", "PMX_PAIR_W"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        out[name] = pkg.solve(p, "hip", ranks=ranks)
+    ref = pkg.solve(p, "cpu")
+    for name, r in out.items():
+        assert r.iters == ref.iters, (name, r.iters, ref.iters)
+        assert np.abs(r.w - ref.w).max() < 1e-10, name
+    assert np.abs(out["triples"].w - out["pairs"].w).max() < 1e-12
+    assert np.abs(out["reread"].w - out["pairs"].w).max() < 1e-12
+
+
+@pytest.mark.parametrize("steps", [6, 7, 8, 9])
+def test_pcg1_triple_w_midrun_materialised(pkg, monkeypatch, steps):
+    """w read mid-solve includes the 0, 1 or 2 deferred steps of the triple schedule."""
+    from conftest import sub
+    p = pkg.PoissonEllipse(M=300, N=200)
+    monkeypatch.setenv("PMX_ALGO", "1")
+    out = {}
+    for cyc in (2, 3):
+        monkeypatch.setenv("PMX_PCG1_WCYCLE", str(cyc))
+        s = sub("models").make_session(p, ranks=2, graph_batch=0)
+        s.init()
+        s.step(steps)
+        s.synchronize()
+        st = s.state()
+        assert st["w_cycle"] == cyc
+        assert st["w_pend_n"] == steps % cyc
+        out[cyc] = s.gather_local_w()
+    assert np.abs(out[3] - out[2]).max() < 1e-14
+
+
+def test_pcg1_fp32_keeps_pairs(pkg, monkeypatch):
+    from conftest import sub
+    monkeypatch.setenv("PMX_ALGO", "1")
+    s = sub("models").make_session(pkg.PoissonEllipse(M=200, N=300), dtype="fp32")
+    s.init()
+    s.step(4)
+    s.synchronize()
+    assert s.state()["w_cycle"] == 2
