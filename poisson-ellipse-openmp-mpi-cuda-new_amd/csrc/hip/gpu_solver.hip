@@ -319,7 +319,8 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
   st.norm = int(spec_.norm);
   st.pair_w = opt_.pair_w ? 1 : 0;
   st.pair_min_beta = opt_.pair_w == 2 ? HUGE_VAL : 1e-3;
-  st.w_cycle = elem_ == 8 ? opt_.wcycle1 : 2;  // fp32 k_pcg1 is built with pairs only
+  st.w_cycle = w_cycle();  // fp32 k_pcg1 is built with pairs only
+  host_k_ = st.it;
   HIP_CHECK(hipMemcpyAsync(state_, &st, sizeof(PcgState), hipMemcpyHostToDevice, s));
   T* w = static_cast<T*>(field_base(0));
   T* r = static_cast<T*>(field_base(1));
@@ -361,7 +362,7 @@ void GpuSubdomainSolver::phase_a_kernel_only(hipStream_t s, int part) {
   if (pcg1_)
     launch_pcg1<T>(geom_, tables_, static_cast<T*>(field_base(0)), static_cast<T*>(field_base(1)),
                    reinterpret_cast<T*>(r2_ + field_off_ * elem_), static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), partials_, state_,
-                   tiles1_, s, part);
+                   tiles1_, s, part, w_sweep_next());
   else if (tiles_.kind == 1)
     launch_pcg_a_wave<T>(geom_, tables_, static_cast<const T*>(field_base(1)),
                          static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(),
@@ -420,6 +421,7 @@ void GpuSubdomainSolver::enqueue_reduce_a(hipStream_t s) {
     const double wts[5] = {h, h, h, h, wdiff};
     launch_reduce_n(partials_, tiles1_.ntiles(), 5, wts, state_->red_c, state_, kSkipIfDone | kBumpIter,
                     reduce_ws_, s);
+    ++host_k_;  // mirrors the S->it bump (see host_k())
     after_launch(s);
     return;
   }
@@ -510,6 +512,9 @@ void GpuSubdomainSolver::load_checkpoint(std::istream& is, hipStream_t s) {
   is.read(buf.data(), std::streamsize(layout_.bytes));
   PMX_CHECK(is.good(), "truncated checkpoint (scalars/halos)");
   HIP_CHECK(hipMemcpy(arena_, buf.data(), layout_.bytes, hipMemcpyHostToDevice));
+  PcgState ck{};
+  std::memcpy(&ck, buf.data() + layout_.state_off, sizeof(PcgState));
+  host_k_ = ck.it;
   if (pcg1_) {
     is.read(buf.data(), std::streamsize(field_bytes_));
     PMX_CHECK(is.good(), "truncated checkpoint (pcg1 r2)");
@@ -540,7 +545,8 @@ double GpuSubdomainSolver::bench_kernel(int which, int abl, int reps, hipStream_
   st.zr[0] = st.zr[1] = 1e-3;
   st.alpha[0] = st.alpha[1] = 1.0;
   for (int q = 0; q < 4; ++q) st.alpha1[q] = st.beta1[q] = 1.0;
-  st.w_cycle = elem_ == 8 ? opt_.wcycle1 : 2;
+  st.w_cycle = w_cycle();
+  host_k_ = st.it;
   st.red_c[0] = 1e-3;
   st.red_c[1] = st.red_c[3] = st.red_c[4] = 1.0;
   st.pair_w = opt_.pair_w ? 1 : 0;
@@ -916,7 +922,14 @@ void PcgDriver::for_each_stream(F&& f) {
   }
 }
 
-void PcgDriver::build_graph() {
+void PcgDriver::advance_host_k(long long n) {
+  for (auto* s : local_) s->set_host_k(s->host_k() + n);
+}
+
+// Captures graph_batch_ iterations starting at w-cycle phase `phase` (the phase of the host
+// iteration counter now).  The capture enqueues nothing for execution, so the host counters are
+// restored afterwards; each launch of the graph advances them by graph_batch_.
+void PcgDriver::build_graph(int phase) {
   TraceRange tr("pmx:build_graph");
   graph_ok_ = false;
   bool single_stream = true;
@@ -930,8 +943,11 @@ void PcgDriver::build_graph() {
     (void)hipGetLastError();
     return;
   }
+  std::vector<long long> k0;
+  for (auto* s : local_) k0.push_back(s->host_k());
   for (int k = 0; k < graph_batch_; ++k) enqueue_one_iteration();
   join_halo();  // a captured batch is self-contained: every forked stream rejoins
+  for (size_t i = 0; i < local_.size(); ++i) local_[i]->set_host_k(k0[i]);
   if (hipStreamEndCapture(streams_[0], &g) != hipSuccess || !g) {
     (void)hipGetLastError();
     return;
@@ -944,16 +960,28 @@ void PcgDriver::build_graph() {
   }
   graphs_.push_back(g);
   execs_.push_back(e);
+  exec_by_phase_[size_t(phase)] = e;
   graph_ok_ = true;
 }
 
 void PcgDriver::enqueue_iterations(int64_t n) {
   TraceRange tr("pmx:enqueue_iterations");
-  if (graph_batch_ > 0 && execs_.empty()) build_graph();
+  const int cyc = local_[0]->w_cycle();
+  for (auto* s : local_) PMX_CHECK(s->host_k() == local_[0]->host_k(), "local solvers out of step");
+  if (exec_by_phase_.empty()) exec_by_phase_.assign(size_t(cyc), nullptr);
   int64_t done = 0;
-  if (graph_ok_) {
-    for (; done + graph_batch_ <= n; done += graph_batch_)
-      HIP_CHECK(hipGraphLaunch(execs_[0], streams_[0]));
+  while (graph_batch_ > 0 && !graph_failed_ && done + graph_batch_ <= n) {
+    const int ph = int(local_[0]->host_k() % cyc);
+    if (!exec_by_phase_[size_t(ph)]) {
+      build_graph(ph);
+      if (!graph_ok_) {
+        graph_failed_ = true;  // not capturable (multi-stream, comm, check mode): eager from now on
+        break;
+      }
+    }
+    HIP_CHECK(hipGraphLaunch(exec_by_phase_[size_t(ph)], streams_[0]));
+    advance_host_k(graph_batch_);
+    done += graph_batch_;
   }
   for (; done < n; ++done) enqueue_one_iteration();
   join_halo();

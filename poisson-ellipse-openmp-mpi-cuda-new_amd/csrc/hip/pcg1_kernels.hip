@@ -304,10 +304,13 @@ done:
 //  * fp32 storage (half the prefetch registers): PF=1 fits 4 waves/SIMD with no spills (127
 //    VGPRs) -- 32768^2 4.54 vs 5.03 ms at 3 waves/SIMD with PF=2 (NOTES #37); PF=2 would spill.
 // Other shapes: whatever the allocator picks.
-template <typename T, int VEC, int WAVES, int PF>
+//  * The sweeps that move w (WS, one in w_cycle) are a kernel of their own: without the w paths
+//    the fp64 plain sweep needs 119 VGPRs and runs at 4 waves/SIMD, the w sweep (151) at 3.
+template <typename T, int VEC, int WAVES, int PF, bool WS>
 constexpr int pcg1_min_waves() {
   if (VEC != 2 || WAVES != 1) return 1;
   if (sizeof(T) == 4 && PF == 1) return 4;
+  if (sizeof(T) == 8 && PF == 1 && !WS) return 4;
   return PF <= 2 ? 3 : 2;
 }
 
@@ -346,8 +349,8 @@ __device__ __forceinline__ bool pcg1_tile(int k, const Pcg1Part& P, int tiles_j,
   return false;
 }
 
-template <typename T, int VEC, int WAVES, int PF>
-__global__ void __launch_bounds__(64 * WAVES, (pcg1_min_waves<T, VEC, WAVES, PF>()))
+template <typename T, int VEC, int WAVES, int PF, bool WS>
+__global__ void __launch_bounds__(64 * WAVES, (pcg1_min_waves<T, VEC, WAVES, PF, WS>()))
 k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
        double* __restrict__ partials, PcgState* S, int TI, int tiles_j, int ntiles, Pcg1Part part) {
   constexpr int WO = 64 * VEC - 4;  // owned columns per tile
@@ -399,6 +402,17 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
     // |alpha| ||p||, so the schedule changes no iteration count, only w's rounding.
     const int cyc = S->w_cycle;
     const int ph = int(k % cyc);
+    // the host launches the w-sweep kernel (WS) exactly on the sweeps k = 0 mod w_cycle; a
+    // mismatch (host and device iteration counters out of step) must not pass silently
+    if ((ph == 0) != WS) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        S->iters = k;
+        S->status = int(Status::kBreakdown);
+        S->nan_flag = 1;
+        S->done = 1;
+      }
+      return;
+    }
     if (ph == 0) {
       c1 = S->alpha1[(k - 1) & 3];
       wm = 1;
@@ -441,11 +455,12 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
   // fp32 storage keeps pairs (w_cycle 2, see init): the triple paths' registers would push the
   // 4-waves/SIMD fp32 kernel (127 VGPRs) into spills
 #define PMX_MARCH_W(F)                                     \
-  if constexpr (sizeof(T) == 4) {                          \
-    if (wm == 0) PMX_MARCH(0, F); else PMX_MARCH(1, F);    \
+  if constexpr (!WS) {                                     \
+    PMX_MARCH(0, F);                                       \
+  } else if constexpr (sizeof(T) == 4) {                   \
+    PMX_MARCH(1, F);                                       \
   } else {                                                 \
     switch (wm) {                                          \
-      case 0: PMX_MARCH(0, F); break;                      \
       case 1: PMX_MARCH(1, F); break;                      \
       case 2: PMX_MARCH(2, F); break;                      \
       default: PMX_MARCH(3, F); break;                     \
@@ -616,7 +631,7 @@ TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf, 
 
 template <typename T>
 void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1,
-                 double* partials, PcgState* S, const TileCfg& tc, hipStream_t s, int part) {
+                 double* partials, PcgState* S, const TileCfg& tc, hipStream_t s, int part, bool wsweep) {
   PMX_CHECK(tc.kind == 3, "launch_pcg1 needs make_pcg1_tiles");
   PMX_CHECK(part >= 0 && part <= 2, "launch_pcg1: part must be 0, 1 or 2");
   const Pcg1Part P{part, tc.tiles_i, tc.ti_lo, tc.ti_hi, tc.tj_lo, tc.tj_hi};
@@ -625,8 +640,15 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
   PMX_CHECK(G.nb == 0 || (G.nx >= 2 && G.ny >= 2), "pcg1 on a decomposed grid needs subdomains >= 2 x 2");
   const int nb = (count + tc.waves - 1) / tc.waves;
   const int bs = 64 * tc.waves;
-#define PMX_PCG1(V, WV, PF) \
-  hipLaunchKernelGGL((k_pcg1<T, V, WV, PF>), dim3(nb), dim3(bs), 0, s, G, Tb, w, r, r2, p0, p1, partials, S, tc.rows, tc.tiles_j, tc.ntiles(), P)
+#define PMX_PCG1(V, WV, PF)                                                                              \
+  do {                                                                                                   \
+    if (wsweep)                                                                                          \
+      hipLaunchKernelGGL((k_pcg1<T, V, WV, PF, true>), dim3(nb), dim3(bs), 0, s, G, Tb, w, r, r2, p0, p1, \
+                         partials, S, tc.rows, tc.tiles_j, tc.ntiles(), P);                              \
+    else                                                                                                 \
+      hipLaunchKernelGGL((k_pcg1<T, V, WV, PF, false>), dim3(nb), dim3(bs), 0, s, G, Tb, w, r, r2, p0,   \
+                         p1, partials, S, tc.rows, tc.tiles_j, tc.ntiles(), P);                          \
+  } while (0)
   // instantiated shapes: the default (VEC 2, 1 wave, prefetch 1) and the ones the sweeps still
   // compare against (prefetch 2-4; 2 or 4 waves per workgroup; VEC 4)
   if (tc.vec == 2 && tc.waves == 1) {
@@ -667,12 +689,12 @@ void launch_reduce_n(const double* partials, int n, int nq, const double* weight
 }
 
 template void launch_pcg1<double>(const DevGeom&, const DevTables&, double*, double*, double*, double*,
-                                  double*, double*, PcgState*, const TileCfg&, hipStream_t, int);
+                                  double*, double*, PcgState*, const TileCfg&, hipStream_t, int, bool);
 template void launch_pcg1_halo<double>(const DevGeom&, double*, double*, double*, double*, HaloBufs<double>,
                                         PcgState*, bool, hipStream_t);
 template void launch_pcg1_halo<float>(const DevGeom&, float*, float*, float*, float*, HaloBufs<float>,
                                        PcgState*, bool, hipStream_t);
 template void launch_pcg1<float>(const DevGeom&, const DevTables&, float*, float*, float*, float*, float*,
-                                 double*, PcgState*, const TileCfg&, hipStream_t, int);
+                                 double*, PcgState*, const TileCfg&, hipStream_t, int, bool);
 
 }  // namespace pmx

@@ -177,6 +177,14 @@ class GpuSubdomainSolver {
   const DevTables& tables() const { return tables_; }
   const TileCfg& tiles() const { return pcg1_ ? tiles1_ : tiles_; }  // pcg_a (or pcg1)
   bool single_pass() const { return pcg1_; }
+  // pcg1: host mirror of the device iteration counter S->it -- the index of the next sweep this
+  // solver enqueues.  init sets it to 0, every enqueued reduction (which bumps S->it on the
+  // device) advances it, load_checkpoint reads it from the checkpoint.  It picks the plain or the
+  // w-moving k_pcg1 (see launch_pcg1); captured graphs depend on its phase modulo w_cycle().
+  long long host_k() const { return host_k_; }
+  void set_host_k(long long k) { host_k_ = k; }
+  int w_cycle() const { return pcg1_ ? (elem_ == 8 ? opt_.wcycle1 : 2) : 1; }
+  bool w_sweep_next() const { return pcg1_ && host_k_ > 0 && host_k_ % w_cycle() == 0; }
   const TileCfg& tiles_b() const { return tiles_b_; }  // pcg_b
   int device() const { return opt_.device; }
   size_t field_bytes() const { return field_bytes_; }
@@ -205,6 +213,7 @@ class GpuSubdomainSolver {
   TileCfg tiles_b_{};  // pcg_b
   TileCfg tiles1_{};   // pcg1
   bool pcg1_ = false;
+  long long host_k_ = 0;
   TileCfg init_tiles_{};
   CommLayout layout_{};
   size_t elem_ = 8, field_bytes_ = 0, field_off_ = 0;
@@ -294,7 +303,7 @@ class PcgDriver {
   void halo_exchange_pcg1(std::vector<hipStream_t>& streams);  // pack -> comm -> unpack
   void enqueue_split_iteration();  // pcg1, decomposed, overlap: interior/frame sweep split
   void join_halo();                // compute stream waits for a pending ghost exchange
-  void build_graph();
+  void build_graph(int phase);
   template <typename F> void for_each_stream(F&& f);
   void poison(std::vector<hipStream_t>& streams);
 
@@ -314,9 +323,14 @@ class PcgDriver {
   bool halo_pending_ = false;  // a ghost exchange on the comm stream not yet joined
   std::vector<hipStream_t> frame_streams_;
   std::vector<hipEvent_t> ev_ar_, ev_fdone_, ev_swept_, ev_pk_;
-  bool graph_ok_ = false;
+  bool graph_ok_ = false;      // the last build_graph succeeded
+  bool graph_failed_ = false;  // capture is not possible for this driver: eager launches
   std::vector<hipGraph_t> graphs_;
   std::vector<hipGraphExec_t> execs_;
+  // one captured batch per phase of the w cycle at its first sweep (pcg1 bakes the plain / w
+  // sweep kernel choice into the graph); nullptr = not built yet
+  std::vector<hipGraphExec_t> exec_by_phase_;
+  void advance_host_k(long long n);
 };
 
 }  // namespace pmx

@@ -86,9 +86,13 @@ void launch_pcg_b_wave(const DevGeom& G, const DevTables& Tb, T* w, T* r, const 
 // part: 0 = every tile; 1 = the interior tiles only (they read no ghost cell, so they may run
 // while the previous sweep's ghost exchange is still in flight); 2 = the frame tiles only.
 // Parts 1 and 2 of one sweep may run concurrently on two streams: they write disjoint partials.
+// wsweep: launch the kernel that moves w; it must be set exactly on the sweeps k >= 1 with
+// k % S->w_cycle == 0 (the caller mirrors the device iteration counter; a mismatch stops the solve
+// with status breakdown and the NaN flag).
 template <typename T>
 void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1,
-                 double* partials, PcgState* S, const TileCfg& tc, hipStream_t s, int part = 0);
+                 double* partials, PcgState* S, const TileCfg& tc, hipStream_t s, int part = 0,
+                 bool wsweep = false);
 
 // pcg1 ghost exchange: pack (unpack=false) the radius-2 edges of the buffers the next sweep reads
 // (selected on the device by S->halo_k) into H.send, or unpack H.recv into their ghost cells.

@@ -169,3 +169,25 @@ def test_pcg1_fp32_keeps_pairs(pkg, monkeypatch):
     s.step(4)
     s.synchronize()
     assert s.state()["w_cycle"] == 2
+
+
+@pytest.mark.parametrize("ranks", [1, 4])
+def test_pcg1_graph_phases_match_eager(pkg, monkeypatch, ranks):
+    """The plain / w-moving sweep kernels are chosen on the host and baked into the captured
+    graphs, one graph per w-cycle phase: batches entered at every phase (eager remainders in
+    between) give bitwise the eager result."""
+    from conftest import sub
+    monkeypatch.setenv("PMX_ALGO", "1")
+    p = pkg.PoissonEllipse(M=400, N=600)
+    out = {}
+    for gb in (0, 32):
+        s = sub("models").make_session(p, ranks=ranks, graph_batch=gb)
+        s.init()
+        for n in (5, 64, 7, 32, 33, 1, 32):
+            s.step(n)
+        s.synchronize()
+        st = s.state()
+        assert not st["nan"] and st["it"] == 1 + 174, st
+        out[gb] = (s.gather_local_w(), st["diff"])
+    assert np.array_equal(out[0][0], out[32][0])
+    assert out[0][1] == out[32][1]

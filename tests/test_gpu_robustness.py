@@ -79,9 +79,12 @@ def test_poisoned_halo_without_exchange_raises_nan_flag(pkg, native, algo):
     assert st["nan"]
 
 
-def test_resume_with_pending_w_step_is_bitwise(pkg, tmp_path):
-    """A checkpoint taken after an odd iteration holds a deferred w step (paired w updates); the
-    resumed solve must apply it exactly like the uninterrupted one."""
+@pytest.mark.parametrize("steps", [7, 8])
+def test_resume_with_pending_w_step_is_bitwise(pkg, tmp_path, steps):
+    """A checkpoint taken mid-cycle holds deferred w steps (pcg1 fp64 moves w on one sweep in
+    three: 1 or 2 steps pending); the resumed solve -- whose host iteration counter comes from the
+    checkpoint and picks the plain / w sweep kernels and graph phase -- must apply them exactly like
+    the uninterrupted one."""
     models = sub("models")
     p = pkg.PoissonEllipse(M=400, N=600)
     path = str(tmp_path / "ck.bin")
@@ -89,9 +92,9 @@ def test_resume_with_pending_w_step_is_bitwise(pkg, tmp_path):
     rr = ref.solve_checkpointed(str(tmp_path / "unused.bin"), every=0)
     a = models.make_session(p, graph_batch=0)
     a.init()
-    a.step(7)
+    a.step(steps)
     a.synchronize()
-    assert a.state()["w_pend"] == 7
+    assert a.state()["w_pend"] == steps and a.state()["w_pend_n"] == steps % 3
     a.save_checkpoint(path)
     b = models.make_session(p)
     rb = b.solve_checkpointed(path, every=0, resume=True)
