@@ -1,0 +1,5 @@
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+for g in "4096 8192" "8192 8192" "1600 2400" "16384 16384"; do
+  echo "=== $g"
+  ABN_GRID="$g" ROUNDS=3 ITERS=${ITERS:-1500} timeout -k 10 500 bash bench/gpu_abn.sh "PMX_PCG1_PF=1" "PMX_PCG1_PF=2" "PMX_PCG1_PF=3" "PMX_PCG1_PF=4" "PMX_PCG1_PF=2 PMX_PCG1_ROWS=16" "PMX_PCG1_PF=1 PMX_PCG1_ROWS=4" | grep -v "round" || exit 1
+done
