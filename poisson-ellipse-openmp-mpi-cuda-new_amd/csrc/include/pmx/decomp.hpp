@@ -4,8 +4,8 @@
 //            decompose_2d         stage2-mpi/poisson_mpi_decomp.cpp:75-111
 //            neighbour map        stage2-mpi/poisson_mpi_decomp.cpp:246-252
 // The default process grid is identical to the reference (P=2 -> 1x2, 4 -> 2x2,
-// 8 -> 2x4).  `Split::kAuto` instead picks the factorisation that minimises the
-// halo perimeter and prefers cutting the slow (row, contiguous-halo) axis.
+// 8 -> 2x4).  `Split::kAuto` instead cuts only the slow (row) axis while the strips stay
+// >= kMinStripRows tall, else minimises the halo perimeter.
 #pragma once
 
 #include <algorithm>
@@ -34,12 +34,21 @@ inline ProcGrid choose_process_grid(int size) {
   return g;
 }
 
+// Split::kAuto uses row strips while they are at least this many rows tall (see make_process_grid)
+constexpr int kMinStripRows = 128;
+
 inline ProcGrid make_process_grid(int size, int M, int N, Split split) {
   if (split == Split::kReference) return choose_process_grid(size);
   if (split == Split::kRows) return ProcGrid{size, 1};
   if (split == Split::kCols) return ProcGrid{1, size};
-  // kAuto: minimise the per-rank halo perimeter (nx + ny), ties -> more x cuts
-  // (x halos are contiguous rows in our row-major [i][j] layout).
+  // kAuto: row strips (py = 1, the longest contiguous rows) when every strip keeps at least
+  // kMinStripRows rows.  The sweep streams whole rows, so at equal points per rank long rows are
+  // faster: 2048x16384 strips 337.6 us/iter vs 4096x8192 blocks 356.9 and 8192x4096 378.9
+  // (profiles/r2/small_shapes/README.md); the ghost exchange (~32 B per column per side in fp64)
+  // runs under the interior sweep and stays well below it while strips are >= 128 rows tall.
+  // Otherwise: the least halo perimeter (nx + ny), ties -> more x cuts (x halos are contiguous
+  // rows in our row-major [i][j] layout).
+  if ((M - 1) / size >= kMinStripRows) return ProcGrid{size, 1};
   ProcGrid best{size, 1};
   double best_cost = 1e300;
   for (int px = 1; px <= size; ++px) {

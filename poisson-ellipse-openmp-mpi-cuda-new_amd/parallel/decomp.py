@@ -9,6 +9,9 @@ from __future__ import annotations
 import math
 
 
+MIN_STRIP_ROWS = 128  # decomp.hpp kMinStripRows
+
+
 def choose_process_grid(size: int) -> tuple[int, int]:
     if size < 1:
         raise ValueError("process count must be >= 1")
@@ -25,7 +28,9 @@ def process_grid(size: int, M: int, N: int, split: str = "reference") -> tuple[i
         return size, 1
     if split == "cols":
         return 1, size
-    if split == "auto":
+    if split == "auto":  # mirror of make_process_grid (decomp.hpp): row strips while >= 128 rows
+        if (M - 1) // size >= MIN_STRIP_ROWS:
+            return size, 1
         best, cost_best = (size, 1), float("inf")
         for px in range(1, size + 1):
             if size % px:

@@ -51,4 +51,6 @@ def test_cover_and_balance(native, M, N, P, split):
 def test_auto_split_prefers_rows(native):
     d = sub("parallel.decomp")
     assert d.process_grid(2, 16384, 16384, "auto") == (2, 1)
-    assert d.process_grid(8, 16384, 16384, "auto") in ((4, 2), (2, 4))
+    assert d.process_grid(8, 16384, 16384, "auto") == (8, 1)  # strips: 2048 rows each
+    assert d.process_grid(8, 800, 1200, "auto") in ((4, 2), (2, 4))  # 99-row strips: too thin
+    assert d.process_grid(4, 513, 100, "auto") == (4, 1)  # exactly 128 rows per strip
