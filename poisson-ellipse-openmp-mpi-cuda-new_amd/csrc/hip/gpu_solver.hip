@@ -8,7 +8,9 @@
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
+#include <cstdio>
 #include <cstring>
+#include <vector>
 #include <istream>
 #include <ostream>
 
@@ -91,6 +93,7 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_PCG1_ROWS", o.rows1);
   env_int("PMX_PCG1_WAVES", o.waves1);
   env_int("PMX_PCG1_PF", o.pf1);
+  env_int("PMX_PCG1_ORDER", o.order1);
   env_int("PMX_PCG1_WCYCLE", o.wcycle1);
   PMX_CHECK(o.wcycle1 == 2 || o.wcycle1 == 3, "pcg1 w cycle must be 2 or 3");
   PMX_CHECK(o.pair_w >= 0 && o.pair_w <= 2, "pair_w must be 0, 1 or 2");
@@ -221,7 +224,17 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
 
   if (pcg1_) {
     tiles1_ = make_pcg1_tiles(G, opt_.vec1, opt_.waves1, opt_.rows1, opt_.pf1, int(elem_));
+#ifdef PMX_WAVE_TRACE
+    if (const char* e = std::getenv("PMX_WAVE_TRACE_IT"); e && e[0]) {
+      wtrace_n_ = tiles1_.ntiles();
+      wtrace_ = pcg1_wave_trace_setup(std::atoll(e), wtrace_n_);
+    }
+#endif
     HIP_CHECK(hipMalloc(&r2_, field_bytes_));
+    if (opt_.order1) {  // ellipse-cut tiles first (their 3-5x longer tiles would trail the sweep)
+      HIP_CHECK(hipMalloc(&tile_order_, 2 * size_t(tiles1_.ntiles()) * sizeof(int)));
+      slow_tiles_ = pcg1_build_order(G, tables_, tiles1_, tile_order_, nullptr);
+    }
   }
 
   init_tiles_ = make_tiles(G, 256, 0);
@@ -251,6 +264,7 @@ void GpuSubdomainSolver::release() noexcept {
   (void)hipDeviceSynchronize();
   if (fields_) (void)hipFree(fields_);
   if (r2_) (void)hipFree(r2_);
+  if (tile_order_) (void)hipFree(tile_order_);
   if (tables_buf_) (void)hipFree(tables_buf_);
   if (partials_) (void)hipFree(partials_);
   if (own_arena_ && arena_) (void)hipFree(arena_);
@@ -258,10 +272,30 @@ void GpuSubdomainSolver::release() noexcept {
   fields_ = r2_ = nullptr;
   arena_ = nullptr;
   tables_buf_ = partials_ = nullptr;
+  tile_order_ = nullptr;
   host_state_ = nullptr;
 }
 
-GpuSubdomainSolver::~GpuSubdomainSolver() { release(); }
+GpuSubdomainSolver::~GpuSubdomainSolver() {
+#ifdef PMX_WAVE_TRACE
+  if (wtrace_) {  // one line per wave: start end xcc hw_id tile part (wall clock: 100 MHz ticks)
+    std::vector<unsigned long long> h(size_t(wtrace_n_) * 4);
+    if (hipMemcpy(h.data(), wtrace_, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
+      const char* fn = std::getenv("PMX_WAVE_TRACE_OUT");
+      if (FILE* f = std::fopen(fn && fn[0] ? fn : "wave_trace.txt", "w")) {
+        for (int b = 0; b < wtrace_n_; ++b) {
+          const unsigned long long* o = &h[size_t(b) * 4];
+          if (o[1]) std::fprintf(f, "%llu %llu %llu %llu %llu %llu\n", o[0], o[1], o[2] >> 32, o[2] & 0xffffffffull,
+                                 o[3] & 0xffffffffffull, o[3] >> 40);
+        }
+        std::fclose(f);
+      }
+    }
+    (void)hipFree(wtrace_);
+  }
+#endif
+  release();
+}
 
 size_t GpuSubdomainSolver::estimate_device_bytes(const ProblemSpec& spec, const Subdomain& sd,
                                                  DType dtype, bool single_pass) {

@@ -36,6 +36,7 @@
 // exchanged: they only feed columns/rows that are not owned, which are neither stored nor summed.
 #include <algorithm>
 #include <cmath>
+#include <vector>
 
 #include "pcg_device.hpp"
 #include "pmx/common.hpp"
@@ -50,6 +51,13 @@ namespace {
 
 constexpr int kNq = 5;  // rho, (Az,z), (Az,p), (Ap,p), |p|^2
 constexpr int kPcg1AutoPf = 1;
+
+#ifdef PMX_WAVE_TRACE
+// Diagnostic build only (bench/wave_trace.sh): per-wave start/end wall clock, XCC and HW ids and
+// tile of ONE chosen sweep, to see how the wave population ramps up and drains.
+__device__ unsigned long long* g_wtrace = nullptr;
+__device__ long long g_wtrace_it = -1;
+#endif
 
 // VEC columns from c0 (c0 - 1 even, so every 2-column chunk is 2-element aligned); chunks are
 // clamped to start <= cmax (cmax - 1 even, cmax + 1 inside the padded row).
@@ -318,11 +326,13 @@ constexpr int pcg1_min_waves() {
 struct Pcg1Part {
   int part;  // 0 all, 1 interior rectangle, 2 frame
   int tiles_i, ti_lo, ti_hi, tj_lo, tj_hi;
+  const int* order;  // position -> tile id (pcg1_build_order), or nullptr: pcg1_tile's order
+  int count;         // tiles of this launch
 };
 
 // k-th tile of the part -> (ti, tj); false past the end.  The frame is enumerated as: tile rows
 // above the interior rectangle, tile rows below it, then the left and right columns beside it.
-__device__ __forceinline__ bool pcg1_tile(int k, const Pcg1Part& P, int tiles_j, int& ti, int& tj) {
+__host__ __device__ inline bool pcg1_tile(int k, const Pcg1Part& P, int tiles_j, int& ti, int& tj) {
   if (P.part == 0) {
     ti = k / tiles_j;
     tj = k - ti * tiles_j;
@@ -354,6 +364,9 @@ __global__ void __launch_bounds__(64 * WAVES, (pcg1_min_waves<T, VEC, WAVES, PF,
 k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
        double* __restrict__ partials, PcgState* S, int TI, int tiles_j, int ntiles, Pcg1Part part) {
   constexpr int WO = 64 * VEC - 4;  // owned columns per tile
+#ifdef PMX_WAVE_TRACE
+  const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (S->done) return;
   const long long k = S->it;  // 0 = the init sweep (alpha = beta = 0: sums of r^0, z^0 only)
   double alpha = 0.0, beta = 0.0, c1 = 0.0, c2 = 0.0;
@@ -434,9 +447,15 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) S->halo_k = k + 1;  // the next exchange fills sweep k+1's inputs
   int ti = 0, tj = 0;
-  if (!pcg1_tile(xcd_remap(blockIdx.x, gridDim.x) * WAVES + __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)),
-                 part, tiles_j, ti, tj))
+  const int pos = xcd_remap(blockIdx.x, gridDim.x) * WAVES + __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  if (part.order) {  // slow (ellipse-cut) tiles first, so they do not trail the sweep
+    if (pos >= part.count) return;
+    const int t = ld_uniform(part.order, pos);
+    ti = t / tiles_j;
+    tj = t - ti * tiles_j;
+  } else if (!pcg1_tile(pos, part, tiles_j, ti, tj)) {
     return;
+  }
   const int id = ti * tiles_j + tj;  // the tile's partials slot, whichever launch covers it
   (void)ntiles;
   const int i0 = 1 + ti * TI, i1 = min(i0 + TI - 1, G.nx);
@@ -480,6 +499,18 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
 #pragma unroll
     for (int q = 0; q < kNq; ++q) partials[int64_t(kNq) * id + q] = acc[q];
   }
+#ifdef PMX_WAVE_TRACE
+  if (g_wtrace && k == g_wtrace_it && (threadIdx.x & 63) == 0) {
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+    unsigned long long* o = g_wtrace + 4 * int64_t(blockIdx.x);
+    o[0] = wt0;
+    o[1] = t1;
+    o[2] = (static_cast<unsigned long long>(xcc) << 32) | hw;
+    o[3] = static_cast<unsigned long long>(id) | (static_cast<unsigned long long>(part.part) << 40);
+  }
+#endif
 }
 
 // Radius-2 ghost exchange of the single-pass iteration (see the header): pack (unpack = 0) copies
@@ -584,7 +615,77 @@ k_reduce_n(const double* __restrict__ part, int n, ReduceWeights wt, double* out
   }
 }
 
+// 1 = the tile marches a row whose coefficient class over the tile's loaded columns is "cut"
+// (row_class 0): those rows rebuild every face from the tables, and such a tile takes 3-5x the
+// median tile time (profiles/r2/small_shapes/README.md, wave traces).  One thread per tile, the
+// same rows and column window as pcg1_march.
+__global__ void k_pcg1_tile_cut(DevGeom G, DevTables Tb, int TI, int tiles_i, int tiles_j, int vec,
+                                unsigned char* cut) {
+  const int id = int(blockIdx.x * blockDim.x + threadIdx.x);
+  if (id >= tiles_i * tiles_j) return;
+  const int ti = id / tiles_j, tj = id - ti * tiles_j;
+  const int i0 = 1 + ti * TI, i1 = min(i0 + TI - 1, G.nx);
+  const int j0 = 1 + tj * (64 * vec - 4);
+  const int gjlo = max(G.gj0 + j0 - 2, 0), gjhi = min(G.gj0 + j0 - 2 + 64 * vec - 1, G.N);
+  unsigned char c = 0;
+  for (int m = i0 - 3; m <= i1 + 2 && !c; ++m) {
+    const int gi = min(max(G.gi0 + m, 0), G.M);
+    RowConst rc;
+    for (int q = 0; q < 4; ++q) {
+      rc.ca0[q] = Tb.acls[4 * gi + q];
+      rc.ca1[q] = Tb.acls[4 * (gi + 1) + q];
+      rc.cb[q] = Tb.bcls[4 * gi + q];
+    }
+    c = row_class(rc, gjlo, gjhi) == 0;
+  }
+  cut[id] = c;
+}
+
 }  // namespace
+
+int pcg1_build_order(const DevGeom& G, const DevTables& Tb, TileCfg& tc, int* d_order, hipStream_t s) {
+  tc.order0 = tc.order1 = nullptr;
+  const int n = tc.ntiles();
+  if (tc.waves != 1 || n == 0) return 0;
+  unsigned char* d_cut = nullptr;
+  HIP_CHECK(hipMalloc(&d_cut, size_t(n)));
+  hipLaunchKernelGGL(k_pcg1_tile_cut, dim3((n + 255) / 256), dim3(256), 0, s, G, Tb, tc.rows, tc.tiles_i,
+                     tc.tiles_j, tc.vec, d_cut);
+  HIP_CHECK(hipGetLastError());
+  std::vector<unsigned char> cut(static_cast<size_t>(n));
+  HIP_CHECK(hipMemcpyAsync(cut.data(), d_cut, size_t(n), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  HIP_CHECK(hipFree(d_cut));
+  std::vector<int> order(2 * size_t(n), 0);
+  int nslow = 0;
+  for (int part = 0; part <= 1; ++part) {
+    const Pcg1Part P{part, tc.tiles_i, tc.ti_lo, tc.ti_hi, tc.tj_lo, tc.tj_hi, nullptr, 0};
+    const int count = part == 0 ? n : tc.interior_tiles();
+    int* o = order.data() + size_t(part) * n;
+    // positions of XCD x (xcd_remap with one wave per workgroup): [x (q+1), ...) as in xcd_remap
+    const int q = count / 8, r = count % 8;
+    for (int x = 0, start = 0; x < 8; ++x) {
+      const int len = q + (x < r ? 1 : 0);
+      int w = start;
+      for (int pass = 0; pass < 2; ++pass)  // slow tiles first, then the rest, each in natural order
+        for (int k = start; k < start + len; ++k) {
+          int ti = 0, tj = 0;
+          PMX_CHECK(pcg1_tile(k, P, tc.tiles_j, ti, tj), "pcg1_build_order: tile enumeration");
+          const int id = ti * tc.tiles_j + tj;
+          if ((cut[size_t(id)] != 0) == (pass == 0)) {
+            o[w++] = id;
+            if (pass == 0 && part == 0) ++nslow;
+          }
+        }
+      start += len;
+    }
+  }
+  HIP_CHECK(hipMemcpyAsync(d_order, order.data(), order.size() * sizeof(int), hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  tc.order0 = d_order;
+  tc.order1 = d_order + n;
+  return nslow;
+}
 
 TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf, int elem) {
   PMX_CHECK(vec == 2 || vec == 4, "pcg1: vec must be 2 or 4");
@@ -634,8 +735,9 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
                  double* partials, PcgState* S, const TileCfg& tc, hipStream_t s, int part, bool wsweep) {
   PMX_CHECK(tc.kind == 3, "launch_pcg1 needs make_pcg1_tiles");
   PMX_CHECK(part >= 0 && part <= 2, "launch_pcg1: part must be 0, 1 or 2");
-  const Pcg1Part P{part, tc.tiles_i, tc.ti_lo, tc.ti_hi, tc.tj_lo, tc.tj_hi};
   const int count = part == 0 ? tc.ntiles() : part == 1 ? tc.interior_tiles() : tc.ntiles() - tc.interior_tiles();
+  const Pcg1Part P{part, tc.tiles_i, tc.ti_lo, tc.ti_hi, tc.tj_lo, tc.tj_hi,
+                   tc.waves == 1 ? (part == 0 ? tc.order0 : part == 1 ? tc.order1 : nullptr) : nullptr, count};
   if (count == 0) return;
   PMX_CHECK(G.nb == 0 || (G.nx >= 2 && G.ny >= 2), "pcg1 on a decomposed grid needs subdomains >= 2 x 2");
   const int nb = (count + tc.waves - 1) / tc.waves;
@@ -687,6 +789,17 @@ void launch_reduce_n(const double* partials, int n, int nq, const double* weight
   hipLaunchKernelGGL(k_reduce_n<kNq>, dim3(nb), dim3(256), 0, s, partials, n, wt, out, S, mode, chunk, ticket);
   HIP_CHECK(hipGetLastError());
 }
+
+#ifdef PMX_WAVE_TRACE
+void* pcg1_wave_trace_setup(long long it, int nwaves) {
+  void* buf = nullptr;
+  HIP_CHECK(hipMalloc(&buf, size_t(nwaves) * 32));
+  HIP_CHECK(hipMemset(buf, 0, size_t(nwaves) * 32));
+  HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_wtrace), &buf, sizeof(buf)));
+  HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_wtrace_it), &it, sizeof(it)));
+  return buf;
+}
+#endif
 
 template void launch_pcg1<double>(const DevGeom&, const DevTables&, double*, double*, double*, double*,
                                   double*, double*, PcgState*, const TileCfg&, hipStream_t, int, bool);

@@ -77,6 +77,8 @@ struct GpuOptions {
   // pcg1 prefetch depth: rows loaded ahead of the row being computed (1..4).  The sweep is
   // latency-bound at 2 waves/SIMD; deeper prefetch spends VGPRs that occupancy does not use.
   int pf1 = 0;  // 0 = auto
+  // pcg1 dispatch order: 1 = tiles cut by the ellipse first within each XCD's share, 0 = natural
+  int order1 = 1;
   // pcg1 w schedule: w is read and written on one sweep in wcycle1 (3 = triples, 2 = pairs).
   // Triples recover p^{k-2} from p^{k-1} and r^{k-1} (one extra stencil), or re-read it when
   // |beta_{k-1}| < 1e-3 or pair_w == 2.  PMX_PCG1_WCYCLE=2|3 overrides.
@@ -226,6 +228,12 @@ class GpuSubdomainSolver {
   char* arena_ = nullptr;
   bool own_arena_ = true;
   PcgState* state_ = nullptr;
+  int* tile_order_ = nullptr;  // pcg1 dispatch order (pcg1_build_order)
+  int slow_tiles_ = 0;
+#ifdef PMX_WAVE_TRACE
+  void* wtrace_ = nullptr;
+  int wtrace_n_ = 0;
+#endif
   PcgState* host_state_ = nullptr;  // pinned
 };
 

@@ -32,6 +32,11 @@ struct TileCfg {
   // kind 3 on decomposed grids: the tiles [ti_lo, ti_hi) x [tj_lo, tj_hi) read no ghost cell of a
   // side that has a neighbour ("interior"); the rest form the frame (see launch_pcg1's part)
   int ti_lo = 0, ti_hi = 0, tj_lo = 0, tj_hi = 0;
+  // kind 3: dispatch order of the whole-grid (order0) and interior (order1) launches: position
+  // -> tile id, the tiles the ellipse cuts first within each XCD's share (pcg1_build_order);
+  // nullptr = natural order
+  const int* order0 = nullptr;
+  const int* order1 = nullptr;
   int interior_tiles() const { return (ti_hi - ti_lo) * (tj_hi - tj_lo); }
   int ntiles() const { return tiles_i * tiles_j; }
 };
@@ -89,6 +94,10 @@ void launch_pcg_b_wave(const DevGeom& G, const DevTables& Tb, T* w, T* r, const 
 // wsweep: launch the kernel that moves w; it must be set exactly on the sweeps k >= 1 with
 // k % S->w_cycle == 0 (the caller mirrors the device iteration counter; a mismatch stops the solve
 // with status breakdown and the NaN flag).
+// Builds tc.order0/order1 in d_order (2 * tc.ntiles() ints): within each XCD's share of the
+// positions, the tiles with cut (slow-path) rows are dispatched first.  Returns their count.
+int pcg1_build_order(const DevGeom& G, const DevTables& Tb, TileCfg& tc, int* d_order, hipStream_t s);
+
 template <typename T>
 void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1,
                  double* partials, PcgState* S, const TileCfg& tc, hipStream_t s, int part = 0,
@@ -96,6 +105,10 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
 
 // pcg1 ghost exchange: pack (unpack=false) the radius-2 edges of the buffers the next sweep reads
 // (selected on the device by S->halo_k) into H.send, or unpack H.recv into their ghost cells.
+#ifdef PMX_WAVE_TRACE
+void* pcg1_wave_trace_setup(long long it, int nwaves);
+#endif
+
 template <typename T>
 void launch_pcg1_halo(const DevGeom& G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, PcgState* S,
                       bool unpack, hipStream_t s);
