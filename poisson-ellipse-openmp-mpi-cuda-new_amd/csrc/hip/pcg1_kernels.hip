@@ -101,13 +101,22 @@ __device__ __forceinline__ RowCo row_co(const DevTables& Tb, int gi, int gjlo, i
   return RowCo{gi, row_class(load_row(Tb, gi), gjlo, gjhi)};
 }
 
-__device__ __forceinline__ void coef(const RowCo& c, const DevTables& Tb, const DevGeom& G, int gj,
-                                     double& a0, double& a1, double& b0, double& b1) {
+// Column constants of a tile's lanes parked in LDS (lane-private slots [4 u + q][lane]) the first
+// time the tile meets a row the ellipse cuts: the cut-row path then reads them with ds_reads
+// instead of 4 vector loads per column and stage, whose waits (vmcnt is in-order) would also
+// drain the row prefetch three times per row.
+__device__ __forceinline__ ColConst col_lds(const double* scol, int u, int lane, int gj) {
+  return ColConst{scol[(4 * u) * 64 + lane], scol[(4 * u + 1) * 64 + lane], scol[(4 * u + 2) * 64 + lane],
+                  scol[(4 * u + 3) * 64 + lane], gj};
+}
+
+__device__ __forceinline__ void coef(const RowCo& c, const DevTables& Tb, const DevGeom& G, const double* scol,
+                                     int u, int lane, int gj, double& a0, double& a1, double& b0, double& b1) {
   if (c.ucls != 0) {
     a0 = a1 = b0 = b1 = c.ucls == 1 ? 1.0 : G.inv_eps;
   } else {
     const RowConst rc = load_row(Tb, c.gi);
-    const ColConst cc = load_col(Tb, gj);
+    const ColConst cc = col_lds(scol, u, lane, gj);
     a0 = face_a0c(cc, rc, G);
     a1 = face_a1c(cc, rc, G);
     b0 = face_b0c(cc, rc, G);
@@ -136,7 +145,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
                                            const T* __restrict__ pold,
                                            T* pnew, int i0, int i1, int j0, int j1,
                                            double alpha, double beta, double c1, double c2,
-                                           double (&acc)[kNq]) {
+                                           double (&acc)[kNq], double* __restrict__ scol) {
   constexpr bool WUP = WM != 0;
   const int64_t P = G.pitch;
   const int lane = threadIdx.x & 63;
@@ -180,6 +189,19 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   for (int u = 0; u < VEC; ++u) Pm2[u] = Pm1[u] = Zm3[u] = Zm2[u] = ro1[u] = po1[u] = po2[u] = 0.0;
   RowCo cB = row_co(Tb, grow(i0 - 3), gjlo, gjhi);  // rows m-1, m-2
   RowCo cC = cB;
+  bool parked = false;  // column constants in LDS (see col_lds)
+  auto park_cols = [&]() {
+#pragma unroll
+    for (int u = 0; u < VEC; ++u) {
+      const ColConst cc = load_col(Tb, gj[u]);
+      scol[(4 * u) * 64 + lane] = cc.ylo;
+      scol[(4 * u + 1) * 64 + lane] = cc.yhi;
+      scol[(4 * u + 2) * 64 + lane] = cc.rh0;
+      scol[(4 * u + 3) * 64 + lane] = cc.rh1;
+    }
+    parked = true;
+  };
+  if (cB.ucls == 0) park_cols();
 
   const int mfirst = i0 - 2, mlast = i1 + 2;
   auto step = [&](int m, const Pcg1Row<T, VEC>& cur, Pcg1Row<T, VEC>& nxt) {
@@ -189,6 +211,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     // ---- stage A: p^k of row m
     const bool rowA = FAST || interior_row(m);
     const RowCo cA = row_co(Tb, grow(m), gjlo, gjhi);
+    if (cA.ucls == 0 && !parked) park_cols();
     double Pm[VEC], rom[VEC], pom[VEC];
 #pragma unroll
     for (int u = 0; u < VEC; ++u) {
@@ -196,7 +219,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
       rom[u] = in ? double(cur.r[u]) : 0.0;
       pom[u] = in ? double(cur.p[u]) : 0.0;
       double a0, a1, b0, b1;
-      coef(cA, Tb, G, gj[u], a0, a1, b0, b1);
+      coef(cA, Tb, G, scol, u, lane, gj[u], a0, a1, b0, b1);
       const double z = zdiv_u<false>(cA.ucls, rom[u], a0, a1, b0, b1, G);
       const double v = __builtin_fma(beta, pom[u], z);
       Pm[u] = in ? double(static_cast<T>(v)) : 0.0;  // the stored (rounded) p^k is the one used
@@ -219,7 +242,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
 #pragma unroll
       for (int u = 0; u < VEC; ++u) {
         double a0, a1, b0, b1;
-        coef(cB, Tb, G, gj[u], a0, a1, b0, b1);
+        coef(cB, Tb, G, scol, u, lane, gj[u], a0, a1, b0, b1);
         const double xjm = u == 0 ? left : Pm1[u - 1];
         const double xjp = u == VEC - 1 ? right : Pm1[u + 1];
         const double Ap = apply_a<false>(Pm1[u], Pm2[u], Pm[u], xjm, xjp, a0, a1, b0, b1, G);
@@ -264,7 +287,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
 #pragma unroll
       for (int u = 0; u < VEC; ++u) {
         double a0, a1, b0, b1;
-        coef(cC, Tb, G, gj[u], a0, a1, b0, b1);
+        coef(cC, Tb, G, scol, u, lane, gj[u], a0, a1, b0, b1);
         const double xjm = u == 0 ? left : Zm2[u - 1];
         const double xjp = u == VEC - 1 ? right : Zm2[u + 1];
         const double Az = apply_a<false>(Zm2[u], Zm3[u], Zm1[u], xjm, xjp, a0, a1, b0, b1, G);
@@ -465,12 +488,14 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
   const T* rold = (k & 1) ? r2 : r;
   T* rnew = (k & 1) ? r : r2;
   double acc[kNq] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  __shared__ double s_col[WAVES * 4 * VEC * 64];  // 4 KB per wave (VEC 2)
+  double* scol = s_col + __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)) * (4 * VEC * 64);
   // interior tile: full width, and the marched rows i0-2..i1+2 / columns j0-2..j0+64*VEC-3 lie
   // strictly inside the global domain (no Dirichlet node in reach)
   const bool fast = VEC == 2 && j1 == j0 + WO - 1 && G.gi0 + i0 - 2 >= 1 && G.gi0 + i1 + 2 <= G.M - 1 &&
                     G.gj0 + j0 - 2 >= 1 && G.gj0 + j0 + 64 * VEC - 3 <= G.N - 1;
 #define PMX_MARCH(E, F) \
-  pcg1_march<T, VEC, PF, E, F>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, acc)
+  pcg1_march<T, VEC, PF, E, F>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, acc, scol)
   // fp32 storage keeps pairs (w_cycle 2, see init): the triple paths' registers would push the
   // 4-waves/SIMD fp32 kernel (127 VGPRs) into spills
 #define PMX_MARCH_W(F)                                     \
