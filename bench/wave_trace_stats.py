@@ -2,7 +2,7 @@
 population ramps up, holds and drains during one sweep, per XCC.
 
 usage: python bench/wave_trace_stats.py trace.txt [--slots N]
-Lines: start end xcc hw_id tile part (100-MHz wall-clock ticks, 10 ns).
+Lines: start end xcc hw_id tile part [prologue_end] (100-MHz wall-clock ticks, 10 ns).
 """
 from __future__ import annotations
 
@@ -24,6 +24,10 @@ def main():
     print(f"{path}: {n} waves, sweep span {span:.1f} us (first start -> last end)")
     print(f"wave duration: median {np.median(dur):.1f} us, p10 {np.percentile(dur, 10):.1f}, "
           f"p90 {np.percentile(dur, 90):.1f}, max {dur.max():.1f}")
+    if a.shape[1] > 6:  # prologue: kernel entry -> tile decoded, before the first row loads
+        pro = (a[:, 6] - st) / 100.0
+        print(f"prologue: median {np.median(pro):.2f} us, p90 {np.percentile(pro, 90):.2f} "
+              f"({np.median(pro) / np.median(dur):.1%} of the median wave)")
     # resident waves over time (1-us bins)
     nb = int(np.ceil(span)) + 1
     occ = np.zeros(nb + 1)

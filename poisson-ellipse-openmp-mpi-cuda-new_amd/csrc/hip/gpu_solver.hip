@@ -278,15 +278,15 @@ void GpuSubdomainSolver::release() noexcept {
 
 GpuSubdomainSolver::~GpuSubdomainSolver() {
 #ifdef PMX_WAVE_TRACE
-  if (wtrace_) {  // one line per wave: start end xcc hw_id tile part (wall clock: 100 MHz ticks)
-    std::vector<unsigned long long> h(size_t(wtrace_n_) * 4);
+  if (wtrace_) {  // one line per wave: start end xcc hw_id tile part prologue_end (100 MHz ticks)
+    std::vector<unsigned long long> h(size_t(wtrace_n_) * 5);
     if (hipMemcpy(h.data(), wtrace_, h.size() * 8, hipMemcpyDeviceToHost) == hipSuccess) {
       const char* fn = std::getenv("PMX_WAVE_TRACE_OUT");
       if (FILE* f = std::fopen(fn && fn[0] ? fn : "wave_trace.txt", "w")) {
         for (int b = 0; b < wtrace_n_; ++b) {
-          const unsigned long long* o = &h[size_t(b) * 4];
-          if (o[1]) std::fprintf(f, "%llu %llu %llu %llu %llu %llu\n", o[0], o[1], o[2] >> 32, o[2] & 0xffffffffull,
-                                 o[3] & 0xffffffffffull, o[3] >> 40);
+          const unsigned long long* o = &h[size_t(b) * 5];
+          if (o[1]) std::fprintf(f, "%llu %llu %llu %llu %llu %llu %llu\n", o[0], o[1], o[2] >> 32, o[2] & 0xffffffffull,
+                                 o[3] & 0xffffffffffull, o[3] >> 40, o[4]);
         }
         std::fclose(f);
       }

@@ -390,32 +390,66 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
 #ifdef PMX_WAVE_TRACE
   const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  if (S->done) return;
-  const long long k = S->it;  // 0 = the init sweep (alpha = beta = 0: sums of r^0, z^0 only)
+  // Prologue: ONE batch of independent scalar loads (state through the constant address space,
+  // the tile's dispatch slot), then scalar math.  Read field by field with waits in between, the
+  // state cost ~8 dependent memory round trips, ~7 us of a ~25-us wave (wave traces,
+  // profiles/r2/prologue/).  Every field read here is one this kernel does not write (the rings
+  // alpha1/beta1/zr are written at slot k, read at k-1 / k-2), so the constant view is exact.
+  typedef const __attribute__((address_space(4))) PcgState CState;
+  const CState* Sc = (const CState*)S;  // NOLINT: address-space cast
+  asm volatile("" ::"s"(S), "s"(part.order), "s"(part.count), "s"(gridDim.x));  // kernel arguments: one batch
+  const int pos = xcd_remap(blockIdx.x, gridDim.x) * WAVES + __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  // branch-free: without an order the load reads a valid dummy (the state's first word)
+  const int* obase = part.order ? part.order : reinterpret_cast<const int*>(S);
+  const int ord = ld_uniform(obase, part.order ? min(pos, part.count - 1) : 0);
+  const int st_done = Sc->done;
+  const long long k = Sc->it;  // 0 = the init sweep (alpha = beta = 0: sums of r^0, z^0 only)
+  double rc[kNq], al[4], be[4];
+#pragma unroll
+  for (int q = 0; q < kNq; ++q) rc[q] = Sc->red_c[q];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    al[q] = Sc->alpha1[q];
+    be[q] = Sc->beta1[q];
+  }
+  const double zr0 = Sc->zr[0], zr1 = Sc->zr[1];
+  const double s_delta = Sc->delta, s_bd_tol = Sc->bd_tol, s_pmb = Sc->pair_min_beta;
+  const long long s_max_iter = Sc->max_iter;
+  const int s_norm = Sc->norm, cyc = Sc->w_cycle;
+  auto ring4 = [](const double (&v)[4], long long i) {
+    const int j = int(i & 3);
+    return j == 0 ? v[0] : j == 1 ? v[1] : j == 2 ? v[2] : v[3];
+  };
+  // every value above is consumed here, so the compiler issues all those loads as one batch
+  // instead of sinking each below the branch that first needs it
+  asm volatile("" ::"s"(st_done), "s"(k), "s"(ord), "s"(rc[0]), "s"(rc[1]), "s"(rc[2]), "s"(rc[3]), "s"(rc[4]),
+               "s"(al[0]), "s"(al[1]), "s"(al[2]), "s"(al[3]), "s"(be[0]), "s"(be[1]), "s"(be[2]), "s"(be[3]),
+               "s"(zr0), "s"(zr1), "s"(s_delta), "s"(s_bd_tol), "s"(s_pmb), "s"(s_max_iter), "s"(s_norm), "s"(cyc));
+  if (st_done) return;
   double alpha = 0.0, beta = 0.0, c1 = 0.0, c2 = 0.0;
   int wm = 0;
   if (k > 0) {
-    const double rho = S->red_c[0];  // rho_{k-1} = (z^{k-1}, r^{k-1})
+    const double rho = rc[0];  // rho_{k-1} = (z^{k-1}, r^{k-1})
     double diff = 0.0;
     if (k >= 2) {
       // stop test of iteration k-1: ||w^k - w^{k-1}|| = |alpha_{k-1}| ||p^{k-1}||
-      diff = fabs(S->alpha1[(k - 1) & 3]) * sqrt(S->red_c[4]);
+      diff = fabs(ring4(al, k - 1)) * sqrt(rc[4]);
       const bool bad = !(diff == diff) || !(rho == rho);
-      if (bad || diff < S->delta || k > S->max_iter) {
+      if (bad || diff < s_delta || k > s_max_iter) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {
           S->diff = diff;
           S->iters = k - 1;
           S->status = bad ? int(Status::kBreakdown)
-                          : (diff < S->delta ? int(Status::kConverged) : int(Status::kMaxIter));
+                          : (diff < s_delta ? int(Status::kConverged) : int(Status::kMaxIter));
           if (bad) S->nan_flag = 1;
           S->done = 1;
         }
         return;
       }
-      beta = rho / S->zr[k & 1];  // rho_{k-2} sits in slot k & 1
+      beta = rho / ((k & 1) ? zr1 : zr0);  // rho_{k-2} sits in slot k & 1
     }
-    const double denom = S->red_c[1] + beta * (2.0 * S->red_c[2] + beta * S->red_c[3]);
-    const bool bd = S->norm == int(Norm::kWeighted) ? fabs(denom) < S->bd_tol : denom < S->bd_tol;
+    const double denom = rc[1] + beta * (2.0 * rc[2] + beta * rc[3]);
+    const bool bd = s_norm == int(Norm::kWeighted) ? fabs(denom) < s_bd_tol : denom < s_bd_tol;
     if (bd || !(denom == denom)) {
       if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (k >= 2) S->diff = diff;
@@ -436,7 +470,6 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
     // below pair_min_beta the sweep re-reads p^{k-2} from the buffer it is about to overwrite.
     // w moves on one sweep in three: 37.3 instead of 40 B/pt per iteration.  The stop test uses
     // |alpha| ||p||, so the schedule changes no iteration count, only w's rounding.
-    const int cyc = S->w_cycle;
     const int ph = int(k % cyc);
     // the host launches the w-sweep kernel (WS) exactly on the sweeps k = 0 mod w_cycle; a
     // mismatch (host and device iteration counters out of step) must not pass silently
@@ -450,12 +483,12 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
       return;
     }
     if (ph == 0) {
-      c1 = S->alpha1[(k - 1) & 3];
+      c1 = ring4(al, k - 1);
       wm = 1;
       if (cyc == 3) {
-        const double bprev = S->beta1[(k - 1) & 3];
-        const double a2 = S->alpha1[(k - 2) & 3];
-        if (fabs(bprev) >= S->pair_min_beta) { wm = 2; c2 = a2 / bprev; }
+        const double bprev = ring4(be, k - 1);
+        const double a2 = ring4(al, k - 2);
+        if (fabs(bprev) >= s_pmb) { wm = 2; c2 = a2 / bprev; }
         else { wm = 3; c2 = a2; }
       }
     }
@@ -470,12 +503,10 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) S->halo_k = k + 1;  // the next exchange fills sweep k+1's inputs
   int ti = 0, tj = 0;
-  const int pos = xcd_remap(blockIdx.x, gridDim.x) * WAVES + __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   if (part.order) {  // slow (ellipse-cut) tiles first, so they do not trail the sweep
     if (pos >= part.count) return;
-    const int t = ld_uniform(part.order, pos);
-    ti = t / tiles_j;
-    tj = t - ti * tiles_j;
+    ti = ord / tiles_j;
+    tj = ord - ti * tiles_j;
   } else if (!pcg1_tile(pos, part, tiles_j, ti, tj)) {
     return;
   }
@@ -488,6 +519,9 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
   const T* rold = (k & 1) ? r2 : r;
   T* rnew = (k & 1) ? r : r2;
   double acc[kNq] = {0.0, 0.0, 0.0, 0.0, 0.0};
+#ifdef PMX_WAVE_TRACE
+  const unsigned long long wtm = __builtin_amdgcn_s_memrealtime();  // end of the prologue
+#endif
   __shared__ double s_col[WAVES * 4 * VEC * 64];  // 4 KB per wave (VEC 2)
   double* scol = s_col + __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)) * (4 * VEC * 64);
   // interior tile: full width, and the marched rows i0-2..i1+2 / columns j0-2..j0+64*VEC-3 lie
@@ -529,11 +563,12 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
     const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
     const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
-    unsigned long long* o = g_wtrace + 4 * int64_t(blockIdx.x);
+    unsigned long long* o = g_wtrace + 5 * int64_t(blockIdx.x);
     o[0] = wt0;
     o[1] = t1;
     o[2] = (static_cast<unsigned long long>(xcc) << 32) | hw;
     o[3] = static_cast<unsigned long long>(id) | (static_cast<unsigned long long>(part.part) << 40);
+    o[4] = wtm;
   }
 #endif
 }
@@ -818,8 +853,8 @@ void launch_reduce_n(const double* partials, int n, int nq, const double* weight
 #ifdef PMX_WAVE_TRACE
 void* pcg1_wave_trace_setup(long long it, int nwaves) {
   void* buf = nullptr;
-  HIP_CHECK(hipMalloc(&buf, size_t(nwaves) * 32));
-  HIP_CHECK(hipMemset(buf, 0, size_t(nwaves) * 32));
+  HIP_CHECK(hipMalloc(&buf, size_t(nwaves) * 40));
+  HIP_CHECK(hipMemset(buf, 0, size_t(nwaves) * 40));
   HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_wtrace), &buf, sizeof(buf)));
   HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_wtrace_it), &it, sizeof(it)));
   return buf;
