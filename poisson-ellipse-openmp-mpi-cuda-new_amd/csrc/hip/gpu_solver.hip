@@ -353,7 +353,7 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
   st.norm = int(spec_.norm);
   st.pair_w = opt_.pair_w ? 1 : 0;
   st.pair_min_beta = opt_.pair_w == 2 ? HUGE_VAL : 1e-3;
-  st.w_cycle = w_cycle();  // fp32 k_pcg1 is built with pairs only
+  st.w_cycle = w_cycle();
   host_k_ = st.it;
   HIP_CHECK(hipMemcpyAsync(state_, &st, sizeof(PcgState), hipMemcpyHostToDevice, s));
   T* w = static_cast<T*>(field_base(0));

@@ -340,7 +340,7 @@ done:
 template <typename T, int VEC, int WAVES, int PF, bool WS>
 constexpr int pcg1_min_waves() {
   if (VEC != 2 || WAVES != 1) return 1;
-  if (sizeof(T) == 4 && PF == 1) return 4;
+  if (sizeof(T) == 4 && PF == 1) return WS ? 3 : 4;  // the fp32 w sweep carries the triple paths
   if (sizeof(T) == 8 && PF == 1 && !WS) return 4;
   return PF <= 2 ? 3 : 2;
 }
@@ -530,13 +530,9 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
                     G.gj0 + j0 - 2 >= 1 && G.gj0 + j0 + 64 * VEC - 3 <= G.N - 1;
 #define PMX_MARCH(E, F) \
   pcg1_march<T, VEC, PF, E, F>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, acc, scol)
-  // fp32 storage keeps pairs (w_cycle 2, see init): the triple paths' registers would push the
-  // 4-waves/SIMD fp32 kernel (127 VGPRs) into spills
 #define PMX_MARCH_W(F)                                     \
   if constexpr (!WS) {                                     \
     PMX_MARCH(0, F);                                       \
-  } else if constexpr (sizeof(T) == 4) {                   \
-    PMX_MARCH(1, F);                                       \
   } else {                                                 \
     switch (wm) {                                          \
       case 1: PMX_MARCH(1, F); break;                      \

@@ -185,7 +185,7 @@ class GpuSubdomainSolver {
   // w-moving k_pcg1 (see launch_pcg1); captured graphs depend on its phase modulo w_cycle().
   long long host_k() const { return host_k_; }
   void set_host_k(long long k) { host_k_ = k; }
-  int w_cycle() const { return pcg1_ ? (elem_ == 8 ? opt_.wcycle1 : 2) : 1; }
+  int w_cycle() const { return pcg1_ ? opt_.wcycle1 : 1; }
   bool w_sweep_next() const { return pcg1_ && host_k_ > 0 && host_k_ % w_cycle() == 0; }
   const TileCfg& tiles_b() const { return tiles_b_; }  // pcg_b
   int device() const { return opt_.device; }

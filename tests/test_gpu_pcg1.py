@@ -161,14 +161,26 @@ def test_pcg1_triple_w_midrun_materialised(pkg, monkeypatch, steps):
     assert np.abs(out[3] - out[2]).max() < 1e-14
 
 
-def test_pcg1_fp32_keeps_pairs(pkg, monkeypatch):
+def test_pcg1_fp32_triples(pkg, monkeypatch):
+    """fp32 storage moves w in triples too (its w sweep is a 3-waves/SIMD kernel of its own): same
+    iteration count as pairs and as the fp64 solve, w within fp32 rounding of the pairs' w."""
     from conftest import sub
     monkeypatch.setenv("PMX_ALGO", "1")
-    s = sub("models").make_session(pkg.PoissonEllipse(M=200, N=300), dtype="fp32")
+    p = pkg.PoissonEllipse(M=400, N=600)
+    s = sub("models").make_session(p, dtype="fp32")
     s.init()
     s.step(4)
     s.synchronize()
-    assert s.state()["w_cycle"] == 2
+    assert s.state()["w_cycle"] == 3
+    out = {}
+    for cyc in (2, 3):
+        monkeypatch.setenv("PMX_PCG1_WCYCLE", str(cyc))
+        out[cyc] = pkg.solve(p, "hip", dtype="fp32")
+    ref = pkg.solve(p, "cpu")
+    assert out[2].iters == out[3].iters  # the w schedule never touches r, p or the stop test
+    assert abs(out[3].iters - ref.iters) <= 2  # fp32 storage rounds r and p
+    assert np.abs(out[3].w - out[2].w).max() < 1e-5
+    assert np.abs(out[3].w - ref.w).max() < 1e-4
 
 
 @pytest.mark.parametrize("ranks", [1, 4])
