@@ -332,11 +332,12 @@ done:
 // Waves per SIMD the register allocation must allow (VEC=2, 1 wave/workgroup):
 //  * fp64: 139 VGPRs at PF=1 and 153 at PF=2 fit 3 waves/SIMD with no spills; forcing 4 (127
 //    VGPRs, 4 spilled) is 2.65% slower (NOTES #36).  PF >= 3 runs at 2.
-//  * fp32 storage (half the prefetch registers): PF=1 fits 4 waves/SIMD with no spills (127
-//    VGPRs) -- 32768^2 4.54 vs 5.03 ms at 3 waves/SIMD with PF=2 (NOTES #37); PF=2 would spill.
+//  * fp32 storage (half the prefetch registers): PF=1 -- 32768^2 4.54 vs 5.03 ms at 3 waves/SIMD
+//    with PF=2 (NOTES #37).
 // Other shapes: whatever the allocator picks.
 //  * The sweeps that move w (WS, one in w_cycle) are a kernel of their own: without the w paths
-//    the fp64 plain sweep needs 119 VGPRs and runs at 4 waves/SIMD, the w sweep (151) at 3.
+//    the plain sweep needs 113 VGPRs in fp64 / 111 in fp32 and runs at 4 waves/SIMD; the w sweep
+//    with the triple paths (149 / 135 VGPRs) at 3 (profiles/r2/prologue/, profiles/r2/fp32_w3/).
 template <typename T, int VEC, int WAVES, int PF, bool WS>
 constexpr int pcg1_min_waves() {
   if (VEC != 2 || WAVES != 1) return 1;
