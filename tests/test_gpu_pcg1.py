@@ -203,3 +203,21 @@ def test_pcg1_graph_phases_match_eager(pkg, monkeypatch, ranks):
         out[gb] = (s.gather_local_w(), st["diff"])
     assert np.array_equal(out[0][0], out[32][0])
     assert out[0][1] == out[32][1]
+
+
+@pytest.mark.parametrize("ranks", [1, 4])
+@pytest.mark.parametrize("dtype", ["fp64", "fp32"])
+def test_pcg1_dispatch_order_bitwise(pkg, monkeypatch, ranks, dtype):
+    """Cut-tiles-first dispatch (pcg1_build_order, the default) only permutes which wave marches
+    which tile: every tile keeps its partial-sum slot, so the result is bitwise that of the
+    natural order (PMX_PCG1_ORDER=0)."""
+    p = pkg.PoissonEllipse(M=800, N=1200)
+    monkeypatch.setenv("PMX_ALGO", "1")
+    out = {}
+    for order in ("0", "1"):
+        monkeypatch.setenv("PMX_PCG1_ORDER", order)
+        out[order] = pkg.solve(p, "hip", ranks=ranks, dtype=dtype)
+    assert out["0"].iters == out["1"].iters
+    if dtype == "fp64":
+        assert out["1"].iters == 989
+    assert np.array_equal(out["0"].w, out["1"].w)
