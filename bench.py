@@ -3,36 +3,62 @@
 
 Metric (BASELINE.json): grid-point updates per second (MLUPS) + iterations-to-tolerance on a
 16384^2 grid at 1/2/4/8 MI355X.  One "step" = one full PCG iteration (halo exchange, A p with
-(Ap,p), w/r update with ||dw|| and (z,r), both all-reduces, p update) -- nothing skipped.
+(Ap,p), w/r update with ||dw|| and (z,r), the all-reduce, p update) -- nothing skipped.
 MLUPS = (M-1)(N-1) * steps / time / 1e6, whole-job aggregate.  The grid is fixed as N grows
 (strong scaling).  Synthetic data = the reference problem itself: F = 1 in the ellipse
 x^2 + 4y^2 < 1, zero initial guess (there is no dataset).
 
     python bench.py --gpus 1 --steps 200 --warmup 20
     python bench.py --gpus 8                  # spawns 8 ranks itself (one per GPU)
-    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \\
         --master-port 29500 bench.py --gpus 8 --steps 200 --warmup 20
 
-Without a launcher (no WORLD_SIZE in the environment) and --gpus N > 1, this process starts the N
-ranks itself -- before anything touches the GPU -- and exits with their status.  A run whose rank
-count differs from --gpus fails; it never measures fewer GPUs than it reports.
+Multi-GPU runs are supervised (reference lifecycle: stage4-mpi+cuda/poisson_mpi_cuda_f.cu:986-1039).
+The process(es) started by the user or by torchrun never touch the GPU: they start the measuring
+ranks as child processes and walk a fallback ladder of transports, each rung in fresh processes:
+    rung 1  native RCCL, iterations captured in hipGraphs, split sweep (the production path)
+    rung 2  native RCCL, eager launches, no split sweep
+    rung 3  torch.distributed ProcessGroupNCCL (= RCCL) driving the same native kernels
+Every rank runs under a progress watchdog: each phase (setup, canary iteration, first graph batch,
+warmup, timed region, tolerance solve) has a deadline; on expiry the rank prints the phase and the
+device's own progress counters (sweeps reduced, ghost exchanges packed / unpacked) and exits, and
+the supervisor moves to the next rung.  The JSON line names the rung that produced it, the transport
+(`comm`), `rccl_graph`, `split_sweep`, the failed rungs, and whether the timed region replayed graphs
+(`timed_path`).  A run whose rank count differs from --gpus fails; it never measures fewer GPUs
+than it reports.
 
-After the timed region a full solve to ||w^{k+1}-w^k|| < 1e-6 reports iters-to-tol and the
-accuracy against the analytic solution (disable with --no-tol-solve).
+After the timed region a full solve to ||w^{k+1}-w^k|| < 1e-6 reports iters-to-tol and the error
+of the solution against the analytic u = (1 - x^2 - 4y^2)/10 (l2_error, max_error; disable with
+--no-tol-solve).  That stop rule is the reference's absolute one: at fine grids it ends well before
+discretisation accuracy (32768^2: L2 error 5.7e-3), exactly as the reference's solver would.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
+import tempfile
+import threading
 import time
 
 BASELINE_MLUPS = 2450.0  # best published reference rate: 2x P100, 2400x3200 (BASELINE.md)
 METRIC = "grid-point updates/sec (MLUPS) + iters-to-tol, 16384^2 grid at 1/2/4/8 MI355X"
+TOL_NOTE = ("stop rule ||w^{k+1}-w^k|| < delta absolute (reference rule); at fine grids the solve ends "
+            "before discretisation accuracy")
+
+# fallback ladder (see the module docstring); `split` None = the driver's default for the transport
+RUNGS = {
+    1: dict(comm="native", rccl_graph=True, split=None),
+    2: dict(comm="native", rccl_graph=False, split=0),
+    3: dict(comm="torch", rccl_graph=False, split=0),
+}
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -43,12 +69,14 @@ def parse():
                     help="CG guard on (Ap,p) (reference: 1e-15; grids beyond ~100000^2 need a smaller value)")
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32", "mixed"],
                     help="mixed = fp32: fp32 storage, fp64 arithmetic and reductions")
-    ap.add_argument("--comm", default="native", choices=["native", "torch"])
+    ap.add_argument("--comm", default="native", choices=["native", "torch"],
+                    help="first rung of the ladder: native RCCL (rung 1) or torch.distributed (rung 3)")
+    ap.add_argument("--ladder", default="on", choices=["on", "off"],
+                    help="multi-GPU: fall back to the next transport when a rung fails or stalls")
     ap.add_argument("--split", default="auto", choices=["reference", "auto", "rows", "cols"],
-                    help="process grid: auto = least ghost volume (1x1, 2x1, 4x1, 4x2 blocks for 1/2/4/8 "
-                         "ranks at 16384^2: wide per-rank blocks run the sweep faster, e.g. 4096x8192 "
-                         "0.388 ms vs the reference's 8192x4096 0.403 ms); reference = the reference's "
-                         "choose_process_grid (1x2, 2x2, 2x4)")
+                    help="process grid: auto = row strips while every strip keeps >= 128 rows, else the "
+                         "least ghost perimeter (16384^2: 2x1, 4x1, 8x1 for 2/4/8 ranks); reference = the "
+                         "reference's choose_process_grid (1x2, 2x2, 2x4)")
     ap.add_argument("--kernel", default="wave", choices=["wave", "lds"],
                     help="wave: wave-tile kernels with DPP lane shifts; lds: workgroup tiles + LDS row ring")
     ap.add_argument("--block", type=int, default=256, help="lds kernels: tile width")
@@ -59,88 +87,312 @@ def parse():
                     help="pcg_b: ring-free 2-row tiles (default) or the software-pipelined ring kernel")
     ap.add_argument("--waves", type=int, default=4, help="wave kernels: wave tiles per workgroup")
     ap.add_argument("--tile-rows", type=int, default=0, help="tile height (0 = auto)")
-    ap.add_argument("--graph-batch", type=int, default=32)
+    ap.add_argument("--graph-batch", type=int, default=32,
+                    help="iterations per captured hipGraph; the timed region replays graphs for any --steps "
+                         "(full batches plus one remainder graph, all captured during warmup)")
     ap.add_argument("--overlap", default="on", choices=["on", "off"],
-                    help="ghost exchange on a second HIP stream, overlapped with the w/r update kernel")
+                    help="ghost exchange on a second HIP stream, overlapped with the sweep")
     ap.add_argument("--exact", action="store_true", help="reference arithmetic order in the fused kernels")
     ap.add_argument("--tol-solve", dest="tol_solve", action="store_true", default=True)
     ap.add_argument("--no-tol-solve", dest="tol_solve", action="store_false")
     ap.add_argument("--tol-time-cap", type=float, default=300.0, help="seconds allowed for the tol solve")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--cpu-dry-run", action="store_true",
-                    help="test the launch/timing/reporting flow on CPU (gloo, plain-PyTorch PCG); "
+                    help="test the launch/ladder/timing/reporting flow on CPU (gloo, plain-PyTorch PCG); "
                          "prints a JSON line marked data=cpu-dry-run, not a measurement")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal: all ranks on GPU 0, native kernels, gloo comm staged through host "
                          "memory (valid=false: not a multi-GPU measurement)")
     ap.add_argument("--rccl-graph", default="on", choices=["on", "off"],
-                    help="multi-rank native path: capture the RCCL calls into the hipGraph batches")
+                    help="rung 1: capture the RCCL calls into the hipGraph batches (off: start at rung 2)")
     ap.add_argument("--profile-phases", type=int, default=0,
                     help="after the run: N eager iterations timed per phase, MAX over ranks, printed as "
                          "the reference's stage-4 buckets on stderr and added to the JSON line")
-    return ap.parse_args()
+    ap.add_argument("--deadline-scale", type=float, default=1.0,
+                    help="multiplies every progress-watchdog deadline")
+    ap.add_argument("--rung-timeout", type=float, default=480.0,
+                    help="supervisor: hard limit (s) for one rung's processes")
+    return ap.parse_args(argv)
 
 
-def spawn_ranks(n: int) -> int:
-    """Start n ranks of this script (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set) and return their
-    status.  Runs before any GPU call in this process; a failing rank stops the others."""
-    import signal
-    import socket
-    import subprocess
+# =============================================================================================
+# progress watchdog (every measuring rank)
+# =============================================================================================
+class Watch:
+    """Per-phase deadlines.  A rank stuck in a phase (a collective whose peer never posts, a kernel
+    that never finishes) cannot be interrupted from Python; this thread reports where it is and ends
+    the process, which is what lets the supervisor move on instead of burning the lease."""
 
-    sock = socket.socket()
-    sock.bind(("127.0.0.1", 0))
-    port = sock.getsockname()[1]
-    sock.close()
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PMX_BENCH_SPAWNED="1")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
-    rc, failed_at = 0, None
+    EXIT_CODE = 87
+
+    def __init__(self, rank: int, scale: float = 1.0):
+        self.rank, self.scale = rank, scale
+        self.name, self.deadline, self.t0 = "start", None, time.monotonic()
+        self.progress = None  # callable -> device progress tuple, or None
+        self._lock = threading.Lock()
+        threading.Thread(target=self._run, daemon=True, name="pmx-watch").start()
+
+    def phase(self, name: str, seconds: float):
+        with self._lock:
+            self.name, self.t0 = name, time.monotonic()
+            self.deadline = self.t0 + seconds * self.scale
+
+    def _run(self):
+        while True:
+            time.sleep(0.25)
+            with self._lock:
+                name, dl, t0 = self.name, self.deadline, self.t0
+            if dl is not None and time.monotonic() > dl:
+                dev = ""
+                try:
+                    pr = self.progress() if self.progress else None
+                    if pr is not None:
+                        dev = (f"; device progress: {pr[0]} sweeps reduced, {pr[1]} ghost exchanges packed, "
+                               f"{pr[2]} unpacked")
+                except Exception as e:  # the diagnosis must not mask the exit
+                    dev = f"; device progress unreadable ({e})"
+                print(f"[bench] rank {self.rank}: no progress in phase '{name}' for "
+                      f"{time.monotonic() - t0:.0f} s{dev}; aborting this rank", file=sys.stderr, flush=True)
+                os._exit(self.EXIT_CODE)
+
+
+def _fault(rung: int, rank: int):
+    """Fault injection for the ladder tests: PMX_BENCH_FAULT='1:hang,2:fail' (optionally '1:hang@0',
+    rank 0 only) -> (kind, phase) for this rung/rank, kind in hang|fail|crash."""
+    spec = os.environ.get("PMX_BENCH_FAULT", "")
+    for item in filter(None, (x.strip() for x in spec.split(","))):
+        r, _, what = item.partition(":")
+        what, _, who = what.partition("@")
+        if int(r) == rung and (not who or int(who) == rank):
+            return what
+    return None
+
+
+# =============================================================================================
+# supervisor (never touches the GPU): starts the measuring ranks, walks the ladder
+# =============================================================================================
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _child_env(rank: int, local_rank: int, world: int, port: int, rung: int, result: str) -> dict:
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    env.update(RANK=str(rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PMX_BENCH_ROLE="child", PMX_BENCH_RUNG=str(rung),
+               PMX_BENCH_RESULT=result)
+    return env
+
+
+def _spawn(env: dict):
+    # children print their diagnostics to our stderr; the only stdout line is the supervisor's
+    return subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env,
+                            stdout=sys.stderr, start_new_session=True)
+
+
+def _kill(p, sig=signal.SIGKILL):
+    if p.poll() is None:
+        try:
+            os.killpg(p.pid, sig)
+        except ProcessLookupError:
+            pass
+
+
+def _ladder(args) -> list[int]:
+    if args.share_gpu:
+        first = 1
+    elif args.comm == "torch":
+        first = 3
+    else:
+        first = 1 if args.rccl_graph == "on" else 2
+    rungs = [r for r in (1, 2, 3) if r >= first]
+    if args.share_gpu:
+        rungs = [1]  # one transport (gloo, host-staged)
+    return rungs if args.ladder == "on" else rungs[:1]
+
+
+def _run_rung_local(args, rung: int, result: str) -> tuple[bool, str]:
+    """All ranks are children of this process (no launcher)."""
+    world = args.gpus
+    port = _free_port()
+    procs = [_spawn(_child_env(r, r, world, port, rung, result)) for r in range(world)]
+    t0, failed_at, reason = time.monotonic(), None, ""
     while True:
         codes = [p.poll() for p in procs]
-        bad = [c for c in codes if c not in (None, 0)]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
         if bad and failed_at is None:
-            rc, failed_at = bad[0], time.time()
-            print(f"[bench] a rank exited with status {rc}; stopping the others", file=sys.stderr, flush=True)
+            failed_at = time.monotonic()
+            reason = f"rank {bad[0][0]} exited with status {bad[0][1]}"
+            print(f"[bench] rung {rung}: {reason}; stopping the other ranks", file=sys.stderr, flush=True)
             for p in procs:
-                if p.poll() is None:
-                    p.send_signal(signal.SIGTERM)
+                _kill(p, signal.SIGTERM)
         if all(c is not None for c in codes):
             break
-        if failed_at is not None and time.time() - failed_at > 20:
+        if failed_at is not None and time.monotonic() - failed_at > 10:
             for p in procs:
-                if p.poll() is None:
-                    p.kill()
+                _kill(p)
+        if failed_at is None and time.monotonic() - t0 > args.rung_timeout:
+            failed_at = time.monotonic()
+            reason = f"rung timeout ({args.rung_timeout:.0f} s)"
+            print(f"[bench] rung {rung}: {reason}; killing its ranks", file=sys.stderr, flush=True)
+            for p in procs:
+                _kill(p)
         time.sleep(0.2)
-    return rc or max(p.returncode for p in procs)
+    ok = failed_at is None and all(p.returncode == 0 for p in procs)
+    if not ok and not reason:
+        reason = f"exit status {[p.returncode for p in procs]}"
+    return ok, reason
 
 
-def main():
-    args = parse()
-    if args.gpus < 1:
-        raise SystemExit("--gpus must be >= 1")
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(spawn_ranks(args.gpus))
+def _run_rung_torchrun(args, rung: int, result: str, store, rank: int, local_rank: int) -> tuple[bool, str]:
+    """One supervisor per rank (torchrun started them): each runs its own rank's child; the
+    supervisors share torchrun's store to agree on a port and to stop early when any rank fails."""
+    import torch
+    import torch.distributed as dist
+
+    world = args.gpus
+    key = f"pmx/rung{rung}"
+    if rank == 0:
+        store.set(f"{key}/port", str(_free_port()))
+    port = int(store.get(f"{key}/port").decode())
+    p = _spawn(_child_env(rank, local_rank, world, port, rung, result))
+    t0, mine = time.monotonic(), ""
+    while True:
+        c = p.poll()
+        if c is not None:
+            if c != 0:
+                mine = f"rank {rank} exited with status {c}"
+                store.set(f"{key}/fail", mine)
+            break
+        if store.check([f"{key}/fail"]):
+            time.sleep(5)  # let this rank's own watchdog / error path report first
+            _kill(p, signal.SIGTERM)
+            time.sleep(2)
+            _kill(p)
+            p.wait()
+            break
+        if time.monotonic() - t0 > args.rung_timeout:
+            mine = f"rank {rank}: rung timeout ({args.rung_timeout:.0f} s)"
+            store.set(f"{key}/fail", mine)
+            _kill(p)
+            p.wait()
+            break
+        time.sleep(0.2)
+    bad = torch.tensor([0 if (p.returncode == 0 and not mine) else 1], dtype=torch.int32)
+    dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+    ok = int(bad.item()) == 0
+    reason = "" if ok else (store.get(f"{key}/fail").decode() if store.check([f"{key}/fail"]) else mine or "failed")
+    return ok, reason
+
+
+def supervise(args) -> int:
+    world = args.gpus
+    launched = "WORLD_SIZE" in os.environ
+    rank = int(os.environ.get("RANK", 0))
+    store = None
+    if launched:
+        if int(os.environ["WORLD_SIZE"]) != world:
+            print(f"[bench] --gpus {world} but {os.environ['WORLD_SIZE']} rank(s) came up (WORLD_SIZE); refusing "
+                  "to report a different GPU count", file=sys.stderr, flush=True)
+            return 2
+        import datetime
+
+        import torch.distributed as dist
+
+        # gloo prints its connection banner on stdout; the supervisor's stdout carries only the JSON
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=60))
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
+        store = dist.distributed_c10d._get_default_store()
+    local_rank = int(os.environ.get("LOCAL_RANK", rank))
+    tmp = tempfile.mkdtemp(prefix="pmx_bench_")
+    attempts, final = [], None
+    for rung in _ladder(args):
+        result = os.path.join(tmp, f"rung{rung}.json")
+        t0 = time.monotonic()
+        if launched:
+            ok, reason = _run_rung_torchrun(args, rung, result, store, rank, local_rank)
+        else:
+            ok, reason = _run_rung_local(args, rung, result)
+        att = dict(rung=rung, **RUNGS[rung], ok=ok, seconds=round(time.monotonic() - t0, 1))
+        if not ok:
+            att["reason"] = reason
+        attempts.append(att)
+        if ok:
+            if rank == 0:
+                with open(result) as f:
+                    final = json.loads(f.read().strip().splitlines()[-1])
+            break
+        print(f"[bench] rung {rung} ({RUNGS[rung]}) failed: {reason}", file=sys.stderr, flush=True)
+    rc = 0
+    if rank == 0:
+        if final is None:
+            print(f"[bench] every rung of the ladder failed: {attempts}", file=sys.stderr, flush=True)
+            rc = 1
+        else:
+            final["ladder"] = attempts
+            line = json.dumps(final)
+            print(line, flush=True)
+            if args.json_out:
+                with open(args.json_out, "w") as f:
+                    f.write(line + "\n")
+    if launched:
+        import torch
+        import torch.distributed as dist
+
+        t = torch.tensor([rc], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        rc = int(t.item())
+        dist.destroy_process_group()
+    return rc
+
+
+# =============================================================================================
+# measuring rank
+# =============================================================================================
+def measure(args) -> int:
     import importlib
 
     import torch
     import torch.distributed as dist
 
-    pmx = importlib.import_module("poisson-ellipse-openmp-mpi-cuda-new_amd")
-    from importlib import import_module
+    pkg_name = "poisson-ellipse-openmp-mpi-cuda-new_amd"
+    pmx = importlib.import_module(pkg_name)
+    launch = importlib.import_module(pkg_name + ".parallel.launch")
+    ds = importlib.import_module(pkg_name + ".parallel.dist_solver")
+    process_grid = importlib.import_module(pkg_name + ".parallel.decomp").process_grid
 
-    launch = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.parallel.launch")
-    ds = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.parallel.dist_solver")
-    process_grid = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.parallel.decomp").process_grid
+    supervised = os.environ.get("PMX_BENCH_ROLE") == "child"
+    rung = int(os.environ.get("PMX_BENCH_RUNG", "1"))
+    cfg = RUNGS[rung]
     dry = args.cpu_dry_run
     share = args.share_gpu and not dry
-    info = launch.init_distributed(device_type="cpu" if (dry or share) else None)
-    world = info.world
-    if world != args.gpus:
-        raise SystemExit(f"[bench] --gpus {args.gpus} but {world} rank(s) came up (WORLD_SIZE); refusing to "
+    env = launch.env_info()
+    watch = Watch(env.rank, args.deadline_scale)
+    fault = _fault(rung, env.rank) if supervised else None
+    if fault == "crash":
+        os._exit(3)
+
+    watch.phase("setup", 300)
+    if env.world != args.gpus:
+        raise SystemExit(f"[bench] --gpus {args.gpus} but {env.world} rank(s) came up (WORLD_SIZE); refusing to "
                          "report a different GPU count")
+    native = not dry and not share and cfg["comm"] == "native"
+    # Python-level coordination (uid broadcast, agreement, barriers, MAX over ranks) stays on gloo for
+    # the native transport: no third (torch) RCCL communicator next to the solver's two
+    backend = "nccl" if (not dry and not share and cfg["comm"] == "torch") else "gloo"
+    info = launch.init_distributed(backend=backend if env.world > 1 else None,
+                                   device_type="cpu" if (dry or share or backend == "gloo") else None)
+    world = info.world
     device = 0 if share else info.local_rank
     if not dry:
         if not torch.cuda.is_available():
@@ -148,6 +400,9 @@ def main():
         if not share and torch.cuda.device_count() < world:
             raise SystemExit(f"[bench] {world} ranks need {world} visible GPUs, found {torch.cuda.device_count()}")
         torch.cuda.set_device(device)
+    if cfg["split"] is not None and not dry:
+        os.environ["PMX_PCG1_SPLIT"] = str(cfg["split"])  # read by the native driver at construction
+    tdev = "cuda" if info.backend == "nccl" else "cpu"
 
     def device_sync():
         if not dry:
@@ -158,62 +413,61 @@ def main():
               waves=args.waves, tile_rows=args.tile_rows, exact=args.exact, graph_batch=args.graph_batch,
               overlap=args.overlap == "on", vec_b=args.vec_b, tile_rows_b=args.tile_rows_b,
               b_ring=args.b_kernel == "ring")
-    comm_used = args.comm
+    if fault == "fail":
+        raise RuntimeError(f"injected failure (PMX_BENCH_FAULT) at rung {rung}")
     if dry:
-        tp = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.models.torch_pcg")
-        comm = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.parallel.comm")
-        runner = tp.TorchPCG(problem, comm=comm.TorchComm() if world > 1 else None, split=args.split)
-        runner.tile = lambda: dict(kind="torch-cpu")
+        tp = importlib.import_module(pkg_name + ".models.torch_pcg")
+        comm = importlib.import_module(pkg_name + ".parallel.comm")
+        runner = ds.TorchRunner(tp.TorchPCG(problem, comm=comm.TorchComm() if world > 1 else None,
+                                            split=args.split), problem, info)
         comm_used = "gloo" if world > 1 else "self"
     elif world == 1:
-        models = import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.models")
-        sess = models.make_session(problem, ranks=1, device=info.local_rank, **kw)
-
-        class Runner:
-            init = sess.init
-            step = sess.step
-            synchronize = sess.synchronize
-
-            @staticmethod
-            def tile():
-                return sess.tile
-
-            @staticmethod
-            def state():
-                return sess.state(0)
-
-            @staticmethod
-            def profile(n):
-                sess.init()
-                ph = sess.profile(int(n))
-                return {"compute": ph["t_kernel_a"] + ph["t_kernel_b"], "copy": 0.0, "comm": ph["t_comm"],
-                        "precond": 0.0, "dot": ph["t_reduce"]}
-
-        runner = Runner()
+        models = importlib.import_module(pkg_name + ".models")
+        runner = ds.SessionRunner(models.make_session(problem, ranks=1, device=info.local_rank, **kw), problem, info)
         comm_used = "self"
+    elif share:
+        runner = ds.DistGpuPCG(problem, info, comm="torch", device=0, **kw)
+        comm_used = "gloo-host-staged"
+    elif cfg["comm"] == "native":
+        runner = ds.DistGpuPCG(problem, info, comm="native", rccl_graph=cfg["rccl_graph"], **kw)
+        comm_used = "rccl"
     else:
-        if share:
-            runner = ds.DistGpuPCG(problem, info, comm="torch", device=0, **kw)
-            comm_used = "gloo-host-staged"
-        else:
-            try:  # setup and RCCL init are agreed collectively: every rank raises, or none does
-                runner = ds.DistGpuPCG(problem, info, comm=args.comm, rccl_graph=args.rccl_graph == "on", **kw)
-            except RuntimeError as e:  # native RCCL bootstrap failed -> portable torch.distributed path
-                if args.comm != "native":
-                    raise
-                print(f"[bench] native RCCL comm failed ({e}); falling back to torch.distributed", file=sys.stderr)
-                runner = ds.DistGpuPCG(problem, info, comm="torch", **kw)
-                comm_used = "torch"
+        runner = ds.DistGpuPCG(problem, info, comm="torch", **kw)
+        comm_used = "torch-nccl"
+    watch.progress = getattr(runner, "progress", None)
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    # ---------------- timed region ----------------
+    # ---------------- canary: one eager iteration, then the first graph batch ----------------
+    watch.phase("canary", 120)
+    runner.init()
+    it0 = runner.state()["it"]
+    if fault == "hang":
+        time.sleep(10 ** 6)  # the watchdog ends this rank
+    runner.step_eager(1)
+    runner.synchronize()
+    stc = runner.state()
+    if stc["it"] != it0 + 1 and not stc["done"]:
+        raise RuntimeError(f"canary iteration: device iteration counter {it0} -> {stc['it']}")
+    watch.phase("first-batch", 120)
+    if getattr(runner, "graphs", False):
+        runner.prepare(args.graph_batch)
+        runner.step(args.graph_batch)
+        runner.synchronize()
+
+    # ---------------- warmup (captures every graph the timed region replays) ----------------
+    watch.phase("warmup", 120 + 0.05 * args.warmup)
     runner.init()
     runner.step(args.warmup)
     runner.synchronize()
+    prepared = runner.prepare(args.steps) if getattr(runner, "graphs", False) else False
     st0 = runner.state()
+    runner.reset_path_stats()
+
+    # ---------------- timed region ----------------
+    watch.phase("timed", 120 + 0.05 * args.steps)
     barrier()
     device_sync()
     t0 = time.perf_counter()
@@ -224,18 +478,22 @@ def main():
     t1 = time.perf_counter()
     dt = t1 - t0
     st1 = runner.state()
+    path = runner.path_stats()
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cpu" if (dry or share) else "cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    tile_desc = runner.tile() if hasattr(runner, "tile") else dict(rows=args.tile_rows, vec=args.vec)
+    timed_path = ("graph" if path["eager_iters"] == 0 and path["graph_iters"] > 0 else
+                  "eager" if path["graph_iters"] == 0 else "mixed")
+    tile_desc = runner.tile()
     valid = (not st1["done"]) and (st1["it"] - st0["it"] == args.steps) and not st1["nan"]
     pts = (args.M - 1) * (args.N - 1)
     mlups = pts * args.steps / dt / 1e6
 
-    # ---------------- iterations to tolerance ----------------
+    # ---------------- iterations to tolerance + accuracy ----------------
     tol = {}
     if args.tol_solve:
+        watch.phase("tol-solve", 120)
         runner.init()
         barrier()
         device_sync()
@@ -247,11 +505,12 @@ def main():
             runner.step(batch)
             launched += batch
             st = runner.state()
+            watch.phase("tol-solve", 120)
             stop = 2 if (st["done"] or launched > max_iter + batch) else 0
             if not stop and time.perf_counter() - ts > args.tol_time_cap:
                 stop = 1
             if world > 1:  # one decision for all ranks: a rank that stops alone would hang the rest
-                flag = torch.tensor([stop], dtype=torch.int32, device="cpu" if (dry or share) else "cuda")
+                flag = torch.tensor([stop], dtype=torch.int32, device=tdev)
                 dist.all_reduce(flag, op=dist.ReduceOp.MAX)
                 stop = int(flag.item())
             if stop:
@@ -260,19 +519,27 @@ def main():
         runner.synchronize()
         barrier()
         tsolve = time.perf_counter() - ts
+        watch.phase("accuracy", 300)
+        err = runner.error_norms()
         tol = dict(iters_to_tol=int(st["iters"]) if st["done"] else None, tol_status=st["status"],
                    tol_final_diff=st["diff"], tol_solve_seconds=round(tsolve, 4),
                    tol_solve_mlups=round(pts * (st["iters"] if st["done"] else st["it"]) / tsolve / 1e6, 1),
-                   tol_time_capped=capped)
+                   tol_time_capped=capped, l2_error=err["l2_error"], max_error=err["max_error"],
+                   max_w=err["max_w"], tol_note=TOL_NOTE)
 
     phases = {}
-    if args.profile_phases > 0 and not dry and hasattr(runner, "profile"):
+    if args.profile_phases > 0 and not dry:
+        watch.phase("profile", 300)
         ph = runner.profile(args.profile_phases)
-        phases = {"phase_seconds_per_iter_max_over_ranks": {k: v / args.profile_phases for k, v in ph.items()}}
+        phases = {"phase_seconds_per_iter_max_over_ranks": {k: v / args.profile_phases for k, v in ph.items()},
+                  "phase_note": "compute = the whole fused sweep (A p, update, D^-1, A z); dot = the device "
+                                "reduction; comm = all-reduce + ghost exchange; copy and precond are 0 by "
+                                "construction (no host staging, D^-1 fused into the sweep)"}
         if info.rank == 0:
             print(f"[bench] {args.profile_phases} profiled iterations (MAX over {world} ranks):\n"
                   + ds.phase_table(ph), file=sys.stderr, flush=True)
 
+    watch.phase("report", 120)
     if info.rank == 0:
         out = {
             "metric": METRIC,
@@ -298,23 +565,50 @@ def main():
                 "process_grid": list(process_grid(world, args.M, args.N, args.split)),
                 "grid": [args.M, args.N],
                 "comm": comm_used,
+                "rung": rung if world > 1 else None,
+                "rccl_graph": bool(comm_used == "rccl" and cfg["rccl_graph"]),
+                "split_sweep": bool(getattr(runner, "split_sweep", False)),
                 "kernel": args.kernel,
                 "tile": tile_desc,
                 "graph_batch": args.graph_batch,
                 "overlap": args.overlap,
                 "exact": args.exact,
             },
+            "timed_path": timed_path,
+            "timed_graph_lengths": path.get("graph_lengths", []),
+            "timed_graph_iters": path["graph_iters"],
+            "timed_eager_iters": path["eager_iters"],
+            "graphs_prepared": bool(prepared),
             "valid": valid and not share,
             "baseline_mlups": BASELINE_MLUPS,
             **tol,
             **phases,
         }
         line = json.dumps(out)
-        print(line, flush=True)
-        if args.json_out:
-            with open(args.json_out, "w") as f:
+        result = os.environ.get("PMX_BENCH_RESULT")
+        if supervised and result:
+            with open(result, "w") as f:
                 f.write(line + "\n")
+        else:
+            print(line, flush=True)
+            if args.json_out:
+                with open(args.json_out, "w") as f:
+                    f.write(line + "\n")
+    watch.phase("shutdown", 120)
     launch.shutdown()
+    return 0
+
+
+def main():
+    args = parse()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if os.environ.get("PMX_BENCH_ROLE") != "child" and args.gpus > 1:
+        sys.exit(supervise(args))
+    if os.environ.get("PMX_BENCH_ROLE") != "child" and int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        raise SystemExit(f"[bench] --gpus {args.gpus} but {os.environ.get('WORLD_SIZE')} rank(s) came up "
+                         "(WORLD_SIZE); refusing to report a different GPU count")
+    sys.exit(measure(args))
 
 
 if __name__ == "__main__":

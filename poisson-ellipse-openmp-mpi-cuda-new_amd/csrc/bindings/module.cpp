@@ -67,6 +67,14 @@ py::dict state_dict(const PcgState& st) {
   return d;
 }
 
+py::dict error_dict(const ErrorStats& e) {
+  py::dict d;
+  d["sum_e2"] = e.sum_e2;
+  d["max_error"] = e.max_e;
+  d["max_w"] = e.max_w;
+  return d;
+}
+
 py::dict stats_dict(const RunStats& r) {
   py::dict d;
   d["iters"] = r.iters;
@@ -282,7 +290,7 @@ PYBIND11_MODULE(_pmx, m) {
   // algorithm is resolved exactly as the solver will (options + environment + device size), so
   // pass the returned "algo" on to SubdomainSolver(algo=...).
   m.def("comm_layout", [](const ProblemSpec& s, int Px, int Py, int rank, const std::string& dtype,
-                          const std::string& kernel, bool exact, int device, int algo) {
+                          const std::string& kernel, bool exact, int device, int algo, int sharing) {
           GpuOptions o = make_options(device, kernel, 256, 0, 4, 0, dtype, exact, 0, false);
           o.algo = algo;
           o = resolve_options(o);
@@ -294,11 +302,31 @@ PYBIND11_MODULE(_pmx, m) {
             total = double(tb);
           }
           const ProcGrid g{Px, Py};
-          const bool sp = choose_single_pass(s, g, o, total, 1);
+          const bool sp = choose_single_pass(s, g, o, total, std::max(1, sharing));
           const Subdomain sd = decompose_2d(s.M, s.N, g, rank);
           return layout_dict(GpuSubdomainSolver::comm_layout(sd, o.dtype, sp));
         }, py::arg("spec"), py::arg("Px"), py::arg("Py"), py::arg("rank"), py::arg("dtype") = "fp64",
-        py::arg("kernel") = "wave", py::arg("exact") = false, py::arg("device") = 0, py::arg("algo") = -1);
+        py::arg("kernel") = "wave", py::arg("exact") = false, py::arg("device") = 0, py::arg("algo") = -1,
+        py::arg("sharing") = 1);
+  m.def("record_comm_sequence", [](const ProblemSpec& s, int world, Split split, int graph_batch, int64_t iters,
+                                   const std::string& dtype, int device) {
+          GpuOptions o = make_options(device, "wave", 256, 0, 4, 0, dtype, false, graph_batch, false);
+          std::vector<std::vector<CommEvent>> logs;
+          {
+            py::gil_scoped_release nogil;
+            HIP_CHECK(hipSetDevice(device));
+            logs = record_comm_sequence(s, world, split, o, iters);
+          }
+          py::list out;
+          for (auto& l : logs) {
+            py::list r;
+            for (auto& e : l) r.append(py::make_tuple(e.comm, e.op, e.count, e.peer));
+            out.append(r);
+          }
+          return out;
+        }, py::arg("spec"), py::arg("world"), py::arg("split") = Split::kAuto, py::arg("graph_batch") = 4,
+        py::arg("iters") = 8, py::arg("dtype") = "fp64", py::arg("device") = 0,
+        "every rank's communication calls on a recording comm (init + iters iterations, captured when graph_batch > 0)");
   m.def("max_square_grid", [](double bytes_per_gpu, int gpus, const std::string& dtype, double reserve) {
     return max_square_grid(bytes_per_gpu, gpus, dtype == "fp64" ? DType::kFp64 : DType::kFp32, reserve);
   }, py::arg("bytes_per_gpu"), py::arg("gpus"), py::arg("dtype") = "fp64", py::arg("reserve") = 0.1);
@@ -350,6 +378,11 @@ PYBIND11_MODULE(_pmx, m) {
       })
       .def("download_field", [](GpuSubdomainSolver& g, int which, uintptr_t s) {
         return to_numpy(g.download_field(which, as_stream(s)), {g.sd().nx + 2, g.sd().ny + 2});
+      })
+      .def("error_norms", [](GpuSubdomainSolver& g, uintptr_t s) {
+        ErrorStats e;
+        { py::gil_scoped_release nogil; e = g.error_norms(as_stream(s)); }
+        return error_dict(e);
       })
       .def("layout", [](GpuSubdomainSolver& g) { return layout_dict(g.layout()); })
       .def("subdomain", [](GpuSubdomainSolver& g) { return sd_dict(g.sd()); })
@@ -431,7 +464,34 @@ PYBIND11_MODULE(_pmx, m) {
              { py::gil_scoped_release g; r = s.profile(n); }
              return stats_dict(r);
            })
-      .def("state", [](Session& s, int i) { return state_dict(s.state(i)); }, py::arg("i") = 0)
+      .def("state", [](Session& s, int i) {
+             PcgState st;
+             { py::gil_scoped_release g; st = s.state(i); }  // blocks on the device: a watchdog thread must run
+             return state_dict(st);
+           }, py::arg("i") = 0)
+      .def("prepare", [](Session& s, int64_t n) { py::gil_scoped_release g; return s.prepare(n); },
+           "capture every graph step(n) would replay now (no execution); False if graphs are off")
+      .def("step_eager", [](Session& s, int64_t n) { py::gil_scoped_release g; s.step_eager(n); })
+      .def("path_stats", [](Session& s) {
+             const PcgDriver::PathStats p = s.path_stats();
+             py::dict d;
+             d["graph_iters"] = p.graph_iters;
+             d["eager_iters"] = p.eager_iters;
+             d["graph_lengths"] = p.graph_lengths;
+             return d;
+           })
+      .def("reset_path_stats", &Session::reset_path_stats)
+      .def_property_readonly("split_sweep", &Session::split_sweep)
+      .def("progress", [](Session& s, int i) {
+             long long v[3];
+             s.progress(i, v);  // host memory only: callable while another thread blocks in the session
+             return py::make_tuple(v[0], v[1], v[2]);
+           }, py::arg("i") = 0)
+      .def("error_norms", [](Session& s) {
+             ErrorStats e;
+             { py::gil_scoped_release g; e = s.error_norms(); }
+             return error_dict(e);
+           })
       .def("bench_kernel", [](Session& s, int which, int abl, int reps) {
              py::gil_scoped_release g;
              s.synchronize();

@@ -17,6 +17,7 @@
 //  * SelfComm  — P = 1.
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <cstring>
 #include <sstream>
 
@@ -97,8 +98,10 @@ class LocalComm final : public Comm {
 // issues them); the send/recv pairs of its halo slots still form one group.
 class RcclRankView final : public Comm {
  public:
-  RcclRankView(ncclComm_t comm, ncclComm_t halo_comm, int nranks, bool capturable)
-      : comm_(comm), halo_comm_(halo_comm), nranks_(nranks), capturable_(capturable) {}
+  RcclRankView(ncclComm_t comm, ncclComm_t halo_comm, int nranks, bool capturable, Comm* owner)
+      : comm_(comm), halo_comm_(halo_comm), nranks_(nranks), capturable_(capturable), owner_(owner) {}
+  void abort() override { owner_->abort(); }  // every rank view of the process shares the fate
+  bool prefers_split() const override { return true; }
   void allreduce(std::vector<GpuSubdomainSolver*>& local, int which,
                  std::vector<hipStream_t>& streams) override {
     PMX_CHECK(local.size() == 1, "a rank view drives one subdomain");
@@ -134,6 +137,7 @@ class RcclRankView final : public Comm {
   ncclComm_t comm_, halo_comm_;
   int nranks_;
   bool capturable_;
+  Comm* owner_;
 };
 
 class RcclComm final : public Comm {
@@ -168,9 +172,16 @@ class RcclComm final : public Comm {
     RCCL_CHECK(ncclGroupEnd());
   }
   ~RcclComm() override {
+    if (aborted_.load()) return;  // ncclCommAbort already released them
     for (auto c : halo_comms_) (void)ncclCommDestroy(c);
     for (auto c : comms_) (void)ncclCommDestroy(c);
   }
+  void abort() override {
+    if (aborted_.exchange(true)) return;
+    for (auto c : halo_comms_) (void)ncclCommAbort(c);
+    for (auto c : comms_) (void)ncclCommAbort(c);
+  }
+  bool prefers_split() const override { return true; }
 
   void allreduce(std::vector<GpuSubdomainSolver*>& local, int which,
                  std::vector<hipStream_t>& streams) override {
@@ -201,7 +212,7 @@ class RcclComm final : public Comm {
   bool graph_capturable() const override { return capturable_; }
   std::unique_ptr<Comm> rank_view(int i) override {
     PMX_CHECK(i >= 0 && i < int(comms_.size()), "rank view index");
-    return std::make_unique<RcclRankView>(comms_[size_t(i)], halo_comms_[size_t(i)], nranks_, capturable_);
+    return std::make_unique<RcclRankView>(comms_[size_t(i)], halo_comms_[size_t(i)], nranks_, capturable_, this);
   }
   void check_health() override {
     for (auto* v : {&comms_, &halo_comms_})
@@ -221,11 +232,44 @@ class RcclComm final : public Comm {
   bool capturable_;
   std::vector<ncclComm_t> comms_;       // scalar all-reduces (compute stream)
   std::vector<ncclComm_t> halo_comms_;  // ghost exchange (comm stream when overlapped)
+  std::atomic<bool> aborted_{false};
+};
+
+// See make_recording_comm.
+class RecordingComm final : public Comm {
+ public:
+  RecordingComm(std::vector<CommEvent>* log, int world) : log_(log), world_(world) {}
+  void allreduce(std::vector<GpuSubdomainSolver*>& local, int which, std::vector<hipStream_t>&) override {
+    PMX_CHECK(local.size() == 1, "a recording comm stands for one rank");
+    log_->push_back({0, "allreduce", GpuSubdomainSolver::reduce_len(which), -1});
+  }
+  void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>&) override {
+    PMX_CHECK(local.size() == 1, "a recording comm stands for one rank");
+    const CommLayout& L = local[0]->layout();
+    log_->push_back({1, "group_start", 0, -1});
+    for (int slot = 0; slot < kHaloSlots; ++slot) {  // the order RcclComm::halo issues them
+      if (!L.active(slot)) continue;
+      log_->push_back({1, "send", L.edge_len[slot], L.peer[slot]});
+      log_->push_back({1, "recv", L.edge_len[slot], L.peer[slot]});
+    }
+    log_->push_back({1, "group_end", 0, -1});
+  }
+  bool prefers_split() const override { return true; }
+  std::string name() const override { return "recording"; }
+  int world_size() const override { return world_; }
+
+ private:
+  std::vector<CommEvent>* log_;
+  int world_;
 };
 
 }  // namespace
 
 std::unique_ptr<Comm> make_self_comm() { return std::make_unique<SelfComm>(); }
+
+std::unique_ptr<Comm> make_recording_comm(std::vector<CommEvent>* log, int world) {
+  return std::make_unique<RecordingComm>(log, world);
+}
 
 std::unique_ptr<Comm> make_local_comm(std::vector<GpuSubdomainSolver*>& local) {
   return std::make_unique<LocalComm>(local);

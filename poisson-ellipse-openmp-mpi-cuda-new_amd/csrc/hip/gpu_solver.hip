@@ -5,6 +5,7 @@
 // cudaDeviceSynchronize, 3x256-KiB partial D2H copies with host summation, host-staged halos.
 // Here per iteration: 4 launches (2 streaming + 2 single-block reductions), zero host syncs,
 // replayed from a hipGraph in batches.
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -95,6 +96,7 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_PCG1_PF", o.pf1);
   env_int("PMX_PCG1_ORDER", o.order1);
   env_int("PMX_PCG1_WCYCLE", o.wcycle1);
+  env_int("PMX_PROGRESS", o.progress);
   PMX_CHECK(o.wcycle1 == 2 || o.wcycle1 == 3, "pcg1 w cycle must be 2 or 3");
   PMX_CHECK(o.pair_w >= 0 && o.pair_w <= 2, "pair_w must be 0, 1 or 2");
   PMX_CHECK(o.algo == -1 || o.algo == 1 || o.algo == 2, "algo must be -1, 1 or 2");
@@ -257,6 +259,63 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   HIP_CHECK(hipMemset(arena_, 0, layout_.bytes));
   state_ = reinterpret_cast<PcgState*>(arena_ + layout_.state_off);
   HIP_CHECK(hipHostMalloc(&host_state_, 2 * sizeof(PcgState), hipHostMallocDefault));
+  if (opt_.progress) {
+    HIP_CHECK(hipHostMalloc(&progress_host_, 64, hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(progress_host_, 0, 64);
+    void* d = nullptr;
+    HIP_CHECK(hipHostGetDevicePointer(&d, progress_host_, 0));
+    progress_dev_ = static_cast<long long*>(d);
+  }
+}
+
+void GpuSubdomainSolver::progress(long long out[3]) const {
+  for (int q = 0; q < 3; ++q)
+    out[q] = progress_host_ ? __atomic_load_n(progress_host_ + q, __ATOMIC_RELAXED) : -1;
+}
+
+ErrorStats GpuSubdomainSolver::error_norms(hipStream_t s) const {
+  HIP_CHECK(hipSetDevice(opt_.device));
+  const PcgState st = read_state(s);
+  // pending w steps, exactly as download_w applies them
+  const void* pp[2] = {nullptr, nullptr};
+  double a[2] = {0.0, 0.0};
+  int npend = 0;
+  if (pcg1_ && st.w_pend_n > 0 && st.w_pend > 0) {
+    npend = st.w_pend_n;
+    for (int q = 0; q < npend; ++q) {
+      const long long j = st.w_pend - (npend - 1) + q;
+      pp[q] = field_base((j & 1) ? 3 : 2);
+      a[q] = st.alpha1[j & 3];
+    }
+  } else if (!pcg1_ && st.w_pend > 0) {
+    npend = 1;
+    pp[0] = field_base((st.w_pend & 1) ? 3 : 2);
+    a[0] = st.alpha[st.w_pend & 1];
+  }
+  constexpr int kMaxBlocks = 1024;
+  double* d_out = nullptr;
+  HIP_CHECK(hipMalloc(&d_out, 3 * kMaxBlocks * sizeof(double)));
+  int nb = 0;
+  if (elem_ == 8)
+    nb = launch_error_norms<double>(geom_, tables_, static_cast<const double*>(field_base(0)),
+                                    static_cast<const double*>(pp[0]), a[0], static_cast<const double*>(pp[1]),
+                                    a[1], npend, d_out, kMaxBlocks, s);
+  else
+    nb = launch_error_norms<float>(geom_, tables_, static_cast<const float*>(field_base(0)),
+                                   static_cast<const float*>(pp[0]), a[0], static_cast<const float*>(pp[1]),
+                                   a[1], npend, d_out, kMaxBlocks, s);
+  std::vector<double> h(3 * size_t(nb));
+  HIP_CHECK(hipMemcpyAsync(h.data(), d_out, h.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  HIP_CHECK(hipFree(d_out));
+  ErrorStats e;
+  e.max_w = -HUGE_VAL;
+  for (int b = 0; b < nb; ++b) {  // block order: deterministic
+    e.sum_e2 += h[3 * size_t(b)];
+    e.max_e = std::max(e.max_e, h[3 * size_t(b) + 1]);
+    e.max_w = std::max(e.max_w, h[3 * size_t(b) + 2]);
+  }
+  return e;
 }
 
 void GpuSubdomainSolver::release() noexcept {
@@ -269,6 +328,8 @@ void GpuSubdomainSolver::release() noexcept {
   if (partials_) (void)hipFree(partials_);
   if (own_arena_ && arena_) (void)hipFree(arena_);
   if (host_state_) (void)hipHostFree(host_state_);
+  if (progress_host_) (void)hipHostFree(progress_host_);
+  progress_host_ = progress_dev_ = nullptr;
   fields_ = r2_ = nullptr;
   arena_ = nullptr;
   tables_buf_ = partials_ = nullptr;
@@ -355,6 +416,9 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
   st.pair_min_beta = opt_.pair_w == 2 ? HUGE_VAL : 1e-3;
   st.w_cycle = w_cycle();
   host_k_ = st.it;
+  if (progress_host_) {  // the device has finished with them: init follows a synchronised state
+    for (int q = 0; q < 3; ++q) __atomic_store_n(progress_host_ + q, 0LL, __ATOMIC_RELAXED);
+  }
   HIP_CHECK(hipMemcpyAsync(state_, &st, sizeof(PcgState), hipMemcpyHostToDevice, s));
   T* w = static_cast<T*>(field_base(0));
   T* r = static_cast<T*>(field_base(1));
@@ -371,7 +435,7 @@ template <typename T>
 void GpuSubdomainSolver::halo_impl(hipStream_t s, bool unpack) {
   launch_pcg1_halo<T>(geom_, static_cast<T*>(field_base(1)), reinterpret_cast<T*>(r2_ + field_off_ * elem_),
                       static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(), state_,
-                      unpack, s);
+                      unpack, s, progress_dev_);
   after_launch(s);
 }
 
@@ -454,7 +518,7 @@ void GpuSubdomainSolver::enqueue_reduce_a(hipStream_t s) {
     const double h = g_.h1h2, wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
     const double wts[5] = {h, h, h, h, wdiff};
     launch_reduce_n(partials_, tiles1_.ntiles(), 5, wts, state_->red_c, state_, kSkipIfDone | kBumpIter,
-                    reduce_ws_, s);
+                    reduce_ws_, s, progress_dev_);
     ++host_k_;  // mirrors the S->it bump (see host_k())
     after_launch(s);
     return;
@@ -728,7 +792,7 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
   // extra launch (16384^2 as 2x2 subdomains on one GPU: 2.647 vs 2.602 ms; 2 strips: 2.416 vs
   // 2.430).  PMX_PCG1_SPLIT=0/1 forces it.
   const char* sp = std::getenv("PMX_PCG1_SPLIT");
-  const bool split_default = comm_->name() == "rccl";
+  const bool split_default = comm_->prefers_split();
   split_ = overlap_ && single_pass_ && (sp && sp[0] ? sp[0] == '1' : split_default);
   if (split_) {
     auto ev = [](std::vector<hipEvent_t>& v) {
@@ -960,64 +1024,109 @@ void PcgDriver::advance_host_k(long long n) {
   for (auto* s : local_) s->set_host_k(s->host_k() + n);
 }
 
-// Captures graph_batch_ iterations starting at w-cycle phase `phase` (the phase of the host
-// iteration counter now).  The capture enqueues nothing for execution, so the host counters are
-// restored afterwards; each launch of the graph advances them by graph_batch_.
-void PcgDriver::build_graph(int phase) {
+// Captures `len` iterations starting at w-cycle phase `phase` (the phase of the host iteration
+// counter now).  The capture enqueues nothing for execution, so the host counters are restored
+// afterwards; each launch of the graph advances them by `len`.
+hipGraphExec_t PcgDriver::build_graph(int phase, int len) {
   TraceRange tr("pmx:build_graph");
-  graph_ok_ = false;
+  (void)phase;
   bool single_stream = true;
   for (auto s : streams_) single_stream &= s == streams_[0];
-  if (graph_batch_ <= 0 || !single_stream || !comm_->graph_capturable()) return;
+  if (graph_batch_ <= 0 || len <= 0 || !single_stream || !comm_->graph_capturable()) return nullptr;
   for (auto* s : local_)
-    if (s->options().check) return;
+    if (s->options().check) return nullptr;
   HIP_CHECK(hipSetDevice(local_[0]->device()));
   hipGraph_t g = nullptr;
   if (hipStreamBeginCapture(streams_[0], hipStreamCaptureModeThreadLocal) != hipSuccess) {
     (void)hipGetLastError();
-    return;
+    return nullptr;
   }
   std::vector<long long> k0;
   for (auto* s : local_) k0.push_back(s->host_k());
-  for (int k = 0; k < graph_batch_; ++k) enqueue_one_iteration();
+  PMX_CHECK(!halo_pending_, "graph capture with an unjoined ghost exchange");
+  for (int k = 0; k < len; ++k) enqueue_one_iteration();
   join_halo();  // a captured batch is self-contained: every forked stream rejoins
   for (size_t i = 0; i < local_.size(); ++i) local_[i]->set_host_k(k0[i]);
   if (hipStreamEndCapture(streams_[0], &g) != hipSuccess || !g) {
     (void)hipGetLastError();
-    return;
+    return nullptr;
   }
   hipGraphExec_t e = nullptr;
   if (hipGraphInstantiate(&e, g, nullptr, nullptr, 0) != hipSuccess) {
     (void)hipGetLastError();
     (void)hipGraphDestroy(g);
-    return;
+    return nullptr;
   }
   graphs_.push_back(g);
   execs_.push_back(e);
-  exec_by_phase_[size_t(phase)] = e;
-  graph_ok_ = true;
+  return e;
+}
+
+hipGraphExec_t PcgDriver::graph_for(int phase, int len) {
+  if (graph_batch_ <= 0 || graph_failed_) return nullptr;
+  const auto key = std::make_pair(phase, len);
+  auto it = exec_by_key_.find(key);
+  if (it != exec_by_key_.end()) return it->second;
+  hipGraphExec_t e = build_graph(phase, len);
+  if (!e) {
+    graph_failed_ = true;  // not capturable (multi-stream, comm, check mode): eager from now on
+    return nullptr;
+  }
+  exec_by_key_[key] = e;
+  return e;
+}
+
+void PcgDriver::note_graph(int len) {
+  path_.graph_iters += len;
+  auto& v = path_.graph_lengths;
+  if (std::find(v.begin(), v.end(), len) == v.end()) v.push_back(len);
+}
+
+bool PcgDriver::prepare(int64_t n) {
+  TraceRange tr("pmx:prepare");
+  const int cyc = local_[0]->w_cycle();
+  std::vector<long long> k0;
+  for (auto* s : local_) k0.push_back(s->host_k());
+  bool ok = graph_batch_ > 0 && !graph_failed_;
+  int64_t done = 0;
+  auto at = [&](int64_t off) {  // host counters as they will be `off` iterations from now
+    for (size_t i = 0; i < local_.size(); ++i) local_[i]->set_host_k(k0[i] + off);
+  };
+  while (ok && done + graph_batch_ <= n) {
+    at(done);
+    ok = graph_for(int((k0[0] + done) % cyc), graph_batch_) != nullptr;
+    done += graph_batch_;
+  }
+  if (ok && done < n) {
+    at(done);
+    ok = graph_for(int((k0[0] + done) % cyc), int(n - done)) != nullptr;
+  }
+  at(0);
+  return ok;
+}
+
+void PcgDriver::enqueue_eager(int64_t n) {
+  for (int64_t k = 0; k < n; ++k) enqueue_one_iteration();
+  path_.eager_iters += n;
+  join_halo();
 }
 
 void PcgDriver::enqueue_iterations(int64_t n) {
   TraceRange tr("pmx:enqueue_iterations");
   const int cyc = local_[0]->w_cycle();
   for (auto* s : local_) PMX_CHECK(s->host_k() == local_[0]->host_k(), "local solvers out of step");
-  if (exec_by_phase_.empty()) exec_by_phase_.assign(size_t(cyc), nullptr);
   int64_t done = 0;
-  while (graph_batch_ > 0 && !graph_failed_ && done + graph_batch_ <= n) {
-    const int ph = int(local_[0]->host_k() % cyc);
-    if (!exec_by_phase_[size_t(ph)]) {
-      build_graph(ph);
-      if (!graph_ok_) {
-        graph_failed_ = true;  // not capturable (multi-stream, comm, check mode): eager from now on
-        break;
-      }
-    }
-    HIP_CHECK(hipGraphLaunch(exec_by_phase_[size_t(ph)], streams_[0]));
-    advance_host_k(graph_batch_);
-    done += graph_batch_;
+  while (done < n) {
+    const int len = int(std::min<int64_t>(graph_batch_, n - done));
+    hipGraphExec_t e = len > 0 ? graph_for(int(local_[0]->host_k() % cyc), len) : nullptr;
+    if (!e) break;
+    HIP_CHECK(hipGraphLaunch(e, streams_[0]));
+    advance_host_k(len);
+    note_graph(len);
+    done += len;
   }
-  for (; done < n; ++done) enqueue_one_iteration();
+  for (int64_t k = done; k < n; ++k) enqueue_one_iteration();
+  path_.eager_iters += n - done;
   join_halo();
 }
 

@@ -5,7 +5,9 @@
 // CDNA-friendly mapping: threadIdx.x runs along the contiguous axis lj (the reference maps it to
 // the strided li axis, :514-515), and coefficients come from the 1D face tables.  Used by the
 // unit tests (each op vs a PyTorch fp64 reference) and by the solver's `naive` kernel mode.
+#include <algorithm>
 #include <climits>
+#include <cmath>
 
 #include "pcg_device.hpp"
 #include "pmx/common.hpp"
@@ -71,6 +73,75 @@ k_dot_partials(DevGeom G, const T* __restrict__ x, const T* __restrict__ y, doub
   block_sum2<256>(s, unused, lds);
   if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
+
+// Error of the solution against the analytic u = F (1 - x^2/ax^2 - y^2/by^2) / (2/ax^2 + 2/by^2)
+// inside D (итоговый отчёт/Этап_4_1213.pdf p.1: (1 - x^2 - 4y^2)/10; the reference never computes
+// it).  w_eff = w + sum_q c_q p_q applies the single-pass solver's pending w steps (see
+// GpuSubdomainSolver::download_w) without moving w to the host.  Per block: sum of e^2 over the
+// owned nodes in D, max |e| in D, max w_eff; the caller finishes on the host (and over ranks).
+template <typename T>
+__global__ void __launch_bounds__(256)
+k_error_norms(DevGeom G, DevTables Tb, const T* __restrict__ w, const T* __restrict__ pa, double ca,
+              const T* __restrict__ pb, double cb, int npend, double* out) {
+  __shared__ double lds[3][256 / kWave];
+  const double den = 2.0 / (G.ax * G.ax) + 2.0 / (G.by * G.by);  // as geo::exact_solution
+  double se = 0.0, me = 0.0, mw = -HUGE_VAL;
+  const int64_t n = int64_t(G.nx) * G.ny;
+  for (int64_t k = int64_t(blockIdx.x) * 256 + threadIdx.x; k < n; k += int64_t(gridDim.x) * 256) {
+    const int li = int(k / G.ny) + 1, lj = int(k % G.ny) + 1;
+    const int64_t c = li * G.pitch + lj;
+    double v = double(w[c]);
+    if (npend > 0) v = __builtin_fma(ca, double(pa[c]), v);
+    if (npend > 1) v = __builtin_fma(cb, double(pb[c]), v);
+    if (npend > 0 && sizeof(T) == 4) v = double(static_cast<float>(v));
+    mw = fmax(mw, v);
+    const double x = Tb.x[G.gi0 + li], y = Tb.y[G.gj0 + lj];
+    if (geo::inside(x, y, G.ax, G.by, G.ref_ellipse != 0)) {
+      const double u = x / G.ax, t = y / G.by;
+      const double q = 1.0 - u * u - t * t;
+      const double e = v - (q > 0.0 ? G.F * q / den : 0.0);
+      se = __builtin_fma(e, e, se);
+      me = fmax(me, fabs(e));
+    }
+  }
+  se = wave_sum_mfma(se);
+  for (int o = 32; o >= 1; o >>= 1) {
+    me = fmax(me, __shfl_xor(me, o));
+    mw = fmax(mw, __shfl_xor(mw, o));
+  }
+  const int wid = threadIdx.x / kWave;
+  if ((threadIdx.x % kWave) == 0) {
+    lds[0][wid] = se;
+    lds[1][wid] = me;
+    lds[2][wid] = mw;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0, b = 0.0, m = -HUGE_VAL;
+    for (int q = 0; q < 256 / kWave; ++q) {
+      a += lds[0][q];
+      b = fmax(b, lds[1][q]);
+      m = fmax(m, lds[2][q]);
+    }
+    out[3 * blockIdx.x] = a;
+    out[3 * blockIdx.x + 1] = b;
+    out[3 * blockIdx.x + 2] = m;
+  }
+}
+
+template <typename T>
+int launch_error_norms(const DevGeom& G, const DevTables& Tb, const T* w, const T* pa, double ca,
+                       const T* pb, double cb, int npend, double* out, int max_blocks, hipStream_t s) {
+  const int64_t n = int64_t(G.nx) * G.ny;
+  const int nb = int(std::max<int64_t>(1, std::min<int64_t>(max_blocks, (n + 255) / 256)));
+  hipLaunchKernelGGL((k_error_norms<T>), dim3(nb), dim3(256), 0, s, G, Tb, w, pa, ca, pb, cb, npend, out);
+  HIP_CHECK(hipGetLastError());
+  return nb;
+}
+template int launch_error_norms<double>(const DevGeom&, const DevTables&, const double*, const double*,
+                                        double, const double*, double, int, double*, int, hipStream_t);
+template int launch_error_norms<float>(const DevGeom&, const DevTables&, const float*, const float*, double,
+                                       const float*, double, int, double*, int, hipStream_t);
 
 // MFMA wave reductions (pcg_device.hpp) on arbitrary data, for the unit tests: per wave64 of x,
 // out[3w] = sum x, out[3w+1] = sum x (packed pair), out[3w+2] = sum x^2 (packed pair)

@@ -579,10 +579,16 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
 // 4 = (field, line)).  Tiny and stream-ordered; launched by the driver between two sweeps.
 template <typename T>
 __global__ void __launch_bounds__(256)
-k_pcg1_halo(DevGeom G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, PcgState* S, int unpack) {
+k_pcg1_halo(DevGeom G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, PcgState* S, int unpack,
+            long long* progress) {
   const int slot = blockIdx.y;
-  if (!unpack && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0)
-    S->halo_k_unpack = S->halo_k;  // see PcgState::halo_k_unpack
+  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0) {
+    if (!unpack) S->halo_k_unpack = S->halo_k;  // see PcgState::halo_k_unpack
+    // host-visible progress (hang diagnosis): [1] = exchanges packed, [2] = exchanges unpacked
+    if (progress)
+      __hip_atomic_store(progress + (unpack ? 2 : 1), (unpack ? S->halo_k_unpack : S->halo_k) + 1,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   if (!((G.nb >> slot) & 1)) return;
   const int f = blockIdx.z >> 1, q = blockIdx.z & 1;
   const int t = blockIdx.x * 256 + threadIdx.x;
@@ -623,7 +629,7 @@ struct ReduceWeights {
 template <int NQ>
 __global__ void __launch_bounds__(256)
 k_reduce_n(const double* __restrict__ part, int n, ReduceWeights wt, double* out, PcgState* S,
-           int mode, double* chunk, unsigned* ticket) {
+           int mode, double* chunk, unsigned* ticket, long long* progress) {
   __shared__ double lds[NQ][256 / kWave];
   __shared__ int last;
   if ((mode & kSkipIfDone) && S->done) return;
@@ -668,6 +674,8 @@ k_reduce_n(const double* __restrict__ part, int n, ReduceWeights wt, double* out
     for (int q = 0; q < NQ; ++q) out[q] = t[q] * wt.w[q];
     if (bad) S->nan_flag = 1;
     if (mode & kBumpIter) S->it += 1;
+    // host-visible progress (hang diagnosis): [0] = sweeps reduced (the device iteration counter)
+    if (progress) __hip_atomic_store(progress, S->it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     *ticket = 0u;  // re-arm for the next launch (stream order makes this visible to it)
   }
 }
@@ -825,16 +833,16 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
 
 template <typename T>
 void launch_pcg1_halo(const DevGeom& G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, PcgState* S,
-                      bool unpack, hipStream_t s) {
+                      bool unpack, hipStream_t s, long long* progress) {
   if (G.nb == 0) return;
   const int len = std::max(G.nx, G.ny);
   hipLaunchKernelGGL(k_pcg1_halo<T>, dim3((len + 255) / 256, kHaloSlots, 4), dim3(256), 0, s, G, r, r2,
-                     p0, p1, H, S, unpack ? 1 : 0);
+                     p0, p1, H, S, unpack ? 1 : 0, progress);
   HIP_CHECK(hipGetLastError());
 }
 
 void launch_reduce_n(const double* partials, int n, int nq, const double* weights, double* out,
-                     PcgState* S, int mode, double* ws, hipStream_t s) {
+                     PcgState* S, int mode, double* ws, hipStream_t s, long long* progress) {
   PMX_CHECK(nq == kNq, "launch_reduce_n: nq must be " << kNq);
   // ~512 partials per block: the loads of a block are 2 rounds per thread, not a latency chain
   // (4096x8192 fp64: 22.9K tiles, 11 -> 44 blocks)
@@ -843,7 +851,8 @@ void launch_reduce_n(const double* partials, int n, int nq, const double* weight
   unsigned* ticket = reinterpret_cast<unsigned*>(chunk + 8 * kReduceMaxBlocks);
   ReduceWeights wt{};
   for (int q = 0; q < nq; ++q) wt.w[q] = weights[q];
-  hipLaunchKernelGGL(k_reduce_n<kNq>, dim3(nb), dim3(256), 0, s, partials, n, wt, out, S, mode, chunk, ticket);
+  hipLaunchKernelGGL(k_reduce_n<kNq>, dim3(nb), dim3(256), 0, s, partials, n, wt, out, S, mode, chunk, ticket,
+                     progress);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -861,9 +870,9 @@ void* pcg1_wave_trace_setup(long long it, int nwaves) {
 template void launch_pcg1<double>(const DevGeom&, const DevTables&, double*, double*, double*, double*,
                                   double*, double*, PcgState*, const TileCfg&, hipStream_t, int, bool);
 template void launch_pcg1_halo<double>(const DevGeom&, double*, double*, double*, double*, HaloBufs<double>,
-                                        PcgState*, bool, hipStream_t);
+                                        PcgState*, bool, hipStream_t, long long*);
 template void launch_pcg1_halo<float>(const DevGeom&, float*, float*, float*, float*, HaloBufs<float>,
-                                       PcgState*, bool, hipStream_t);
+                                       PcgState*, bool, hipStream_t, long long*);
 template void launch_pcg1<float>(const DevGeom&, const DevTables&, float*, float*, float*, float*, float*,
                                  double*, PcgState*, const TileCfg&, hipStream_t, int, bool);
 

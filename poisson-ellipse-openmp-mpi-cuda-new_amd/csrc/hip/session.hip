@@ -33,7 +33,10 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
 
   // one iteration algorithm for every subdomain (and every process: the choice only depends on
   // global data, see choose_single_pass)
-  GpuOptions base = resolve_options(cfg_.opt);
+  GpuOptions pre = cfg_.opt;
+  // a multi-process RCCL run tracks device progress for its hang watchdog (GpuOptions::progress)
+  if (cfg_.comm == CommKind::kRccl && cfg_.world > 1) pre.progress = 1;
+  GpuOptions base = resolve_options(pre);
   if (base.algo == -1) {
     HIP_CHECK(hipSetDevice(cfg_.devices[0]));
     size_t free_b = 0, total_b = 0;
@@ -104,8 +107,17 @@ void Session::for_drivers(const std::function<void(size_t, PcgDriver&)>& f) {
         HIP_CHECK(hipSetDevice(solvers_[i]->device()));
         f(i, *drivers_[i]);
       } catch (...) {
-        std::lock_guard<std::mutex> lk(mu);
-        if (!err) err = std::current_exception();
+        bool first = false;
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          if (!err) {
+            err = std::current_exception();
+            first = true;
+          }
+        }
+        // The other threads may be blocked on collectives this rank will never post: abort the
+        // communicator so they return with an error and the join below cannot hang.
+        if (first && comm_) comm_->abort();
       }
     });
   for (auto& t : th) t.join();
@@ -115,6 +127,51 @@ void Session::for_drivers(const std::function<void(size_t, PcgDriver&)>& f) {
 hipStream_t Session::stream_of(int i) const {
   require_connected();
   return threaded_ ? drivers_.at(size_t(i))->streams()[0] : drivers_[0]->streams().at(size_t(i));
+}
+
+bool Session::prepare(int64_t n) {
+  std::vector<char> ok(drivers_.size(), 0);
+  for_drivers([&](size_t i, PcgDriver& d) { ok[i] = d.prepare(n) ? 1 : 0; });
+  bool all = true;
+  for (char c : ok) all &= c != 0;
+  return all;
+}
+
+void Session::step_eager(int64_t n) {
+  for_drivers([n](size_t, PcgDriver& d) { d.enqueue_eager(n); });
+}
+
+PcgDriver::PathStats Session::path_stats() const {
+  require_connected();
+  PcgDriver::PathStats p = drivers_[0]->path_stats();
+  for (auto& d : drivers_)
+    PMX_CHECK(d->path_stats().graph_iters == p.graph_iters && d->path_stats().eager_iters == p.eager_iters,
+              "drivers disagree on the launch path");
+  return p;
+}
+
+void Session::reset_path_stats() {
+  for (auto& d : drivers_) d->reset_path_stats();
+}
+
+bool Session::split_sweep() const {
+  require_connected();
+  return drivers_[0]->split_sweep();
+}
+
+void Session::progress(int i, long long out[3]) const { solvers_.at(size_t(i))->progress(out); }
+
+ErrorStats Session::error_norms() {
+  synchronize();
+  ErrorStats t;
+  t.max_w = -HUGE_VAL;
+  for (size_t i = 0; i < solvers_.size(); ++i) {
+    const ErrorStats e = solvers_[i]->error_norms(stream_of(int(i)));
+    t.sum_e2 += e.sum_e2;
+    t.max_e = std::max(t.max_e, e.max_e);
+    t.max_w = std::max(t.max_w, e.max_w);
+  }
+  return t;
 }
 
 void Session::init() {
@@ -238,6 +295,31 @@ RunStats Session::solve_checkpointed(const std::string& save_path, int64_t every
   const bool resume = !resume_path.empty();
   if (resume) load_checkpoint(resume_path);
   return solve_impl(poll_batches, !resume, every, save_path);
+}
+
+std::vector<std::vector<CommEvent>> record_comm_sequence(const ProblemSpec& spec, int world, Split split,
+                                                         const GpuOptions& opt, int64_t iters) {
+  const ProcGrid pg = make_process_grid(world, spec.M, spec.N, split);
+  GpuOptions o = resolve_options(opt);
+  if (o.algo == -1) o.algo = choose_single_pass(spec, pg, o, 0.0, world) ? 1 : 2;
+  std::vector<std::unique_ptr<GpuSubdomainSolver>> solvers;
+  std::vector<std::vector<CommEvent>> logs(static_cast<size_t>(world));
+  std::vector<std::unique_ptr<Comm>> comms;
+  std::vector<std::unique_ptr<PcgDriver>> drivers;
+  for (int r = 0; r < world; ++r) {
+    solvers.push_back(std::make_unique<GpuSubdomainSolver>(spec, decompose_2d(spec.M, spec.N, pg, r), o));
+    comms.push_back(make_recording_comm(&logs[size_t(r)], world));
+    drivers.push_back(std::make_unique<PcgDriver>(std::vector<GpuSubdomainSolver*>{solvers.back().get()},
+                                                  comms.back().get(), o.graph_batch));
+  }
+  // each rank's driver on its own (nothing is exchanged; the values are garbage, the call
+  // sequence is what counts): init, then `iters` iterations -- captured when graph_batch > 0
+  for (auto& d : drivers) {
+    d->init();
+    d->enqueue_iterations(iters);
+    d->synchronize();
+  }
+  return logs;
 }
 
 int64_t max_square_grid(double bytes_per_gpu, int gpus, DType dtype, double reserve_fraction) {

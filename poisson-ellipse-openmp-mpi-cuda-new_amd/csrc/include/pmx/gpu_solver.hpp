@@ -17,6 +17,7 @@
 #include <cstdint>
 #include <functional>
 #include <iosfwd>
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -83,6 +84,11 @@ struct GpuOptions {
   // Triples recover p^{k-2} from p^{k-1} and r^{k-1} (one extra stencil), or re-read it when
   // |beta_{k-1}| < 1e-3 or pair_w == 2.  PMX_PCG1_WCYCLE=2|3 overrides.
   int wcycle1 = 3;
+  // Host-mapped progress counters written by the device (sweeps reduced, ghost exchanges packed /
+  // unpacked), readable without any HIP call -- how a hang watchdog tells which step a stuck rank
+  // is in.  One 8-B system-scope store per kernel; on for multi-rank RCCL sessions.  PMX_PROGRESS
+  // overrides.
+  int progress = 0;
   bool resolved = false;  // environment overrides already applied (resolve_options)
 };
 
@@ -96,6 +102,14 @@ bool choose_single_pass(const ProblemSpec& spec, const ProcGrid& grid, const Gpu
 
 // The comm arena: PcgState (the all-reduce buffers) and one send + one receive buffer per halo
 // slot (pmx/device_types.hpp kHaloSlots), all sends first, then all receives.
+// Error of the local solution against the analytic one (k_error_norms), before any reduction
+// over ranks: l2_error = sqrt(h1 h2 sum_e2) once summed over all ranks.
+struct ErrorStats {
+  double sum_e2 = 0.0;  // sum of (w - u)^2 over the owned nodes in D
+  double max_e = 0.0;   // max |w - u| over the owned nodes in D
+  double max_w = 0.0;   // max w over the owned nodes
+};
+
 struct CommLayout {
   size_t state_off = 0;          // PcgState
   size_t send_off[kHaloSlots] = {};
@@ -151,6 +165,13 @@ class GpuSubdomainSolver {
   void load_checkpoint(std::istream& is, hipStream_t s);
 
   PcgState read_state(hipStream_t s) const;  // synchronous D2H of the scalars
+  // device-side error norms of the current w (pending steps applied); synchronous
+  ErrorStats error_norms(hipStream_t s) const;
+  // host-mapped progress counters (GpuOptions::progress): sweeps reduced, ghost exchanges packed,
+  // exchanges unpacked.  Plain host reads, no HIP call: safe from a watchdog thread.  All -1 when
+  // progress tracking is off.
+  void progress(long long out[3]) const;
+  bool progress_enabled() const { return progress_dev_ != nullptr; }
   // Kernel isolation benchmark: pins the scalar state to a mid-solve iteration and launches
   // k_pcg_a (which=0) or k_pcg_b (which=1) alone `reps` times; returns ms per launch.  Leaves
   // the solver state invalid (call enqueue_init afterwards).
@@ -235,6 +256,8 @@ class GpuSubdomainSolver {
   int wtrace_n_ = 0;
 #endif
   PcgState* host_state_ = nullptr;  // pinned
+  long long* progress_host_ = nullptr;  // host-mapped, coherent (GpuOptions::progress)
+  long long* progress_dev_ = nullptr;   // its device address, or nullptr (off)
 };
 
 // ---------------------------------------------------------------------------
@@ -254,6 +277,12 @@ class Comm {
   virtual void check_health() {}
   virtual std::string name() const = 0;
   virtual int world_size() const = 0;
+  // The pcg1 split sweep is the default with this transport (its exchange is the long pole).
+  virtual bool prefers_split() const { return false; }
+  // Error path of a threaded driver set: make every operation in flight or blocked on this
+  // communicator return (RCCL: ncclCommAbort), so the other driver threads fail instead of
+  // waiting for a rank that will never post.  The communicator is unusable afterwards.
+  virtual void abort() {}
   // A communicator for local rank i alone, for a driver thread that owns just that rank (one host
   // thread per device).  Non-owning: valid while this communicator lives.
   virtual std::unique_ptr<Comm> rank_view(int i);
@@ -267,6 +296,19 @@ std::unique_ptr<Comm> make_rccl_comm(const std::string& unique_id, int nranks,
                                      const std::vector<int>& ranks, const std::vector<int>& devices,
                                      bool capturable);
 std::string rccl_unique_id();
+
+// One communication call as a rank's driver issued it (RecordingComm, tests): comm 0 = the
+// scalar communicator, 1 = the halo communicator; op "allreduce" (count = doubles), or a halo
+// group ("group_start", "send"/"recv" with element count and peer rank, "group_end").
+struct CommEvent {
+  int comm;
+  std::string op;
+  int count;
+  int peer;
+};
+// Records the calls instead of communicating (no data moves).  Mimics RCCL's driver defaults
+// (prefers_split), so a driver on it issues exactly the sequence it would issue on RCCL.
+std::unique_ptr<Comm> make_recording_comm(std::vector<CommEvent>* log, int world);
 
 struct RunStats {
   int64_t iters = 0;
@@ -305,13 +347,34 @@ class PcgDriver {
   std::vector<hipStream_t>& streams() { return streams_; }
   bool overlapped() const { return overlap_; }
   bool poisoned() const { return poison_; }
+  // pcg1 split sweep in use (interior tiles overlap the previous exchange, see enqueue_split_iteration)
+  bool split_sweep() const { return split_; }
+
+  // Which path ran: iterations replayed from captured graphs / enqueued as individual launches
+  // since the last reset, and the graph lengths used (bench.py reports them for its timed region).
+  struct PathStats {
+    int64_t graph_iters = 0, eager_iters = 0;
+    std::vector<int> graph_lengths;  // distinct lengths, in first-use order
+  };
+  const PathStats& path_stats() const { return path_; }
+  void reset_path_stats() { path_ = PathStats{}; }
+  // Capture -- without running anything -- every graph that enqueue_iterations(n) issued now would
+  // replay (full batches of graph_batch and the remainder), so a timed region replays graphs only
+  // and pays no capture.  False when this driver cannot capture (graph_batch 0, check mode, a
+  // non-capturable comm, several streams).
+  bool prepare(int64_t n);
+  // n iterations as individual launches, never from a graph (the bench's canary iteration)
+  void enqueue_eager(int64_t n);
 
  private:
   void enqueue_one_iteration();
   void halo_exchange_pcg1(std::vector<hipStream_t>& streams);  // pack -> comm -> unpack
   void enqueue_split_iteration();  // pcg1, decomposed, overlap: interior/frame sweep split
   void join_halo();                // compute stream waits for a pending ghost exchange
-  void build_graph(int phase);
+  // captured batch of `len` iterations starting at w-cycle phase `phase`, built on first use;
+  // nullptr when capture is impossible (graph_failed_ is then set)
+  hipGraphExec_t graph_for(int phase, int len);
+  hipGraphExec_t build_graph(int phase, int len);
   template <typename F> void for_each_stream(F&& f);
   void poison(std::vector<hipStream_t>& streams);
 
@@ -331,13 +394,14 @@ class PcgDriver {
   bool halo_pending_ = false;  // a ghost exchange on the comm stream not yet joined
   std::vector<hipStream_t> frame_streams_;
   std::vector<hipEvent_t> ev_ar_, ev_fdone_, ev_swept_, ev_pk_;
-  bool graph_ok_ = false;      // the last build_graph succeeded
   bool graph_failed_ = false;  // capture is not possible for this driver: eager launches
   std::vector<hipGraph_t> graphs_;
   std::vector<hipGraphExec_t> execs_;
-  // one captured batch per phase of the w cycle at its first sweep (pcg1 bakes the plain / w
-  // sweep kernel choice into the graph); nullptr = not built yet
-  std::vector<hipGraphExec_t> exec_by_phase_;
+  // captured batches by (phase of the w cycle at their first sweep, length): pcg1 bakes the plain /
+  // w sweep kernel choice into the graph
+  std::map<std::pair<int, int>, hipGraphExec_t> exec_by_key_;
+  PathStats path_;
+  void note_graph(int len);
   void advance_host_k(long long n);
 };
 

@@ -111,7 +111,7 @@ void* pcg1_wave_trace_setup(long long it, int nwaves);
 
 template <typename T>
 void launch_pcg1_halo(const DevGeom& G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, PcgState* S,
-                      bool unpack, hipStream_t s);
+                      bool unpack, hipStream_t s, long long* progress = nullptr);
 
 // Halo/compute overlap: r^{k+1} on the subdomain edges that have a neighbour,
 // written to the send buffers only, with exactly the arithmetic of pcg_b.  Runs first so the
@@ -130,9 +130,11 @@ constexpr int kReduceNOffset = 2 * kReduceMaxBlocks + 2;
 constexpr int kReduceWsDoubles = kReduceNOffset + 8 * kReduceMaxBlocks + 2;
 void launch_reduce(const double* partials, int n, int nq, double w0, double w1, double* out,
                    PcgState* S, int mode, double* ws, hipStream_t s);
-// the same for nq = 5 interleaved values (k_pcg1 partials), out[q] = sum_q * weights[q]
+// the same for nq = 5 interleaved values (k_pcg1 partials), out[q] = sum_q * weights[q].
+// progress: optional host-mapped counters (GpuSubdomainSolver::progress): [0] <- S->it after the
+// bump; launch_pcg1_halo writes [1] (exchanges packed) and [2] (exchanges unpacked).
 void launch_reduce_n(const double* partials, int n, int nq, const double* weights, double* out,
-                     PcgState* S, int mode, double* ws, hipStream_t s);
+                     PcgState* S, int mode, double* ws, hipStream_t s, long long* progress = nullptr);
 
 // Deterministic in-process "all-reduce" across P subdomains on one device (LocalComm):
 // out_k[q] = sum_r in_r[q] for every k, summed in rank order.
@@ -159,5 +161,12 @@ void launch_precond(const DevGeom& G, const DevTables& Tb, const T* r, T* z, boo
 template <typename T>
 int launch_dot_partials(const DevGeom& G, const T* x, const T* y, double* partials, int max_blocks,
                         hipStream_t s);
+
+// Error vs the analytic solution (k_error_norms): per block (sum e^2 in D, max |e| in D, max w)
+// into out[3 * nblocks]; w_eff = w + ca pa (+ cb pb) for npend = 1 (2) pending w steps.  Returns
+// the number of blocks used.
+template <typename T>
+int launch_error_norms(const DevGeom& G, const DevTables& Tb, const T* w, const T* pa, double ca,
+                       const T* pb, double cb, int npend, double* out, int max_blocks, hipStream_t s);
 
 }  // namespace pmx

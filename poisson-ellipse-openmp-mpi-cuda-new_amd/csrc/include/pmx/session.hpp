@@ -55,6 +55,16 @@ class Session {
   RunStats profile(int64_t n);  // threaded: every bucket is the MAX over the owned ranks
   PcgState state(int i = 0);
   bool threaded() const { return threaded_; }  // one host thread per owned rank
+  // capture every graph step(n) would replay now, without running (PcgDriver::prepare)
+  bool prepare(int64_t n);
+  void step_eager(int64_t n);  // n iterations as individual launches (canary)
+  PcgDriver::PathStats path_stats() const;
+  void reset_path_stats();
+  bool split_sweep() const;
+  // host-mapped device progress of owned rank i (GpuSubdomainSolver::progress); no HIP call
+  void progress(int i, long long out[3]) const;
+  // error vs the analytic solution over the owned subdomains (sum of e^2, max |e|, max w)
+  ErrorStats error_norms();
 
   const ProcGrid& grid() const { return pg_; }
   int num_local() const { return int(solvers_.size()); }
@@ -90,6 +100,12 @@ class Session {
 // Largest square grid whose fields fit into `bytes_per_gpu` on `gpus` devices (SURVEY §5.7:
 // subgrids sized against 288 GB HBM per MI355X): the default single pass keeps 5 fields, 8 B/pt
 // each in fp64 and 4 B/pt in fp32.
+// Every rank's communication calls for `iters` iterations of its own driver on a RecordingComm (all
+// ranks on the current device of opt.device, nothing exchanged): the test that every rank issues the
+// same sequence of collectives and matching send/recv groups per captured batch.
+std::vector<std::vector<CommEvent>> record_comm_sequence(const ProblemSpec& spec, int world, Split split,
+                                                         const GpuOptions& opt, int64_t iters);
+
 int64_t max_square_grid(double bytes_per_gpu, int gpus, DType dtype, double reserve_fraction = 0.1);
 
 }  // namespace pmx

@@ -91,6 +91,18 @@ class PoissonEllipse:
             return X * X + 4.0 * Y * Y < 1.0
         return (X / self.ax) ** 2 + (Y / self.by) ** 2 < 1.0
 
+    def local_error_stats(self, sd: dict, local: np.ndarray) -> dict:
+        """Unreduced error statistics of one subdomain's interior block (nx x ny, global nodes
+        i_start..i_end x j_start..j_end): the host twin of the device k_error_norms."""
+        x, y = self.coords()
+        X, Y = np.meshgrid(x[sd["i_start"]:sd["i_end"] + 1], y[sd["j_start"]:sd["j_end"] + 1], indexing="ij")
+        u = self.exact_solution(X, Y)
+        m = (X * X + 4.0 * Y * Y < 1.0) if self.is_reference_ellipse() else \
+            ((X / self.ax) ** 2 + (Y / self.by) ** 2 < 1.0)
+        e = np.where(m, local - u, 0.0)
+        return {"sum_e2": float((e * e).sum()), "max_error": float(np.abs(e).max(initial=0.0)),
+                "max_w": float(local.max(initial=-np.inf))}
+
     def error_norms(self, w: np.ndarray) -> dict:
         """L2 (h-weighted) and max error of a (M+1)x(N+1) solution vs the analytic one, in D."""
         x, y = self.coords()

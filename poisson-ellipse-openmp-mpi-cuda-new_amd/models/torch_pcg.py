@@ -96,6 +96,11 @@ class TorchPCG:
     def state(self) -> dict:
         return dict(it=self.k, done=self.done, iters=self.iters, status=self.status, diff=self.diff, nan=False)
 
+    def local_error_stats(self) -> dict:
+        """Unreduced (sum e^2, max |e|, max w) of this rank's block vs the analytic solution."""
+        wl = self.w[1:-1, 1:-1].to(torch.float64).cpu().numpy()
+        return self.p.local_error_stats(self.sd, wl)
+
     def synchronize(self):
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)

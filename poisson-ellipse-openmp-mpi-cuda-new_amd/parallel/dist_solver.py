@@ -133,19 +133,28 @@ class DistGpuPCG:
             self.sd = self.session.subdomain(0)
             self.single_pass = self.session.tile["algo"] == "pcg1"
         elif comm == "torch":
+            # ranks sharing this device (share-gpu rehearsal: all of them) count against its memory
+            # in the pcg1/pcg2 choice, which every rank makes identically from global data
+            sharing = info.world if device is not None else 1
             lay = self.n.comm_layout(self.spec, self.Px, self.Py, info.rank, dtype=dtype, kernel=kernel,
-                                     exact=exact, device=self.device, algo=algo)
+                                     exact=exact, device=self.device, algo=algo, sharing=sharing)
             self.single_pass = bool(lay["single_pass"])
-            self.arena = torch.zeros(lay["bytes"] + 256, dtype=torch.uint8, device=f"cuda:{self.device}")
-            base = self.arena.data_ptr()
-            pad = (-base) % 256
-            self.arena_view = self.arena[pad:pad + lay["bytes"]]
-            self.solver = self.n.SubdomainSolver(self.spec, self.Px, self.Py, info.rank, device=self.device,
-                                                 kernel=kernel, block=block, vec=vec, waves=waves,
-                                                 tile_rows=tile_rows, dtype=dtype, exact=exact, arena=base + pad,
-                                                 vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b,
-                                                 b_ring=b_ring, algo=1 if self.single_pass else 2)
+            self.solver, err = None, None
+            try:  # sizing / allocation: reported collectively, so no rank waits alone in a collective
+                self.arena = torch.zeros(lay["bytes"] + 256, dtype=torch.uint8, device=f"cuda:{self.device}")
+                base = self.arena.data_ptr()
+                pad = (-base) % 256
+                self.arena_view = self.arena[pad:pad + lay["bytes"]]
+                self.solver = self.n.SubdomainSolver(
+                    self.spec, self.Px, self.Py, info.rank, device=self.device, kernel=kernel, block=block,
+                    vec=vec, waves=waves, tile_rows=tile_rows, dtype=dtype, exact=exact, arena=base + pad,
+                    vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b, b_ring=b_ring,
+                    algo=1 if self.single_pass else 2)
+            except Exception as e:
+                err = e
+            agree(info, err is None, f"solver setup ({err})" if err else "solver setup", self.device)
             assert self.solver.single_pass == self.single_pass
+            self.path = {"graph_iters": 0, "eager_iters": 0, "graph_lengths": []}
             self.sd = self.solver.subdomain()
             tdt = torch.float64 if dtype == "fp64" else torch.float32
             el = lay["elem"]
@@ -162,6 +171,52 @@ class DistGpuPCG:
             self.tcomm = TorchComm() if info.world > 1 else None
         else:
             raise ValueError(f"unknown comm {comm!r}")
+
+    # ---- launch path / progress / accuracy ----
+    @property
+    def split_sweep(self) -> bool:
+        return bool(self.session.split_sweep) if self.comm_kind == "native" else False
+
+    @property
+    def graphs(self) -> bool:
+        return self.comm_kind == "native" and self.graph_batch > 0
+
+    def prepare(self, n: int) -> bool:
+        """Capture the graphs step(n) will replay (native path); False when it runs eagerly."""
+        return bool(self.session.prepare(int(n))) if self.comm_kind == "native" else False
+
+    def step_eager(self, n: int):
+        if self.comm_kind == "native":
+            self.session.step_eager(int(n))
+        else:
+            self.step(n)
+
+    def path_stats(self) -> dict:
+        return dict(self.session.path_stats()) if self.comm_kind == "native" else dict(self.path)
+
+    def reset_path_stats(self):
+        if self.comm_kind == "native":
+            self.session.reset_path_stats()
+        else:
+            self.path = {"graph_iters": 0, "eager_iters": 0, "graph_lengths": []}
+
+    def progress(self):
+        """(sweeps reduced, exchanges packed, exchanges unpacked) from host-mapped device counters, or
+        None.  Reads host memory only: safe from a watchdog thread while the main thread blocks."""
+        if self.comm_kind != "native":
+            return None
+        v = self.session.progress(0)
+        return None if v[0] < 0 else tuple(int(x) for x in v)
+
+    def local_error_stats(self) -> dict:
+        if self.comm_kind == "native":
+            return dict(self.session.error_norms())
+        torch.cuda.synchronize(self.device)
+        return dict(self.solver.error_norms(self._stream()))
+
+    def error_norms(self) -> dict:
+        """L2 (h-weighted) and max error vs the analytic solution, max w -- over all ranks."""
+        return reduce_error_stats(self.local_error_stats(), self.problem, self.info, self.device)
 
     def tile(self) -> dict:
         if self.comm_kind == "native":
@@ -209,6 +264,7 @@ class DistGpuPCG:
             self.session.step(n)
             return
         s = self._stream()
+        self.path["eager_iters"] += int(n)
         for _ in range(n):
             self.solver.enqueue_phase_a(s)
             if self.single_pass:
@@ -324,6 +380,102 @@ class DistGpuPCG:
         return res
 
 
+class SessionRunner:
+    """bench.py's runner interface over a single-process native Session (1 GPU, self comm)."""
+
+    def __init__(self, session, problem, info: DistInfo):
+        self.s, self.problem, self.info = session, problem, info
+        self.graphs = True
+
+    def init(self):
+        self.s.init()
+
+    def step(self, n: int):
+        self.s.step(int(n))
+
+    def step_eager(self, n: int):
+        self.s.step_eager(int(n))
+
+    def synchronize(self):
+        self.s.synchronize()
+
+    def state(self) -> dict:
+        return self.s.state(0)
+
+    def tile(self) -> dict:
+        return self.s.tile
+
+    def prepare(self, n: int) -> bool:
+        return bool(self.s.prepare(int(n)))
+
+    def path_stats(self) -> dict:
+        return dict(self.s.path_stats())
+
+    def reset_path_stats(self):
+        self.s.reset_path_stats()
+
+    @property
+    def split_sweep(self) -> bool:
+        return bool(self.s.split_sweep)
+
+    def progress(self):
+        v = self.s.progress(0)
+        return None if v[0] < 0 else tuple(int(x) for x in v)
+
+    def error_norms(self) -> dict:
+        return reduce_error_stats(dict(self.s.error_norms()), self.problem, self.info)
+
+    def profile(self, n: int) -> dict:
+        self.s.init()
+        ph = self.s.profile(int(n))
+        return {"compute": ph["t_kernel_a"] + ph["t_kernel_b"], "copy": 0.0, "comm": ph["t_comm"],
+                "precond": 0.0, "dot": ph["t_reduce"]}
+
+
+class TorchRunner:
+    """bench.py's runner interface over the plain-PyTorch PCG (CPU dry runs: flow tests)."""
+
+    graphs = False
+    split_sweep = False
+
+    def __init__(self, pcg, problem, info: DistInfo):
+        self.pcg, self.problem, self.info = pcg, problem, info
+        self.path = {"graph_iters": 0, "eager_iters": 0, "graph_lengths": []}
+
+    def init(self):
+        self.pcg.init()
+
+    def step(self, n: int):
+        self.path["eager_iters"] += int(n)
+        self.pcg.step(int(n))
+
+    step_eager = step
+
+    def synchronize(self):
+        self.pcg.synchronize()
+
+    def state(self) -> dict:
+        return self.pcg.state()
+
+    def tile(self) -> dict:
+        return dict(kind="torch-cpu")
+
+    def prepare(self, n: int) -> bool:
+        return False
+
+    def path_stats(self) -> dict:
+        return dict(self.path)
+
+    def reset_path_stats(self):
+        self.path = {"graph_iters": 0, "eager_iters": 0, "graph_lengths": []}
+
+    def progress(self):
+        return None
+
+    def error_norms(self) -> dict:
+        return reduce_error_stats(self.pcg.local_error_stats(), self.problem, self.info)
+
+
 def reduce_max(vals: dict, info: DistInfo, device: int = 0) -> dict:
     """MAX over ranks of a dict of floats (MPI_Reduce(MAX), stage4-mpi+cuda/poisson_mpi_cuda_f.cu:963-967)."""
     keys = list(vals)
@@ -332,6 +484,20 @@ def reduce_max(vals: dict, info: DistInfo, device: int = 0) -> dict:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return {k: float(v) for k, v in zip(keys, t.tolist())}
     return dict(vals)
+
+
+def reduce_error_stats(local: dict, problem, info: DistInfo, device: int = 0) -> dict:
+    """Finish per-rank (sum e^2, max |e|, max w) into l2_error / max_error / max_w over all ranks."""
+    if info.world > 1:
+        cdev = _comm_device(info, device)
+        t = torch.tensor([float(local["sum_e2"])], dtype=torch.float64, device=cdev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        m = torch.tensor([float(local["max_error"]), float(local["max_w"])], dtype=torch.float64, device=cdev)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        sum_e2, max_e, max_w = float(t.item()), float(m[0].item()), float(m[1].item())
+    else:
+        sum_e2, max_e, max_w = float(local["sum_e2"]), float(local["max_error"]), float(local["max_w"])
+    return {"l2_error": float(np.sqrt(sum_e2 * problem.h1 * problem.h2)), "max_error": max_e, "max_w": max_w}
 
 
 def phase_table(buckets: dict, scale: float = 1.0) -> str:

@@ -1,0 +1,111 @@
+"""bench.py multi-GPU supervision (CPU dry runs): the fallback ladder and the progress watchdog.
+
+The supervisor (bench.py itself, or one process per rank under torchrun) never touches the GPU; it
+starts the measuring ranks as fresh child processes, one rung of the ladder at a time:
+native RCCL + graphs + split sweep -> native eager -> torch.distributed.  Faults are injected with
+PMX_BENCH_FAULT ('<rung>:<hang|fail|crash>[@rank]'); a hang must be ended by the per-phase watchdog
+(exit 87, phase printed) and the JSON must name the rung that produced it and the failed rungs.
+Reference rank lifecycle: stage4-mpi+cuda/poisson_mpi_cuda_f.cu:986-1039."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT, free_port
+
+BASE = ["--cpu-dry-run", "--M", "64", "--N", "96", "--steps", "4", "--warmup", "1", "--deadline-scale", "0.05"]
+
+
+def _env(fault=None):
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "PMX_BENCH_ROLE", "PMX_BENCH_FAULT"):
+        env.pop(k, None)
+    if fault:
+        env["PMX_BENCH_FAULT"] = fault
+    return env
+
+
+def _spawned(n, fault=None, extra=()):
+    return subprocess.run([sys.executable, "bench.py", "--gpus", str(n), *BASE, *extra], cwd=ROOT,
+                          capture_output=True, text=True, timeout=300, env=_env(fault))
+
+
+def _torchrun(n, fault=None, extra=()):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", str(n), *BASE, *extra]
+    return subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=400, env=_env(fault))
+
+
+def _one_json(p):
+    lines = [json.loads(l) for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, p.stdout  # the supervisor's stdout carries the JSON line only
+    return lines[0]
+
+
+def test_ladder_advances_past_hang_and_failure():
+    p = _spawned(2, "1:hang@1,2:fail")
+    assert p.returncode == 0, p.stderr[-3000:]
+    j = _one_json(p)
+    assert j["config"]["rung"] == 3
+    lad = j["ladder"]
+    assert [a["rung"] for a in lad] == [1, 2, 3] and [a["ok"] for a in lad] == [False, False, True]
+    assert "status 87" in lad[0]["reason"]  # the watchdog ended the hung rung
+    assert "status 1" in lad[1]["reason"]
+    assert "no progress in phase 'canary'" in p.stderr
+    assert j["valid"] and j["tol_status"] == "converged" and j["n_gpus"] == 2
+
+
+def test_ladder_under_torchrun():
+    """One supervisor per torchrun rank: they agree on a fresh port per rung through torchrun's store
+    and stop their children when any rank fails."""
+    p = _torchrun(2, "1:crash@0,2:hang")
+    assert p.returncode == 0, p.stderr[-3000:]
+    j = _one_json(p)
+    assert j["config"]["rung"] == 3
+    assert [a["ok"] for a in j["ladder"]] == [False, False, True]
+    assert "status 3" in j["ladder"][0]["reason"] and "status 87" in j["ladder"][1]["reason"]
+
+
+def test_ladder_first_rung_success_records_path():
+    p = _spawned(2)
+    assert p.returncode == 0, p.stderr[-3000:]
+    j = _one_json(p)
+    assert j["config"]["rung"] == 1 and len(j["ladder"]) == 1 and j["ladder"][0]["ok"]
+    for k in ("timed_path", "timed_graph_iters", "timed_eager_iters", "l2_error", "max_error", "tol_note"):
+        assert k in j
+    assert j["timed_path"] == "eager" and j["timed_eager_iters"] == 4  # the CPU runner has no graphs
+    assert {"comm", "rccl_graph", "split_sweep", "rung"} <= set(j["config"])
+    # the analytic-solution error of the tol solve (64x96: ~2e-3, far above the solve tolerance)
+    assert 1e-4 < j["l2_error"] < 1e-2 and j["max_error"] >= j["l2_error"] / 2
+
+
+def test_every_rung_failing_fails_the_job():
+    p = _spawned(2, "1:fail,2:fail,3:crash")
+    assert p.returncode != 0
+    assert not [l for l in p.stdout.splitlines() if l.strip()]
+    assert "every rung of the ladder failed" in p.stderr
+
+
+def test_ladder_off_stops_at_the_first_rung():
+    p = _spawned(2, "1:fail", extra=("--ladder", "off"))
+    assert p.returncode != 0 and not p.stdout.strip()
+
+
+@pytest.mark.parametrize("comm,first", [("torch", 3)])
+def test_comm_torch_starts_at_rung_3(comm, first):
+    p = _spawned(2, extra=("--comm", comm))
+    assert p.returncode == 0, p.stderr[-3000:]
+    j = _one_json(p)
+    assert j["config"]["rung"] == first and [a["rung"] for a in j["ladder"]] == [first]
+
+
+def test_single_rank_watchdog_reports_phase():
+    """A single rank (no supervisor) is watched too: an injected hang ends with the phase named."""
+    env = _env("1:hang")
+    env["PMX_BENCH_ROLE"] = "child"  # as a supervised rank, so the fault hook is armed
+    p = subprocess.run([sys.executable, "bench.py", *BASE], cwd=ROOT, capture_output=True, text=True,
+                       timeout=120, env=env)
+    assert p.returncode == 87
+    assert "no progress in phase 'canary'" in p.stderr
