@@ -769,6 +769,19 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
   for (auto* s : local_)
     PMX_CHECK(s->single_pass() == single_pass_, "local subdomains disagree on the iteration algorithm");
   overlap_ = any_nb && local_[0]->options().overlap;
+  // One hardware queue per process (GPU_MAX_HW_QUEUES=1): every stream lands on it, so forking the
+  // halo / frame work onto side streams cannot overlap anything -- and ROCm 7.2 segfaults inside
+  // hipGraphLaunch on a captured graph with forked branches in that configuration (traced with
+  // PMX_DEBUG_GRAPH, bench/probe/hwq_probe.py).  The driver then runs the unforked schedule.
+  // PMX_FORK_ONE_QUEUE=1 keeps the forks (eager only) to test that their event ordering needs no
+  // concurrently resident streams.
+  if (const char* q = std::getenv("GPU_MAX_HW_QUEUES"); q && std::atoi(q) == 1) {
+    const char* keep = std::getenv("PMX_FORK_ONE_QUEUE");
+    if (keep && keep[0] == '1')
+      graph_failed_ = overlap_;  // forked schedule, eager launches
+    else
+      overlap_ = false;
+  }
   const char* env = std::getenv("PMX_POISON_HALOS");
   poison_ = any_nb && (local_[0]->options().poison_halos || (env && env[0] == '1'));
   if (overlap_) {
@@ -1027,8 +1040,29 @@ void PcgDriver::advance_host_k(long long n) {
 // Captures `len` iterations starting at w-cycle phase `phase` (the phase of the host iteration
 // counter now).  The capture enqueues nothing for execution, so the host counters are restored
 // afterwards; each launch of the graph advances them by `len`.
+namespace {
+// PMX_DEBUG_GRAPH=1: one stderr line per graph API step (locating failures inside the HIP runtime)
+bool debug_graph() {
+  static const bool on = [] {
+    const char* e = std::getenv("PMX_DEBUG_GRAPH");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+#define PMX_GDBG(...)                      \
+  do {                                     \
+    if (debug_graph()) {                   \
+      std::fprintf(stderr, "[pmx-graph] "); \
+      std::fprintf(stderr, __VA_ARGS__);   \
+      std::fprintf(stderr, "\n");          \
+      std::fflush(stderr);                 \
+    }                                      \
+  } while (0)
+}  // namespace
+
 hipGraphExec_t PcgDriver::build_graph(int phase, int len) {
   TraceRange tr("pmx:build_graph");
+  PMX_GDBG("build phase %d len %d", phase, len);
   (void)phase;
   bool single_stream = true;
   for (auto s : streams_) single_stream &= s == streams_[0];
@@ -1044,19 +1078,27 @@ hipGraphExec_t PcgDriver::build_graph(int phase, int len) {
   std::vector<long long> k0;
   for (auto* s : local_) k0.push_back(s->host_k());
   PMX_CHECK(!halo_pending_, "graph capture with an unjoined ghost exchange");
+  PMX_GDBG("capture begun");
   for (int k = 0; k < len; ++k) enqueue_one_iteration();
   join_halo();  // a captured batch is self-contained: every forked stream rejoins
   for (size_t i = 0; i < local_.size(); ++i) local_[i]->set_host_k(k0[i]);
+  PMX_GDBG("enqueued; ending capture");
   if (hipStreamEndCapture(streams_[0], &g) != hipSuccess || !g) {
     (void)hipGetLastError();
     return nullptr;
   }
   hipGraphExec_t e = nullptr;
+  if (debug_graph()) {
+    size_t nn = 0;
+    (void)hipGraphGetNodes(g, nullptr, &nn);
+    PMX_GDBG("captured %zu nodes; instantiating", nn);
+  }
   if (hipGraphInstantiate(&e, g, nullptr, nullptr, 0) != hipSuccess) {
     (void)hipGetLastError();
     (void)hipGraphDestroy(g);
     return nullptr;
   }
+  PMX_GDBG("instantiated");
   graphs_.push_back(g);
   execs_.push_back(e);
   return e;
@@ -1120,7 +1162,9 @@ void PcgDriver::enqueue_iterations(int64_t n) {
     const int len = int(std::min<int64_t>(graph_batch_, n - done));
     hipGraphExec_t e = len > 0 ? graph_for(int(local_[0]->host_k() % cyc), len) : nullptr;
     if (!e) break;
+    PMX_GDBG("launch len %d", len);
     HIP_CHECK(hipGraphLaunch(e, streams_[0]));
+    PMX_GDBG("launched");
     advance_host_k(len);
     note_graph(len);
     done += len;

@@ -104,31 +104,51 @@ for gb in (0, 16):
     s = pkg.make_session(pkg.PoissonEllipse(M=600, N=900), ranks=4, split=sys.argv[3], graph_batch=gb)
     st = s.solve(1)
     out.append(np.concatenate([s.local_w(i).ravel() for i in range(4)]))
-    out.append(np.array([st["iters"]], dtype=float))
+    out.append(np.array([st["iters"], float(s.overlapped), float(s.path_stats()["graph_iters"] > 0)]))
 np.save(sys.argv[2], np.concatenate(out))
 """
 
 
+def _hwq_run(tmp_path, split, **env_extra):
+    out = str(tmp_path / f"hwq_{split}_{'_'.join(f'{k}{v}' for k, v in env_extra.items())}.npy")
+    env = dict(os.environ, PMX_PCG1_SPLIT="1", **env_extra)
+    p = subprocess.run([sys.executable, "-c", _HWQ_SCRIPT, ROOT, out, split], capture_output=True, text=True,
+                       timeout=150, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return np.load(out)
+
+
 @pytest.mark.parametrize("split", ["reference", "rows"])
 def test_split_sweep_needs_no_concurrent_queues(pkg, tmp_path, monkeypatch, split):
-    """The forked compute/frame/comm streams of the split sweep, eager and captured, on ONE hardware
-    queue (HIP then serialises them in submission order): nothing may wait on a stream that cannot
-    run, and the result is bitwise the default one."""
+    """The forked compute/frame/comm streams of the split sweep with fewer hardware queues than
+    streams (HIP then shares queues, serialising in submission order): nothing may wait on a stream
+    that cannot run, and every result is bitwise the default one.
+      * GPU_MAX_HW_QUEUES=1 + PMX_FORK_ONE_QUEUE=1: the forked schedule, eager (graphs off);
+      * GPU_MAX_HW_QUEUES=1: the driver's one-queue policy (unforked schedule, graphs on) -- a forked
+        graph segfaults inside hipGraphLaunch there (ROCm 7.2);
+      * GPU_MAX_HW_QUEUES=2: forked schedule and forked graphs."""
     monkeypatch.setenv("PMX_PCG1_SPLIT", "1")
     ref = []
     for gb in (0, 16):
         s = pkg.make_session(pkg.PoissonEllipse(M=600, N=900), ranks=4, split=split, graph_batch=gb)
         st = s.solve(1)
+        assert s.split_sweep and s.overlapped
         ref.append(np.concatenate([s.local_w(i).ravel() for i in range(4)]))
-        ref.append(np.array([st["iters"]], dtype=float))
-    ref = np.concatenate(ref)
-    out = str(tmp_path / "hwq1.npy")
-    env = dict(os.environ, GPU_MAX_HW_QUEUES="1", PMX_PCG1_SPLIT="1")
-    p = subprocess.run([sys.executable, "-c", _HWQ_SCRIPT, ROOT, out, split], capture_output=True, text=True,
-                       timeout=150, env=env)
-    assert p.returncode == 0, p.stderr[-3000:]
-    got = np.load(out)
-    assert np.array_equal(got, ref)
+        ref.append(np.array([st["iters"]]))
+    assert np.array_equal(ref[0], ref[2]) and ref[1][0] == ref[3][0]  # graph == eager
+    n = ref[0].size
+
+    def check(got, overlapped, graphs):
+        for k in (0, 1):
+            o = k * (n + 3)
+            assert np.array_equal(got[o:o + n], ref[0]), (k, overlapped)
+            assert got[o + n] == ref[1][0]
+            assert got[o + n + 1] == float(overlapped)
+        assert got[n + 3 + n + 2] == float(graphs)  # the graph_batch=16 run replayed graphs or not
+
+    check(_hwq_run(tmp_path, split, GPU_MAX_HW_QUEUES="1", PMX_FORK_ONE_QUEUE="1"), True, False)
+    check(_hwq_run(tmp_path, split, GPU_MAX_HW_QUEUES="1"), False, True)
+    check(_hwq_run(tmp_path, split, GPU_MAX_HW_QUEUES="2"), True, True)
 
 
 def _check_sequences(logs, world):
