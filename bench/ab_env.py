@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""Interleaved same-box A/B of solver configurations that differ only in PMX_* environment knobs.
+
+    python bench/ab_env.py --shape 16384x16384 --shape 2048x16384 \
+        --cfg base: --cfg s4:PMX_PCG1_SUPER=4 --rounds 3 --iters 200
+
+Every round runs every (shape, config) once, in the same process: set the environment, build a
+fresh 1-GPU session (the knobs are read when a solver is built), init, warm up, time `iters`
+graph-replayed iterations between device synchronisations.  Prints one JSON line per measurement
+and a median table (us/iteration).  --tol adds one full solve per (shape, config) at the end and
+reports its iteration count (the knobs must not change it).
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", action="append", required=True, help="MxN")
+    ap.add_argument("--cfg", action="append", required=True, help="name:KEY=V,KEY=V (empty: defaults)")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--dtype", default="fp64")
+    ap.add_argument("--ranks", type=int, default=1, help="LocalComm subdomains on the one GPU")
+    ap.add_argument("--split", default="auto")
+    ap.add_argument("--tol", action="store_true")
+    a = ap.parse_args()
+    pkg = importlib.import_module("poisson-ellipse-openmp-mpi-cuda-new_amd")
+    cfgs = []
+    for c in a.cfg:
+        name, _, kv = c.partition(":")
+        env = dict(x.split("=", 1) for x in kv.split(",") if x)
+        cfgs.append((name, env))
+    knobs = sorted({k for _, e in cfgs for k in e})
+    shapes = [tuple(int(v) for v in s.split("x")) for s in a.shape]
+    res = {}
+
+    def session(M, N, env):
+        for k in knobs:
+            os.environ.pop(k, None)
+        os.environ.update(env)
+        return pkg.make_session(pkg.PoissonEllipse(M=M, N=N), ranks=a.ranks, split=a.split, dtype=a.dtype)
+
+    for rnd in range(a.rounds):
+        for (M, N) in shapes:
+            for name, env in cfgs:
+                s = session(M, N, env)
+                s.init()
+                s.step(a.warmup)
+                s.prepare(a.iters)
+                s.synchronize()
+                t0 = time.perf_counter()
+                s.step(a.iters)
+                s.synchronize()
+                us = (time.perf_counter() - t0) / a.iters * 1e6
+                st = s.state(0)
+                ok = not st["done"] and not st["nan"]
+                res.setdefault((M, N, name), []).append(us)
+                print(json.dumps(dict(round=rnd, M=M, N=N, cfg=name, us_per_iter=round(us, 2), ok=ok,
+                                      path=s.path_stats())), flush=True)
+                del s
+    print("\nmedian us/iteration", flush=True)
+    print("shape".ljust(14) + "".join(n.rjust(12) for n, _ in cfgs))
+    for (M, N) in shapes:
+        base = statistics.median(res[(M, N, cfgs[0][0])])
+        row = f"{M}x{N}".ljust(14)
+        for name, _ in cfgs:
+            m = statistics.median(res[(M, N, name)])
+            row += f"{m:9.1f}({m / base:.3f})".rjust(12) if name != cfgs[0][0] else f"{m:12.1f}"
+        print(row, flush=True)
+    if a.tol:
+        for (M, N) in shapes:
+            for name, env in cfgs:
+                s = session(M, N, env)
+                t0 = time.perf_counter()
+                st = s.solve(4)
+                print(json.dumps(dict(M=M, N=N, cfg=name, iters=st["iters"], status=st["status"],
+                                      seconds=round(time.perf_counter() - t0, 2))), flush=True)
+                del s
+
+
+if __name__ == "__main__":
+    main()

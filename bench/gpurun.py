@@ -9,7 +9,15 @@ its limit (exit codes 124/134/137/139 or >128); an ordinary non-zero exit (a fai
 recorded and the next step still runs.  Results land in gpurun_out/<study>/ on this machine;
 copy the summaries worth keeping into profiles/.
 
-Studies that back kept profiles name themselves in the profile's README.
+Fixed studies (STUDIES) and parametrised ones (`<study> -- <arguments>`):
+    ab        -- bench/ab_env.py arguments: interleaved same-box A/B of PMX_* knobs
+    pmc       -- tag:ENV=V,... configurations, --args for bench.py, --passes (PMC_PASSES)
+    timeline  -- grids MxN: rocprofv3 kernel trace of the CLI + bench/trace_timeline.py
+    validate  -- GPU suite, smoke(), default bench
+    share     -- rank counts: supervised multi-rank rehearsal on the one GPU
+    cli       -- quoted pmx argument strings
+Studies that back kept profiles name themselves in the profile's README; bench/RETIRED.md maps
+the round-1/2 one-off gpu_*.sh scripts onto these.
 """
 from __future__ import annotations
 
@@ -49,11 +57,115 @@ STUDIES: dict[str, list[tuple[str, int, str]]] = {
         ("bench_default", 300, bench("--gpus 1 --steps 20 --warmup 5")),
         ("bench_200", 300, bench("--gpus 1 --steps 200 --warmup 20 --no-tol-solve")),
     ],
+    # round 3: super-row dispatch + alternating march direction (halo-row reuse in L2)
+    "super_ab": [
+        ("ab", 900, "python -u bench/ab_env.py --shape 16384x16384 --shape 2048x16384 --cfg base: "
+                    "--cfg s2:PMX_PCG1_SUPER=2 --cfg s4:PMX_PCG1_SUPER=4 --cfg s8:PMX_PCG1_SUPER=8 "
+                    "--rounds 3 --iters 200"),
+        ("tol", 300, "python -u bench/ab_env.py --shape 16384x16384 --cfg s4:PMX_PCG1_SUPER=4 --rounds 1 "
+                     "--iters 20 --tol"),
+    ],
+    "dir_ab": [
+        ("ab", 900, "python -u bench/ab_env.py --shape 16384x16384 --shape 2048x16384 --cfg base: "
+                    "--cfg rev:PMX_PCG1_ALT=2 --cfg alt:PMX_PCG1_ALT=1 --cfg s4fwd:PMX_PCG1_SUPER=4,PMX_PCG1_ALT=0 "
+                    "--cfg s2fwd:PMX_PCG1_SUPER=2,PMX_PCG1_ALT=0 --rounds 3 --iters 200"),
+        ("rocprof_bench", 300, f"{ROCPROF} -d gpurun_out/dir_ab/rp -o run -- "
+                               + bench("--gpus 1 --steps 60 --warmup 10 --no-tol-solve")),
+    ],
     "profile_default": [
         ("rocprof_bench", 300, f"{ROCPROF} -d gpurun_out/profile_default/rp -o run -- "
                                + bench("--gpus 1 --steps 60 --warmup 10 --no-tol-solve")),
     ],
 }
+
+
+PMC_PASSES = {
+    "ea_rd": "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum",
+    "ea_wr": "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_HIT_sum TCC_MISS_sum",
+    "sq1": "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES "
+           "SQ_WAIT_INST_ANY",
+    "sq2": "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY SQ_WAIT_ANY "
+           "SQ_INST_LEVEL_VMEM SQ_IFETCH SQ_INSTS_VALU_FMA_F64",
+    "lat": "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE GRBM_COUNT",
+}
+
+
+def pmc_study(study: str, configs: dict[str, str], args: str, passes=("ea_rd", "ea_wr")):
+    """One rocprofv3 counter pass per (config, pass), kernel counters only, each under its own
+    SIGKILL limit; then bench/pmc_summary.py over the study directory."""
+    steps = []
+    for tag, env in configs.items():
+        for p in passes:
+            pre = f"env {env} " if env else ""
+            steps.append((f"{tag}_{p}", 100, f"{pre}timeout -s KILL 90 rocprofv3 --pmc {PMC_PASSES[p]} "
+                                              f"--output-format csv -d gpurun_out/{study}/{tag}_{p} -o run -- "
+                                              f"python3 bench.py {args}"))
+    steps.append(("summary", 60, f"python3 bench/pmc_summary.py gpurun_out/{study}"))
+    return steps
+
+
+PMC_ARGS = "--steps 6 --warmup 1 --graph-batch 0 --no-tol-solve"
+
+
+# ---- parametrised studies: `python bench/gpurun.py <study> -- <study arguments>` ----
+def _ab(argv):
+    """interleaved same-box A/B of environment knobs: the arguments go to bench/ab_env.py"""
+    return [("ab", 1000, "python -u bench/ab_env.py " + " ".join(shlex.quote(a) for a in argv))]
+
+
+def _pmc(argv):
+    """counter passes per configuration: tag:ENV=V,ENV=V ... [--args 'bench.py args'] [--passes a,b]"""
+    ap = argparse.ArgumentParser(prog="pmc")
+    ap.add_argument("cfg", nargs="+")
+    ap.add_argument("--args", default=PMC_ARGS)
+    ap.add_argument("--passes", default="ea_rd,ea_wr")
+    a = ap.parse_args(argv)
+    cfgs = {c.split(":", 1)[0]: " ".join(c.split(":", 1)[1].split(",")) if ":" in c else "" for c in a.cfg}
+    return pmc_study("pmc", cfgs, a.args, tuple(a.passes.split(",")))
+
+
+def _timeline(argv):
+    """kernel durations and gaps per iteration: rocprofv3 --kernel-trace of the pmx CLI per grid
+    (MxN ...), then bench/trace_timeline.py; extra pmx arguments after --pmx"""
+    ap = argparse.ArgumentParser(prog="timeline")
+    ap.add_argument("grids", nargs="+")
+    ap.add_argument("--iters", type=int, default=600)
+    ap.add_argument("--pmx", default="")
+    a = ap.parse_args(argv)
+    steps = []
+    for g in a.grids:
+        M, N = g.split("x")
+        steps.append((f"trace_{g}", 150, f"rocprofv3 --kernel-trace --output-format csv -d gpurun_out/timeline/{g} "
+                                         f"-o run -- poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx {M} {N} "
+                                         f"--max-iter {a.iters} --json {a.pmx}"))
+        steps.append((f"timeline_{g}", 60, f"python3 bench/trace_timeline.py gpurun_out/timeline/{g}/run_kernel_trace.csv "
+                                           f"--skip 50"))
+    return steps
+
+
+def _validate(argv):
+    """the round-end tiers: GPU suite, smoke(), default bench (+ optional extra bench.py args)"""
+    extra = " ".join(argv)
+    return [("pytest_gpu", 1100, f"{PYTEST} tests -m gpu"),
+            ("smoke", 200, "python -c 'import __graft_entry__ as g; g.smoke()'"),
+            ("bench_default", 300, bench(f"--gpus 1 --steps 20 --warmup 5 {extra}"))]
+
+
+def _share(argv):
+    """multi-rank rehearsal on the one GPU under the supervisor: ranks ... [-- bench.py args]"""
+    ranks = [int(x) for x in argv if x.isdigit()] or [2, 4, 8]
+    extra = " ".join(x for x in argv if not x.isdigit())
+    return [(f"share{n}", 420, bench(f"--gpus {n} --share-gpu --steps 20 --warmup 5 {extra}")) for n in ranks]
+
+
+def _cli(argv):
+    """pmx CLI runs, one step per quoted argument string: 'M N --flags' ..."""
+    return [(f"pmx{i}", 600, f"poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx {a} --json") for i, a in enumerate(argv)]
+
+
+PARAMETRISED = {"ab": _ab, "pmc": _pmc, "timeline": _timeline, "validate": _validate, "share": _share, "cli": _cli}
+STUDIES["pmc_super"] = pmc_study("pmc_super", {"base": "", "s4": "PMX_PCG1_SUPER=4"}, PMC_ARGS,
+                                 ("ea_rd", "ea_wr", "lat"))
 
 
 def script(name: str, steps) -> str:
@@ -75,11 +187,14 @@ def script(name: str, steps) -> str:
 
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("study", choices=sorted(STUDIES))
+    ap.add_argument("study", choices=sorted(STUDIES) + sorted(PARAMETRISED))
     ap.add_argument("--dry", action="store_true", help="write and print the script, do not run it")
     ap.add_argument("--timeout", type=int, default=0, help="gpurun limit (default: sum of the steps + 120 s)")
-    a = ap.parse_args()
-    steps = STUDIES[a.study]
+    argv = sys.argv[1:]
+    cut = argv.index("--") if "--" in argv else len(argv)
+    a = ap.parse_args(argv[:cut])
+    rest = argv[cut + 1:]  # arguments of a parametrised study
+    steps = PARAMETRISED[a.study](rest) if a.study in PARAMETRISED else STUDIES[a.study]
     os.makedirs(os.path.join(ROOT, "bench", ".runs"), exist_ok=True)
     path = os.path.join("bench", ".runs", f"{a.study}.sh")
     with open(os.path.join(ROOT, path), "w") as f:
