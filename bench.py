@@ -18,7 +18,10 @@ The process(es) started by the user or by torchrun never touch the GPU: they sta
 ranks as child processes and walk a fallback ladder of transports, each rung in fresh processes:
     rung 1  native RCCL, iterations captured in hipGraphs, split sweep (the production path)
     rung 2  native RCCL, eager launches, no split sweep
-    rung 3  torch.distributed ProcessGroupNCCL (= RCCL) driving the same native kernels
+    rung 3  native IPC transport (peer arenas mapped with hipIpcOpenMemHandle, epoch flags; no
+            RCCL at all), graphs and split sweep
+    rung 4  torch.distributed ProcessGroupNCCL (= RCCL) driving the same native kernels
+A --share-gpu rehearsal (every rank on GPU 0) starts at rung 3, then rung 4 over gloo.
 Every rank runs under a progress watchdog: each phase (setup, canary iteration, first graph batch,
 warmup, timed region, tolerance solve) has a deadline; on expiry the rank prints the phase and the
 device's own progress counters (sweeps reduced, ghost exchanges packed / unpacked) and exits, and
@@ -54,7 +57,8 @@ TOL_NOTE = ("stop rule ||w^{k+1}-w^k|| < delta absolute (reference rule); at fin
 RUNGS = {
     1: dict(comm="native", rccl_graph=True, split=None),
     2: dict(comm="native", rccl_graph=False, split=0),
-    3: dict(comm="torch", rccl_graph=False, split=0),
+    3: dict(comm="ipc", rccl_graph=False, split=None),
+    4: dict(comm="torch", rccl_graph=False, split=0),
 }
 
 
@@ -69,8 +73,9 @@ def parse(argv=None):
                     help="CG guard on (Ap,p) (reference: 1e-15; grids beyond ~100000^2 need a smaller value)")
     ap.add_argument("--dtype", default="fp64", choices=["fp64", "fp32", "mixed"],
                     help="mixed = fp32: fp32 storage, fp64 arithmetic and reductions")
-    ap.add_argument("--comm", default="native", choices=["native", "torch"],
-                    help="first rung of the ladder: native RCCL (rung 1) or torch.distributed (rung 3)")
+    ap.add_argument("--comm", default="native", choices=["native", "ipc", "torch"],
+                    help="first rung of the ladder: native RCCL (rung 1), the IPC transport (rung 3) or "
+                         "torch.distributed (rung 4)")
     ap.add_argument("--ladder", default="on", choices=["on", "off"],
                     help="multi-GPU: fall back to the next transport when a rung fails or stalls")
     ap.add_argument("--split", default="auto", choices=["reference", "auto", "rows", "cols"],
@@ -202,15 +207,13 @@ def _kill(p, sig=signal.SIGKILL):
 
 
 def _ladder(args) -> list[int]:
-    if args.share_gpu:
-        first = 1
-    elif args.comm == "torch":
+    if args.comm == "torch":
+        first = 4
+    elif args.comm == "ipc" or args.share_gpu:  # RCCL refuses two ranks on one device
         first = 3
     else:
         first = 1 if args.rccl_graph == "on" else 2
-    rungs = [r for r in (1, 2, 3) if r >= first]
-    if args.share_gpu:
-        rungs = [1]  # one transport (gloo, host-staged)
+    rungs = [r for r in (1, 2, 3, 4) if r >= first]
     return rungs if args.ladder == "on" else rungs[:1]
 
 
@@ -386,9 +389,8 @@ def measure(args) -> int:
     if env.world != args.gpus:
         raise SystemExit(f"[bench] --gpus {args.gpus} but {env.world} rank(s) came up (WORLD_SIZE); refusing to "
                          "report a different GPU count")
-    native = not dry and not share and cfg["comm"] == "native"
     # Python-level coordination (uid broadcast, agreement, barriers, MAX over ranks) stays on gloo for
-    # the native transport: no third (torch) RCCL communicator next to the solver's two
+    # the native transports: no third (torch) RCCL communicator next to the solver's two
     backend = "nccl" if (not dry and not share and cfg["comm"] == "torch") else "gloo"
     info = launch.init_distributed(backend=backend if env.world > 1 else None,
                                    device_type="cpu" if (dry or share or backend == "gloo") else None)
@@ -425,9 +427,15 @@ def measure(args) -> int:
         models = importlib.import_module(pkg_name + ".models")
         runner = ds.SessionRunner(models.make_session(problem, ranks=1, device=info.local_rank, **kw), problem, info)
         comm_used = "self"
+    elif share and cfg["comm"] == "ipc":
+        runner = ds.DistGpuPCG(problem, info, comm="ipc", device=0, **kw)
+        comm_used = "ipc"
     elif share:
         runner = ds.DistGpuPCG(problem, info, comm="torch", device=0, **kw)
         comm_used = "gloo-host-staged"
+    elif cfg["comm"] == "ipc":
+        runner = ds.DistGpuPCG(problem, info, comm="ipc", **kw)
+        comm_used = "ipc"
     elif cfg["comm"] == "native":
         runner = ds.DistGpuPCG(problem, info, comm="native", rccl_graph=cfg["rccl_graph"], **kw)
         comm_used = "rccl"
@@ -554,7 +562,7 @@ def measure(args) -> int:
             "vs_baseline": round(mlups / BASELINE_MLUPS, 2),
             "dtype": args.dtype,
             "data": "cpu-dry-run (plain-PyTorch PCG on CPU: flow test, not a measurement)" if dry else
-                    ("share-gpu rehearsal (all ranks on one GPU, gloo host-staged comm: not a measurement)"
+                    (f"share-gpu rehearsal (all ranks on one GPU, {comm_used} transport: not a measurement)"
                      if share else "synthetic (reference problem: F=1 in ellipse x^2+4y^2<1, zero initial guess)"),
             "config": {
                 "model": f"fictitious-domain Poisson ellipse, Jacobi-PCG, {args.M}x{args.N}",

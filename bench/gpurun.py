@@ -50,6 +50,11 @@ STUDIES: dict[str, list[tuple[str, int, str]]] = {
         ("share8", 420, bench("--gpus 8 --share-gpu --M 4096 --N 4096 --steps 20 --warmup 5")),
     ],
     # the whole GPU suite as the driver runs it
+    "ipc": [
+        ("pytest_ipc", 600, f"{PYTEST} tests/test_gpu_dist.py -k 'ipc or share'"),
+        ("pytest_launch", 420, f"{PYTEST} tests/test_gpu_launch_path.py -k 'bench'"),
+        ("share8", 420, bench("--gpus 8 --share-gpu --M 4096 --N 4096 --steps 20 --warmup 5")),
+    ],
     "pytest_gpu": [
         ("pytest_gpu", 1100, f"{PYTEST} tests -m gpu"),
     ],
@@ -71,6 +76,11 @@ STUDIES: dict[str, list[tuple[str, int, str]]] = {
                     "--cfg s2fwd:PMX_PCG1_SUPER=2,PMX_PCG1_ALT=0 --rounds 3 --iters 200"),
         ("rocprof_bench", 300, f"{ROCPROF} -d gpurun_out/dir_ab/rp -o run -- "
                                + bench("--gpus 1 --steps 60 --warmup 10 --no-tol-solve")),
+    ],
+    "bands_ab": [
+        ("ab", 900, "python -u bench/ab_env.py --shape 16384x16384 --shape 2048x16384 --cfg base: "
+                    "--cfg b2:PMX_PCG1_BANDS=2 --cfg b3:PMX_PCG1_BANDS=3 --cfg b4:PMX_PCG1_BANDS=4 "
+                    "--rounds 3 --iters 200"),
     ],
     "profile_default": [
         ("rocprof_bench", 300, f"{ROCPROF} -d gpurun_out/profile_default/rp -o run -- "

@@ -409,6 +409,7 @@ PYBIND11_MODULE(_pmx, m) {
              if (comm == "self") c.comm = CommKind::kSelf;
              else if (comm == "local") c.comm = CommKind::kLocal;
              else if (comm == "rccl") c.comm = CommKind::kRccl;
+             else if (comm == "ipc") c.comm = CommKind::kIpc;
              else PMX_CHECK(false, "unknown comm " << comm);
              if (!uid.is_none()) c.rccl_uid = uid.cast<std::string>();
              c.ranks = ranks;
@@ -427,6 +428,15 @@ PYBIND11_MODULE(_pmx, m) {
            py::arg("waves_b") = 0, py::arg("tile_rows_b") = -1, py::arg("poison_halos") = false,
            py::arg("b_ring") = false, py::arg("algo") = -1, py::arg("defer_connect") = false,
            py::arg("threaded") = -1)
+      .def("ipc_export", [](Session& s) { return py::bytes(s.ipc_export()); },
+           "IPC session: this rank's memory handles (pass every rank's to connect_ipc)")
+      .def("connect_ipc", [](Session& s, std::vector<py::bytes> ex) {
+             std::vector<std::string> v;
+             for (auto& b : ex) v.push_back(std::string(b));
+             s.set_ipc_exports(v);
+             py::gil_scoped_release g;
+             s.connect();
+           })
       .def("connect", [](Session& s) { py::gil_scoped_release g; s.connect(); },
            "create the communicator and driver (sessions built with defer_connect=True)")
       .def_property_readonly("connected", &Session::connected)

@@ -1,0 +1,304 @@
+// IpcComm: a device-resident multi-process transport without RCCL (SURVEY §5.8 "peer-mapped direct
+// halo stores"; verdict r2 item 6).
+//
+// One rank per process, ranks on one GPU (the 1-GPU test box) or on several (peer access over
+// xGMI): every rank exports its comm arena (the send/recv halo slots and the PcgState scalars) and a
+// small IpcBlock of flags with hipIpcGetMemHandle, opens its peers' with hipIpcOpenMemHandle, and
+// then moves data with its own kernels, ordered by monotonic epoch flags:
+//
+//   all-reduce   publish the local sums into IpcBlock::pub[c & 1], raise red_flag = c, wait until
+//                every rank's red_flag >= c, sum the published values in rank order (the LocalComm
+//                order: results are bitwise those of LocalComm / one process with P subdomains)
+//   halo         before packing exchange e: wait until every neighbour acknowledged exchange e-1
+//                (ack >= e-1 posts); pack (the solver's own kernels); post: halo_flag = e;
+//                pull: wait for each neighbour's halo_flag >= e, copy its send slot into our recv
+//                slot; ack[slot] = e; unpack (the solver's own kernel)
+//
+// The parity-indexed pub[] and the acks are what make the schedule race-free with the overlapped
+// and split sweeps: a rank may be a whole sweep ahead of a neighbour, never two exchanges.  Waits
+// spin on system-scope acquire loads with a wall-clock timeout (PMX_IPC_TIMEOUT_MS, default 20 s):
+// on expiry the kernel records the error, stops the solve (done flag, status breakdown) and
+// check_health() throws, so a dead peer cannot hang the GPU.  Remote data is read with
+// non-temporal loads after the acquire (no stale cache line of an earlier epoch is reused).
+// Graph-capturable: every operation is a kernel with fixed arguments, epochs live on the device.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pmx/common.hpp"
+#include "pmx/gpu_solver.hpp"
+
+namespace pmx {
+
+namespace {
+
+struct alignas(256) IpcBlock {
+  unsigned long long red_flag;   // all-reduces published by this rank
+  unsigned long long halo_flag;  // ghost exchanges posted by this rank
+  unsigned long long red_count;  // this rank's own counters (only its kernels touch them)
+  unsigned long long halo_count;
+  unsigned long long ack[kHaloSlots];  // exchanges pulled from the neighbour across slot s
+  int err;                             // 1 = a wait timed out
+  int pad;
+  double pub[2][8];                    // published local sums, by all-reduce parity
+};
+
+constexpr int kMaxIpcRanks = 64;
+
+struct IpcPeers {
+  IpcBlock* all[kMaxIpcRanks];  // every rank's block (ours included), IPC-mapped
+  IpcBlock* nbr[kHaloSlots];    // block of the neighbour across slot s (nullptr: none)
+  const void* src[kHaloSlots];  // its send slot facing us (opposite slot), IPC-mapped
+  void* dst[kHaloSlots];        // our recv slot
+  int len[kHaloSlots];          // elements
+};
+
+__device__ inline unsigned long long ld_acq(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ inline void st_rel(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Spin until *flag >= target or the wall clock (100 MHz) passes the deadline.  On timeout: record
+// the error and stop the solve.  Called by one lane.
+__device__ bool wait_ge(const unsigned long long* flag, unsigned long long target, long long timeout_ticks,
+                        IpcBlock* own, PcgState* S) {
+  const long long t0 = wall_clock64();
+  while (ld_acq(flag) < target) {
+    if (wall_clock64() - t0 > timeout_ticks) {
+      __hip_atomic_store(&own->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      S->nan_flag = 1;
+      S->status = int(Status::kBreakdown);
+      S->done = 1;
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+  return true;
+}
+
+__global__ void k_ipc_allreduce(IpcPeers P, int world, int me, double* buf, int n, PcgState* S,
+                                long long timeout) {
+  if (threadIdx.x != 0) return;
+  IpcBlock* own = P.all[me];
+  const unsigned long long c = own->red_count + 1;
+  own->red_count = c;
+  const int par = int(c & 1);
+  for (int q = 0; q < n; ++q) own->pub[par][q] = buf[q];
+  st_rel(&own->red_flag, c);
+  for (int r = 0; r < world; ++r)
+    if (!wait_ge(&P.all[r]->red_flag, c, timeout, own, S)) return;
+  for (int q = 0; q < n; ++q) {  // rank order, as LocalComm
+    double s = 0.0;
+    for (int r = 0; r < world; ++r) s += __builtin_nontemporal_load(&P.all[r]->pub[par][q]);
+    buf[q] = s;
+  }
+}
+
+// before packing exchange e = halo_count + 1: every neighbour pulled exchange e - 1
+__global__ void k_ipc_wait_acks(IpcPeers P, int me, PcgState* S, long long timeout) {
+  if (threadIdx.x != 0) return;
+  IpcBlock* own = P.all[me];
+  const unsigned long long posted = own->halo_count;
+  for (int s = 0; s < kHaloSlots; ++s)
+    if (P.nbr[s] && !wait_ge(&P.nbr[s]->ack[opposite_slot(s)], posted, timeout, own, S)) return;
+}
+
+__global__ void k_ipc_post(IpcPeers P, int me) {
+  if (threadIdx.x != 0) return;
+  IpcBlock* own = P.all[me];
+  const unsigned long long c = own->halo_count + 1;
+  own->halo_count = c;
+  st_rel(&own->halo_flag, c);  // the pack kernel before us has finished: its slots are in memory
+}
+
+// grid (blocks per slot, 8 slots): every block's lane 0 waits for the neighbour's post, then the
+// block copies its share of the slot (non-temporal loads of the remote slot)
+template <typename T>
+__global__ void __launch_bounds__(256) k_ipc_pull(IpcPeers P, int me, PcgState* S, long long timeout) {
+  const int s = blockIdx.y;
+  if (!P.nbr[s]) return;
+  __shared__ int ok;
+  IpcBlock* own = P.all[me];
+  if (threadIdx.x == 0) ok = wait_ge(&P.nbr[s]->halo_flag, own->halo_count, timeout, own, S) ? 1 : 0;
+  __syncthreads();
+  if (!ok) return;
+  const T* src = static_cast<const T*>(P.src[s]);
+  T* dst = static_cast<T*>(P.dst[s]);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < P.len[s]; i += gridDim.x * 256)
+    dst[i] = __builtin_nontemporal_load(src + i);
+}
+
+__global__ void k_ipc_ack(IpcPeers P, int me) {
+  if (threadIdx.x != 0) return;
+  IpcBlock* own = P.all[me];
+  for (int s = 0; s < kHaloSlots; ++s)
+    if (P.nbr[s]) st_rel(&own->ack[s], own->halo_count);
+}
+
+std::string handle_bytes(void* p) {
+  hipIpcMemHandle_t h;
+  HIP_CHECK(hipIpcGetMemHandle(&h, p));
+  return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
+}
+
+void* open_handle(const std::string& b) {
+  PMX_CHECK(b.size() == sizeof(hipIpcMemHandle_t), "bad IPC handle size " << b.size());
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, b.data(), sizeof(h));
+  void* p = nullptr;
+  HIP_CHECK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+  return p;
+}
+
+class IpcComm final : public Comm {
+ public:
+  IpcComm(GpuSubdomainSolver* local, int world) : local_(local), world_(world) {
+    PMX_CHECK(world >= 1 && world <= kMaxIpcRanks, "IpcComm supports 1.." << kMaxIpcRanks << " ranks");
+    HIP_CHECK(hipSetDevice(local->device()));
+    HIP_CHECK(hipMalloc(&block_, sizeof(IpcBlock)));
+    HIP_CHECK(hipMemset(block_, 0, sizeof(IpcBlock)));
+    const char* t = std::getenv("PMX_IPC_TIMEOUT_MS");
+    timeout_ = (t && t[0] ? std::atoll(t) : 20000LL) * 100000LL;  // wall_clock64: 100 MHz
+  }
+  ~IpcComm() override {
+    (void)hipSetDevice(local_->device());
+    (void)hipDeviceSynchronize();
+    for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
+    if (block_) (void)hipFree(block_);
+  }
+
+  // this rank's exports: device id, arena handle, block handle
+  std::string export_handles() const {
+    const int dev = local_->device();
+    std::string out(reinterpret_cast<const char*>(&dev), sizeof(dev));
+    out += handle_bytes(reinterpret_cast<void*>(local_->arena_ptr()));
+    out += handle_bytes(block_);
+    return out;
+  }
+
+  // every rank's export_handles(), indexed by rank
+  void attach(const std::vector<std::string>& peers) {
+    PMX_CHECK(int(peers.size()) == world_, "IpcComm::attach needs one export per rank");
+    const int me = local_->sd().rank;
+    const size_t hs = sizeof(hipIpcMemHandle_t);
+    std::vector<char*> arenas(size_t(world_), nullptr);
+    std::memset(&P_, 0, sizeof(P_));
+    for (int r = 0; r < world_; ++r) {
+      const std::string& e = peers[size_t(r)];
+      PMX_CHECK(e.size() == sizeof(int) + 2 * hs, "bad IPC export of rank " << r);
+      if (r == me) {
+        arenas[size_t(r)] = reinterpret_cast<char*>(local_->arena_ptr());
+        P_.all[r] = block_;
+        continue;
+      }
+      int dev = 0;
+      std::memcpy(&dev, e.data(), sizeof(int));
+      if (dev != local_->device()) {  // peer GPU: map its memory over xGMI
+        const hipError_t pe = hipDeviceEnablePeerAccess(dev, 0);
+        if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled) HIP_CHECK(pe);
+        (void)hipGetLastError();
+      }
+      arenas[size_t(r)] = static_cast<char*>(open_handle(e.substr(sizeof(int), hs)));
+      opened_.push_back(arenas[size_t(r)]);
+      P_.all[r] = static_cast<IpcBlock*>(open_handle(e.substr(sizeof(int) + hs, hs)));
+      opened_.push_back(P_.all[r]);
+    }
+    const CommLayout& L = local_->layout();
+    for (int s = 0; s < kHaloSlots; ++s) {
+      if (!L.active(s)) continue;
+      const int q = L.peer[s];
+      PMX_CHECK(q >= 0 && q < world_ && q != me, "IpcComm: bad neighbour " << q << " on slot " << s);
+      // the neighbour's layout mirrors ours across the shared edge: its slot opposite(s) carries
+      // the same number of elements at its own send offset, which a rank computes locally from the
+      // neighbour's subdomain (comm_layout is a pure function of it)
+      const Subdomain nsd = decompose_2d(local_->spec().M, local_->spec().N, local_->sd().grid, q);
+      const CommLayout NL = GpuSubdomainSolver::comm_layout(nsd, local_->options().dtype, local_->single_pass());
+      const int os = opposite_slot(s);
+      PMX_CHECK(NL.edge_len[os] == L.edge_len[s], "IpcComm: slot lengths disagree with rank " << q);
+      P_.nbr[s] = P_.all[q];
+      P_.src[s] = arenas[size_t(q)] + NL.send_off[os];
+      P_.dst[s] = local_->recv_dev(s);
+      P_.len[s] = L.edge_len[s];
+      maxlen_ = std::max(maxlen_, L.edge_len[s]);
+    }
+    attached_ = true;
+  }
+
+  void allreduce(std::vector<GpuSubdomainSolver*>& local, int which, std::vector<hipStream_t>& streams) override {
+    require(local);
+    if (world_ == 1) return;
+    hipLaunchKernelGGL(k_ipc_allreduce, dim3(1), dim3(64), 0, streams[0], P_, world_, local_->sd().rank,
+                       local_->reduce_buf(which), GpuSubdomainSolver::reduce_len(which), local_->state_dev(),
+                       timeout_);
+    HIP_CHECK(hipGetLastError());
+  }
+  void before_pack(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>& streams) override {
+    require(local);
+    if (maxlen_ == 0) return;
+    hipLaunchKernelGGL(k_ipc_wait_acks, dim3(1), dim3(64), 0, streams[0], P_, local_->sd().rank,
+                       local_->state_dev(), timeout_);
+    HIP_CHECK(hipGetLastError());
+  }
+  void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>& streams) override {
+    require(local);
+    if (maxlen_ == 0) return;
+    const int me = local_->sd().rank;
+    hipLaunchKernelGGL(k_ipc_post, dim3(1), dim3(64), 0, streams[0], P_, me);
+    const int bx = std::max(1, std::min(64, (maxlen_ + 255) / 256));
+    if (local_->layout().elem == 8)
+      hipLaunchKernelGGL(k_ipc_pull<double>, dim3(bx, kHaloSlots), dim3(256), 0, streams[0], P_, me,
+                         local_->state_dev(), timeout_);
+    else
+      hipLaunchKernelGGL(k_ipc_pull<float>, dim3(bx, kHaloSlots), dim3(256), 0, streams[0], P_, me,
+                         local_->state_dev(), timeout_);
+    hipLaunchKernelGGL(k_ipc_ack, dim3(1), dim3(64), 0, streams[0], P_, me);
+    HIP_CHECK(hipGetLastError());
+  }
+  void check_health() override {
+    int err = 0;
+    HIP_CHECK(hipMemcpy(&err, &block_->err, sizeof(int), hipMemcpyDeviceToHost));
+    PMX_CHECK(err == 0, "IPC transport: a wait for a peer rank timed out (PMX_IPC_TIMEOUT_MS); the solve "
+                        "was stopped");
+  }
+  bool prefers_split() const override { return true; }
+  std::string name() const override { return "ipc"; }
+  int world_size() const override { return world_; }
+
+ private:
+  void require(std::vector<GpuSubdomainSolver*>& local) const {
+    PMX_CHECK(attached_, "IpcComm used before attach()");
+    PMX_CHECK(local.size() == 1 && local[0] == local_, "IpcComm drives exactly its own rank");
+  }
+  GpuSubdomainSolver* local_;
+  int world_;
+  IpcBlock* block_ = nullptr;
+  IpcPeers P_{};
+  std::vector<void*> opened_;
+  int maxlen_ = 0;
+  long long timeout_ = 0;
+  bool attached_ = false;
+};
+
+}  // namespace
+
+std::unique_ptr<Comm> make_ipc_comm(GpuSubdomainSolver* local, int world) {
+  return std::make_unique<IpcComm>(local, world);
+}
+std::string ipc_export(Comm* c) {
+  auto* ic = dynamic_cast<IpcComm*>(c);
+  PMX_CHECK(ic, "not an IPC communicator");
+  return ic->export_handles();
+}
+void ipc_attach(Comm* c, const std::vector<std::string>& peers) {
+  auto* ic = dynamic_cast<IpcComm*>(c);
+  PMX_CHECK(ic, "not an IPC communicator");
+  ic->attach(peers);
+}
+
+}  // namespace pmx

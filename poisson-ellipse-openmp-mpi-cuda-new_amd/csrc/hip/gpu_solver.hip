@@ -95,6 +95,9 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_PCG1_WAVES", o.waves1);
   env_int("PMX_PCG1_PF", o.pf1);
   env_int("PMX_PCG1_ORDER", o.order1);
+  env_int("PMX_PCG1_SUPER", o.super1);
+  env_int("PMX_PCG1_ALT", o.alt1);
+  env_int("PMX_PCG1_BANDS", o.bands1);
   env_int("PMX_PCG1_WCYCLE", o.wcycle1);
   env_int("PMX_PROGRESS", o.progress);
   PMX_CHECK(o.wcycle1 == 2 || o.wcycle1 == 3, "pcg1 w cycle must be 2 or 3");
@@ -233,6 +236,9 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     }
 #endif
     HIP_CHECK(hipMalloc(&r2_, field_bytes_));
+    tiles1_.super = opt_.super1;
+    tiles1_.bands = opt_.bands1;
+    tiles1_.alt = opt_.alt1 >= 0 ? opt_.alt1 : (opt_.super1 > 0 ? 1 : 0);
     if (opt_.order1) {  // ellipse-cut tiles first (their 3-5x longer tiles would trail the sweep)
       HIP_CHECK(hipMalloc(&tile_order_, 2 * size_t(tiles1_.ntiles()) * sizeof(int)));
       slow_tiles_ = pcg1_build_order(G, tables_, tiles1_, tile_order_, nullptr);
@@ -854,6 +860,8 @@ void PcgDriver::synchronize() {
 
 void PcgDriver::init() {
   TraceRange tr("pmx:init");
+  // pcg2's k_init packs r^0 into the send slots
+  if (!single_pass_ && any_nb_) comm_->before_pack(local_, streams_);
   for (size_t i = 0; i < local_.size(); ++i) local_[i]->enqueue_init(streams_[i]);
   if (single_pass_) {
     // ghosts of r^0 -> sweep 0 ((z^0, r^0), (A z^0, z^0); it 0 -> 1) -> all-reduce -> ghosts of
@@ -882,6 +890,7 @@ void PcgDriver::poison(std::vector<hipStream_t>& streams) {
 }
 
 void PcgDriver::halo_exchange_pcg1(std::vector<hipStream_t>& streams) {
+  comm_->before_pack(local_, streams);
   for (size_t i = 0; i < local_.size(); ++i) {
     HIP_CHECK(hipSetDevice(local_[i]->device()));
     local_[i]->enqueue_halo_pack(streams[i]);
@@ -919,6 +928,7 @@ void PcgDriver::enqueue_split_iteration() {
     HIP_CHECK(hipEventRecord(ev_swept_[u], streams_[i]));
     HIP_CHECK(hipStreamWaitEvent(comm_streams_[i], ev_swept_[u], 0));
   });
+  comm_->before_pack(local_, comm_streams_);
   for (size_t i = 0; i < local_.size(); ++i) {
     HIP_CHECK(hipSetDevice(local_[i]->device()));
     local_[i]->enqueue_halo_pack(comm_streams_[i]);
@@ -990,6 +1000,7 @@ void PcgDriver::enqueue_one_iteration() {
   }
   comm_->allreduce(local_, 0, streams_);
   if (!overlap_) {
+    if (any_nb_) comm_->before_pack(local_, streams_);  // k_pcg_b packs the send slots
     for (size_t i = 0; i < local_.size(); ++i) {
       HIP_CHECK(hipSetDevice(local_[i]->device()));
       local_[i]->enqueue_phase_b(streams_[i]);
@@ -1003,6 +1014,7 @@ void PcgDriver::enqueue_one_iteration() {
   //             comm stream           `-> halo send/recv ------------------------------'
   // The next pcg_a is the only reader of the recv buffers and the next edge kernel the next
   // writer of the send buffers; both come after the join.
+  comm_->before_pack(local_, streams_);
   for (size_t i = 0; i < local_.size(); ++i) {
     HIP_CHECK(hipSetDevice(local_[i]->device()));
     local_[i]->enqueue_pack(streams_[i]);

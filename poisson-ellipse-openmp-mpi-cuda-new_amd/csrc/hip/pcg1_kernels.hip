@@ -139,7 +139,12 @@ struct Pcg1Row {
 // domain, VEC = 2): no Dirichlet masks, and ownership is a fixed lane set (lanes 1..62 own both
 // their columns, lanes 0 and 63 none), so the sums accumulate unmasked and are masked once at the
 // end.  Same arithmetic as the general path, so a point's values never depend on its tile.
-template <typename T, int VEC, int PF, int WM, bool FAST>
+// DIR: +1 marches the tile top-down (rows i0-2 .. i1+2), -1 bottom-up (i1+2 .. i0-2).  The stencil
+// is symmetric in i, so the pipeline only swaps which stored row is i-1 and which i+1; every
+// point gets the same arithmetic either way (only the order of the per-lane partial sums over
+// rows differs).  Alternating directions make vertically adjacent tiles that start together read
+// their shared halo rows at the same time (see pcg1_build_order).
+template <typename T, int VEC, int PF, int WM, bool FAST, int DIR>
 __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb, T* __restrict__ w,
                                            const T* __restrict__ rold, T* __restrict__ rnew,
                                            const T* __restrict__ pold,
@@ -175,7 +180,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     load_cols<T, VEC>(rold + int64_t(mc) * P, c0, cmax, b.r);
     load_cols<T, VEC>(pold + int64_t(mc) * P, c0, cmax, b.p);
     if constexpr (WUP) {  // w of the row stage B handles next step
-      const int wc = min(max(m - 1, -1), G.nx + 2);
+      const int wc = min(max(m - DIR, -1), G.nx + 2);
       load_cols<T, VEC>(w + int64_t(wc) * P, c0, cmax, b.w);
       // p^{k-2} still sits in the buffer this sweep overwrites with p^k: the owner of a point
       // reads it here, before its own store of that row (rows it does not own are never used)
@@ -187,7 +192,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   double Pm2[VEC], Pm1[VEC], Zm3[VEC], Zm2[VEC], ro1[VEC], po1[VEC], po2[VEC];
 #pragma unroll
   for (int u = 0; u < VEC; ++u) Pm2[u] = Pm1[u] = Zm3[u] = Zm2[u] = ro1[u] = po1[u] = po2[u] = 0.0;
-  RowCo cB = row_co(Tb, grow(i0 - 3), gjlo, gjhi);  // rows m-1, m-2
+  RowCo cB = row_co(Tb, grow(DIR > 0 ? i0 - 3 : i1 + 3), gjlo, gjhi);  // rows m-DIR, m-2 DIR
   RowCo cC = cB;
   bool parked = false;  // column constants in LDS (see col_lds)
   auto park_cols = [&]() {
@@ -203,11 +208,11 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   };
   if (cB.ucls == 0) park_cols();
 
-  const int mfirst = i0 - 2, mlast = i1 + 2;
+  const int mfirst = DIR > 0 ? i0 - 2 : i1 + 2, mlast = DIR > 0 ? i1 + 2 : i0 - 2;
   auto step = [&](int m, const Pcg1Row<T, VEC>& cur, Pcg1Row<T, VEC>& nxt) {
     // PF rows ahead, unconditional (a branch around loads forces vmcnt(0)); past the tile's last
     // row re-read that row (a cache hit) instead of the next tile's rows
-    fetch(min(m + PF, mlast), nxt);
+    fetch(DIR > 0 ? min(m + PF, mlast) : max(m - PF, mlast), nxt);
     // ---- stage A: p^k of row m
     const bool rowA = FAST || interior_row(m);
     const RowCo cA = row_co(Tb, grow(m), gjlo, gjhi);
@@ -224,9 +229,10 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
       const double v = __builtin_fma(beta, pom[u], z);
       Pm[u] = in ? double(static_cast<T>(v)) : 0.0;  // the stored (rounded) p^k is the one used
     }
-    // ---- stage B: A p^k, r^k, z^k of row m-1 (j neighbours by DPP; edge lanes get 0, their
-    // results only feed columns that are not owned)
-    const int mb = m - 1;
+    // ---- stage B: A p^k, r^k, z^k of row m-DIR (j neighbours by DPP; edge lanes get 0, their
+    // results only feed columns that are not owned).  Rows i-1 / i+1 of it: Pm2 / Pm (DIR +1),
+    // Pm / Pm2 (DIR -1).
+    const int mb = m - DIR;
     const bool rowB = FAST || interior_row(mb);
     const bool ownB = mb >= i0 && mb <= i1;
     double Zm1[VEC];
@@ -245,7 +251,8 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
         coef(cB, Tb, G, scol, u, lane, gj[u], a0, a1, b0, b1);
         const double xjm = u == 0 ? left : Pm1[u - 1];
         const double xjp = u == VEC - 1 ? right : Pm1[u + 1];
-        const double Ap = apply_a<false>(Pm1[u], Pm2[u], Pm[u], xjm, xjp, a0, a1, b0, b1, G);
+        const double Ap = apply_a<false>(Pm1[u], DIR > 0 ? Pm2[u] : Pm[u], DIR > 0 ? Pm[u] : Pm2[u], xjm, xjp,
+                                         a0, a1, b0, b1, G);
         const bool in = FAST || (rowB && colin[u]);
         const double rn = double(static_cast<T>(upd_r<false>(ro1[u], alpha, Ap)));
         rs[u] = static_cast<T>(in ? rn : 0.0);
@@ -258,7 +265,8 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
           // r^{k-2} = r^{k-1} + alpha_{k-1} A p^{k-1};  p^{k-2} = (p^{k-1} - D^-1 r^{k-2}) / beta_{k-1}
           const double xm = u == 0 ? oleft : po1[u - 1];
           const double xp = u == VEC - 1 ? oright : po1[u + 1];
-          const double Apo = apply_a<false>(po1[u], po2[u], pom[u], xm, xp, a0, a1, b0, b1, G);
+          const double Apo = apply_a<false>(po1[u], DIR > 0 ? po2[u] : pom[u], DIR > 0 ? pom[u] : po2[u], xm,
+                                            xp, a0, a1, b0, b1, G);
           const double zo = zdiv_u<false>(cB.ucls, __builtin_fma(c1, Apo, ro1[u]), a0, a1, b0, b1, G);
           const double t = __builtin_fma(c2, po1[u] - zo, double(cur.w[u]));
           ws[u] = static_cast<T>(__builtin_fma(alpha, Pm1[u], __builtin_fma(c1, po1[u], t)));
@@ -279,8 +287,8 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
       store_cols<T, VEC>(pnew + o, c0, ps, FAST || own_all, own);
       if constexpr (WUP) store_cols<T, VEC>(w + o, c0, ws, FAST || own_all, own);
     }
-    // ---- stage C: A z^k of row m-2
-    const int mcr = m - 2;
+    // ---- stage C: A z^k of row m-2 DIR
+    const int mcr = m - 2 * DIR;
     if (mcr >= i0 && mcr <= i1) {
       const double left = dpp_shift_f64<kWaveShr1>(Zm2[VEC - 1], 0.0);
       const double right = dpp_shift_f64<kWaveShl1>(Zm2[0], 0.0);
@@ -290,7 +298,8 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
         coef(cC, Tb, G, scol, u, lane, gj[u], a0, a1, b0, b1);
         const double xjm = u == 0 ? left : Zm2[u - 1];
         const double xjp = u == VEC - 1 ? right : Zm2[u + 1];
-        const double Az = apply_a<false>(Zm2[u], Zm3[u], Zm1[u], xjm, xjp, a0, a1, b0, b1, G);
+        const double Az = apply_a<false>(Zm2[u], DIR > 0 ? Zm3[u] : Zm1[u], DIR > 0 ? Zm1[u] : Zm3[u], xjm, xjp,
+                                         a0, a1, b0, b1, G);
         if (FAST || own[u]) {
           acc[1] += Az * Zm2[u];
           acc[2] += Az * Pm2[u];
@@ -314,12 +323,12 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   // slot q and refills the slot step m - 1 consumed
   Pcg1Row<T, VEC> buf[PF + 1];
 #pragma unroll
-  for (int q = 0; q < PF; ++q) fetch(min(mfirst + q, mlast), buf[q]);
-  for (int m = mfirst; m <= mlast; m += PF + 1) {
+  for (int q = 0; q < PF; ++q) fetch(DIR > 0 ? min(mfirst + q, mlast) : max(mfirst - q, mlast), buf[q]);
+  for (int m = mfirst; DIR > 0 ? m <= mlast : m >= mlast; m += DIR * (PF + 1)) {
 #pragma unroll
     for (int q = 0; q <= PF; ++q) {
-      if (m + q > mlast) goto done;
-      step(m + q, buf[q], buf[(q + PF) % (PF + 1)]);
+      if (DIR > 0 ? m + q > mlast : m - q < mlast) goto done;
+      step(m + DIR * q, buf[q], buf[(q + PF) % (PF + 1)]);
     }
   }
 done:
@@ -352,6 +361,7 @@ struct Pcg1Part {
   int tiles_i, ti_lo, ti_hi, tj_lo, tj_hi;
   const int* order;  // position -> tile id (pcg1_build_order), or nullptr: pcg1_tile's order
   int count;         // tiles of this launch
+  int alt;           // 1: tiles with even ti march bottom-up, 2: every tile (TileCfg::alt)
 };
 
 // k-th tile of the part -> (ti, tj); false past the end.  The frame is enumerated as: tile rows
@@ -529,8 +539,16 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
   // strictly inside the global domain (no Dirichlet node in reach)
   const bool fast = VEC == 2 && j1 == j0 + WO - 1 && G.gi0 + i0 - 2 >= 1 && G.gi0 + i1 + 2 <= G.M - 1 &&
                     G.gj0 + j0 - 2 >= 1 && G.gj0 + j0 + 64 * VEC - 3 <= G.N - 1;
-#define PMX_MARCH(E, F) \
-  pcg1_march<T, VEC, PF, E, F>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, acc, scol)
+  const bool rev = part.alt == 2 || (part.alt == 1 && !(ti & 1));  // a function of the tile alone
+#define PMX_MARCH(E, F)                                                                                   \
+  do {                                                                                                   \
+    if (rev)                                                                                             \
+      pcg1_march<T, VEC, PF, E, F, -1>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, \
+                                       acc, scol);                                                       \
+    else                                                                                                 \
+      pcg1_march<T, VEC, PF, E, F, 1>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2,  \
+                                      acc, scol);                                                        \
+  } while (0)
 #define PMX_MARCH_W(F)                                     \
   if constexpr (!WS) {                                     \
     PMX_MARCH(0, F);                                       \
@@ -724,24 +742,48 @@ int pcg1_build_order(const DevGeom& G, const DevTables& Tb, TileCfg& tc, int* d_
   std::vector<int> order(2 * size_t(n), 0);
   int nslow = 0;
   for (int part = 0; part <= 1; ++part) {
-    const Pcg1Part P{part, tc.tiles_i, tc.ti_lo, tc.ti_hi, tc.tj_lo, tc.tj_hi, nullptr, 0};
+    const Pcg1Part P{part, tc.tiles_i, tc.ti_lo, tc.ti_hi, tc.tj_lo, tc.tj_hi, nullptr, 0, 0};
     const int count = part == 0 ? n : tc.interior_tiles();
     int* o = order.data() + size_t(part) * n;
     // positions of XCD x (xcd_remap with one wave per workgroup): [x (q+1), ...) as in xcd_remap
     const int q = count / 8, r = count % 8;
+    const int S = std::max(1, tc.super);
+    std::vector<int> ids;
     for (int x = 0, start = 0; x < 8; ++x) {
       const int len = q + (x < r ? 1 : 0);
+      // this XCD's tiles (a band of tile rows), dispatched super-row by super-row, column by
+      // column inside a super-row (S = 1: row-major)
+      ids.clear();
+      for (int k = start; k < start + len; ++k) {
+        int ti = 0, tj = 0;
+        PMX_CHECK(pcg1_tile(k, P, tc.tiles_j, ti, tj), "pcg1_build_order: tile enumeration");
+        ids.push_back(ti * tc.tiles_j + tj);
+      }
+      std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) {
+        const int ta = a / tc.tiles_j, tb = b / tc.tiles_j;
+        const int ka[3] = {ta / S, a % tc.tiles_j, ta % S}, kb[3] = {tb / S, b % tc.tiles_j, tb % S};
+        return std::lexicographical_compare(ka, ka + 3, kb, kb + 3);
+      });
+      // bands > 1: the chunk's tiles split into `bands` consecutive runs dispatched round-robin, so
+      // a tile's lower neighbour starts ~bands tile rows of dispatches later (a lag closer to the
+      // time the upper tile reaches the rows they share)
+      const int B = std::max(1, std::min(tc.bands, int(ids.size())));
+      if (B > 1) {
+        std::vector<int> il;
+        il.reserve(ids.size());
+        const size_t per = (ids.size() + B - 1) / B;
+        for (size_t k = 0; k < per; ++k)
+          for (int b = 0; b < B; ++b)
+            if (b * per + k < ids.size() && k < per) il.push_back(ids[b * per + k]);
+        ids.swap(il);
+      }
       int w = start;
-      for (int pass = 0; pass < 2; ++pass)  // slow tiles first, then the rest, each in natural order
-        for (int k = start; k < start + len; ++k) {
-          int ti = 0, tj = 0;
-          PMX_CHECK(pcg1_tile(k, P, tc.tiles_j, ti, tj), "pcg1_build_order: tile enumeration");
-          const int id = ti * tc.tiles_j + tj;
+      for (int pass = 0; pass < 2; ++pass)  // slow tiles first, then the rest, each in that order
+        for (int id : ids)
           if ((cut[size_t(id)] != 0) == (pass == 0)) {
             o[w++] = id;
             if (pass == 0 && part == 0) ++nslow;
           }
-        }
       start += len;
     }
   }
@@ -802,7 +844,8 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
   PMX_CHECK(part >= 0 && part <= 2, "launch_pcg1: part must be 0, 1 or 2");
   const int count = part == 0 ? tc.ntiles() : part == 1 ? tc.interior_tiles() : tc.ntiles() - tc.interior_tiles();
   const Pcg1Part P{part, tc.tiles_i, tc.ti_lo, tc.ti_hi, tc.tj_lo, tc.tj_hi,
-                   tc.waves == 1 ? (part == 0 ? tc.order0 : part == 1 ? tc.order1 : nullptr) : nullptr, count};
+                   tc.waves == 1 ? (part == 0 ? tc.order0 : part == 1 ? tc.order1 : nullptr) : nullptr, count,
+                   tc.alt};
   if (count == 0) return;
   PMX_CHECK(G.nb == 0 || (G.nx >= 2 && G.ny >= 2), "pcg1 on a decomposed grid needs subdomains >= 2 x 2");
   const int nb = (count + tc.waves - 1) / tc.waves;

@@ -30,12 +30,14 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
     PMX_CHECK(cfg_.world == 1, "self comm needs world == 1 (use local or rccl)");
   if (cfg_.comm == CommKind::kLocal)
     PMX_CHECK(int(cfg_.ranks.size()) == cfg_.world, "local comm owns every rank");
+  if (cfg_.comm == CommKind::kIpc)
+    PMX_CHECK(cfg_.ranks.size() == 1, "the IPC transport runs one rank per process");
 
   // one iteration algorithm for every subdomain (and every process: the choice only depends on
   // global data, see choose_single_pass)
   GpuOptions pre = cfg_.opt;
   // a multi-process RCCL run tracks device progress for its hang watchdog (GpuOptions::progress)
-  if (cfg_.comm == CommKind::kRccl && cfg_.world > 1) pre.progress = 1;
+  if ((cfg_.comm == CommKind::kRccl || cfg_.comm == CommKind::kIpc) && cfg_.world > 1) pre.progress = 1;
   GpuOptions base = resolve_options(pre);
   if (base.algo == -1) {
     HIP_CHECK(hipSetDevice(cfg_.devices[0]));
@@ -54,11 +56,22 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
   if (!cfg_.defer_connect) connect();
 }
 
+std::string Session::ipc_export() {
+  PMX_CHECK(cfg_.comm == CommKind::kIpc, "ipc_export needs an IPC session");
+  if (!comm_) comm_ = make_ipc_comm(solvers_[0].get(), cfg_.world);
+  return pmx::ipc_export(comm_.get());
+}
+
 void Session::connect() {
   PMX_CHECK(drivers_.empty(), "session already connected");
   std::vector<GpuSubdomainSolver*> raw;
   for (auto& s : solvers_) raw.push_back(s.get());
   switch (cfg_.comm) {
+    case CommKind::kIpc:
+      if (!comm_) comm_ = make_ipc_comm(raw[0], cfg_.world);
+      if (cfg_.world == 1 && cfg_.ipc_exports.empty()) cfg_.ipc_exports.push_back(pmx::ipc_export(comm_.get()));
+      ipc_attach(comm_.get(), cfg_.ipc_exports);
+      break;
     case CommKind::kSelf: comm_ = make_self_comm(); break;
     case CommKind::kLocal: comm_ = make_local_comm(raw); break;
     case CommKind::kRccl:

@@ -66,7 +66,7 @@ struct GpuOptions {
   int pair_w = 1;
   // Iteration algorithm: 2 = pcg2 (k_pcg_a + k_pcg_b, two reductions, radius-1 halo), 1 = pcg1
   // (single-pass k_pcg1, one 5-value reduction, radius-2 halo with corners), -1 = auto (pcg1
-  // where it applies: wave kernels, not exact, fp64 storage, every subdomain >= 2 x 2 and the 5th
+  // where it applies: wave kernels, not exact, any storage type, every subdomain >= 2 x 2 and the 5th
   // field fits into the device).  The choice depends only on global data (problem, process grid,
   // options, device size), so every rank of a distributed run makes the same one.
   // PMX_ALGO=-1|1|2 overrides.  pcg1 matches the reference iteration counts and pcg2's solution
@@ -80,6 +80,13 @@ struct GpuOptions {
   int pf1 = 0;  // 0 = auto
   // pcg1 dispatch order: 1 = tiles cut by the ellipse first within each XCD's share, 0 = natural
   int order1 = 1;
+  // pcg1 halo-row reuse (TileCfg::super / alt): super-rows of `super1` tile rows dispatched column by
+  // column, even tile rows marching bottom-up.  0 = row-major order, every tile top-down.
+  // PMX_PCG1_SUPER overrides.
+  int super1 = 0;
+  int bands1 = 1;  // sub-bands per XCD chunk dispatched round-robin (PMX_PCG1_BANDS)
+  int alt1 = -1;  // march directions: -1 = alternate iff super1 > 0, 0 = all top-down, 1 = alternate,
+                  // 2 = all bottom-up (PMX_PCG1_ALT; ablations)
   // pcg1 w schedule: w is read and written on one sweep in wcycle1 (3 = triples, 2 = pairs).
   // Triples recover p^{k-2} from p^{k-1} and r^{k-1} (one extra stencil), or re-read it when
   // |beta_{k-1}| < 1e-3 or pair_w == 2.  PMX_PCG1_WCYCLE=2|3 overrides.
@@ -277,6 +284,9 @@ class Comm {
   virtual void check_health() {}
   virtual std::string name() const = 0;
   virtual int world_size() const = 0;
+  // Called before every kernel that writes this rank's send slots (the next exchange's pack): a
+  // transport whose peers read those slots in place (IpcComm) waits here until they have.
+  virtual void before_pack(std::vector<GpuSubdomainSolver*>&, std::vector<hipStream_t>&) {}
   // The pcg1 split sweep is the default with this transport (its exchange is the long pole).
   virtual bool prefers_split() const { return false; }
   // Error path of a threaded driver set: make every operation in flight or blocked on this
@@ -296,6 +306,13 @@ std::unique_ptr<Comm> make_rccl_comm(const std::string& unique_id, int nranks,
                                      const std::vector<int>& ranks, const std::vector<int>& devices,
                                      bool capturable);
 std::string rccl_unique_id();
+
+// IPC transport (comm/ipc_comm.hip): one rank per process, peers' arenas mapped with
+// hipIpcOpenMemHandle.  Two-phase setup: construct, ipc_export() on every rank, exchange the
+// strings out of band, ipc_attach() with all of them (indexed by rank).
+std::unique_ptr<Comm> make_ipc_comm(GpuSubdomainSolver* local, int world);
+std::string ipc_export(Comm* ipc);
+void ipc_attach(Comm* ipc, const std::vector<std::string>& exports);
 
 // One communication call as a rank's driver issued it (RecordingComm, tests): comm 0 = the
 // scalar communicator, 1 = the halo communicator; op "allreduce" (count = doubles), or a halo

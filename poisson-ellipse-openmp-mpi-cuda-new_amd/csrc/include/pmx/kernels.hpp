@@ -37,6 +37,12 @@ struct TileCfg {
   // nullptr = natural order
   const int* order0 = nullptr;
   const int* order1 = nullptr;
+  // kind 3 halo-row reuse: tiles with even ti march bottom-up (alt), and the order tables dispatch
+  // `super` vertically adjacent tiles (a super-row) back to back, column by column, so the pair
+  // across each inner boundary reads its shared halo rows at the same time (0 = row-major order)
+  int alt = 0;
+  int super = 0;
+  int bands = 1;  // order tables: sub-bands per XCD chunk dispatched round-robin (pcg1_build_order)
   int interior_tiles() const { return (ti_hi - ti_lo) * (tj_hi - tj_lo); }
   int ntiles() const { return tiles_i * tiles_j; }
 };

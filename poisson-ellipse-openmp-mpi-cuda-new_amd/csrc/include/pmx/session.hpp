@@ -11,7 +11,7 @@
 
 namespace pmx {
 
-enum class CommKind : int { kSelf = 0, kLocal = 1, kRccl = 2 };
+enum class CommKind : int { kSelf = 0, kLocal = 1, kRccl = 2, kIpc = 3 };
 
 struct SessionConfig {
   ProblemSpec spec;
@@ -22,6 +22,7 @@ struct SessionConfig {
   std::vector<int> ranks;        // ranks owned by this process (default: all for self/local)
   std::vector<int> devices;      // device per owned rank (default: opt.device)
   std::string rccl_uid;          // for kRccl
+  std::vector<std::string> ipc_exports;  // for kIpc: every rank's Session::ipc_export(), by rank
   bool rccl_graph = false;       // capture RCCL calls into the hipGraph
   // Build the solvers only; the communicator and driver are created by Session::connect().  A
   // multi-process caller checks that every rank allocated its subdomain before any rank enters
@@ -38,6 +39,9 @@ class Session {
   explicit Session(const SessionConfig& cfg);
   ~Session();
   void connect();  // comm + driver (called by the constructor unless cfg.defer_connect)
+  // kIpc (defer_connect): this rank's IPC export; hand every rank's to set_ipc_exports, then connect
+  std::string ipc_export();
+  void set_ipc_exports(const std::vector<std::string>& e) { cfg_.ipc_exports = e; }
   bool connected() const { return !drivers_.empty(); }
 
   void init();

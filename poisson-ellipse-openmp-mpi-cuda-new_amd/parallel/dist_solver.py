@@ -100,6 +100,7 @@ class DistGpuPCG:
         self.problem = problem
         self.info = info
         self.comm_kind = comm
+        self.native = comm in ("native", "ipc")  # the native Session drives the iteration
         self.device = info.local_rank if device is None else device
         self.n = _native()
         self.spec = problem.to_native()
@@ -130,6 +131,36 @@ class DistGpuPCG:
                 except Exception as e:
                     err = e
                 agree(info, err is None, f"RCCL communicator initialisation ({err})", self.device)
+            self.sd = self.session.subdomain(0)
+            self.single_pass = self.session.tile["algo"] == "pcg1"
+        elif comm == "ipc":
+            # device-resident transport without RCCL (csrc/comm/ipc_comm.hip): every rank exports its
+            # comm arena and flag block with hipIpcGetMemHandle, the handles travel over
+            # torch.distributed, and every rank maps its peers'
+            self.session, err = None, None
+            try:
+                self.session = self.n.Session(
+                    self.spec, world=info.world, comm="ipc", split=getattr(self.n.Split, split),
+                    device=self.device, kernel=kernel, block=block, vec=vec, waves=waves, tile_rows=tile_rows,
+                    dtype=dtype, exact=exact, graph_batch=graph_batch, ranks=[info.rank], devices=[self.device],
+                    overlap=overlap, vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b, b_ring=b_ring,
+                    algo=algo, defer_connect=True)
+                mine = self.session.ipc_export()
+            except Exception as e:
+                err, mine = e, b""
+            agree(info, err is None, f"native solver setup ({err})" if err else "native solver setup", self.device)
+            exports = [None] * info.world
+            if info.world > 1:
+                dist.all_gather_object(exports, mine)
+            else:
+                exports = [mine]
+            with _Watchdog(init_timeout, "IPC transport setup"):
+                try:
+                    self.session.connect_ipc(exports)
+                    err = None
+                except Exception as e:
+                    err = e
+                agree(info, err is None, f"IPC transport setup ({err})", self.device)
             self.sd = self.session.subdomain(0)
             self.single_pass = self.session.tile["algo"] == "pcg1"
         elif comm == "torch":
@@ -175,27 +206,27 @@ class DistGpuPCG:
     # ---- launch path / progress / accuracy ----
     @property
     def split_sweep(self) -> bool:
-        return bool(self.session.split_sweep) if self.comm_kind == "native" else False
+        return bool(self.session.split_sweep) if self.native else False
 
     @property
     def graphs(self) -> bool:
-        return self.comm_kind == "native" and self.graph_batch > 0
+        return self.native and self.graph_batch > 0
 
     def prepare(self, n: int) -> bool:
         """Capture the graphs step(n) will replay (native path); False when it runs eagerly."""
-        return bool(self.session.prepare(int(n))) if self.comm_kind == "native" else False
+        return bool(self.session.prepare(int(n))) if self.native else False
 
     def step_eager(self, n: int):
-        if self.comm_kind == "native":
+        if self.native:
             self.session.step_eager(int(n))
         else:
             self.step(n)
 
     def path_stats(self) -> dict:
-        return dict(self.session.path_stats()) if self.comm_kind == "native" else dict(self.path)
+        return dict(self.session.path_stats()) if self.native else dict(self.path)
 
     def reset_path_stats(self):
-        if self.comm_kind == "native":
+        if self.native:
             self.session.reset_path_stats()
         else:
             self.path = {"graph_iters": 0, "eager_iters": 0, "graph_lengths": []}
@@ -203,13 +234,13 @@ class DistGpuPCG:
     def progress(self):
         """(sweeps reduced, exchanges packed, exchanges unpacked) from host-mapped device counters, or
         None.  Reads host memory only: safe from a watchdog thread while the main thread blocks."""
-        if self.comm_kind != "native":
+        if not self.native:
             return None
         v = self.session.progress(0)
         return None if v[0] < 0 else tuple(int(x) for x in v)
 
     def local_error_stats(self) -> dict:
-        if self.comm_kind == "native":
+        if self.native:
             return dict(self.session.error_norms())
         torch.cuda.synchronize(self.device)
         return dict(self.solver.error_norms(self._stream()))
@@ -219,7 +250,7 @@ class DistGpuPCG:
         return reduce_error_stats(self.local_error_stats(), self.problem, self.info, self.device)
 
     def tile(self) -> dict:
-        if self.comm_kind == "native":
+        if self.native:
             return self.session.tile
         return dict(ntiles=self.solver.ntiles, algo="pcg1" if self.single_pass else "pcg2")
 
@@ -244,7 +275,7 @@ class DistGpuPCG:
         self.solver.enqueue_halo_unpack(s)
 
     def init(self):
-        if self.comm_kind == "native":
+        if self.native:
             self.session.init()
             return
         s = self._stream()
@@ -260,7 +291,7 @@ class DistGpuPCG:
         torch.cuda.synchronize(self.device)
 
     def step(self, n: int):
-        if self.comm_kind == "native":
+        if self.native:
             self.session.step(n)
             return
         s = self._stream()
@@ -277,18 +308,18 @@ class DistGpuPCG:
                 self._exchange()
 
     def synchronize(self):
-        if self.comm_kind == "native":
+        if self.native:
             self.session.synchronize()
         torch.cuda.synchronize(self.device)
 
     def state(self) -> dict:
-        if self.comm_kind == "native":
+        if self.native:
             return self.session.state(0)
         return self.solver.read_state(self._stream())
 
     def local_w(self) -> np.ndarray:
         """This rank's interior block of w (nx x ny, fp64)."""
-        if self.comm_kind == "native":
+        if self.native:
             return self.session.local_w(0)
         return self.solver.download_w(self._stream())
 
@@ -296,7 +327,7 @@ class DistGpuPCG:
         """Per-phase times of n eager iterations (native path), reduced with MAX over ranks and
         mapped onto the reference's 5 stage-4 buckets (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:
         956-980).  Restarts the solver (init) first; values are seconds for the n iterations."""
-        if self.comm_kind == "native":
+        if self.native:
             self.session.init()
             ph = self.session.profile(int(n))
             vals = {"compute": ph["t_kernel_a"] + ph["t_kernel_b"], "copy": 0.0, "comm": ph["t_comm"],

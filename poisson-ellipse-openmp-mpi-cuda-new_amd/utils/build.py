@@ -39,6 +39,7 @@ HIP_SOURCES = [
     "hip/gpu_solver.hip",
     "hip/session.hip",
     "comm/comm.hip",
+    "comm/ipc_comm.hip",
 ]
 CPU_SOURCES = ["cpu/cpu_pcg.cpp"]
 BIND_SOURCES = ["bindings/module.cpp"]

@@ -49,7 +49,7 @@ def test_bench_torchrun_dry_run(n):
     assert len(lines) == 1, p.stdout  # rank 0 only
     _check(lines[0], n, 6, 2)
     assert lines[0]["config"]["parallelism"] == f"domain{n}"
-    pg = lines[0]["config"]["process_grid"]  # default split "auto": least ghost volume
+    pg = lines[0]["config"]["process_grid"]  # default split "auto": row strips while >= 128 rows, else least halo perimeter
     assert lines[0]["config"]["split"] == "auto" and pg[0] * pg[1] == n
 
 

@@ -1,9 +1,9 @@
 """bench.py multi-GPU supervision (CPU dry runs): the fallback ladder and the progress watchdog.
 
 The supervisor (bench.py itself, or one process per rank under torchrun) never touches the GPU; it
-starts the measuring ranks as fresh child processes, one rung of the ladder at a time:
-native RCCL + graphs + split sweep -> native eager -> torch.distributed.  Faults are injected with
-PMX_BENCH_FAULT ('<rung>:<hang|fail|crash>[@rank]'); a hang must be ended by the per-phase watchdog
+starts the measuring ranks as fresh child processes, one rung of the ladder at a time: native
+RCCL + graphs + split sweep -> native eager -> native IPC transport -> torch.distributed.  Faults
+are injected with PMX_BENCH_FAULT ('<rung>:<hang|fail|crash>[@rank]'); a hang must be ended by the per-phase watchdog
 (exit 87, phase printed) and the JSON must name the rung that produced it and the failed rungs.
 Reference rank lifecycle: stage4-mpi+cuda/poisson_mpi_cuda_f.cu:986-1039."""
 import json
@@ -82,7 +82,7 @@ def test_ladder_first_rung_success_records_path():
 
 
 def test_every_rung_failing_fails_the_job():
-    p = _spawned(2, "1:fail,2:fail,3:crash")
+    p = _spawned(2, "1:fail,2:fail,3:crash,4:fail")
     assert p.returncode != 0
     assert not [l for l in p.stdout.splitlines() if l.strip()]
     assert "every rung of the ladder failed" in p.stderr
@@ -93,8 +93,8 @@ def test_ladder_off_stops_at_the_first_rung():
     assert p.returncode != 0 and not p.stdout.strip()
 
 
-@pytest.mark.parametrize("comm,first", [("torch", 3)])
-def test_comm_torch_starts_at_rung_3(comm, first):
+@pytest.mark.parametrize("comm,first", [("torch", 4), ("ipc", 3)])
+def test_comm_flag_picks_the_first_rung(comm, first):
     p = _spawned(2, extra=("--comm", comm))
     assert p.returncode == 0, p.stderr[-3000:]
     j = _one_json(p)

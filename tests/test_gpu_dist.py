@@ -28,11 +28,12 @@ def gpu(pkg):
     assert torch.cuda.is_available() and pkg.load_native().device_count() > 0, "no HIP device"
 
 
-def _run(tmp_path, world, M, N, algo=-1, split="reference", dtype="fp64"):
-    out = str(tmp_path / f"w{world}_{algo}_{split}")
+def _run(tmp_path, world, M, N, algo=-1, split="reference", dtype="fp64", comm="torch", graph_batch=32):
+    out = str(tmp_path / f"w{world}_{algo}_{split}_{comm}_{graph_batch}")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), WORKER, "--M", str(M), "--N", str(N),
-           "--algo", str(algo), "--split", split, "--dtype", dtype, "--out", out]
+           "--algo", str(algo), "--split", split, "--dtype", dtype, "--out", out, "--comm", comm,
+           "--graph-batch", str(graph_batch)]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=170, env=env)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
@@ -68,7 +69,8 @@ def test_native_multiprocess_odd_blocks(pkg, tmp_path):
 
 
 def test_bench_share_gpu_rehearsal(tmp_path):
-    """bench.py --gpus 2 spawns its own ranks; --share-gpu runs them on GPU 0 (valid=false)."""
+    """bench.py --gpus 2 spawns its own ranks; --share-gpu runs them on GPU 0 over the IPC transport
+    (valid=false)."""
     p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--share-gpu", "--M", "512", "--N", "512",
                         "--steps", "20", "--warmup", "4", "--tol-time-cap", "60", "--profile-phases", "8"],
                        cwd=ROOT, capture_output=True, text=True, timeout=170)
@@ -77,8 +79,44 @@ def test_bench_share_gpu_rehearsal(tmp_path):
     assert len(lines) == 1
     j = lines[0]
     assert j["n_gpus"] == 2 and j["valid"] is False and j["tol_status"] == "converged"
-    assert j["config"]["comm"] == "gloo-host-staged" and j["config"]["tile"]["algo"] == "pcg1"
-    # phase buckets of the torch-comm path, MAX over the 2 ranks, table printed by rank 0 only
+    assert j["config"]["comm"] == "ipc" and j["config"]["tile"]["algo"] == "pcg1"
+    # phase buckets of the native session over the IPC transport, MAX over the 2 ranks, table printed
+    # by rank 0 only
     ph = j["phase_seconds_per_iter_max_over_ranks"]
     assert set(ph) == {"compute", "copy", "comm", "precond", "dot"} and ph["compute"] > 0 and ph["comm"] > 0
     assert p.stderr.count("max over ranks)") == 5
+
+
+@pytest.mark.parametrize("world,split,algo,expect", [
+    (2, "reference", -1, "pcg1"),
+    (3, "cols", 1, "pcg1"),
+    (4, "reference", 1, "pcg1"),    # corners: diagonal neighbours exchange through IPC too
+    (6, "auto", 1, "pcg1"),
+    (4, "reference", 2, "pcg2"),
+    (3, "rows", 2, "pcg2"),
+])
+def test_ipc_transport_matches_single_rank(pkg, tmp_path, world, split, algo, expect):
+    """The device-resident IPC transport (csrc/comm/ipc_comm.hip) between 2..6 processes on the one
+    GPU, graphs and (pcg1) the split sweep on: the same iterations as one rank and w to 1e-11."""
+    M, N = 400, 600
+    meta, w = _run(tmp_path, world, M, N, algo, split, comm="ipc")
+    assert meta["world"] == world and meta["algo"] == expect and meta["comm"] == "ipc"
+    assert meta["graph_iters"] > 0 and meta["eager_iters"] == 0  # every iteration replayed a graph
+    assert meta["split_sweep"] == (expect == "pcg1")
+    ref = pkg.solve(pkg.PoissonEllipse(M=M, N=N), "hip", ranks=1)
+    assert meta["iters"] == ref.iters == 546 and meta["status"] == "converged"
+    assert np.abs(w - ref.w).max() < 1e-11
+
+
+def test_ipc_transport_bitwise_equals_localcomm(pkg, tmp_path):
+    """Rank-ordered sums and exact ghost copies: 4 processes over IPC give bit-for-bit the solution
+    of one process driving the same 4 subdomains (LocalComm), eager and captured."""
+    M, N = 300, 500
+    p = pkg.PoissonEllipse(M=M, N=N)
+    s = pkg.make_session(p, ranks=4, split="reference")
+    st = s.solve(1)
+    ref = s.gather_local_w()
+    for gb in (0, 16):
+        meta, w = _run(tmp_path, 4, M, N, 1, "reference", comm="ipc", graph_batch=gb)
+        assert meta["iters"] == st["iters"]
+        assert np.array_equal(w, ref), (gb, np.abs(w - ref).max())

@@ -213,6 +213,12 @@ def test_bench_times_the_graph_path(pkg):
 
 def test_bench_share_gpu_rehearsal_supervised(pkg):
     j = _bench(["--gpus", "2", "--share-gpu", "--M", "512", "--N", "512", "--steps", "10", "--warmup", "2"])
-    assert j["n_gpus"] == 2 and j["config"]["rung"] == 1 and j["ladder"][0]["ok"]
-    assert j["config"]["comm"] == "gloo-host-staged" and j["valid"] is False
+    # RCCL refuses two ranks on one device: the rehearsal starts at the IPC transport (rung 3)
+    assert j["n_gpus"] == 2 and j["config"]["rung"] == 3 and j["ladder"][0]["ok"]
+    assert j["config"]["comm"] == "ipc" and j["valid"] is False
+    assert j["timed_path"] == "graph" and j["config"]["split_sweep"] is True
     assert j["tol_status"] == "converged" and j["l2_error"] > 0
+    g = _bench(["--gpus", "2", "--share-gpu", "--comm", "torch", "--M", "512", "--N", "512", "--steps", "10",
+                "--warmup", "2"])
+    assert g["config"]["rung"] == 4 and g["config"]["comm"] == "gloo-host-staged"
+    assert g["iters_to_tol"] == j["iters_to_tol"]
