@@ -3,6 +3,10 @@
 
     python bench/ab_env.py --shape 16384x16384 --shape 2048x16384 \
         --cfg base: --cfg s4:PMX_PCG1_SUPER=4 --rounds 3 --iters 200
+    python bench/ab_env.py --pkg old=bench/ab/pmx_base --cfg old@old: --cfg new: ...   # binary A/B
+
+A configuration `name@pkg:ENV` runs the package copy registered with --pkg pkg=DIR (a build of an
+earlier commit, e.g. from a git worktree, copied under bench/ab/; gitignored) in the same process.
 
 Every round runs every (shape, config) once, in the same process: set the environment, build a
 fresh 1-GPU session (the knobs are read when a solver is built), init, warm up, time `iters`
@@ -34,8 +38,14 @@ def main():
     ap.add_argument("--ranks", type=int, default=1, help="LocalComm subdomains on the one GPU")
     ap.add_argument("--split", default="auto")
     ap.add_argument("--tol", action="store_true")
+    ap.add_argument("--pkg", action="append", default=[], help="name=DIR: another copy of the package")
     a = ap.parse_args()
-    pkg = importlib.import_module("poisson-ellipse-openmp-mpi-cuda-new_amd")
+    pkgs = {"": importlib.import_module("poisson-ellipse-openmp-mpi-cuda-new_amd")}
+    for spec in a.pkg:
+        name, _, d = spec.partition("=")
+        d = os.path.abspath(d)
+        sys.path.insert(0, os.path.dirname(d))
+        pkgs[name] = importlib.import_module(os.path.basename(d))
     cfgs = []
     for c in a.cfg:
         name, _, kv = c.partition(":")
@@ -45,16 +55,17 @@ def main():
     shapes = [tuple(int(v) for v in s.split("x")) for s in a.shape]
     res = {}
 
-    def session(M, N, env):
+    def session(M, N, env, name):
         for k in knobs:
             os.environ.pop(k, None)
         os.environ.update(env)
+        pkg = pkgs[name.partition("@")[2]]
         return pkg.make_session(pkg.PoissonEllipse(M=M, N=N), ranks=a.ranks, split=a.split, dtype=a.dtype)
 
     for rnd in range(a.rounds):
         for (M, N) in shapes:
             for name, env in cfgs:
-                s = session(M, N, env)
+                s = session(M, N, env, name)
                 s.init()
                 s.step(a.warmup)
                 s.prepare(a.iters)
@@ -81,7 +92,7 @@ def main():
     if a.tol:
         for (M, N) in shapes:
             for name, env in cfgs:
-                s = session(M, N, env)
+                s = session(M, N, env, name)
                 t0 = time.perf_counter()
                 st = s.solve(4)
                 print(json.dumps(dict(M=M, N=N, cfg=name, iters=st["iters"], status=st["status"],

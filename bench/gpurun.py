@@ -82,6 +82,13 @@ STUDIES: dict[str, list[tuple[str, int, str]]] = {
                     "--cfg b2:PMX_PCG1_BANDS=2 --cfg b3:PMX_PCG1_BANDS=3 --cfg b4:PMX_PCG1_BANDS=4 "
                     "--rounds 3 --iters 200"),
     ],
+    # binary A/B against a build of the previous commit copied to bench/ab/pmx_base (gitignored)
+    "bin_ab": [
+        ("fp64", 600, "python -u bench/ab_env.py --pkg old=bench/ab/pmx_base --shape 16384x16384 "
+                      "--shape 2048x16384 --cfg old@old: --cfg new: --rounds 4 --iters 300"),
+        ("fp32", 600, "python -u bench/ab_env.py --pkg old=bench/ab/pmx_base --shape 16384x16384 "
+                      "--shape 32768x32768 --dtype fp32 --cfg old@old: --cfg new: --rounds 3 --iters 200"),
+    ],
     "profile_default": [
         ("rocprof_bench", 300, f"{ROCPROF} -d gpurun_out/profile_default/rp -o run -- "
                                + bench("--gpus 1 --steps 60 --warmup 10 --no-tol-solve")),
