@@ -83,6 +83,13 @@ STUDIES: dict[str, list[tuple[str, int, str]]] = {
                     "--rounds 3 --iters 200"),
     ],
     # binary A/B against a build of the previous commit copied to bench/ab/pmx_base (gitignored)
+    "bin_ab_tests": [
+        ("pytest_pcg1", 600, f"{PYTEST} tests/test_gpu_pcg1.py tests/test_gpu_solver.py tests/test_gpu_launch_path.py"),
+        ("fp64", 600, "python -u bench/ab_env.py --pkg old=bench/ab/pmx_base --shape 16384x16384 "
+                      "--shape 2048x16384 --cfg old@old: --cfg new: --rounds 4 --iters 300"),
+        ("fp32", 600, "python -u bench/ab_env.py --pkg old=bench/ab/pmx_base --shape 16384x16384 "
+                      "--shape 32768x32768 --dtype fp32 --cfg old@old: --cfg new: --rounds 3 --iters 200"),
+    ],
     "bin_ab": [
         ("fp64", 600, "python -u bench/ab_env.py --pkg old=bench/ab/pmx_base --shape 16384x16384 "
                       "--shape 2048x16384 --cfg old@old: --cfg new: --rounds 4 --iters 300"),

@@ -208,14 +208,16 @@ GpuOptions make_options(int device, const std::string& kernel, int block, int ve
 
 PYBIND11_MODULE(_pmx, m) {
   m.doc() = "pmx: MI355X-native fictitious-domain Poisson PCG (native core)";
+  // module-local types: a second copy of the package (an older build, bench/ab_env.py --pkg) can be
+  // imported into the same process for same-box binary A/B runs
   py::register_exception<pmx::Error>(m, "PmxError", PyExc_RuntimeError);
 
-  py::enum_<Norm>(m, "Norm").value("weighted", Norm::kWeighted).value("unweighted", Norm::kUnweighted);
-  py::enum_<Split>(m, "Split")
+  py::enum_<Norm>(m, "Norm", py::module_local()).value("weighted", Norm::kWeighted).value("unweighted", Norm::kUnweighted);
+  py::enum_<Split>(m, "Split", py::module_local())
       .value("reference", Split::kReference).value("auto", Split::kAuto)
       .value("rows", Split::kRows).value("cols", Split::kCols);
 
-  py::class_<ProblemSpec>(m, "ProblemSpec")
+  py::class_<ProblemSpec>(m, "ProblemSpec", py::module_local())
       .def(py::init<>())
       .def_readwrite("M", &ProblemSpec::M).def_readwrite("N", &ProblemSpec::N)
       .def_readwrite("A1", &ProblemSpec::A1).def_readwrite("B1", &ProblemSpec::B1)
@@ -331,7 +333,7 @@ PYBIND11_MODULE(_pmx, m) {
     return max_square_grid(bytes_per_gpu, gpus, dtype == "fp64" ? DType::kFp64 : DType::kFp32, reserve);
   }, py::arg("bytes_per_gpu"), py::arg("gpus"), py::arg("dtype") = "fp64", py::arg("reserve") = 0.1);
 
-  py::class_<OpContext>(m, "OpContext")
+  py::class_<OpContext>(m, "OpContext", py::module_local())
       .def(py::init<const ProblemSpec&, int, int, int, int64_t, int>(), py::arg("spec"),
            py::arg("Px"), py::arg("Py"), py::arg("rank"), py::arg("pitch"), py::arg("device") = 0)
       .def("subdomain", &OpContext::subdomain)
@@ -341,7 +343,7 @@ PYBIND11_MODULE(_pmx, m) {
       .def("dot", &OpContext::dot);
 
   // Single subdomain solver on caller-chosen streams/arena (Python-orchestrated comm path).
-  py::class_<GpuSubdomainSolver>(m, "SubdomainSolver")
+  py::class_<GpuSubdomainSolver>(m, "SubdomainSolver", py::module_local())
       .def(py::init([](const ProblemSpec& s, int Px, int Py, int rank, int device,
                        const std::string& kernel, int block, int vec, int waves, int tile_rows,
                        const std::string& dtype, bool exact, uintptr_t arena, bool check, int vec_b,
@@ -390,7 +392,7 @@ PYBIND11_MODULE(_pmx, m) {
       .def_property_readonly("device_bytes", &GpuSubdomainSolver::device_bytes)
       .def_property_readonly("ntiles", [](GpuSubdomainSolver& g) { return g.tiles().ntiles(); });
 
-  py::class_<Session>(m, "Session")
+  py::class_<Session>(m, "Session", py::module_local())
       .def(py::init([](const ProblemSpec& s, int world, const std::string& comm, Split split,
                        int device, const std::string& kernel, int block, int vec, int waves,
                        int tile_rows, const std::string& dtype, bool exact, int graph_batch,

@@ -92,6 +92,8 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_ALGO", o.algo);
   env_int("PMX_PCG1_VEC", o.vec1);
   env_int("PMX_PCG1_ROWS", o.rows1);
+  env_int("PMX_PCG1_ROWS_W", o.rows1w);
+  env_int("PMX_PCG1_PF_W", o.pf1w);
   env_int("PMX_PCG1_WAVES", o.waves1);
   env_int("PMX_PCG1_PF", o.pf1);
   env_int("PMX_PCG1_ORDER", o.order1);
@@ -239,15 +241,29 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     tiles1_.super = opt_.super1;
     tiles1_.bands = opt_.bands1;
     tiles1_.alt = opt_.alt1 >= 0 ? opt_.alt1 : (opt_.super1 > 0 ? 1 : 0);
-    if (opt_.order1) {  // ellipse-cut tiles first (their 3-5x longer tiles would trail the sweep)
-      HIP_CHECK(hipMalloc(&tile_order_, 2 * size_t(tiles1_.ntiles()) * sizeof(int)));
-      slow_tiles_ = pcg1_build_order(G, tables_, tiles1_, tile_order_, nullptr);
+    tiles1w_ = make_pcg1_tiles(G, opt_.vec1, opt_.waves1, opt_.rows1w ? opt_.rows1w : tiles1_.rows,
+                               opt_.pf1w ? opt_.pf1w : tiles1_.pf, int(elem_));
+    tiles1w_.super = tiles1_.super;
+    tiles1w_.bands = tiles1_.bands;
+    tiles1w_.alt = tiles1_.alt;
+    const bool same_w = tiles1w_.rows == tiles1_.rows;
+    // dispatch order tables with the tiles' row classes; order1: the ellipse-cut tiles first
+    // within each XCD's share (their 3-5x longer tiles would trail the sweep)
+    HIP_CHECK(hipMalloc(&tile_order_, 3 * size_t(tiles1_.ntiles()) * sizeof(Pcg1Slot)));
+    slow_tiles_ = pcg1_build_order(G, tables_, tiles1_, tile_order_, opt_.order1 != 0, nullptr);
+    if (same_w) {
+      tiles1w_.order0 = tiles1_.order0;
+      tiles1w_.order1 = tiles1_.order1;
+      tiles1w_.order2 = tiles1_.order2;
+    } else {
+      HIP_CHECK(hipMalloc(&tile_order_w_, 3 * size_t(tiles1w_.ntiles()) * sizeof(Pcg1Slot)));
+      (void)pcg1_build_order(G, tables_, tiles1w_, tile_order_w_, opt_.order1 != 0, nullptr);
     }
   }
 
   init_tiles_ = make_tiles(G, 256, 0);
   const size_t npart = size_t(std::max({tiles_.ntiles(), tiles_b_.ntiles(), init_tiles_.ntiles(),
-                                        pcg1_ ? tiles1_.ntiles() : 0}));
+                                        pcg1_ ? std::max(tiles1_.ntiles(), tiles1w_.ntiles()) : 0}));
   npart_ = npart;
   HIP_CHECK(hipMalloc(&partials_, (npart * 5 + kReduceWsDoubles) * sizeof(double)));
   reduce_ws_ = partials_ + npart * 5;
@@ -330,6 +346,7 @@ void GpuSubdomainSolver::release() noexcept {
   if (fields_) (void)hipFree(fields_);
   if (r2_) (void)hipFree(r2_);
   if (tile_order_) (void)hipFree(tile_order_);
+  if (tile_order_w_) (void)hipFree(tile_order_w_);
   if (tables_buf_) (void)hipFree(tables_buf_);
   if (partials_) (void)hipFree(partials_);
   if (own_arena_ && arena_) (void)hipFree(arena_);
@@ -339,7 +356,7 @@ void GpuSubdomainSolver::release() noexcept {
   fields_ = r2_ = nullptr;
   arena_ = nullptr;
   tables_buf_ = partials_ = nullptr;
-  tile_order_ = nullptr;
+  tile_order_ = tile_order_w_ = nullptr;
   host_state_ = nullptr;
 }
 
@@ -466,7 +483,7 @@ void GpuSubdomainSolver::phase_a_kernel_only(hipStream_t s, int part) {
   if (pcg1_)
     launch_pcg1<T>(geom_, tables_, static_cast<T*>(field_base(0)), static_cast<T*>(field_base(1)),
                    reinterpret_cast<T*>(r2_ + field_off_ * elem_), static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), partials_, state_,
-                   tiles1_, s, part, w_sweep_next());
+                   tiles1_for(w_sweep_next()), s, part, w_sweep_next());
   else if (tiles_.kind == 1)
     launch_pcg_a_wave<T>(geom_, tables_, static_cast<const T*>(field_base(1)),
                          static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(),
@@ -523,7 +540,9 @@ void GpuSubdomainSolver::enqueue_reduce_a(hipStream_t s) {
   if (pcg1_) {
     const double h = g_.h1h2, wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
     const double wts[5] = {h, h, h, h, wdiff};
-    launch_reduce_n(partials_, tiles1_.ntiles(), 5, wts, state_->red_c, state_, kSkipIfDone | kBumpIter,
+    // the sweep just enqueued (host_k not bumped yet) wrote one partial per tile of its tiling
+    launch_reduce_n(partials_, tiles1_for(w_sweep_next()).ntiles(), 5, wts, state_->red_c, state_,
+                    kSkipIfDone | kBumpIter,
                     reduce_ws_, s, progress_dev_);
     ++host_k_;  // mirrors the S->it bump (see host_k())
     after_launch(s);

@@ -36,6 +36,8 @@
 // exchanged: they only feed columns/rows that are not owned, which are neither stored nor summed.
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "pcg_device.hpp"
@@ -50,6 +52,11 @@ using namespace dev;
 namespace {
 
 constexpr int kNq = 5;  // rho, (Az,z), (Az,p), (Ap,p), |p|^2
+#ifdef PMX_PCG1_REVERSE
+constexpr bool kPcg1Reverse = true;
+#else
+constexpr bool kPcg1Reverse = false;
+#endif
 constexpr int kPcg1AutoPf = 1;
 
 #ifdef PMX_WAVE_TRACE
@@ -124,6 +131,17 @@ __device__ __forceinline__ void coef(const RowCo& c, const DevTables& Tb, const 
   }
 }
 
+// f(integral_constant<int, 0>) && f(integral_constant<int, 1>) && ... (N calls at most, stops at
+// the first false): a loop body whose step number is a compile-time constant
+template <typename F, int... I>
+__device__ __forceinline__ bool static_for_while_impl(F&& f, std::integer_sequence<int, I...>) {
+  return (f(std::integral_constant<int, I>{}) && ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ bool static_for_while(F&& f) {
+  return static_for_while_impl(f, std::make_integer_sequence<int, N>{});
+}
+
 template <typename T, int VEC>
 struct Pcg1Row {
   T r[VEC], p[VEC], w[VEC], q[VEC];  // q: p^{k-2} (WM 3 only)
@@ -150,7 +168,8 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
                                            const T* __restrict__ pold,
                                            T* pnew, int i0, int i1, int j0, int j1,
                                            double alpha, double beta, double c1, double c2,
-                                           double (&acc)[kNq], double* __restrict__ scol) {
+                                           double (&acc)[kNq], double* __restrict__ scol,
+                                           unsigned long long cls, bool use_cls) {
   constexpr bool WUP = WM != 0;
   const int64_t P = G.pitch;
   const int lane = threadIdx.x & 63;
@@ -173,6 +192,11 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   for (int u = 0; u < VEC; ++u) own_any |= own[u];
   const int gjlo = max(G.gj0 + j0 - 2, 0), gjhi = min(G.gj0 + j0 - 2 + 64 * VEC - 1, G.N);
   auto grow = [&](int m) { return min(max(G.gi0 + m, 0), G.M); };  // table row of local row m
+  // row m's class: from the slot's bits (Pcg1Slot) or from the tables
+  auto row_of = [&](int m) {
+    if (DIR > 0 && use_cls) return RowCo{grow(m), int((cls >> (2 * (m - i0 + 3))) & 3ull)};
+    return row_co(Tb, grow(m), gjlo, gjhi);
+  };
   auto interior_row = [&](int m) { return G.gi0 + m >= 1 && G.gi0 + m <= G.M - 1; };
 
   auto fetch = [&](int m, Pcg1Row<T, VEC>& b) {
@@ -192,7 +216,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   double Pm2[VEC], Pm1[VEC], Zm3[VEC], Zm2[VEC], ro1[VEC], po1[VEC], po2[VEC];
 #pragma unroll
   for (int u = 0; u < VEC; ++u) Pm2[u] = Pm1[u] = Zm3[u] = Zm2[u] = ro1[u] = po1[u] = po2[u] = 0.0;
-  RowCo cB = row_co(Tb, grow(DIR > 0 ? i0 - 3 : i1 + 3), gjlo, gjhi);  // rows m-DIR, m-2 DIR
+  RowCo cB = row_of(DIR > 0 ? i0 - 3 : i1 + 3);  // rows m-DIR, m-2 DIR
   RowCo cC = cB;
   bool parked = false;  // column constants in LDS (see col_lds)
   auto park_cols = [&]() {
@@ -215,7 +239,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     fetch(DIR > 0 ? min(m + PF, mlast) : max(m - PF, mlast), nxt);
     // ---- stage A: p^k of row m
     const bool rowA = FAST || interior_row(m);
-    const RowCo cA = row_co(Tb, grow(m), gjlo, gjhi);
+    const RowCo cA = row_of(m);
     if (cA.ucls == 0 && !parked) park_cols();
     double Pm[VEC], rom[VEC], pom[VEC];
 #pragma unroll
@@ -359,7 +383,7 @@ constexpr int pcg1_min_waves() {
 struct Pcg1Part {
   int part;  // 0 all, 1 interior rectangle, 2 frame
   int tiles_i, ti_lo, ti_hi, tj_lo, tj_hi;
-  const int* order;  // position -> tile id (pcg1_build_order), or nullptr: pcg1_tile's order
+  const Pcg1Slot* order;  // position -> tile + row classes (pcg1_build_order), or nullptr: pcg1_tile's order
   int count;         // tiles of this launch
   int alt;           // 1: tiles with even ti march bottom-up, 2: every tile (TileCfg::alt)
 };
@@ -410,9 +434,11 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
   const CState* Sc = (const CState*)S;  // NOLINT: address-space cast
   asm volatile("" ::"s"(S), "s"(part.order), "s"(part.count), "s"(gridDim.x));  // kernel arguments: one batch
   const int pos = xcd_remap(blockIdx.x, gridDim.x) * WAVES + __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
-  // branch-free: without an order the load reads a valid dummy (the state's first word)
-  const int* obase = part.order ? part.order : reinterpret_cast<const int*>(S);
-  const int ord = ld_uniform(obase, part.order ? min(pos, part.count - 1) : 0);
+  // branch-free: without an order the load reads a valid dummy (the state's first 16 bytes)
+  const Pcg1Slot* obase = part.order ? part.order : reinterpret_cast<const Pcg1Slot*>(S);
+  const int oi = part.order ? min(pos, part.count - 1) : 0;
+  const int ord = ld_uniform(&obase[oi].id, 0);
+  const unsigned long long ocls = ld_uniform(&obase[oi].cls, 0);
   const int st_done = Sc->done;
   const long long k = Sc->it;  // 0 = the init sweep (alpha = beta = 0: sums of r^0, z^0 only)
   double rc[kNq], al[4], be[4];
@@ -433,7 +459,7 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
   };
   // every value above is consumed here, so the compiler issues all those loads as one batch
   // instead of sinking each below the branch that first needs it
-  asm volatile("" ::"s"(st_done), "s"(k), "s"(ord), "s"(rc[0]), "s"(rc[1]), "s"(rc[2]), "s"(rc[3]), "s"(rc[4]),
+  asm volatile("" ::"s"(st_done), "s"(k), "s"(ord), "s"(ocls), "s"(rc[0]), "s"(rc[1]), "s"(rc[2]), "s"(rc[3]), "s"(rc[4]),
                "s"(al[0]), "s"(al[1]), "s"(al[2]), "s"(al[3]), "s"(be[0]), "s"(be[1]), "s"(be[2]), "s"(be[3]),
                "s"(zr0), "s"(zr1), "s"(s_delta), "s"(s_bd_tol), "s"(s_pmb), "s"(s_max_iter), "s"(s_norm), "s"(cyc));
   if (st_done) return;
@@ -539,16 +565,25 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
   // strictly inside the global domain (no Dirichlet node in reach)
   const bool fast = VEC == 2 && j1 == j0 + WO - 1 && G.gi0 + i0 - 2 >= 1 && G.gi0 + i1 + 2 <= G.M - 1 &&
                     G.gj0 + j0 - 2 >= 1 && G.gj0 + j0 + 64 * VEC - 3 <= G.N - 1;
+  const bool use_cls = part.order != nullptr && TI + 5 <= 64 / 2;  // 2 bits for each of the TI+5 rows
+#ifdef PMX_PCG1_REVERSE
+  // study build only (NOTES #46-#47: bottom-up marches lose ~4%): tiles with even ti (alt 1) or
+  // every tile (alt 2) march bottom-up
   const bool rev = part.alt == 2 || (part.alt == 1 && !(ti & 1));  // a function of the tile alone
 #define PMX_MARCH(E, F)                                                                                   \
   do {                                                                                                   \
     if (rev)                                                                                             \
       pcg1_march<T, VEC, PF, E, F, -1>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, \
-                                       acc, scol);                                                       \
+                                       acc, scol, ocls, use_cls);                                                       \
     else                                                                                                 \
       pcg1_march<T, VEC, PF, E, F, 1>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2,  \
-                                      acc, scol);                                                        \
+                                      acc, scol, ocls, use_cls);                                                        \
   } while (0)
+#else
+#define PMX_MARCH(E, F) \
+  pcg1_march<T, VEC, PF, E, F, 1>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, acc, scol, \
+                                  ocls, use_cls)
+#endif
 #define PMX_MARCH_W(F)                                     \
   if constexpr (!WS) {                                     \
     PMX_MARCH(0, F);                                       \
@@ -698,12 +733,13 @@ k_reduce_n(const double* __restrict__ part, int n, ReduceWeights wt, double* out
   }
 }
 
-// 1 = the tile marches a row whose coefficient class over the tile's loaded columns is "cut"
-// (row_class 0): those rows rebuild every face from the tables, and such a tile takes 3-5x the
-// median tile time (profiles/r2/small_shapes/README.md, wave traces).  One thread per tile, the
-// same rows and column window as pcg1_march.
-__global__ void k_pcg1_tile_cut(DevGeom G, DevTables Tb, int TI, int tiles_i, int tiles_j, int vec,
-                                unsigned char* cut) {
+// Per tile: the coefficient class of each row its march visits (rows i0-3 .. i1+2 over the tile's
+// loaded columns, 2 bits per row, see Pcg1Slot) and whether any of them is "cut" (class 0: those
+// rows rebuild every face from the tables, and such a tile takes 3-5x the median tile time,
+// profiles/r2/small_shapes/README.md).  One thread per tile, the same rows and column window as
+// pcg1_march.
+__global__ void k_pcg1_tile_classes(DevGeom G, DevTables Tb, int TI, int tiles_i, int tiles_j, int vec,
+                                    unsigned long long* cls, unsigned char* cut) {
   const int id = int(blockIdx.x * blockDim.x + threadIdx.x);
   if (id >= tiles_i * tiles_j) return;
   const int ti = id / tiles_j, tj = id - ti * tiles_j;
@@ -711,7 +747,8 @@ __global__ void k_pcg1_tile_cut(DevGeom G, DevTables Tb, int TI, int tiles_i, in
   const int j0 = 1 + tj * (64 * vec - 4);
   const int gjlo = max(G.gj0 + j0 - 2, 0), gjhi = min(G.gj0 + j0 - 2 + 64 * vec - 1, G.N);
   unsigned char c = 0;
-  for (int m = i0 - 3; m <= i1 + 2 && !c; ++m) {
+  unsigned long long bits = 0;
+  for (int m = i0 - 3; m <= i1 + 2; ++m) {
     const int gi = min(max(G.gi0 + m, 0), G.M);
     RowConst rc;
     for (int q = 0; q < 4; ++q) {
@@ -719,32 +756,42 @@ __global__ void k_pcg1_tile_cut(DevGeom G, DevTables Tb, int TI, int tiles_i, in
       rc.ca1[q] = Tb.acls[4 * (gi + 1) + q];
       rc.cb[q] = Tb.bcls[4 * gi + q];
     }
-    c = row_class(rc, gjlo, gjhi) == 0;
+    const int u = row_class(rc, gjlo, gjhi);
+    c |= u == 0;
+    const int r = m - (i0 - 3);
+    if (r < 32) bits |= static_cast<unsigned long long>(u) << (2 * r);
   }
   cut[id] = c;
+  cls[id] = bits;
 }
 
 }  // namespace
 
-int pcg1_build_order(const DevGeom& G, const DevTables& Tb, TileCfg& tc, int* d_order, hipStream_t s) {
-  tc.order0 = tc.order1 = nullptr;
+int pcg1_build_order(const DevGeom& G, const DevTables& Tb, TileCfg& tc, Pcg1Slot* d_order, bool slow_first,
+                     hipStream_t s) {
+  tc.order0 = tc.order1 = tc.order2 = nullptr;
   const int n = tc.ntiles();
   if (tc.waves != 1 || n == 0) return 0;
   unsigned char* d_cut = nullptr;
+  unsigned long long* d_cls = nullptr;
   HIP_CHECK(hipMalloc(&d_cut, size_t(n)));
-  hipLaunchKernelGGL(k_pcg1_tile_cut, dim3((n + 255) / 256), dim3(256), 0, s, G, Tb, tc.rows, tc.tiles_i,
-                     tc.tiles_j, tc.vec, d_cut);
+  HIP_CHECK(hipMalloc(&d_cls, size_t(n) * sizeof(unsigned long long)));
+  hipLaunchKernelGGL(k_pcg1_tile_classes, dim3((n + 255) / 256), dim3(256), 0, s, G, Tb, tc.rows, tc.tiles_i,
+                     tc.tiles_j, tc.vec, d_cls, d_cut);
   HIP_CHECK(hipGetLastError());
   std::vector<unsigned char> cut(static_cast<size_t>(n));
+  std::vector<unsigned long long> cls(static_cast<size_t>(n));
   HIP_CHECK(hipMemcpyAsync(cut.data(), d_cut, size_t(n), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipMemcpyAsync(cls.data(), d_cls, size_t(n) * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
   HIP_CHECK(hipFree(d_cut));
-  std::vector<int> order(2 * size_t(n), 0);
+  HIP_CHECK(hipFree(d_cls));
+  std::vector<Pcg1Slot> order(3 * size_t(n), Pcg1Slot{0, 0, 0ull});
   int nslow = 0;
-  for (int part = 0; part <= 1; ++part) {
+  for (int part = 0; part <= 2; ++part) {
     const Pcg1Part P{part, tc.tiles_i, tc.ti_lo, tc.ti_hi, tc.tj_lo, tc.tj_hi, nullptr, 0, 0};
-    const int count = part == 0 ? n : tc.interior_tiles();
-    int* o = order.data() + size_t(part) * n;
+    const int count = part == 0 ? n : part == 1 ? tc.interior_tiles() : n - tc.interior_tiles();
+    Pcg1Slot* o = order.data() + size_t(part) * n;
     // positions of XCD x (xcd_remap with one wave per workgroup): [x (q+1), ...) as in xcd_remap
     const int q = count / 8, r = count % 8;
     const int S = std::max(1, tc.super);
@@ -759,11 +806,12 @@ int pcg1_build_order(const DevGeom& G, const DevTables& Tb, TileCfg& tc, int* d_
         PMX_CHECK(pcg1_tile(k, P, tc.tiles_j, ti, tj), "pcg1_build_order: tile enumeration");
         ids.push_back(ti * tc.tiles_j + tj);
       }
-      std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) {
-        const int ta = a / tc.tiles_j, tb = b / tc.tiles_j;
-        const int ka[3] = {ta / S, a % tc.tiles_j, ta % S}, kb[3] = {tb / S, b % tc.tiles_j, tb % S};
-        return std::lexicographical_compare(ka, ka + 3, kb, kb + 3);
-      });
+      if (S > 1)
+        std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) {
+          const int ta = a / tc.tiles_j, tb = b / tc.tiles_j;
+          const int ka[3] = {ta / S, a % tc.tiles_j, ta % S}, kb[3] = {tb / S, b % tc.tiles_j, tb % S};
+          return std::lexicographical_compare(ka, ka + 3, kb, kb + 3);
+        });
       // bands > 1: the chunk's tiles split into `bands` consecutive runs dispatched round-robin, so
       // a tile's lower neighbour starts ~bands tile rows of dispatches later (a lag closer to the
       // time the upper tile reaches the rows they share)
@@ -774,23 +822,24 @@ int pcg1_build_order(const DevGeom& G, const DevTables& Tb, TileCfg& tc, int* d_
         const size_t per = (ids.size() + B - 1) / B;
         for (size_t k = 0; k < per; ++k)
           for (int b = 0; b < B; ++b)
-            if (b * per + k < ids.size() && k < per) il.push_back(ids[b * per + k]);
+            if (b * per + k < ids.size()) il.push_back(ids[b * per + k]);
         ids.swap(il);
       }
       int w = start;
-      for (int pass = 0; pass < 2; ++pass)  // slow tiles first, then the rest, each in that order
+      for (int pass = 0; pass < (slow_first ? 2 : 1); ++pass)  // slow tiles first, then the rest
         for (int id : ids)
-          if ((cut[size_t(id)] != 0) == (pass == 0)) {
-            o[w++] = id;
-            if (pass == 0 && part == 0) ++nslow;
+          if (!slow_first || (cut[size_t(id)] != 0) == (pass == 0)) {
+            o[w++] = Pcg1Slot{id, 0, cls[size_t(id)]};
+            if (slow_first && pass == 0 && part == 0) ++nslow;
           }
       start += len;
     }
   }
-  HIP_CHECK(hipMemcpyAsync(d_order, order.data(), order.size() * sizeof(int), hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(d_order, order.data(), order.size() * sizeof(Pcg1Slot), hipMemcpyHostToDevice, s));
   HIP_CHECK(hipStreamSynchronize(s));
   tc.order0 = d_order;
   tc.order1 = d_order + n;
+  tc.order2 = d_order + 2 * size_t(n);
   return nslow;
 }
 
@@ -844,7 +893,7 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
   PMX_CHECK(part >= 0 && part <= 2, "launch_pcg1: part must be 0, 1 or 2");
   const int count = part == 0 ? tc.ntiles() : part == 1 ? tc.interior_tiles() : tc.ntiles() - tc.interior_tiles();
   const Pcg1Part P{part, tc.tiles_i, tc.ti_lo, tc.ti_hi, tc.tj_lo, tc.tj_hi,
-                   tc.waves == 1 ? (part == 0 ? tc.order0 : part == 1 ? tc.order1 : nullptr) : nullptr, count,
+                   tc.waves == 1 ? (part == 0 ? tc.order0 : part == 1 ? tc.order1 : tc.order2) : nullptr, count,
                    tc.alt};
   if (count == 0) return;
   PMX_CHECK(G.nb == 0 || (G.nx >= 2 && G.ny >= 2), "pcg1 on a decomposed grid needs subdomains >= 2 x 2");
@@ -859,17 +908,22 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
       hipLaunchKernelGGL((k_pcg1<T, V, WV, PF, false>), dim3(nb), dim3(bs), 0, s, G, Tb, w, r, r2, p0,   \
                          p1, partials, S, tc.rows, tc.tiles_j, tc.ntiles(), P);                          \
   } while (0)
-  // instantiated shapes: the default (VEC 2, 1 wave, prefetch 1) and the ones the sweeps still
-  // compare against (prefetch 2-4; 2 or 4 waves per workgroup; VEC 4)
-  if (tc.vec == 2 && tc.waves == 1) {
-    if (tc.pf == 1) PMX_PCG1(2, 1, 1);
-    else if (tc.pf == 2) PMX_PCG1(2, 1, 2);
-    else if (tc.pf == 3) PMX_PCG1(2, 1, 3);
-    else PMX_PCG1(2, 1, 4);
-  }
+  // instantiated shapes: the default (VEC 2, 1 wave, prefetch 1) and prefetch 2.  The other
+  // shapes of the round-1/2 sweeps (prefetch 3-4, 2 or 4 waves per workgroup, VEC 4: all slower,
+  // NOTES #23, #40) need a PMX_PCG1_ALL_SHAPES build
+  PMX_CHECK(tc.alt == 0 || kPcg1Reverse, "pcg1: alternating march directions need a PMX_PCG1_REVERSE build");
+  if (tc.vec == 2 && tc.waves == 1 && tc.pf == 1) PMX_PCG1(2, 1, 1);
+  else if (tc.vec == 2 && tc.waves == 1 && tc.pf == 2) PMX_PCG1(2, 1, 2);
+#ifdef PMX_PCG1_ALL_SHAPES
+  else if (tc.vec == 2 && tc.waves == 1 && tc.pf == 3) PMX_PCG1(2, 1, 3);
+  else if (tc.vec == 2 && tc.waves == 1) PMX_PCG1(2, 1, 4);
   else if (tc.vec == 2 && tc.waves == 4) PMX_PCG1(2, 4, 1);
   else if (tc.vec == 2 && tc.waves == 2) PMX_PCG1(2, 2, 1);
   else PMX_PCG1(4, 1, 1);
+#else
+  else PMX_CHECK(false, "pcg1 shape vec " << tc.vec << " x " << tc.waves << " waves, prefetch " << tc.pf
+                                          << " is only instantiated in a PMX_PCG1_ALL_SHAPES build");
+#endif
 #undef PMX_PCG1
   HIP_CHECK(hipGetLastError());
 }

@@ -75,6 +75,9 @@ struct GpuOptions {
   // pcg1 tile shape (rows1 = 0: auto).  VEC=2 x 1 wave/workgroup won the 16384^2 sweeps
   // (bench/gpu_pcg1_sweep.sh; VEC=4 needs 256 VGPRs and is 35% slower).
   int vec1 = 2, waves1 = 1, rows1 = 0;
+  // the w-moving sweep (one in w_cycle, a kernel of its own at 3 waves/SIMD) may use its own tile
+  // height and prefetch depth: 0 = as the plain sweep (PMX_PCG1_ROWS_W, PMX_PCG1_PF_W)
+  int rows1w = 0, pf1w = 0;
   // pcg1 prefetch depth: rows loaded ahead of the row being computed (1..4).  The sweep is
   // latency-bound at 2 waves/SIMD; deeper prefetch spends VGPRs that occupancy does not use.
   int pf1 = 0;  // 0 = auto
@@ -242,6 +245,8 @@ class GpuSubdomainSolver {
   TileCfg tiles_{};    // pcg_a
   TileCfg tiles_b_{};  // pcg_b
   TileCfg tiles1_{};   // pcg1
+  TileCfg tiles1w_{};  // pcg1, the w-moving sweeps (GpuOptions::rows1w / pf1w)
+  const TileCfg& tiles1_for(bool wsweep) const { return wsweep ? tiles1w_ : tiles1_; }
   bool pcg1_ = false;
   long long host_k_ = 0;
   TileCfg init_tiles_{};
@@ -256,7 +261,8 @@ class GpuSubdomainSolver {
   char* arena_ = nullptr;
   bool own_arena_ = true;
   PcgState* state_ = nullptr;
-  int* tile_order_ = nullptr;  // pcg1 dispatch order (pcg1_build_order)
+  Pcg1Slot* tile_order_ = nullptr;    // pcg1 dispatch order + row classes (pcg1_build_order)
+  Pcg1Slot* tile_order_w_ = nullptr;  // ... of tiles1w_ when its shape differs
   int slow_tiles_ = 0;
 #ifdef PMX_WAVE_TRACE
   void* wtrace_ = nullptr;

@@ -16,6 +16,16 @@
 
 namespace pmx {
 
+// One dispatch slot of a pcg1 order table: the tile, and the coefficient class (2 bits: 0 cut,
+// 1 all faces inside D, 2 all outside) of each row r = 0..31 the tile's march visits, row r being
+// local row i0 - 3 + r (the pipeline's initial row, then rows i0-2 .. i1+2).  With the classes in
+// the slot a wave finds a row's class with a shift instead of ~11 scalar loads and ~20 compares.
+struct Pcg1Slot {
+  int id;
+  int pad;
+  unsigned long long cls;
+};
+
 struct TileCfg {
   int kind = 0;       // 0: workgroup tile + LDS row ring (pcg_kernels.hip)
                       // 1: wave tile + DPP lane shifts, software-pipelined register ring
@@ -35,8 +45,9 @@ struct TileCfg {
   // kind 3: dispatch order of the whole-grid (order0) and interior (order1) launches: position
   // -> tile id, the tiles the ellipse cuts first within each XCD's share (pcg1_build_order);
   // nullptr = natural order
-  const int* order0 = nullptr;
-  const int* order1 = nullptr;
+  const Pcg1Slot* order0 = nullptr;
+  const Pcg1Slot* order1 = nullptr;
+  const Pcg1Slot* order2 = nullptr;  // the frame tiles
   // kind 3 halo-row reuse: tiles with even ti march bottom-up (alt), and the order tables dispatch
   // `super` vertically adjacent tiles (a super-row) back to back, column by column, so the pair
   // across each inner boundary reads its shared halo rows at the same time (0 = row-major order)
@@ -100,9 +111,11 @@ void launch_pcg_b_wave(const DevGeom& G, const DevTables& Tb, T* w, T* r, const 
 // wsweep: launch the kernel that moves w; it must be set exactly on the sweeps k >= 1 with
 // k % S->w_cycle == 0 (the caller mirrors the device iteration counter; a mismatch stops the solve
 // with status breakdown and the NaN flag).
-// Builds tc.order0/order1 in d_order (2 * tc.ntiles() ints): within each XCD's share of the
-// positions, the tiles with cut (slow-path) rows are dispatched first.  Returns their count.
-int pcg1_build_order(const DevGeom& G, const DevTables& Tb, TileCfg& tc, int* d_order, hipStream_t s);
+// Builds tc.order0/order1/order2 in d_order (3 * tc.ntiles() slots): per launch part, the tiles of
+// each XCD's share of the positions with their row classes; slow_first: the tiles with cut
+// (slow-path) rows go first within each share.  Returns the number of such tiles.
+int pcg1_build_order(const DevGeom& G, const DevTables& Tb, TileCfg& tc, Pcg1Slot* d_order, bool slow_first,
+                     hipStream_t s);
 
 template <typename T>
 void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1,
