@@ -83,6 +83,21 @@ STUDIES: dict[str, list[tuple[str, int, str]]] = {
                     "--rounds 3 --iters 200"),
     ],
     # binary A/B against a build of the previous commit copied to bench/ab/pmx_base (gitignored)
+    "pf_ab": [
+        ("fp64", 600, "python -u bench/ab_env.py --shape 16384x16384 --shape 2048x16384 --cfg base: "
+                      "--cfg pf2:PMX_PCG1_PF=2 --cfg pf2w1:PMX_PCG1_PF=2,PMX_PCG1_PF_W=1 --rounds 4 --iters 300"),
+        ("fp32", 600, "python -u bench/ab_env.py --shape 16384x16384 --shape 32768x32768 --dtype fp32 --cfg base: "
+                      "--cfg pf2:PMX_PCG1_PF=2 --cfg pf3:PMX_PCG1_PF=3 --cfg pf2w1:PMX_PCG1_PF=2,PMX_PCG1_PF_W=1 "
+                      "--cfg pf3w2:PMX_PCG1_PF=3,PMX_PCG1_PF_W=2 --cfg pf3w1:PMX_PCG1_PF=3,PMX_PCG1_PF_W=1 "
+                      "--rounds 3 --iters 200"),
+    ],
+    "pf_ab2": [
+        ("fp64", 900, "python -u bench/ab_env.py --shape 16384x16384 --shape 8192x16384 --shape 4096x16384 "
+                      "--shape 2048x16384 --cfg base: --cfg pf2:PMX_PCG1_PF=2 --rounds 5 --iters 300"),
+        ("fp32", 600, "python -u bench/ab_env.py --shape 16384x16384 --shape 32768x32768 --shape 2048x16384 "
+                      "--dtype fp32 --cfg r24: --cfg r16:PMX_PCG1_ROWS=16 --cfg r20:PMX_PCG1_ROWS=20 "
+                      "--cfg r32:PMX_PCG1_ROWS=32 --cfg pf1:PMX_PCG1_PF=1 --rounds 3 --iters 200"),
+    ],
     "bin_ab_tests": [
         ("pytest_pcg1", 600, f"{PYTEST} tests/test_gpu_pcg1.py tests/test_gpu_solver.py tests/test_gpu_launch_path.py"),
         ("fp64", 600, "python -u bench/ab_env.py --pkg old=bench/ab/pmx_base --shape 16384x16384 "

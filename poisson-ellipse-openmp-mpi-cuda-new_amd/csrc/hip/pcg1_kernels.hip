@@ -371,12 +371,13 @@ done:
 //  * The sweeps that move w (WS, one in w_cycle) are a kernel of their own: without the w paths
 //    the plain sweep needs 113 VGPRs in fp64 / 111 in fp32 and runs at 4 waves/SIMD; the w sweep
 //    with the triple paths (149 / 135 VGPRs) at 3 (profiles/r2/prologue/, profiles/r2/fp32_w3/).
+//  * (round 3) the plain sweeps with deeper prefetch still fit 4 waves/SIMD: fp32 PF 2/3 (119 / 121
+//    VGPRs) and fp64 PF 2 (131 free, 128 forced).
 template <typename T, int VEC, int WAVES, int PF, bool WS>
 constexpr int pcg1_min_waves() {
   if (VEC != 2 || WAVES != 1) return 1;
-  if (sizeof(T) == 4 && PF == 1) return WS ? 3 : 4;  // the fp32 w sweep carries the triple paths
-  if (sizeof(T) == 8 && PF == 1 && !WS) return 4;
-  return PF <= 2 ? 3 : 2;
+  if (!WS && (PF == 1 || (sizeof(T) == 4 && PF <= 3) || (sizeof(T) == 8 && PF == 2))) return 4;
+  return PF <= 2 ? 3 : 2;  // the w sweeps (triple paths) and fp64 PF 3
 }
 
 // Which tiles a launch covers (launch_pcg1's part) and where tile k of that launch sits.
@@ -854,10 +855,11 @@ TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf, 
   t.vec = vec;
   t.waves = waves;
   t.block = 64 * vec - 4;  // owned columns per tile
-  // fp32 storage: PF 1 at 4 waves/SIMD (see pcg1_min_waves) with 24-row tiles
-  // (profiles/r2/fp32_pcg1_sweep.txt)
+  // fp32 storage: 24-row tiles (profiles/r2/fp32_pcg1_sweep.txt)
   const bool fp32 = elem == 4;
-  t.pf = pf ? pf : (vec == 2 && waves == 1 ? kPcg1AutoPf : 1);
+  // fp32 storage: prefetch 2 rows (its plain sweep still fits 4 waves/SIMD at 117 VGPRs); half-size
+  // rows keep too few bytes in flight at depth 1: 32768^2 -10%, 16384^2 -3% (profiles/r3/prefetch/)
+  t.pf = pf ? pf : (vec == 2 && waves == 1 ? (fp32 ? 2 : kPcg1AutoPf) : 1);
   t.tiles_j = (G.ny + t.block - 1) / t.block;
   if (rows <= 0) {
     // tall tiles keep the 4 extra marched rows cheap; shorter only when the grid is small
@@ -914,8 +916,8 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
   PMX_CHECK(tc.alt == 0 || kPcg1Reverse, "pcg1: alternating march directions need a PMX_PCG1_REVERSE build");
   if (tc.vec == 2 && tc.waves == 1 && tc.pf == 1) PMX_PCG1(2, 1, 1);
   else if (tc.vec == 2 && tc.waves == 1 && tc.pf == 2) PMX_PCG1(2, 1, 2);
-#ifdef PMX_PCG1_ALL_SHAPES
   else if (tc.vec == 2 && tc.waves == 1 && tc.pf == 3) PMX_PCG1(2, 1, 3);
+#ifdef PMX_PCG1_ALL_SHAPES
   else if (tc.vec == 2 && tc.waves == 1) PMX_PCG1(2, 1, 4);
   else if (tc.vec == 2 && tc.waves == 4) PMX_PCG1(2, 4, 1);
   else if (tc.vec == 2 && tc.waves == 2) PMX_PCG1(2, 2, 1);
