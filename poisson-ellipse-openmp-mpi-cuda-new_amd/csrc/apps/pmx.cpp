@@ -308,7 +308,10 @@ int run_hip(Cli& c, double t_prog) {
               << "   Host<->Device copy time (max over ranks)        ~ " << 0.0 << " s\n"
               << "   MPI halo exchange time (max over ranks)         ~ " << ph.t_comm * scale << " s\n"
               << "   Preconditioner CPU part time (max over ranks)   ~ " << 0.0 << " s\n"
-              << "   Dot products time (max over ranks)              ~ " << ph.t_reduce * scale << " s\n";
+              << "   Dot products time (max over ranks)              ~ " << ph.t_reduce * scale << " s\n"
+              << "   (buckets of the fused iteration: compute = the whole single sweep (A p, r/w update,\n"
+              << "    D^{-1} r, A z); copy and preconditioner are 0 by construction -- no host staging, D^{-1}\n"
+              << "    fused into the sweep; dot = the device reduction; MPI = all-reduce + ghost exchange)\n";
   }
   std::cout << "M=" << s.M << ", N=" << s.N << " | Iter=" << st.iters << " | Total Time=" << std::fixed
             << std::setprecision(6) << (t_after - t_prog) << " s\n"
