@@ -111,6 +111,13 @@ STUDIES: dict[str, list[tuple[str, int, str]]] = {
         ("fp32", 600, "python -u bench/ab_env.py --pkg old=bench/ab/pmx_base --shape 16384x16384 "
                       "--shape 32768x32768 --dtype fp32 --cfg old@old: --cfg new: --rounds 3 --iters 200"),
     ],
+    # standalone bench records (BASELINE configs 2/5 and the headline)
+    "records": [
+        ("bench_default", 300, bench("--gpus 1 --steps 20 --warmup 5")),
+        ("fp32_16384", 300, bench("--gpus 1 --dtype fp32 --steps 200 --warmup 20")),
+        ("fp32_32768", 500, bench("--gpus 1 --dtype fp32 --M 32768 --N 32768 --steps 100 --warmup 10")),
+        ("fp64_4096", 200, bench("--gpus 1 --M 4096 --N 4096 --steps 200 --warmup 20")),
+    ],
     "profile_default": [
         ("rocprof_bench", 300, f"{ROCPROF} -d gpurun_out/profile_default/rp -o run -- "
                                + bench("--gpus 1 --steps 60 --warmup 10 --no-tol-solve")),
