@@ -707,20 +707,20 @@ k_reduce_n(const double* __restrict__ part, int n, ReduceWeights wt, double* out
   __syncthreads();
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) chunk[NQ * blockIdx.x + q] = (lds[q][0] + lds[q][1]) + (lds[q][2] + lds[q][3]);
-    __threadfence();
-    last = atomicAdd(ticket, 1u) == unsigned(nb - 1);
+    for (int q = 0; q < NQ; ++q)
+      st_publish(chunk + NQ * blockIdx.x + q, (lds[q][0] + lds[q][1]) + (lds[q][2] + lds[q][3]));
+    last = ticket_arrive_last(ticket, nb);
   }
   __syncthreads();
   if (!last || threadIdx.x >= kWave) return;  // wave 0 of the last block finishes (full EXEC)
-  __threadfence();
-  const volatile double* c = chunk;
   const int l = int(threadIdx.x);
   double t[NQ];
   bool bad = false;
 #pragma unroll
+  for (int q = 0; q < NQ; ++q) t[q] = l < nb ? ld_published(chunk + NQ * l + q) : 0.0;  // all in flight
+#pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    t[q] = wave_sum_mfma(l < nb ? c[NQ * l + q] : 0.0);
+    t[q] = wave_sum_mfma(t[q]);
     bad |= !(t[q] == t[q]) || isinf(t[q]);
   }
   if (l == 0) {

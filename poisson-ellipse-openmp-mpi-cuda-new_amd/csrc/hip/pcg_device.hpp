@@ -44,6 +44,25 @@ __device__ __forceinline__ T ld_uniform(const T* p, int i) {
   typedef const __attribute__((address_space(4))) T CT;
   return ((CT*)p)[i];
 }
+// Hand-off between the blocks of one launch (the ticketed last-block reductions): each block
+// publishes its chunk sums write-through (relaxed agent-scope atomic stores, sc1), drains them
+// (vmcnt 0) before its relaxed ticket add, and the last arriver reads every chunk with agent-scope
+// atomic loads (sc1, past its CU's L1).  No __threadfence(): that is an L2 writeback plus an L2
+// invalidate (~3.5 us each side) in a kernel of a few microseconds.
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) unsigned gunsigned;
+__device__ __forceinline__ void st_publish(double* p, double v) {
+  __hip_atomic_store((gdouble*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // NOLINT
+}
+__device__ __forceinline__ double ld_published(const double* p) {
+  return __hip_atomic_load((gdouble*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // NOLINT
+}
+// true for the block whose arrival completes the count (n arrivals in all)
+__device__ __forceinline__ bool ticket_arrive_last(unsigned* ticket, int n) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the published chunk is in L2 first
+  return __hip_atomic_fetch_add((gunsigned*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==  // NOLINT
+         unsigned(n - 1);
+}
 __device__ __forceinline__ RowConst load_row(const DevTables& T, int gi) {
   RowConst r;
   gi = __builtin_amdgcn_readfirstlane(gi);

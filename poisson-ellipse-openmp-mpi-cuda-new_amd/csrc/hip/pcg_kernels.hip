@@ -368,18 +368,15 @@ k_reduce(const double* __restrict__ part, int n, double w0, double w1, double* o
   double b = (s1[0] + s1[1]) + (s1[2] + s1[3]);
   block_sum2<256>(a, b, lds);
   if (threadIdx.x == 0) {
-    chunk[2 * blockIdx.x] = a;
-    chunk[2 * blockIdx.x + 1] = b;
-    __threadfence();
-    last = atomicAdd(ticket, 1u) == unsigned(nb - 1);
+    st_publish(chunk + 2 * blockIdx.x, a);
+    st_publish(chunk + 2 * blockIdx.x + 1, b);
+    last = ticket_arrive_last(ticket, nb);
   }
   __syncthreads();
   if (!last || threadIdx.x >= kWave) return;  // wave 0 of the last block finishes (full EXEC)
-  __threadfence();
-  const volatile double* c = chunk;
   const int l = int(threadIdx.x);
-  double ta = l < nb ? c[2 * l] : 0.0;
-  double tb = l < nb ? c[2 * l + 1] : 0.0;
+  double ta = l < nb ? ld_published(chunk + 2 * l) : 0.0;
+  double tb = l < nb ? ld_published(chunk + 2 * l + 1) : 0.0;
   wave_sum2_mfma(ta, tb);
   if (l == 0) {
     out[0] = ta * w0;
