@@ -172,20 +172,25 @@ def _pmc(argv):
 
 def _timeline(argv):
     """kernel durations and gaps per iteration: rocprofv3 --kernel-trace of the pmx CLI per grid
-    (MxN ...), then bench/trace_timeline.py; extra pmx arguments after --pmx"""
+    (MxN ...), then bench/trace_timeline.py; extra pmx arguments after --pmx.  --case TAG 'M N args'
+    (repeatable) adds runs with their own pmx arguments; --ranks P passes P subdomains to every run
+    (LocalComm on the one GPU) and per-subdomain sweep times to the summary."""
     ap = argparse.ArgumentParser(prog="timeline")
-    ap.add_argument("grids", nargs="+")
+    ap.add_argument("grids", nargs="*")
     ap.add_argument("--iters", type=int, default=600)
     ap.add_argument("--pmx", default="")
+    ap.add_argument("--ranks", type=int, default=1)
+    ap.add_argument("--case", nargs=2, action="append", default=[], metavar=("TAG", "ARGS"))
     a = ap.parse_args(argv)
+    cases = [(g, " ".join(g.split("x")) + " " + a.pmx) for g in a.grids] + [tuple(c) for c in a.case]
+    rk = f" --ranks {a.ranks}" if a.ranks > 1 else ""
     steps = []
-    for g in a.grids:
-        M, N = g.split("x")
-        steps.append((f"trace_{g}", 150, f"rocprofv3 --kernel-trace --output-format csv -d gpurun_out/timeline/{g} "
-                                         f"-o run -- poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx {M} {N} "
-                                         f"--max-iter {a.iters} --json {a.pmx}"))
-        steps.append((f"timeline_{g}", 60, f"python3 bench/trace_timeline.py gpurun_out/timeline/{g}/run_kernel_trace.csv "
-                                           f"--skip 50"))
+    for tag, args in cases:
+        steps.append((f"trace_{tag}", 150, f"rocprofv3 --kernel-trace --output-format csv -d gpurun_out/timeline/{tag} "
+                                           f"-o run -- poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx {args} "
+                                           f"--max-iter {a.iters} --json{rk}"))
+        steps.append((f"timeline_{tag}", 60, f"python3 bench/trace_timeline.py gpurun_out/timeline/{tag}/run_kernel_trace.csv "
+                                             f"--skip 50{rk}"))
     return steps
 
 
@@ -208,6 +213,43 @@ def _cli(argv):
     """pmx CLI runs, one step per quoted argument string: 'M N --flags' ..."""
     return [(f"pmx{i}", 600, f"poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx {a} --json") for i, a in enumerate(argv)]
 
+
+# round 3: fp32 stencil arithmetic on fp32 storage (PMX_ARITH32) against the fp64-register sweep,
+# and the per-rank cost of the reference 2x4 blocks vs row strips (LocalComm, 8 subdomains)
+STUDIES["arith32"] = [
+    ("ab", 900, "python -u bench/ab_env.py --dtype fp32 --shape 16384x16384 --shape 32768x32768 "
+                "--cfg f64arith: --cfg f32arith:PMX_ARITH32=1 --rounds 3 --iters 100 --tol"),
+    ("bench_800", 200, "env PMX_ARITH32=1 " + bench("--gpus 1 --M 800 --N 1200 --dtype fp32 --steps 20 --warmup 5")),
+    ("bench_16k", 300, "env PMX_ARITH32=1 " + bench("--gpus 1 --dtype fp32 --steps 20 --warmup 5")),
+]
+# fp32 arithmetic: tile height, prefetch depth, and a 5-waves/SIMD plain sweep (package copy
+# bench/ab/w5 built with PMX_EXTRA_HIP_FLAGS=-DPMX_PCG1_F32_WAVES=5)
+STUDIES["f32tune"] = [
+    ("ab", 1100, "python -u bench/ab_env.py --dtype fp32 --shape 16384x16384 --shape 32768x32768 --pkg w5=bench/ab/w5 "
+                 "--cfg base:PMX_ARITH32=1 --cfg w5@w5:PMX_ARITH32=1 --cfg r32:PMX_ARITH32=1,PMX_PCG1_ROWS=32 "
+                 "--cfg r48:PMX_ARITH32=1,PMX_PCG1_ROWS=48 --cfg r16:PMX_ARITH32=1,PMX_PCG1_ROWS=16 "
+                 "--cfg pf3:PMX_ARITH32=1,PMX_PCG1_PF=3 --cfg pf1:PMX_ARITH32=1,PMX_PCG1_PF=1 --rounds 3 --iters 60"),
+]
+# allocation placement: subdomains 5-7 of an 8-way LocalComm run sweep ~8-10% faster than 0-4
+STUDIES["placement"] = [
+    ("multi", 300, "python -u bench/probe/placement.py --multi 6"),
+    ("hold", 600, "python -u bench/probe/placement.py --hold 0 --hold 16 --hold 48 --hold 120 --rounds 2"),
+    ("pytest_f32", 300, f"{PYTEST} tests/test_gpu_pcg1.py -k 'fp32' tests/test_gpu_cli.py"),
+]
+STUDIES["stagger"] = [
+    ("stagger", 900, "python -u bench/probe/placement.py --rounds 2 --cfg sep:PMX_FIELD_STAGGER=-1 "
+                     "--cfg s0:PMX_FIELD_STAGGER=0 --cfg s4k:PMX_FIELD_STAGGER=4096 --cfg s64k:PMX_FIELD_STAGGER=65536 "
+                     "--cfg s256k:PMX_FIELD_STAGGER=262144 --cfg s1m:PMX_FIELD_STAGGER=1048576 "
+                     "--cfg s2m4k:PMX_FIELD_STAGGER=2101248 --cfg s8m:PMX_FIELD_STAGGER=8388608"),
+    ("multi", 300, "python -u bench/probe/placement.py --multi 6"),
+]
+STUDIES["blocks8"] = [
+    ("ab_ref", 600, "python -u bench/ab_env.py --ranks 8 --split reference --shape 16384x16384 --cfg ref: "
+                    "--rounds 3 --iters 100"),
+    ("ab_rows", 600, "python -u bench/ab_env.py --ranks 8 --split rows --shape 16384x16384 --cfg rows: "
+                     "--rounds 3 --iters 100"),
+] + _timeline(["--ranks", "8", "--iters", "300", "--case", "ref", "16384 16384 --split reference",
+               "--case", "rows", "16384 16384 --split rows"])
 
 PARAMETRISED = {"ab": _ab, "pmc": _pmc, "timeline": _timeline, "validate": _validate, "share": _share, "cli": _cli}
 STUDIES["pmc_super"] = pmc_study("pmc_super", {"base": "", "s4": "PMX_PCG1_SUPER=4"}, PMC_ARGS,

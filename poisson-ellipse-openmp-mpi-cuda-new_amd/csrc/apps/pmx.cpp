@@ -101,10 +101,11 @@ Cli parse(int argc, char** argv) {
     else if (a == "--split") c.split = val();
     else if (a == "--dtype") {
       const std::string v = val();
-      // mixed == fp32: fields stored in fp32, every stencil/update evaluated in fp64 registers,
-      // all reductions and PCG scalars in fp64
+      // fp32: fields and the single-pass sweep's stencil arithmetic in fp32; mixed: fp32 fields,
+      // every stencil/update in fp64 registers.  Both keep reductions and PCG scalars in fp64.
       if (v != "fp64" && v != "fp32" && v != "mixed") usage("--dtype fp64|fp32|mixed");
       c.opt.dtype = v == "fp64" ? DType::kFp64 : DType::kFp32;
+      c.opt.arith32 = v == "fp32" ? 1 : 0;
     } else if (a == "--norm") {
       const std::string v = val();
       if (v != "weighted" && v != "unweighted") usage("--norm weighted|unweighted");
@@ -243,7 +244,7 @@ int run_plan(const Cli& c) {
   (void)hipGetLastError();
   const int gpus = std::max(1, c.gpus);
   std::cout << "plan: M=" << s.M << ", N=" << s.N << ", " << ranks << " subdomain(s) as " << pg.Px << " x "
-            << pg.Py << ", dtype " << (c.opt.dtype == DType::kFp64 ? "fp64" : "fp32") << "\n"
+            << pg.Py << ", dtype " << dtype_name(c.opt) << "\n"
             << "memory: " << dev_src << "\n";
   const int subs_per_device = c.gpus > 1 ? 1 : ranks;  // LocalComm: every subdomain on one device
   const bool single_pass = choose_single_pass(s, pg, resolve_options(c.opt), dev_bytes, subs_per_device);
@@ -323,7 +324,7 @@ int run_hip(Cli& c, double t_prog) {
     const ErrorNorms e = error_norms(s, w);
     JsonLine j;
     j.ks("backend", "hip").kv("M", s.M).kv("N", s.N).kv("ranks", cfg.world).ks("comm", sess.comm_name())
-        .ks("dtype", c.opt.dtype == DType::kFp64 ? "fp64" : "fp32").kv("iters", st.iters)
+        .ks("dtype", dtype_name(c.opt)).kv("iters", st.iters)
         .ks("status", status_name(st.status)).kv("solve_seconds", st.solve_seconds)
         .kv("init_seconds", st.init_seconds)
         .kv("mlups", double(s.M - 1) * (s.N - 1) * st.iters / st.solve_seconds / 1e6)

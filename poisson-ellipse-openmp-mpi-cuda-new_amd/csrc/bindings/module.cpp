@@ -190,8 +190,10 @@ GpuOptions make_options(int device, const std::string& kernel, int block, int ve
   o.block = block;
   o.tile_rows = tile_rows;
   PMX_CHECK(dtype == "fp64" || dtype == "fp32" || dtype == "mixed",
-            "dtype must be fp64, fp32 or mixed (= fp32 storage, fp64 arithmetic), got " << dtype);
+            "dtype must be fp64, fp32 (fp32 storage and stencil arithmetic) or mixed (fp32 storage, fp64 "
+            "arithmetic), got " << dtype);
   o.dtype = dtype == "fp64" ? DType::kFp64 : DType::kFp32;
+  o.arith32 = dtype == "fp32" ? 1 : 0;
   o.exact = exact;
   o.graph_batch = graph_batch;
   o.check = check;

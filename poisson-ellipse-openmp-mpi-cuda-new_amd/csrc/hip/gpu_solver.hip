@@ -102,6 +102,7 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_PCG1_BANDS", o.bands1);
   env_int("PMX_PCG1_WCYCLE", o.wcycle1);
   env_int("PMX_PROGRESS", o.progress);
+  env_int("PMX_ARITH32", o.arith32);
   PMX_CHECK(o.wcycle1 == 2 || o.wcycle1 == 3, "pcg1 w cycle must be 2 or 3");
   PMX_CHECK(o.pair_w >= 0 && o.pair_w <= 2, "pair_w must be 0, 1 or 2");
   PMX_CHECK(o.algo == -1 || o.algo == 1 || o.algo == 2, "algo must be -1, 1 or 2");
@@ -171,6 +172,9 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
   }
 }
 
+// Bytes between consecutive fields of the one field allocation (see construct).
+constexpr long long kFieldStagger = 0;
+
 void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   const GpuOptions& opt = opt_;
   const ProblemSpec& spec = spec_;
@@ -205,7 +209,16 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
                               "device is ~"
                            << max_square_grid(double(total_b), 1, opt.dtype) << "^2 (pmx --plan)");
   }
-  HIP_CHECK(hipMalloc(&fields_, 4 * field_bytes_));
+  // One allocation for all fields.  The stagger between consecutive fields decides how their rows
+  // fall onto HBM channels/banks relative to each other: every sweep streams the same row of 4-5
+  // fields at once (PMX_FIELD_STAGGER bytes, multiple of 256; -1 = r2 allocated on its own).
+  long long stagger = kFieldStagger;
+  if (const char* e = std::getenv("PMX_FIELD_STAGGER"); e && e[0]) stagger = std::atoll(e);
+  PMX_CHECK(stagger == -1 || (stagger >= 0 && stagger % 256 == 0), "PMX_FIELD_STAGGER: -1 or a multiple of 256");
+  own_r2_ = stagger == -1 && pcg1_;
+  field_stride_ = field_bytes_ + size_t(std::max(0LL, stagger));
+  const int nfields = pcg1_ && !own_r2_ ? 5 : 4;
+  HIP_CHECK(hipMalloc(&fields_, size_t(nfields) * field_stride_));
 
   // 1D face tables
   tables_ = upload_tables(spec, &tables_buf_);
@@ -237,13 +250,18 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
       wtrace_ = pcg1_wave_trace_setup(std::atoll(e), wtrace_n_);
     }
 #endif
-    HIP_CHECK(hipMalloc(&r2_, field_bytes_));
+    if (own_r2_)
+      HIP_CHECK(hipMalloc(&r2_, field_bytes_));
+    else
+      r2_ = field_raw(4);
     tiles1_.super = opt_.super1;
+    tiles1_.arith32 = elem_ == 4 && opt_.arith32 ? 1 : 0;
     tiles1_.bands = opt_.bands1;
     tiles1_.alt = opt_.alt1 >= 0 ? opt_.alt1 : (opt_.super1 > 0 ? 1 : 0);
     tiles1w_ = make_pcg1_tiles(G, opt_.vec1, opt_.waves1, opt_.rows1w ? opt_.rows1w : tiles1_.rows,
                                opt_.pf1w ? opt_.pf1w : tiles1_.pf, int(elem_));
     tiles1w_.super = tiles1_.super;
+    tiles1w_.arith32 = tiles1_.arith32;
     tiles1w_.bands = tiles1_.bands;
     tiles1w_.alt = tiles1_.alt;
     const bool same_w = tiles1w_.rows == tiles1_.rows;
@@ -344,7 +362,7 @@ void GpuSubdomainSolver::release() noexcept {
   (void)hipSetDevice(opt_.device);
   (void)hipDeviceSynchronize();
   if (fields_) (void)hipFree(fields_);
-  if (r2_) (void)hipFree(r2_);
+  if (r2_ && own_r2_) (void)hipFree(r2_);
   if (tile_order_) (void)hipFree(tile_order_);
   if (tile_order_w_) (void)hipFree(tile_order_w_);
   if (tables_buf_) (void)hipFree(tables_buf_);
@@ -396,13 +414,13 @@ size_t GpuSubdomainSolver::estimate_device_bytes(const ProblemSpec& spec, const 
 size_t GpuSubdomainSolver::device_bytes() const {
   const size_t tables = (4 * size_t(spec_.M + 2) + 4 * size_t(spec_.N + 2)) * sizeof(double) +
                         8 * size_t(spec_.M + 2) * sizeof(int);
-  return (r2_ ? 5 : 4) * field_bytes_ + tables + (npart_ * 5 + kReduceWsDoubles) * sizeof(double) +
+  return (r2_ ? 5 : 4) * field_stride_ + tables + (npart_ * 5 + kReduceWsDoubles) * sizeof(double) +
          (own_arena_ ? layout_.bytes : 0);
 }
 
 void* GpuSubdomainSolver::field_base(int which) const {
   PMX_CHECK(which >= 0 && which < 4, "field index");
-  return fields_ + which * field_bytes_ + field_off_ * elem_;
+  return field_raw(which) + field_off_ * elem_;
 }
 
 template <typename T>
@@ -424,7 +442,7 @@ void GpuSubdomainSolver::after_launch(hipStream_t s) const {
 
 template <typename T>
 void GpuSubdomainSolver::init_impl(hipStream_t s) {
-  HIP_CHECK(hipMemsetAsync(fields_, 0, 4 * field_bytes_, s));
+  for (int f = 0; f < 4; ++f) HIP_CHECK(hipMemsetAsync(field_raw(f), 0, field_bytes_, s));
   if (r2_) HIP_CHECK(hipMemsetAsync(r2_, 0, field_bytes_, s));
   HIP_CHECK(hipMemsetAsync(arena_, 0, layout_.bytes, s));
   PcgState& st = host_state_[1];  // template (never rewritten while a copy is in flight)
@@ -599,7 +617,8 @@ void GpuSubdomainSolver::save_checkpoint(std::ostream& os, hipStream_t s) const 
   h.arena_bytes = int64_t(layout_.bytes); h.max_iter = spec_.effective_max_iter(); h.delta = spec_.delta;
   os.write(reinterpret_cast<const char*>(&h), sizeof(h));
   std::vector<char> buf(std::max(4 * field_bytes_, layout_.bytes));
-  HIP_CHECK(hipMemcpy(buf.data(), fields_, 4 * field_bytes_, hipMemcpyDeviceToHost));
+  for (int f = 0; f < 4; ++f)
+    HIP_CHECK(hipMemcpy(buf.data() + size_t(f) * field_bytes_, field_raw(f), field_bytes_, hipMemcpyDeviceToHost));
   os.write(buf.data(), std::streamsize(4 * field_bytes_));
   HIP_CHECK(hipMemcpy(buf.data(), arena_, layout_.bytes, hipMemcpyDeviceToHost));
   os.write(buf.data(), std::streamsize(layout_.bytes));
@@ -631,7 +650,8 @@ void GpuSubdomainSolver::load_checkpoint(std::istream& is, hipStream_t s) {
   is.read(buf.data(), std::streamsize(4 * field_bytes_));
   PMX_CHECK(is.good(), "truncated checkpoint (fields)");
   HIP_CHECK(hipStreamSynchronize(s));
-  HIP_CHECK(hipMemcpy(fields_, buf.data(), 4 * field_bytes_, hipMemcpyHostToDevice));
+  for (int f = 0; f < 4; ++f)
+    HIP_CHECK(hipMemcpy(field_raw(f), buf.data() + size_t(f) * field_bytes_, field_bytes_, hipMemcpyHostToDevice));
   is.read(buf.data(), std::streamsize(layout_.bytes));
   PMX_CHECK(is.good(), "truncated checkpoint (scalars/halos)");
   HIP_CHECK(hipMemcpy(arena_, buf.data(), layout_.bytes, hipMemcpyHostToDevice));

@@ -58,6 +58,14 @@ constexpr bool kPcg1Reverse = true;
 constexpr bool kPcg1Reverse = false;
 #endif
 constexpr int kPcg1AutoPf = 1;
+// waves/SIMD bounds of the fp32-arithmetic sweeps (plain, w)
+#ifndef PMX_PCG1_F32_WAVES
+#define PMX_PCG1_F32_WAVES 4
+#endif
+#ifndef PMX_PCG1_F32_WAVES_W
+#define PMX_PCG1_F32_WAVES_W 4
+#endif
+constexpr int kPcg1F32Waves = PMX_PCG1_F32_WAVES, kPcg1F32WavesW = PMX_PCG1_F32_WAVES_W;
 
 #ifdef PMX_WAVE_TRACE
 // Diagnostic build only (bench/wave_trace.sh): per-wave start/end wall clock, XCC and HW ids and
@@ -131,6 +139,63 @@ __device__ __forceinline__ void coef(const RowCo& c, const DevTables& Tb, const 
   }
 }
 
+// Stencil arithmetic in the sweep's compute type C.  C = double: the shared helpers of
+// pcg_device.hpp, bit-identical to every other fp64 kernel.  C = float (fp32 storage with fp32
+// arithmetic, GpuOptions::arith32): the same formulas in fp32 with the class coefficients, 1/h^2
+// and 1/D rounded once to fp32 (ArithF, built per wave from DevGeom); cut faces are evaluated
+// exactly in fp64 and rounded.  The 5 partial sums stay fp64 in both (products of two fp32 values
+// are exact in fp64).  Half the registers of the fp64 pipeline and packed-fp32 friendly: the fp32
+// sweep is issue-bound in fp64 arithmetic (profiles/r3/kernel_ab/pmc_fp32_16384.md).
+struct ArithF {
+  float cx, cy, dinv_in, dinv_out, inv_eps;
+};
+
+__device__ __forceinline__ double fma_c(double a, double b, double c) { return __builtin_fma(a, b, c); }
+__device__ __forceinline__ float fma_c(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+
+template <typename C>
+__device__ __forceinline__ void coef_c(const RowCo& c, const DevTables& Tb, const DevGeom& G, const ArithF& F,
+                                       const double* scol, int u, int lane, int gj, C& a0, C& a1, C& b0, C& b1) {
+  if constexpr (std::is_same_v<C, double>) {
+    coef(c, Tb, G, scol, u, lane, gj, a0, a1, b0, b1);
+  } else {
+    if (c.ucls != 0) {
+      a0 = a1 = b0 = b1 = c.ucls == 1 ? 1.0f : F.inv_eps;
+    } else {
+      double d0, d1, e0, e1;
+      coef(c, Tb, G, scol, u, lane, gj, d0, d1, e0, e1);
+      a0 = float(d0); a1 = float(d1); b0 = float(e0); b1 = float(e1);
+    }
+  }
+}
+
+template <typename C>
+__device__ __forceinline__ C zdiv_c(int ucls, C r, C a0, C a1, C b0, C b1, const DevGeom& G, const ArithF& F) {
+  if constexpr (std::is_same_v<C, double>) {
+    return zdiv_u<false>(ucls, r, a0, a1, b0, b1, G);
+  } else {
+    if (ucls == 1) return r * F.dinv_in;
+    if (ucls == 2) return r * F.dinv_out;
+    const bool in = (a0 == 1.0f) & (a1 == 1.0f) & (b0 == 1.0f) & (b1 == 1.0f);
+    const bool out = (a0 == F.inv_eps) & (a1 == F.inv_eps) & (b0 == F.inv_eps) & (b1 == F.inv_eps);
+    if (in) return r * F.dinv_in;
+    if (out) return r * F.dinv_out;
+    return r / __builtin_fmaf(a1 + a0, F.cx, (b1 + b0) * F.cy);
+  }
+}
+
+template <typename C>
+__device__ __forceinline__ C apply_c(C pc, C pim, C pip, C pjm, C pjp, C a0, C a1, C b0, C b1, const DevGeom& G,
+                                     const ArithF& F) {
+  if constexpr (std::is_same_v<C, double>) {
+    return apply_a<false>(pc, pim, pip, pjm, pjp, a0, a1, b0, b1, G);
+  } else {
+    const float x = __builtin_fmaf(a1, pc - pip, a0 * (pc - pim));
+    const float y = __builtin_fmaf(b1, pc - pjp, b0 * (pc - pjm));
+    return __builtin_fmaf(F.cx, x, F.cy * y);
+  }
+}
+
 // f(integral_constant<int, 0>) && f(integral_constant<int, 1>) && ... (N calls at most, stops at
 // the first false): a loop body whose step number is a compile-time constant
 template <typename F, int... I>
@@ -162,15 +227,16 @@ struct Pcg1Row {
 // point gets the same arithmetic either way (only the order of the per-lane partial sums over
 // rows differs).  Alternating directions make vertically adjacent tiles that start together read
 // their shared halo rows at the same time (see pcg1_build_order).
-template <typename T, int VEC, int PF, int WM, bool FAST, int DIR>
-__device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb, T* __restrict__ w,
+template <typename T, typename C, int VEC, int PF, int WM, bool FAST, int DIR>
+__device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb, const ArithF& F, T* __restrict__ w,
                                            const T* __restrict__ rold, T* __restrict__ rnew,
                                            const T* __restrict__ pold,
                                            T* pnew, int i0, int i1, int j0, int j1,
-                                           double alpha, double beta, double c1, double c2,
+                                           double alpha_d, double beta_d, double c1_d, double c2_d,
                                            double (&acc)[kNq], double* __restrict__ scol,
                                            unsigned long long cls, bool use_cls) {
   constexpr bool WUP = WM != 0;
+  const C alpha = C(alpha_d), beta = C(beta_d), c1 = C(c1_d), c2 = C(c2_d);
   const int64_t P = G.pitch;
   const int lane = threadIdx.x & 63;
   const int c0 = j0 - 2 + lane * VEC;
@@ -213,9 +279,9 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   };
 
   // pipeline registers
-  double Pm2[VEC], Pm1[VEC], Zm3[VEC], Zm2[VEC], ro1[VEC], po1[VEC], po2[VEC];
+  C Pm2[VEC], Pm1[VEC], Zm3[VEC], Zm2[VEC], ro1[VEC], po1[VEC], po2[VEC];
 #pragma unroll
-  for (int u = 0; u < VEC; ++u) Pm2[u] = Pm1[u] = Zm3[u] = Zm2[u] = ro1[u] = po1[u] = po2[u] = 0.0;
+  for (int u = 0; u < VEC; ++u) Pm2[u] = Pm1[u] = Zm3[u] = Zm2[u] = ro1[u] = po1[u] = po2[u] = C(0);
   RowCo cB = row_of(DIR > 0 ? i0 - 3 : i1 + 3);  // rows m-DIR, m-2 DIR
   RowCo cC = cB;
   bool parked = false;  // column constants in LDS (see col_lds)
@@ -241,17 +307,17 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     const bool rowA = FAST || interior_row(m);
     const RowCo cA = row_of(m);
     if (cA.ucls == 0 && !parked) park_cols();
-    double Pm[VEC], rom[VEC], pom[VEC];
+    C Pm[VEC], rom[VEC], pom[VEC];
 #pragma unroll
     for (int u = 0; u < VEC; ++u) {
       const bool in = FAST || (rowA && colin[u]);
-      rom[u] = in ? double(cur.r[u]) : 0.0;
-      pom[u] = in ? double(cur.p[u]) : 0.0;
-      double a0, a1, b0, b1;
-      coef(cA, Tb, G, scol, u, lane, gj[u], a0, a1, b0, b1);
-      const double z = zdiv_u<false>(cA.ucls, rom[u], a0, a1, b0, b1, G);
-      const double v = __builtin_fma(beta, pom[u], z);
-      Pm[u] = in ? double(static_cast<T>(v)) : 0.0;  // the stored (rounded) p^k is the one used
+      rom[u] = in ? C(cur.r[u]) : C(0);
+      pom[u] = in ? C(cur.p[u]) : C(0);
+      C a0, a1, b0, b1;
+      coef_c<C>(cA, Tb, G, F, scol, u, lane, gj[u], a0, a1, b0, b1);
+      const C z = zdiv_c<C>(cA.ucls, rom[u], a0, a1, b0, b1, G, F);
+      const C v = fma_c(beta, pom[u], z);
+      Pm[u] = in ? C(static_cast<T>(v)) : C(0);  // the stored (rounded) p^k is the one used
     }
     // ---- stage B: A p^k, r^k, z^k of row m-DIR (j neighbours by DPP; edge lanes get 0, their
     // results only feed columns that are not owned).  Rows i-1 / i+1 of it: Pm2 / Pm (DIR +1),
@@ -259,49 +325,49 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     const int mb = m - DIR;
     const bool rowB = FAST || interior_row(mb);
     const bool ownB = mb >= i0 && mb <= i1;
-    double Zm1[VEC];
+    C Zm1[VEC];
     T rs[VEC], ps[VEC], ws[VEC];
     {
-      const double left = dpp_shift_f64<kWaveShr1>(Pm1[VEC - 1], 0.0);
-      const double right = dpp_shift_f64<kWaveShl1>(Pm1[0], 0.0);
-      double oleft = 0.0, oright = 0.0;
+      const C left = dpp_shift<kWaveShr1>(Pm1[VEC - 1], C(0));
+      const C right = dpp_shift<kWaveShl1>(Pm1[0], C(0));
+      C oleft = C(0), oright = C(0);
       if constexpr (WM == 2) {
-        oleft = dpp_shift_f64<kWaveShr1>(po1[VEC - 1], 0.0);
-        oright = dpp_shift_f64<kWaveShl1>(po1[0], 0.0);
+        oleft = dpp_shift<kWaveShr1>(po1[VEC - 1], C(0));
+        oright = dpp_shift<kWaveShl1>(po1[0], C(0));
       }
 #pragma unroll
       for (int u = 0; u < VEC; ++u) {
-        double a0, a1, b0, b1;
-        coef(cB, Tb, G, scol, u, lane, gj[u], a0, a1, b0, b1);
-        const double xjm = u == 0 ? left : Pm1[u - 1];
-        const double xjp = u == VEC - 1 ? right : Pm1[u + 1];
-        const double Ap = apply_a<false>(Pm1[u], DIR > 0 ? Pm2[u] : Pm[u], DIR > 0 ? Pm[u] : Pm2[u], xjm, xjp,
-                                         a0, a1, b0, b1, G);
+        C a0, a1, b0, b1;
+        coef_c<C>(cB, Tb, G, F, scol, u, lane, gj[u], a0, a1, b0, b1);
+        const C xjm = u == 0 ? left : Pm1[u - 1];
+        const C xjp = u == VEC - 1 ? right : Pm1[u + 1];
+        const C Ap = apply_c<C>(Pm1[u], DIR > 0 ? Pm2[u] : Pm[u], DIR > 0 ? Pm[u] : Pm2[u], xjm, xjp,
+                                a0, a1, b0, b1, G, F);
         const bool in = FAST || (rowB && colin[u]);
-        const double rn = double(static_cast<T>(upd_r<false>(ro1[u], alpha, Ap)));
-        rs[u] = static_cast<T>(in ? rn : 0.0);
-        const double zn = zdiv_u<false>(cB.ucls, rn, a0, a1, b0, b1, G);
-        Zm1[u] = in ? zn : 0.0;
+        const C rn = C(static_cast<T>(fma_c(-alpha, Ap, ro1[u])));  // = upd_r<false>
+        rs[u] = static_cast<T>(in ? rn : C(0));
+        const C zn = zdiv_c<C>(cB.ucls, rn, a0, a1, b0, b1, G, F);
+        Zm1[u] = in ? zn : C(0);
         ps[u] = static_cast<T>(Pm1[u]);
         if constexpr (WM == 1) {
-          ws[u] = static_cast<T>(__builtin_fma(alpha, Pm1[u], __builtin_fma(c1, po1[u], double(cur.w[u]))));
+          ws[u] = static_cast<T>(fma_c(alpha, Pm1[u], fma_c(c1, po1[u], C(cur.w[u]))));
         } else if constexpr (WM == 2) {
           // r^{k-2} = r^{k-1} + alpha_{k-1} A p^{k-1};  p^{k-2} = (p^{k-1} - D^-1 r^{k-2}) / beta_{k-1}
-          const double xm = u == 0 ? oleft : po1[u - 1];
-          const double xp = u == VEC - 1 ? oright : po1[u + 1];
-          const double Apo = apply_a<false>(po1[u], DIR > 0 ? po2[u] : pom[u], DIR > 0 ? pom[u] : po2[u], xm,
-                                            xp, a0, a1, b0, b1, G);
-          const double zo = zdiv_u<false>(cB.ucls, __builtin_fma(c1, Apo, ro1[u]), a0, a1, b0, b1, G);
-          const double t = __builtin_fma(c2, po1[u] - zo, double(cur.w[u]));
-          ws[u] = static_cast<T>(__builtin_fma(alpha, Pm1[u], __builtin_fma(c1, po1[u], t)));
+          const C xm = u == 0 ? oleft : po1[u - 1];
+          const C xp = u == VEC - 1 ? oright : po1[u + 1];
+          const C Apo = apply_c<C>(po1[u], DIR > 0 ? po2[u] : pom[u], DIR > 0 ? pom[u] : po2[u], xm,
+                                   xp, a0, a1, b0, b1, G, F);
+          const C zo = zdiv_c<C>(cB.ucls, fma_c(c1, Apo, ro1[u]), a0, a1, b0, b1, G, F);
+          const C t = fma_c(c2, po1[u] - zo, C(cur.w[u]));
+          ws[u] = static_cast<T>(fma_c(alpha, Pm1[u], fma_c(c1, po1[u], t)));
         } else if constexpr (WM == 3) {
-          const double t = __builtin_fma(c2, double(cur.q[u]), double(cur.w[u]));
-          ws[u] = static_cast<T>(__builtin_fma(alpha, Pm1[u], __builtin_fma(c1, po1[u], t)));
+          const C t = fma_c(c2, C(cur.q[u]), C(cur.w[u]));
+          ws[u] = static_cast<T>(fma_c(alpha, Pm1[u], fma_c(c1, po1[u], t)));
         }
         if (ownB && (FAST || own[u])) {
-          acc[0] += Zm1[u] * rn;
-          acc[3] += Ap * Pm1[u];
-          acc[4] += Pm1[u] * Pm1[u];
+          acc[0] += double(Zm1[u]) * double(rn);
+          acc[3] += double(Ap) * double(Pm1[u]);
+          acc[4] += double(Pm1[u]) * double(Pm1[u]);
         }
       }
     }
@@ -314,19 +380,19 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     // ---- stage C: A z^k of row m-2 DIR
     const int mcr = m - 2 * DIR;
     if (mcr >= i0 && mcr <= i1) {
-      const double left = dpp_shift_f64<kWaveShr1>(Zm2[VEC - 1], 0.0);
-      const double right = dpp_shift_f64<kWaveShl1>(Zm2[0], 0.0);
+      const C left = dpp_shift<kWaveShr1>(Zm2[VEC - 1], C(0));
+      const C right = dpp_shift<kWaveShl1>(Zm2[0], C(0));
 #pragma unroll
       for (int u = 0; u < VEC; ++u) {
-        double a0, a1, b0, b1;
-        coef(cC, Tb, G, scol, u, lane, gj[u], a0, a1, b0, b1);
-        const double xjm = u == 0 ? left : Zm2[u - 1];
-        const double xjp = u == VEC - 1 ? right : Zm2[u + 1];
-        const double Az = apply_a<false>(Zm2[u], DIR > 0 ? Zm3[u] : Zm1[u], DIR > 0 ? Zm1[u] : Zm3[u], xjm, xjp,
-                                         a0, a1, b0, b1, G);
+        C a0, a1, b0, b1;
+        coef_c<C>(cC, Tb, G, F, scol, u, lane, gj[u], a0, a1, b0, b1);
+        const C xjm = u == 0 ? left : Zm2[u - 1];
+        const C xjp = u == VEC - 1 ? right : Zm2[u + 1];
+        const C Az = apply_c<C>(Zm2[u], DIR > 0 ? Zm3[u] : Zm1[u], DIR > 0 ? Zm1[u] : Zm3[u], xjm, xjp,
+                                a0, a1, b0, b1, G, F);
         if (FAST || own[u]) {
-          acc[1] += Az * Zm2[u];
-          acc[2] += Az * Pm2[u];
+          acc[1] += double(Az) * double(Zm2[u]);
+          acc[2] += double(Az) * double(Pm2[u]);
         }
       }
     }
@@ -373,9 +439,12 @@ done:
 //    with the triple paths (149 / 135 VGPRs) at 3 (profiles/r2/prologue/, profiles/r2/fp32_w3/).
 //  * (round 3) the plain sweeps with deeper prefetch still fit 4 waves/SIMD: fp32 PF 2/3 (119 / 121
 //    VGPRs) and fp64 PF 2 (131 free, 128 forced).
-template <typename T, int VEC, int WAVES, int PF, bool WS>
+//  * fp32 arithmetic (C = float): the fp32 pipeline needs about half the registers; whatever the
+//    allocator picks at the 4-wave bound of the plain sweep (see kPcg1F32Waves).
+template <typename T, typename C, int VEC, int WAVES, int PF, bool WS>
 constexpr int pcg1_min_waves() {
   if (VEC != 2 || WAVES != 1) return 1;
+  if (std::is_same_v<C, float>) return WS ? kPcg1F32WavesW : kPcg1F32Waves;
   if (!WS && (PF == 1 || (sizeof(T) == 4 && PF <= 3) || (sizeof(T) == 8 && PF == 2))) return 4;
   return PF <= 2 ? 3 : 2;  // the w sweeps (triple paths) and fp64 PF 3
 }
@@ -418,8 +487,8 @@ __host__ __device__ inline bool pcg1_tile(int k, const Pcg1Part& P, int tiles_j,
   return false;
 }
 
-template <typename T, int VEC, int WAVES, int PF, bool WS>
-__global__ void __launch_bounds__(64 * WAVES, (pcg1_min_waves<T, VEC, WAVES, PF, WS>()))
+template <typename T, typename C, int VEC, int WAVES, int PF, bool WS>
+__global__ void __launch_bounds__(64 * WAVES, (pcg1_min_waves<T, C, VEC, WAVES, PF, WS>()))
 k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
        double* __restrict__ partials, PcgState* S, int TI, int tiles_j, int ntiles, Pcg1Part part) {
   constexpr int WO = 64 * VEC - 4;  // owned columns per tile
@@ -567,6 +636,7 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
   const bool fast = VEC == 2 && j1 == j0 + WO - 1 && G.gi0 + i0 - 2 >= 1 && G.gi0 + i1 + 2 <= G.M - 1 &&
                     G.gj0 + j0 - 2 >= 1 && G.gj0 + j0 + 64 * VEC - 3 <= G.N - 1;
   const bool use_cls = part.order != nullptr && TI + 5 <= 64 / 2;  // 2 bits for each of the TI+5 rows
+  const ArithF AF{float(G.cx), float(G.cy), float(G.dinv_in), float(G.dinv_out), float(G.inv_eps)};
 #ifdef PMX_PCG1_REVERSE
   // study build only (NOTES #46-#47: bottom-up marches lose ~4%): tiles with even ti (alt 1) or
   // every tile (alt 2) march bottom-up
@@ -574,16 +644,16 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
 #define PMX_MARCH(E, F)                                                                                   \
   do {                                                                                                   \
     if (rev)                                                                                             \
-      pcg1_march<T, VEC, PF, E, F, -1>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, \
-                                       acc, scol, ocls, use_cls);                                                       \
+      pcg1_march<T, C, VEC, PF, E, F, -1>(G, Tb, AF, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, \
+                                          c2, acc, scol, ocls, use_cls);                                         \
     else                                                                                                 \
-      pcg1_march<T, VEC, PF, E, F, 1>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2,  \
-                                      acc, scol, ocls, use_cls);                                                        \
+      pcg1_march<T, C, VEC, PF, E, F, 1>(G, Tb, AF, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, \
+                                         c2, acc, scol, ocls, use_cls);                                          \
   } while (0)
 #else
-#define PMX_MARCH(E, F) \
-  pcg1_march<T, VEC, PF, E, F, 1>(G, Tb, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, acc, scol, \
-                                  ocls, use_cls)
+#define PMX_MARCH(E, F)                                                                                          \
+  pcg1_march<T, C, VEC, PF, E, F, 1>(G, Tb, AF, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, acc, \
+                                     scol, ocls, use_cls)
 #endif
 #define PMX_MARCH_W(F)                                     \
   if constexpr (!WS) {                                     \
@@ -901,14 +971,23 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
   PMX_CHECK(G.nb == 0 || (G.nx >= 2 && G.ny >= 2), "pcg1 on a decomposed grid needs subdomains >= 2 x 2");
   const int nb = (count + tc.waves - 1) / tc.waves;
   const int bs = 64 * tc.waves;
-#define PMX_PCG1(V, WV, PF)                                                                              \
+#define PMX_PCG1_C(C, V, WV, PF)                                                                         \
   do {                                                                                                   \
     if (wsweep)                                                                                          \
-      hipLaunchKernelGGL((k_pcg1<T, V, WV, PF, true>), dim3(nb), dim3(bs), 0, s, G, Tb, w, r, r2, p0, p1, \
-                         partials, S, tc.rows, tc.tiles_j, tc.ntiles(), P);                              \
-    else                                                                                                 \
-      hipLaunchKernelGGL((k_pcg1<T, V, WV, PF, false>), dim3(nb), dim3(bs), 0, s, G, Tb, w, r, r2, p0,   \
+      hipLaunchKernelGGL((k_pcg1<T, C, V, WV, PF, true>), dim3(nb), dim3(bs), 0, s, G, Tb, w, r, r2, p0,  \
                          p1, partials, S, tc.rows, tc.tiles_j, tc.ntiles(), P);                          \
+    else                                                                                                 \
+      hipLaunchKernelGGL((k_pcg1<T, C, V, WV, PF, false>), dim3(nb), dim3(bs), 0, s, G, Tb, w, r, r2, p0, \
+                         p1, partials, S, tc.rows, tc.tiles_j, tc.ntiles(), P);                          \
+  } while (0)
+  // fp32 arithmetic: fp32 storage only, the default tile shape (VEC 2, 1 wave) and prefetch 1-3
+#define PMX_PCG1(V, WV, PF)                                                                              \
+  do {                                                                                                   \
+    if constexpr (std::is_same_v<T, float> && V == 2 && WV == 1 && PF <= 3) {                            \
+      if (tc.arith32) { PMX_PCG1_C(float, V, WV, PF); break; }                                           \
+    }                                                                                                    \
+    PMX_CHECK(!tc.arith32, "pcg1: fp32 arithmetic needs fp32 storage, VEC 2 x 1 wave and prefetch <= 3"); \
+    PMX_PCG1_C(double, V, WV, PF);                                                                       \
   } while (0)
   // instantiated shapes: the default (VEC 2, 1 wave, prefetch 1) and prefetch 2.  The other
   // shapes of the round-1/2 sweeps (prefetch 3-4, 2 or 4 waves per workgroup, VEC 4: all slower,
@@ -927,6 +1006,7 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
                                           << " is only instantiated in a PMX_PCG1_ALL_SHAPES build");
 #endif
 #undef PMX_PCG1
+#undef PMX_PCG1_C
   HIP_CHECK(hipGetLastError());
 }
 

@@ -81,6 +81,10 @@ struct GpuOptions {
   // pcg1 prefetch depth: rows loaded ahead of the row being computed (1..4).  The sweep is
   // latency-bound at 2 waves/SIMD; deeper prefetch spends VGPRs that occupancy does not use.
   int pf1 = 0;  // 0 = auto
+  // pcg1 with fp32 storage: 1 = the sweep's stencil arithmetic in fp32 too (fp64 partial sums,
+  // reductions and PCG scalars), 0 = fp64 registers (the default "fp32 storage" path).  fp64 storage
+  // ignores it.  PMX_ARITH32=0|1 overrides.
+  int arith32 = 0;
   // pcg1 dispatch order: 1 = tiles cut by the ellipse first within each XCD's share, 0 = natural
   int order1 = 1;
   // pcg1 halo-row reuse (TileCfg::super / alt): super-rows of `super1` tile rows dispatched column by
@@ -101,6 +105,11 @@ struct GpuOptions {
   int progress = 0;
   bool resolved = false;  // environment overrides already applied (resolve_options)
 };
+
+// "fp64", "fp32" (fp32 storage + fp32 stencil arithmetic) or "mixed" (fp32 storage, fp64 arithmetic)
+inline const char* dtype_name(const GpuOptions& o) {
+  return o.dtype == DType::kFp64 ? "fp64" : (o.arith32 ? "fp32" : "mixed");
+}
 
 // Environment overrides (PMX_ALGO, PMX_PAIR_W, PMX_PCG1_*) applied to a copy of `opt`.
 GpuOptions resolve_options(const GpuOptions& opt);
@@ -252,8 +261,14 @@ class GpuSubdomainSolver {
   TileCfg init_tiles_{};
   CommLayout layout_{};
   size_t elem_ = 8, field_bytes_ = 0, field_off_ = 0;
-  char* fields_ = nullptr;  // 4 fields, rows -1 .. nx+2
+  // Fields w, r, p0, p1 (and pcg1's r2) in ONE allocation, field f at fields_ + f * field_stride_
+  // (field_bytes_ + a stagger, see construct); rows -1 .. nx+2 each.  PMX_FIELD_STAGGER=-1 keeps the
+  // round-1/2 layout (r2 a separate allocation) for A/B studies.
+  char* fields_ = nullptr;
   char* r2_ = nullptr;      // pcg1 only: the second r buffer (r is double-buffered there)
+  size_t field_stride_ = 0;
+  bool own_r2_ = false;     // r2_ is its own allocation (PMX_FIELD_STAGGER=-1)
+  char* field_raw(int f) const { return fields_ + size_t(f) * field_stride_; }
   double* tables_buf_ = nullptr;
   double* partials_ = nullptr;
   size_t npart_ = 0;

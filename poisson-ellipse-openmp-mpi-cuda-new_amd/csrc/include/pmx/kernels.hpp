@@ -54,6 +54,7 @@ struct TileCfg {
   int alt = 0;
   int super = 0;
   int bands = 1;  // order tables: sub-bands per XCD chunk dispatched round-robin (pcg1_build_order)
+  int arith32 = 0;  // kind 3 with fp32 storage: 1 = fp32 stencil arithmetic (GpuOptions::arith32)
   int interior_tiles() const { return (ti_hi - ti_lo) * (tj_hi - tj_lo); }
   int ntiles() const { return tiles_i * tiles_j; }
 };

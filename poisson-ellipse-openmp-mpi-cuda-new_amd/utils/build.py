@@ -46,6 +46,9 @@ BIND_SOURCES = ["bindings/module.cpp"]
 
 COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC / 'include'}", "-Wall", "-Wno-unused-result"]
 HIP_FLAGS = [f"--offload-arch={ARCH}", "-munsafe-fp-atomics"]
+# study builds only (e.g. a package copy under bench/ab/ with other compile-time kernel bounds):
+# extra hipcc flags such as -DPMX_PCG1_F32_WAVES=5
+HIP_FLAGS += os.environ.get("PMX_EXTRA_HIP_FLAGS", "").split()
 CPU_FLAGS = ["-fopenmp", "-ffp-contract=off"]
 # host-only translation units that use the HIP runtime API (bindings, CLI): plain g++
 HOST_HIP_FLAGS = ["-D__HIP_PLATFORM_AMD__", "-DPMX_WITH_HIP", f"-I{ROCM / 'include'}"]

@@ -183,6 +183,22 @@ def test_pcg1_fp32_triples(pkg, monkeypatch):
     assert np.abs(out[3].w - ref.w).max() < 1e-4
 
 
+@pytest.mark.parametrize("M,N", [(400, 600), (800, 1200)])
+def test_pcg1_fp32_arithmetic(pkg, M, N):
+    """--dtype fp32 evaluates the single-pass sweep's stencils in fp32 (fp64 partial sums, reductions
+    and scalars); --dtype mixed keeps the fp64 registers on the same fp32 storage.  Both stay within
+    2 iterations of the fp64 count (546 / 989) and within fp32 rounding of its solution, and the two
+    really run different arithmetic."""
+    p = pkg.PoissonEllipse(M=M, N=N)
+    f64 = pkg.solve(p, "hip")
+    f32 = pkg.solve(p, "hip", dtype="fp32")
+    mix = pkg.solve(p, "hip", dtype="mixed")
+    for r in (f32, mix):
+        assert r.status == "converged" and abs(r.iters - f64.iters) <= 2, (r.iters, f64.iters)
+        assert np.abs(r.w - f64.w).max() < 1e-4
+    assert np.abs(f32.w - mix.w).max() > 0.0
+
+
 @pytest.mark.parametrize("ranks", [1, 4])
 def test_pcg1_graph_phases_match_eager(pkg, monkeypatch, ranks):
     """The plain / w-moving sweep kernels are chosen on the host and baked into the captured
