@@ -240,8 +240,20 @@ STUDIES["stagger"] = [
     ("stagger", 900, "python -u bench/probe/placement.py --rounds 2 --cfg sep:PMX_FIELD_STAGGER=-1 "
                      "--cfg s0:PMX_FIELD_STAGGER=0 --cfg s4k:PMX_FIELD_STAGGER=4096 --cfg s64k:PMX_FIELD_STAGGER=65536 "
                      "--cfg s256k:PMX_FIELD_STAGGER=262144 --cfg s1m:PMX_FIELD_STAGGER=1048576 "
-                     "--cfg s2m4k:PMX_FIELD_STAGGER=2101248 --cfg s8m:PMX_FIELD_STAGGER=8388608"),
+                     "--cfg s2m4k:PMX_FIELD_STAGGER=2101248 --cfg s8m:PMX_FIELD_STAGGER=8388608 "
+                     "--cfg contig:PMX_FIELD_CONTIG=1"),
     ("multi", 300, "python -u bench/probe/placement.py --multi 6"),
+]
+STUDIES["alloc"] = [
+    ("multi8", 400, "env PMX_DEBUG_ALLOC=1 python -u bench/probe/placement.py --multi 8"),
+]
+# placement probe (GpuSubdomainSolver::place_fields): off vs the default 4 candidates, fresh processes
+STUDIES["place"] = [
+    ("probe_ab", 600, "python -u bench/probe/placement.py --rounds 3 --cfg off:PMX_PLACEMENT=1 --cfg k4: "
+                      "--cfg k2:PMX_PLACEMENT=2"),
+    ("bench_default", 300, bench("--gpus 1 --steps 20 --warmup 5")),
+    ("bench_fp32_16k", 300, bench("--gpus 1 --dtype fp32 --steps 20 --warmup 5")),
+    ("bench_fp32_32k", 400, bench("--gpus 1 --M 32768 --N 32768 --dtype fp32 --steps 20 --warmup 5")),
 ]
 STUDIES["blocks8"] = [
     ("ab_ref", 600, "python -u bench/ab_env.py --ranks 8 --split reference --shape 16384x16384 --cfg ref: "

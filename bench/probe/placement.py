@@ -50,8 +50,11 @@ def child(a):
     p = pkg.PoissonEllipse(M=a.M, N=a.N)
     if a.multi:
         ss = [pkg.make_session(p, dtype=a.dtype) for _ in range(a.multi)]
-        for k, s in enumerate(ss):
-            print(json.dumps(dict(session=k, us=round(time_session(s, a.iters), 1))), flush=True)
+        # forward, then reverse: a slow ALLOCATION stays slow in both passes, a slow PERIOD does not
+        order = list(range(a.multi))
+        for pas, ks in enumerate((order, order[::-1])):
+            for k in ks:
+                print(json.dumps(dict(session=k, pass_=pas, us=round(time_session(ss[k], a.iters), 1))), flush=True)
     else:
         s = pkg.make_session(p, dtype=a.dtype)
         print(json.dumps(dict(hold_gb=a.child_hold, us=round(time_session(s, a.iters), 1))), flush=True)

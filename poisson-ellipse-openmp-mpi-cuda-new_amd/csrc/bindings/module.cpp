@@ -536,6 +536,11 @@ PYBIND11_MODULE(_pmx, m) {
         py::dict d = one(s.solver(0).tiles());
         if (!s.solver(0).single_pass()) d["b"] = one(s.solver(0).tiles_b());
         d["algo"] = s.solver(0).single_pass() ? "pcg1" : "pcg2";
+        if (!s.solver(0).placement_ms().empty()) {
+          py::list l;
+          for (float v : s.solver(0).placement_ms()) l.append(v);
+          d["placement_probe_ms"] = l;  // 3 plain sweeps per candidate field block, min kept
+        }
         return d;
       });
 }

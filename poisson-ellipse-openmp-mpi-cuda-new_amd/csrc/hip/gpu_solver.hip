@@ -174,6 +174,8 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
 
 // Bytes between consecutive fields of the one field allocation (see construct).
 constexpr long long kFieldStagger = 0;
+// Field blocks the placement probe compares (see place_fields); 1 = off.
+constexpr int kPlacementCandidates = 5;
 
 void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   const GpuOptions& opt = opt_;
@@ -218,7 +220,16 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   own_r2_ = stagger == -1 && pcg1_;
   field_stride_ = field_bytes_ + size_t(std::max(0LL, stagger));
   const int nfields = pcg1_ && !own_r2_ ? 5 : 4;
-  HIP_CHECK(hipMalloc(&fields_, size_t(nfields) * field_stride_));
+  // PMX_FIELD_CONTIG=1 (study): physically contiguous VRAM for the fields (hipDeviceMallocContiguous)
+  if (const char* e = std::getenv("PMX_FIELD_CONTIG"); e && e[0] == '1')
+    HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&fields_), size_t(nfields) * field_stride_,
+                                    hipDeviceMallocContiguous));
+  else
+    HIP_CHECK(hipMalloc(&fields_, size_t(nfields) * field_stride_));
+  if (const char* e = std::getenv("PMX_DEBUG_ALLOC"); e && e[0] == '1')
+    std::fprintf(stderr, "pmx alloc: fields %p (%zu B, mod 1G %zu, mod 2M %zu)\n", static_cast<void*>(fields_),
+                 size_t(nfields) * field_stride_, size_t(reinterpret_cast<uintptr_t>(fields_) % (size_t(1) << 30)),
+                 size_t(reinterpret_cast<uintptr_t>(fields_) % (size_t(1) << 21)));
 
   // 1D face tables
   tables_ = upload_tables(spec, &tables_buf_);
@@ -305,6 +316,66 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     void* d = nullptr;
     HIP_CHECK(hipHostGetDevicePointer(&d, progress_host_, 0));
     progress_dev_ = static_cast<long long*>(d);
+  }
+  if (pcg1_) place_fields();
+}
+
+// Field placement probe.  On MI355X the same sweep runs ~7% faster or slower depending on WHERE its
+// fields were allocated: a property of the allocation, stable for its lifetime and across passes
+// (8 sessions alive in one process, timed forward then in reverse: the first 2-3 allocations of
+// ~10.8 GB at 2.145 ms/iteration at 16384^2 fp64, later ones at 1.99 ms -- profiles/r3/placement/;
+// the field stagger inside the block and physically contiguous memory do not help).  So the solver
+// allocates up to K candidate blocks while free memory allows (10% headroom kept), times a few
+// plain sweeps on each (zeroed fields, the init sweep's k = 0 arithmetic; init() resets everything
+// afterwards), keeps the fastest and frees the others.  Construction-time only: nothing in the
+// iteration changes.  PMX_PLACEMENT=K overrides kPlacementCandidates (1 = off).  Skipped with an
+// external (IPC-shared) arena or a separately allocated r2.
+void GpuSubdomainSolver::place_fields() {
+  int K = kPlacementCandidates;
+  if (const char* e = std::getenv("PMX_PLACEMENT"); e && e[0]) K = std::atoi(e);
+  if (K <= 1 || !own_arena_ || own_r2_) return;
+  const size_t block = 5 * field_stride_;
+  std::vector<char*> cand{fields_};
+  while (int(cand.size()) < K) {
+    size_t free_b = 0, total_b = 0;
+    HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+    if (free_b < block + total_b / 10) break;
+    char* p = nullptr;
+    if (hipMalloc(&p, block) != hipSuccess) {
+      (void)hipGetLastError();
+      break;
+    }
+    cand.push_back(p);
+  }
+  if (cand.size() > 1) {
+    hipStream_t s;
+    hipEvent_t e0, e1;
+    HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreate(&e0));
+    HIP_CHECK(hipEventCreate(&e1));
+    const long long hk = host_k_;
+    host_k_ = 0;  // plain sweep
+    placement_ms_.assign(cand.size(), 0.f);
+    for (size_t c = 0; c < cand.size(); ++c) {
+      fields_ = cand[c];
+      r2_ = field_raw(4);
+      HIP_CHECK(hipMemsetAsync(fields_, 0, block, s));
+      enqueue_kernel_a(s);  // warm-up
+      HIP_CHECK(hipEventRecord(e0, s));
+      for (int q = 0; q < 3; ++q) enqueue_kernel_a(s);
+      HIP_CHECK(hipEventRecord(e1, s));
+      HIP_CHECK(hipEventSynchronize(e1));
+      HIP_CHECK(hipEventElapsedTime(&placement_ms_[c], e0, e1));
+    }
+    host_k_ = hk;
+    const size_t best = size_t(std::min_element(placement_ms_.begin(), placement_ms_.end()) - placement_ms_.begin());
+    for (size_t c = 0; c < cand.size(); ++c)
+      if (c != best) HIP_CHECK(hipFree(cand[c]));
+    fields_ = cand[best];
+    r2_ = field_raw(4);
+    HIP_CHECK(hipEventDestroy(e0));
+    HIP_CHECK(hipEventDestroy(e1));
+    HIP_CHECK(hipStreamDestroy(s));
   }
 }
 

@@ -230,6 +230,7 @@ class GpuSubdomainSolver {
   const TileCfg& tiles_b() const { return tiles_b_; }  // pcg_b
   int device() const { return opt_.device; }
   size_t field_bytes() const { return field_bytes_; }
+  const std::vector<float>& placement_ms() const { return placement_ms_; }
   void* field_base(int which) const;  // pointer to local (0,0)
   size_t device_bytes() const;        // total device memory owned
 
@@ -269,6 +270,8 @@ class GpuSubdomainSolver {
   size_t field_stride_ = 0;
   bool own_r2_ = false;     // r2_ is its own allocation (PMX_FIELD_STAGGER=-1)
   char* field_raw(int f) const { return fields_ + size_t(f) * field_stride_; }
+  void place_fields();                // placement probe (see gpu_solver.hip)
+  std::vector<float> placement_ms_;   // probe: ms per candidate block (the kept one is the min)
   double* tables_buf_ = nullptr;
   double* partials_ = nullptr;
   size_t npart_ = 0;
