@@ -255,6 +255,17 @@ STUDIES["place"] = [
     ("bench_fp32_16k", 300, bench("--gpus 1 --dtype fp32 --steps 20 --warmup 5")),
     ("bench_fp32_32k", 400, bench("--gpus 1 --M 32768 --N 32768 --dtype fp32 --steps 20 --warmup 5")),
 ]
+STUDIES["hiphold"] = [
+    ("hold", 900, "env PMX_PLACEMENT=1 PLACEMENT_HOLD_API=hip python -u bench/probe/placement.py --rounds 1 "
+                  "--hold 0 --hold 12 --hold 24 --hold 48 --hold 96"),
+    ("hold32k", 900, "env PMX_PLACEMENT=1 PLACEMENT_HOLD_API=hip python -u bench/probe/placement.py --rounds 1 "
+                     "--M 32768 --N 32768 --dtype fp32 --iters 30 --hold 0 --hold 24 --hold 48 --hold 96"),
+]
+STUDIES["place2"] = [
+    ("probe32k", 900, "python -u bench/probe/placement.py --rounds 3 --M 32768 --N 32768 --dtype fp32 --iters 30 "
+                      "--cfg off:PMX_PLACEMENT=1 --cfg k5:"),
+    ("probe16k", 600, "python -u bench/probe/placement.py --rounds 3 --cfg off:PMX_PLACEMENT=1 --cfg k5:"),
+]
 STUDIES["blocks8"] = [
     ("ab_ref", 600, "python -u bench/ab_env.py --ranks 8 --split reference --shape 16384x16384 --cfg ref: "
                     "--rounds 3 --iters 100"),

@@ -46,7 +46,17 @@ def child(a):
     import torch
 
     pkg = importlib.import_module("poisson-ellipse-openmp-mpi-cuda-new_amd")
-    hold = torch.empty(int(a.child_hold * (1 << 30)), dtype=torch.uint8, device="cuda") if a.child_hold else None
+    hold = None
+    if a.child_hold and os.environ.get("PLACEMENT_HOLD_API") == "hip":  # raw hipMalloc, not torch's allocator
+        import ctypes
+
+        torch.cuda.init()
+        hip = ctypes.CDLL("libamdhip64.so.7")
+        hold = ctypes.c_void_p()
+        rc = hip.hipMalloc(ctypes.byref(hold), ctypes.c_size_t(int(a.child_hold * (1 << 30))))
+        assert rc == 0, rc
+    elif a.child_hold:
+        hold = torch.empty(int(a.child_hold * (1 << 30)), dtype=torch.uint8, device="cuda")
     p = pkg.PoissonEllipse(M=a.M, N=a.N)
     if a.multi:
         ss = [pkg.make_session(p, dtype=a.dtype) for _ in range(a.multi)]

@@ -325,11 +325,22 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
 // (8 sessions alive in one process, timed forward then in reverse: the first 2-3 allocations of
 // ~10.8 GB at 2.145 ms/iteration at 16384^2 fp64, later ones at 1.99 ms -- profiles/r3/placement/;
 // the field stagger inside the block and physically contiguous memory do not help).  So the solver
-// allocates up to K candidate blocks while free memory allows (10% headroom kept), times a few
-// plain sweeps on each (zeroed fields, the init sweep's k = 0 arithmetic; init() resets everything
-// afterwards), keeps the fastest and frees the others.  Construction-time only: nothing in the
+// allocates up to K candidate blocks while free memory allows (10% headroom kept), times 3
+// plain sweeps on each with the fields in rotating roles (probe_sweeps: every field read and
+// written; zeroed fields, the init sweep's k = 0 arithmetic; init() resets everything afterwards), keeps the fastest and frees the others.  Construction-time only: nothing in the
 // iteration changes.  PMX_PLACEMENT=K overrides kPlacementCandidates (1 = off).  Skipped with an
 // external (IPC-shared) arena or a separately allocated r2.
+// Plain sweeps (k = 0 arithmetic) with the five field blocks in rotating roles, so that every field
+// of the candidate block is read and written: role set q reads r = F[q], p = F[q+3] and writes
+// r2 = F[q+4], p0 = F[q+2] (indices mod 5; F = w, r, p0, p1, r2).
+template <typename T>
+void GpuSubdomainSolver::probe_sweeps(hipStream_t s, int first, int count) {
+  auto F = [&](int f) { return reinterpret_cast<T*>(field_raw(f % 5) + field_off_ * elem_); };
+  for (int q = first; q < first + count; ++q)
+    launch_pcg1<T>(geom_, tables_, F(q + 1), F(q), F(q + 4), F(q + 2), F(q + 3), partials_, state_,
+                   tiles1_, s, 0, false);
+}
+
 void GpuSubdomainSolver::place_fields() {
   int K = kPlacementCandidates;
   if (const char* e = std::getenv("PMX_PLACEMENT"); e && e[0]) K = std::atoi(e);
@@ -360,9 +371,9 @@ void GpuSubdomainSolver::place_fields() {
       fields_ = cand[c];
       r2_ = field_raw(4);
       HIP_CHECK(hipMemsetAsync(fields_, 0, block, s));
-      enqueue_kernel_a(s);  // warm-up
+      if (elem_ == 8) probe_sweeps<double>(s, 0, 1); else probe_sweeps<float>(s, 0, 1);  // warm-up
       HIP_CHECK(hipEventRecord(e0, s));
-      for (int q = 0; q < 3; ++q) enqueue_kernel_a(s);
+      if (elem_ == 8) probe_sweeps<double>(s, 0, 3); else probe_sweeps<float>(s, 0, 3);
       HIP_CHECK(hipEventRecord(e1, s));
       HIP_CHECK(hipEventSynchronize(e1));
       HIP_CHECK(hipEventElapsedTime(&placement_ms_[c], e0, e1));

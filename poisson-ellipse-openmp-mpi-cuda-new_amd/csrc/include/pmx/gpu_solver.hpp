@@ -271,6 +271,8 @@ class GpuSubdomainSolver {
   bool own_r2_ = false;     // r2_ is its own allocation (PMX_FIELD_STAGGER=-1)
   char* field_raw(int f) const { return fields_ + size_t(f) * field_stride_; }
   void place_fields();                // placement probe (see gpu_solver.hip)
+  template <typename T>
+  void probe_sweeps(hipStream_t s, int first, int count);
   std::vector<float> placement_ms_;   // probe: ms per candidate block (the kept one is the min)
   double* tables_buf_ = nullptr;
   double* partials_ = nullptr;

@@ -183,6 +183,23 @@ def test_pcg1_fp32_triples(pkg, monkeypatch):
     assert np.abs(out[3].w - ref.w).max() < 1e-4
 
 
+def test_placement_probe(pkg, monkeypatch):
+    """The field placement probe times every candidate block it could allocate and keeps one;
+    PMX_PLACEMENT=1 switches it off.  Either way the solve is the same (bitwise: the probe only
+    chooses WHERE the fields live)."""
+    from conftest import sub
+    p = pkg.PoissonEllipse(M=400, N=600)
+    s = sub("models").make_session(p)
+    probe = s.tile.get("placement_probe_ms")
+    assert probe and len(probe) >= 2 and all(v > 0 for v in probe)
+    a = pkg.solve(p, "hip")
+    monkeypatch.setenv("PMX_PLACEMENT", "1")
+    s1 = sub("models").make_session(p)
+    assert "placement_probe_ms" not in s1.tile
+    b = pkg.solve(p, "hip")
+    assert a.iters == b.iters == 546 and np.array_equal(a.w, b.w)
+
+
 @pytest.mark.parametrize("M,N", [(400, 600), (800, 1200)])
 def test_pcg1_fp32_arithmetic(pkg, M, N):
     """--dtype fp32 evaluates the single-pass sweep's stencils in fp32 (fp64 partial sums, reductions
