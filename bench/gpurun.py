@@ -266,6 +266,19 @@ STUDIES["place2"] = [
                       "--cfg off:PMX_PLACEMENT=1 --cfg k5:"),
     ("probe16k", 600, "python -u bench/probe/placement.py --rounds 3 --cfg off:PMX_PLACEMENT=1 --cfg k5:"),
 ]
+# BASELINE config 4's 2D blocks on the bench path: 8 supervised ranks sharing the GPU, reference 2x4
+STUDIES["share_ref"] = [
+    ("pytest_new", 300, f"{PYTEST} tests/test_gpu_pcg1.py -k 'placement or fp32'"),
+    ("share8_ref", 420, bench("--gpus 8 --share-gpu --M 4096 --N 4096 --split reference --steps 20 --warmup 5")),
+    ("share8_ref16k", 420, bench("--gpus 8 --share-gpu --split reference --steps 20 --warmup 5 --no-tol-solve")),
+]
+# binary A/B of the working tree against bench/ab/base (a build of the last commit)
+STUDIES["bin_ab2"] = [
+    ("fp64", 600, "python -u bench/ab_env.py --pkg base=bench/ab/base --shape 16384x16384 --shape 2048x16384 "
+                  "--cfg old@base: --cfg new: --rounds 3 --iters 100"),
+    ("fp32", 600, "python -u bench/ab_env.py --dtype fp32 --pkg base=bench/ab/base --shape 16384x16384 "
+                  "--shape 32768x32768 --cfg old@base: --cfg new: --rounds 3 --iters 60"),
+]
 STUDIES["blocks8"] = [
     ("ab_ref", 600, "python -u bench/ab_env.py --ranks 8 --split reference --shape 16384x16384 --cfg ref: "
                     "--rounds 3 --iters 100"),

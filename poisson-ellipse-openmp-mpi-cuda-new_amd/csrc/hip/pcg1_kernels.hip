@@ -76,12 +76,24 @@ __device__ long long g_wtrace_it = -1;
 
 // VEC columns from c0 (c0 - 1 even, so every 2-column chunk is 2-element aligned); chunks are
 // clamped to start <= cmax (cmax - 1 even, cmax + 1 inside the padded row).
+// Addresses: the row pointer is wave-uniform and every column index is >= -2, so row - 2 plus an
+// UNSIGNED 32-bit byte offset lets the compiler use the SGPR-base form (global_load v, voff, s[base])
+// instead of a 64-bit VGPR address per access (two VALU adds each).
+template <typename T>
+__device__ __forceinline__ const T* col_ptr(const T* row, int c) {
+  return reinterpret_cast<const T*>(reinterpret_cast<const char*>(row - 2) + unsigned(c + 2) * unsigned(sizeof(T)));
+}
+template <typename T>
+__device__ __forceinline__ T* col_ptr(T* row, int c) {
+  return reinterpret_cast<T*>(reinterpret_cast<char*>(row - 2) + unsigned(c + 2) * unsigned(sizeof(T)));
+}
+
 template <typename T, int VEC>
 __device__ __forceinline__ void load_cols(const T* row, int c0, int cmax, T (&out)[VEC]) {
 #pragma unroll
   for (int q = 0; q < VEC / 2; ++q) {
     T v[2];
-    vload_raw<T, 2>(row + min(c0 + 2 * q, cmax), v);
+    vload_raw<T, 2>(col_ptr(row, min(c0 + 2 * q, cmax)), v);
     out[2 * q] = v[0];
     out[2 * q + 1] = v[1];
   }
@@ -94,12 +106,12 @@ __device__ __forceinline__ void store_cols(T* row, int c0, const T (&in)[VEC], b
 #pragma unroll
     for (int q = 0; q < VEC / 2; ++q) {
       const T v[2] = {in[2 * q], in[2 * q + 1]};
-      vstore<T, 2>(row + c0 + 2 * q, v);
+      vstore<T, 2>(col_ptr(row, c0 + 2 * q), v);
     }
   } else {
 #pragma unroll
     for (int u = 0; u < VEC; ++u)
-      if (own[u]) row[c0 + u] = in[u];
+      if (own[u]) *col_ptr(row, c0 + u) = in[u];
   }
 }
 
@@ -196,6 +208,32 @@ __device__ __forceinline__ C apply_c(C pc, C pim, C pip, C pjm, C pjp, C a0, C a
   }
 }
 
+// A x on the VEC columns of a lane: centre xc, rows i-1 / i+1 xim / xip, the lane neighbours'
+// edge columns left / right (DPP).  fp32 with VEC = 2: both columns in packed fp32 (v_pk_*), the
+// same per-column fmaf sequence as apply_c (bit-identical results).
+template <typename C, int VEC>
+__device__ __forceinline__ void apply_row(const C (&xc)[VEC], const C (&xim)[VEC], const C (&xip)[VEC], C left,
+                                          C right, const C (&a0)[VEC], const C (&a1)[VEC], const C (&b0)[VEC],
+                                          const C (&b1)[VEC], const DevGeom& G, const ArithF& F, C (&out)[VEC]) {
+  if constexpr (std::is_same_v<C, float> && VEC == 2) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 pc = {xc[0], xc[1]}, pim = {xim[0], xim[1]}, pip = {xip[0], xip[1]};
+    const f2 pjm = {left, xc[0]}, pjp = {xc[1], right};
+    const f2 A0 = {a0[0], a0[1]}, A1 = {a1[0], a1[1]}, B0 = {b0[0], b0[1]}, B1 = {b1[0], b1[1]};
+    const f2 x = __builtin_elementwise_fma(A1, pc - pip, A0 * (pc - pim));
+    const f2 y = __builtin_elementwise_fma(B1, pc - pjp, B0 * (pc - pjm));
+    const f2 cx = {F.cx, F.cx}, cy = {F.cy, F.cy};
+    const f2 r = __builtin_elementwise_fma(cx, x, cy * y);
+    out[0] = r.x;
+    out[1] = r.y;
+  } else {
+#pragma unroll
+    for (int u = 0; u < VEC; ++u)
+      out[u] = apply_c<C>(xc[u], xim[u], xip[u], u == 0 ? left : xc[u - 1], u == VEC - 1 ? right : xc[u + 1], a0[u],
+                          a1[u], b0[u], b1[u], G, F);
+  }
+}
+
 // f(integral_constant<int, 0>) && f(integral_constant<int, 1>) && ... (N calls at most, stops at
 // the first false): a loop body whose step number is a compile-time constant
 template <typename F, int... I>
@@ -236,6 +274,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
                                            double (&acc)[kNq], double* __restrict__ scol,
                                            unsigned long long cls, bool use_cls) {
   constexpr bool WUP = WM != 0;
+  constexpr bool PK = std::is_same_v<C, float> && VEC == 2;  // packed fp32 stencils (apply_row)
   const C alpha = C(alpha_d), beta = C(beta_d), c1 = C(c1_d), c2 = C(c2_d);
   const int64_t P = G.pitch;
   const int lane = threadIdx.x & 63;
@@ -335,29 +374,39 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
         oleft = dpp_shift<kWaveShr1>(po1[VEC - 1], C(0));
         oright = dpp_shift<kWaveShl1>(po1[0], C(0));
       }
+      // packed fp32: the row's coefficients first, then both columns' stencils in v_pk_* ops; fp64
+      // keeps the per-column interleaving (fewer live registers)
+      C a0[VEC], a1[VEC], b0[VEC], b1[VEC], Ap[VEC], Apo[VEC];
+      if constexpr (PK) {
+#pragma unroll
+        for (int u = 0; u < VEC; ++u) coef_c<C>(cB, Tb, G, F, scol, u, lane, gj[u], a0[u], a1[u], b0[u], b1[u]);
+        apply_row<C, VEC>(Pm1, DIR > 0 ? Pm2 : Pm, DIR > 0 ? Pm : Pm2, left, right, a0, a1, b0, b1, G, F, Ap);
+        // p^{k-2} recovery (WM 2): A p^{k-1}
+        if constexpr (WM == 2)
+          apply_row<C, VEC>(po1, DIR > 0 ? po2 : pom, DIR > 0 ? pom : po2, oleft, oright, a0, a1, b0, b1, G, F, Apo);
+      }
 #pragma unroll
       for (int u = 0; u < VEC; ++u) {
-        C a0, a1, b0, b1;
-        coef_c<C>(cB, Tb, G, F, scol, u, lane, gj[u], a0, a1, b0, b1);
-        const C xjm = u == 0 ? left : Pm1[u - 1];
-        const C xjp = u == VEC - 1 ? right : Pm1[u + 1];
-        const C Ap = apply_c<C>(Pm1[u], DIR > 0 ? Pm2[u] : Pm[u], DIR > 0 ? Pm[u] : Pm2[u], xjm, xjp,
-                                a0, a1, b0, b1, G, F);
+        if constexpr (!PK) {
+          coef_c<C>(cB, Tb, G, F, scol, u, lane, gj[u], a0[u], a1[u], b0[u], b1[u]);
+          Ap[u] = apply_c<C>(Pm1[u], DIR > 0 ? Pm2[u] : Pm[u], DIR > 0 ? Pm[u] : Pm2[u], u == 0 ? left : Pm1[u - 1],
+                             u == VEC - 1 ? right : Pm1[u + 1], a0[u], a1[u], b0[u], b1[u], G, F);
+          if constexpr (WM == 2)
+            Apo[u] = apply_c<C>(po1[u], DIR > 0 ? po2[u] : pom[u], DIR > 0 ? pom[u] : po2[u],
+                                u == 0 ? oleft : po1[u - 1], u == VEC - 1 ? oright : po1[u + 1], a0[u], a1[u], b0[u],
+                                b1[u], G, F);
+        }
         const bool in = FAST || (rowB && colin[u]);
-        const C rn = C(static_cast<T>(fma_c(-alpha, Ap, ro1[u])));  // = upd_r<false>
+        const C rn = C(static_cast<T>(fma_c(-alpha, Ap[u], ro1[u])));  // = upd_r<false>
         rs[u] = static_cast<T>(in ? rn : C(0));
-        const C zn = zdiv_c<C>(cB.ucls, rn, a0, a1, b0, b1, G, F);
+        const C zn = zdiv_c<C>(cB.ucls, rn, a0[u], a1[u], b0[u], b1[u], G, F);
         Zm1[u] = in ? zn : C(0);
         ps[u] = static_cast<T>(Pm1[u]);
         if constexpr (WM == 1) {
           ws[u] = static_cast<T>(fma_c(alpha, Pm1[u], fma_c(c1, po1[u], C(cur.w[u]))));
         } else if constexpr (WM == 2) {
           // r^{k-2} = r^{k-1} + alpha_{k-1} A p^{k-1};  p^{k-2} = (p^{k-1} - D^-1 r^{k-2}) / beta_{k-1}
-          const C xm = u == 0 ? oleft : po1[u - 1];
-          const C xp = u == VEC - 1 ? oright : po1[u + 1];
-          const C Apo = apply_c<C>(po1[u], DIR > 0 ? po2[u] : pom[u], DIR > 0 ? pom[u] : po2[u], xm,
-                                   xp, a0, a1, b0, b1, G, F);
-          const C zo = zdiv_c<C>(cB.ucls, fma_c(c1, Apo, ro1[u]), a0, a1, b0, b1, G, F);
+          const C zo = zdiv_c<C>(cB.ucls, fma_c(c1, Apo[u], ro1[u]), a0[u], a1[u], b0[u], b1[u], G, F);
           const C t = fma_c(c2, po1[u] - zo, C(cur.w[u]));
           ws[u] = static_cast<T>(fma_c(alpha, Pm1[u], fma_c(c1, po1[u], t)));
         } else if constexpr (WM == 3) {
@@ -366,7 +415,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
         }
         if (ownB && (FAST || own[u])) {
           acc[0] += double(Zm1[u]) * double(rn);
-          acc[3] += double(Ap) * double(Pm1[u]);
+          acc[3] += double(Ap[u]) * double(Pm1[u]);
           acc[4] += double(Pm1[u]) * double(Pm1[u]);
         }
       }
@@ -382,17 +431,22 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     if (mcr >= i0 && mcr <= i1) {
       const C left = dpp_shift<kWaveShr1>(Zm2[VEC - 1], C(0));
       const C right = dpp_shift<kWaveShl1>(Zm2[0], C(0));
+      C a0[VEC], a1[VEC], b0[VEC], b1[VEC], Az[VEC];
+      if constexpr (PK) {
+#pragma unroll
+        for (int u = 0; u < VEC; ++u) coef_c<C>(cC, Tb, G, F, scol, u, lane, gj[u], a0[u], a1[u], b0[u], b1[u]);
+        apply_row<C, VEC>(Zm2, DIR > 0 ? Zm3 : Zm1, DIR > 0 ? Zm1 : Zm3, left, right, a0, a1, b0, b1, G, F, Az);
+      }
 #pragma unroll
       for (int u = 0; u < VEC; ++u) {
-        C a0, a1, b0, b1;
-        coef_c<C>(cC, Tb, G, F, scol, u, lane, gj[u], a0, a1, b0, b1);
-        const C xjm = u == 0 ? left : Zm2[u - 1];
-        const C xjp = u == VEC - 1 ? right : Zm2[u + 1];
-        const C Az = apply_c<C>(Zm2[u], DIR > 0 ? Zm3[u] : Zm1[u], DIR > 0 ? Zm1[u] : Zm3[u], xjm, xjp,
-                                a0, a1, b0, b1, G, F);
+        if constexpr (!PK) {
+          coef_c<C>(cC, Tb, G, F, scol, u, lane, gj[u], a0[u], a1[u], b0[u], b1[u]);
+          Az[u] = apply_c<C>(Zm2[u], DIR > 0 ? Zm3[u] : Zm1[u], DIR > 0 ? Zm1[u] : Zm3[u], u == 0 ? left : Zm2[u - 1],
+                             u == VEC - 1 ? right : Zm2[u + 1], a0[u], a1[u], b0[u], b1[u], G, F);
+        }
         if (FAST || own[u]) {
-          acc[1] += double(Az) * double(Zm2[u]);
-          acc[2] += double(Az) * double(Pm2[u]);
+          acc[1] += double(Az[u]) * double(Zm2[u]);
+          acc[2] += double(Az[u]) * double(Pm2[u]);
         }
       }
     }
