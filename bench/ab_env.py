@@ -39,7 +39,14 @@ def main():
     ap.add_argument("--split", default="auto")
     ap.add_argument("--tol", action="store_true")
     ap.add_argument("--pkg", action="append", default=[], help="name=DIR: another copy of the package")
+    ap.add_argument("--fresh", action="store_true",
+                    help="every (round, shape, config) in a fresh child process: sessions created in a "
+                         "long-lived process land on faster or slower memory by their allocation "
+                         "history (profiles/r3/placement/), which swamps small kernel differences")
+    ap.add_argument("--only", default="", help=argparse.SUPPRESS)  # child of --fresh: "round:M:N:cfg"
     a = ap.parse_args()
+    if a.fresh and not a.only:
+        return fresh_parent(a)
     pkgs = {"": importlib.import_module("poisson-ellipse-openmp-mpi-cuda-new_amd")}
     for spec in a.pkg:
         name, _, d = spec.partition("=")
@@ -62,9 +69,12 @@ def main():
         pkg = pkgs[name.partition("@")[2]]
         return pkg.make_session(pkg.PoissonEllipse(M=M, N=N), ranks=a.ranks, split=a.split, dtype=a.dtype)
 
+    only = tuple(a.only.split(":")) if a.only else None
     for rnd in range(a.rounds):
         for (M, N) in shapes:
             for name, env in cfgs:
+                if only and (str(rnd), str(M), str(N), name) != only:
+                    continue
                 s = session(M, N, env, name)
                 s.init()
                 s.step(a.warmup)
@@ -80,6 +90,8 @@ def main():
                 print(json.dumps(dict(round=rnd, M=M, N=N, cfg=name, us_per_iter=round(us, 2), ok=ok,
                                       path=s.path_stats())), flush=True)
                 del s
+    if only:
+        return
     print("\nmedian us/iteration", flush=True)
     print("shape".ljust(14) + "".join(n.rjust(12) for n, _ in cfgs))
     for (M, N) in shapes:
@@ -98,6 +110,34 @@ def main():
                 print(json.dumps(dict(M=M, N=N, cfg=name, iters=st["iters"], status=st["status"],
                                       seconds=round(time.perf_counter() - t0, 2))), flush=True)
                 del s
+
+
+def fresh_parent(a):
+    import subprocess
+
+    argv = [x for x in sys.argv[1:] if x != "--fresh"]
+    res, cfgs = {}, [c.partition(":")[0] for c in a.cfg]
+    for rnd in range(a.rounds):
+        for s in a.shape:
+            M, N = s.split("x")
+            for name in cfgs:
+                p = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), *argv, "--only",
+                                    f"{rnd}:{M}:{N}:{name}"], capture_output=True, text=True, timeout=600)
+                lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+                if p.returncode != 0 or not lines:
+                    print(p.stdout, p.stderr, flush=True)
+                    raise SystemExit(p.returncode or 1)
+                print(lines[-1], flush=True)
+                res.setdefault((s, name), []).append(json.loads(lines[-1])["us_per_iter"])
+    print("\nmedian us/iteration (fresh process per measurement)", flush=True)
+    print("shape".ljust(14) + "".join(n.rjust(12) for n in cfgs))
+    for s in a.shape:
+        base = statistics.median(res[(s, cfgs[0])])
+        row = s.ljust(14)
+        for name in cfgs:
+            m = statistics.median(res[(s, name)])
+            row += f"{m:9.1f}({m / base:.3f})".rjust(12) if name != cfgs[0] else f"{m:12.1f}"
+        print(row, flush=True)
 
 
 if __name__ == "__main__":

@@ -279,6 +279,22 @@ STUDIES["bin_ab2"] = [
     ("fp32", 600, "python -u bench/ab_env.py --dtype fp32 --pkg base=bench/ab/base --shape 16384x16384 "
                   "--shape 32768x32768 --cfg old@base: --cfg new: --rounds 3 --iters 60"),
 ]
+# round 3, after the SGPR-base addressing: fp64 tile height / prefetch, fp32 w sweep at 3 waves
+STUDIES["tune3"] = [
+    ("fp64", 800, "python -u bench/ab_env.py --shape 16384x16384 --shape 2048x16384 --cfg base: "
+                  "--cfg pf2:PMX_PCG1_PF=2,PMX_PCG1_PF_W=1 --cfg r6:PMX_PCG1_ROWS=6 --cfg r10:PMX_PCG1_ROWS=10 "
+                  "--cfg r12:PMX_PCG1_ROWS=12 --rounds 3 --iters 100"),
+    ("fp32", 600, "python -u bench/ab_env.py --dtype fp32 --pkg w3=bench/ab/w3 --shape 16384x16384 "
+                  "--shape 32768x32768 --cfg new: --cfg w3@w3: --rounds 3 --iters 60"),
+]
+STUDIES["fresh_ab"] = [
+    ("fp64", 1000, "python -u bench/ab_env.py --fresh --pkg base=bench/ab/base --shape 16384x16384 --shape 2048x16384 "
+                   "--cfg old@base: --cfg new: --cfg r10:PMX_PCG1_ROWS=10 --cfg r12:PMX_PCG1_ROWS=12 --rounds 3 --iters 100"),
+]
+STUDIES["manyk"] = [
+    ("k", 900, "python -u bench/probe/placement.py --rounds 2 --cfg k5: --cfg k12:PMX_PLACEMENT=12 "
+               "--cfg k20:PMX_PLACEMENT=20"),
+]
 STUDIES["blocks8"] = [
     ("ab_ref", 600, "python -u bench/ab_env.py --ranks 8 --split reference --shape 16384x16384 --cfg ref: "
                     "--rounds 3 --iters 100"),

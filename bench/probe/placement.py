@@ -67,7 +67,9 @@ def child(a):
                 print(json.dumps(dict(session=k, pass_=pas, us=round(time_session(ss[k], a.iters), 1))), flush=True)
     else:
         s = pkg.make_session(p, dtype=a.dtype)
-        print(json.dumps(dict(hold_gb=a.child_hold, us=round(time_session(s, a.iters), 1))), flush=True)
+        us = round(time_session(s, a.iters), 1)
+        probe = [round(v, 3) for v in s.tile.get("placement_probe_ms", [])]
+        print(json.dumps(dict(hold_gb=a.child_hold, us=us, probe=probe)), flush=True)
     del hold
 
 
