@@ -404,6 +404,8 @@ def measure(args) -> int:
         torch.cuda.set_device(device)
     if cfg["split"] is not None and not dry:
         os.environ["PMX_PCG1_SPLIT"] = str(cfg["split"])  # read by the native driver at construction
+    if share:  # ranks sharing one GPU: no placement probe (its candidate blocks would crowd the others)
+        os.environ.setdefault("PMX_PLACEMENT", "1")
     tdev = "cuda" if info.backend == "nccl" else "cpu"
 
     def device_sync():
@@ -493,7 +495,8 @@ def measure(args) -> int:
         dt = float(t.item())
     timed_path = ("graph" if path["eager_iters"] == 0 and path["graph_iters"] > 0 else
                   "eager" if path["graph_iters"] == 0 else "mixed")
-    tile_desc = runner.tile()
+    tile_desc = dict(runner.tile())
+    tile_desc.pop("placement_probe_ms", None)  # the summary ("placement") stays; the list can be long
     valid = (not st1["done"]) and (st1["it"] - st0["it"] == args.steps) and not st1["nan"]
     pts = (args.M - 1) * (args.N - 1)
     mlups = pts * args.steps / dt / 1e6

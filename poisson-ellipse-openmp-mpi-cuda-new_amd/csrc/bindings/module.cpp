@@ -1,3 +1,4 @@
+#include <algorithm>
 // Python bindings of the native pmx library (module `_pmx`).
 //
 // The binding layer is deliberately thin: device buffers are passed as integer pointers and
@@ -537,9 +538,20 @@ PYBIND11_MODULE(_pmx, m) {
         if (!s.solver(0).single_pass()) d["b"] = one(s.solver(0).tiles_b());
         d["algo"] = s.solver(0).single_pass() ? "pcg1" : "pcg2";
         if (!s.solver(0).placement_ms().empty()) {
+          // 3 plain sweeps per candidate field block (rotating field roles), the fastest kept
+          std::vector<float> v = s.solver(0).placement_ms();
           py::list l;
-          for (float v : s.solver(0).placement_ms()) l.append(v);
-          d["placement_probe_ms"] = l;  // 3 plain sweeps per candidate field block, min kept
+          for (float x : v) l.append(x);
+          d["placement_probe_ms"] = l;
+          const auto mn = std::min_element(v.begin(), v.end());
+          py::dict q;
+          q["candidates"] = v.size();
+          q["kept"] = size_t(mn - v.begin());
+          q["kept_ms"] = *mn;
+          q["first_ms"] = v[0];
+          std::sort(v.begin(), v.end());
+          q["median_ms"] = v[v.size() / 2];
+          d["placement"] = q;
         }
         return d;
       });

@@ -174,8 +174,8 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
 
 // Bytes between consecutive fields of the one field allocation (see construct).
 constexpr long long kFieldStagger = 0;
-// Field blocks the placement probe compares (see place_fields); 1 = off.
-constexpr int kPlacementCandidates = 5;
+// Field blocks the placement probe may compare (see place_fields); 1 = off.
+constexpr int kPlacementCandidates = 160;
 
 void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   const GpuOptions& opt = opt_;
@@ -320,16 +320,20 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   if (pcg1_) place_fields();
 }
 
-// Field placement probe.  On MI355X the same sweep runs ~7% faster or slower depending on WHERE its
-// fields were allocated: a property of the allocation, stable for its lifetime and across passes
-// (8 sessions alive in one process, timed forward then in reverse: the first 2-3 allocations of
-// ~10.8 GB at 2.145 ms/iteration at 16384^2 fp64, later ones at 1.99 ms -- profiles/r3/placement/;
-// the field stagger inside the block and physically contiguous memory do not help).  So the solver
-// allocates up to K candidate blocks while free memory allows (10% headroom kept), times 3
-// plain sweeps on each with the fields in rotating roles (probe_sweeps: every field read and
-// written; zeroed fields, the init sweep's k = 0 arithmetic; init() resets everything afterwards), keeps the fastest and frees the others.  Construction-time only: nothing in the
-// iteration changes.  PMX_PLACEMENT=K overrides kPlacementCandidates (1 = off).  Skipped with an
-// external (IPC-shared) arena or a separately allocated r2.
+// Field placement probe.  On MI355X the same sweep runs at one of (at least) three rates depending
+// on WHERE its fields were allocated: a property of the allocation, stable for its lifetime and
+// across passes (8 sessions alive in one process, timed forward then in reverse).  At 16384^2 fp64,
+// 3 plain sweeps of a candidate block take ~5.45, ~4.97 or ~4.55-4.63 ms, and the iteration runs
+// at ~2150 / ~1995 / ~1810 us; in a fresh process the first blocks are slow, mostly mid-rate ones
+// follow and the fast ones appeared only ~15 blocks (~170 GB) in -- profiles/r3/placement/.  So the
+// solver allocates candidate blocks while 1/8 of the device memory that was free stays free (at
+// most K; blocks under 256 MB are not probed), times 3 plain sweeps on each with the five fields in rotating roles (probe_sweeps:
+// every field read and written; zeroed fields, the init sweep's k = 0 arithmetic; init() resets
+// everything afterwards), keeps the fastest and frees the others.  Construction time only (~10 ms
+// per 10 GB candidate); nothing in the iteration changes.  PMX_PLACEMENT=K overrides
+// kPlacementCandidates (1 = off: bench.py --share-gpu ranks and the multi-process GPU tests, whose
+// processes share one device).  Skipped with an external (IPC-shared) arena or a separately
+// allocated r2.
 // Plain sweeps (k = 0 arithmetic) with the five field blocks in rotating roles, so that every field
 // of the candidate block is read and written: role set q reads r = F[q], p = F[q+3] and writes
 // r2 = F[q+4], p0 = F[q+2] (indices mod 5; F = w, r, p0, p1, r2).
@@ -344,13 +348,15 @@ void GpuSubdomainSolver::probe_sweeps(hipStream_t s, int first, int count) {
 void GpuSubdomainSolver::place_fields() {
   int K = kPlacementCandidates;
   if (const char* e = std::getenv("PMX_PLACEMENT"); e && e[0]) K = std::atoi(e);
-  if (K <= 1 || !own_arena_ || own_r2_) return;
   const size_t block = 5 * field_stride_;
+  if (K <= 1 || !own_arena_ || own_r2_ || block < (size_t(256) << 20)) return;  // small grids: latency-bound
   std::vector<char*> cand{fields_};
+  size_t free0 = 0, total_b = 0;
+  HIP_CHECK(hipMemGetInfo(&free0, &total_b));
   while (int(cand.size()) < K) {
-    size_t free_b = 0, total_b = 0;
+    size_t free_b = 0;
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-    if (free_b < block + total_b / 10) break;
+    if (free_b < block + std::max(free0 / 8, size_t(4) << 30)) break;
     char* p = nullptr;
     if (hipMalloc(&p, block) != hipSuccess) {
       (void)hipGetLastError();

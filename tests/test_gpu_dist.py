@@ -34,7 +34,7 @@ def _run(tmp_path, world, M, N, algo=-1, split="reference", dtype="fp64", comm="
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), WORKER, "--M", str(M), "--N", str(N),
            "--algo", str(algo), "--split", split, "--dtype", dtype, "--out", out, "--comm", comm,
            "--graph-batch", str(graph_batch)]
-    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env = dict(os.environ, OMP_NUM_THREADS="1", PMX_PLACEMENT="1")  # ranks share the GPU: no placement probe
     p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=170, env=env)
     assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-4000:])
     with open(out + ".json") as f:
