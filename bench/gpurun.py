@@ -295,6 +295,12 @@ STUDIES["manyk"] = [
     ("k", 900, "python -u bench/probe/placement.py --rounds 2 --cfg k5: --cfg k12:PMX_PLACEMENT=12 "
                "--cfg k20:PMX_PLACEMENT=20"),
 ]
+STUDIES["records3"] = [
+    ("fp32_16k", 300, bench("--gpus 1 --dtype fp32 --steps 20 --warmup 5")),
+    ("fp32_32k", 400, bench("--gpus 1 --M 32768 --N 32768 --dtype fp32 --steps 20 --warmup 5")),
+    ("fp64_4096", 200, bench("--gpus 1 --M 4096 --N 4096 --steps 20 --warmup 5")),
+    ("strip_2048", 200, bench("--gpus 1 --M 2048 --N 16384 --steps 200 --warmup 20 --no-tol-solve")),
+]
 STUDIES["blocks8"] = [
     ("ab_ref", 600, "python -u bench/ab_env.py --ranks 8 --split reference --shape 16384x16384 --cfg ref: "
                     "--rounds 3 --iters 100"),
