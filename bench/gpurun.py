@@ -301,6 +301,14 @@ STUDIES["records3"] = [
     ("fp64_4096", 200, bench("--gpus 1 --M 4096 --N 4096 --steps 20 --warmup 5")),
     ("strip_2048", 200, bench("--gpus 1 --M 2048 --N 16384 --steps 200 --warmup 20 --no-tol-solve")),
 ]
+STUDIES["ranks3"] = [
+    ("strip_8192", 200, bench("--gpus 1 --M 8192 --N 16384 --steps 100 --warmup 20 --no-tol-solve")),
+    ("strip_4096", 200, bench("--gpus 1 --M 4096 --N 16384 --steps 200 --warmup 20 --no-tol-solve")),
+    ("block_8192x4096", 200, bench("--gpus 1 --M 8192 --N 4096 --steps 200 --warmup 20 --no-tol-solve")),
+    ("timeline_2048", 150, "rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ranks3/tl2048 -o run -- "
+                           "poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx 2048 16384 --max-iter 600 --json"),
+    ("timeline_2048_sum", 60, "python3 bench/trace_timeline.py gpurun_out/ranks3/tl2048/run_kernel_trace.csv --skip 200"),
+]
 STUDIES["blocks8"] = [
     ("ab_ref", 600, "python -u bench/ab_env.py --ranks 8 --split reference --shape 16384x16384 --cfg ref: "
                     "--rounds 3 --iters 100"),
