@@ -89,13 +89,31 @@ __device__ __forceinline__ T* col_ptr(T* row, int c) {
 }
 
 template <typename T, int VEC>
+__device__ __forceinline__ void load_cols_nt(const T* row, int c0, int cmax, T (&out)[VEC]) {
+#pragma unroll
+  for (int q = 0; q < VEC / 2; ++q) {
+    typedef T V __attribute__((ext_vector_type(2)));
+    const V v = __builtin_nontemporal_load(reinterpret_cast<const V*>(col_ptr(row, min(c0 + 2 * q, cmax))));
+    out[2 * q] = v[0];
+    out[2 * q + 1] = v[1];
+  }
+}
+
+template <typename T, int VEC>
 __device__ __forceinline__ void load_cols(const T* row, int c0, int cmax, T (&out)[VEC]) {
 #pragma unroll
   for (int q = 0; q < VEC / 2; ++q) {
+#ifdef PMX_PCG1_NT_LOADS  // study build: streaming hint on every field load
+    typedef T V __attribute__((ext_vector_type(2)));
+    const V v = __builtin_nontemporal_load(reinterpret_cast<const V*>(col_ptr(row, min(c0 + 2 * q, cmax))));
+    out[2 * q] = v[0];
+    out[2 * q + 1] = v[1];
+#else
     T v[2];
     vload_raw<T, 2>(col_ptr(row, min(c0 + 2 * q, cmax)), v);
     out[2 * q] = v[0];
     out[2 * q + 1] = v[1];
+#endif
   }
 }
 
@@ -317,11 +335,27 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
 
   auto fetch = [&](int m, Pcg1Row<T, VEC>& b) {
     const int mc = min(max(m, -1), G.nx + 2);  // rows -1 .. nx+2 exist (2 ghost layers)
+#ifdef PMX_PCG1_NT_PRIV
+    // study build: rows no vertically adjacent tile marches (i0+2 .. i1-2) with the streaming hint,
+    // so the L2 keeps the shared halo rows longer
+    if (mc >= i0 + 2 && mc <= i1 - 2) {
+      load_cols_nt<T, VEC>(rold + int64_t(mc) * P, c0, cmax, b.r);
+      load_cols_nt<T, VEC>(pold + int64_t(mc) * P, c0, cmax, b.p);
+    } else {
+      load_cols<T, VEC>(rold + int64_t(mc) * P, c0, cmax, b.r);
+      load_cols<T, VEC>(pold + int64_t(mc) * P, c0, cmax, b.p);
+    }
+#else
     load_cols<T, VEC>(rold + int64_t(mc) * P, c0, cmax, b.r);
     load_cols<T, VEC>(pold + int64_t(mc) * P, c0, cmax, b.p);
+#endif
     if constexpr (WUP) {  // w of the row stage B handles next step
       const int wc = min(max(m - DIR, -1), G.nx + 2);
+#ifdef PMX_PCG1_NT_PRIV
+      load_cols_nt<T, VEC>(w + int64_t(wc) * P, c0, cmax, b.w);
+#else
       load_cols<T, VEC>(w + int64_t(wc) * P, c0, cmax, b.w);
+#endif
       // p^{k-2} still sits in the buffer this sweep overwrites with p^k: the owner of a point
       // reads it here, before its own store of that row (rows it does not own are never used)
       if constexpr (WM == 3) load_cols<T, VEC>(pnew + int64_t(wc) * P, c0, cmax, b.q);
