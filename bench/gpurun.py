@@ -309,6 +309,13 @@ STUDIES["ranks3"] = [
                            "poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx 2048 16384 --max-iter 600 --json"),
     ("timeline_2048_sum", 60, "python3 bench/trace_timeline.py gpurun_out/ranks3/tl2048/run_kernel_trace.csv --skip 200"),
 ]
+STUDIES["batch4"] = [
+    ("ntp", 700, "python -u bench/ab_env.py --fresh --pkg ntp=bench/ab/ntp --shape 16384x16384 --shape 2048x16384 "
+                 "--cfg base: --cfg ntp@ntp: --rounds 4 --iters 200"),
+    ("fp32_16k", 300, bench("--gpus 1 --dtype fp32 --steps 20 --warmup 5")),
+    ("fp32_32k", 400, bench("--gpus 1 --M 32768 --N 32768 --dtype fp32 --steps 20 --warmup 5")),
+    ("fp64_32k", 400, bench("--gpus 1 --M 32768 --N 32768 --steps 20 --warmup 5 --tol-time-cap 200")),
+]
 STUDIES["blocks8"] = [
     ("ab_ref", 600, "python -u bench/ab_env.py --ranks 8 --split reference --shape 16384x16384 --cfg ref: "
                     "--rounds 3 --iters 100"),

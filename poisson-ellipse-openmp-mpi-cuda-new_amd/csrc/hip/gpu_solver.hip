@@ -364,14 +364,19 @@ void GpuSubdomainSolver::place_fields() {
     }
     cand.push_back(p);
   }
-  if (cand.size() > 1) {
-    hipStream_t s;
-    hipEvent_t e0, e1;
+  if (cand.size() == 1) return;
+  auto keep_only = [&](size_t keep) {  // free every other candidate, point the fields at `keep`
+    for (size_t c = 0; c < cand.size(); ++c)
+      if (c != keep) (void)hipFree(cand[c]);
+    fields_ = cand[keep];
+    r2_ = field_raw(4);
+  };
+  hipStream_t s = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  try {
     HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreate(&e0));
     HIP_CHECK(hipEventCreate(&e1));
-    const long long hk = host_k_;
-    host_k_ = 0;  // plain sweep
     placement_ms_.assign(cand.size(), 0.f);
     for (size_t c = 0; c < cand.size(); ++c) {
       fields_ = cand[c];
@@ -384,16 +389,16 @@ void GpuSubdomainSolver::place_fields() {
       HIP_CHECK(hipEventSynchronize(e1));
       HIP_CHECK(hipEventElapsedTime(&placement_ms_[c], e0, e1));
     }
-    host_k_ = hk;
-    const size_t best = size_t(std::min_element(placement_ms_.begin(), placement_ms_.end()) - placement_ms_.begin());
-    for (size_t c = 0; c < cand.size(); ++c)
-      if (c != best) HIP_CHECK(hipFree(cand[c]));
-    fields_ = cand[best];
-    r2_ = field_raw(4);
-    HIP_CHECK(hipEventDestroy(e0));
-    HIP_CHECK(hipEventDestroy(e1));
-    HIP_CHECK(hipStreamDestroy(s));
+  } catch (...) {  // keep the first block (the solver's own), release the candidates, then report
+    if (s) (void)hipStreamSynchronize(s);
+    keep_only(0);
+    placement_ms_.clear();
+    throw;
   }
+  keep_only(size_t(std::min_element(placement_ms_.begin(), placement_ms_.end()) - placement_ms_.begin()));
+  HIP_CHECK(hipEventDestroy(e0));
+  HIP_CHECK(hipEventDestroy(e1));
+  HIP_CHECK(hipStreamDestroy(s));
 }
 
 void GpuSubdomainSolver::progress(long long out[3]) const {
