@@ -204,8 +204,11 @@ def _validate(argv):
 
 def _share(argv):
     """multi-rank rehearsal on the one GPU under the supervisor: ranks ... [-- bench.py args]"""
-    ranks = [int(x) for x in argv if x.isdigit()] or [2, 4, 8]
-    extra = " ".join(x for x in argv if not x.isdigit())
+    lead = 0  # rank counts are the leading integers; everything after goes to bench.py
+    while lead < len(argv) and argv[lead].isdigit():
+        lead += 1
+    ranks = [int(x) for x in argv[:lead]] or [2, 4, 8]
+    extra = " ".join(argv[lead:])
     return [(f"share{n}", 420, bench(f"--gpus {n} --share-gpu --steps 20 --warmup 5 {extra}")) for n in ranks]
 
 
