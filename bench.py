@@ -16,19 +16,28 @@ x^2 + 4y^2 < 1, zero initial guess (there is no dataset).
 Multi-GPU runs are supervised (reference lifecycle: stage4-mpi+cuda/poisson_mpi_cuda_f.cu:986-1039).
 The process(es) started by the user or by torchrun never touch the GPU: they start the measuring
 ranks as child processes and walk a fallback ladder of transports, each rung in fresh processes:
-    rung 1  native RCCL, iterations captured in hipGraphs, split sweep (the production path)
-    rung 2  native RCCL, eager launches, no split sweep
+    rung 1  native RCCL, iterations captured in hipGraphs, split sweep, ghost exchange on its own
+            communicator and stream, overlapped with the sweep (the production path)
+    rung 2  native RCCL, fully serialized: eager launches, ONE communicator, every call on the compute
+            stream in a fixed order (all-reduce, then the send/recv group: the reference's own
+            ordering, stage4-mpi+cuda/poisson_mpi_cuda_f.cu:851-943) -- no two RCCL kernels are ever
+            in flight together, which removes the two-communicator interlock rung 1 could hit
     rung 3  native IPC transport (peer arenas mapped with hipIpcOpenMemHandle, epoch flags; no
             RCCL at all), graphs and split sweep
     rung 4  torch.distributed ProcessGroupNCCL (= RCCL) driving the same native kernels
 A --share-gpu rehearsal (every rank on GPU 0) starts at rung 3, then rung 4 over gloo.
-Every rank runs under a progress watchdog: each phase (setup, canary iteration, first graph batch,
-warmup, timed region, tolerance solve) has a deadline; on expiry the rank prints the phase and the
-device's own progress counters (sweeps reduced, ghost exchanges packed / unpacked) and exits, and
-the supervisor moves to the next rung.  The JSON line names the rung that produced it, the transport
-(`comm`), `rccl_graph`, `split_sweep`, the failed rungs, and whether the timed region replayed graphs
-(`timed_path`).  A run whose rank count differs from --gpus fails; it never measures fewer GPUs
-than it reports.
+Every rank runs under a progress watchdog: each phase (setup, comm-init, canary iteration, first
+graph batch, warmup, timed region, tolerance solve) has a deadline (DEADLINES); on expiry the rank
+prints the phase and the device's own progress counters (sweeps reduced, ghost exchanges packed /
+unpacked) and exits, and the supervisor moves on.  Failures are classified by the phase the failing
+rank was in: a rung that fails in comm-init (the RCCL communicator initialisation) skips the other
+RCCL rung, whose initialisation is identical.  The whole ladder runs within --ladder-budget seconds
+(540: rung caps RUNG_CAP, each hang ends at its phase deadline), so even a rung-1 hang plus a rung-2
+hang leave rung 3 its full cap.  The JSON line names the rung that produced it, the transport
+(`comm`), `rccl_graph`, `split_sweep`, every attempt with its phase, and whether the timed region
+replayed graphs (`timed_path`); if every rung fails it is still printed, with value null and
+valid false.  A run whose rank count differs from --gpus fails; it never measures fewer GPUs than it
+reports.
 
 After the timed region a full solve to ||w^{k+1}-w^k|| < 1e-6 reports iters-to-tol and the error
 of the solution against the analytic u = (1 - x^2 - 4y^2)/10 (l2_error, max_error; disable with
@@ -53,13 +62,24 @@ METRIC = "grid-point updates/sec (MLUPS) + iters-to-tol, 16384^2 grid at 1/2/4/8
 TOL_NOTE = ("stop rule ||w^{k+1}-w^k|| < delta absolute (reference rule); at fine grids the solve ends "
             "before discretisation accuracy")
 
-# fallback ladder (see the module docstring); `split` None = the driver's default for the transport
+# fallback ladder (see the module docstring); `split` None = the driver's default for the transport,
+# `overlap` None = --overlap
 RUNGS = {
-    1: dict(comm="native", rccl_graph=True, split=None),
-    2: dict(comm="native", rccl_graph=False, split=0),
-    3: dict(comm="ipc", rccl_graph=False, split=None),
-    4: dict(comm="torch", rccl_graph=False, split=0),
+    1: dict(comm="native", rccl_graph=True, split=None, overlap=None),
+    2: dict(comm="native", rccl_graph=False, split=0, overlap=False),
+    3: dict(comm="ipc", rccl_graph=False, split=None, overlap=None),
+    4: dict(comm="torch", rccl_graph=False, split=0, overlap=None),
 }
+# Per-phase watchdog deadlines (seconds, x --deadline-scale); comm-init is set by DistGpuPCG (its RCCL
+# / IPC initialisation watchdog + 15 s).  No phase of a healthy 16384^2 run comes close: setup
+# (process group, solver, placement probe) takes ~5-20 s, the rest is sub-second per poll.
+DEADLINES = {"setup": 120, "comm-init": 105, "canary": 60, "first-batch": 60, "warmup": 60, "timed": 60,
+             "tol-solve": 60, "accuracy": 90, "profile": 300, "report": 60, "shutdown": 60}
+COMM_INIT_TIMEOUT = 90.0  # DistGpuPCG's own watchdog around the blocking RCCL / IPC initialisation
+# Hard per-rung limits of the supervisor (a rung normally ends far earlier: success in ~30-60 s, a
+# hang at its phase deadline).  Worst case rung 1 + rung 2 = 360 s of a 540-s ladder budget.
+RUNG_CAP = {1: 210.0, 2: 150.0, 3: 240.0, 4: 240.0}
+LADDER_BUDGET = 540.0
 
 
 def parse(argv=None):
@@ -100,7 +120,7 @@ def parse(argv=None):
     ap.add_argument("--exact", action="store_true", help="reference arithmetic order in the fused kernels")
     ap.add_argument("--tol-solve", dest="tol_solve", action="store_true", default=True)
     ap.add_argument("--no-tol-solve", dest="tol_solve", action="store_false")
-    ap.add_argument("--tol-time-cap", type=float, default=300.0, help="seconds allowed for the tol solve")
+    ap.add_argument("--tol-time-cap", type=float, default=100.0, help="seconds allowed for the tol solve")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--cpu-dry-run", action="store_true",
                     help="test the launch/ladder/timing/reporting flow on CPU (gloo, plain-PyTorch PCG); "
@@ -115,8 +135,13 @@ def parse(argv=None):
                          "the reference's stage-4 buckets on stderr and added to the JSON line")
     ap.add_argument("--deadline-scale", type=float, default=1.0,
                     help="multiplies every progress-watchdog deadline")
-    ap.add_argument("--rung-timeout", type=float, default=480.0,
-                    help="supervisor: hard limit (s) for one rung's processes")
+    ap.add_argument("--rung-timeout", type=float, default=0.0,
+                    help="supervisor: hard limit (s) for one rung's processes (0 = RUNG_CAP per rung)")
+    ap.add_argument("--ladder-budget", type=float, default=LADDER_BUDGET,
+                    help="supervisor: wall-clock budget (s) of the whole ladder")
+    ap.add_argument("--placement", type=int, default=8,
+                    help="placement probe: candidate field blocks timed, the fastest kept (0 = off; "
+                         "bounded by 0.5 s and half the free memory; off when ranks share a GPU)")
     return ap.parse_args(argv)
 
 
@@ -126,21 +151,34 @@ def parse(argv=None):
 class Watch:
     """Per-phase deadlines.  A rank stuck in a phase (a collective whose peer never posts, a kernel
     that never finishes) cannot be interrupted from Python; this thread reports where it is and ends
-    the process, which is what lets the supervisor move on instead of burning the lease."""
+    the process, which is what lets the supervisor move on instead of burning the lease.  The current
+    phase is also written to `phase_file` (when given), so the supervisor can classify a failure by
+    the phase the rank died in."""
 
     EXIT_CODE = 87
 
-    def __init__(self, rank: int, scale: float = 1.0):
-        self.rank, self.scale = rank, scale
+    def __init__(self, rank: int, scale: float = 1.0, phase_file: str | None = None):
+        self.rank, self.scale, self.phase_file = rank, scale, phase_file
         self.name, self.deadline, self.t0 = "start", None, time.monotonic()
         self.progress = None  # callable -> device progress tuple, or None
+        self.on_phase = None  # fault-injection hook: called with the phase name after it is entered
         self._lock = threading.Lock()
         threading.Thread(target=self._run, daemon=True, name="pmx-watch").start()
 
-    def phase(self, name: str, seconds: float):
+    def phase(self, name: str, seconds: float | None = None):
+        seconds = DEADLINES[name] if seconds is None else seconds
         with self._lock:
             self.name, self.t0 = name, time.monotonic()
             self.deadline = self.t0 + seconds * self.scale
+        if self.phase_file:
+            try:
+                with open(self.phase_file + ".tmp", "w") as f:
+                    f.write(name)
+                os.replace(self.phase_file + ".tmp", self.phase_file)
+            except OSError:
+                pass
+        if self.on_phase:
+            self.on_phase(name)
 
     def _run(self):
         while True:
@@ -163,14 +201,16 @@ class Watch:
 
 def _fault(rung: int, rank: int):
     """Fault injection for the ladder tests: PMX_BENCH_FAULT='1:hang,2:fail' (optionally '1:hang@0',
-    rank 0 only) -> (kind, phase) for this rung/rank, kind in hang|fail|crash."""
+    rank 0 only) -> (kind, phase) for this rung/rank: kind in hang|fail|crash, phase "canary"
+    (hang), "setup" (fail) or, with the suffix -init ('1:hang-init'), "comm-init"."""
     spec = os.environ.get("PMX_BENCH_FAULT", "")
     for item in filter(None, (x.strip() for x in spec.split(","))):
         r, _, what = item.partition(":")
         what, _, who = what.partition("@")
         if int(r) == rung and (not who or int(who) == rank):
-            return what
-    return None
+            kind, _, tag = what.partition("-")
+            return kind, ("comm-init" if tag == "init" else "canary" if kind == "hang" else "setup")
+    return None, None
 
 
 # =============================================================================================
@@ -217,29 +257,78 @@ def _ladder(args) -> list[int]:
     return rungs if args.ladder == "on" else rungs[:1]
 
 
-def _run_rung_local(args, rung: int, result: str) -> tuple[bool, str]:
-    """All ranks are children of this process (no launcher)."""
+# phases in the order a rank passes them (the least advanced rank of a failed rung is its cause: the
+# others wait for it in a collective and time out in a later phase)
+PHASE_ORDER = ("start", "setup", "comm-init", "canary", "first-batch", "warmup", "timed", "tol-solve",
+               "accuracy", "profile", "report", "shutdown")
+
+
+def least_advanced(phases) -> str:
+    known = [p for p in phases if p in PHASE_ORDER]
+    return min(known, key=PHASE_ORDER.index) if known else (list(phases) or [""])[0]
+
+
+def _read_phase(result: str, rank: int) -> str:
+    try:
+        with open(f"{result}.phase.{rank}") as f:
+            return f.read().strip() or "start"
+    except OSError:
+        return "start"  # died before its watchdog wrote anything (interpreter start, imports)
+
+
+def skipped_after(rung: int, phase: str, remaining: list[int]) -> list[int]:
+    """Rungs made pointless by a failure of `rung` in `phase`: an RCCL rung that failed while
+    initialising its communicator takes the other RCCL rung with it (identical ncclCommInitRank;
+    rung 2 only changes the schedule AFTER initialisation)."""
+    if phase == "comm-init" and RUNGS[rung]["comm"] == "native":
+        return [r for r in remaining if RUNGS[r]["comm"] == "native"]
+    return []
+
+
+KILL_GRACE = 10.0  # after a failure or the cap: SIGTERM, then SIGKILL this much later
+
+
+def rung_cap(args, rung: int, budget_left: float) -> float:
+    cap = args.rung_timeout if args.rung_timeout > 0 else RUNG_CAP[rung]
+    return max(0.0, min(cap, budget_left - KILL_GRACE))
+
+
+def worst_case_ladder_seconds(args) -> float:
+    """Upper bound of the ladder's wall time with rungs 1 and 2 hanging and rung 3 succeeding: each
+    rung ends at its cap at the latest, the supervisor adds its 10-s kill grace (deadline scale 1)."""
+    ladder = _ladder(args)
+    t = 0.0
+    for r in ladder[:3]:
+        t += rung_cap(args, r, args.ladder_budget - t) + KILL_GRACE
+    return t
+
+
+def _run_rung_local(args, rung: int, result: str, cap: float) -> tuple[bool, str, str]:
+    """All ranks are children of this process (no launcher).  -> (ok, reason, phase of the failure)."""
     world = args.gpus
     port = _free_port()
     procs = [_spawn(_child_env(r, r, world, port, rung, result)) for r in range(world)]
-    t0, failed_at, reason = time.monotonic(), None, ""
+    t0, failed_at, reason, phase = time.monotonic(), None, "", ""
     while True:
         codes = [p.poll() for p in procs]
         bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
         if bad and failed_at is None:
             failed_at = time.monotonic()
-            reason = f"rank {bad[0][0]} exited with status {bad[0][1]}"
+            phase = least_advanced([_read_phase(result, r) for r in range(world)])
+            reason = (f"rank {bad[0][0]} exited with status {bad[0][1]} in phase '{_read_phase(result, bad[0][0])}'"
+                      f" (least advanced rank: '{phase}')")
             print(f"[bench] rung {rung}: {reason}; stopping the other ranks", file=sys.stderr, flush=True)
             for p in procs:
                 _kill(p, signal.SIGTERM)
         if all(c is not None for c in codes):
             break
-        if failed_at is not None and time.monotonic() - failed_at > 10:
+        if failed_at is not None and time.monotonic() - failed_at > KILL_GRACE:
             for p in procs:
                 _kill(p)
-        if failed_at is None and time.monotonic() - t0 > args.rung_timeout:
+        if failed_at is None and time.monotonic() - t0 > cap:
             failed_at = time.monotonic()
-            reason = f"rung timeout ({args.rung_timeout:.0f} s)"
+            phase = least_advanced([_read_phase(result, r) for r in range(world)])
+            reason = f"rung timeout ({cap:.0f} s) in phase '{phase}'"
             print(f"[bench] rung {rung}: {reason}; killing its ranks", file=sys.stderr, flush=True)
             for p in procs:
                 _kill(p)
@@ -247,12 +336,15 @@ def _run_rung_local(args, rung: int, result: str) -> tuple[bool, str]:
     ok = failed_at is None and all(p.returncode == 0 for p in procs)
     if not ok and not reason:
         reason = f"exit status {[p.returncode for p in procs]}"
-    return ok, reason
+    return ok, reason, phase
 
 
-def _run_rung_torchrun(args, rung: int, result: str, store, rank: int, local_rank: int) -> tuple[bool, str]:
+def _run_rung_torchrun(args, rung: int, result: str, cap: float, store, rank: int,
+                       local_rank: int) -> tuple[bool, str, str]:
     """One supervisor per rank (torchrun started them): each runs its own rank's child; the
-    supervisors share torchrun's store to agree on a port and to stop early when any rank fails."""
+    supervisors share torchrun's store to agree on a port and to stop early when any rank fails.
+    The first failure's reason and phase go through the store, so every supervisor walks the
+    ladder identically."""
     import torch
     import torch.distributed as dist
 
@@ -263,12 +355,16 @@ def _run_rung_torchrun(args, rung: int, result: str, store, rank: int, local_ran
     port = int(store.get(f"{key}/port").decode())
     p = _spawn(_child_env(rank, local_rank, world, port, rung, result))
     t0, mine = time.monotonic(), ""
+
+    def report(reason):
+        store.compare_set(f"{key}/fail", "", reason)
+
     while True:
         c = p.poll()
         if c is not None:
             if c != 0:
-                mine = f"rank {rank} exited with status {c}"
-                store.set(f"{key}/fail", mine)
+                mine = f"rank {rank} exited with status {c} in phase '{_read_phase(result, rank)}'"
+                report(mine)
             break
         if store.check([f"{key}/fail"]):
             time.sleep(5)  # let this rank's own watchdog / error path report first
@@ -277,18 +373,37 @@ def _run_rung_torchrun(args, rung: int, result: str, store, rank: int, local_ran
             _kill(p)
             p.wait()
             break
-        if time.monotonic() - t0 > args.rung_timeout:
-            mine = f"rank {rank}: rung timeout ({args.rung_timeout:.0f} s)"
-            store.set(f"{key}/fail", mine)
+        if time.monotonic() - t0 > cap:
+            mine = f"rank {rank}: rung timeout ({cap:.0f} s) in phase '{_read_phase(result, rank)}'"
+            report(mine)
             _kill(p)
             p.wait()
             break
         time.sleep(0.2)
+    store.set(f"{key}/phase/{rank}", _read_phase(result, rank))
     bad = torch.tensor([0 if (p.returncode == 0 and not mine) else 1], dtype=torch.int32)
-    dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+    dist.all_reduce(bad, op=dist.ReduceOp.MAX)  # after it, every rank's phase is in the store
     ok = int(bad.item()) == 0
-    reason = "" if ok else (store.get(f"{key}/fail").decode() if store.check([f"{key}/fail"]) else mine or "failed")
-    return ok, reason
+    if ok:
+        return True, "", ""
+    phase = least_advanced([store.get(f"{key}/phase/{r}").decode() for r in range(world)])
+    reason = store.get(f"{key}/fail").decode() if store.check([f"{key}/fail"]) else mine or "failed"
+    return False, f"{reason} (least advanced rank: '{phase}')", phase
+
+
+def _failed_record(args, attempts) -> dict:
+    """The JSON line when every rung failed: no measurement, the ladder's reasons."""
+    return {"metric": METRIC, "value": None, "unit": "MLUPS", "n_gpus": args.gpus, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": args.dtype,
+            "data": "none: every rung of the transport ladder failed (see ladder)",
+            "config": {"model": f"fictitious-domain Poisson ellipse, Jacobi-PCG, {args.M}x{args.N}",
+                       "global_batch": 1, "seq_len": (args.M - 1) * (args.N - 1),
+                       "parallelism": f"domain{args.gpus}", "split": args.split, "grid": [args.M, args.N],
+                       "rung": None},
+            "valid": False, "baseline_mlups": BASELINE_MLUPS,
+            "error": "every rung of the ladder failed: " + "; ".join(
+                f"rung {a['rung']}: {a.get('reason', 'skipped')}" for a in attempts)}
 
 
 def supervise(args) -> int:
@@ -319,35 +434,50 @@ def supervise(args) -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", rank))
     tmp = tempfile.mkdtemp(prefix="pmx_bench_")
     attempts, final = [], None
-    for rung in _ladder(args):
+    ladder = _ladder(args)
+    skip = set()
+    t_ladder = time.monotonic()
+    for i, rung in enumerate(ladder):
+        if rung in skip:
+            attempts.append(dict(rung=rung, **RUNGS[rung], ok=False, skipped=True,
+                                 reason="skipped: an earlier rung failed in its identical comm-init"))
+            continue
+        left = args.ladder_budget - (time.monotonic() - t_ladder)
+        cap = rung_cap(args, rung, left)
+        if cap < 30.0:
+            attempts.append(dict(rung=rung, **RUNGS[rung], ok=False, skipped=True,
+                                 reason=f"skipped: ladder budget spent ({left:.0f} s left)"))
+            continue
         result = os.path.join(tmp, f"rung{rung}.json")
         t0 = time.monotonic()
         if launched:
-            ok, reason = _run_rung_torchrun(args, rung, result, store, rank, local_rank)
+            ok, reason, phase = _run_rung_torchrun(args, rung, result, cap, store, rank, local_rank)
         else:
-            ok, reason = _run_rung_local(args, rung, result)
+            ok, reason, phase = _run_rung_local(args, rung, result, cap)
         att = dict(rung=rung, **RUNGS[rung], ok=ok, seconds=round(time.monotonic() - t0, 1))
         if not ok:
-            att["reason"] = reason
+            att["reason"], att["phase"] = reason, phase
         attempts.append(att)
         if ok:
             if rank == 0:
                 with open(result) as f:
                     final = json.loads(f.read().strip().splitlines()[-1])
             break
+        skip |= set(skipped_after(rung, phase, ladder[i + 1:]))
         print(f"[bench] rung {rung} ({RUNGS[rung]}) failed: {reason}", file=sys.stderr, flush=True)
     rc = 0
     if rank == 0:
         if final is None:
             print(f"[bench] every rung of the ladder failed: {attempts}", file=sys.stderr, flush=True)
+            final = _failed_record(args, attempts)
             rc = 1
-        else:
-            final["ladder"] = attempts
-            line = json.dumps(final)
-            print(line, flush=True)
-            if args.json_out:
-                with open(args.json_out, "w") as f:
-                    f.write(line + "\n")
+        final["ladder"] = attempts
+        final["ladder_seconds"] = round(time.monotonic() - t_ladder, 1)
+        line = json.dumps(final)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
     if launched:
         import torch
         import torch.distributed as dist
@@ -380,17 +510,26 @@ def measure(args) -> int:
     dry = args.cpu_dry_run
     share = args.share_gpu and not dry
     env = launch.env_info()
-    watch = Watch(env.rank, args.deadline_scale)
-    fault = _fault(rung, env.rank) if supervised else None
+    result_path = os.environ.get("PMX_BENCH_RESULT")
+    watch = Watch(env.rank, args.deadline_scale,
+                  phase_file=f"{result_path}.phase.{env.rank}" if supervised and result_path else None)
+    fault, fault_phase = _fault(rung, env.rank) if supervised else (None, None)
     if fault == "crash":
         os._exit(3)
 
-    watch.phase("setup", 300)
+    def on_phase(name):  # fault injection at the phase it names
+        if fault and name == fault_phase:
+            if fault == "hang":
+                time.sleep(10 ** 6)  # the watchdog ends this rank
+            raise RuntimeError(f"injected failure (PMX_BENCH_FAULT) at rung {rung}, phase {name}")
+
+    watch.on_phase = on_phase
+    watch.phase("setup")
     if env.world != args.gpus:
         raise SystemExit(f"[bench] --gpus {args.gpus} but {env.world} rank(s) came up (WORLD_SIZE); refusing to "
                          "report a different GPU count")
     # Python-level coordination (uid broadcast, agreement, barriers, MAX over ranks) stays on gloo for
-    # the native transports: no third (torch) RCCL communicator next to the solver's two
+    # the native transports: no third (torch) RCCL communicator next to the solver's
     backend = "nccl" if (not dry and not share and cfg["comm"] == "torch") else "gloo"
     info = launch.init_distributed(backend=backend if env.world > 1 else None,
                                    device_type="cpu" if (dry or share or backend == "gloo") else None)
@@ -404,8 +543,7 @@ def measure(args) -> int:
         torch.cuda.set_device(device)
     if cfg["split"] is not None and not dry:
         os.environ["PMX_PCG1_SPLIT"] = str(cfg["split"])  # read by the native driver at construction
-    if share:  # ranks sharing one GPU: no placement probe (its candidate blocks would crowd the others)
-        os.environ.setdefault("PMX_PLACEMENT", "1")
+    overlap = (args.overlap == "on") if cfg["overlap"] is None else cfg["overlap"]
     tdev = "cuda" if info.backend == "nccl" else "cpu"
 
     def device_sync():
@@ -415,34 +553,35 @@ def measure(args) -> int:
     problem = pmx.PoissonEllipse(M=args.M, N=args.N, breakdown_tol=args.breakdown_tol)
     kw = dict(split=args.split, dtype=args.dtype, kernel=args.kernel, block=args.block, vec=args.vec,
               waves=args.waves, tile_rows=args.tile_rows, exact=args.exact, graph_batch=args.graph_batch,
-              overlap=args.overlap == "on", vec_b=args.vec_b, tile_rows_b=args.tile_rows_b,
+              overlap=overlap, vec_b=args.vec_b, tile_rows_b=args.tile_rows_b,
               b_ring=args.b_kernel == "ring")
-    if fault == "fail":
-        raise RuntimeError(f"injected failure (PMX_BENCH_FAULT) at rung {rung}")
+    dkw = dict(kw, placement=0 if share else args.placement, phase=watch.phase, init_timeout=COMM_INIT_TIMEOUT)
     if dry:
         tp = importlib.import_module(pkg_name + ".models.torch_pcg")
         comm = importlib.import_module(pkg_name + ".parallel.comm")
+        watch.phase("comm-init")
         runner = ds.TorchRunner(tp.TorchPCG(problem, comm=comm.TorchComm() if world > 1 else None,
                                             split=args.split), problem, info)
         comm_used = "gloo" if world > 1 else "self"
     elif world == 1:
         models = importlib.import_module(pkg_name + ".models")
-        runner = ds.SessionRunner(models.make_session(problem, ranks=1, device=info.local_rank, **kw), problem, info)
+        runner = ds.SessionRunner(models.make_session(problem, ranks=1, device=info.local_rank,
+                                                      placement=args.placement, **kw), problem, info)
         comm_used = "self"
     elif share and cfg["comm"] == "ipc":
-        runner = ds.DistGpuPCG(problem, info, comm="ipc", device=0, **kw)
+        runner = ds.DistGpuPCG(problem, info, comm="ipc", device=0, **dkw)
         comm_used = "ipc"
     elif share:
-        runner = ds.DistGpuPCG(problem, info, comm="torch", device=0, **kw)
+        runner = ds.DistGpuPCG(problem, info, comm="torch", device=0, **dkw)
         comm_used = "gloo-host-staged"
     elif cfg["comm"] == "ipc":
-        runner = ds.DistGpuPCG(problem, info, comm="ipc", **kw)
+        runner = ds.DistGpuPCG(problem, info, comm="ipc", **dkw)
         comm_used = "ipc"
     elif cfg["comm"] == "native":
-        runner = ds.DistGpuPCG(problem, info, comm="native", rccl_graph=cfg["rccl_graph"], **kw)
+        runner = ds.DistGpuPCG(problem, info, comm="native", rccl_graph=cfg["rccl_graph"], **dkw)
         comm_used = "rccl"
     else:
-        runner = ds.DistGpuPCG(problem, info, comm="torch", **kw)
+        runner = ds.DistGpuPCG(problem, info, comm="torch", **dkw)
         comm_used = "torch-nccl"
     watch.progress = getattr(runner, "progress", None)
 
@@ -451,24 +590,22 @@ def measure(args) -> int:
             dist.barrier()
 
     # ---------------- canary: one eager iteration, then the first graph batch ----------------
-    watch.phase("canary", 120)
+    watch.phase("canary")
     runner.init()
     it0 = runner.state()["it"]
-    if fault == "hang":
-        time.sleep(10 ** 6)  # the watchdog ends this rank
     runner.step_eager(1)
     runner.synchronize()
     stc = runner.state()
     if stc["it"] != it0 + 1 and not stc["done"]:
         raise RuntimeError(f"canary iteration: device iteration counter {it0} -> {stc['it']}")
-    watch.phase("first-batch", 120)
+    watch.phase("first-batch")
     if getattr(runner, "graphs", False):
         runner.prepare(args.graph_batch)
         runner.step(args.graph_batch)
         runner.synchronize()
 
     # ---------------- warmup (captures every graph the timed region replays) ----------------
-    watch.phase("warmup", 120 + 0.05 * args.warmup)
+    watch.phase("warmup", DEADLINES["warmup"] + 0.05 * args.warmup)
     runner.init()
     runner.step(args.warmup)
     runner.synchronize()
@@ -477,7 +614,7 @@ def measure(args) -> int:
     runner.reset_path_stats()
 
     # ---------------- timed region ----------------
-    watch.phase("timed", 120 + 0.05 * args.steps)
+    watch.phase("timed", DEADLINES["timed"] + 0.05 * args.steps)
     barrier()
     device_sync()
     t0 = time.perf_counter()
@@ -504,7 +641,7 @@ def measure(args) -> int:
     # ---------------- iterations to tolerance + accuracy ----------------
     tol = {}
     if args.tol_solve:
-        watch.phase("tol-solve", 120)
+        watch.phase("tol-solve")
         runner.init()
         barrier()
         device_sync()
@@ -516,7 +653,7 @@ def measure(args) -> int:
             runner.step(batch)
             launched += batch
             st = runner.state()
-            watch.phase("tol-solve", 120)
+            watch.phase("tol-solve")
             stop = 2 if (st["done"] or launched > max_iter + batch) else 0
             if not stop and time.perf_counter() - ts > args.tol_time_cap:
                 stop = 1
@@ -530,7 +667,7 @@ def measure(args) -> int:
         runner.synchronize()
         barrier()
         tsolve = time.perf_counter() - ts
-        watch.phase("accuracy", 300)
+        watch.phase("accuracy")
         err = runner.error_norms()
         tol = dict(iters_to_tol=int(st["iters"]) if st["done"] else None, tol_status=st["status"],
                    tol_final_diff=st["diff"], tol_solve_seconds=round(tsolve, 4),
@@ -540,7 +677,7 @@ def measure(args) -> int:
 
     phases = {}
     if args.profile_phases > 0 and not dry:
-        watch.phase("profile", 300)
+        watch.phase("profile")
         ph = runner.profile(args.profile_phases)
         phases = {"phase_seconds_per_iter_max_over_ranks": {k: v / args.profile_phases for k, v in ph.items()},
                   "phase_note": "compute = the whole fused sweep (A p, update, D^-1, A z); dot = the device "
@@ -550,7 +687,7 @@ def measure(args) -> int:
             print(f"[bench] {args.profile_phases} profiled iterations (MAX over {world} ranks):\n"
                   + ds.phase_table(ph), file=sys.stderr, flush=True)
 
-    watch.phase("report", 120)
+    watch.phase("report")
     if info.rank == 0:
         out = {
             "metric": METRIC,
@@ -582,7 +719,8 @@ def measure(args) -> int:
                 "kernel": args.kernel,
                 "tile": tile_desc,
                 "graph_batch": args.graph_batch,
-                "overlap": args.overlap,
+                "overlap": "on" if overlap else "off",
+                "rccl_communicators": (2 if overlap else 1) if comm_used == "rccl" else None,
                 "exact": args.exact,
             },
             "timed_path": timed_path,
@@ -596,16 +734,15 @@ def measure(args) -> int:
             **phases,
         }
         line = json.dumps(out)
-        result = os.environ.get("PMX_BENCH_RESULT")
-        if supervised and result:
-            with open(result, "w") as f:
+        if supervised and result_path:
+            with open(result_path, "w") as f:
                 f.write(line + "\n")
         else:
             print(line, flush=True)
             if args.json_out:
                 with open(args.json_out, "w") as f:
                     f.write(line + "\n")
-    watch.phase("shutdown", 120)
+    watch.phase("shutdown")
     launch.shutdown()
     return 0
 

@@ -13,7 +13,7 @@
 //       [--dump sol.txt] [--dump-stride s] [--json] [--banner stage0..stage4]
 //       [--profile-phases N] [--check] [--overlap on|off] [--poison-halos]
 //       [--checkpoint FILE [--checkpoint-every K]] [--resume FILE]
-//       [--sweep-grids 10x10,20x20,40x40] [--sweep-threads 2,4,8,16] [--plan]
+//       [--sweep-grids 10x10,20x20,40x40] [--sweep-threads 2,4,8,16] [--plan] [--placement K]
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
@@ -61,7 +61,7 @@ struct Cli {
                "           [--dump FILE] [--dump-stride S] [--json] [--banner stage0..stage4]\n"
                "           [--profile-phases N] [--check] [--overlap on|off] [--poison-halos]\n"
                "           [--checkpoint FILE [--checkpoint-every K]] [--resume FILE]\n"
-               "           [--sweep-grids MxN,MxN,...] [--sweep-threads T,T,...] [--plan]\n";
+               "           [--sweep-grids MxN,MxN,...] [--sweep-threads T,T,...] [--plan] [--placement K]\n";
   std::exit(msg ? 2 : 0);
 }
 
@@ -139,6 +139,7 @@ Cli parse(int argc, char** argv) {
     else if (a == "--check") c.opt.check = true;
     else if (a == "--poison-halos") c.opt.poison_halos = true;
     else if (a == "--plan") c.plan = true;
+    else if (a == "--placement") c.opt.placement = std::atoi(val().c_str());  // probe K field blocks
     else if (a == "--sweep-grids") {
       std::string v = val() + ",";
       for (size_t p = 0, q; (q = v.find(',', p)) != std::string::npos; p = q + 1) {

@@ -180,8 +180,12 @@ class OpContext {
 GpuOptions make_options(int device, const std::string& kernel, int block, int vec, int waves,
                         int tile_rows, const std::string& dtype, bool exact, int graph_batch, bool check,
                         bool overlap = true, int vec_b = 0, int waves_b = 0, int tile_rows_b = -1,
-                        bool poison_halos = false, bool b_ring = false, int algo = -1) {
+                        bool poison_halos = false, bool b_ring = false, int algo = -1, int placement = 0,
+                        double placement_budget_s = 0.5, double placement_keep_free = 0.5) {
   GpuOptions o;
+  o.placement = placement;
+  o.placement_budget_s = placement_budget_s;
+  o.placement_keep_free = placement_keep_free;
   o.algo = algo;
   o.device = device;
   PMX_CHECK(kernel == "lds" || kernel == "wave", "kernel must be lds or wave, got " << kernel);
@@ -290,6 +294,31 @@ PYBIND11_MODULE(_pmx, m) {
     if (fp32) launch_wave_sums<float>(reinterpret_cast<const float*>(x), reinterpret_cast<float*>(out), nwaves, as_stream(stream));
     else launch_wave_sums<double>(reinterpret_cast<const double*>(x), reinterpret_cast<double*>(out), nwaves, as_stream(stream));
   }, py::arg("x"), py::arg("out"), py::arg("nwaves"), py::arg("fp32") = false, py::arg("stream") = 0);
+  // Reduction hand-off stress (tests): `nsets` back-to-back launches of the multi-block ticketed
+  // reduction on ONE workspace (as a solver does), set j reducing parts[j] (n x nq interleaved
+  // doubles) into out[j * nq ..]; nq = 5: k_reduce_n (pcg1), nq = 1 or 2: k_reduce (pcg2).
+  m.def("reduce_stress", [](uintptr_t parts, int n, int nq, int nsets, uintptr_t out, uintptr_t stream) {
+    PMX_CHECK(nq == 1 || nq == 2 || nq == 5, "nq must be 1, 2 or 5");
+    hipStream_t s = as_stream(stream);
+    double* ws = nullptr;
+    PcgState* st = nullptr;
+    HIP_CHECK(hipMalloc(&ws, kReduceWsDoubles * sizeof(double)));
+    HIP_CHECK(hipMalloc(&st, sizeof(PcgState)));
+    HIP_CHECK(hipMemsetAsync(ws, 0, kReduceWsDoubles * sizeof(double), s));
+    HIP_CHECK(hipMemsetAsync(st, 0, sizeof(PcgState), s));
+    const double ones[5] = {1.0, 1.0, 1.0, 1.0, 1.0};
+    const double* P = reinterpret_cast<const double*>(parts);
+    double* O = reinterpret_cast<double*>(out);
+    for (int j = 0; j < nsets; ++j) {
+      if (nq == 5)
+        launch_reduce_n(P + size_t(j) * n * nq, n, nq, ones, O + size_t(j) * nq, st, 0, ws, s);
+      else
+        launch_reduce(P + size_t(j) * n * nq, n, nq, 1.0, 1.0, O + size_t(j) * nq, st, 0, ws, s);
+    }
+    HIP_CHECK(hipStreamSynchronize(s));
+    HIP_CHECK(hipFree(ws));
+    HIP_CHECK(hipFree(st));
+  }, py::arg("parts"), py::arg("n"), py::arg("nq"), py::arg("nsets"), py::arg("out"), py::arg("stream") = 0);
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   // Arena layout for a Python-orchestrated solver (DistGpuPCG comm="torch").  The iteration
   // algorithm is resolved exactly as the solver will (options + environment + device size), so
@@ -314,8 +343,8 @@ PYBIND11_MODULE(_pmx, m) {
         py::arg("kernel") = "wave", py::arg("exact") = false, py::arg("device") = 0, py::arg("algo") = -1,
         py::arg("sharing") = 1);
   m.def("record_comm_sequence", [](const ProblemSpec& s, int world, Split split, int graph_batch, int64_t iters,
-                                   const std::string& dtype, int device) {
-          GpuOptions o = make_options(device, "wave", 256, 0, 4, 0, dtype, false, graph_batch, false);
+                                   const std::string& dtype, int device, bool overlap) {
+          GpuOptions o = make_options(device, "wave", 256, 0, 4, 0, dtype, false, graph_batch, false, overlap);
           std::vector<std::vector<CommEvent>> logs;
           {
             py::gil_scoped_release nogil;
@@ -325,13 +354,14 @@ PYBIND11_MODULE(_pmx, m) {
           py::list out;
           for (auto& l : logs) {
             py::list r;
-            for (auto& e : l) r.append(py::make_tuple(e.comm, e.op, e.count, e.peer));
+            for (auto& e : l) r.append(py::make_tuple(e.comm, e.op, e.count, e.peer, e.stream));
             out.append(r);
           }
           return out;
         }, py::arg("spec"), py::arg("world"), py::arg("split") = Split::kAuto, py::arg("graph_batch") = 4,
-        py::arg("iters") = 8, py::arg("dtype") = "fp64", py::arg("device") = 0,
-        "every rank's communication calls on a recording comm (init + iters iterations, captured when graph_batch > 0)");
+        py::arg("iters") = 8, py::arg("dtype") = "fp64", py::arg("device") = 0, py::arg("overlap") = true,
+        "every rank's communication calls on a recording comm (init + iters iterations, captured when "
+        "graph_batch > 0): (comm, op, count, peer, stream) tuples");
   m.def("max_square_grid", [](double bytes_per_gpu, int gpus, const std::string& dtype, double reserve) {
     return max_square_grid(bytes_per_gpu, gpus, dtype == "fp64" ? DType::kFp64 : DType::kFp32, reserve);
   }, py::arg("bytes_per_gpu"), py::arg("gpus"), py::arg("dtype") = "fp64", py::arg("reserve") = 0.1);
@@ -401,12 +431,14 @@ PYBIND11_MODULE(_pmx, m) {
                        int tile_rows, const std::string& dtype, bool exact, int graph_batch,
                        bool check, py::object uid, std::vector<int> ranks, std::vector<int> devices,
                        bool rccl_graph, bool overlap, int vec_b, int waves_b, int tile_rows_b,
-                       bool poison_halos, bool b_ring, int algo, bool defer_connect, int threaded) {
+                       bool poison_halos, bool b_ring, int algo, bool defer_connect, int threaded,
+                       int placement, double placement_budget_s, double placement_keep_free, int sharing) {
              SessionConfig c;
+             c.sharing = sharing;
              c.spec = s;
              c.opt = make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact,
                                   graph_batch, check, overlap, vec_b, waves_b, tile_rows_b, poison_halos,
-                                  b_ring, algo);
+                                  b_ring, algo, placement, placement_budget_s, placement_keep_free);
              c.defer_connect = defer_connect;
              c.threaded = threaded;
              c.split = split;
@@ -432,7 +464,8 @@ PYBIND11_MODULE(_pmx, m) {
            py::arg("rccl_graph") = false, py::arg("overlap") = true, py::arg("vec_b") = 0,
            py::arg("waves_b") = 0, py::arg("tile_rows_b") = -1, py::arg("poison_halos") = false,
            py::arg("b_ring") = false, py::arg("algo") = -1, py::arg("defer_connect") = false,
-           py::arg("threaded") = -1)
+           py::arg("threaded") = -1, py::arg("placement") = 0, py::arg("placement_budget_s") = 0.5,
+           py::arg("placement_keep_free") = 0.5, py::arg("sharing") = 0)
       .def("ipc_export", [](Session& s) { return py::bytes(s.ipc_export()); },
            "IPC session: this rank's memory handles (pass every rank's to connect_ipc)")
       .def("connect_ipc", [](Session& s, std::vector<py::bytes> ex) {
@@ -551,6 +584,7 @@ PYBIND11_MODULE(_pmx, m) {
           q["first_ms"] = v[0];
           std::sort(v.begin(), v.end());
           q["median_ms"] = v[v.size() / 2];
+          q["seconds"] = s.solver(0).placement_seconds();
           d["placement"] = q;
         }
         return d;

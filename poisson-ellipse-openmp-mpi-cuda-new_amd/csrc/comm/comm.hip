@@ -19,6 +19,7 @@
 
 #include <atomic>
 #include <cstring>
+#include <memory>
 #include <sstream>
 
 #include "pmx/common.hpp"
@@ -93,42 +94,64 @@ class LocalComm final : public Comm {
   double** ptrs_ = nullptr;
 };
 
+// Shared by an RcclComm and its rank views: set once ncclCommAbort has released the communicators.
+// Every entry point checks it first, so a driver thread that returns from a blocked call after
+// another thread's abort gets an error instead of touching freed handles.
+using AbortFlag = std::shared_ptr<std::atomic<bool>>;
+
+void require_live(const AbortFlag& f) {
+  PMX_CHECK(!f->load(), "RCCL communicator was aborted after a failure on another driver thread; this "
+                        "session cannot communicate any more");
+}
+
+void check_async(ncclComm_t c) {
+  ncclResult_t async = ncclSuccess;
+  RCCL_CHECK(ncclCommGetAsyncError(c, &async));
+  if (async != ncclSuccess && async != ncclInProgress)
+    ::pmx::fail(__FILE__, __LINE__, std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
+}
+
+// The halo send/recv pairs of one rank (active slots, RcclComm::halo's order).
+void rccl_halo_calls(GpuSubdomainSolver* s, ncclComm_t comm, hipStream_t stream) {
+  const CommLayout& L = s->layout();
+  const ncclDataType_t t = L.elem == 8 ? ncclFloat64 : ncclFloat32;
+  for (int slot = 0; slot < kHaloSlots; ++slot) {
+    if (!L.active(slot)) continue;
+    RCCL_CHECK(ncclSend(s->send_dev(slot), L.edge_len[slot], t, L.peer[slot], comm, stream));
+    RCCL_CHECK(ncclRecv(s->recv_dev(slot), L.edge_len[slot], t, L.peer[slot], comm, stream));
+  }
+}
+
 // One local rank of an RcclComm, driven by its own host thread: its collectives need no
 // ncclGroupStart/End across local ranks (RCCL matches them per communicator, whichever thread
 // issues them); the send/recv pairs of its halo slots still form one group.
 class RcclRankView final : public Comm {
  public:
-  RcclRankView(ncclComm_t comm, ncclComm_t halo_comm, int nranks, bool capturable, Comm* owner)
-      : comm_(comm), halo_comm_(halo_comm), nranks_(nranks), capturable_(capturable), owner_(owner) {}
+  RcclRankView(ncclComm_t comm, ncclComm_t halo_comm, int nranks, bool capturable, Comm* owner, AbortFlag aborted)
+      : comm_(comm), halo_comm_(halo_comm), nranks_(nranks), capturable_(capturable), owner_(owner),
+        aborted_(std::move(aborted)) {}
   void abort() override { owner_->abort(); }  // every rank view of the process shares the fate
   bool prefers_split() const override { return true; }
   void allreduce(std::vector<GpuSubdomainSolver*>& local, int which,
                  std::vector<hipStream_t>& streams) override {
+    require_live(aborted_);
     PMX_CHECK(local.size() == 1, "a rank view drives one subdomain");
     double* buf = local[0]->reduce_buf(which);
     RCCL_CHECK(ncclAllReduce(buf, buf, GpuSubdomainSolver::reduce_len(which), ncclFloat64, ncclSum, comm_,
                              streams[0]));
   }
   void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>& streams) override {
+    require_live(aborted_);
     PMX_CHECK(local.size() == 1, "a rank view drives one subdomain");
-    const CommLayout& L = local[0]->layout();
-    const ncclDataType_t t = L.elem == 8 ? ncclFloat64 : ncclFloat32;
     RCCL_CHECK(ncclGroupStart());
-    for (int slot = 0; slot < kHaloSlots; ++slot) {
-      if (!L.active(slot)) continue;
-      RCCL_CHECK(ncclSend(local[0]->send_dev(slot), L.edge_len[slot], t, L.peer[slot], halo_comm_, streams[0]));
-      RCCL_CHECK(ncclRecv(local[0]->recv_dev(slot), L.edge_len[slot], t, L.peer[slot], halo_comm_, streams[0]));
-    }
+    rccl_halo_calls(local[0], halo_comm_, streams[0]);
     RCCL_CHECK(ncclGroupEnd());
   }
   bool graph_capturable() const override { return capturable_; }
   void check_health() override {
-    for (auto c : {comm_, halo_comm_}) {
-      ncclResult_t async = ncclSuccess;
-      RCCL_CHECK(ncclCommGetAsyncError(c, &async));
-      if (async != ncclSuccess && async != ncclInProgress)
-        ::pmx::fail(__FILE__, __LINE__, std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
-    }
+    require_live(aborted_);
+    check_async(comm_);
+    if (halo_comm_ != comm_) check_async(halo_comm_);
   }
   std::string name() const override { return "rccl"; }
   int world_size() const override { return nranks_; }
@@ -138,13 +161,14 @@ class RcclRankView final : public Comm {
   int nranks_;
   bool capturable_;
   Comm* owner_;
+  AbortFlag aborted_;
 };
 
 class RcclComm final : public Comm {
  public:
   RcclComm(const std::string& uid, int nranks, const std::vector<int>& ranks,
-           const std::vector<int>& devices, bool capturable)
-      : nranks_(nranks), capturable_(capturable) {
+           const std::vector<int>& devices, bool capturable, bool split_halo)
+      : nranks_(nranks), capturable_(capturable), split_(split_halo) {
     PMX_CHECK(uid.size() == sizeof(ncclUniqueId), "bad ncclUniqueId size " << uid.size());
     PMX_CHECK(ranks.size() == devices.size() && !ranks.empty(), "ranks/devices mismatch");
     ncclUniqueId id;
@@ -161,6 +185,10 @@ class RcclComm final : public Comm {
       }
       RCCL_CHECK(ncclGroupEnd());
     }
+    if (!split_halo) {  // serialized schedule: one communicator for everything
+      halo_comms_ = comms_;
+      return;
+    }
     // A second communicator (same ranks) carries the halos, so the ghost exchange on the comm
     // stream and the all-reduce on the compute stream never queue behind each other.
     halo_comms_.resize(comms_.size());
@@ -172,19 +200,20 @@ class RcclComm final : public Comm {
     RCCL_CHECK(ncclGroupEnd());
   }
   ~RcclComm() override {
-    if (aborted_.load()) return;  // ncclCommAbort already released them
-    for (auto c : halo_comms_) (void)ncclCommDestroy(c);
+    if (aborted_->load()) return;  // ncclCommAbort already released them
+    if (split_) for (auto c : halo_comms_) (void)ncclCommDestroy(c);
     for (auto c : comms_) (void)ncclCommDestroy(c);
   }
   void abort() override {
-    if (aborted_.exchange(true)) return;
-    for (auto c : halo_comms_) (void)ncclCommAbort(c);
+    if (aborted_->exchange(true)) return;
+    if (split_) for (auto c : halo_comms_) (void)ncclCommAbort(c);
     for (auto c : comms_) (void)ncclCommAbort(c);
   }
   bool prefers_split() const override { return true; }
 
   void allreduce(std::vector<GpuSubdomainSolver*>& local, int which,
                  std::vector<hipStream_t>& streams) override {
+    require_live(aborted_);
     RCCL_CHECK(ncclGroupStart());
     for (size_t i = 0; i < local.size(); ++i) {
       double* buf = local[i]->reduce_buf(which);
@@ -195,34 +224,22 @@ class RcclComm final : public Comm {
   }
 
   void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>& streams) override {
+    require_live(aborted_);
     RCCL_CHECK(ncclGroupStart());
-    for (size_t i = 0; i < local.size(); ++i) {
-      GpuSubdomainSolver* s = local[i];
-      const CommLayout& L = s->layout();
-      const ncclDataType_t t = L.elem == 8 ? ncclFloat64 : ncclFloat32;
-      for (int slot = 0; slot < kHaloSlots; ++slot) {
-        if (!L.active(slot)) continue;
-        RCCL_CHECK(ncclSend(s->send_dev(slot), L.edge_len[slot], t, L.peer[slot], halo_comms_[i], streams[i]));
-        RCCL_CHECK(ncclRecv(s->recv_dev(slot), L.edge_len[slot], t, L.peer[slot], halo_comms_[i], streams[i]));
-      }
-    }
+    for (size_t i = 0; i < local.size(); ++i) rccl_halo_calls(local[i], halo_comms_[i], streams[i]);
     RCCL_CHECK(ncclGroupEnd());
   }
 
   bool graph_capturable() const override { return capturable_; }
   std::unique_ptr<Comm> rank_view(int i) override {
     PMX_CHECK(i >= 0 && i < int(comms_.size()), "rank view index");
-    return std::make_unique<RcclRankView>(comms_[size_t(i)], halo_comms_[size_t(i)], nranks_, capturable_, this);
+    return std::make_unique<RcclRankView>(comms_[size_t(i)], halo_comms_[size_t(i)], nranks_, capturable_, this,
+                                          aborted_);
   }
   void check_health() override {
-    for (auto* v : {&comms_, &halo_comms_})
-      for (auto c : *v) {
-        ncclResult_t async = ncclSuccess;
-        RCCL_CHECK(ncclCommGetAsyncError(c, &async));
-        if (async != ncclSuccess && async != ncclInProgress)
-          ::pmx::fail(__FILE__, __LINE__,
-                      std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
-      }
+    require_live(aborted_);
+    for (auto c : comms_) check_async(c);
+    if (split_) for (auto c : halo_comms_) check_async(c);
   }
   std::string name() const override { return "rccl"; }
   int world_size() const override { return nranks_; }
@@ -230,45 +247,52 @@ class RcclComm final : public Comm {
  private:
   int nranks_;
   bool capturable_;
+  bool split_;                          // halo_comms_ are their own communicators
   std::vector<ncclComm_t> comms_;       // scalar all-reduces (compute stream)
-  std::vector<ncclComm_t> halo_comms_;  // ghost exchange (comm stream when overlapped)
-  std::atomic<bool> aborted_{false};
+  std::vector<ncclComm_t> halo_comms_;  // ghost exchange (comm stream when overlapped); == comms_ unsplit
+  AbortFlag aborted_ = std::make_shared<std::atomic<bool>>(false);
 };
 
 // See make_recording_comm.
 class RecordingComm final : public Comm {
  public:
-  RecordingComm(std::vector<CommEvent>* log, int world) : log_(log), world_(world) {}
-  void allreduce(std::vector<GpuSubdomainSolver*>& local, int which, std::vector<hipStream_t>&) override {
+  RecordingComm(std::vector<CommEvent>* log, int world, bool split_halo)
+      : log_(log), world_(world), halo_id_(split_halo ? 1 : 0) {}
+  void allreduce(std::vector<GpuSubdomainSolver*>& local, int which, std::vector<hipStream_t>& streams) override {
     PMX_CHECK(local.size() == 1, "a recording comm stands for one rank");
-    log_->push_back({0, "allreduce", GpuSubdomainSolver::reduce_len(which), -1});
+    log_->push_back({0, "allreduce", GpuSubdomainSolver::reduce_len(which), -1, sid(streams)});
   }
-  void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>&) override {
+  void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>& streams) override {
     PMX_CHECK(local.size() == 1, "a recording comm stands for one rank");
     const CommLayout& L = local[0]->layout();
-    log_->push_back({1, "group_start", 0, -1});
+    const long long st = sid(streams);
+    log_->push_back({halo_id_, "group_start", 0, -1, st});
     for (int slot = 0; slot < kHaloSlots; ++slot) {  // the order RcclComm::halo issues them
       if (!L.active(slot)) continue;
-      log_->push_back({1, "send", L.edge_len[slot], L.peer[slot]});
-      log_->push_back({1, "recv", L.edge_len[slot], L.peer[slot]});
+      log_->push_back({halo_id_, "send", L.edge_len[slot], L.peer[slot], st});
+      log_->push_back({halo_id_, "recv", L.edge_len[slot], L.peer[slot], st});
     }
-    log_->push_back({1, "group_end", 0, -1});
+    log_->push_back({halo_id_, "group_end", 0, -1, st});
   }
   bool prefers_split() const override { return true; }
   std::string name() const override { return "recording"; }
   int world_size() const override { return world_; }
 
  private:
+  static long long sid(const std::vector<hipStream_t>& s) {
+    return static_cast<long long>(reinterpret_cast<uintptr_t>(s.at(0)));
+  }
   std::vector<CommEvent>* log_;
   int world_;
+  int halo_id_;
 };
 
 }  // namespace
 
 std::unique_ptr<Comm> make_self_comm() { return std::make_unique<SelfComm>(); }
 
-std::unique_ptr<Comm> make_recording_comm(std::vector<CommEvent>* log, int world) {
-  return std::make_unique<RecordingComm>(log, world);
+std::unique_ptr<Comm> make_recording_comm(std::vector<CommEvent>* log, int world, bool split_halo) {
+  return std::make_unique<RecordingComm>(log, world, split_halo);
 }
 
 std::unique_ptr<Comm> make_local_comm(std::vector<GpuSubdomainSolver*>& local) {
@@ -277,8 +301,8 @@ std::unique_ptr<Comm> make_local_comm(std::vector<GpuSubdomainSolver*>& local) {
 
 std::unique_ptr<Comm> make_rccl_comm(const std::string& unique_id, int nranks,
                                      const std::vector<int>& ranks, const std::vector<int>& devices,
-                                     bool capturable) {
-  return std::make_unique<RcclComm>(unique_id, nranks, ranks, devices, capturable);
+                                     bool capturable, bool split_halo) {
+  return std::make_unique<RcclComm>(unique_id, nranks, ranks, devices, capturable, split_halo);
 }
 
 std::string rccl_unique_id() {

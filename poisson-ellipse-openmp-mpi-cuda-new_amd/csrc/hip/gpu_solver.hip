@@ -103,6 +103,7 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_PCG1_WCYCLE", o.wcycle1);
   env_int("PMX_PROGRESS", o.progress);
   env_int("PMX_ARITH32", o.arith32);
+  env_int("PMX_PLACEMENT", o.placement);
   PMX_CHECK(o.wcycle1 == 2 || o.wcycle1 == 3, "pcg1 w cycle must be 2 or 3");
   PMX_CHECK(o.pair_w >= 0 && o.pair_w <= 2, "pair_w must be 0, 1 or 2");
   PMX_CHECK(o.algo == -1 || o.algo == 1 || o.algo == 2, "algo must be -1, 1 or 2");
@@ -174,8 +175,6 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
 
 // Bytes between consecutive fields of the one field allocation (see construct).
 constexpr long long kFieldStagger = 0;
-// Field blocks the placement probe may compare (see place_fields); 1 = off.
-constexpr int kPlacementCandidates = 160;
 
 void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   const GpuOptions& opt = opt_;
@@ -324,16 +323,15 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
 // on WHERE its fields were allocated: a property of the allocation, stable for its lifetime and
 // across passes (8 sessions alive in one process, timed forward then in reverse).  At 16384^2 fp64,
 // 3 plain sweeps of a candidate block take ~5.45, ~4.97 or ~4.55-4.63 ms, and the iteration runs
-// at ~2150 / ~1995 / ~1810 us; in a fresh process the first blocks are slow, mostly mid-rate ones
-// follow and the fast ones appeared only ~15 blocks (~170 GB) in -- profiles/r3/placement/.  So the
-// solver allocates candidate blocks while 1/8 of the device memory that was free stays free (at
-// most K; blocks under 256 MB are not probed), times 3 plain sweeps on each with the five fields in rotating roles (probe_sweeps:
-// every field read and written; zeroed fields, the init sweep's k = 0 arithmetic; init() resets
-// everything afterwards), keeps the fastest and frees the others.  Construction time only (~10 ms
-// per 10 GB candidate); nothing in the iteration changes.  PMX_PLACEMENT=K overrides
-// kPlacementCandidates (1 = off: bench.py --share-gpu ranks and the multi-process GPU tests, whose
-// processes share one device).  Skipped with an external (IPC-shared) arena or a separately
-// allocated r2.
+// at ~2150 / ~1995 / ~1810 us -- profiles/r3/placement/, profiles/r4/placement/.  So the solver may
+// allocate candidate blocks and keep the fastest: at most opt.placement of them (GpuOptions), while
+// opt.placement_keep_free of the memory that was free stays free and for at most
+// opt.placement_budget_s seconds; blocks under 256 MB are not probed (latency-bound grids).  Each
+// candidate: 3 plain sweeps with the five fields in rotating roles (probe_sweeps: every field read
+// and written; zeroed fields, the init sweep's k = 0 arithmetic; init() resets everything
+// afterwards).  Construction time only; nothing in the iteration changes.  Off by default (the
+// library) and for ranks that share a device; skipped with an external (IPC-shared) arena or a
+// separately allocated r2.
 // Plain sweeps (k = 0 arithmetic) with the five field blocks in rotating roles, so that every field
 // of the candidate block is read and written: role set q reads r = F[q], p = F[q+3] and writes
 // r2 = F[q+4], p0 = F[q+2] (indices mod 5; F = w, r, p0, p1, r2).
@@ -346,17 +344,19 @@ void GpuSubdomainSolver::probe_sweeps(hipStream_t s, int first, int count) {
 }
 
 void GpuSubdomainSolver::place_fields() {
-  int K = kPlacementCandidates;
-  if (const char* e = std::getenv("PMX_PLACEMENT"); e && e[0]) K = std::atoi(e);
+  const int K = opt_.placement;
   const size_t block = 5 * field_stride_;
   if (K <= 1 || !own_arena_ || own_r2_ || block < (size_t(256) << 20)) return;  // small grids: latency-bound
+  const double t0 = now_s();
   std::vector<char*> cand{fields_};
   size_t free0 = 0, total_b = 0;
   HIP_CHECK(hipMemGetInfo(&free0, &total_b));
+  const size_t keep = std::max(size_t(double(free0) * std::clamp(opt_.placement_keep_free, 0.0, 1.0)),
+                               size_t(4) << 30);
   while (int(cand.size()) < K) {
     size_t free_b = 0;
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-    if (free_b < block + std::max(free0 / 8, size_t(4) << 30)) break;
+    if (free_b < block + keep) break;
     char* p = nullptr;
     if (hipMalloc(&p, block) != hipSuccess) {
       (void)hipGetLastError();
@@ -364,7 +364,10 @@ void GpuSubdomainSolver::place_fields() {
     }
     cand.push_back(p);
   }
-  if (cand.size() == 1) return;
+  if (cand.size() == 1) {
+    placement_s_ = now_s() - t0;
+    return;
+  }
   auto keep_only = [&](size_t keep) {  // free every other candidate, point the fields at `keep`
     for (size_t c = 0; c < cand.size(); ++c)
       if (c != keep) (void)hipFree(cand[c]);
@@ -377,8 +380,10 @@ void GpuSubdomainSolver::place_fields() {
     HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreate(&e0));
     HIP_CHECK(hipEventCreate(&e1));
-    placement_ms_.assign(cand.size(), 0.f);
+    placement_ms_.clear();
     for (size_t c = 0; c < cand.size(); ++c) {
+      if (c > 0 && now_s() - t0 > opt_.placement_budget_s) break;  // time budget: the rest stay untimed
+      placement_ms_.push_back(0.f);
       fields_ = cand[c];
       r2_ = field_raw(4);
       HIP_CHECK(hipMemsetAsync(fields_, 0, block, s));
@@ -399,6 +404,7 @@ void GpuSubdomainSolver::place_fields() {
   HIP_CHECK(hipEventDestroy(e0));
   HIP_CHECK(hipEventDestroy(e1));
   HIP_CHECK(hipStreamDestroy(s));
+  placement_s_ = now_s() - t0;
 }
 
 void GpuSubdomainSolver::progress(long long out[3]) const {
@@ -1223,8 +1229,18 @@ hipGraphExec_t PcgDriver::build_graph(int phase, int len) {
   for (auto* s : local_) k0.push_back(s->host_k());
   PMX_CHECK(!halo_pending_, "graph capture with an unjoined ghost exchange");
   PMX_GDBG("capture begun");
-  for (int k = 0; k < len; ++k) enqueue_one_iteration();
-  join_halo();  // a captured batch is self-contained: every forked stream rejoins
+  try {
+    for (int k = 0; k < len; ++k) enqueue_one_iteration();
+    join_halo();  // a captured batch is self-contained: every forked stream rejoins
+  } catch (...) {  // e.g. an aborted communicator: end the capture so the stream stays usable
+    halo_pending_ = false;
+    for (size_t i = 0; i < local_.size(); ++i) local_[i]->set_host_k(k0[i]);
+    hipGraph_t dead = nullptr;
+    (void)hipStreamEndCapture(streams_[0], &dead);
+    if (dead) (void)hipGraphDestroy(dead);
+    (void)hipGetLastError();
+    throw;
+  }
   for (size_t i = 0; i < local_.size(); ++i) local_[i]->set_host_k(k0[i]);
   PMX_GDBG("enqueued; ending capture");
   if (hipStreamEndCapture(streams_[0], &g) != hipSuccess || !g) {

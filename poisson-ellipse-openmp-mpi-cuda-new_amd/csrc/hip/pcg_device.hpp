@@ -49,6 +49,14 @@ __device__ __forceinline__ T ld_uniform(const T* p, int i) {
 // (vmcnt 0) before its relaxed ticket add, and the last arriver reads every chunk with agent-scope
 // atomic loads (sc1, past its CU's L1).  No __threadfence(): that is an L2 writeback plus an L2
 // invalidate (~3.5 us each side) in a kernel of a few microseconds.
+// Memory-model status: relaxed atomics give no happens-before edge in the HIP/C++ model; this is
+// the hardware-level form MI355X_MICROARCH.md lists as measured valid on gfx950 / ROCm 7.2 ('Valid
+// forms', first row of its hand-off table: one lane per storing workgroup, sc1 stores, vmcnt(0)
+// before one agent-scope add to an unsharded counter, the last adder loads sc1 after its add
+// returned, the other lanes after a workgroup barrier; <= 1 workgroup per CU -- the reductions run
+// <= 64 blocks).  Not an architectural guarantee: tests/test_gpu_ops.py::
+// test_reduction_handoff_stress checks every result of 200 back-to-back launches on one workspace
+// under uneven load against the exactly rounded host sum.
 typedef __attribute__((address_space(1))) double gdouble;
 typedef __attribute__((address_space(1))) unsigned gunsigned;
 __device__ __forceinline__ void st_publish(double* p, double v) {

@@ -45,6 +45,7 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
     int per_device = 0;  // subdomains sharing the busiest device
     for (int d : cfg_.devices) per_device = std::max<int>(per_device, int(std::count(cfg_.devices.begin(), cfg_.devices.end(), d)));
+    per_device = std::max(per_device, cfg_.sharing);
     base.algo = choose_single_pass(cfg_.spec, pg_, base, double(total_b), per_device) ? 1 : 2;
   }
   for (size_t i = 0; i < cfg_.ranks.size(); ++i) {
@@ -75,7 +76,8 @@ void Session::connect() {
     case CommKind::kSelf: comm_ = make_self_comm(); break;
     case CommKind::kLocal: comm_ = make_local_comm(raw); break;
     case CommKind::kRccl:
-      comm_ = make_rccl_comm(cfg_.rccl_uid, cfg_.world, cfg_.ranks, cfg_.devices, cfg_.rccl_graph);
+      // overlap off = the serialized schedule: one communicator, every call on the compute stream
+      comm_ = make_rccl_comm(cfg_.rccl_uid, cfg_.world, cfg_.ranks, cfg_.devices, cfg_.rccl_graph, cfg_.opt.overlap);
       break;
   }
   // one host thread per GPU.  Several owned ranks on distinct devices (pmx --gpus G)
@@ -321,7 +323,7 @@ std::vector<std::vector<CommEvent>> record_comm_sequence(const ProblemSpec& spec
   std::vector<std::unique_ptr<PcgDriver>> drivers;
   for (int r = 0; r < world; ++r) {
     solvers.push_back(std::make_unique<GpuSubdomainSolver>(spec, decompose_2d(spec.M, spec.N, pg, r), o));
-    comms.push_back(make_recording_comm(&logs[size_t(r)], world));
+    comms.push_back(make_recording_comm(&logs[size_t(r)], world, o.overlap));
     drivers.push_back(std::make_unique<PcgDriver>(std::vector<GpuSubdomainSolver*>{solvers.back().get()},
                                                   comms.back().get(), o.graph_batch));
   }

@@ -103,6 +103,14 @@ struct GpuOptions {
   // is in.  One 8-B system-scope store per kernel; on for multi-rank RCCL sessions.  PMX_PROGRESS
   // overrides.
   int progress = 0;
+  // Field placement probe (GpuSubdomainSolver::place_fields): up to `placement` candidate field
+  // blocks are allocated and timed and the fastest is kept; 0 or 1 = off (the library default: a
+  // probe briefly takes device memory a co-resident process might need).  Bounded by
+  // placement_budget_s of probing and by keeping placement_keep_free of the free memory free.
+  // bench.py turns it on unless ranks share the device.  PMX_PLACEMENT=K overrides.
+  int placement = 0;
+  double placement_budget_s = 0.5;
+  double placement_keep_free = 0.5;
   bool resolved = false;  // environment overrides already applied (resolve_options)
 };
 
@@ -231,6 +239,7 @@ class GpuSubdomainSolver {
   int device() const { return opt_.device; }
   size_t field_bytes() const { return field_bytes_; }
   const std::vector<float>& placement_ms() const { return placement_ms_; }
+  double placement_seconds() const { return placement_s_; }  // wall time of the probe (0: off)
   void* field_base(int which) const;  // pointer to local (0,0)
   size_t device_bytes() const;        // total device memory owned
 
@@ -274,6 +283,7 @@ class GpuSubdomainSolver {
   template <typename T>
   void probe_sweeps(hipStream_t s, int first, int count);
   std::vector<float> placement_ms_;   // probe: ms per candidate block (the kept one is the min)
+  double placement_s_ = 0.0;
   double* tables_buf_ = nullptr;
   double* partials_ = nullptr;
   size_t npart_ = 0;
@@ -327,10 +337,15 @@ class Comm {
 std::unique_ptr<Comm> make_self_comm();
 std::unique_ptr<Comm> make_local_comm(std::vector<GpuSubdomainSolver*>& local);
 // RCCL: one communicator per local solver.  `unique_id` is the 128-byte ncclUniqueId,
-// `ranks` the global ranks of the local solvers, `nranks` the world size.
+// `ranks` the global ranks of the local solvers, `nranks` the world size.  `split_halo`: a second
+// communicator (ncclCommSplit) carries the ghost exchange, so the exchange on the comm stream and the
+// all-reduce on the compute stream never queue behind each other (overlapped schedules).  Without it
+// every call goes through ONE communicator -- the serialized schedule (overlap off), where halo and
+// all-reduce are issued on one stream in a fixed order and no two RCCL kernels are ever in flight
+// together (bench.py rung 2).
 std::unique_ptr<Comm> make_rccl_comm(const std::string& unique_id, int nranks,
                                      const std::vector<int>& ranks, const std::vector<int>& devices,
-                                     bool capturable);
+                                     bool capturable, bool split_halo = true);
 std::string rccl_unique_id();
 
 // IPC transport (comm/ipc_comm.hip): one rank per process, peers' arenas mapped with
@@ -341,17 +356,20 @@ std::string ipc_export(Comm* ipc);
 void ipc_attach(Comm* ipc, const std::vector<std::string>& exports);
 
 // One communication call as a rank's driver issued it (RecordingComm, tests): comm 0 = the
-// scalar communicator, 1 = the halo communicator; op "allreduce" (count = doubles), or a halo
-// group ("group_start", "send"/"recv" with element count and peer rank, "group_end").
+// scalar communicator, 1 = the halo communicator (0 too without a split halo communicator); op
+// "allreduce" (count = doubles), or a halo group ("group_start", "send"/"recv" with element count
+// and peer rank, "group_end"); `stream` = the HIP stream the call was issued on.
 struct CommEvent {
   int comm;
   std::string op;
   int count;
   int peer;
+  long long stream;
 };
 // Records the calls instead of communicating (no data moves).  Mimics RCCL's driver defaults
-// (prefers_split), so a driver on it issues exactly the sequence it would issue on RCCL.
-std::unique_ptr<Comm> make_recording_comm(std::vector<CommEvent>* log, int world);
+// (prefers_split) and its communicator layout (`split_halo` as make_rccl_comm), so a driver on it
+// issues exactly the sequence it would issue on RCCL.
+std::unique_ptr<Comm> make_recording_comm(std::vector<CommEvent>* log, int world, bool split_halo = true);
 
 struct RunStats {
   int64_t iters = 0;

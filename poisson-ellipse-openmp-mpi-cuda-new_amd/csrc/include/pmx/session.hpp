@@ -32,6 +32,11 @@ struct SessionConfig {
   // several owned ranks on distinct devices, i.e. `pmx --gpus G`), 1 = always (RCCL only; with a
   // single rank it exercises the threaded path on one GPU), 0 = one host thread drives all ranks.
   int threaded = -1;
+  // Subdomains of the whole job that share the busiest device (0 = count this session's own
+  // `devices`).  A multi-process job whose ranks share one GPU (bench.py --share-gpu, IPC
+  // rehearsals) passes its world size, so every transport makes the same pcg1/pcg2 choice
+  // (choose_single_pass) as the torch path's comm_layout(sharing=...).
+  int sharing = 0;
 };
 
 class Session {

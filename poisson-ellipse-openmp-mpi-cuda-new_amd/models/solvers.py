@@ -80,7 +80,8 @@ def make_session(problem: PoissonEllipse, ranks: int = 1, split: str = "referenc
                  dtype: str = "fp64", kernel: str = "wave", block: int = 256, vec: int = 0, waves: int = 4,
                  tile_rows: int = 0, exact: bool = False, graph_batch: int = 32, check: bool = False,
                  overlap: bool = True, vec_b: int = 0, waves_b: int = 0, tile_rows_b: int = -1,
-                 poison_halos: bool = False, b_ring: bool = False):
+                 poison_halos: bool = False, b_ring: bool = False, placement: int = 0,
+                 placement_budget_s: float = 0.5, placement_keep_free: float = 0.5):
     """Native GPU session with `ranks` subdomains on one device (LocalComm when ranks > 1).
 
     overlap: ghost exchange on a second stream concurrent with pcg_b (only matters for ranks > 1).
@@ -88,13 +89,18 @@ def make_session(problem: PoissonEllipse, ranks: int = 1, split: str = "referenc
     kernel="wave": wave-tile kernels with DPP neighbour shifts (vec columns/lane, `waves` tiles per
     workgroup); kernel="lds": workgroup tiles with an LDS row ring (`block` columns).  vec=0 picks
     the measured best per kernel (pcg_a 4, pcg_b 2 in fp64); *_b override pcg_b's shape alone.
-    pcg_b runs the ring-free 2-row kernel by default; b_ring=True selects the pipelined one."""
+    pcg_b runs the ring-free 2-row kernel by default; b_ring=True selects the pipelined one.
+
+    placement: up to this many candidate field blocks are timed and the fastest kept (0 = off, the
+    default; bounded by placement_budget_s seconds and by leaving placement_keep_free of the free
+    device memory free -- see GpuSubdomainSolver::place_fields)."""
     n = _native()
     return n.Session(problem.to_native(), world=int(ranks), comm="self" if ranks == 1 else "local",
                      split=getattr(n.Split, split), device=device, kernel=kernel, block=block, vec=vec,
                      waves=waves, tile_rows=tile_rows, dtype=dtype, exact=exact, graph_batch=graph_batch,
                      check=check, overlap=overlap, vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b,
-                     poison_halos=poison_halos, b_ring=b_ring)
+                     poison_halos=poison_halos, b_ring=b_ring, placement=placement,
+                     placement_budget_s=placement_budget_s, placement_keep_free=placement_keep_free)
 
 
 def solve_hip(problem: PoissonEllipse, ranks: int = 1, keep_solution: bool = True, poll_batches: int = 1,

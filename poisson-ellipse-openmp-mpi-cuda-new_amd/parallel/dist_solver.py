@@ -96,7 +96,13 @@ class DistGpuPCG:
                  dtype: str = "fp64", kernel: str = "wave", block: int = 256, vec: int = 0, waves: int = 4,
                  tile_rows: int = 0, exact: bool = False, graph_batch: int = 32, rccl_graph: bool = True,
                  overlap: bool = True, vec_b: int = 0, waves_b: int = 0, tile_rows_b: int = -1,
-                 b_ring: bool = False, algo: int = -1, init_timeout: float = 300.0, device: int | None = None):
+                 b_ring: bool = False, algo: int = -1, init_timeout: float = 90.0, device: int | None = None,
+                 placement: int = 0, phase=None):
+        """placement: candidate field blocks of the placement probe (0 = off; forced off when ranks share
+        a device).  phase(name, seconds): progress-watchdog hook (bench.py's Watch.phase); called with
+        "comm-init" before the blocking communicator initialisation, whose own watchdog is
+        init_timeout.  overlap=False is the serialized schedule: one RCCL communicator, every call on
+        the compute stream in a fixed order."""
         self.problem = problem
         self.info = info
         self.comm_kind = comm
@@ -107,6 +113,13 @@ class DistGpuPCG:
         self.Px, self.Py = process_grid(info.world, problem.M, problem.N, split)
         self.graph_batch = graph_batch
         torch.cuda.set_device(self.device)
+        # ranks sharing this device (an explicit device, or more local ranks than GPUs): no placement
+        # probe (its candidate blocks would crowd the peers), and the pcg1/pcg2 choice counts them all
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", info.world))
+        self.shared = device is not None or local_world > torch.cuda.device_count()
+        sharing = info.world if self.shared else 1
+        placement = 0 if self.shared else placement
+        phase = phase or (lambda name, seconds: None)
         if comm == "native":
             uid = [self.n.rccl_unique_id() if info.rank == 0 else None]
             if info.world > 1:
@@ -119,11 +132,12 @@ class DistGpuPCG:
                     dtype=dtype, exact=exact, graph_batch=graph_batch if rccl_graph else 0, uid=uid[0],
                     ranks=[info.rank], devices=[self.device], rccl_graph=rccl_graph, overlap=overlap,
                     vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b, b_ring=b_ring, algo=algo,
-                    defer_connect=True)
+                    defer_connect=True, placement=placement, sharing=sharing)
             except Exception as e:  # sizing / allocation: reported collectively below
                 err = e
             agree(info, err is None, f"native solver setup ({err})" if err else "native solver setup",
                   self.device)
+            phase("comm-init", init_timeout + 15)
             with _Watchdog(init_timeout, "RCCL communicator initialisation"):
                 try:
                     self.session.connect()
@@ -144,7 +158,7 @@ class DistGpuPCG:
                     device=self.device, kernel=kernel, block=block, vec=vec, waves=waves, tile_rows=tile_rows,
                     dtype=dtype, exact=exact, graph_batch=graph_batch, ranks=[info.rank], devices=[self.device],
                     overlap=overlap, vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b, b_ring=b_ring,
-                    algo=algo, defer_connect=True)
+                    algo=algo, defer_connect=True, placement=placement, sharing=sharing)
                 mine = self.session.ipc_export()
             except Exception as e:
                 err, mine = e, b""
@@ -154,6 +168,7 @@ class DistGpuPCG:
                 dist.all_gather_object(exports, mine)
             else:
                 exports = [mine]
+            phase("comm-init", init_timeout + 15)
             with _Watchdog(init_timeout, "IPC transport setup"):
                 try:
                     self.session.connect_ipc(exports)
@@ -166,7 +181,6 @@ class DistGpuPCG:
         elif comm == "torch":
             # ranks sharing this device (share-gpu rehearsal: all of them) count against its memory
             # in the pcg1/pcg2 choice, which every rank makes identically from global data
-            sharing = info.world if device is not None else 1
             lay = self.n.comm_layout(self.spec, self.Px, self.Py, info.rank, dtype=dtype, kernel=kernel,
                                      exact=exact, device=self.device, algo=algo, sharing=sharing)
             self.single_pass = bool(lay["single_pass"])
@@ -199,6 +213,7 @@ class DistGpuPCG:
             self.sends = [self.arena_view[o:o + n * el].view(tdt) for o, n in zip(lay["send_off"], lay["edge_len"])]
             self.recvs = [self.arena_view[o:o + n * el].view(tdt) for o, n in zip(lay["recv_off"], lay["edge_len"])]
             self.peers = [p if n > 0 else -1 for p, n in zip(lay["peer"], lay["edge_len"])]
+            phase("comm-init", init_timeout + 15)
             self.tcomm = TorchComm() if info.world > 1 else None
         else:
             raise ValueError(f"unknown comm {comm!r}")

@@ -152,8 +152,8 @@ def test_split_sweep_needs_no_concurrent_queues(pkg, tmp_path, monkeypatch, spli
 
 
 def _check_sequences(logs, world):
-    # 1. the collective (scalar communicator) sequence is identical on every rank
-    coll = [[e for e in l if e[0] == 0] for l in logs]
+    # 1. the collective sequence is identical on every rank
+    coll = [[e[:4] for e in l if e[1] == "allreduce"] for l in logs]
     assert all(c == coll[0] for c in coll) and len(coll[0]) > 0
     # 2. the per-rank order of calls over both communicators is the same skeleton
     skel = [[(e[0], e[1]) for e in l if e[1] in ("allreduce", "group_start", "group_end")] for l in logs]
@@ -175,9 +175,9 @@ def _check_sequences(logs, world):
     assert ng > 0 and all(len(g) == ng for g in groups)
     for g in range(ng):
         for r in range(world):
-            for (_, op, cnt, peer) in groups[r][g]:
+            for (comm, op, cnt, peer, _) in groups[r][g]:
                 want = "recv" if op == "send" else "send"
-                assert (1, want, cnt, r) in groups[peer][g], (g, r, op, peer)
+                assert (comm, want, cnt, r) in [e[:4] for e in groups[peer][g]], (g, r, op, peer)
 
 
 @pytest.mark.parametrize("split,graph_batch", [("reference", 4), ("auto", 4), ("reference", 0)])
@@ -190,6 +190,27 @@ def test_every_rank_issues_the_same_comm_sequence(native, pkg, split, graph_batc
     n_ar = sum(1 for e in logs[0] if e[1] == "allreduce")
     assert n_ar == 1 + 8  # init + one 5-double all-reduce per iteration
     assert all(e[2] == 5 for e in logs[0] if e[1] == "allreduce")
+
+
+@pytest.mark.parametrize("split", ["reference", "auto"])
+def test_serialized_schedule_uses_one_stream_and_one_communicator(native, pkg, split):
+    """bench.py rung 2 (overlap off): every collective and every halo group of a rank goes through ONE
+    communicator on ONE stream, in a fixed order -- no two RCCL kernels are ever in flight together
+    (the reference's own ordering, stage4-mpi+cuda/poisson_mpi_cuda_f.cu:851-943).  The overlapped
+    schedule (rung 1) puts the halo groups on their own communicator and stream."""
+    spec = pkg.PoissonEllipse(M=256, N=384).to_native()
+    logs = native.record_comm_sequence(spec, 8, getattr(native.Split, split), 0, 8, overlap=False)
+    _check_sequences(logs, 8)
+    for l in logs:
+        assert len({e[4] for e in l}) == 1 and {e[0] for e in l} == {0}
+        ops = [e[1] for e in l if e[1] in ("allreduce", "group_start")]
+        # init: halo, sweep 0, all-reduce, halo; then per iteration: all-reduce, halo
+        assert ops == ["group_start", "allreduce", "group_start"] + ["allreduce", "group_start"] * 8
+    logs = native.record_comm_sequence(spec, 8, getattr(native.Split, split), 0, 8, overlap=True)
+    for l in logs:
+        ar = {e[4] for e in l if e[1] == "allreduce"}
+        halo = {e[4] for e in l if e[0] == 1}
+        assert len(ar) == 1 and halo and not (ar & halo)
 
 
 def _bench(args, timeout=300):

@@ -85,3 +85,38 @@ def test_mfma_wave_reductions(native, dev, dtype, tol):
     o = out.cpu().double()
     scale = torch.stack([xr.abs().sum(1)] * 2 + [(xr * xr).sum(1)], 1).flatten()
     assert ((o - ref).abs() <= tol * scale).all(), (o - ref).abs().max()
+
+
+@pytest.mark.parametrize("nq", [5, 2, 1])
+def test_reduction_handoff_stress(native, nq):
+    """The multi-block reductions hand their chunk sums to the last-arriving block (sc1 stores, a
+    vmcnt wait, an agent-scope ticket; the last block reads with sc1 loads -- a measured-valid
+    inter-workgroup hand-off on gfx950, MI355X_MICROARCH.md 'Valid forms', row 1).  Stress it the way
+    a stale chunk would show: 64 blocks, 200 back-to-back launches on ONE workspace with new data
+    each time, under uneven load (a bandwidth-heavy kernel on another stream).  Every result must
+    match the exactly rounded host sum to fp64 summation accuracy -- a stale chunk of the previous
+    launch would be off by ~1/64 of the sum -- and two runs must agree bitwise (fixed order)."""
+    import math
+
+    n, nsets = 40000, 200  # n / 512 >= 64: the maximum block count
+    g = torch.Generator(device="cuda").manual_seed(nq)
+    parts = torch.rand(nsets, n, nq, dtype=torch.float64, device="cuda", generator=g) + 0.5
+    side = torch.cuda.Stream()
+    hog = torch.empty(1 << 28, dtype=torch.float32, device="cuda")
+    outs = []
+    for rep in range(2):
+        out = torch.zeros(nsets, nq, dtype=torch.float64, device="cuda")
+        torch.cuda.synchronize()
+        with torch.cuda.stream(side):
+            for _ in range(20):
+                hog.mul_(1.0000001)
+        native.reduce_stress(parts.data_ptr(), n, nq, nsets, out.data_ptr(),
+                             torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        outs.append(out.cpu().numpy())
+    assert np.array_equal(outs[0], outs[1])
+    host = parts.cpu().numpy()
+    for j in range(nsets):
+        for q in range(nq):
+            exact = math.fsum(host[j, :, q])
+            assert abs(outs[0][j, q] - exact) <= 1e-13 * exact, (j, q, outs[0][j, q], exact)

@@ -184,18 +184,22 @@ def test_pcg1_fp32_triples(pkg, monkeypatch):
 
 
 def test_placement_probe(pkg, monkeypatch):
-    """The field placement probe times every candidate block it could allocate and keeps one;
-    PMX_PLACEMENT=1 switches it off.  Either way the solve is the same (bitwise: the probe only
-    chooses WHERE the fields live)."""
+    """The field placement probe (opt-in: placement=K) times the candidate blocks it could allocate
+    within its bounds and keeps one; off by default.  Either way the solve is the same (bitwise: the
+    probe only chooses WHERE the fields live)."""
     from conftest import sub
     p = pkg.PoissonEllipse(M=4000, N=4000)  # blocks under 256 MB are not probed
-    s = sub("models").make_session(p)
+    s = sub("models").make_session(p, placement=4)
     probe = s.tile.get("placement_probe_ms")
-    assert probe and len(probe) >= 2 and all(v > 0 for v in probe)
-    a = pkg.solve(p, "hip")
-    monkeypatch.setenv("PMX_PLACEMENT", "1")
-    s1 = sub("models").make_session(p)
-    assert "placement_probe_ms" not in s1.tile
+    assert probe and 2 <= len(probe) <= 4 and all(v > 0 for v in probe)
+    pl = s.tile["placement"]
+    assert pl["candidates"] == len(probe) and 0 < pl["seconds"] < 5
+    a = pkg.solve(p, "hip", placement=4)
+    s0 = sub("models").make_session(p)
+    assert "placement_probe_ms" not in s0.tile  # the library default: no probe
+    # a zero time budget times the solver's own block only: nothing to choose
+    s2 = sub("models").make_session(p, placement=4, placement_budget_s=0.0)
+    assert len(s2.tile.get("placement_probe_ms", [0])) == 1
     b = pkg.solve(p, "hip")
     assert a.iters == b.iters and np.array_equal(a.w, b.w)
 

@@ -273,3 +273,22 @@ def test_threaded_needs_rccl(pkg):
     n = pkg.load_native()
     with pytest.raises(RuntimeError, match="RCCL"):
         n.Session(pkg.PoissonEllipse(M=40, N=40).to_native(), world=2, comm="local", threaded=1)
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_threaded_failure_aborts_the_communicator_safely(pkg, overlap, tmp_path):
+    """A failure on a driver thread aborts the RCCL communicator (so peers blocked in collectives
+    return); every later call on the session must then fail with a clear error instead of touching
+    the freed communicator (ncclCommGetAsyncError in state(), collectives in step()).  overlap=False
+    is the single-communicator (serialized) layout of bench.py's rung 2."""
+    n = pkg.load_native()
+    p = pkg.PoissonEllipse(M=200, N=300)
+    s = n.Session(p.to_native(), world=1, comm="rccl", uid=n.rccl_unique_id(), ranks=[0], devices=[0],
+                  threaded=1, overlap=overlap)
+    bad = str(tmp_path / "no_such_dir" / "ck.bin")  # the checkpoint callback throws on the driver thread
+    with pytest.raises(RuntimeError, match="checkpoint"):
+        s.solve_checkpointed(bad, every=10)
+    with pytest.raises(RuntimeError, match="aborted"):
+        s.state(0)
+    with pytest.raises(RuntimeError, match="aborted"):
+        s.step(4)
