@@ -141,7 +141,10 @@ def parse(argv=None):
                     help="supervisor: wall-clock budget (s) of the whole ladder")
     ap.add_argument("--placement", type=int, default=8,
                     help="placement probe: candidate field blocks timed, the fastest kept (0 = off; "
-                         "bounded by 0.5 s and half the free memory; off when ranks share a GPU)")
+                         "bounded by --placement-budget and --placement-keep-free; off when ranks share a GPU)")
+    ap.add_argument("--placement-budget", type=float, default=0.5, help="placement probe: seconds of probing")
+    ap.add_argument("--placement-keep-free", type=float, default=0.5,
+                    help="placement probe: fraction of the free device memory left free")
     return ap.parse_args(argv)
 
 
@@ -555,7 +558,9 @@ def measure(args) -> int:
               waves=args.waves, tile_rows=args.tile_rows, exact=args.exact, graph_batch=args.graph_batch,
               overlap=overlap, vec_b=args.vec_b, tile_rows_b=args.tile_rows_b,
               b_ring=args.b_kernel == "ring")
-    dkw = dict(kw, placement=0 if share else args.placement, phase=watch.phase, init_timeout=COMM_INIT_TIMEOUT)
+    pkw = dict(placement=0 if share else args.placement, placement_budget_s=args.placement_budget,
+               placement_keep_free=args.placement_keep_free)
+    dkw = dict(kw, **pkw, phase=watch.phase, init_timeout=COMM_INIT_TIMEOUT)
     if dry:
         tp = importlib.import_module(pkg_name + ".models.torch_pcg")
         comm = importlib.import_module(pkg_name + ".parallel.comm")
@@ -565,8 +570,8 @@ def measure(args) -> int:
         comm_used = "gloo" if world > 1 else "self"
     elif world == 1:
         models = importlib.import_module(pkg_name + ".models")
-        runner = ds.SessionRunner(models.make_session(problem, ranks=1, device=info.local_rank,
-                                                      placement=args.placement, **kw), problem, info)
+        runner = ds.SessionRunner(models.make_session(problem, ranks=1, device=info.local_rank, **pkw, **kw),
+                                  problem, info)
         comm_used = "self"
     elif share and cfg["comm"] == "ipc":
         runner = ds.DistGpuPCG(problem, info, comm="ipc", device=0, **dkw)

@@ -2,7 +2,7 @@
 """Interleaved same-box A/B of solver configurations that differ only in PMX_* environment knobs.
 
     python bench/ab_env.py --shape 16384x16384 --shape 2048x16384 \
-        --cfg base: --cfg s4:PMX_PCG1_SUPER=4 --rounds 3 --iters 200
+        --cfg base: --cfg r12:PMX_PCG1_ROWS=12 --rounds 3 --iters 200
     python bench/ab_env.py --pkg old=bench/ab/pmx_base --cfg old@old: --cfg new: ...   # binary A/B
 
 A configuration `name@pkg:ENV` runs the package copy registered with --pkg pkg=DIR (a build of an

@@ -62,26 +62,6 @@ STUDIES: dict[str, list[tuple[str, int, str]]] = {
         ("bench_default", 300, bench("--gpus 1 --steps 20 --warmup 5")),
         ("bench_200", 300, bench("--gpus 1 --steps 200 --warmup 20 --no-tol-solve")),
     ],
-    # round 3: super-row dispatch + alternating march direction (halo-row reuse in L2)
-    "super_ab": [
-        ("ab", 900, "python -u bench/ab_env.py --shape 16384x16384 --shape 2048x16384 --cfg base: "
-                    "--cfg s2:PMX_PCG1_SUPER=2 --cfg s4:PMX_PCG1_SUPER=4 --cfg s8:PMX_PCG1_SUPER=8 "
-                    "--rounds 3 --iters 200"),
-        ("tol", 300, "python -u bench/ab_env.py --shape 16384x16384 --cfg s4:PMX_PCG1_SUPER=4 --rounds 1 "
-                     "--iters 20 --tol"),
-    ],
-    "dir_ab": [
-        ("ab", 900, "python -u bench/ab_env.py --shape 16384x16384 --shape 2048x16384 --cfg base: "
-                    "--cfg rev:PMX_PCG1_ALT=2 --cfg alt:PMX_PCG1_ALT=1 --cfg s4fwd:PMX_PCG1_SUPER=4,PMX_PCG1_ALT=0 "
-                    "--cfg s2fwd:PMX_PCG1_SUPER=2,PMX_PCG1_ALT=0 --rounds 3 --iters 200"),
-        ("rocprof_bench", 300, f"{ROCPROF} -d gpurun_out/dir_ab/rp -o run -- "
-                               + bench("--gpus 1 --steps 60 --warmup 10 --no-tol-solve")),
-    ],
-    "bands_ab": [
-        ("ab", 900, "python -u bench/ab_env.py --shape 16384x16384 --shape 2048x16384 --cfg base: "
-                    "--cfg b2:PMX_PCG1_BANDS=2 --cfg b3:PMX_PCG1_BANDS=3 --cfg b4:PMX_PCG1_BANDS=4 "
-                    "--rounds 3 --iters 200"),
-    ],
     # binary A/B against a build of the previous commit copied to bench/ab/pmx_base (gitignored)
     "pf_ab": [
         ("fp64", 600, "python -u bench/ab_env.py --shape 16384x16384 --shape 2048x16384 --cfg base: "
@@ -239,14 +219,6 @@ STUDIES["placement"] = [
     ("hold", 600, "python -u bench/probe/placement.py --hold 0 --hold 16 --hold 48 --hold 120 --rounds 2"),
     ("pytest_f32", 300, f"{PYTEST} tests/test_gpu_pcg1.py -k 'fp32' tests/test_gpu_cli.py"),
 ]
-STUDIES["stagger"] = [
-    ("stagger", 900, "python -u bench/probe/placement.py --rounds 2 --cfg sep:PMX_FIELD_STAGGER=-1 "
-                     "--cfg s0:PMX_FIELD_STAGGER=0 --cfg s4k:PMX_FIELD_STAGGER=4096 --cfg s64k:PMX_FIELD_STAGGER=65536 "
-                     "--cfg s256k:PMX_FIELD_STAGGER=262144 --cfg s1m:PMX_FIELD_STAGGER=1048576 "
-                     "--cfg s2m4k:PMX_FIELD_STAGGER=2101248 --cfg s8m:PMX_FIELD_STAGGER=8388608 "
-                     "--cfg contig:PMX_FIELD_CONTIG=1"),
-    ("multi", 300, "python -u bench/probe/placement.py --multi 6"),
-]
 STUDIES["alloc"] = [
     ("multi8", 400, "env PMX_DEBUG_ALLOC=1 python -u bench/probe/placement.py --multi 8"),
 ]
@@ -327,9 +299,40 @@ STUDIES["blocks8"] = [
 ] + _timeline(["--ranks", "8", "--iters", "300", "--case", "ref", "16384 16384 --split reference",
                "--case", "rows", "16384 16384 --split rows"])
 
+# round 4: placement mechanism -- per-candidate TLB and memory-side counters of the probe's sweeps
+PLACEMENT_PASSES = {
+    "utcl1": "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum "
+             "TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum",
+    "utcl1b": "TCP_UTCL1_TRANSLATION_MISS_UNDER_MISS_sum TCP_UTCL1_STALL_MULTI_MISS_sum "
+              "TCP_UTCL1_SERIALIZATION_STALL_sum TCP_UTCL1_THRASHING_STALL_sum",
+    "lat": "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE GRBM_COUNT",
+    "ea": "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_WRREQ_sum",
+}
+
+
+def placement_pmc_steps(study: str, k: int = 24) -> list:
+    steps = []
+    for tag, counters in PLACEMENT_PASSES.items():
+        steps.append((tag, 100, f"bash -c 'timeout -s KILL 90 rocprofv3 --pmc {counters} --output-format csv "
+                                f"-d gpurun_out/{study}/{tag} -o run -- python3 bench/probe/placement_pmc.py child "
+                                f"--k {k} > gpurun_out/{study}/{tag}.json'"))
+    steps.append(("summary", 60, f"python3 bench/probe/placement_pmc.py summary gpurun_out/{study}"))
+    return steps
+
+
+# round 4, first contact: the suite (abort guards, serialized comm schedule, reduction stress,
+# opt-in placement), smoke, the default bench (bounded probe) against the round-3 probe, a kernel
+# profile, and the placement counter passes
+STUDIES["r4a"] = [
+    ("pytest_gpu", 700, f"{PYTEST} tests -m gpu"),
+    ("smoke", 120, "python -c 'import __graft_entry__ as g; g.smoke()'"),
+    ("bench_default", 300, bench("--gpus 1 --steps 20 --warmup 5")),
+    ("bench_probe_r3", 300, bench("--gpus 1 --steps 20 --warmup 5 --placement 160 --placement-budget 60 "
+                                  "--placement-keep-free 0.125 --no-tol-solve")),
+    ("bench_noprobe", 300, bench("--gpus 1 --steps 20 --warmup 5 --placement 0 --no-tol-solve")),
+] + placement_pmc_steps("r4a")
+
 PARAMETRISED = {"ab": _ab, "pmc": _pmc, "timeline": _timeline, "validate": _validate, "share": _share, "cli": _cli}
-STUDIES["pmc_super"] = pmc_study("pmc_super", {"base": "", "s4": "PMX_PCG1_SUPER=4"}, PMC_ARGS,
-                                 ("ea_rd", "ea_wr", "lat"))
 
 
 def script(name: str, steps) -> str:

@@ -9,8 +9,9 @@ alive), each configuration in a fresh child process, configurations interleaved 
 
     python bench/probe/placement.py --hold 0 --hold 16 --hold 64 --rounds 2
     python bench/probe/placement.py --multi 4      # 4 sessions alive in one process, each timed
-    python bench/probe/placement.py --cfg s0:PMX_FIELD_STAGGER=0 --cfg sep:PMX_FIELD_STAGGER=-1
+    python bench/probe/placement.py --cfg off: --cfg k8:PMX_PLACEMENT=8
                                                    # environment configurations, fresh child each
+                                                   # (the library's probe is off unless PMX_PLACEMENT=K)
 """
 from __future__ import annotations
 

@@ -97,9 +97,6 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_PCG1_WAVES", o.waves1);
   env_int("PMX_PCG1_PF", o.pf1);
   env_int("PMX_PCG1_ORDER", o.order1);
-  env_int("PMX_PCG1_SUPER", o.super1);
-  env_int("PMX_PCG1_ALT", o.alt1);
-  env_int("PMX_PCG1_BANDS", o.bands1);
   env_int("PMX_PCG1_WCYCLE", o.wcycle1);
   env_int("PMX_PROGRESS", o.progress);
   env_int("PMX_ARITH32", o.arith32);
@@ -173,8 +170,6 @@ GpuSubdomainSolver::GpuSubdomainSolver(const ProblemSpec& spec, const Subdomain&
   }
 }
 
-// Bytes between consecutive fields of the one field allocation (see construct).
-constexpr long long kFieldStagger = 0;
 
 void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   const GpuOptions& opt = opt_;
@@ -210,21 +205,12 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
                               "device is ~"
                            << max_square_grid(double(total_b), 1, opt.dtype) << "^2 (pmx --plan)");
   }
-  // One allocation for all fields.  The stagger between consecutive fields decides how their rows
-  // fall onto HBM channels/banks relative to each other: every sweep streams the same row of 4-5
-  // fields at once (PMX_FIELD_STAGGER bytes, multiple of 256; -1 = r2 allocated on its own).
-  long long stagger = kFieldStagger;
-  if (const char* e = std::getenv("PMX_FIELD_STAGGER"); e && e[0]) stagger = std::atoll(e);
-  PMX_CHECK(stagger == -1 || (stagger >= 0 && stagger % 256 == 0), "PMX_FIELD_STAGGER: -1 or a multiple of 256");
-  own_r2_ = stagger == -1 && pcg1_;
-  field_stride_ = field_bytes_ + size_t(std::max(0LL, stagger));
-  const int nfields = pcg1_ && !own_r2_ ? 5 : 4;
-  // PMX_FIELD_CONTIG=1 (study): physically contiguous VRAM for the fields (hipDeviceMallocContiguous)
-  if (const char* e = std::getenv("PMX_FIELD_CONTIG"); e && e[0] == '1')
-    HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&fields_), size_t(nfields) * field_stride_,
-                                    hipDeviceMallocContiguous));
-  else
-    HIP_CHECK(hipMalloc(&fields_, size_t(nfields) * field_stride_));
+  // One allocation for all fields (field f at fields_ + f * field_bytes_).  The offset between the
+  // fields (0 ... 8 MiB of stagger) and physically contiguous memory were measured: no gain
+  // (profiles/r3/placement/stagger.log); where the block lands is what matters (place_fields).
+  field_stride_ = field_bytes_;
+  const int nfields = pcg1_ ? 5 : 4;
+  HIP_CHECK(hipMalloc(&fields_, size_t(nfields) * field_stride_));
   if (const char* e = std::getenv("PMX_DEBUG_ALLOC"); e && e[0] == '1')
     std::fprintf(stderr, "pmx alloc: fields %p (%zu B, mod 1G %zu, mod 2M %zu)\n", static_cast<void*>(fields_),
                  size_t(nfields) * field_stride_, size_t(reinterpret_cast<uintptr_t>(fields_) % (size_t(1) << 30)),
@@ -260,20 +246,11 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
       wtrace_ = pcg1_wave_trace_setup(std::atoll(e), wtrace_n_);
     }
 #endif
-    if (own_r2_)
-      HIP_CHECK(hipMalloc(&r2_, field_bytes_));
-    else
-      r2_ = field_raw(4);
-    tiles1_.super = opt_.super1;
+    r2_ = field_raw(4);
     tiles1_.arith32 = elem_ == 4 && opt_.arith32 ? 1 : 0;
-    tiles1_.bands = opt_.bands1;
-    tiles1_.alt = opt_.alt1 >= 0 ? opt_.alt1 : (opt_.super1 > 0 ? 1 : 0);
     tiles1w_ = make_pcg1_tiles(G, opt_.vec1, opt_.waves1, opt_.rows1w ? opt_.rows1w : tiles1_.rows,
                                opt_.pf1w ? opt_.pf1w : tiles1_.pf, int(elem_));
-    tiles1w_.super = tiles1_.super;
     tiles1w_.arith32 = tiles1_.arith32;
-    tiles1w_.bands = tiles1_.bands;
-    tiles1w_.alt = tiles1_.alt;
     const bool same_w = tiles1w_.rows == tiles1_.rows;
     // dispatch order tables with the tiles' row classes; order1: the ellipse-cut tiles first
     // within each XCD's share (their 3-5x longer tiles would trail the sweep)
@@ -330,8 +307,7 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
 // candidate: 3 plain sweeps with the five fields in rotating roles (probe_sweeps: every field read
 // and written; zeroed fields, the init sweep's k = 0 arithmetic; init() resets everything
 // afterwards).  Construction time only; nothing in the iteration changes.  Off by default (the
-// library) and for ranks that share a device; skipped with an external (IPC-shared) arena or a
-// separately allocated r2.
+// library) and for ranks that share a device; skipped with an external (IPC-shared) arena.
 // Plain sweeps (k = 0 arithmetic) with the five field blocks in rotating roles, so that every field
 // of the candidate block is read and written: role set q reads r = F[q], p = F[q+3] and writes
 // r2 = F[q+4], p0 = F[q+2] (indices mod 5; F = w, r, p0, p1, r2).
@@ -346,7 +322,7 @@ void GpuSubdomainSolver::probe_sweeps(hipStream_t s, int first, int count) {
 void GpuSubdomainSolver::place_fields() {
   const int K = opt_.placement;
   const size_t block = 5 * field_stride_;
-  if (K <= 1 || !own_arena_ || own_r2_ || block < (size_t(256) << 20)) return;  // small grids: latency-bound
+  if (K <= 1 || !own_arena_ || block < (size_t(256) << 20)) return;  // small grids: latency-bound
   const double t0 = now_s();
   std::vector<char*> cand{fields_};
   size_t free0 = 0, total_b = 0;
@@ -461,7 +437,6 @@ void GpuSubdomainSolver::release() noexcept {
   (void)hipSetDevice(opt_.device);
   (void)hipDeviceSynchronize();
   if (fields_) (void)hipFree(fields_);
-  if (r2_ && own_r2_) (void)hipFree(r2_);
   if (tile_order_) (void)hipFree(tile_order_);
   if (tile_order_w_) (void)hipFree(tile_order_w_);
   if (tables_buf_) (void)hipFree(tables_buf_);

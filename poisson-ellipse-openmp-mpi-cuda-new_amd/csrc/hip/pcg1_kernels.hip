@@ -52,11 +52,6 @@ using namespace dev;
 namespace {
 
 constexpr int kNq = 5;  // rho, (Az,z), (Az,p), (Ap,p), |p|^2
-#ifdef PMX_PCG1_REVERSE
-constexpr bool kPcg1Reverse = true;
-#else
-constexpr bool kPcg1Reverse = false;
-#endif
 constexpr int kPcg1AutoPf = 1;
 // waves/SIMD bounds of the fp32-arithmetic sweeps (plain, w)
 #ifndef PMX_PCG1_F32_WAVES
@@ -89,31 +84,13 @@ __device__ __forceinline__ T* col_ptr(T* row, int c) {
 }
 
 template <typename T, int VEC>
-__device__ __forceinline__ void load_cols_nt(const T* row, int c0, int cmax, T (&out)[VEC]) {
-#pragma unroll
-  for (int q = 0; q < VEC / 2; ++q) {
-    typedef T V __attribute__((ext_vector_type(2)));
-    const V v = __builtin_nontemporal_load(reinterpret_cast<const V*>(col_ptr(row, min(c0 + 2 * q, cmax))));
-    out[2 * q] = v[0];
-    out[2 * q + 1] = v[1];
-  }
-}
-
-template <typename T, int VEC>
 __device__ __forceinline__ void load_cols(const T* row, int c0, int cmax, T (&out)[VEC]) {
 #pragma unroll
   for (int q = 0; q < VEC / 2; ++q) {
-#ifdef PMX_PCG1_NT_LOADS  // study build: streaming hint on every field load
-    typedef T V __attribute__((ext_vector_type(2)));
-    const V v = __builtin_nontemporal_load(reinterpret_cast<const V*>(col_ptr(row, min(c0 + 2 * q, cmax))));
-    out[2 * q] = v[0];
-    out[2 * q + 1] = v[1];
-#else
     T v[2];
     vload_raw<T, 2>(col_ptr(row, min(c0 + 2 * q, cmax)), v);
     out[2 * q] = v[0];
     out[2 * q + 1] = v[1];
-#endif
   }
 }
 
@@ -121,21 +98,17 @@ __device__ __forceinline__ void load_cols(const T* row, int c0, int cmax, T (&ou
 // sweep, and fewer dirty lines sit in the XCD L2s when the sweep ends (the kernel-end writeback is
 // part of every kernel boundary).  Fresh-process A/B, 4 rounds: 16384^2 fp64 1845.9 -> 1796.3 us
 // (-2.7%, every nt run below every plain-store run), 2048x16384 263.4 -> 254.5 us
-// (profiles/r3/nt_stores/).  PMX_PCG1_TEMPORAL_STORES builds the plain stores (study).
+// (profiles/r3/nt_stores/).  Non-temporal LOADS lose (+10-22%: the L2 reuse of halo rows and
+// overlapping columns matters, NOTES #60-61).
 template <typename T, int VEC>
 __device__ __forceinline__ void store_cols(T* row, int c0, const T (&in)[VEC], bool all,
                                            const bool (&own)[VEC]) {
   if (all) {
 #pragma unroll
     for (int q = 0; q < VEC / 2; ++q) {
-#ifndef PMX_PCG1_TEMPORAL_STORES
       typedef T V __attribute__((ext_vector_type(2)));
       const V v = {in[2 * q], in[2 * q + 1]};
       __builtin_nontemporal_store(v, reinterpret_cast<V*>(col_ptr(row, c0 + 2 * q)));
-#else
-      const T v[2] = {in[2 * q], in[2 * q + 1]};
-      vstore<T, 2>(col_ptr(row, c0 + 2 * q), v);
-#endif
     }
   } else {
 #pragma unroll
@@ -289,12 +262,10 @@ struct Pcg1Row {
 // domain, VEC = 2): no Dirichlet masks, and ownership is a fixed lane set (lanes 1..62 own both
 // their columns, lanes 0 and 63 none), so the sums accumulate unmasked and are masked once at the
 // end.  Same arithmetic as the general path, so a point's values never depend on its tile.
-// DIR: +1 marches the tile top-down (rows i0-2 .. i1+2), -1 bottom-up (i1+2 .. i0-2).  The stencil
-// is symmetric in i, so the pipeline only swaps which stored row is i-1 and which i+1; every
-// point gets the same arithmetic either way (only the order of the per-lane partial sums over
-// rows differs).  Alternating directions make vertically adjacent tiles that start together read
-// their shared halo rows at the same time (see pcg1_build_order).
-template <typename T, typename C, int VEC, int PF, int WM, bool FAST, int DIR>
+// The tile marches top-down, rows i0-2 .. i1+2.  (Bottom-up and alternating marches, super-row and
+// banded dispatch orders were tried to make vertically adjacent tiles share their halo rows in L2:
+// all slower, NOTES #30, #46-48.)
+template <typename T, typename C, int VEC, int PF, int WM, bool FAST>
 __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb, const ArithF& F, T* __restrict__ w,
                                            const T* __restrict__ rold, T* __restrict__ rnew,
                                            const T* __restrict__ pold,
@@ -328,34 +299,18 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   auto grow = [&](int m) { return min(max(G.gi0 + m, 0), G.M); };  // table row of local row m
   // row m's class: from the slot's bits (Pcg1Slot) or from the tables
   auto row_of = [&](int m) {
-    if (DIR > 0 && use_cls) return RowCo{grow(m), int((cls >> (2 * (m - i0 + 3))) & 3ull)};
+    if (use_cls) return RowCo{grow(m), int((cls >> (2 * (m - i0 + 3))) & 3ull)};
     return row_co(Tb, grow(m), gjlo, gjhi);
   };
   auto interior_row = [&](int m) { return G.gi0 + m >= 1 && G.gi0 + m <= G.M - 1; };
 
   auto fetch = [&](int m, Pcg1Row<T, VEC>& b) {
     const int mc = min(max(m, -1), G.nx + 2);  // rows -1 .. nx+2 exist (2 ghost layers)
-#ifdef PMX_PCG1_NT_PRIV
-    // study build: rows no vertically adjacent tile marches (i0+2 .. i1-2) with the streaming hint,
-    // so the L2 keeps the shared halo rows longer
-    if (mc >= i0 + 2 && mc <= i1 - 2) {
-      load_cols_nt<T, VEC>(rold + int64_t(mc) * P, c0, cmax, b.r);
-      load_cols_nt<T, VEC>(pold + int64_t(mc) * P, c0, cmax, b.p);
-    } else {
-      load_cols<T, VEC>(rold + int64_t(mc) * P, c0, cmax, b.r);
-      load_cols<T, VEC>(pold + int64_t(mc) * P, c0, cmax, b.p);
-    }
-#else
     load_cols<T, VEC>(rold + int64_t(mc) * P, c0, cmax, b.r);
     load_cols<T, VEC>(pold + int64_t(mc) * P, c0, cmax, b.p);
-#endif
     if constexpr (WUP) {  // w of the row stage B handles next step
-      const int wc = min(max(m - DIR, -1), G.nx + 2);
-#ifdef PMX_PCG1_NT_PRIV
-      load_cols_nt<T, VEC>(w + int64_t(wc) * P, c0, cmax, b.w);
-#else
+      const int wc = min(max(m - 1, -1), G.nx + 2);
       load_cols<T, VEC>(w + int64_t(wc) * P, c0, cmax, b.w);
-#endif
       // p^{k-2} still sits in the buffer this sweep overwrites with p^k: the owner of a point
       // reads it here, before its own store of that row (rows it does not own are never used)
       if constexpr (WM == 3) load_cols<T, VEC>(pnew + int64_t(wc) * P, c0, cmax, b.q);
@@ -366,7 +321,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   C Pm2[VEC], Pm1[VEC], Zm3[VEC], Zm2[VEC], ro1[VEC], po1[VEC], po2[VEC];
 #pragma unroll
   for (int u = 0; u < VEC; ++u) Pm2[u] = Pm1[u] = Zm3[u] = Zm2[u] = ro1[u] = po1[u] = po2[u] = C(0);
-  RowCo cB = row_of(DIR > 0 ? i0 - 3 : i1 + 3);  // rows m-DIR, m-2 DIR
+  RowCo cB = row_of(i0 - 3);  // rows m-1, m-2
   RowCo cC = cB;
   bool parked = false;  // column constants in LDS (see col_lds)
   auto park_cols = [&]() {
@@ -382,11 +337,11 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   };
   if (cB.ucls == 0) park_cols();
 
-  const int mfirst = DIR > 0 ? i0 - 2 : i1 + 2, mlast = DIR > 0 ? i1 + 2 : i0 - 2;
+  const int mfirst = i0 - 2, mlast = i1 + 2;
   auto step = [&](int m, const Pcg1Row<T, VEC>& cur, Pcg1Row<T, VEC>& nxt) {
     // PF rows ahead, unconditional (a branch around loads forces vmcnt(0)); past the tile's last
     // row re-read that row (a cache hit) instead of the next tile's rows
-    fetch(DIR > 0 ? min(m + PF, mlast) : max(m - PF, mlast), nxt);
+    fetch(min(m + PF, mlast), nxt);
     // ---- stage A: p^k of row m
     const bool rowA = FAST || interior_row(m);
     const RowCo cA = row_of(m);
@@ -403,10 +358,9 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
       const C v = fma_c(beta, pom[u], z);
       Pm[u] = in ? C(static_cast<T>(v)) : C(0);  // the stored (rounded) p^k is the one used
     }
-    // ---- stage B: A p^k, r^k, z^k of row m-DIR (j neighbours by DPP; edge lanes get 0, their
-    // results only feed columns that are not owned).  Rows i-1 / i+1 of it: Pm2 / Pm (DIR +1),
-    // Pm / Pm2 (DIR -1).
-    const int mb = m - DIR;
+    // ---- stage B: A p^k, r^k, z^k of row m-1 (j neighbours by DPP; edge lanes get 0, their
+    // results only feed columns that are not owned).  Rows i-1 / i+1 of it: Pm2 / Pm.
+    const int mb = m - 1;
     const bool rowB = FAST || interior_row(mb);
     const bool ownB = mb >= i0 && mb <= i1;
     C Zm1[VEC];
@@ -425,19 +379,19 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
       if constexpr (PK) {
 #pragma unroll
         for (int u = 0; u < VEC; ++u) coef_c<C>(cB, Tb, G, F, scol, u, lane, gj[u], a0[u], a1[u], b0[u], b1[u]);
-        apply_row<C, VEC>(Pm1, DIR > 0 ? Pm2 : Pm, DIR > 0 ? Pm : Pm2, left, right, a0, a1, b0, b1, G, F, Ap);
+        apply_row<C, VEC>(Pm1, Pm2, Pm, left, right, a0, a1, b0, b1, G, F, Ap);
         // p^{k-2} recovery (WM 2): A p^{k-1}
         if constexpr (WM == 2)
-          apply_row<C, VEC>(po1, DIR > 0 ? po2 : pom, DIR > 0 ? pom : po2, oleft, oright, a0, a1, b0, b1, G, F, Apo);
+          apply_row<C, VEC>(po1, po2, pom, oleft, oright, a0, a1, b0, b1, G, F, Apo);
       }
 #pragma unroll
       for (int u = 0; u < VEC; ++u) {
         if constexpr (!PK) {
           coef_c<C>(cB, Tb, G, F, scol, u, lane, gj[u], a0[u], a1[u], b0[u], b1[u]);
-          Ap[u] = apply_c<C>(Pm1[u], DIR > 0 ? Pm2[u] : Pm[u], DIR > 0 ? Pm[u] : Pm2[u], u == 0 ? left : Pm1[u - 1],
+          Ap[u] = apply_c<C>(Pm1[u], Pm2[u], Pm[u], u == 0 ? left : Pm1[u - 1],
                              u == VEC - 1 ? right : Pm1[u + 1], a0[u], a1[u], b0[u], b1[u], G, F);
           if constexpr (WM == 2)
-            Apo[u] = apply_c<C>(po1[u], DIR > 0 ? po2[u] : pom[u], DIR > 0 ? pom[u] : po2[u],
+            Apo[u] = apply_c<C>(po1[u], po2[u], pom[u],
                                 u == 0 ? oleft : po1[u - 1], u == VEC - 1 ? oright : po1[u + 1], a0[u], a1[u], b0[u],
                                 b1[u], G, F);
         }
@@ -471,8 +425,8 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
       store_cols<T, VEC>(pnew + o, c0, ps, FAST || own_all, own);
       if constexpr (WUP) store_cols<T, VEC>(w + o, c0, ws, FAST || own_all, own);
     }
-    // ---- stage C: A z^k of row m-2 DIR
-    const int mcr = m - 2 * DIR;
+    // ---- stage C: A z^k of row m-2
+    const int mcr = m - 2;
     if (mcr >= i0 && mcr <= i1) {
       const C left = dpp_shift<kWaveShr1>(Zm2[VEC - 1], C(0));
       const C right = dpp_shift<kWaveShl1>(Zm2[0], C(0));
@@ -480,13 +434,13 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
       if constexpr (PK) {
 #pragma unroll
         for (int u = 0; u < VEC; ++u) coef_c<C>(cC, Tb, G, F, scol, u, lane, gj[u], a0[u], a1[u], b0[u], b1[u]);
-        apply_row<C, VEC>(Zm2, DIR > 0 ? Zm3 : Zm1, DIR > 0 ? Zm1 : Zm3, left, right, a0, a1, b0, b1, G, F, Az);
+        apply_row<C, VEC>(Zm2, Zm3, Zm1, left, right, a0, a1, b0, b1, G, F, Az);
       }
 #pragma unroll
       for (int u = 0; u < VEC; ++u) {
         if constexpr (!PK) {
           coef_c<C>(cC, Tb, G, F, scol, u, lane, gj[u], a0[u], a1[u], b0[u], b1[u]);
-          Az[u] = apply_c<C>(Zm2[u], DIR > 0 ? Zm3[u] : Zm1[u], DIR > 0 ? Zm1[u] : Zm3[u], u == 0 ? left : Zm2[u - 1],
+          Az[u] = apply_c<C>(Zm2[u], Zm3[u], Zm1[u], u == 0 ? left : Zm2[u - 1],
                              u == VEC - 1 ? right : Zm2[u + 1], a0[u], a1[u], b0[u], b1[u], G, F);
         }
         if (FAST || own[u]) {
@@ -512,12 +466,12 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   // slot q and refills the slot step m - 1 consumed
   Pcg1Row<T, VEC> buf[PF + 1];
 #pragma unroll
-  for (int q = 0; q < PF; ++q) fetch(DIR > 0 ? min(mfirst + q, mlast) : max(mfirst - q, mlast), buf[q]);
-  for (int m = mfirst; DIR > 0 ? m <= mlast : m >= mlast; m += DIR * (PF + 1)) {
+  for (int q = 0; q < PF; ++q) fetch(min(mfirst + q, mlast), buf[q]);
+  for (int m = mfirst; m <= mlast; m += PF + 1) {
 #pragma unroll
     for (int q = 0; q <= PF; ++q) {
-      if (DIR > 0 ? m + q > mlast : m - q < mlast) goto done;
-      step(m + DIR * q, buf[q], buf[(q + PF) % (PF + 1)]);
+      if (m + q > mlast) goto done;
+      step(m + q, buf[q], buf[(q + PF) % (PF + 1)]);
     }
   }
 done:
@@ -554,7 +508,6 @@ struct Pcg1Part {
   int tiles_i, ti_lo, ti_hi, tj_lo, tj_hi;
   const Pcg1Slot* order;  // position -> tile + row classes (pcg1_build_order), or nullptr: pcg1_tile's order
   int count;         // tiles of this launch
-  int alt;           // 1: tiles with even ti march bottom-up, 2: every tile (TileCfg::alt)
 };
 
 // k-th tile of the part -> (ti, tj); false past the end.  The frame is enumerated as: tile rows
@@ -736,24 +689,9 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
                     G.gj0 + j0 - 2 >= 1 && G.gj0 + j0 + 64 * VEC - 3 <= G.N - 1;
   const bool use_cls = part.order != nullptr && TI + 5 <= 64 / 2;  // 2 bits for each of the TI+5 rows
   const ArithF AF{float(G.cx), float(G.cy), float(G.dinv_in), float(G.dinv_out), float(G.inv_eps)};
-#ifdef PMX_PCG1_REVERSE
-  // study build only (NOTES #46-#47: bottom-up marches lose ~4%): tiles with even ti (alt 1) or
-  // every tile (alt 2) march bottom-up
-  const bool rev = part.alt == 2 || (part.alt == 1 && !(ti & 1));  // a function of the tile alone
-#define PMX_MARCH(E, F)                                                                                   \
-  do {                                                                                                   \
-    if (rev)                                                                                             \
-      pcg1_march<T, C, VEC, PF, E, F, -1>(G, Tb, AF, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, \
-                                          c2, acc, scol, ocls, use_cls);                                         \
-    else                                                                                                 \
-      pcg1_march<T, C, VEC, PF, E, F, 1>(G, Tb, AF, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, \
-                                         c2, acc, scol, ocls, use_cls);                                          \
-  } while (0)
-#else
-#define PMX_MARCH(E, F)                                                                                          \
-  pcg1_march<T, C, VEC, PF, E, F, 1>(G, Tb, AF, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, acc, \
-                                     scol, ocls, use_cls)
-#endif
+#define PMX_MARCH(E, F)                                                                                       \
+  pcg1_march<T, C, VEC, PF, E, F>(G, Tb, AF, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, acc, \
+                                  scol, ocls, use_cls)
 #define PMX_MARCH_W(F)                                     \
   if constexpr (!WS) {                                     \
     PMX_MARCH(0, F);                                       \
@@ -959,41 +897,20 @@ int pcg1_build_order(const DevGeom& G, const DevTables& Tb, TileCfg& tc, Pcg1Slo
   std::vector<Pcg1Slot> order(3 * size_t(n), Pcg1Slot{0, 0, 0ull});
   int nslow = 0;
   for (int part = 0; part <= 2; ++part) {
-    const Pcg1Part P{part, tc.tiles_i, tc.ti_lo, tc.ti_hi, tc.tj_lo, tc.tj_hi, nullptr, 0, 0};
+    const Pcg1Part P{part, tc.tiles_i, tc.ti_lo, tc.ti_hi, tc.tj_lo, tc.tj_hi, nullptr, 0};
     const int count = part == 0 ? n : part == 1 ? tc.interior_tiles() : n - tc.interior_tiles();
     Pcg1Slot* o = order.data() + size_t(part) * n;
     // positions of XCD x (xcd_remap with one wave per workgroup): [x (q+1), ...) as in xcd_remap
     const int q = count / 8, r = count % 8;
-    const int S = std::max(1, tc.super);
     std::vector<int> ids;
     for (int x = 0, start = 0; x < 8; ++x) {
       const int len = q + (x < r ? 1 : 0);
-      // this XCD's tiles (a band of tile rows), dispatched super-row by super-row, column by
-      // column inside a super-row (S = 1: row-major)
+      // this XCD's tiles (a band of tile rows), row-major
       ids.clear();
       for (int k = start; k < start + len; ++k) {
         int ti = 0, tj = 0;
         PMX_CHECK(pcg1_tile(k, P, tc.tiles_j, ti, tj), "pcg1_build_order: tile enumeration");
         ids.push_back(ti * tc.tiles_j + tj);
-      }
-      if (S > 1)
-        std::stable_sort(ids.begin(), ids.end(), [&](int a, int b) {
-          const int ta = a / tc.tiles_j, tb = b / tc.tiles_j;
-          const int ka[3] = {ta / S, a % tc.tiles_j, ta % S}, kb[3] = {tb / S, b % tc.tiles_j, tb % S};
-          return std::lexicographical_compare(ka, ka + 3, kb, kb + 3);
-        });
-      // bands > 1: the chunk's tiles split into `bands` consecutive runs dispatched round-robin, so
-      // a tile's lower neighbour starts ~bands tile rows of dispatches later (a lag closer to the
-      // time the upper tile reaches the rows they share)
-      const int B = std::max(1, std::min(tc.bands, int(ids.size())));
-      if (B > 1) {
-        std::vector<int> il;
-        il.reserve(ids.size());
-        const size_t per = (ids.size() + B - 1) / B;
-        for (size_t k = 0; k < per; ++k)
-          for (int b = 0; b < B; ++b)
-            if (b * per + k < ids.size()) il.push_back(ids[b * per + k]);
-        ids.swap(il);
       }
       int w = start;
       for (int pass = 0; pass < (slow_first ? 2 : 1); ++pass)  // slow tiles first, then the rest
@@ -1064,8 +981,7 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
   PMX_CHECK(part >= 0 && part <= 2, "launch_pcg1: part must be 0, 1 or 2");
   const int count = part == 0 ? tc.ntiles() : part == 1 ? tc.interior_tiles() : tc.ntiles() - tc.interior_tiles();
   const Pcg1Part P{part, tc.tiles_i, tc.ti_lo, tc.ti_hi, tc.tj_lo, tc.tj_hi,
-                   tc.waves == 1 ? (part == 0 ? tc.order0 : part == 1 ? tc.order1 : tc.order2) : nullptr, count,
-                   tc.alt};
+                   tc.waves == 1 ? (part == 0 ? tc.order0 : part == 1 ? tc.order1 : tc.order2) : nullptr, count};
   if (count == 0) return;
   PMX_CHECK(G.nb == 0 || (G.nx >= 2 && G.ny >= 2), "pcg1 on a decomposed grid needs subdomains >= 2 x 2");
   const int nb = (count + tc.waves - 1) / tc.waves;
@@ -1091,7 +1007,6 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
   // instantiated shapes: the default (VEC 2, 1 wave, prefetch 1) and prefetch 2.  The other
   // shapes of the round-1/2 sweeps (prefetch 3-4, 2 or 4 waves per workgroup, VEC 4: all slower,
   // NOTES #23, #40) need a PMX_PCG1_ALL_SHAPES build
-  PMX_CHECK(tc.alt == 0 || kPcg1Reverse, "pcg1: alternating march directions need a PMX_PCG1_REVERSE build");
   if (tc.vec == 2 && tc.waves == 1 && tc.pf == 1) PMX_PCG1(2, 1, 1);
   else if (tc.vec == 2 && tc.waves == 1 && tc.pf == 2) PMX_PCG1(2, 1, 2);
   else if (tc.vec == 2 && tc.waves == 1 && tc.pf == 3) PMX_PCG1(2, 1, 3);

@@ -87,13 +87,6 @@ struct GpuOptions {
   int arith32 = 0;
   // pcg1 dispatch order: 1 = tiles cut by the ellipse first within each XCD's share, 0 = natural
   int order1 = 1;
-  // pcg1 halo-row reuse (TileCfg::super / alt): super-rows of `super1` tile rows dispatched column by
-  // column, even tile rows marching bottom-up.  0 = row-major order, every tile top-down.
-  // PMX_PCG1_SUPER overrides.
-  int super1 = 0;
-  int bands1 = 1;  // sub-bands per XCD chunk dispatched round-robin (PMX_PCG1_BANDS)
-  int alt1 = -1;  // march directions: -1 = alternate iff super1 > 0, 0 = all top-down, 1 = alternate,
-                  // 2 = all bottom-up (PMX_PCG1_ALT; ablations)
   // pcg1 w schedule: w is read and written on one sweep in wcycle1 (3 = triples, 2 = pairs).
   // Triples recover p^{k-2} from p^{k-1} and r^{k-1} (one extra stencil), or re-read it when
   // |beta_{k-1}| < 1e-3 or pair_w == 2.  PMX_PCG1_WCYCLE=2|3 overrides.
@@ -271,13 +264,11 @@ class GpuSubdomainSolver {
   TileCfg init_tiles_{};
   CommLayout layout_{};
   size_t elem_ = 8, field_bytes_ = 0, field_off_ = 0;
-  // Fields w, r, p0, p1 (and pcg1's r2) in ONE allocation, field f at fields_ + f * field_stride_
-  // (field_bytes_ + a stagger, see construct); rows -1 .. nx+2 each.  PMX_FIELD_STAGGER=-1 keeps the
-  // round-1/2 layout (r2 a separate allocation) for A/B studies.
+  // Fields w, r, p0, p1 (and pcg1's r2) in ONE allocation, field f at fields_ + f * field_stride_;
+  // rows -1 .. nx+2 each.
   char* fields_ = nullptr;
   char* r2_ = nullptr;      // pcg1 only: the second r buffer (r is double-buffered there)
   size_t field_stride_ = 0;
-  bool own_r2_ = false;     // r2_ is its own allocation (PMX_FIELD_STAGGER=-1)
   char* field_raw(int f) const { return fields_ + size_t(f) * field_stride_; }
   void place_fields();                // placement probe (see gpu_solver.hip)
   template <typename T>

@@ -48,12 +48,6 @@ struct TileCfg {
   const Pcg1Slot* order0 = nullptr;
   const Pcg1Slot* order1 = nullptr;
   const Pcg1Slot* order2 = nullptr;  // the frame tiles
-  // kind 3 halo-row reuse: tiles with even ti march bottom-up (alt), and the order tables dispatch
-  // `super` vertically adjacent tiles (a super-row) back to back, column by column, so the pair
-  // across each inner boundary reads its shared halo rows at the same time (0 = row-major order)
-  int alt = 0;
-  int super = 0;
-  int bands = 1;  // order tables: sub-bands per XCD chunk dispatched round-robin (pcg1_build_order)
   int arith32 = 0;  // kind 3 with fp32 storage: 1 = fp32 stencil arithmetic (GpuOptions::arith32)
   int interior_tiles() const { return (ti_hi - ti_lo) * (tj_hi - tj_lo); }
   int ntiles() const { return tiles_i * tiles_j; }
