@@ -142,6 +142,10 @@ def parse(argv=None):
     ap.add_argument("--placement", type=int, default=8,
                     help="placement probe: candidate field blocks timed, the fastest kept (0 = off; "
                          "bounded by --placement-budget and --placement-keep-free; off when ranks share a GPU)")
+    ap.add_argument("--loopback-rank", type=int, default=-1,
+                    help="timing rehearsal on ONE GPU (valid=false): rank R of the --gpus-rank decomposition "
+                         "alone, ghosts served from its own rows by device copies, all-reduce skipped -- the "
+                         "real per-rank schedule (split sweep, frame stream, exchange copies) at full speed")
     ap.add_argument("--placement-budget", type=float, default=0.5, help="placement probe: seconds of probing")
     ap.add_argument("--placement-keep-free", type=float, default=0.5,
                     help="placement probe: fraction of the free device memory left free")
@@ -752,10 +756,69 @@ def measure(args) -> int:
     return 0
 
 
+def measure_loopback(args) -> int:
+    """One rank of the --gpus-rank job alone on this GPU (LoopbackComm): per-rank iteration time of
+    the real schedule.  Prints one JSON line (valid=false: not a multi-GPU measurement)."""
+    import importlib
+
+    import torch
+
+    pkg_name = "poisson-ellipse-openmp-mpi-cuda-new_amd"
+    pmx = importlib.import_module(pkg_name)
+    native = pmx.load_native()
+    if not torch.cuda.is_available():
+        raise SystemExit("--loopback-rank needs an MI355X")
+    if not 0 <= args.loopback_rank < args.gpus:
+        raise SystemExit("--loopback-rank must be in [0, --gpus)")
+    problem = pmx.PoissonEllipse(M=args.M, N=args.N, breakdown_tol=args.breakdown_tol)
+    s = native.Session(problem.to_native(), world=args.gpus, comm="loopback", split=getattr(native.Split, args.split),
+                       ranks=[args.loopback_rank], devices=[0], dtype=args.dtype, graph_batch=args.graph_batch,
+                       overlap=args.overlap == "on", placement=args.placement,
+                       placement_budget_s=args.placement_budget, placement_keep_free=args.placement_keep_free)
+    sd = s.subdomain(0)
+    s.init()
+    s.step(args.warmup)
+    s.synchronize()
+    prepared = s.prepare(args.steps)
+    st0 = s.state(0)
+    s.reset_path_stats()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    s.step(args.steps)
+    s.synchronize()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    st1 = s.state(0)
+    path = s.path_stats()
+    pts = sd["nx"] * sd["ny"]
+    tile = dict(s.tile)
+    tile.pop("placement_probe_ms", None)
+    out = {
+        "metric": "per-rank iteration time of one rank of a multi-GPU decomposition (loopback rehearsal)",
+        "value": round(dt / args.steps * 1e6, 2), "unit": "us/iteration", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": False,
+        "dtype": args.dtype,
+        "data": f"loopback: rank {args.loopback_rank} of {args.gpus} alone, ghosts from its own rows, no all-reduce",
+        "config": {"grid": [args.M, args.N], "world": args.gpus, "rank": args.loopback_rank, "split": args.split,
+                   "process_grid": list(s.grid), "subdomain": [sd["nx"], sd["ny"]], "comm": s.comm_name,
+                   "split_sweep": bool(s.split_sweep), "direct_rows": bool(s.direct_rows), "tile": tile,
+                   "graph_batch": args.graph_batch, "overlap": args.overlap},
+        "rank_mlups": round(pts * args.steps / dt / 1e6, 1),
+        "timed_path": "graph" if path["eager_iters"] == 0 else "mixed",
+        "graphs_prepared": bool(prepared),
+        "iterations_ran": int(st1["it"] - st0["it"]), "stopped": bool(st1["done"]),
+        "valid": False,
+    }
+    print(json.dumps(out), flush=True)
+    return 0
+
+
 def main():
     args = parse()
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
+    if args.loopback_rank >= 0:
+        sys.exit(measure_loopback(args))
     if os.environ.get("PMX_BENCH_ROLE") != "child" and args.gpus > 1:
         sys.exit(supervise(args))
     if os.environ.get("PMX_BENCH_ROLE") != "child" and int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:

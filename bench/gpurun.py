@@ -330,7 +330,25 @@ STUDIES["r4a"] = [
     ("bench_probe_r3", 300, bench("--gpus 1 --steps 20 --warmup 5 --placement 160 --placement-budget 60 "
                                   "--placement-keep-free 0.125 --no-tol-solve")),
     ("bench_noprobe", 300, bench("--gpus 1 --steps 20 --warmup 5 --placement 0 --no-tol-solve")),
-] + placement_pmc_steps("r4a")
+] + [
+    # per-rank cost of the 8-GPU iteration on one GPU (verdict r3 item 2): the middle strip of 8 and
+    # an interior 2x4 block, against the strip with no neighbours
+    ("loop_strip3", 200, bench("--gpus 8 --loopback-rank 3 --steps 300 --warmup 30")),
+    ("loop_strip3_packed", 200, "env PMX_DIRECT_ROWS=0 " + bench("--gpus 8 --loopback-rank 3 --steps 300 --warmup 30")),
+    ("loop_block5", 200, bench("--gpus 8 --loopback-rank 5 --split reference --steps 300 --warmup 30")),
+    ("strip_alone", 200, bench("--gpus 1 --M 2048 --N 16384 --steps 300 --warmup 30 --no-tol-solve")),
+    ("tl_strip3", 200, "rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/r4a/tl_strip3 "
+                       "-o run -- python3 bench.py --gpus 8 --loopback-rank 3 --steps 300 --warmup 30"),
+    ("tl_strip3_sum", 60, "python3 bench/loopback_timeline.py gpurun_out/r4a/tl_strip3"),
+    ("tl_block5", 200, "rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/r4a/tl_block5 "
+                       "-o run -- python3 bench.py --gpus 8 --loopback-rank 5 --split reference --steps 300 --warmup 30"),
+    ("tl_block5_sum", 60, "python3 bench/loopback_timeline.py gpurun_out/r4a/tl_block5"),
+    ("tl_alone", 200, "rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r4a/tl_alone -o run -- "
+                      "python3 bench.py --gpus 1 --M 2048 --N 16384 --steps 300 --warmup 30 --no-tol-solve"),
+    ("tl_alone_sum", 60, "python3 bench/loopback_timeline.py gpurun_out/r4a/tl_alone"),
+]
+
+STUDIES["r4p"] = placement_pmc_steps("r4p")
 
 PARAMETRISED = {"ab": _ab, "pmc": _pmc, "timeline": _timeline, "validate": _validate, "share": _share, "cli": _cli}
 

@@ -447,6 +447,7 @@ PYBIND11_MODULE(_pmx, m) {
              else if (comm == "local") c.comm = CommKind::kLocal;
              else if (comm == "rccl") c.comm = CommKind::kRccl;
              else if (comm == "ipc") c.comm = CommKind::kIpc;
+             else if (comm == "loopback") c.comm = CommKind::kLoopback;
              else PMX_CHECK(false, "unknown comm " << comm);
              if (!uid.is_none()) c.rccl_uid = uid.cast<std::string>();
              c.ranks = ranks;
@@ -530,6 +531,7 @@ PYBIND11_MODULE(_pmx, m) {
            })
       .def("reset_path_stats", &Session::reset_path_stats)
       .def_property_readonly("split_sweep", &Session::split_sweep)
+      .def_property_readonly("direct_rows", &Session::direct_rows)
       .def("progress", [](Session& s, int i) {
              long long v[3];
              s.progress(i, v);  // host memory only: callable while another thread blocks in the session

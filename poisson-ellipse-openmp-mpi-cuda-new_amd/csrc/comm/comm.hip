@@ -41,6 +41,17 @@ std::unique_ptr<Comm> Comm::rank_view(int) {
 
 namespace {
 
+// The neighbour's message that pairs with `m` (opposite slot, same field).
+const HaloMsg& partner(const HaloMsgs& theirs, const HaloMsg& m) {
+  for (int q = 0; q < theirs.n; ++q)
+    if (theirs.m[q].slot == opposite_slot(m.slot) && theirs.m[q].field == m.field) {
+      PMX_CHECK(theirs.m[q].count == m.count, "ghost message sizes disagree across slot " << m.slot);
+      return theirs.m[q];
+    }
+  PMX_CHECK(false, "no partner message for slot " << m.slot << " field " << m.field);
+  return theirs.m[0];
+}
+
 class SelfComm final : public Comm {
  public:
   void allreduce(std::vector<GpuSubdomainSolver*>&, int, std::vector<hipStream_t>&) override {}
@@ -76,16 +87,16 @@ class LocalComm final : public Comm {
   }
   void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>& streams) override {
     for (auto* s : local) {
-      const CommLayout& L = s->layout();
-      for (int slot = 0; slot < kHaloSlots; ++slot) {
-        if (!L.active(slot)) continue;
-        GpuSubdomainSolver* o = local[L.peer[slot]];
-        HIP_CHECK(hipMemcpyAsync(s->recv_dev(slot), o->send_dev(opposite_slot(slot)),
-                                 size_t(L.edge_len[slot]) * L.elem, hipMemcpyDeviceToDevice,
+      const HaloMsgs mine = s->halo_msgs();
+      for (int q = 0; q < mine.n; ++q) {
+        const HaloMsg& m = mine.m[q];
+        const HaloMsg& o = partner(local[m.peer]->halo_msgs(), m);
+        HIP_CHECK(hipMemcpyAsync(m.recv, o.send, size_t(m.count) * s->layout().elem, hipMemcpyDeviceToDevice,
                                  streams[0]));
       }
     }
   }
+  bool direct_rows() const override { return true; }
   std::string name() const override { return "local"; }
   int world_size() const override { return n_; }
 
@@ -111,16 +122,39 @@ void check_async(ncclComm_t c) {
     ::pmx::fail(__FILE__, __LINE__, std::string("RCCL asynchronous error: ") + ncclGetErrorString(async));
 }
 
-// The halo send/recv pairs of one rank (active slots, RcclComm::halo's order).
+// The halo send/recv pairs of one rank (GpuSubdomainSolver::halo_msgs order: by slot, then field;
+// a neighbour issues its partner messages in the same order, so RCCL pairs them per peer).
 void rccl_halo_calls(GpuSubdomainSolver* s, ncclComm_t comm, hipStream_t stream) {
-  const CommLayout& L = s->layout();
-  const ncclDataType_t t = L.elem == 8 ? ncclFloat64 : ncclFloat32;
-  for (int slot = 0; slot < kHaloSlots; ++slot) {
-    if (!L.active(slot)) continue;
-    RCCL_CHECK(ncclSend(s->send_dev(slot), L.edge_len[slot], t, L.peer[slot], comm, stream));
-    RCCL_CHECK(ncclRecv(s->recv_dev(slot), L.edge_len[slot], t, L.peer[slot], comm, stream));
+  const ncclDataType_t t = s->layout().elem == 8 ? ncclFloat64 : ncclFloat32;
+  const HaloMsgs ms = s->halo_msgs();
+  for (int q = 0; q < ms.n; ++q) {
+    const HaloMsg& m = ms.m[q];
+    RCCL_CHECK(ncclSend(m.send, size_t(m.count), t, m.peer, comm, stream));
+    RCCL_CHECK(ncclRecv(m.recv, size_t(m.count), t, m.peer, comm, stream));
   }
 }
+
+// See make_loopback_comm.
+class LoopbackComm final : public Comm {
+ public:
+  void allreduce(std::vector<GpuSubdomainSolver*>&, int, std::vector<hipStream_t>&) override {}
+  void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>& streams) override {
+    PMX_CHECK(local.size() == 1, "the loopback comm stands for one rank");
+    const HaloMsgs ms = local[0]->halo_msgs();
+    for (int q = 0; q < ms.n; ++q) {
+      const HaloMsg& m = ms.m[q];
+      const void* src = m.send;  // an edge rank's lone slot: its own send span
+      for (int o = 0; o < ms.n; ++o)
+        if (ms.m[o].slot == opposite_slot(m.slot) && ms.m[o].field == m.field) src = ms.m[o].send;
+      HIP_CHECK(hipMemcpyAsync(m.recv, src, size_t(m.count) * local[0]->layout().elem, hipMemcpyDeviceToDevice,
+                               streams[0]));
+    }
+  }
+  bool prefers_split() const override { return true; }  // as RCCL
+  bool direct_rows() const override { return true; }
+  std::string name() const override { return "loopback"; }
+  int world_size() const override { return 1; }
+};
 
 // One local rank of an RcclComm, driven by its own host thread: its collectives need no
 // ncclGroupStart/End across local ranks (RCCL matches them per communicator, whichever thread
@@ -148,6 +182,7 @@ class RcclRankView final : public Comm {
     RCCL_CHECK(ncclGroupEnd());
   }
   bool graph_capturable() const override { return capturable_; }
+  bool direct_rows() const override { return true; }
   void check_health() override {
     require_live(aborted_);
     check_async(comm_);
@@ -231,6 +266,7 @@ class RcclComm final : public Comm {
   }
 
   bool graph_capturable() const override { return capturable_; }
+  bool direct_rows() const override { return true; }
   std::unique_ptr<Comm> rank_view(int i) override {
     PMX_CHECK(i >= 0 && i < int(comms_.size()), "rank view index");
     return std::make_unique<RcclRankView>(comms_[size_t(i)], halo_comms_[size_t(i)], nranks_, capturable_, this,
@@ -264,17 +300,17 @@ class RecordingComm final : public Comm {
   }
   void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>& streams) override {
     PMX_CHECK(local.size() == 1, "a recording comm stands for one rank");
-    const CommLayout& L = local[0]->layout();
     const long long st = sid(streams);
     log_->push_back({halo_id_, "group_start", 0, -1, st});
-    for (int slot = 0; slot < kHaloSlots; ++slot) {  // the order RcclComm::halo issues them
-      if (!L.active(slot)) continue;
-      log_->push_back({halo_id_, "send", L.edge_len[slot], L.peer[slot], st});
-      log_->push_back({halo_id_, "recv", L.edge_len[slot], L.peer[slot], st});
+    const HaloMsgs ms = local[0]->halo_msgs();
+    for (int q = 0; q < ms.n; ++q) {  // the order RcclComm::halo issues them
+      log_->push_back({halo_id_, "send", ms.m[q].count, ms.m[q].peer, st});
+      log_->push_back({halo_id_, "recv", ms.m[q].count, ms.m[q].peer, st});
     }
     log_->push_back({halo_id_, "group_end", 0, -1, st});
   }
   bool prefers_split() const override { return true; }
+  bool direct_rows() const override { return true; }
   std::string name() const override { return "recording"; }
   int world_size() const override { return world_; }
 
@@ -290,6 +326,7 @@ class RecordingComm final : public Comm {
 }  // namespace
 
 std::unique_ptr<Comm> make_self_comm() { return std::make_unique<SelfComm>(); }
+std::unique_ptr<Comm> make_loopback_comm() { return std::make_unique<LoopbackComm>(); }
 
 std::unique_ptr<Comm> make_recording_comm(std::vector<CommEvent>* log, int world, bool split_halo) {
   return std::make_unique<RecordingComm>(log, world, split_halo);

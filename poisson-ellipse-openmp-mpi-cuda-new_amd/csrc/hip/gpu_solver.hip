@@ -554,13 +554,46 @@ void GpuSubdomainSolver::halo_impl(hipStream_t s, bool unpack) {
   after_launch(s);
 }
 
+void GpuSubdomainSolver::set_direct_rows(bool on) {
+  PMX_CHECK(!on || can_direct_rows(), "direct-row ghost exchange needs pcg1 on a row strip (x neighbours only)");
+  direct_rows_ = on;
+}
+
+HaloMsgs GpuSubdomainSolver::halo_msgs() const {
+  HaloMsgs out;
+  if (!direct_rows_) {  // the packed slot buffers of the comm arena
+    for (int slot = 0; slot < kHaloSlots; ++slot)
+      if (layout_.active(slot))
+        out.m[out.n++] = HaloMsg{slot, 0, layout_.peer[slot], layout_.edge_len[slot], send_dev(slot), recv_dev(slot)};
+    return out;
+  }
+  // sweep t reads r^{t-1} from (t & 1 ? r2 : r) and p^{t-1} from (t & 1 ? p0 : p1) (k_pcg1)
+  const long long t = halo_target_;
+  char* fr = (t & 1) ? r2_ + field_off_ * elem_ : static_cast<char*>(field_base(1));
+  char* fp = static_cast<char*>(field_base((t & 1) ? 2 : 3));
+  const int64_t P = geom_.pitch;
+  // rows q, q+1 as one span: row q whole (its padding ends with column -1 of row q+1) and row q+1's
+  // columns 0 .. ny+1; on a row strip the ghost columns are Dirichlet zeros on both sides
+  const int count = int(P + sd_.ny + 2);
+  for (int slot = 0; slot < 2; ++slot) {
+    if (layout_.peer[slot] < 0) continue;
+    const int64_t srow = slot == 0 ? 1 : sd_.nx - 1, rrow = slot == 0 ? -1 : sd_.nx + 1;
+    for (int f = 0; f < 2; ++f) {
+      char* base = f == 0 ? fr : fp;
+      out.m[out.n++] = HaloMsg{slot, f, layout_.peer[slot], count, base + srow * P * int64_t(elem_),
+                               base + rrow * P * int64_t(elem_)};
+    }
+  }
+  return out;
+}
+
 void GpuSubdomainSolver::enqueue_halo_pack(hipStream_t s) {
-  if (!pcg1_ || geom_.nb == 0) return;
+  if (!pcg1_ || geom_.nb == 0 || direct_rows_) return;
   if (opt_.dtype == DType::kFp64) halo_impl<double>(s, false); else halo_impl<float>(s, false);
 }
 
 void GpuSubdomainSolver::enqueue_halo_unpack(hipStream_t s) {
-  if (!pcg1_ || geom_.nb == 0) return;
+  if (!pcg1_ || geom_.nb == 0 || direct_rows_) return;
   if (opt_.dtype == DType::kFp64) halo_impl<double>(s, true); else halo_impl<float>(s, true);
 }
 
@@ -665,6 +698,12 @@ static void pack_impl(const GpuSubdomainSolver& g, HaloBufs<T> H, hipStream_t s)
 }
 
 void GpuSubdomainSolver::enqueue_poison_recv(hipStream_t s) {
+  if (direct_rows_) {  // the ghost rows the next exchange writes
+    const HaloMsgs ms = halo_msgs();
+    for (int q = 0; q < ms.n; ++q)
+      HIP_CHECK(hipMemsetAsync(ms.m[q].recv, 0xFF, size_t(ms.m[q].count) * elem_, s));
+    return;
+  }
   const size_t off = layout_.recv_off[0];
   HIP_CHECK(hipMemsetAsync(arena_ + off, 0xFF, layout_.bytes - off, s));  // all-ones = NaN
 }
@@ -888,6 +927,13 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
   for (auto* s : local_)
     PMX_CHECK(s->single_pass() == single_pass_, "local subdomains disagree on the iteration algorithm");
   overlap_ = any_nb && local_[0]->options().overlap;
+  // Direct-row ghost exchange (row strips): no pack/unpack launches; PMX_DIRECT_ROWS=0 turns it off
+  // (A/B).  Every local solver must qualify (they exchange with each other under LocalComm).
+  bool direct = single_pass_ && any_nb && comm_->direct_rows();
+  for (auto* s : local_) direct &= s->can_direct_rows();
+  if (const char* d = std::getenv("PMX_DIRECT_ROWS"); d && d[0] == '0') direct = false;
+  direct_ = direct;
+  for (auto* s : local_) s->set_direct_rows(direct_);
   // One hardware queue per process (GPU_MAX_HW_QUEUES=1): every stream lands on it, so forking the
   // halo / frame work onto side streams cannot overlap anything -- and ROCm 7.2 segfaults inside
   // hipGraphLaunch on a captured graph with forked branches in that configuration (traced with
@@ -979,13 +1025,13 @@ void PcgDriver::init() {
   if (single_pass_) {
     // ghosts of r^0 -> sweep 0 ((z^0, r^0), (A z^0, z^0); it 0 -> 1) -> all-reduce -> ghosts of
     // sweep 0's outputs, which sweep 1 reads
-    if (any_nb_) halo_exchange_pcg1(streams_);
+    if (any_nb_) halo_exchange_pcg1(streams_, local_[0]->host_k());
     for (size_t i = 0; i < local_.size(); ++i) {
       HIP_CHECK(hipSetDevice(local_[i]->device()));
       local_[i]->enqueue_phase_a(streams_[i]);
     }
     comm_->allreduce(local_, 2, streams_);
-    if (any_nb_) halo_exchange_pcg1(streams_);
+    if (any_nb_) halo_exchange_pcg1(streams_, local_[0]->host_k());
   } else {
     comm_->allreduce(local_, 1, streams_);
     poison(streams_);
@@ -1002,7 +1048,12 @@ void PcgDriver::poison(std::vector<hipStream_t>& streams) {
   }
 }
 
-void PcgDriver::halo_exchange_pcg1(std::vector<hipStream_t>& streams) {
+void PcgDriver::set_halo_target(long long k) {
+  for (auto* s : local_) s->set_halo_target(k);
+}
+
+void PcgDriver::halo_exchange_pcg1(std::vector<hipStream_t>& streams, long long target) {
+  set_halo_target(target);
   comm_->before_pack(local_, streams);
   for (size_t i = 0; i < local_.size(); ++i) {
     HIP_CHECK(hipSetDevice(local_[i]->device()));
@@ -1047,6 +1098,7 @@ void PcgDriver::enqueue_split_iteration() {
     local_[i]->enqueue_halo_pack(comm_streams_[i]);
   }
   for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipEventRecord(ev_pk_[u], comm_streams_[i])); });
+  set_halo_target(local_[0]->host_k() + 1);  // the sweep just enqueued is host_k; the next reads its outputs
   poison(comm_streams_);
   comm_->halo(local_, comm_streams_);
   for (size_t i = 0; i < local_.size(); ++i) {
@@ -1086,7 +1138,7 @@ void PcgDriver::enqueue_one_iteration() {
         local_[i]->enqueue_phase_a(streams_[i]);
       }
       comm_->allreduce(local_, 2, streams_);  // no-op for SelfComm
-      if (any_nb_) halo_exchange_pcg1(streams_);
+      if (any_nb_) halo_exchange_pcg1(streams_, local_[0]->host_k());  // the reduction bumped host_k
       return;
     }
     for (size_t i = 0; i < local_.size(); ++i) {
@@ -1097,7 +1149,7 @@ void PcgDriver::enqueue_one_iteration() {
       HIP_CHECK(hipEventRecord(ev_packed_[u], streams_[i]));
       HIP_CHECK(hipStreamWaitEvent(comm_streams_[i], ev_packed_[u], 0));
     });
-    halo_exchange_pcg1(comm_streams_);
+    halo_exchange_pcg1(comm_streams_, local_[0]->host_k() + 1);  // before the reduction's bump
     for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipEventRecord(ev_halo_[u], comm_streams_[i])); });
     for (size_t i = 0; i < local_.size(); ++i) {
       HIP_CHECK(hipSetDevice(local_[i]->device()));
@@ -1261,7 +1313,7 @@ void PcgDriver::note_graph(int len) {
 
 bool PcgDriver::prepare(int64_t n) {
   TraceRange tr("pmx:prepare");
-  const int cyc = local_[0]->w_cycle();
+  const int cyc = graph_period();
   std::vector<long long> k0;
   for (auto* s : local_) k0.push_back(s->host_k());
   bool ok = graph_batch_ > 0 && !graph_failed_;
@@ -1290,7 +1342,7 @@ void PcgDriver::enqueue_eager(int64_t n) {
 
 void PcgDriver::enqueue_iterations(int64_t n) {
   TraceRange tr("pmx:enqueue_iterations");
-  const int cyc = local_[0]->w_cycle();
+  const int cyc = graph_period();
   for (auto* s : local_) PMX_CHECK(s->host_k() == local_[0]->host_k(), "local solvers out of step");
   int64_t done = 0;
   while (done < n) {
@@ -1390,7 +1442,7 @@ RunStats PcgDriver::profile_phases(int64_t n) {
     }
     HIP_CHECK(hipEventRecord(e[5], s0));
     if (single_pass_) {
-      if (any_nb_) halo_exchange_pcg1(streams_);
+      if (any_nb_) halo_exchange_pcg1(streams_, local_[0]->host_k());
     } else {
       comm_->halo(local_, streams_);
     }

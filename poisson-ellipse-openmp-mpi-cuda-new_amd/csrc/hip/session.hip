@@ -32,6 +32,8 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
     PMX_CHECK(int(cfg_.ranks.size()) == cfg_.world, "local comm owns every rank");
   if (cfg_.comm == CommKind::kIpc)
     PMX_CHECK(cfg_.ranks.size() == 1, "the IPC transport runs one rank per process");
+  if (cfg_.comm == CommKind::kLoopback)
+    PMX_CHECK(cfg_.ranks.size() == 1, "loopback runs exactly one rank of the decomposition");
 
   // one iteration algorithm for every subdomain (and every process: the choice only depends on
   // global data, see choose_single_pass)
@@ -74,6 +76,7 @@ void Session::connect() {
       ipc_attach(comm_.get(), cfg_.ipc_exports);
       break;
     case CommKind::kSelf: comm_ = make_self_comm(); break;
+    case CommKind::kLoopback: comm_ = make_loopback_comm(); break;
     case CommKind::kLocal: comm_ = make_local_comm(raw); break;
     case CommKind::kRccl:
       // overlap off = the serialized schedule: one communicator, every call on the compute stream
@@ -172,6 +175,11 @@ void Session::reset_path_stats() {
 bool Session::split_sweep() const {
   require_connected();
   return drivers_[0]->split_sweep();
+}
+
+bool Session::direct_rows() const {
+  require_connected();
+  return drivers_[0]->direct_rows();
 }
 
 void Session::progress(int i, long long out[3]) const { solvers_.at(size_t(i))->progress(out); }

@@ -130,6 +130,20 @@ struct ErrorStats {
   double max_w = 0.0;   // max w over the owned nodes
 };
 
+// One ghost message of a rank: `count` elements from `send` go to the neighbour across `slot`
+// (rank `peer`), and `count` elements from that neighbour land at `recv`.  `field` orders the
+// messages of one slot (0 = r, 1 = p in the direct-row exchange; 0 for packed slots): the
+// neighbour's message with slot opposite_slot(slot) and the same field is the partner.
+struct HaloMsg {
+  int slot, field, peer, count;
+  void* send;
+  void* recv;
+};
+struct HaloMsgs {
+  HaloMsg m[2 * kHaloSlots];
+  int n = 0;
+};
+
 struct CommLayout {
   size_t state_off = 0;          // PcgState
   size_t send_off[kHaloSlots] = {};
@@ -178,6 +192,23 @@ class GpuSubdomainSolver {
   void enqueue_halo_pack(hipStream_t s);
   void enqueue_halo_unpack(hipStream_t s);
   void enqueue_poison_recv(hipStream_t s);  // recv buffers <- NaN (poison_halos debug mode)
+
+  // Direct-row ghost exchange (pcg1 on row strips: x neighbours only, no y / corner neighbours).
+  // The two owned edge rows of r^k and p^k are sent straight from the fields and received straight
+  // into the two ghost rows of the buffers sweep k+1 reads: no pack / unpack kernels, no slot
+  // buffers (a row span, padding included, is contiguous).  The driver turns it on when its
+  // communicator moves arbitrary device spans (Comm::direct_rows).
+  bool can_direct_rows() const {
+    return pcg1_ && (geom_.nb & ~(kNbXlo | kNbXhi)) == 0 && sd_.nx >= 2;
+  }
+  void set_direct_rows(bool on);
+  bool direct_rows() const { return direct_rows_; }
+  // pcg1: the next Comm::halo call fills the inputs of sweep k (r^{k-1}, p^{k-1}); the driver sets
+  // it before every exchange (the direct-row spans alternate between the double buffers)
+  void set_halo_target(long long k) { halo_target_ = k; }
+  long long halo_target() const { return halo_target_; }
+  // this rank's messages of the next exchange, in the order every transport issues them
+  HaloMsgs halo_msgs() const;
 
   // Checkpoint: the 4 fields with ghosts, the PCG scalars and the halo buffers,
   // i.e. everything the next iteration reads.  Synchronous; written at batch boundaries.
@@ -261,6 +292,8 @@ class GpuSubdomainSolver {
   const TileCfg& tiles1_for(bool wsweep) const { return wsweep ? tiles1w_ : tiles1_; }
   bool pcg1_ = false;
   long long host_k_ = 0;
+  bool direct_rows_ = false;
+  long long halo_target_ = 0;
   TileCfg init_tiles_{};
   CommLayout layout_{};
   size_t elem_ = 8, field_bytes_ = 0, field_off_ = 0;
@@ -314,6 +347,9 @@ class Comm {
   // Called before every kernel that writes this rank's send slots (the next exchange's pack): a
   // transport whose peers read those slots in place (IpcComm) waits here until they have.
   virtual void before_pack(std::vector<GpuSubdomainSolver*>&, std::vector<hipStream_t>&) {}
+  // The transport moves any device span a rank's halo_msgs() names (not only its packed slot
+  // buffers), so the driver may use the direct-row exchange (GpuSubdomainSolver::set_direct_rows).
+  virtual bool direct_rows() const { return false; }
   // The pcg1 split sweep is the default with this transport (its exchange is the long pole).
   virtual bool prefers_split() const { return false; }
   // Error path of a threaded driver set: make every operation in flight or blocked on this
@@ -326,6 +362,12 @@ class Comm {
 };
 
 std::unique_ptr<Comm> make_self_comm();
+// bench.py --loopback-rank: ONE rank of a P-rank decomposition alone on this device.  Every ghost
+// message is served from the rank's own data (recv of slot s <- its own send of the opposite slot,
+// or of s itself on an edge rank: a device copy of the real size on the exchange's stream), and the
+// all-reduce is skipped: the real per-rank schedule (split sweep, frame stream, events, copies) runs
+// at full speed as a timing rehearsal; the numbers it computes are meaningless.
+std::unique_ptr<Comm> make_loopback_comm();
 std::unique_ptr<Comm> make_local_comm(std::vector<GpuSubdomainSolver*>& local);
 // RCCL: one communicator per local solver.  `unique_id` is the 128-byte ncclUniqueId,
 // `ranks` the global ranks of the local solvers, `nranks` the world size.  `split_halo`: a second
@@ -401,6 +443,7 @@ class PcgDriver {
   bool poisoned() const { return poison_; }
   // pcg1 split sweep in use (interior tiles overlap the previous exchange, see enqueue_split_iteration)
   bool split_sweep() const { return split_; }
+  bool direct_rows() const { return direct_; }
 
   // Which path ran: iterations replayed from captured graphs / enqueued as individual launches
   // since the last reset, and the graph lengths used (bench.py reports them for its timed region).
@@ -420,7 +463,12 @@ class PcgDriver {
 
  private:
   void enqueue_one_iteration();
-  void halo_exchange_pcg1(std::vector<hipStream_t>& streams);  // pack -> comm -> unpack
+  // pack -> comm -> unpack, filling the inputs of sweep `target` (direct rows: comm only)
+  void halo_exchange_pcg1(std::vector<hipStream_t>& streams, long long target);
+  void set_halo_target(long long k);
+  // captured batches depend on the w-cycle phase of their first sweep, and with direct rows also on
+  // its parity (the exchanged spans alternate between the double buffers)
+  int graph_period() const { return local_[0]->w_cycle() * (direct_ ? 2 : 1); }
   void enqueue_split_iteration();  // pcg1, decomposed, overlap: interior/frame sweep split
   void join_halo();                // compute stream waits for a pending ghost exchange
   // captured batch of `len` iterations starting at w-cycle phase `phase`, built on first use;
@@ -439,6 +487,7 @@ class PcgDriver {
   bool poison_ = false;
   bool single_pass_ = false;
   bool any_nb_ = false;
+  bool direct_ = false;  // direct-row ghost exchange (GpuSubdomainSolver::set_direct_rows)
   std::vector<hipStream_t> comm_streams_;
   std::vector<hipEvent_t> ev_packed_, ev_halo_;
   // split sweep (pcg1 with neighbours and overlap): the frame tiles run on their own stream

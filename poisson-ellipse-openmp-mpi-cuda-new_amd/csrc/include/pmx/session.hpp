@@ -11,7 +11,7 @@
 
 namespace pmx {
 
-enum class CommKind : int { kSelf = 0, kLocal = 1, kRccl = 2, kIpc = 3 };
+enum class CommKind : int { kSelf = 0, kLocal = 1, kRccl = 2, kIpc = 3, kLoopback = 4 };
 
 struct SessionConfig {
   ProblemSpec spec;
@@ -70,6 +70,7 @@ class Session {
   PcgDriver::PathStats path_stats() const;
   void reset_path_stats();
   bool split_sweep() const;
+  bool direct_rows() const;
   // host-mapped device progress of owned rank i (GpuSubdomainSolver::progress); no HIP call
   void progress(int i, long long out[3]) const;
   // error vs the analytic solution over the owned subdomains (sum of e^2, max |e|, max w)

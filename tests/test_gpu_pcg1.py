@@ -258,3 +258,58 @@ def test_pcg1_dispatch_order_bitwise(pkg, monkeypatch, ranks, dtype):
     if dtype == "fp64":
         assert out["1"].iters == 989
     assert np.array_equal(out["0"].w, out["1"].w)
+
+
+@pytest.mark.parametrize("ranks,grid", [(2, (400, 600)), (3, (211, 157)), (5, (400, 600))])
+@pytest.mark.parametrize("graph_batch,overlap,split_sweep", [(0, False, "0"), (16, True, "0"), (16, True, "1"),
+                                                             (0, True, "1")])
+def test_direct_row_exchange_bitwise(pkg, monkeypatch, ranks, grid, graph_batch, overlap, split_sweep):
+    """Row strips exchange their two edge rows of r and p straight between the fields (no pack /
+    unpack kernels; the spans alternate with the double buffers, so graphs are keyed by parity too).
+    Bitwise the packed exchange's result, with every schedule (serial, overlapped, split sweep;
+    eager and graph-replayed); 2-D blocks keep the packed exchange."""
+    from conftest import sub
+    p = pkg.PoissonEllipse(M=grid[0], N=grid[1])
+    monkeypatch.setenv("PMX_PCG1_SPLIT", split_sweep)
+    out = {}
+    for direct in ("1", "0"):
+        monkeypatch.setenv("PMX_DIRECT_ROWS", direct)
+        s = sub("models").make_session(p, ranks=ranks, split="rows", graph_batch=graph_batch, overlap=overlap)
+        assert s.direct_rows == (direct == "1")
+        st = s.solve(1)
+        out[direct] = (st["iters"], s.gather_local_w())
+    assert out["1"][0] == out["0"][0]
+    assert np.array_equal(out["1"][1], out["0"][1])
+    monkeypatch.delenv("PMX_DIRECT_ROWS")
+    assert not sub("models").make_session(p, ranks=4, split="reference").direct_rows  # 2 x 2 blocks
+
+
+def test_direct_rows_poisoned_ghosts(pkg, monkeypatch):
+    """PMX_POISON_HALOS NaN-fills the ghost rows the direct exchange writes before every exchange:
+    a complete exchange leaves no trace (same iterations, no NaN flag)."""
+    p = pkg.PoissonEllipse(M=400, N=600)
+    ref = pkg.solve(p, "hip", ranks=3, split="rows")
+    monkeypatch.setenv("PMX_POISON_HALOS", "1")
+    r = pkg.solve(p, "hip", ranks=3, split="rows")
+    assert r.iters == ref.iters == 546 and not r.extra["nan"]
+    assert np.array_equal(r.w, ref.w)
+
+
+@pytest.mark.parametrize("rank,split", [(3, "rows"), (0, "rows"), (5, "reference")])
+def test_loopback_rank_runs_the_real_schedule(pkg, native, rank, split):
+    """bench.py --loopback-rank: one rank of an 8-rank decomposition alone on the GPU, ghosts served
+    from its own rows (device copies of the real sizes), all-reduce skipped: split sweep, frame
+    stream and graphs run as in the 8-GPU job."""
+    p = pkg.PoissonEllipse(M=2048, N=2048)
+    s = native.Session(p.to_native(), world=8, comm="loopback", split=getattr(native.Split, split), ranks=[rank],
+                       devices=[0], graph_batch=16)
+    assert s.comm_name == "loopback" and s.split_sweep
+    assert s.direct_rows == (split == "rows")
+    s.init()
+    it0 = s.state(0)["it"]
+    s.prepare(48)
+    s.reset_path_stats()
+    s.step(48)
+    s.synchronize()
+    st = s.state(0)
+    assert s.path_stats()["graph_iters"] == 48 and st["it"] - it0 == 48 and not st["done"]
