@@ -142,6 +142,9 @@ def parse(argv=None):
     ap.add_argument("--placement", type=int, default=8,
                     help="placement probe: candidate field blocks timed, the fastest kept (0 = off; "
                          "bounded by --placement-budget and --placement-keep-free; off when ranks share a GPU)")
+    ap.add_argument("--persistent", default="auto", choices=["auto", "on", "off"],
+                    help="persistent iteration (one launch per batch, in-kernel grid barrier + reduction): auto = "
+                         "fp64 single-subdomain grids whose fields fit the Infinity Cache (<= 192 MB)")
     ap.add_argument("--loopback-rank", type=int, default=-1,
                     help="timing rehearsal on ONE GPU (valid=false): rank R of the --gpus-rank decomposition "
                          "alone, ghosts served from its own rows by device copies, all-reduce skipped -- the "
@@ -562,6 +565,7 @@ def measure(args) -> int:
               waves=args.waves, tile_rows=args.tile_rows, exact=args.exact, graph_batch=args.graph_batch,
               overlap=overlap, vec_b=args.vec_b, tile_rows_b=args.tile_rows_b,
               b_ring=args.b_kernel == "ring")
+    persistent = {"auto": -1, "on": 1, "off": 0}[args.persistent]
     pkw = dict(placement=0 if share else args.placement, placement_budget_s=args.placement_budget,
                placement_keep_free=args.placement_keep_free)
     dkw = dict(kw, **pkw, phase=watch.phase, init_timeout=COMM_INIT_TIMEOUT)
@@ -574,8 +578,8 @@ def measure(args) -> int:
         comm_used = "gloo" if world > 1 else "self"
     elif world == 1:
         models = importlib.import_module(pkg_name + ".models")
-        runner = ds.SessionRunner(models.make_session(problem, ranks=1, device=info.local_rank, **pkw, **kw),
-                                  problem, info)
+        runner = ds.SessionRunner(models.make_session(problem, ranks=1, device=info.local_rank, persistent=persistent,
+                                                      **pkw, **kw), problem, info)
         comm_used = "self"
     elif share and cfg["comm"] == "ipc":
         runner = ds.DistGpuPCG(problem, info, comm="ipc", device=0, **dkw)
@@ -639,8 +643,10 @@ def measure(args) -> int:
         t = torch.tensor([dt], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    timed_path = ("graph" if path["eager_iters"] == 0 and path["graph_iters"] > 0 else
-                  "eager" if path["graph_iters"] == 0 else "mixed")
+    pers = path.get("persistent_iters", 0)
+    timed_path = ("persistent" if pers > 0 and path["eager_iters"] == 0 and path["graph_iters"] == 0 else
+                  "graph" if path["eager_iters"] == 0 and path["graph_iters"] > 0 and pers == 0 else
+                  "eager" if path["graph_iters"] == 0 and pers == 0 else "mixed")
     tile_desc = dict(runner.tile())
     tile_desc.pop("placement_probe_ms", None)  # the summary ("placement") stays; the list can be long
     valid = (not st1["done"]) and (st1["it"] - st0["it"] == args.steps) and not st1["nan"]
@@ -736,6 +742,7 @@ def measure(args) -> int:
             "timed_graph_lengths": path.get("graph_lengths", []),
             "timed_graph_iters": path["graph_iters"],
             "timed_eager_iters": path["eager_iters"],
+            "timed_persistent_iters": pers,
             "graphs_prepared": bool(prepared),
             "valid": valid and not share,
             "baseline_mlups": BASELINE_MLUPS,

@@ -181,8 +181,9 @@ GpuOptions make_options(int device, const std::string& kernel, int block, int ve
                         int tile_rows, const std::string& dtype, bool exact, int graph_batch, bool check,
                         bool overlap = true, int vec_b = 0, int waves_b = 0, int tile_rows_b = -1,
                         bool poison_halos = false, bool b_ring = false, int algo = -1, int placement = 0,
-                        double placement_budget_s = 0.5, double placement_keep_free = 0.5) {
+                        double placement_budget_s = 0.5, double placement_keep_free = 0.5, int persistent = -1) {
   GpuOptions o;
+  o.persistent = persistent;
   o.placement = placement;
   o.placement_budget_s = placement_budget_s;
   o.placement_keep_free = placement_keep_free;
@@ -432,13 +433,14 @@ PYBIND11_MODULE(_pmx, m) {
                        bool check, py::object uid, std::vector<int> ranks, std::vector<int> devices,
                        bool rccl_graph, bool overlap, int vec_b, int waves_b, int tile_rows_b,
                        bool poison_halos, bool b_ring, int algo, bool defer_connect, int threaded,
-                       int placement, double placement_budget_s, double placement_keep_free, int sharing) {
+                       int placement, double placement_budget_s, double placement_keep_free, int sharing,
+                       int persistent) {
              SessionConfig c;
              c.sharing = sharing;
              c.spec = s;
              c.opt = make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact,
                                   graph_batch, check, overlap, vec_b, waves_b, tile_rows_b, poison_halos,
-                                  b_ring, algo, placement, placement_budget_s, placement_keep_free);
+                                  b_ring, algo, placement, placement_budget_s, placement_keep_free, persistent);
              c.defer_connect = defer_connect;
              c.threaded = threaded;
              c.split = split;
@@ -466,7 +468,7 @@ PYBIND11_MODULE(_pmx, m) {
            py::arg("waves_b") = 0, py::arg("tile_rows_b") = -1, py::arg("poison_halos") = false,
            py::arg("b_ring") = false, py::arg("algo") = -1, py::arg("defer_connect") = false,
            py::arg("threaded") = -1, py::arg("placement") = 0, py::arg("placement_budget_s") = 0.5,
-           py::arg("placement_keep_free") = 0.5, py::arg("sharing") = 0)
+           py::arg("placement_keep_free") = 0.5, py::arg("sharing") = 0, py::arg("persistent") = -1)
       .def("ipc_export", [](Session& s) { return py::bytes(s.ipc_export()); },
            "IPC session: this rank's memory handles (pass every rank's to connect_ipc)")
       .def("connect_ipc", [](Session& s, std::vector<py::bytes> ex) {
@@ -526,12 +528,14 @@ PYBIND11_MODULE(_pmx, m) {
              py::dict d;
              d["graph_iters"] = p.graph_iters;
              d["eager_iters"] = p.eager_iters;
+             d["persistent_iters"] = p.persistent_iters;
              d["graph_lengths"] = p.graph_lengths;
              return d;
            })
       .def("reset_path_stats", &Session::reset_path_stats)
       .def_property_readonly("split_sweep", &Session::split_sweep)
       .def_property_readonly("direct_rows", &Session::direct_rows)
+      .def_property_readonly("persistent", &Session::persistent)
       .def("progress", [](Session& s, int i) {
              long long v[3];
              s.progress(i, v);  // host memory only: callable while another thread blocks in the session
@@ -572,6 +576,12 @@ PYBIND11_MODULE(_pmx, m) {
         py::dict d = one(s.solver(0).tiles());
         if (!s.solver(0).single_pass()) d["b"] = one(s.solver(0).tiles_b());
         d["algo"] = s.solver(0).single_pass() ? "pcg1" : "pcg2";
+        if (s.solver(0).persistent()) {
+          py::dict pd = one(s.solver(0).tiles_persistent());
+          pd["workgroups"] = s.solver(0).persistent_workgroups();
+          pd["threads"] = kPersistThreads;
+          d["persistent"] = pd;
+        }
         if (!s.solver(0).placement_ms().empty()) {
           // 3 plain sweeps per candidate field block (rotating field roles), the fastest kept
           std::vector<float> v = s.solver(0).placement_ms();

@@ -21,6 +21,26 @@
 // check_health() throws, so a dead peer cannot hang the GPU.  Remote data is read with
 // non-temporal loads after the acquire (no stale cache line of an earlier epoch is reused).
 // Graph-capturable: every operation is a kernel with fixed arguments, epochs live on the device.
+//
+// Memory model across devices (peers on other GPUs over xGMI, or processes sharing one GPU):
+//  * Flags (IpcBlock) live in UNCACHED device memory (hipExtMallocWithFlags(hipDeviceMallocUncached),
+//    MTYPE UC): every load and store of a flag goes to the owning device's memory, whichever GPU
+//    issues it, so a spinning peer never polls a line cached in its own (per-XCD, non-coherent) L2
+//    and a flag store is visible to every device once it completes.  Coarse-grained hipMalloc
+//    memory would only be coherent where the caches happen to be written back / invalidated;
+//    PMX_IPC_COARSE=1 restores it (A/B).
+//  * Payload (the send slots of the comm arena, coarse-grained, read by peers in place): written by
+//    the pack kernel with plain stores.  Every kernel boundary writes the XCD L2s back (gfx950:
+//    the per-XCD L2s are not coherent, so the end-of-kernel release covers all of them), and
+//    k_ipc_post -- a later kernel in stream order -- raises the flag with a system-scope release
+//    (buffer_wbl2 sc0 sc1 + the store): when a peer sees the flag, the payload is in memory.
+//  * The reader acquires at system scope (ld_acq: the load plus buffer_inv sc0 sc1 -- its L1 and its
+//    L2's lines of non-local memory are invalidated) and then reads the payload with non-temporal
+//    loads: no line of an earlier epoch can be served from its caches.
+//  * Reuse: a rank packs exchange e only after every neighbour acknowledged e-1 (k_ipc_wait_acks),
+//    so a payload is never overwritten while a peer may still read it.
+//  * Same-GPU ranks (the one-GPU box) take the same path; there the peer is the same L2 hierarchy
+//    and the uncached flags only cost a few hundred ns per poll.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -161,7 +181,11 @@ class IpcComm final : public Comm {
   IpcComm(GpuSubdomainSolver* local, int world) : local_(local), world_(world) {
     PMX_CHECK(world >= 1 && world <= kMaxIpcRanks, "IpcComm supports 1.." << kMaxIpcRanks << " ranks");
     HIP_CHECK(hipSetDevice(local->device()));
-    HIP_CHECK(hipMalloc(&block_, sizeof(IpcBlock)));
+    const char* coarse = std::getenv("PMX_IPC_COARSE");
+    if (coarse && coarse[0] == '1')
+      HIP_CHECK(hipMalloc(&block_, sizeof(IpcBlock)));
+    else  // flags every device reads and writes coherently (see the memory-model notes above)
+      HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&block_), sizeof(IpcBlock), hipDeviceMallocUncached));
     HIP_CHECK(hipMemset(block_, 0, sizeof(IpcBlock)));
     const char* t = std::getenv("PMX_IPC_TIMEOUT_MS");
     timeout_ = (t && t[0] ? std::atoll(t) : 20000LL) * 100000LL;  // wall_clock64: 100 MHz

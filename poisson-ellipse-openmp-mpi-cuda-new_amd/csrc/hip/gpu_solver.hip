@@ -101,6 +101,7 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_PROGRESS", o.progress);
   env_int("PMX_ARITH32", o.arith32);
   env_int("PMX_PLACEMENT", o.placement);
+  env_int("PMX_PERSISTENT", o.persistent);
   PMX_CHECK(o.wcycle1 == 2 || o.wcycle1 == 3, "pcg1 w cycle must be 2 or 3");
   PMX_CHECK(o.pair_w >= 0 && o.pair_w <= 2, "pair_w must be 0, 1 or 2");
   PMX_CHECK(o.algo == -1 || o.algo == 1 || o.algo == 2, "algo must be -1, 1 or 2");
@@ -264,6 +265,24 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
       HIP_CHECK(hipMalloc(&tile_order_w_, 3 * size_t(tiles1w_.ntiles()) * sizeof(Pcg1Slot)));
       (void)pcg1_build_order(G, tables_, tiles1w_, tile_order_w_, opt_.order1 != 0, nullptr);
     }
+  }
+
+  if (pcg1_) {
+    // persistent iteration: latency-bound grids whose fields sit in the 256 MB Infinity Cache
+    const bool eligible = G.nb == 0 && elem_ == 8 && !opt.check;
+    PMX_CHECK(opt_.persistent != 1 || eligible, "the persistent iteration needs fp64 and an undecomposed grid");
+    persist_ = eligible && (opt_.persistent == 1 || (opt_.persistent == -1 && 5.0 * double(field_bytes_) <= 192e6));
+  }
+  if (persist_) {
+    pwg_ = pcg1_persist_max_wg(opt.device);
+    // one tile per wave: rows so that the tile count matches the resident waves
+    const int waves = pwg_ * (kPersistThreads / 64), tj = (sd.ny + 123) / 124;
+    const int want_rows = std::max(1, (waves + tj - 1) / tj);
+    const int ti = opt_.rows1 ? opt_.rows1 : std::max(2, (sd.nx + want_rows - 1) / want_rows);
+    tilesP_ = make_pcg1_tiles(G, 2, 1, ti, opt_.pf1 ? opt_.pf1 : 1, int(elem_));
+    HIP_CHECK(hipMalloc(&tile_order_p_, 3 * size_t(tilesP_.ntiles()) * sizeof(Pcg1Slot)));
+    (void)pcg1_build_order(G, tables_, tilesP_, tile_order_p_, true, nullptr);
+    HIP_CHECK(hipMalloc(&pws_, sizeof(PersistWs)));
   }
 
   init_tiles_ = make_tiles(G, 256, 0);
@@ -439,6 +458,10 @@ void GpuSubdomainSolver::release() noexcept {
   if (fields_) (void)hipFree(fields_);
   if (tile_order_) (void)hipFree(tile_order_);
   if (tile_order_w_) (void)hipFree(tile_order_w_);
+  if (tile_order_p_) (void)hipFree(tile_order_p_);
+  if (pws_) (void)hipFree(pws_);
+  tile_order_p_ = nullptr;
+  pws_ = nullptr;
   if (tables_buf_) (void)hipFree(tables_buf_);
   if (partials_) (void)hipFree(partials_);
   if (own_arena_ && arena_) (void)hipFree(arena_);
@@ -551,6 +574,20 @@ void GpuSubdomainSolver::halo_impl(hipStream_t s, bool unpack) {
   launch_pcg1_halo<T>(geom_, static_cast<T*>(field_base(1)), reinterpret_cast<T*>(r2_ + field_off_ * elem_),
                       static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(), state_,
                       unpack, s, progress_dev_);
+  after_launch(s);
+}
+
+void GpuSubdomainSolver::enqueue_persistent(hipStream_t s, long long n) {
+  PMX_CHECK(persist_, "persistent iteration not set up for this solver");
+  if (n <= 0) return;
+  HIP_CHECK(hipSetDevice(opt_.device));
+  const double h = g_.h1h2, wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
+  const double wts[5] = {h, h, h, h, wdiff};
+  launch_pcg1_persist<double>(geom_, tables_, static_cast<double*>(field_base(0)), static_cast<double*>(field_base(1)),
+                              reinterpret_cast<double*>(r2_ + field_off_ * elem_), static_cast<double*>(field_base(2)),
+                              static_cast<double*>(field_base(3)), state_, pws_, tilesP_, pwg_, host_k_ + n - 1, wts,
+                              s);
+  host_k_ += n;  // as n reductions would (the device stops early on its own)
   after_launch(s);
 }
 
@@ -934,6 +971,8 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
   if (const char* d = std::getenv("PMX_DIRECT_ROWS"); d && d[0] == '0') direct = false;
   direct_ = direct;
   for (auto* s : local_) s->set_direct_rows(direct_);
+  // graph_batch 0 asks for individual launches: the persistent path replaces the graph replays only
+  persistent_ = graph_batch_ > 0 && local_.size() == 1 && !any_nb && local_[0]->persistent();
   // One hardware queue per process (GPU_MAX_HW_QUEUES=1): every stream lands on it, so forking the
   // halo / frame work onto side streams cannot overlap anything -- and ROCm 7.2 segfaults inside
   // hipGraphLaunch on a captured graph with forked branches in that configuration (traced with
@@ -1313,6 +1352,7 @@ void PcgDriver::note_graph(int len) {
 
 bool PcgDriver::prepare(int64_t n) {
   TraceRange tr("pmx:prepare");
+  if (persistent_) return true;  // nothing to capture: one launch per batch
   const int cyc = graph_period();
   std::vector<long long> k0;
   for (auto* s : local_) k0.push_back(s->host_k());
@@ -1342,6 +1382,12 @@ void PcgDriver::enqueue_eager(int64_t n) {
 
 void PcgDriver::enqueue_iterations(int64_t n) {
   TraceRange tr("pmx:enqueue_iterations");
+  if (persistent_) {
+    HIP_CHECK(hipSetDevice(local_[0]->device()));
+    local_[0]->enqueue_persistent(streams_[0], n);
+    path_.persistent_iters += n;
+    return;
+  }
   const int cyc = graph_period();
   for (auto* s : local_) PMX_CHECK(s->host_k() == local_[0]->host_k(), "local solvers out of step");
   int64_t done = 0;
@@ -1375,7 +1421,8 @@ RunStats PcgDriver::solve(int poll_batches, bool do_init, int64_t ckpt_every,
   if (do_init) init();
   const double t1 = now_s();
   st.init_seconds = t1 - t0;
-  const int64_t batch = std::max(1, graph_batch_ > 0 ? graph_batch_ : 16) * std::max(1, poll_batches);
+  // persistent: the device stops on its own inside a launch, so long launches cost nothing extra
+  const int64_t batch = std::max(1, persistent_ ? 512 : graph_batch_ > 0 ? graph_batch_ : 16) * std::max(1, poll_batches);
   const int64_t max_iter = local_[0]->spec().effective_max_iter();
   PcgState s = state(0);
   int64_t last_ckpt = s.it;

@@ -150,6 +150,26 @@ void launch_reduce(const double* partials, int n, int nq, double w0, double w1, 
 void launch_reduce_n(const double* partials, int n, int nq, const double* weights, double* out,
                      PcgState* S, int mode, double* ws, hipStream_t s, long long* progress = nullptr);
 
+// Persistent single-pass iteration (pcg1_persist.hip): nwg workgroups of kPersistThreads stay
+// resident and run sweeps host_k .. k_end with an in-kernel grid barrier and reduction, leaving
+// PcgState exactly as the launch-per-sweep path would (undecomposed grids; see the file header).
+// `ws` holds the polled words (the first kPersistPolled bytes, zeroed before every launch) and the
+// per-workgroup partials; weights: the 5 sums' weights as for launch_reduce_n.
+constexpr int kPersistMaxWg = 1024;
+constexpr int kPersistThreads = 512;  // 8 waves per workgroup (2 per SIMD), one workgroup per CU
+struct PersistWs {
+  unsigned long long arrive;  // grid barrier arrivals (monotonic within a launch)
+  unsigned long long err;     // 1: a barrier wait timed out (the solve is stopped)
+  unsigned long long pad[6];
+  double part[2][5 * kPersistMaxWg];  // per-workgroup partial sums, by barrier parity
+};
+constexpr size_t kPersistPolled = 64;
+template <typename T>
+int launch_pcg1_persist(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1, PcgState* S,
+                        PersistWs* ws, const TileCfg& tc, int nwg, long long k_end, const double* weights,
+                        hipStream_t s);
+int pcg1_persist_max_wg(int device);  // workgroups that are always co-resident (one per CU)
+
 // Deterministic in-process "all-reduce" across P subdomains on one device (LocalComm):
 // out_k[q] = sum_r in_r[q] for every k, summed in rank order.
 void launch_local_allreduce(double* const* bufs, int nranks, int nq, hipStream_t s);

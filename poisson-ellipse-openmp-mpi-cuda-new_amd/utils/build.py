@@ -35,6 +35,7 @@ HIP_SOURCES = [
     "hip/pcg_kernels.hip",
     "hip/pcg_kernels_dpp.hip",
     "hip/pcg1_kernels.hip",
+    "hip/pcg1_persist.hip",
     "hip/ops_kernels.hip",
     "hip/gpu_solver.hip",
     "hip/session.hip",
