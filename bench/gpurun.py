@@ -33,6 +33,14 @@ PYTEST = "python -u -m pytest -x -v --timeout 170 --timeout-method thread"
 ROCPROF = "rocprofv3 --kernel-trace --stats"
 
 
+# The Python processes (tests, bench.py) run torch's bundled HIP runtime and RCCL (ROCm 7.0 builds,
+# SONAMEs libamdhip64.so.7 / librccl.so.1, loaded by `import torch` before _pmx.so); the CLI and the
+# probes link /opt/rocm (7.2).  TORCH_RT + cmd + "'" runs a probe on torch's runtime instead.
+TORCH_RT = ("bash -c 'TL=$(python3 -c \"import torch, os; print(os.path.dirname(torch.__file__))\")/lib; "
+            "mkdir -p /tmp/pmx_torchrt && ln -sf $TL/libamdhip64.so /tmp/pmx_torchrt/libamdhip64.so.7 && "
+            "LD_LIBRARY_PATH=/tmp/pmx_torchrt:$TL ")
+
+
 def bench(args: str) -> str:
     return f"python -u bench.py {args}"
 
@@ -346,9 +354,28 @@ STUDIES["r4a"] = [
     ("tl_alone", 200, "rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r4a/tl_alone -o run -- "
                       "python3 bench.py --gpus 1 --M 2048 --N 16384 --steps 300 --warmup 30 --no-tol-solve"),
     ("tl_alone_sum", 60, "python3 bench/loopback_timeline.py gpurun_out/r4a/tl_alone"),
+    ("persist_800", 200, bench("--gpus 1 --M 800 --N 1200 --steps 500 --warmup 50")),
+    ("persist_1600", 200, bench("--gpus 1 --M 1600 --N 2400 --steps 500 --warmup 50")),
+    ("graphs_800", 200, bench("--gpus 1 --M 800 --N 1200 --steps 500 --warmup 50 --persistent off")),
+    # verdict r3 item 7, LAST (a host segfault ends the call): the forked-graph shape without pmx code
+    ("graph_fork_default", 60, "bench/probe/graph_fork 3 20 4"),
+    ("graph_fork_torchrt", 60, TORCH_RT + "bench/probe/graph_fork 3 20 4'"),
+    ("graph_fork_hwq1", 60, "env GPU_MAX_HW_QUEUES=1 bench/probe/graph_fork 3 20 4"),
+    ("graph_fork_hwq1_torchrt", 60, TORCH_RT + "GPU_MAX_HW_QUEUES=1 bench/probe/graph_fork 3 20 4'"),
 ]
 
 STUDIES["r4p"] = placement_pmc_steps("r4p")
+# round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
+# BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
+STUDIES["r4b"] = [
+    ("phases_800", 200, bench("--gpus 1 --M 800 --N 1200 --steps 200 --warmup 20 --profile-phases 200")),
+    ("phases_1600", 200, bench("--gpus 1 --M 1600 --N 2400 --steps 200 --warmup 20 --profile-phases 200")),
+    ("phases_2400", 200, bench("--gpus 1 --M 2400 --N 3200 --steps 200 --warmup 20 --profile-phases 200")),
+    ("strip32k_fp32", 200, bench("--gpus 1 --M 4096 --N 32768 --dtype fp32 --steps 200 --warmup 20 --no-tol-solve")),
+    ("strip32k_mixed", 200, bench("--gpus 1 --M 4096 --N 32768 --dtype mixed --steps 200 --warmup 20 --no-tol-solve")),
+    ("strip32k_fp64", 200, bench("--gpus 1 --M 4096 --N 32768 --steps 200 --warmup 20 --no-tol-solve")),
+    ("plan_device", 60, "poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx 32768 32768 --plan --gpus 8 --split auto"),
+]
 
 PARAMETRISED = {"ab": _ab, "pmc": _pmc, "timeline": _timeline, "validate": _validate, "share": _share, "cli": _cli}
 

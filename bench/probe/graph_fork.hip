@@ -35,6 +35,10 @@ int main(int argc, char** argv) {
   const char* hwq = std::getenv("GPU_MAX_HW_QUEUES");
   std::printf("graph_fork: iters/graph %d, launches %d, copies/iter %d, GPU_MAX_HW_QUEUES=%s\n", iters, launches,
               copies, hwq ? hwq : "(default)");
+  int rt = 0, drv = 0;
+  CK(hipRuntimeGetVersion(&rt));
+  CK(hipDriverGetVersion(&drv));
+  std::printf("HIP runtime %d, driver %d\n", rt, drv);
   std::fflush(stdout);
   unsigned long long* counter = nullptr;
   CK(hipMalloc(&counter, 8 * sizeof(unsigned long long)));

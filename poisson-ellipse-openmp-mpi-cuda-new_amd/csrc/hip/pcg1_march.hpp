@@ -67,6 +67,46 @@ __device__ __forceinline__ void store_cols(T* row, int c0, const T (&in)[VEC], b
   }
 }
 
+// Write-through variant (WT, the persistent kernel): buffer stores with the sc1 bit, so the bytes
+// leave the XCD L2 at once and a consumer in another workgroup of the same launch sees them after
+// the producer's vmcnt drain and its own agent acquire -- no L2 writeback fence per sweep
+// (MI355X_MICROARCH.md, publish-large: write-through wins for tens of KB per workgroup).  The row
+// pointer is wave-uniform (an SGPR resource), the column offset per lane; byte offsets stay below
+// 2 GB (persistent grids are <= 192 MB of fields).
+template <typename T, int VEC>
+__device__ __forceinline__ void store_cols_wt(T* row, int c0, const T (&in)[VEC], bool all, const bool (&own)[VEC]) {
+  constexpr int kSc1 = 16;  // aux bits: sc1
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row - 2, 0, 0x7fffffff, 0x00020000);
+  if (all) {
+#pragma unroll
+    for (int q = 0; q < VEC / 2; ++q) {
+      const unsigned off = unsigned(c0 + 2 * q + 2) * unsigned(sizeof(T));
+      if constexpr (sizeof(T) == 8) {
+        typedef double d2 __attribute__((ext_vector_type(2)));
+        typedef unsigned u4 __attribute__((ext_vector_type(4)));
+        const d2 v = {in[2 * q], in[2 * q + 1]};
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), rs, off, 0, kSc1);
+      } else {
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        const f2 v = {in[2 * q], in[2 * q + 1]};
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rs, off, 0, kSc1);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < VEC; ++u)
+      if (own[u]) {
+        const unsigned off = unsigned(c0 + u + 2) * unsigned(sizeof(T));
+        typedef unsigned u2 __attribute__((ext_vector_type(2)));
+        if constexpr (sizeof(T) == 8)
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, in[u]), rs, off, 0, kSc1);
+        else
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, in[u]), rs, off, 0, kSc1);
+      }
+  }
+}
+
 // One row of the tile: its table row and wave-uniform coefficient class.  Only these 2 scalars
 // travel down the 3-stage pipeline; the row's face constants (20 SGPRs) are re-read from the
 // tables on the rare rows the ellipse cuts, which keeps 3 live rows from spilling SGPRs.  The
@@ -215,7 +255,7 @@ struct Pcg1Row {
 // The tile marches top-down, rows i0-2 .. i1+2.  (Bottom-up and alternating marches, super-row and
 // banded dispatch orders were tried to make vertically adjacent tiles share their halo rows in L2:
 // all slower, NOTES #30, #46-48.)
-template <typename T, typename C, int VEC, int PF, int WM, bool FAST>
+template <typename T, typename C, int VEC, int PF, int WM, bool FAST, bool WT = false>
 __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb, const ArithF& F, T* __restrict__ w,
                                            const T* __restrict__ rold, T* __restrict__ rnew,
                                            const T* __restrict__ pold,
@@ -371,9 +411,15 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     }
     if (ownB && (FAST ? own_all : own_any)) {
       const int64_t o = int64_t(mb) * P;
-      store_cols<T, VEC>(rnew + o, c0, rs, FAST || own_all, own);
-      store_cols<T, VEC>(pnew + o, c0, ps, FAST || own_all, own);
-      if constexpr (WUP) store_cols<T, VEC>(w + o, c0, ws, FAST || own_all, own);
+      if constexpr (WT) {
+        store_cols_wt<T, VEC>(rnew + o, c0, rs, FAST || own_all, own);
+        store_cols_wt<T, VEC>(pnew + o, c0, ps, FAST || own_all, own);
+        if constexpr (WUP) store_cols_wt<T, VEC>(w + o, c0, ws, FAST || own_all, own);
+      } else {
+        store_cols<T, VEC>(rnew + o, c0, rs, FAST || own_all, own);
+        store_cols<T, VEC>(pnew + o, c0, ps, FAST || own_all, own);
+        if constexpr (WUP) store_cols<T, VEC>(w + o, c0, ws, FAST || own_all, own);
+      }
     }
     // ---- stage C: A z^k of row m-2
     const int mcr = m - 2;

@@ -10,8 +10,10 @@
 //
 //   sweep k:  every wave marches its tiles of the pcg1 tiling (pcg1_march: the same arithmetic as
 //             k_pcg1, so every point gets bit-identical values for equal scalars);
-//   publish:  the wave sums -> one 5-value partial per workgroup (sc1 stores), every wave drains its
-//             field stores (vmcnt 0), one agent-scope release per workgroup (the XCD L2 written back);
+//   publish:  the wave sums -> one 5-value partial per workgroup (sc1 stores); the fields are stored
+//             write-through (sc1 buffer stores) and every wave drains them (vmcnt 0) before its
+//             workgroup arrives, so no L2 writeback fence is needed (PMX_PERSIST_WT=0: k_pcg1's
+//             non-temporal stores + one agent-scope release per workgroup instead);
 //   barrier:  one monotonic arrival counter (relaxed agent-scope add, relaxed polls with s_sleep,
 //             bounded by a wall-clock timeout that stops the solve instead of hanging the GPU);
 //   acquire:  one agent-scope acquire per workgroup, then every workgroup sums the NWG partials in
@@ -30,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "pcg1_march.hpp"
 #include "pcg_device.hpp"
@@ -55,7 +58,9 @@ __device__ __forceinline__ unsigned long long ld_relaxed(const unsigned long lon
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <typename T, typename C, int PF>
+// WT: field stores write-through (sc1): the publish needs no L2 writeback fence.  Else plain
+// non-temporal stores (k_pcg1's) and one agent release per workgroup and sweep.
+template <typename T, typename C, int PF, bool WT>
 __global__ void __launch_bounds__(kPersistThreads, kPersistWaves / 4)
 k_pcg1_persist(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1, PcgState* S,
                PersistWs* ws, PersistArgs A) {
@@ -175,8 +180,8 @@ k_pcg1_persist(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T
       const bool use_cls = A.TI + 5 <= 64 / 2;
       double t[kNq] = {0.0, 0.0, 0.0, 0.0, 0.0};
 #define PMX_PMARCH(E, F)                                                                                        \
-  pcg1_march<T, C, VEC, PF, E, F>(G, Tb, AF, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, t, \
-                                  scol, ocls, use_cls)
+  pcg1_march<T, C, VEC, PF, E, F, WT>(G, Tb, AF, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, \
+                                      t, scol, ocls, use_cls)
 #define PMX_PMARCH_W(F)                  \
   switch (wm) {                          \
     case 0: PMX_PMARCH(0, F); break;     \
@@ -215,8 +220,12 @@ k_pcg1_persist(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T
         for (int wv = 0; wv < kPersistWaves; ++wv) v += s_sum[wv][q];
         st_publish(slot + q, v);
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the XCD L2's dirty field lines
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (ROCm 7.2 may drop the fence's own wait)
+      if constexpr (!WT) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the XCD L2's dirty field lines
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (ROCm 7.2 may drop the fence's own wait)
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the partial's sc1 stores
+      }
       __hip_atomic_fetch_add(&ws->arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // ---- grid barrier: every workgroup of sweep `gen` has arrived
       const unsigned long long target = gen * (unsigned long long)nwg;
@@ -296,12 +305,19 @@ int launch_pcg1_persist(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2
   // every polled word zeroed before EVERY launch (a memset node when captured)
   HIP_CHECK(hipMemsetAsync(ws, 0, kPersistPolled, s));
   static_assert(sizeof(T) == 8, "pcg1p: fp64 storage");
-  if (tc.pf == 2)
-    hipLaunchKernelGGL((k_pcg1_persist<T, double, 2>), dim3(nwg), dim3(kPersistThreads), 0, s, G, Tb, w, r, r2,
-                       p0, p1, S, ws, A);
-  else
-    hipLaunchKernelGGL((k_pcg1_persist<T, double, 1>), dim3(nwg), dim3(kPersistThreads), 0, s, G, Tb, w, r, r2,
-                       p0, p1, S, ws, A);
+  static const bool wt = [] {  // PMX_PERSIST_WT=0: non-temporal stores + release fence (A/B)
+    const char* e = std::getenv("PMX_PERSIST_WT");
+    return !(e && e[0] == '0');
+  }();
+#define PMX_PERSIST_LAUNCH(PF, WT)                                                                          \
+  hipLaunchKernelGGL((k_pcg1_persist<T, double, PF, WT>), dim3(nwg), dim3(kPersistThreads), 0, s, G, Tb, w, r, \
+                     r2, p0, p1, S, ws, A)
+  if (tc.pf == 2) {
+    if (wt) PMX_PERSIST_LAUNCH(2, true); else PMX_PERSIST_LAUNCH(2, false);
+  } else {
+    if (wt) PMX_PERSIST_LAUNCH(1, true); else PMX_PERSIST_LAUNCH(1, false);
+  }
+#undef PMX_PERSIST_LAUNCH
   HIP_CHECK(hipGetLastError());
   return nwg;
 }
