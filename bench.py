@@ -147,8 +147,8 @@ def parse(argv=None):
                          "fp64 single-subdomain grids whose fields fit the Infinity Cache (<= 192 MB)")
     ap.add_argument("--loopback-rank", type=int, default=-1,
                     help="timing rehearsal on ONE GPU (valid=false): rank R of the --gpus-rank decomposition "
-                         "alone, ghosts served from its own rows by device copies, all-reduce skipped -- the "
-                         "real per-rank schedule (split sweep, frame stream, exchange copies) at full speed")
+                         "alone, ghosts filled by device copies of the real sizes (from zeros), all-reduce "
+                         "skipped -- the real per-rank schedule (split sweep, frame stream, copies) at full speed")
     ap.add_argument("--placement-budget", type=float, default=0.5, help="placement probe: seconds of probing")
     ap.add_argument("--placement-keep-free", type=float, default=0.5,
                     help="placement probe: fraction of the free device memory left free")
@@ -805,7 +805,8 @@ def measure_loopback(args) -> int:
         "value": round(dt / args.steps * 1e6, 2), "unit": "us/iteration", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": False,
         "dtype": args.dtype,
-        "data": f"loopback: rank {args.loopback_rank} of {args.gpus} alone, ghosts from its own rows, no all-reduce",
+        "data": f"loopback: rank {args.loopback_rank} of {args.gpus} alone, ghosts copied from a zero buffer "
+                "(Dirichlet), no all-reduce",
         "config": {"grid": [args.M, args.N], "world": args.gpus, "rank": args.loopback_rank, "split": args.split,
                    "process_grid": list(s.grid), "subdomain": [sd["nx"], sd["ny"]], "comm": s.comm_name,
                    "split_sweep": bool(s.split_sweep), "direct_rows": bool(s.direct_rows), "tile": tile,

@@ -320,6 +320,8 @@ PYBIND11_MODULE(_pmx, m) {
     HIP_CHECK(hipFree(ws));
     HIP_CHECK(hipFree(st));
   }, py::arg("parts"), py::arg("n"), py::arg("nq"), py::arg("nsets"), py::arg("out"), py::arg("stream") = 0);
+  m.def("persistent_trace", []() { return pcg1_persist_trace(); },
+        "PMX_PERSIST_TRACE=k: wall-clock stamps of sweep k of the last persistent launch (see kernels.hpp)");
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   // Arena layout for a Python-orchestrated solver (DistGpuPCG comm="torch").  The iteration
   // algorithm is resolved exactly as the solver will (options + environment + device size), so

@@ -17,6 +17,7 @@
 //  * SelfComm  — P = 1.
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstring>
 #include <memory>
@@ -137,23 +138,38 @@ void rccl_halo_calls(GpuSubdomainSolver* s, ncclComm_t comm, hipStream_t stream)
 // See make_loopback_comm.
 class LoopbackComm final : public Comm {
  public:
+  ~LoopbackComm() override {
+    if (zeros_) (void)hipFree(zeros_);
+  }
   void allreduce(std::vector<GpuSubdomainSolver*>&, int, std::vector<hipStream_t>&) override {}
   void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>& streams) override {
     PMX_CHECK(local.size() == 1, "the loopback comm stands for one rank");
     const HaloMsgs ms = local[0]->halo_msgs();
-    for (int q = 0; q < ms.n; ++q) {
-      const HaloMsg& m = ms.m[q];
-      const void* src = m.send;  // an edge rank's lone slot: its own send span
-      for (int o = 0; o < ms.n; ++o)
-        if (ms.m[o].slot == opposite_slot(m.slot) && ms.m[o].field == m.field) src = ms.m[o].send;
-      HIP_CHECK(hipMemcpyAsync(m.recv, src, size_t(m.count) * local[0]->layout().elem, hipMemcpyDeviceToDevice,
-                               streams[0]));
+    const size_t elem = local[0]->layout().elem;
+    size_t need = 0;
+    for (int q = 0; q < ms.n; ++q) need = std::max(need, size_t(ms.m[q].count) * elem);
+    if (need > zeros_bytes_) {  // first exchange: init(), never inside a graph capture
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      HIP_CHECK(hipStreamIsCapturing(streams[0], &cs));
+      PMX_CHECK(cs == hipStreamCaptureStatusNone, "loopback: first exchange inside a graph capture");
+      if (zeros_) HIP_CHECK(hipFree(zeros_));
+      HIP_CHECK(hipMalloc(&zeros_, need));
+      HIP_CHECK(hipMemset(zeros_, 0, need));
+      zeros_bytes_ = need;
     }
+    // every ghost becomes a Dirichlet zero: each rank solves a well-posed problem on its own block
+    for (int q = 0; q < ms.n; ++q)
+      HIP_CHECK(hipMemcpyAsync(ms.m[q].recv, zeros_, size_t(ms.m[q].count) * elem, hipMemcpyDeviceToDevice,
+                               streams[0]));
   }
   bool prefers_split() const override { return true; }  // as RCCL
   bool direct_rows() const override { return true; }
   std::string name() const override { return "loopback"; }
   int world_size() const override { return 1; }
+
+ private:
+  void* zeros_ = nullptr;
+  size_t zeros_bytes_ = 0;
 };
 
 // One local rank of an RcclComm, driven by its own host thread: its collectives need no

@@ -33,6 +33,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <vector>
 
 #include "pcg1_march.hpp"
 #include "pcg_device.hpp"
@@ -52,7 +53,14 @@ struct PersistArgs {
   long long k_end;        // the last sweep index this launch may run
   double wt[kNq];         // weights of the 5 sums (h1 h2, and the stop-test norm weight)
   long long timeout;      // barrier wait limit in wall_clock64 ticks (100 MHz)
+  // diagnostics (PMX_PERSIST_TRACE=k): wall-clock stamps of sweep `trace_k` -- per wave its march
+  // start / end, per workgroup its barrier arrival / exit (100 MHz ticks); nullptr = off
+  unsigned long long* trace;
+  long long trace_k;
 };
+
+unsigned long long* g_trace = nullptr;  // host copy of the trace buffer (one per process)
+int g_trace_n = 0;
 
 __device__ __forceinline__ unsigned long long ld_relaxed(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -162,6 +170,8 @@ k_pcg1_persist(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T
       }
     }
     if (leader) S->halo_k = k + 1;
+    const bool tr = A.trace && k == A.trace_k;
+    if (tr && lane == 0) A.trace[2 * gwave] = wall_clock64();
 
     // ---- sweep k: this wave's tiles
     T* pnew = (k & 1) ? p1 : p0;
@@ -200,6 +210,7 @@ k_pcg1_persist(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T
       for (int q = 0; q < kNq; ++q) acc[q] += t[q];
     }
 
+    if (tr && lane == 0) A.trace[2 * gwave + 1] = wall_clock64();
     // ---- publish: wave sums -> workgroup partial (fixed order), field stores drained and released
     wave_sum2_mfma(acc[0], acc[1]);
     wave_sum2_mfma(acc[2], acc[3]);
@@ -227,6 +238,7 @@ k_pcg1_persist(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the partial's sc1 stores
       }
       __hip_atomic_fetch_add(&ws->arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tr) A.trace[2 * nwaves + 2 * blockIdx.x] = wall_clock64();
       // ---- grid barrier: every workgroup of sweep `gen` has arrived
       const unsigned long long target = gen * (unsigned long long)nwg;
       const long long t0 = wall_clock64();
@@ -242,6 +254,7 @@ k_pcg1_persist(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // ONE acquire: this CU's L1 drops stale lines
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       s_stop = stop;
+      if (tr) A.trace[2 * nwaves + 2 * blockIdx.x + 1] = wall_clock64();
     }
     __syncthreads();
     if (s_stop) {  // a workgroup never arrived: stop the solve (the host sees status breakdown + NaN)
@@ -302,6 +315,21 @@ int launch_pcg1_persist(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2
   A.k_end = k_end;
   for (int q = 0; q < kNq; ++q) A.wt[q] = weights[q];
   A.timeout = 200000000LL;  // 2 s of wall clock per barrier wait
+  static const long long trace_k = [] {
+    const char* e = std::getenv("PMX_PERSIST_TRACE");
+    return e && e[0] ? std::atoll(e) : -1LL;
+  }();
+  if (trace_k >= 0) {
+    const int n = 2 * nwg * (kPersistThreads / 64) + 2 * nwg;
+    if (!g_trace || g_trace_n < n) {
+      if (g_trace) HIP_CHECK(hipFree(g_trace));
+      HIP_CHECK(hipMalloc(&g_trace, size_t(n) * 8));
+      g_trace_n = n;
+    }
+    HIP_CHECK(hipMemsetAsync(g_trace, 0, size_t(n) * 8, s));
+    A.trace = g_trace;
+    A.trace_k = trace_k;
+  }
   // every polled word zeroed before EVERY launch (a memset node when captured)
   HIP_CHECK(hipMemsetAsync(ws, 0, kPersistPolled, s));
   static_assert(sizeof(T) == 8, "pcg1p: fp64 storage");
@@ -320,6 +348,12 @@ int launch_pcg1_persist(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2
 #undef PMX_PERSIST_LAUNCH
   HIP_CHECK(hipGetLastError());
   return nwg;
+}
+
+std::vector<unsigned long long> pcg1_persist_trace() {
+  std::vector<unsigned long long> h(static_cast<size_t>(g_trace_n));
+  if (g_trace_n) HIP_CHECK(hipMemcpy(h.data(), g_trace, h.size() * 8, hipMemcpyDeviceToHost));
+  return h;
 }
 
 int pcg1_persist_max_wg(int device) {

@@ -378,10 +378,10 @@ class Comm {
 
 std::unique_ptr<Comm> make_self_comm();
 // bench.py --loopback-rank: ONE rank of a P-rank decomposition alone on this device.  Every ghost
-// message is served from the rank's own data (recv of slot s <- its own send of the opposite slot,
-// or of s itself on an edge rank: a device copy of the real size on the exchange's stream), and the
-// all-reduce is skipped: the real per-rank schedule (split sweep, frame stream, events, copies) runs
-// at full speed as a timing rehearsal; the numbers it computes are meaningless.
+// message is a device copy of the real size on the exchange's stream -- from a zero buffer, so the
+// rank solves its block with Dirichlet ghosts (a well-posed problem that runs as long as the real
+// one) -- and the all-reduce is skipped: the real per-rank schedule (split sweep, frame stream,
+// events, copies) runs at full speed as a timing rehearsal.
 std::unique_ptr<Comm> make_loopback_comm();
 std::unique_ptr<Comm> make_local_comm(std::vector<GpuSubdomainSolver*>& local);
 // RCCL: one communicator per local solver.  `unique_id` is the 128-byte ncclUniqueId,

@@ -12,6 +12,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 #include "pmx/device_types.hpp"
 
 namespace pmx {
@@ -169,6 +171,9 @@ int launch_pcg1_persist(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2
                         PersistWs* ws, const TileCfg& tc, int nwg, long long k_end, const double* weights,
                         hipStream_t s);
 int pcg1_persist_max_wg(int device);  // workgroups that are always co-resident (one per CU)
+// PMX_PERSIST_TRACE=k: stamps of sweep k of the last launch -- 2 per wave (march start, end), then 2
+// per workgroup (barrier arrival, exit); wall_clock64 ticks (100 MHz)
+std::vector<unsigned long long> pcg1_persist_trace();
 
 // Deterministic in-process "all-reduce" across P subdomains on one device (LocalComm):
 // out_k[q] = sum_r in_r[q] for every k, summed in rank order.

@@ -210,8 +210,11 @@ def test_serialized_schedule_uses_one_stream_and_one_communicator(native, pkg, s
     logs = native.record_comm_sequence(spec, 8, getattr(native.Split, split), 0, 8, overlap=True)
     for l in logs:
         ar = {e[4] for e in l if e[1] == "allreduce"}
-        halo = {e[4] for e in l if e[0] == 1}
-        assert len(ar) == 1 and halo and not (ar & halo)
+        groups = [e for e in l if e[1] == "group_start"]
+        assert all(g[0] == 1 for g in groups)  # the halo communicator
+        # init's two exchanges run in order on the compute stream; every iteration's on the comm stream
+        halo = {g[4] for g in groups[2:]}
+        assert len(ar) == 1 and len(halo) == 1 and not (ar & halo)
 
 
 def _bench(args, timeout=300):

@@ -297,9 +297,9 @@ def test_direct_rows_poisoned_ghosts(pkg, monkeypatch):
 
 @pytest.mark.parametrize("rank,split", [(3, "rows"), (0, "rows"), (5, "reference")])
 def test_loopback_rank_runs_the_real_schedule(pkg, native, rank, split):
-    """bench.py --loopback-rank: one rank of an 8-rank decomposition alone on the GPU, ghosts served
-    from its own rows (device copies of the real sizes), all-reduce skipped: split sweep, frame
-    stream and graphs run as in the 8-GPU job."""
+    """bench.py --loopback-rank: one rank of an 8-rank decomposition alone on the GPU, ghosts filled by
+    device copies of the real sizes (from zeros: Dirichlet), all-reduce skipped: split sweep, frame
+    stream and graphs run as in the 8-GPU job, and the solve keeps iterating."""
     p = pkg.PoissonEllipse(M=2048, N=2048)
     s = native.Session(p.to_native(), world=8, comm="loopback", split=getattr(native.Split, split), ranks=[rank],
                        devices=[0], graph_batch=16)
