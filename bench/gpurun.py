@@ -365,6 +365,18 @@ STUDIES["r4a"] = [
 ]
 
 STUDIES["r4p"] = placement_pmc_steps("r4p")
+# round 4, second contact: the full suite after the fixes, the persistent kernel's anatomy (write-
+# through stores vs non-temporal + release fence), the loopback strip (Dirichlet ghosts) + timeline
+STUDIES["r4c"] = [
+    ("pytest_gpu", 800, f"{PYTEST} tests -m gpu"),
+    ("persist_trace", 200, "python3 -u bench/probe/persist_trace.py 800x1200 1600x2400 2400x3200"),
+    ("persist_trace_nowt", 200, "env PMX_PERSIST_WT=0 python3 -u bench/probe/persist_trace.py 800x1200 1600x2400"),
+    ("loop_strip3", 200, bench("--gpus 8 --loopback-rank 3 --steps 300 --warmup 30")),
+    ("loop_strip3_packed", 200, "env PMX_DIRECT_ROWS=0 " + bench("--gpus 8 --loopback-rank 3 --steps 300 --warmup 30")),
+    ("tl_strip3", 200, "rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/r4c/tl_strip3 "
+                       "-o run -- python3 bench.py --gpus 8 --loopback-rank 3 --steps 300 --warmup 30"),
+    ("tl_strip3_sum", 60, "python3 bench/loopback_timeline.py gpurun_out/r4c/tl_strip3"),
+]
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [
