@@ -275,13 +275,20 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   }
   if (persist_) {
     pwg_ = pcg1_persist_max_wg(opt.device);
-    // one tile per wave: rows so that the tile count matches the resident waves
+    // ~2 tiles per resident wave (the static schedule balances cut tiles against plain ones), but
+    // no shorter than 4 rows (a tile marches 4 extra rows); PMX_PERSIST_ROWS overrides
     const int waves = pwg_ * (kPersistThreads / 64), tj = (sd.ny + 123) / 124;
-    const int want_rows = std::max(1, (waves + tj - 1) / tj);
-    const int ti = opt_.rows1 ? opt_.rows1 : std::max(2, (sd.nx + want_rows - 1) / want_rows);
+    const int want_rows = std::max(1, (2 * waves + tj - 1) / tj);
+    int ti = std::max(4, (sd.nx + want_rows - 1) / want_rows);
+    if (const char* e = std::getenv("PMX_PERSIST_ROWS"); e && e[0]) ti = std::max(1, std::atoi(e));
     tilesP_ = make_pcg1_tiles(G, 2, 1, ti, opt_.pf1 ? opt_.pf1 : 1, int(elem_));
-    HIP_CHECK(hipMalloc(&tile_order_p_, 3 * size_t(tilesP_.ntiles()) * sizeof(Pcg1Slot)));
+    HIP_CHECK(hipMalloc(&tile_order_p_, 4 * size_t(tilesP_.ntiles()) * sizeof(Pcg1Slot)));
     (void)pcg1_build_order(G, tables_, tilesP_, tile_order_p_, true, nullptr);
+    HIP_CHECK(hipMalloc(&sched_offs_p_, (size_t(waves) + 1) * sizeof(int)));
+    sched_p_ = tile_order_p_ + 3 * size_t(tilesP_.ntiles());
+    double cut_cost = 2.0;  // a cut row step vs a class-uniform one, with the coefficient carry (NOTES)
+    if (const char* e = std::getenv("PMX_PERSIST_CUT_COST"); e && e[0]) cut_cost = std::atof(e);
+    pcg1_persist_schedule(tilesP_, waves, cut_cost, sched_p_, sched_offs_p_);
     HIP_CHECK(hipMalloc(&pws_, sizeof(PersistWs)));
   }
 
@@ -459,6 +466,9 @@ void GpuSubdomainSolver::release() noexcept {
   if (tile_order_) (void)hipFree(tile_order_);
   if (tile_order_w_) (void)hipFree(tile_order_w_);
   if (tile_order_p_) (void)hipFree(tile_order_p_);
+  if (sched_offs_p_) (void)hipFree(sched_offs_p_);
+  sched_offs_p_ = nullptr;
+  sched_p_ = nullptr;
   if (pws_) (void)hipFree(pws_);
   tile_order_p_ = nullptr;
   pws_ = nullptr;
@@ -585,8 +595,8 @@ void GpuSubdomainSolver::enqueue_persistent(hipStream_t s, long long n) {
   const double wts[5] = {h, h, h, h, wdiff};
   launch_pcg1_persist<double>(geom_, tables_, static_cast<double*>(field_base(0)), static_cast<double*>(field_base(1)),
                               reinterpret_cast<double*>(r2_ + field_off_ * elem_), static_cast<double*>(field_base(2)),
-                              static_cast<double*>(field_base(3)), state_, pws_, tilesP_, pwg_, host_k_ + n - 1, wts,
-                              s);
+                              static_cast<double*>(field_base(3)), state_, pws_, tilesP_, sched_p_, sched_offs_p_, pwg_,
+                              host_k_ + n - 1, wts, s);
   host_k_ += n;  // as n reductions would (the device stops early on its own)
   after_launch(s);
 }

@@ -255,14 +255,20 @@ struct Pcg1Row {
 // The tile marches top-down, rows i0-2 .. i1+2.  (Bottom-up and alternating marches, super-row and
 // banded dispatch orders were tried to make vertically adjacent tiles share their halo rows in L2:
 // all slower, NOTES #30, #46-48.)
-template <typename T, typename C, int VEC, int PF, int WM, bool FAST, bool WT = false>
+// CC (coefficient carry, the persistent kernel): a row the ellipse cuts has its face coefficients
+// evaluated ONCE, in stage A, and parked in a lane-private LDS ring (kring: 3 rows x VEC x 4 values
+// per lane) for stages B and C, instead of three evaluations per row -- on cut rows the exact face
+// formulas (fp64 divisions at quarter rate, executed by the whole wave for the few cut lanes) are
+// what makes a cut tile 3-5x slower than its neighbours, and at the reference's small grids the
+// slowest tile is the sweep.  Class-uniform rows never touch the ring.  Same values, same results.
+template <typename T, typename C, int VEC, int PF, int WM, bool FAST, bool WT = false, bool CC = false>
 __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb, const ArithF& F, T* __restrict__ w,
                                            const T* __restrict__ rold, T* __restrict__ rnew,
                                            const T* __restrict__ pold,
                                            T* pnew, int i0, int i1, int j0, int j1,
                                            double alpha_d, double beta_d, double c1_d, double c2_d,
                                            double (&acc)[kNq], double* __restrict__ scol,
-                                           unsigned long long cls, bool use_cls) {
+                                           unsigned long long cls, bool use_cls, double* __restrict__ kring = nullptr) {
   constexpr bool WUP = WM != 0;
   constexpr bool PK = std::is_same_v<C, float> && VEC == 2;  // packed fp32 stencils (apply_row)
   const C alpha = C(alpha_d), beta = C(beta_d), c1 = C(c1_d), c2 = C(c2_d);
@@ -293,6 +299,18 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     return row_co(Tb, grow(m), gjlo, gjhi);
   };
   auto interior_row = [&](int m) { return G.gi0 + m >= 1 && G.gi0 + m <= G.M - 1; };
+  // CC ring slot of row m (m >= -3), value q in {a0, a1, b0, b1} of column u
+  auto ring = [&](int m, int u, int q) -> double& { return kring[(((m + 3) % 3 * VEC + u) * 4 + q) * 64 + lane]; };
+  // coefficients of a row in stage B / C: from the ring when CC carries them, else rebuilt
+  auto coef_at = [&](const RowCo& c, int m, int u, C& a0, C& a1, C& b0, C& b1) {
+    if constexpr (CC) {
+      if (c.ucls == 0) {
+        a0 = C(ring(m, u, 0)); a1 = C(ring(m, u, 1)); b0 = C(ring(m, u, 2)); b1 = C(ring(m, u, 3));
+        return;
+      }
+    }
+    coef_c<C>(c, Tb, G, F, scol, u, lane, gj[u], a0, a1, b0, b1);
+  };
 
   auto fetch = [&](int m, Pcg1Row<T, VEC>& b) {
     const int mc = min(max(m, -1), G.nx + 2);  // rows -1 .. nx+2 exist (2 ghost layers)
@@ -326,6 +344,17 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     parked = true;
   };
   if (cB.ucls == 0) park_cols();
+  if constexpr (CC) {  // row i0-3 enters stage B at the first step without passing stage A
+    if (cB.ucls == 0) {
+#pragma unroll
+      for (int u = 0; u < VEC; ++u) {
+        C a0, a1, b0, b1;
+        coef_c<C>(cB, Tb, G, F, scol, u, lane, gj[u], a0, a1, b0, b1);
+        ring(i0 - 3, u, 0) = double(a0); ring(i0 - 3, u, 1) = double(a1);
+        ring(i0 - 3, u, 2) = double(b0); ring(i0 - 3, u, 3) = double(b1);
+      }
+    }
+  }
 
   const int mfirst = i0 - 2, mlast = i1 + 2;
   auto step = [&](int m, const Pcg1Row<T, VEC>& cur, Pcg1Row<T, VEC>& nxt) {
@@ -344,6 +373,12 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
       pom[u] = in ? C(cur.p[u]) : C(0);
       C a0, a1, b0, b1;
       coef_c<C>(cA, Tb, G, F, scol, u, lane, gj[u], a0, a1, b0, b1);
+      if constexpr (CC) {
+        if (cA.ucls == 0) {
+          ring(m, u, 0) = double(a0); ring(m, u, 1) = double(a1);
+          ring(m, u, 2) = double(b0); ring(m, u, 3) = double(b1);
+        }
+      }
       const C z = zdiv_c<C>(cA.ucls, rom[u], a0, a1, b0, b1, G, F);
       const C v = fma_c(beta, pom[u], z);
       Pm[u] = in ? C(static_cast<T>(v)) : C(0);  // the stored (rounded) p^k is the one used
@@ -368,7 +403,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
       C a0[VEC], a1[VEC], b0[VEC], b1[VEC], Ap[VEC], Apo[VEC];
       if constexpr (PK) {
 #pragma unroll
-        for (int u = 0; u < VEC; ++u) coef_c<C>(cB, Tb, G, F, scol, u, lane, gj[u], a0[u], a1[u], b0[u], b1[u]);
+        for (int u = 0; u < VEC; ++u) coef_at(cB, mb, u, a0[u], a1[u], b0[u], b1[u]);
         apply_row<C, VEC>(Pm1, Pm2, Pm, left, right, a0, a1, b0, b1, G, F, Ap);
         // p^{k-2} recovery (WM 2): A p^{k-1}
         if constexpr (WM == 2)
@@ -377,7 +412,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
 #pragma unroll
       for (int u = 0; u < VEC; ++u) {
         if constexpr (!PK) {
-          coef_c<C>(cB, Tb, G, F, scol, u, lane, gj[u], a0[u], a1[u], b0[u], b1[u]);
+          coef_at(cB, mb, u, a0[u], a1[u], b0[u], b1[u]);
           Ap[u] = apply_c<C>(Pm1[u], Pm2[u], Pm[u], u == 0 ? left : Pm1[u - 1],
                              u == VEC - 1 ? right : Pm1[u + 1], a0[u], a1[u], b0[u], b1[u], G, F);
           if constexpr (WM == 2)
@@ -429,13 +464,13 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
       C a0[VEC], a1[VEC], b0[VEC], b1[VEC], Az[VEC];
       if constexpr (PK) {
 #pragma unroll
-        for (int u = 0; u < VEC; ++u) coef_c<C>(cC, Tb, G, F, scol, u, lane, gj[u], a0[u], a1[u], b0[u], b1[u]);
+        for (int u = 0; u < VEC; ++u) coef_at(cC, mcr, u, a0[u], a1[u], b0[u], b1[u]);
         apply_row<C, VEC>(Zm2, Zm3, Zm1, left, right, a0, a1, b0, b1, G, F, Az);
       }
 #pragma unroll
       for (int u = 0; u < VEC; ++u) {
         if constexpr (!PK) {
-          coef_c<C>(cC, Tb, G, F, scol, u, lane, gj[u], a0[u], a1[u], b0[u], b1[u]);
+          coef_at(cC, mcr, u, a0[u], a1[u], b0[u], b1[u]);
           Az[u] = apply_c<C>(Zm2[u], Zm3[u], Zm1[u], u == 0 ? left : Zm2[u - 1],
                              u == VEC - 1 ? right : Zm2[u + 1], a0[u], a1[u], b0[u], b1[u], G, F);
         }

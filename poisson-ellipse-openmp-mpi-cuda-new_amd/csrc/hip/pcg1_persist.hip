@@ -33,6 +33,9 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <functional>
+#include <queue>
+#include <utility>
 #include <vector>
 
 #include "pcg1_march.hpp"
@@ -49,7 +52,8 @@ constexpr int kPersistWaves = kPersistThreads / 64;
 
 struct PersistArgs {
   int TI, tiles_j, ntiles;
-  const Pcg1Slot* order;  // position -> tile (cut tiles first within each XCD's share)
+  const Pcg1Slot* order;  // the static schedule: wave w marches order[offs[w] .. offs[w+1])
+  const int* offs;
   long long k_end;        // the last sweep index this launch may run
   double wt[kNq];         // weights of the 5 sums (h1 h2, and the stop-test norm weight)
   long long timeout;      // barrier wait limit in wall_clock64 ticks (100 MHz)
@@ -80,9 +84,11 @@ k_pcg1_persist(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T
   const int gwave = int(blockIdx.x) * kPersistWaves + wave;
   const int nwaves = nwg * kPersistWaves;
   __shared__ double s_col[kPersistWaves * 4 * VEC * 64];
+  __shared__ double s_ring[kPersistWaves * 3 * VEC * 4 * 64];  // cut-row coefficient carry (pcg1_march CC)
   __shared__ double s_sum[kPersistWaves][kNq];
   __shared__ int s_stop;
   double* scol = s_col + wave * (4 * VEC * 64);
+  double* kring = s_ring + wave * (3 * VEC * 4 * 64);
   const ArithF AF{float(G.cx), float(G.cy), float(G.dinv_in), float(G.dinv_out), float(G.inv_eps)};
 
   // state at entry (written by earlier kernels: visible at this kernel's start).  The PCG scalars
@@ -179,7 +185,8 @@ k_pcg1_persist(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T
     const T* rold = (k & 1) ? r2 : r;
     T* rnew = (k & 1) ? r : r2;
     double acc[kNq] = {0.0, 0.0, 0.0, 0.0, 0.0};
-    for (int pos = gwave; pos < A.ntiles; pos += nwaves) {
+    const int q0 = A.offs[gwave], q1 = A.offs[gwave + 1];
+    for (int pos = q0; pos < q1; ++pos) {
       const int id = A.order[pos].id;
       const unsigned long long ocls = A.order[pos].cls;
       const int ti = id / A.tiles_j, tj = id - ti * A.tiles_j;
@@ -190,8 +197,8 @@ k_pcg1_persist(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T
       const bool use_cls = A.TI + 5 <= 64 / 2;
       double t[kNq] = {0.0, 0.0, 0.0, 0.0, 0.0};
 #define PMX_PMARCH(E, F)                                                                                        \
-  pcg1_march<T, C, VEC, PF, E, F, WT>(G, Tb, AF, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, \
-                                      t, scol, ocls, use_cls)
+  pcg1_march<T, C, VEC, PF, E, F, WT, true>(G, Tb, AF, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, \
+                                            c2, t, scol, ocls, use_cls, kring)
 #define PMX_PMARCH_W(F)                  \
   switch (wm) {                          \
     case 0: PMX_PMARCH(0, F); break;     \
@@ -302,8 +309,8 @@ k_pcg1_persist(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T
 
 template <typename T>
 int launch_pcg1_persist(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1, PcgState* S,
-                        PersistWs* ws, const TileCfg& tc, int nwg, long long k_end, const double* weights,
-                        hipStream_t s) {
+                        PersistWs* ws, const TileCfg& tc, const Pcg1Slot* sched, const int* offs, int nwg,
+                        long long k_end, const double* weights, hipStream_t s) {
   PMX_CHECK(tc.kind == 3 && tc.vec == 2 && tc.waves == 1 && tc.order0, "pcg1p needs VEC 2 wave tiles with an order");
   PMX_CHECK(nwg >= 1 && nwg <= kPersistMaxWg, "pcg1p: 1.." << kPersistMaxWg << " workgroups");
   PMX_CHECK(G.nb == 0, "pcg1p runs undecomposed grids only");
@@ -311,7 +318,8 @@ int launch_pcg1_persist(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2
   A.TI = tc.rows;
   A.tiles_j = tc.tiles_j;
   A.ntiles = tc.ntiles();
-  A.order = tc.order0;
+  A.order = sched;
+  A.offs = offs;
   A.k_end = k_end;
   for (int q = 0; q < kNq; ++q) A.wt[q] = weights[q];
   A.timeout = 200000000LL;  // 2 s of wall clock per barrier wait
@@ -363,7 +371,48 @@ int pcg1_persist_max_wg(int device) {
 }
 
 template int launch_pcg1_persist<double>(const DevGeom&, const DevTables&, double*, double*, double*, double*,
-                                         double*, PcgState*, PersistWs*, const TileCfg&, int, long long,
-                                         const double*, hipStream_t);
+                                         double*, PcgState*, PersistWs*, const TileCfg&, const Pcg1Slot*,
+                                         const int*, int, long long, const double*, hipStream_t);
+
+void pcg1_persist_schedule(const TileCfg& tc, int nwaves, double cut_row_cost, Pcg1Slot* d_sched, int* d_offs) {
+  const int n = tc.ntiles();
+  std::vector<Pcg1Slot> ord(static_cast<size_t>(n));
+  HIP_CHECK(hipMemcpy(ord.data(), tc.order0, ord.size() * sizeof(Pcg1Slot), hipMemcpyDeviceToHost));
+  // cost of a tile in row steps: TI + 4 marched rows, each cut row (class 0) cut_row_cost more
+  const int rows = tc.rows + 5;  // classes of rows i0-3 .. i1+2 (Pcg1Slot), when they fit 64 bits
+  std::vector<double> cost(ord.size());
+  for (size_t t = 0; t < ord.size(); ++t) {
+    int ncut = 0;
+    if (rows <= 32) {
+      for (int q = 0; q < rows; ++q) ncut += ((ord[t].cls >> (2 * q)) & 3ull) == 0;
+    }
+    cost[t] = tc.rows + 4 + cut_row_cost * ncut;
+  }
+  // longest-processing-time-first onto the least loaded wave (ties: the lowest wave index), so the
+  // slowest wave -- the sweep -- carries as little as a static schedule allows; fixed, so every run
+  // and every sweep sums the same partials in the same order
+  std::vector<int> idx(ord.size());
+  for (size_t t = 0; t < idx.size(); ++t) idx[t] = int(t);
+  std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return cost[size_t(a)] > cost[size_t(b)]; });
+  typedef std::pair<double, int> Load;
+  std::priority_queue<Load, std::vector<Load>, std::greater<Load>> heap;
+  for (int w = 0; w < nwaves; ++w) heap.push({0.0, w});
+  std::vector<std::vector<int>> per(static_cast<size_t>(nwaves));
+  for (int t : idx) {
+    Load l = heap.top();
+    heap.pop();
+    per[size_t(l.second)].push_back(t);
+    heap.push({l.first + cost[size_t(t)], l.second});
+  }
+  std::vector<Pcg1Slot> sched;
+  std::vector<int> offs(1, 0);
+  sched.reserve(ord.size());
+  for (auto& v : per) {
+    for (int t : v) sched.push_back(ord[size_t(t)]);
+    offs.push_back(int(sched.size()));
+  }
+  HIP_CHECK(hipMemcpy(d_sched, sched.data(), sched.size() * sizeof(Pcg1Slot), hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpy(d_offs, offs.data(), offs.size() * sizeof(int), hipMemcpyHostToDevice));
+}
 
 }  // namespace pmx

@@ -307,6 +307,8 @@ class GpuSubdomainSolver {
   bool persist_ = false;
   TileCfg tilesP_{};
   Pcg1Slot* tile_order_p_ = nullptr;
+  Pcg1Slot* sched_p_ = nullptr;  // the persistent kernel's static schedule (inside tile_order_p_)
+  int* sched_offs_p_ = nullptr;
   PersistWs* pws_ = nullptr;
   int pwg_ = 0;
   TileCfg init_tiles_{};

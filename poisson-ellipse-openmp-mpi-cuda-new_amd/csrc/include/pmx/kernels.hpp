@@ -168,8 +168,13 @@ struct PersistWs {
 constexpr size_t kPersistPolled = 64;
 template <typename T>
 int launch_pcg1_persist(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1, PcgState* S,
-                        PersistWs* ws, const TileCfg& tc, int nwg, long long k_end, const double* weights,
-                        hipStream_t s);
+                        PersistWs* ws, const TileCfg& tc, const Pcg1Slot* sched, const int* offs, int nwg,
+                        long long k_end, const double* weights, hipStream_t s);
+// The persistent kernel's static schedule: tc's tiles (tc.order0, with their row classes) onto
+// `nwaves` waves, longest first onto the least loaded wave, a cut row costing cut_row_cost row steps
+// more; d_sched (tc.ntiles() slots) lists wave 0's tiles, then wave 1's ..., d_offs (nwaves + 1)
+// where each wave's list starts.
+void pcg1_persist_schedule(const TileCfg& tc, int nwaves, double cut_row_cost, Pcg1Slot* d_sched, int* d_offs);
 int pcg1_persist_max_wg(int device);  // workgroups that are always co-resident (one per CU)
 // PMX_PERSIST_TRACE=k: stamps of sweep k of the last launch -- 2 per wave (march start, end), then 2
 // per workgroup (barrier arrival, exit); wall_clock64 ticks (100 MHz)

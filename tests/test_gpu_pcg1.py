@@ -306,10 +306,13 @@ def test_loopback_rank_runs_the_real_schedule(pkg, native, rank, split):
     assert s.comm_name == "loopback" and s.split_sweep
     assert s.direct_rows == (split == "rows")
     s.init()
-    it0 = s.state(0)["it"]
+    s.step(16)  # warmup, as bench.py --loopback-rank
+    s.synchronize()
+    st0 = s.state(0)
+    assert st0["it"] == 17 and not st0["done"], st0
     s.prepare(48)
     s.reset_path_stats()
     s.step(48)
     s.synchronize()
     st = s.state(0)
-    assert s.path_stats()["graph_iters"] == 48 and st["it"] - it0 == 48 and not st["done"]
+    assert s.path_stats()["graph_iters"] == 48 and st["it"] - st0["it"] == 48 and not st["done"], st
