@@ -139,12 +139,12 @@ def parse(argv=None):
                     help="supervisor: hard limit (s) for one rung's processes (0 = RUNG_CAP per rung)")
     ap.add_argument("--ladder-budget", type=float, default=LADDER_BUDGET,
                     help="supervisor: wall-clock budget (s) of the whole ladder")
-    ap.add_argument("--placement", type=int, default=8,
+    ap.add_argument("--placement", type=int, default=16,
                     help="placement probe: candidate field blocks timed, the fastest kept (0 = off; "
                          "bounded by --placement-budget and --placement-keep-free; off when ranks share a GPU)")
     ap.add_argument("--persistent", default="auto", choices=["auto", "on", "off"],
                     help="persistent iteration (one launch per batch, in-kernel grid barrier + reduction): auto = "
-                         "fp64 single-subdomain grids whose fields fit the Infinity Cache (<= 192 MB)")
+                         "fp64 single-subdomain grids whose fields fit the Infinity Cache (<= 64 MB, ~1.6 M points)")
     ap.add_argument("--loopback-rank", type=int, default=-1,
                     help="timing rehearsal on ONE GPU (valid=false): rank R of the --gpus-rank decomposition "
                          "alone, ghosts filled by device copies of the real sizes (from zeros), all-reduce "
@@ -805,8 +805,9 @@ def measure_loopback(args) -> int:
         "value": round(dt / args.steps * 1e6, 2), "unit": "us/iteration", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 4), "higher_is_better": False,
         "dtype": args.dtype,
-        "data": f"loopback: rank {args.loopback_rank} of {args.gpus} alone, ghosts copied from a zero buffer "
-                "(Dirichlet), no all-reduce",
+        "data": f"loopback: rank {args.loopback_rank} of {args.gpus} alone, ghosts written as zeros (Dirichlet) "
+                "by one fill launch per exchange; all-reduce and transfer stand-ins: "
+                f"{os.environ.get('PMX_LOOPBACK_AR_US', '0')} / {os.environ.get('PMX_LOOPBACK_HALO_US', '0')} us",
         "config": {"grid": [args.M, args.N], "world": args.gpus, "rank": args.loopback_rank, "split": args.split,
                    "process_grid": list(s.grid), "subdomain": [sd["nx"], sd["ny"]], "comm": s.comm_name,
                    "split_sweep": bool(s.split_sweep), "direct_rows": bool(s.direct_rows), "tile": tile,

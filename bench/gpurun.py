@@ -377,6 +377,48 @@ STUDIES["r4c"] = [
                        "-o run -- python3 bench.py --gpus 8 --loopback-rank 3 --steps 300 --warmup 30"),
     ("tl_strip3_sum", 60, "python3 bench/loopback_timeline.py gpurun_out/r4c/tl_strip3"),
 ]
+# round 4, third contact: the suite, the persistent kernel with cut-row carry + LPT schedule, the
+# loopback rank with one fill launch per exchange: split sweep vs halo-under-all-reduce, with and
+# without transfer / all-reduce stand-in delays; then the placement counter passes
+_LB = "--gpus 8 --loopback-rank 3 --steps 300 --warmup 30"
+_LB5 = "--gpus 8 --loopback-rank 5 --split reference --steps 300 --warmup 30"
+_DELAY = "env PMX_LOOPBACK_AR_US=15 PMX_LOOPBACK_HALO_US=20 "
+STUDIES["suite"] = [("pytest_gpu", 1000, f"{PYTEST} tests -m gpu")]
+STUDIES["r4d"] = [
+    ("persist_trace", 200, "python3 -u bench/probe/persist_trace.py 800x1200 1600x2400 2400x3200"),
+    ("lb3_split", 120, bench(_LB)),
+    ("lb3_nosplit", 120, "env PMX_PCG1_SPLIT=0 " + bench(_LB)),
+    ("lb3_split_d", 120, _DELAY + bench(_LB)),
+    ("lb3_nosplit_d", 120, _DELAY + "PMX_PCG1_SPLIT=0 " + bench(_LB)),
+    ("lb3_packed_nosplit_d", 120, _DELAY + "PMX_PCG1_SPLIT=0 PMX_DIRECT_ROWS=0 " + bench(_LB)),
+    ("lb5_split", 120, bench(_LB5)),
+    ("lb5_nosplit", 120, "env PMX_PCG1_SPLIT=0 " + bench(_LB5)),
+    ("lb5_nosplit_d", 120, _DELAY + "PMX_PCG1_SPLIT=0 " + bench(_LB5)),
+    ("block_alone", 200, bench("--gpus 1 --M 8192 --N 4096 --steps 300 --warmup 30 --no-tol-solve")),
+    ("tl_lb3", 200, "rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r4d/tl_lb3 -o run -- "
+                    "python3 bench.py " + _LB),
+    ("tl_lb3_sum", 60, "python3 bench/loopback_timeline.py gpurun_out/r4d/tl_lb3"),
+] + placement_pmc_steps("r4d")
+
+# the split sweep without the pack join (direct rows), then the suite
+STUDIES["r4e"] = [
+    ("lb3_split", 120, bench(_LB)),
+    ("lb3_split_d", 120, _DELAY + bench(_LB)),
+    ("lb5_split", 120, bench(_LB5)),
+    ("pytest_gpu", 900, f"{PYTEST} tests -m gpu"),
+]
+
+STUDIES["r4f"] = [
+    ("pytest_gpu", 600, f"{PYTEST} tests -m gpu"),
+    ("persist_pf2", 150, "env PMX_PCG1_PF=2 python3 -u bench/probe/persist_trace.py 800x1200 1600x2400"),
+    ("phases_800", 120, bench("--gpus 1 --M 800 --N 1200 --steps 200 --warmup 20 --profile-phases 200")),
+    ("phases_1600", 120, bench("--gpus 1 --M 1600 --N 2400 --steps 200 --warmup 20 --profile-phases 200")),
+    ("phases_2400", 120, bench("--gpus 1 --M 2400 --N 3200 --steps 200 --warmup 20 --profile-phases 200")),
+    ("tl_800", 120, "rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r4f/tl_800 -o run -- "
+                    "python3 bench.py --gpus 1 --M 800 --N 1200 --steps 300 --warmup 30 --persistent off --no-tol-solve"),
+    ("tl_800_sum", 60, "python3 bench/loopback_timeline.py gpurun_out/r4f/tl_800"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

@@ -19,6 +19,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <sstream>
@@ -136,31 +138,60 @@ void rccl_halo_calls(GpuSubdomainSolver* s, ncclComm_t comm, hipStream_t stream)
 }
 
 // See make_loopback_comm.
+// Loopback exchange: ONE launch writes every receive span of the exchange, a workgroup per
+// message -- the shape of an RCCL send/recv group (one kernel, a channel block per peer), not of
+// per-message blits, which queue hundreds of workgroups behind a running sweep (profiles/r4/loopback).
+// `delay` (100 MHz ticks, PMX_LOOPBACK_HALO_US) holds each block resident first, standing in for
+// the xGMI transfer; the all-reduce stand-in (PMX_LOOPBACK_AR_US) is the same kernel with no spans.
+struct LoopbackSpans {
+  unsigned* dst[2 * kHaloSlots];
+  unsigned words[2 * kHaloSlots];
+  int n;
+  unsigned long long delay;
+};
+
+__global__ void __launch_bounds__(256) k_loopback_fill(LoopbackSpans sp) {
+  if (sp.delay) {
+    const unsigned long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < sp.delay) __builtin_amdgcn_s_sleep(8);
+  }
+  if (int(blockIdx.x) >= sp.n) return;
+  unsigned* d = sp.dst[blockIdx.x];
+  const unsigned n = sp.words[blockIdx.x];
+  for (unsigned i = threadIdx.x; i < n; i += blockDim.x) d[i] = 0u;  // Dirichlet zero ghosts
+}
+
+unsigned long long loopback_ticks(const char* env) {
+  const char* v = std::getenv(env);
+  return v && v[0] ? static_cast<unsigned long long>(std::atof(v) * 100.0) : 0ull;  // 100 MHz clock
+}
+
 class LoopbackComm final : public Comm {
  public:
-  ~LoopbackComm() override {
-    if (zeros_) (void)hipFree(zeros_);
+  void allreduce(std::vector<GpuSubdomainSolver*>&, int, std::vector<hipStream_t>& streams) override {
+    if (!ar_delay_) return;
+    LoopbackSpans sp{};
+    sp.delay = ar_delay_;
+    hipLaunchKernelGGL(k_loopback_fill, dim3(1), dim3(64), 0, streams[0], sp);
+    HIP_CHECK(hipGetLastError());
   }
-  void allreduce(std::vector<GpuSubdomainSolver*>&, int, std::vector<hipStream_t>&) override {}
   void halo(std::vector<GpuSubdomainSolver*>& local, std::vector<hipStream_t>& streams) override {
     PMX_CHECK(local.size() == 1, "the loopback comm stands for one rank");
     const HaloMsgs ms = local[0]->halo_msgs();
     const size_t elem = local[0]->layout().elem;
-    size_t need = 0;
-    for (int q = 0; q < ms.n; ++q) need = std::max(need, size_t(ms.m[q].count) * elem);
-    if (need > zeros_bytes_) {  // first exchange: init(), never inside a graph capture
-      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-      HIP_CHECK(hipStreamIsCapturing(streams[0], &cs));
-      PMX_CHECK(cs == hipStreamCaptureStatusNone, "loopback: first exchange inside a graph capture");
-      if (zeros_) HIP_CHECK(hipFree(zeros_));
-      HIP_CHECK(hipMalloc(&zeros_, need));
-      HIP_CHECK(hipMemset(zeros_, 0, need));
-      zeros_bytes_ = need;
-    }
+    LoopbackSpans sp{};
+    sp.delay = halo_delay_;
     // every ghost becomes a Dirichlet zero: each rank solves a well-posed problem on its own block
-    for (int q = 0; q < ms.n; ++q)
-      HIP_CHECK(hipMemcpyAsync(ms.m[q].recv, zeros_, size_t(ms.m[q].count) * elem, hipMemcpyDeviceToDevice,
-                               streams[0]));
+    for (int q = 0; q < ms.n; ++q) {
+      const size_t bytes = size_t(ms.m[q].count) * elem;
+      PMX_CHECK(bytes % 4 == 0 && reinterpret_cast<uintptr_t>(ms.m[q].recv) % 4 == 0,
+                "loopback: receive span not word aligned");
+      sp.dst[sp.n] = static_cast<unsigned*>(ms.m[q].recv);
+      sp.words[sp.n++] = static_cast<unsigned>(bytes / 4);
+    }
+    if (sp.n == 0) return;
+    hipLaunchKernelGGL(k_loopback_fill, dim3(sp.n), dim3(256), 0, streams[0], sp);
+    HIP_CHECK(hipGetLastError());
   }
   bool prefers_split() const override { return true; }  // as RCCL
   bool direct_rows() const override { return true; }
@@ -168,8 +199,8 @@ class LoopbackComm final : public Comm {
   int world_size() const override { return 1; }
 
  private:
-  void* zeros_ = nullptr;
-  size_t zeros_bytes_ = 0;
+  unsigned long long halo_delay_ = loopback_ticks("PMX_LOOPBACK_HALO_US");
+  unsigned long long ar_delay_ = loopback_ticks("PMX_LOOPBACK_AR_US");
 };
 
 // One local rank of an RcclComm, driven by its own host thread: its collectives need no

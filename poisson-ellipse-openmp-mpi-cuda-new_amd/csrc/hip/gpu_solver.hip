@@ -268,10 +268,14 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   }
 
   if (pcg1_) {
-    // persistent iteration: latency-bound grids whose fields sit in the 256 MB Infinity Cache
+    // persistent iteration: latency-bound grids whose fields sit in the 256 MB Infinity Cache.  Auto
+    // only up to ~1.6 M points: 800x1200 46.6 vs 49.7 us/iter for the graph replays, but 1600x2400
+    // 70.6 vs 61.0 and 2400x3200 117 vs 91 -- with one 8-wave workgroup per CU (LDS) each wave's
+    // row march is latency-serial, and past ~2 tiles per wave the replays' occupancy wins
+    // (profiles/r4/persist/)
     const bool eligible = G.nb == 0 && elem_ == 8 && !opt.check;
     PMX_CHECK(opt_.persistent != 1 || eligible, "the persistent iteration needs fp64 and an undecomposed grid");
-    persist_ = eligible && (opt_.persistent == 1 || (opt_.persistent == -1 && 5.0 * double(field_bytes_) <= 192e6));
+    persist_ = eligible && (opt_.persistent == 1 || (opt_.persistent == -1 && 5.0 * double(field_bytes_) <= 64e6));
   }
   if (persist_) {
     pwg_ = pcg1_persist_max_wg(opt.device);
@@ -1161,7 +1165,14 @@ void PcgDriver::enqueue_split_iteration() {
     local_[i]->enqueue_reduce_a(streams_[i]);
   }
   comm_->allreduce(local_, 2, streams_);
-  for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipStreamWaitEvent(streams_[i], ev_pk_[u], 0)); });
+  // Packed slots: sweep k+1 rewrites the edge lines the pack of sweep k reads.  Direct rows have no
+  // pack: the exchange sends rows 1-2 / nx-1..nx of r_{k+1}, p_{k+1} in place and receives into
+  // their ghost rows; sweep k+1 writes the other parity (r_{k+2}, p_{k+2}), its interior tiles read
+  // no ghost row, and its frame tiles wait for ev_halo -- so the compute stream needs no join here
+  // and the next interior starts right after the all-reduce (one cross-queue wait per iteration
+  // instead of two: loopback strip 3 of 8, profiles/r4/loopback/).
+  if (!direct_)
+    for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipStreamWaitEvent(streams_[i], ev_pk_[u], 0)); });
 }
 
 void PcgDriver::join_halo() {
