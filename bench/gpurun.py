@@ -121,6 +121,9 @@ PMC_PASSES = {
     "sq2": "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY SQ_WAIT_ANY "
            "SQ_INST_LEVEL_VMEM SQ_IFETCH SQ_INSTS_VALU_FMA_F64",
     "lat": "TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE GRBM_COUNT",
+    "icache": "SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE",
+    "sq3": "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY "
+           "SQ_IFETCH",
 }
 
 
@@ -417,6 +420,49 @@ STUDIES["r4f"] = [
     ("tl_800", 120, "rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r4f/tl_800 -o run -- "
                     "python3 bench.py --gpus 1 --M 800 --N 1200 --steps 300 --warmup 30 --persistent off --no-tol-solve"),
     ("tl_800_sum", 60, "python3 bench/loopback_timeline.py gpurun_out/r4f/tl_800"),
+]
+
+# instruction supply: k_pcg1 is ~350 KB of code per variant (the I-cache is 64 KB per 2 CUs); is
+# the march fetch-bound?  16384^2 and 800x1200 (graph path), counters per dispatch
+_SMALL = "--M 800 --N 1200 --steps 30 --warmup 3 --graph-batch 0 --no-tol-solve --persistent off"
+STUDIES["r4g"] = (pmc_study("r4g", {"big": ""}, PMC_ARGS + " --placement 0", ("icache", "sq3"))[:-1]
+                  + pmc_study("r4g", {"small": ""}, _SMALL, ("icache", "sq3"))[:-1]
+                  + [("summary_big", 60, "python3 bench/pmc_summary.py gpurun_out/r4g --n 16384"),
+                     ("summary_small", 60, "python3 bench/pmc_summary.py gpurun_out/r4g --n 1000"),
+                     ("pytest_gpu", 700, f"{PYTEST} tests -m gpu")])
+
+# latency-bound grids: shorter tiles = more waves and fewer serial row steps per wave
+_G8 = "--gpus 1 --M 800 --N 1200 --steps 500 --warmup 50 --no-tol-solve"
+_G16 = "--gpus 1 --M 1600 --N 2400 --steps 500 --warmup 50 --no-tol-solve"
+STUDIES["r4h"] = [
+    ("g800_rows4", 60, bench(_G8 + " --persistent off")),
+    ("g800_rows2", 60, "env PMX_PCG1_ROWS=2 PMX_PCG1_ROWS_W=2 " + bench(_G8 + " --persistent off")),
+    ("g800_rows1", 60, "env PMX_PCG1_ROWS=1 PMX_PCG1_ROWS_W=1 " + bench(_G8 + " --persistent off")),
+    ("p800", 60, bench(_G8)),
+    ("p800_rows2", 60, "env PMX_PERSIST_ROWS=2 " + bench(_G8)),
+    ("g1600_rows8", 60, bench(_G16 + " --persistent off")),
+    ("g1600_rows4", 60, "env PMX_PCG1_ROWS=4 PMX_PCG1_ROWS_W=4 " + bench(_G16 + " --persistent off")),
+    ("g1600_rows2", 60, "env PMX_PCG1_ROWS=2 PMX_PCG1_ROWS_W=2 " + bench(_G16 + " --persistent off")),
+    ("phases_800", 120, bench("--gpus 1 --M 800 --N 1200 --steps 200 --warmup 20 --profile-phases 200")),
+    ("phases_1600", 120, bench("--gpus 1 --M 1600 --N 2400 --steps 200 --warmup 20 --profile-phases 200")),
+    ("phases_2400", 120, bench("--gpus 1 --M 2400 --N 3200 --steps 200 --warmup 20 --profile-phases 200")),
+    ("pytest_gpu", 700, f"{PYTEST} tests -m gpu"),
+]
+
+_G4 = "--gpus 1 --M 400 --N 600 --steps 500 --warmup 50 --no-tol-solve"
+_G24 = "--gpus 1 --M 2400 --N 3200 --steps 500 --warmup 50 --no-tol-solve"
+STUDIES["r4i"] = [
+    ("g400", 60, bench(_G4 + " --persistent off")),
+    ("p400", 60, bench(_G4 + " --persistent on")),
+    ("g800", 60, bench(_G8 + " --persistent off")),
+    ("p800", 60, bench(_G8 + " --persistent on")),
+    ("g1600", 60, bench(_G16 + " --persistent off")),
+    ("g2400", 60, bench(_G24 + " --persistent off")),
+    ("g400_b", 60, bench(_G4 + " --persistent off")),
+    ("p400_b", 60, bench(_G4 + " --persistent on")),
+    ("g800_b", 60, bench(_G8 + " --persistent off")),
+    ("p800_b", 60, bench(_G8 + " --persistent on")),
+    ("pytest_gpu", 700, f"{PYTEST} tests -m gpu"),
 ]
 
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),

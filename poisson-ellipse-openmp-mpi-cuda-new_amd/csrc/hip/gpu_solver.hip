@@ -280,10 +280,11 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   if (persist_) {
     pwg_ = pcg1_persist_max_wg(opt.device);
     // ~2 tiles per resident wave (the static schedule balances cut tiles against plain ones), but
-    // no shorter than 4 rows (a tile marches 4 extra rows); PMX_PERSIST_ROWS overrides
+    // no shorter than 2 rows (a tile marches 4 extra rows; 800x1200: 2 rows 43.2, 4 rows 46.5 us);
+    // PMX_PERSIST_ROWS overrides
     const int waves = pwg_ * (kPersistThreads / 64), tj = (sd.ny + 123) / 124;
     const int want_rows = std::max(1, (2 * waves + tj - 1) / tj);
-    int ti = std::max(4, (sd.nx + want_rows - 1) / want_rows);
+    int ti = std::max(2, (sd.nx + want_rows - 1) / want_rows);
     if (const char* e = std::getenv("PMX_PERSIST_ROWS"); e && e[0]) ti = std::max(1, std::atoi(e));
     tilesP_ = make_pcg1_tiles(G, 2, 1, ti, opt_.pf1 ? opt_.pf1 : 1, int(elem_));
     HIP_CHECK(hipMalloc(&tile_order_p_, 4 * size_t(tilesP_.ntiles()) * sizeof(Pcg1Slot)));
@@ -986,7 +987,8 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
   direct_ = direct;
   for (auto* s : local_) s->set_direct_rows(direct_);
   // graph_batch 0 asks for individual launches: the persistent path replaces the graph replays only
-  persistent_ = graph_batch_ > 0 && local_.size() == 1 && !any_nb && local_[0]->persistent();
+  persistent_ = graph_batch_ > 0 && local_.size() == 1 && !any_nb && comm_->world_size() == 1 &&
+                local_[0]->persistent();
   // One hardware queue per process (GPU_MAX_HW_QUEUES=1): every stream lands on it, so forking the
   // halo / frame work onto side streams cannot overlap anything -- and ROCm 7.2 segfaults inside
   // hipGraphLaunch on a captured graph with forked branches in that configuration (traced with
@@ -1442,8 +1444,11 @@ RunStats PcgDriver::solve(int poll_batches, bool do_init, int64_t ckpt_every,
   if (do_init) init();
   const double t1 = now_s();
   st.init_seconds = t1 - t0;
-  // persistent: the device stops on its own inside a launch, so long launches cost nothing extra
-  const int64_t batch = std::max(1, persistent_ ? 512 : graph_batch_ > 0 ? graph_batch_ : 16) * std::max(1, poll_batches);
+  // persistent: the device stops on its own inside a launch, so long launches cost nothing extra --
+  // but no longer than the checkpoint cadence asks for
+  int64_t base = graph_batch_ > 0 ? graph_batch_ : 16;
+  if (persistent_) base = ckpt_every > 0 && on_checkpoint ? std::clamp<int64_t>(ckpt_every, 1, 512) : 512;
+  const int64_t batch = base * std::max(1, poll_batches);
   const int64_t max_iter = local_[0]->spec().effective_max_iter();
   PcgState s = state(0);
   int64_t last_ckpt = s.it;
@@ -1472,17 +1477,26 @@ RunStats PcgDriver::solve(int poll_batches, bool do_init, int64_t ckpt_every,
 
 RunStats PcgDriver::profile_phases(int64_t n) {
   TraceRange tr("pmx:profile_phases");
-  // Eager iterations with an event after every step, all on the compute stream(s) (no overlap, so
-  // each step's time is its own).  Events on the first device's stream; on a multi-device
-  // driver the other streams are joined by the collectives.  Single pass: kernel_a = the sweep,
-  // kernel_b = 0, reduce = the 5-value reduction, allreduce = red_c, halo = pack + exchange +
-  // unpack.
+  // Eager iterations with an event after every step that enqueues work, all on the compute
+  // stream(s) (no overlap, so each step's time is its own).  Events on the first device's stream;
+  // on a multi-device driver the other streams are joined by the collectives.  Single pass:
+  // kernel_a = the sweep, kernel_b = 0, reduce = the 5-value reduction, allreduce = red_c, halo =
+  // pack + exchange + unpack.  A step with nothing to enqueue (the all-reduce of one rank, the
+  // exchange of an undecomposed grid, pcg2's second half in pcg1) records no event: two back-to-back
+  // timing events cost ~5 us of marker latency, which would otherwise show up as that bucket's time.
   RunStats st;
   HIP_CHECK(hipSetDevice(local_[0]->device()));
   hipStream_t s0 = streams_[0];
-  constexpr int kEv = 7;
-  std::vector<hipEvent_t> ev(size_t(n) * kEv + 1);
+  enum Bucket { kA, kB, kRed, kAr, kHalo };
+  const bool ar = comm_->world_size() > 1;
+  std::vector<hipEvent_t> ev(size_t(n) * 7 + 1);
+  std::vector<int> bucket(ev.size(), -1);
   for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+  size_t ne = 0;
+  auto mark = [&](int b) {
+    bucket[ne] = b;
+    HIP_CHECK(hipEventRecord(ev[ne++], s0));
+  };
   auto each = [&](auto&& f) {
     for (size_t i = 0; i < local_.size(); ++i) {
       HIP_CHECK(hipSetDevice(local_[i]->device()));
@@ -1490,47 +1504,44 @@ RunStats PcgDriver::profile_phases(int64_t n) {
     }
     HIP_CHECK(hipSetDevice(local_[0]->device()));
   };
-  HIP_CHECK(hipEventRecord(ev[0], s0));
+  mark(-1);
   for (int64_t k = 0; k < n; ++k) {
-    hipEvent_t* e = &ev[size_t(k) * kEv + 1];
     each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_kernel_a(s); });
-    HIP_CHECK(hipEventRecord(e[0], s0));
+    mark(kA);
     each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_reduce_a(s); });
-    HIP_CHECK(hipEventRecord(e[1], s0));
-    comm_->allreduce(local_, single_pass_ ? 2 : 0, streams_);
-    HIP_CHECK(hipEventRecord(e[2], s0));
-    if (!single_pass_) each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_kernel_b(s, true); });
-    HIP_CHECK(hipEventRecord(e[3], s0));
+    mark(kRed);
+    if (ar) {
+      comm_->allreduce(local_, single_pass_ ? 2 : 0, streams_);
+      mark(kAr);
+    }
     if (!single_pass_) {
+      each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_kernel_b(s, true); });
+      mark(kB);
       each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_reduce_b(s); });
-      HIP_CHECK(hipEventRecord(e[4], s0));
-      comm_->allreduce(local_, 1, streams_);
-    } else {
-      HIP_CHECK(hipEventRecord(e[4], s0));
+      mark(kRed);
+      if (ar) {
+        comm_->allreduce(local_, 1, streams_);
+        mark(kAr);
+      }
     }
-    HIP_CHECK(hipEventRecord(e[5], s0));
-    if (single_pass_) {
-      if (any_nb_) halo_exchange_pcg1(streams_, local_[0]->host_k());
-    } else {
-      comm_->halo(local_, streams_);
+    if (any_nb_) {
+      if (single_pass_) halo_exchange_pcg1(streams_, local_[0]->host_k());
+      else comm_->halo(local_, streams_);
+      mark(kHalo);
     }
-    HIP_CHECK(hipEventRecord(e[6], s0));
   }
   synchronize();
-  auto sec = [](hipEvent_t a, hipEvent_t b) {
+  double t[5] = {0, 0, 0, 0, 0};
+  for (size_t i = 1; i < ne; ++i) {
     float v = 0.f;
-    HIP_CHECK(hipEventElapsedTime(&v, a, b));
-    return double(v) * 1e-3;
-  };
-  for (int64_t k = 0; k < n; ++k) {
-    hipEvent_t* e = &ev[size_t(k) * kEv + 1];
-    hipEvent_t start = k == 0 ? ev[0] : ev[size_t(k - 1) * kEv + 1 + 6];
-    st.t_kernel_a += sec(start, e[0]);
-    st.t_reduce += sec(e[0], e[1]) + sec(e[3], e[4]);
-    st.t_allreduce += sec(e[1], e[2]) + sec(e[4], e[5]);
-    st.t_kernel_b += sec(e[2], e[3]);
-    st.t_halo += sec(e[5], e[6]);
+    HIP_CHECK(hipEventElapsedTime(&v, ev[i - 1], ev[i]));
+    t[bucket[i]] += double(v) * 1e-3;
   }
+  st.t_kernel_a = t[kA];
+  st.t_kernel_b = t[kB];
+  st.t_reduce = t[kRed];
+  st.t_allreduce = t[kAr];
+  st.t_halo = t[kHalo];
   st.t_comm = st.t_allreduce + st.t_halo;
   for (auto& e : ev) (void)hipEventDestroy(e);
   st.launched = n;

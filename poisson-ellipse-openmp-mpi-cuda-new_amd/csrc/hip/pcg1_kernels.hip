@@ -544,6 +544,11 @@ TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf, 
     // keep fewer DRAM rows in flight and win despite the 4 extra marched rows.
     rows = fp32 ? 24 : 8;
     while (rows > 4 && int64_t((G.nx + rows - 1) / rows) * t.tiles_j < 8192) rows /= 2;
+    // the reference's smallest grid (800x1200: 2000 tiles of 4 rows, ~2 waves per SIMD) is bound by
+    // one wave's serial row march: 2-row tiles double the waves and cut the march from 8 row steps
+    // to 6 -- 50.1 -> 41.6 us/iteration; 1 row (5 steps, 4x the rows marched) 47.1; at 1600x2400
+    // (8000 tiles of 4 rows) 2 rows lose, 60.8 -> 73.1 (profiles/r4/persist/rows_*.log)
+    if (rows == 4 && int64_t((G.nx + 3) / 4) * t.tiles_j < 4096) rows = 2;
   }
   PMX_CHECK(rows >= 1 && rows <= 4096, "pcg1: tile rows must be in [1, 4096]");
   t.rows = rows;

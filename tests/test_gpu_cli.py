@@ -33,9 +33,16 @@ def test_stage4_format_and_phase_buckets():
     assert any(l.startswith("M=400, N=600 | Iter=546 | Total Time=") for l in lines)
     j = last_json(out)
     assert j["iters"] == 546 and j["ranks"] == 2 and j["comm"] == "local"
-    for k in ("phase_kernel_a_s", "phase_kernel_b_s", "phase_reduce_s", "phase_allreduce_s", "phase_halo_s"):
+    # single pass: no second sweep, so its bucket is exactly 0 (no event pair around nothing)
+    for k in ("phase_kernel_a_s", "phase_reduce_s", "phase_allreduce_s", "phase_halo_s"):
         assert j[k] > 0, k
+    assert j["phase_kernel_b_s"] == 0
     assert abs(j["l2_error"] - 3.0607e-4) < 2e-7
+    # the two-sweep iteration (--exact) times its second sweep; one rank times no communication
+    j2 = last_json(run(400, 600, "--backend", "hip", "--ranks", 2, "--exact", "--profile-phases", 30, "--json"))
+    assert j2["phase_kernel_b_s"] > 0 and j2["phase_halo_s"] > 0
+    j1 = last_json(run(400, 600, "--backend", "hip", "--profile-phases", 30, "--json"))
+    assert j1["phase_allreduce_s"] == 0 and j1["phase_halo_s"] == 0 and j1["phase_kernel_a_s"] > 0
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "mixed"])
