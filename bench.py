@@ -144,7 +144,7 @@ def parse(argv=None):
                          "bounded by --placement-budget and --placement-keep-free; off when ranks share a GPU)")
     ap.add_argument("--persistent", default="auto", choices=["auto", "on", "off"],
                     help="persistent iteration (one launch per batch, in-kernel grid barrier + reduction): auto = "
-                         "fp64 single-subdomain grids whose fields fit the Infinity Cache (<= 64 MB, ~1.6 M points)")
+                         "fp64 single-subdomain grids whose fields fit the Infinity Cache (<= 16 MB, ~0.4 M points)")
     ap.add_argument("--loopback-rank", type=int, default=-1,
                     help="timing rehearsal on ONE GPU (valid=false): rank R of the --gpus-rank decomposition "
                          "alone, ghosts filled by device copies of the real sizes (from zeros), all-reduce "

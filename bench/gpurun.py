@@ -465,6 +465,37 @@ STUDIES["r4i"] = [
     ("pytest_gpu", 700, f"{PYTEST} tests -m gpu"),
 ]
 
+STUDIES["r4j"] = [
+    ("ckpt_probe", 120, "python3 -u bench/probe/ckpt_probe.py"),
+    ("pytest_gpu", 900, f"{PYTEST} tests -m gpu"),
+]
+
+# the per-rank iteration of the 2/4/8-GPU jobs on one box, against the same subdomain with no
+# neighbours (same box, same binary): middle ranks, split sweep (the RCCL default), with and
+# without the transfer / all-reduce stand-ins
+_ALONE = "--gpus 1 --steps 300 --warmup 30 --no-tol-solve --placement 0"
+STUDIES["r4k"] = [
+    ("alone_8192", 120, bench(_ALONE + " --M 8192 --N 16384")),
+    ("lb2_r0", 120, bench("--gpus 2 --loopback-rank 0 --steps 300 --warmup 30 --placement 0")),
+    ("lb2_r0_d", 120, _DELAY + bench("--gpus 2 --loopback-rank 0 --steps 300 --warmup 30 --placement 0")),
+    ("alone_4096", 120, bench(_ALONE + " --M 4096 --N 16384")),
+    ("lb4_r1", 120, bench("--gpus 4 --loopback-rank 1 --steps 300 --warmup 30 --placement 0")),
+    ("lb4_r1_d", 120, _DELAY + bench("--gpus 4 --loopback-rank 1 --steps 300 --warmup 30 --placement 0")),
+    ("alone_2048", 120, bench(_ALONE + " --M 2048 --N 16384")),
+    ("lb8_r3", 120, bench(_LB + " --placement 0")),
+    ("lb8_r3_d", 120, _DELAY + bench(_LB + " --placement 0")),
+    ("lb8_r3_nosplit", 120, "env PMX_PCG1_SPLIT=0 " + bench(_LB + " --placement 0")),
+    ("alone_2048_b", 120, bench(_ALONE + " --M 2048 --N 16384")),
+    ("lb8_r3_b", 120, bench(_LB + " --placement 0")),
+    ("tl_lb8_r3", 200, "rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r4k/tl_lb8_r3 -o run -- "
+                       "python3 bench.py " + _LB + " --placement 0"),
+    ("tl_lb8_r3_sum", 60, "python3 bench/loopback_timeline.py gpurun_out/r4k/tl_lb8_r3"),
+    ("tl_alone_2048", 200, "rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r4k/tl_alone_2048 -o run -- "
+                           "python3 bench.py " + _ALONE + " --M 2048 --N 16384"),
+    ("tl_alone_2048_sum", 60, "python3 bench/loopback_timeline.py gpurun_out/r4k/tl_alone_2048"),
+    ("pytest_gpu", 600, f"{PYTEST} tests -m gpu"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

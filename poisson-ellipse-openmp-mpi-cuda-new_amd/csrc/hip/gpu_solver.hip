@@ -269,13 +269,13 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
 
   if (pcg1_) {
     // persistent iteration: latency-bound grids whose fields sit in the 256 MB Infinity Cache.  Auto
-    // only up to ~1.6 M points: 800x1200 46.6 vs 49.7 us/iter for the graph replays, but 1600x2400
-    // 70.6 vs 61.0 and 2400x3200 117 vs 91 -- with one 8-wave workgroup per CU (LDS) each wave's
-    // row march is latency-serial, and past ~2 tiles per wave the replays' occupancy wins
-    // (profiles/r4/persist/)
+    // only up to ~0.4 M points: 400x600 35.3 vs 36.9 us/iter for the graph replays, but 800x1200
+    // 43.8 vs 41.4 (2-row tiles both), 1600x2400 70.6 vs 61.0 -- with one 8-wave workgroup per CU
+    // (LDS) each wave's row march is latency-serial, and once the grid has more tiles than resident
+    // waves the replays' occupancy wins (profiles/r4/persist/)
     const bool eligible = G.nb == 0 && elem_ == 8 && !opt.check;
     PMX_CHECK(opt_.persistent != 1 || eligible, "the persistent iteration needs fp64 and an undecomposed grid");
-    persist_ = eligible && (opt_.persistent == 1 || (opt_.persistent == -1 && 5.0 * double(field_bytes_) <= 64e6));
+    persist_ = eligible && (opt_.persistent == 1 || (opt_.persistent == -1 && 5.0 * double(field_bytes_) <= 16e6));
   }
   if (persist_) {
     pwg_ = pcg1_persist_max_wg(opt.device);

@@ -37,13 +37,14 @@ def test_persistent_goldens(pkg, grid, iters):
 
 
 def test_auto_choice(pkg):
-    assert _sess(pkg, 800, 1200, -1).persistent            # 38 MB of fields: Infinity Cache
-    assert not _sess(pkg, 800, 1200, 0).persistent
-    assert not _sess(pkg, 800, 1200, -1, graph_batch=0).persistent  # individual launches asked for
-    assert not _sess(pkg, 1600, 2400, -1).persistent       # 154 MB: the graph replays' occupancy wins
+    assert _sess(pkg, 400, 600, -1).persistent             # 10 MB of fields: one launch per batch
+    assert not _sess(pkg, 400, 600, 0).persistent
+    assert not _sess(pkg, 400, 600, -1, graph_batch=0).persistent  # individual launches asked for
+    assert not _sess(pkg, 800, 1200, -1).persistent        # 38 MB: the graph replays' occupancy wins
+    assert _sess(pkg, 800, 1200, 1).persistent             # ... but it runs there when asked for
     assert not _sess(pkg, 3000, 4000, -1).persistent       # 480 MB of fields: bandwidth-bound, graphs
-    assert not _sess(pkg, 800, 1200, -1, ranks=4).persistent  # decomposed: LocalComm graphs
-    assert not _sess(pkg, 800, 1200, -1, dtype="fp32").persistent
+    assert not _sess(pkg, 400, 600, -1, ranks=4).persistent  # decomposed: LocalComm graphs
+    assert not _sess(pkg, 400, 600, -1, dtype="fp32").persistent
 
 
 @pytest.mark.parametrize("grid", [(400, 600), (800, 1200), (97, 130)])
