@@ -496,9 +496,27 @@ STUDIES["r4k"] = [
     ("pytest_gpu", 600, f"{PYTEST} tests -m gpu"),
 ]
 
+PYTEST_ALL = "python -u -m pytest -v --timeout 170 --timeout-method thread"
+STUDIES["r4l"] = [
+    ("threaded_failure_alone", 120, f"{PYTEST} tests/test_gpu_solver.py -m gpu -k threaded_failure"),
+    ("block_alone", 120, bench(_ALONE + " --M 8192 --N 4096")),
+    ("lb5_split", 120, bench(_LB5 + " --placement 0")),
+    ("lb5_split_d", 120, _DELAY + bench(_LB5 + " --placement 0")),
+    ("lb8_r3", 120, bench(_LB + " --placement 0")),
+    ("pytest_gpu_all", 800, f"{PYTEST_ALL} tests -m gpu"),
+]
+
+STUDIES["r4m"] = [
+    ("fixed", 200, f"{PYTEST} tests/test_gpu_solver.py tests/test_gpu_launch_path.py -m gpu "
+                   "-k 'threaded_failure or progress_counters or serialized or comm_sequence'"),
+    ("pytest_gpu_all", 800, f"{PYTEST_ALL} tests -m gpu"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [
+    ("bench_driver_1", 300, bench("--gpus 1 --steps 20 --warmup 5")),
+    ("bench_driver_2", 300, bench("--gpus 1 --steps 20 --warmup 5")),
     ("phases_800", 200, bench("--gpus 1 --M 800 --N 1200 --steps 200 --warmup 20 --profile-phases 200")),
     ("phases_1600", 200, bench("--gpus 1 --M 1600 --N 2400 --steps 200 --warmup 20 --profile-phases 200")),
     ("phases_2400", 200, bench("--gpus 1 --M 2400 --N 3200 --steps 200 --warmup 20 --profile-phases 200")),

@@ -397,8 +397,20 @@ PYBIND11_MODULE(_pmx, m) {
            py::arg("check") = false, py::arg("vec_b") = 0, py::arg("waves_b") = 0,
            py::arg("tile_rows_b") = -1, py::arg("b_ring") = false, py::arg("algo") = -1)
       .def("enqueue_init", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_init(as_stream(s)); })
-      .def("enqueue_halo_pack", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_halo_pack(as_stream(s)); })
-      .def("enqueue_halo_unpack", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_halo_unpack(as_stream(s)); })
+      // pcg1: the exchange's target sweep (its buffer parity); default: the sweep the host enqueues
+      // next (host_k, bumped by each reduction) -- what PcgDriver passes
+      .def("enqueue_halo_pack",
+           [](GpuSubdomainSolver& g, uintptr_t s, long long target) {
+             g.set_halo_target(target < 0 ? g.host_k() : target);
+             g.enqueue_halo_pack(as_stream(s));
+           },
+           py::arg("stream"), py::arg("target") = -1)
+      .def("enqueue_halo_unpack",
+           [](GpuSubdomainSolver& g, uintptr_t s, long long target) {
+             g.set_halo_target(target < 0 ? g.host_k() : target);
+             g.enqueue_halo_unpack(as_stream(s));
+           },
+           py::arg("stream"), py::arg("target") = -1)
       .def_property_readonly("single_pass", &GpuSubdomainSolver::single_pass)
       .def("enqueue_phase_a", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_phase_a(as_stream(s)); })
       .def("enqueue_kernel_a", [](GpuSubdomainSolver& g, uintptr_t s) { g.enqueue_kernel_a(as_stream(s)); })

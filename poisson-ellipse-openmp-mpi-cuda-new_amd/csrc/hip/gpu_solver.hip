@@ -587,7 +587,7 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
 template <typename T>
 void GpuSubdomainSolver::halo_impl(hipStream_t s, bool unpack) {
   launch_pcg1_halo<T>(geom_, static_cast<T*>(field_base(1)), reinterpret_cast<T*>(r2_ + field_off_ * elem_),
-                      static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(), state_,
+                      static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(), halo_target_,
                       unpack, s, progress_dev_);
   after_launch(s);
 }
@@ -1042,7 +1042,6 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
       ev(ev_ar_);
       ev(ev_fdone_);
       ev(ev_swept_);
-      ev(ev_pk_);
     }
     if (same_device) frame_streams_.resize(local_.size(), frame_streams_[0]);
   }
@@ -1058,7 +1057,7 @@ PcgDriver::~PcgDriver() {
       last = s;
     }
   }
-  for (auto* v : {&ev_packed_, &ev_halo_, &ev_ar_, &ev_fdone_, &ev_swept_, &ev_pk_})
+  for (auto* v : {&ev_packed_, &ev_halo_, &ev_ar_, &ev_fdone_, &ev_swept_})
     for (auto e : *v) (void)hipEventDestroy(e);
 }
 
@@ -1125,8 +1124,8 @@ void PcgDriver::halo_exchange_pcg1(std::vector<hipStream_t>& streams, long long 
 // Split sweep k (pcg1, decomposed, overlap on).  Streams C (compute), F (frame), H (comm):
 //   C: [all-reduce k-1] -> ev_ar -> interior tiles of sweep k ----------> wait F -> ev_swept ->
 //   F:                     wait ev_ar (+ ev_halo of k-1) -> frame tiles -'
-//   C: reduce -> all-reduce k -> wait ev_pk (the next sweep rewrites halo_k, which the pack reads)
-//   H: wait ev_swept -> pack -> ev_pk -> send/recv -> unpack -> ev_halo (joined by the next F, or
+//   C: reduce -> all-reduce k (no join: see the end of enqueue_split_iteration)
+//   H: wait ev_swept -> pack -> send/recv -> unpack -> ev_halo (joined by the next F, or
 //      by C at the end of the batch: join_halo)
 // So the ghost exchange of sweep k runs under the reduction, the all-reduce AND the interior of
 // sweep k+1; only the frame tiles (a few % of the sweep) wait for it.
@@ -1147,13 +1146,12 @@ void PcgDriver::enqueue_split_iteration() {
     HIP_CHECK(hipEventRecord(ev_swept_[u], streams_[i]));
     HIP_CHECK(hipStreamWaitEvent(comm_streams_[i], ev_swept_[u], 0));
   });
+  set_halo_target(local_[0]->host_k() + 1);  // the sweep just enqueued is host_k; the next reads its outputs
   comm_->before_pack(local_, comm_streams_);
   for (size_t i = 0; i < local_.size(); ++i) {
     HIP_CHECK(hipSetDevice(local_[i]->device()));
     local_[i]->enqueue_halo_pack(comm_streams_[i]);
   }
-  for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipEventRecord(ev_pk_[u], comm_streams_[i])); });
-  set_halo_target(local_[0]->host_k() + 1);  // the sweep just enqueued is host_k; the next reads its outputs
   poison(comm_streams_);
   comm_->halo(local_, comm_streams_);
   for (size_t i = 0; i < local_.size(); ++i) {
@@ -1167,14 +1165,13 @@ void PcgDriver::enqueue_split_iteration() {
     local_[i]->enqueue_reduce_a(streams_[i]);
   }
   comm_->allreduce(local_, 2, streams_);
-  // Packed slots: sweep k+1 rewrites the edge lines the pack of sweep k reads.  Direct rows have no
-  // pack: the exchange sends rows 1-2 / nx-1..nx of r_{k+1}, p_{k+1} in place and receives into
-  // their ghost rows; sweep k+1 writes the other parity (r_{k+2}, p_{k+2}), its interior tiles read
-  // no ghost row, and its frame tiles wait for ev_halo -- so the compute stream needs no join here
-  // and the next interior starts right after the all-reduce (one cross-queue wait per iteration
-  // instead of two: loopback strip 3 of 8, profiles/r4/loopback/).
-  if (!direct_)
-    for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipStreamWaitEvent(streams_[i], ev_pk_[u], 0)); });
+  // No join of the comm stream here: the exchange (packed or direct rows) reads the edge lines of
+  // r_{k+1}, p_{k+1} and writes their ghost cells, with the buffer parity in its launch arguments;
+  // sweep k+1 writes the other parity (r_{k+2}, p_{k+2}), its interior tiles read no ghost cell and
+  // its frame tiles wait for ev_halo.  Sweep k+2, the next writer of these buffers, follows the
+  // all-reduce of k+1, which follows that frame.  So the next interior starts right after the
+  // all-reduce: one cross-queue wait per iteration instead of two (loopback strip 3 of 8: 293 ->
+  // 266 us, profiles/r4/loopback/).
 }
 
 void PcgDriver::join_halo() {
@@ -1406,6 +1403,9 @@ void PcgDriver::enqueue_eager(int64_t n) {
 void PcgDriver::enqueue_iterations(int64_t n) {
   TraceRange tr("pmx:enqueue_iterations");
   if (persistent_) {
+    // the launch makes no communicator call (world 1), so an aborted one is caught here, as every
+    // other path's first collective would
+    comm_->check_health();
     HIP_CHECK(hipSetDevice(local_[0]->device()));
     local_[0]->enqueue_persistent(streams_[0], n);
     path_.persistent_iters += n;

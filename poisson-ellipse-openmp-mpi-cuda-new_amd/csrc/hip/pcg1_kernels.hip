@@ -320,24 +320,23 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
 }
 
 // Radius-2 ghost exchange of the single-pass iteration (see the header): pack (unpack = 0) copies
-// the owned edge lines of the buffers the NEXT sweep reads -- sweep S->halo_k reads
-// r^{k-1} = (k & 1 ? r2 : r) and p^{k-1} = (k & 1 ? p0 : p1) -- into the send slots; unpack copies
-// the receive slots into the ghost cells of the same buffers.  Slot layout: sides
+// the owned edge lines of the buffers the NEXT sweep reads -- sweep kk (the exchange's target,
+// known on the host and baked into captured graphs, which are therefore keyed by its parity) reads
+// r^{k-1} = (kk & 1 ? r2 : r) and p^{k-1} = (kk & 1 ? p0 : p1) -- into the send slots; unpack
+// copies the receive slots into the ghost cells of the same buffers.  No device state is read, so
+// the next sweep (which writes S) never has to wait for a pack.  Slot layout: sides
 // [field][line][pos] (field 0 = r, 1 = p; line q = ghost row/column -1+q on the receiving side,
 // ordered by increasing index), corners [field].  Grid: (ceil(max(nx, ny) / 256), 8 slots,
 // 4 = (field, line)).  Tiny and stream-ordered; launched by the driver between two sweeps.
 template <typename T>
 __global__ void __launch_bounds__(256)
-k_pcg1_halo(DevGeom G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, PcgState* S, int unpack,
+k_pcg1_halo(DevGeom G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, long long kk, int unpack,
             long long* progress) {
   const int slot = blockIdx.y;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0) {
-    if (!unpack) S->halo_k_unpack = S->halo_k;  // see PcgState::halo_k_unpack
-    // host-visible progress (hang diagnosis): [1] = exchanges packed, [2] = exchanges unpacked
-    if (progress)
-      __hip_atomic_store(progress + (unpack ? 2 : 1), (unpack ? S->halo_k_unpack : S->halo_k) + 1,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  // host-visible progress (hang diagnosis): [1] = exchanges packed, [2] = exchanges unpacked --
+  // counted, since kk is baked into graphs that replay at later iterations of the same parity
+  if (progress && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0)
+    __hip_atomic_fetch_add(progress + (unpack ? 2 : 1), 1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (!((G.nb >> slot) & 1)) return;
   const int f = blockIdx.z >> 1, q = blockIdx.z & 1;
   const int t = blockIdx.x * 256 + threadIdx.x;
@@ -360,7 +359,6 @@ k_pcg1_halo(DevGeom G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, PcgState* S, in
     lj = yhi ? (unpack ? ny + 1 : ny) : (unpack ? 0 : 1);
     idx = f;
   }
-  const long long kk = unpack ? S->halo_k_unpack : S->halo_k;
   T* fld = f == 0 ? ((kk & 1) ? r2 : r) : ((kk & 1) ? p0 : p1);
   const int64_t o = int64_t(li) * G.pitch + lj;
   if (unpack)
@@ -618,12 +616,12 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
 }
 
 template <typename T>
-void launch_pcg1_halo(const DevGeom& G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, PcgState* S,
+void launch_pcg1_halo(const DevGeom& G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, long long target,
                       bool unpack, hipStream_t s, long long* progress) {
   if (G.nb == 0) return;
   const int len = std::max(G.nx, G.ny);
   hipLaunchKernelGGL(k_pcg1_halo<T>, dim3((len + 255) / 256, kHaloSlots, 4), dim3(256), 0, s, G, r, r2,
-                     p0, p1, H, S, unpack ? 1 : 0, progress);
+                     p0, p1, H, target, unpack ? 1 : 0, progress);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -656,9 +654,9 @@ void* pcg1_wave_trace_setup(long long it, int nwaves) {
 template void launch_pcg1<double>(const DevGeom&, const DevTables&, double*, double*, double*, double*,
                                   double*, double*, PcgState*, const TileCfg&, hipStream_t, int, bool);
 template void launch_pcg1_halo<double>(const DevGeom&, double*, double*, double*, double*, HaloBufs<double>,
-                                        PcgState*, bool, hipStream_t, long long*);
+                                        long long, bool, hipStream_t, long long*);
 template void launch_pcg1_halo<float>(const DevGeom&, float*, float*, float*, float*, HaloBufs<float>,
-                                       PcgState*, bool, hipStream_t, long long*);
+                                       long long, bool, hipStream_t, long long*);
 template void launch_pcg1<float>(const DevGeom&, const DevTables&, float*, float*, float*, float*, float*,
                                  double*, PcgState*, const TileCfg&, hipStream_t, int, bool);
 

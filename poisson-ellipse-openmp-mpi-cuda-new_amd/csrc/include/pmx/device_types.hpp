@@ -77,11 +77,10 @@ struct alignas(64) PcgState {
   // (Ap,p) (weighted) and |p|^2 (weighted per norm) of the last sweep.
   double red_c[5];
   // Single-pass halo: index of the sweep whose input buffers (r^{k-1}, p^{k-1}) the next ghost
-  // exchange fills.  Written by sweep k (= k + 1) and by init (= 0); read by the pack kernel,
-  // which the next sweep waits for.  The pack copies it to halo_k_unpack for the unpack kernel,
-  // which may still run while the next sweep's interior tiles (and their halo_k write) run.
+  // exchange fills.  Written by sweep k (= k + 1) and by init (= 0) for diagnostics; the exchange
+  // kernels take their target from the host (round 4), so nothing on the device reads it.
   long long halo_k;
-  long long halo_k_unpack;
+  long long halo_k_unpack;  // unused since round 4 (kept: checkpoint files hold PcgState)
   // Single-pass w schedule (pcg1): w is read and written on one sweep in w_cycle (2 = pairs, 3 =
   // triples, see k_pcg1).  alpha1/beta1 hold alpha_k / beta_k at slot k & 3; w_pend_n steps
   // (p^{w_pend - w_pend_n + 1} .. p^{w_pend}, both still in the two p buffers) are not yet in w.

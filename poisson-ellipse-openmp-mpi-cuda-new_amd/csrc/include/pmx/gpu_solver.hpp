@@ -486,7 +486,9 @@ class PcgDriver {
   void set_halo_target(long long k);
   // captured batches depend on the w-cycle phase of their first sweep, and with direct rows also on
   // its parity (the exchanged spans alternate between the double buffers)
-  int graph_period() const { return local_[0]->w_cycle() * (direct_ ? 2 : 1); }
+  // pcg1 with neighbours: every exchange names its target sweep's buffer parity in its launch
+  // arguments (direct spans or pack/unpack), so a captured batch is only valid at its parity
+  int graph_period() const { return local_[0]->w_cycle() * (single_pass_ && any_nb_ ? 2 : 1); }
   void enqueue_split_iteration();  // pcg1, decomposed, overlap: interior/frame sweep split
   void join_halo();                // compute stream waits for a pending ghost exchange
   // captured batch of `len` iterations starting at w-cycle phase `phase`, built on first use;
@@ -513,7 +515,7 @@ class PcgDriver {
   bool split_ = false;
   bool halo_pending_ = false;  // a ghost exchange on the comm stream not yet joined
   std::vector<hipStream_t> frame_streams_;
-  std::vector<hipEvent_t> ev_ar_, ev_fdone_, ev_swept_, ev_pk_;
+  std::vector<hipEvent_t> ev_ar_, ev_fdone_, ev_swept_;
   bool graph_failed_ = false;  // capture is not possible for this driver: eager launches
   std::vector<hipGraph_t> graphs_;
   std::vector<hipGraphExec_t> execs_;

@@ -119,14 +119,14 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
                  double* partials, PcgState* S, const TileCfg& tc, hipStream_t s, int part = 0,
                  bool wsweep = false);
 
-// pcg1 ghost exchange: pack (unpack=false) the radius-2 edges of the buffers the next sweep reads
-// (selected on the device by S->halo_k) into H.send, or unpack H.recv into their ghost cells.
+// pcg1 ghost exchange: pack (unpack=false) the radius-2 edges of the buffers sweep `target` reads
+// (parity of target) into H.send, or unpack H.recv into their ghost cells.
 #ifdef PMX_WAVE_TRACE
 void* pcg1_wave_trace_setup(long long it, int nwaves);
 #endif
 
 template <typename T>
-void launch_pcg1_halo(const DevGeom& G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, PcgState* S,
+void launch_pcg1_halo(const DevGeom& G, T* r, T* r2, T* p0, T* p1, HaloBufs<T> H, long long target,
                       bool unpack, hipStream_t s, long long* progress = nullptr);
 
 // Halo/compute overlap: r^{k+1} on the subdomain edges that have a neighbour,
@@ -148,7 +148,7 @@ void launch_reduce(const double* partials, int n, int nq, double w0, double w1, 
                    PcgState* S, int mode, double* ws, hipStream_t s);
 // the same for nq = 5 interleaved values (k_pcg1 partials), out[q] = sum_q * weights[q].
 // progress: optional host-mapped counters (GpuSubdomainSolver::progress): [0] <- S->it after the
-// bump; launch_pcg1_halo writes [1] (exchanges packed) and [2] (exchanges unpacked).
+// bump; launch_pcg1_halo counts [1] (exchanges packed) and [2] (exchanges unpacked).
 void launch_reduce_n(const double* partials, int n, int nq, const double* weights, double* out,
                      PcgState* S, int mode, double* ws, hipStream_t s, long long* progress = nullptr);
 
