@@ -648,7 +648,9 @@ def measure(args) -> int:
                   "graph" if path["eager_iters"] == 0 and path["graph_iters"] > 0 and pers == 0 else
                   "eager" if path["graph_iters"] == 0 and pers == 0 else "mixed")
     tile_desc = dict(runner.tile())
-    tile_desc.pop("placement_probe_ms", None)  # the summary ("placement") stays; the list can be long
+    probe = tile_desc.pop("placement_probe_ms", None)
+    if probe and isinstance(tile_desc.get("placement"), dict) and len(probe) <= 32:
+        tile_desc["placement"] = dict(tile_desc["placement"], probe_ms=[round(float(x), 3) for x in probe])
     valid = (not st1["done"]) and (st1["it"] - st0["it"] == args.steps) and not st1["nan"]
     pts = (args.M - 1) * (args.N - 1)
     mlups = pts * args.steps / dt / 1e6

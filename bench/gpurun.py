@@ -512,6 +512,22 @@ STUDIES["r4m"] = [
     ("pytest_gpu_all", 800, f"{PYTEST_ALL} tests -m gpu"),
 ]
 
+# the w sweep: recover p^{k-2} with an extra stencil (default) or re-read it (PMX_PAIR_W=2, +8 B/pt,
+# fewer VGPRs); both with the bounded placement probe, fresh processes
+STUDIES["r4n"] = [
+    ("ab_pairw", 600, "python -u bench/ab_env.py --fresh --shape 16384x16384 --shape 2048x16384 "
+                      "--cfg base:PMX_PLACEMENT=12 --cfg rr:PMX_PLACEMENT=12,PMX_PAIR_W=2 --rounds 4 --iters 200"),
+    ("smoke", 120, "python -c 'import __graft_entry__ as g; g.smoke()'"),
+]
+
+# placement: does the sweep rate follow the physical region the allocator reaches?  Candidates
+# allocated after a spacer of 0 / 120 / 170 / 220 GB held untouched (PMX_PLACEMENT_SPACER_GB)
+_SP = "--gpus 1 --steps 20 --warmup 5 --no-tol-solve --placement 12 --placement-budget 5 --placement-keep-free 0.02"
+STUDIES["r4o"] = [(f"sp{g}", 150, f"env PMX_PLACEMENT_SPACER_GB={g} " + bench(_SP)) for g in (0, 120, 170, 220)] + [
+    ("sp0_b", 150, "env PMX_PLACEMENT_SPACER_GB=0 " + bench(_SP)),
+    ("sp170_b", 150, "env PMX_PLACEMENT_SPACER_GB=170 " + bench(_SP)),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

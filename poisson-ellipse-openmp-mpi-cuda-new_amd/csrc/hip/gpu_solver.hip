@@ -360,6 +360,26 @@ void GpuSubdomainSolver::place_fields() {
   HIP_CHECK(hipMemGetInfo(&free0, &total_b));
   const size_t keep = std::max(size_t(double(free0) * std::clamp(opt_.placement_keep_free, 0.0, 1.0)),
                                size_t(4) << 30);
+  // study knob (PMX_PLACEMENT_SPACER_GB): hold this much memory, untouched, while the candidates
+  // are allocated -- does the rate follow the physical region the allocator reaches?
+  std::vector<char*> spacer;
+  if (const char* e = std::getenv("PMX_PLACEMENT_SPACER_GB"); e && e[0]) {
+    size_t want = size_t(std::atof(e) * double(1ull << 30));
+    while (want > 0) {
+      const size_t chunk = std::min(want, size_t(8) << 30);
+      char* p = nullptr;
+      if (hipMalloc(&p, chunk) != hipSuccess) {
+        (void)hipGetLastError();
+        break;
+      }
+      spacer.push_back(p);
+      want -= chunk;
+    }
+  }
+  struct SpacerFree {
+    std::vector<char*>& v;
+    ~SpacerFree() { for (char* p : v) (void)hipFree(p); }
+  } spacer_free{spacer};
   while (int(cand.size()) < K) {
     size_t free_b = 0;
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
