@@ -528,6 +528,19 @@ STUDIES["r4o"] = [(f"sp{g}", 150, f"env PMX_PLACEMENT_SPACER_GB={g} " + bench(_S
     ("sp170_b", 150, "env PMX_PLACEMENT_SPACER_GB=170 " + bench(_SP)),
 ]
 
+# the bench defaults after r4o: 8 candidates past a 100-GB spacer, 0.5 s of timed sweeps, 30% of
+# the free memory kept free; fresh driver-command runs + the 2-GPU per-rank block
+STUDIES["r4p2"] = [
+    ("driver_1", 300, bench("--gpus 1 --steps 20 --warmup 5")),
+    ("driver_2", 300, bench("--gpus 1 --steps 20 --warmup 5 --no-tol-solve")),
+    ("driver_3", 300, bench("--gpus 1 --steps 20 --warmup 5 --no-tol-solve")),
+    ("alone_8192", 120, bench("--gpus 1 --steps 300 --warmup 30 --no-tol-solve --M 8192 --N 16384")),
+    ("alone_8192_nosp", 120, bench("--gpus 1 --steps 300 --warmup 30 --no-tol-solve --M 8192 --N 16384 "
+                                   "--placement-spacer 0")),
+    ("fp32_16k", 200, bench("--gpus 1 --steps 20 --warmup 5 --dtype fp32 --no-tol-solve")),
+    ("mixed_32k", 300, bench("--gpus 1 --steps 20 --warmup 5 --dtype mixed --M 32768 --N 32768 --no-tol-solve")),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

@@ -360,11 +360,16 @@ void GpuSubdomainSolver::place_fields() {
   HIP_CHECK(hipMemGetInfo(&free0, &total_b));
   const size_t keep = std::max(size_t(double(free0) * std::clamp(opt_.placement_keep_free, 0.0, 1.0)),
                                size_t(4) << 30);
-  // study knob (PMX_PLACEMENT_SPACER_GB): hold this much memory, untouched, while the candidates
-  // are allocated -- does the rate follow the physical region the allocator reaches?
+  // spacer: memory held untouched while the candidates are allocated, so they come from the region
+  // past it (the fast blocks show up ~100 GB into a fresh process's allocations; study r4o).  Only
+  // for big blocks, and only as much as leaves room for two candidates inside the keep_free bound.
   std::vector<char*> spacer;
-  if (const char* e = std::getenv("PMX_PLACEMENT_SPACER_GB"); e && e[0]) {
-    size_t want = size_t(std::atof(e) * double(1ull << 30));
+  double spacer_gb = opt_.placement_spacer_gb;
+  if (const char* e = std::getenv("PMX_PLACEMENT_SPACER_GB"); e && e[0]) spacer_gb = std::atof(e);
+  if (spacer_gb > 0.0 && block >= (size_t(2) << 30)) {
+    const size_t room = free0 > keep + 2 * block ? free0 - keep - 2 * block : 0;
+    size_t want = std::min(size_t(spacer_gb * double(1ull << 30)), room);
+    spacer_bytes_ = want;
     while (want > 0) {
       const size_t chunk = std::min(want, size_t(8) << 30);
       char* p = nullptr;
@@ -395,6 +400,9 @@ void GpuSubdomainSolver::place_fields() {
     placement_s_ = now_s() - t0;
     return;
   }
+  // the time budget bounds the timed sweeps; allocation (the driver clears reused VRAM) is reported
+  // in placement_seconds but not charged to it
+  const double t_probe = now_s();
   auto keep_only = [&](size_t keep) {  // free every other candidate, point the fields at `keep`
     for (size_t c = 0; c < cand.size(); ++c)
       if (c != keep) (void)hipFree(cand[c]);
@@ -409,7 +417,7 @@ void GpuSubdomainSolver::place_fields() {
     HIP_CHECK(hipEventCreate(&e1));
     placement_ms_.clear();
     for (size_t c = 0; c < cand.size(); ++c) {
-      if (c > 0 && now_s() - t0 > opt_.placement_budget_s) break;  // time budget: the rest stay untimed
+      if (c > 0 && now_s() - t_probe > opt_.placement_budget_s) break;  // time budget: the rest stay untimed
       placement_ms_.push_back(0.f);
       fields_ = cand[c];
       r2_ = field_raw(4);
