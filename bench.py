@@ -139,7 +139,7 @@ def parse(argv=None):
                     help="supervisor: hard limit (s) for one rung's processes (0 = RUNG_CAP per rung)")
     ap.add_argument("--ladder-budget", type=float, default=LADDER_BUDGET,
                     help="supervisor: wall-clock budget (s) of the whole ladder")
-    ap.add_argument("--placement", type=int, default=8,
+    ap.add_argument("--placement", type=int, default=12,
                     help="placement probe: candidate field blocks timed, the fastest kept (0 = off; "
                          "bounded by --placement-budget and --placement-keep-free; off when ranks share a GPU)")
     ap.add_argument("--persistent", default="auto", choices=["auto", "on", "off"],
@@ -150,11 +150,8 @@ def parse(argv=None):
                          "alone, ghosts filled by device copies of the real sizes (from zeros), all-reduce "
                          "skipped -- the real per-rank schedule (split sweep, frame stream, copies) at full speed")
     ap.add_argument("--placement-budget", type=float, default=0.5, help="placement probe: seconds of probing")
-    ap.add_argument("--placement-keep-free", type=float, default=0.3,
+    ap.add_argument("--placement-keep-free", type=float, default=0.5,
                     help="placement probe: fraction of the free device memory left free")
-    ap.add_argument("--placement-spacer", type=float, default=100.0,
-                    help="placement probe: GB held untouched while the candidates are allocated (field "
-                         "blocks >= 2 GB; counted in --placement-keep-free; profiles/r4/placement/)")
     return ap.parse_args(argv)
 
 
@@ -570,7 +567,7 @@ def measure(args) -> int:
               b_ring=args.b_kernel == "ring")
     persistent = {"auto": -1, "on": 1, "off": 0}[args.persistent]
     pkw = dict(placement=0 if share else args.placement, placement_budget_s=args.placement_budget,
-               placement_keep_free=args.placement_keep_free, placement_spacer_gb=args.placement_spacer)
+               placement_keep_free=args.placement_keep_free)
     dkw = dict(kw, **pkw, phase=watch.phase, init_timeout=COMM_INIT_TIMEOUT)
     if dry:
         tp = importlib.import_module(pkg_name + ".models.torch_pcg")
@@ -786,8 +783,7 @@ def measure_loopback(args) -> int:
     s = native.Session(problem.to_native(), world=args.gpus, comm="loopback", split=getattr(native.Split, args.split),
                        ranks=[args.loopback_rank], devices=[0], dtype=args.dtype, graph_batch=args.graph_batch,
                        overlap=args.overlap == "on", placement=args.placement,
-                       placement_budget_s=args.placement_budget, placement_keep_free=args.placement_keep_free,
-                       placement_spacer_gb=args.placement_spacer)
+                       placement_budget_s=args.placement_budget, placement_keep_free=args.placement_keep_free)
     sd = s.subdomain(0)
     s.init()
     s.step(args.warmup)

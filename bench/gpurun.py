@@ -520,6 +520,7 @@ STUDIES["r4n"] = [
     ("smoke", 120, "python -c 'import __graft_entry__ as g; g.smoke()'"),
 ]
 
+# (r4o / r4q / r4r: historical -- the spacer and prewarm knobs they set were removed after r4r)
 # placement: does the sweep rate follow the physical region the allocator reaches?  Candidates
 # allocated after a spacer of 0 / 120 / 170 / 220 GB held untouched (PMX_PLACEMENT_SPACER_GB)
 _SP = "--gpus 1 --steps 20 --warmup 5 --no-tol-solve --placement 12 --placement-budget 5 --placement-keep-free 0.02"
@@ -539,6 +540,39 @@ STUDIES["r4p2"] = [
                                    "--placement-spacer 0")),
     ("fp32_16k", 200, bench("--gpus 1 --steps 20 --warmup 5 --dtype fp32 --no-tol-solve")),
     ("mixed_32k", 300, bench("--gpus 1 --steps 20 --warmup 5 --dtype mixed --M 32768 --N 32768 --no-tol-solve")),
+]
+
+# placement: is "fast" the memory the driver had to clear?  Pre-written scratch (freed before the
+# candidates) vs none, each with and without the spacer, repeated
+_PW = "--gpus 1 --steps 20 --warmup 5 --no-tol-solve --placement 8"
+STUDIES["r4q"] = [
+    ("ctrl_1", 150, bench(_PW)),
+    ("pw150_1", 150, "env PMX_PLACEMENT_PREWARM_GB=150 " + bench(_PW)),
+    ("pw150_nosp_1", 150, "env PMX_PLACEMENT_PREWARM_GB=150 " + bench(_PW + " --placement-spacer 0")),
+    ("ctrl_2", 150, bench(_PW)),
+    ("pw150_2", 150, "env PMX_PLACEMENT_PREWARM_GB=150 " + bench(_PW)),
+    ("pw150_nosp_2", 150, "env PMX_PLACEMENT_PREWARM_GB=150 " + bench(_PW + " --placement-spacer 0")),
+    ("pw250_nosp", 150, "env PMX_PLACEMENT_PREWARM_GB=250 " + bench(_PW + " --placement-spacer 0")),
+    ("ctrl_3", 150, bench(_PW)),
+]
+
+# the probe times 6 real iterations per candidate: does its ranking now predict the bench rate?
+STUDIES["r4r"] = [
+    ("sp_1", 150, bench(_PW)),
+    ("nosp_1", 150, bench(_PW + " --placement-spacer 0")),
+    ("sp_2", 150, bench(_PW)),
+    ("nosp_2", 150, bench(_PW + " --placement-spacer 0")),
+    ("sp_3", 150, bench(_PW)),
+    ("nosp_3", 150, bench(_PW + " --placement-spacer 0")),
+    ("p16_half", 150, bench(_PW + " --placement 16 --placement-spacer 0 --placement-keep-free 0.5")),
+]
+
+# the bench defaults after r4r (12 candidates timed by 6 real iterations, half of the free HBM)
+STUDIES["r4s"] = [
+    ("driver_1", 300, bench("--gpus 1 --steps 20 --warmup 5")),
+    ("driver_2", 200, bench("--gpus 1 --steps 20 --warmup 5 --no-tol-solve")),
+    ("driver_3", 200, bench("--gpus 1 --steps 20 --warmup 5 --no-tol-solve")),
+    ("pytest_gpu", 700, f"{PYTEST} tests -m gpu"),
 ]
 
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),

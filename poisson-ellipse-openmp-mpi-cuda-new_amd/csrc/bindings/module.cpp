@@ -181,11 +181,9 @@ GpuOptions make_options(int device, const std::string& kernel, int block, int ve
                         int tile_rows, const std::string& dtype, bool exact, int graph_batch, bool check,
                         bool overlap = true, int vec_b = 0, int waves_b = 0, int tile_rows_b = -1,
                         bool poison_halos = false, bool b_ring = false, int algo = -1, int placement = 0,
-                        double placement_budget_s = 0.5, double placement_keep_free = 0.5, int persistent = -1,
-                        double placement_spacer_gb = 0.0) {
+                        double placement_budget_s = 0.5, double placement_keep_free = 0.5, int persistent = -1) {
   GpuOptions o;
   o.persistent = persistent;
-  o.placement_spacer_gb = placement_spacer_gb;
   o.placement = placement;
   o.placement_budget_s = placement_budget_s;
   o.placement_keep_free = placement_keep_free;
@@ -450,14 +448,13 @@ PYBIND11_MODULE(_pmx, m) {
                        bool rccl_graph, bool overlap, int vec_b, int waves_b, int tile_rows_b,
                        bool poison_halos, bool b_ring, int algo, bool defer_connect, int threaded,
                        int placement, double placement_budget_s, double placement_keep_free, int sharing,
-                       int persistent, double placement_spacer_gb) {
+                       int persistent) {
              SessionConfig c;
              c.sharing = sharing;
              c.spec = s;
              c.opt = make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact,
                                   graph_batch, check, overlap, vec_b, waves_b, tile_rows_b, poison_halos,
-                                  b_ring, algo, placement, placement_budget_s, placement_keep_free, persistent,
-                                  placement_spacer_gb);
+                                  b_ring, algo, placement, placement_budget_s, placement_keep_free, persistent);
              c.defer_connect = defer_connect;
              c.threaded = threaded;
              c.split = split;
@@ -485,8 +482,7 @@ PYBIND11_MODULE(_pmx, m) {
            py::arg("waves_b") = 0, py::arg("tile_rows_b") = -1, py::arg("poison_halos") = false,
            py::arg("b_ring") = false, py::arg("algo") = -1, py::arg("defer_connect") = false,
            py::arg("threaded") = -1, py::arg("placement") = 0, py::arg("placement_budget_s") = 0.5,
-           py::arg("placement_keep_free") = 0.5, py::arg("sharing") = 0, py::arg("persistent") = -1,
-           py::arg("placement_spacer_gb") = 0.0)
+           py::arg("placement_keep_free") = 0.5, py::arg("sharing") = 0, py::arg("persistent") = -1)
       .def("ipc_export", [](Session& s) { return py::bytes(s.ipc_export()); },
            "IPC session: this rank's memory handles (pass every rank's to connect_ipc)")
       .def("connect_ipc", [](Session& s, std::vector<py::bytes> ex) {
@@ -615,7 +611,6 @@ PYBIND11_MODULE(_pmx, m) {
           std::sort(v.begin(), v.end());
           q["median_ms"] = v[v.size() / 2];
           q["seconds"] = s.solver(0).placement_seconds();
-          q["spacer_gb"] = double(s.solver(0).placement_spacer_bytes()) / double(1ull << 30);
           d["placement"] = q;
         }
         return d;

@@ -334,20 +334,21 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
 // at ~2150 / ~1995 / ~1810 us -- profiles/r3/placement/, profiles/r4/placement/.  So the solver may
 // allocate candidate blocks and keep the fastest: at most opt.placement of them (GpuOptions), while
 // opt.placement_keep_free of the memory that was free stays free and for at most
-// opt.placement_budget_s seconds; blocks under 256 MB are not probed (latency-bound grids).  Each
-// candidate: 3 plain sweeps with the five fields in rotating roles (probe_sweeps: every field read
-// and written; zeroed fields, the init sweep's k = 0 arithmetic; init() resets everything
-// afterwards).  Construction time only; nothing in the iteration changes.  Off by default (the
-// library) and for ranks that share a device; skipped with an external (IPC-shared) arena.
-// Plain sweeps (k = 0 arithmetic) with the five field blocks in rotating roles, so that every field
-// of the candidate block is read and written: role set q reads r = F[q], p = F[q+3] and writes
-// r2 = F[q+4], p0 = F[q+2] (indices mod 5; F = w, r, p0, p1, r2).
-template <typename T>
-void GpuSubdomainSolver::probe_sweeps(hipStream_t s, int first, int count) {
-  auto F = [&](int f) { return reinterpret_cast<T*>(field_raw(f % 5) + field_off_ * elem_); };
-  for (int q = first; q < first + count; ++q)
-    launch_pcg1<T>(geom_, tables_, F(q + 1), F(q), F(q + 4), F(q + 2), F(q + 3), partials_, state_,
-                   tiles1_, s, 0, false);
+// opt.placement_budget_s seconds of timing; blocks under 256 MB are not probed (latency-bound
+// grids).  Each candidate: 6 real iterations (probe_iterations; init() resets everything afterwards).
+// Construction time only; nothing in the iteration changes.  Off by default (the library) and for
+// ranks that share a device; skipped with an external (IPC-shared) arena.
+// One candidate's rate: the iteration itself, in its real buffer roles -- init, two untimed
+// iterations, then 6 timed ones (a whole parity x w-cycle period: plain and w sweeps with r / r2 and
+// p0 / p1 in both assignments).  Round 4: the earlier probe (3 plain sweeps with the fields in
+// rotating roles) ranked blocks whose iteration rates differ by 7% within 1% of each other
+// (profiles/r4/placement/).  No ghost exchange (timing only); the driver's init() resets everything.
+void GpuSubdomainSolver::probe_iterations(hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  enqueue_init(s);
+  for (int k = 0; k < 2; ++k) enqueue_phase_a(s);
+  HIP_CHECK(hipEventRecord(e0, s));
+  for (int k = 0; k < 6; ++k) enqueue_phase_a(s);
+  HIP_CHECK(hipEventRecord(e1, s));
 }
 
 void GpuSubdomainSolver::place_fields() {
@@ -360,31 +361,6 @@ void GpuSubdomainSolver::place_fields() {
   HIP_CHECK(hipMemGetInfo(&free0, &total_b));
   const size_t keep = std::max(size_t(double(free0) * std::clamp(opt_.placement_keep_free, 0.0, 1.0)),
                                size_t(4) << 30);
-  // spacer: memory held untouched while the candidates are allocated, so they come from the region
-  // past it (the fast blocks show up ~100 GB into a fresh process's allocations; study r4o).  Only
-  // for big blocks, and only as much as leaves room for two candidates inside the keep_free bound.
-  std::vector<char*> spacer;
-  double spacer_gb = opt_.placement_spacer_gb;
-  if (const char* e = std::getenv("PMX_PLACEMENT_SPACER_GB"); e && e[0]) spacer_gb = std::atof(e);
-  if (spacer_gb > 0.0 && block >= (size_t(2) << 30)) {
-    const size_t room = free0 > keep + 2 * block ? free0 - keep - 2 * block : 0;
-    size_t want = std::min(size_t(spacer_gb * double(1ull << 30)), room);
-    spacer_bytes_ = want;
-    while (want > 0) {
-      const size_t chunk = std::min(want, size_t(8) << 30);
-      char* p = nullptr;
-      if (hipMalloc(&p, chunk) != hipSuccess) {
-        (void)hipGetLastError();
-        break;
-      }
-      spacer.push_back(p);
-      want -= chunk;
-    }
-  }
-  struct SpacerFree {
-    std::vector<char*>& v;
-    ~SpacerFree() { for (char* p : v) (void)hipFree(p); }
-  } spacer_free{spacer};
   while (int(cand.size()) < K) {
     size_t free_b = 0;
     HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
@@ -421,11 +397,7 @@ void GpuSubdomainSolver::place_fields() {
       placement_ms_.push_back(0.f);
       fields_ = cand[c];
       r2_ = field_raw(4);
-      HIP_CHECK(hipMemsetAsync(fields_, 0, block, s));
-      if (elem_ == 8) probe_sweeps<double>(s, 0, 1); else probe_sweeps<float>(s, 0, 1);  // warm-up
-      HIP_CHECK(hipEventRecord(e0, s));
-      if (elem_ == 8) probe_sweeps<double>(s, 0, 3); else probe_sweeps<float>(s, 0, 3);
-      HIP_CHECK(hipEventRecord(e1, s));
+      probe_iterations(s, e0, e1);
       HIP_CHECK(hipEventSynchronize(e1));
       HIP_CHECK(hipEventElapsedTime(&placement_ms_[c], e0, e1));
     }

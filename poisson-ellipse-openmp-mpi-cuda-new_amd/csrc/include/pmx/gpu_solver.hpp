@@ -109,10 +109,6 @@ struct GpuOptions {
   int persistent = -1;
   double placement_budget_s = 0.5;
   double placement_keep_free = 0.5;
-  // Spacer (GB) held untouched while the probe's candidates are allocated, for field blocks of
-  // >= 2 GB: the fast rate is found past ~100 GB of allocation (profiles/r4/placement/spacer_*).
-  // Counts toward placement_keep_free.  PMX_PLACEMENT_SPACER_GB overrides.
-  double placement_spacer_gb = 0.0;
   bool resolved = false;  // environment overrides already applied (resolve_options)
 };
 
@@ -278,7 +274,6 @@ class GpuSubdomainSolver {
   size_t field_bytes() const { return field_bytes_; }
   const std::vector<float>& placement_ms() const { return placement_ms_; }
   double placement_seconds() const { return placement_s_; }  // wall time of the probe (0: off)
-  size_t placement_spacer_bytes() const { return spacer_bytes_; }  // spacer the probe held
   void* field_base(int which) const;  // pointer to local (0,0)
   size_t device_bytes() const;        // total device memory owned
 
@@ -326,11 +321,9 @@ class GpuSubdomainSolver {
   size_t field_stride_ = 0;
   char* field_raw(int f) const { return fields_ + size_t(f) * field_stride_; }
   void place_fields();                // placement probe (see gpu_solver.hip)
-  template <typename T>
-  void probe_sweeps(hipStream_t s, int first, int count);
+  void probe_iterations(hipStream_t s, hipEvent_t e0, hipEvent_t e1);
   std::vector<float> placement_ms_;   // probe: ms per candidate block (the kept one is the min)
   double placement_s_ = 0.0;
-  size_t spacer_bytes_ = 0;
   double* tables_buf_ = nullptr;
   double* partials_ = nullptr;
   size_t npart_ = 0;

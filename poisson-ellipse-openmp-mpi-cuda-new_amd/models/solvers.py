@@ -81,8 +81,7 @@ def make_session(problem: PoissonEllipse, ranks: int = 1, split: str = "referenc
                  tile_rows: int = 0, exact: bool = False, graph_batch: int = 32, check: bool = False,
                  overlap: bool = True, vec_b: int = 0, waves_b: int = 0, tile_rows_b: int = -1,
                  poison_halos: bool = False, b_ring: bool = False, placement: int = 0,
-                 placement_budget_s: float = 0.5, placement_keep_free: float = 0.5, persistent: int = -1,
-                 placement_spacer_gb: float = 0.0):
+                 placement_budget_s: float = 0.5, placement_keep_free: float = 0.5, persistent: int = -1):
     """Native GPU session with `ranks` subdomains on one device (LocalComm when ranks > 1).
 
     overlap: ghost exchange on a second stream concurrent with pcg_b (only matters for ranks > 1).
@@ -94,8 +93,7 @@ def make_session(problem: PoissonEllipse, ranks: int = 1, split: str = "referenc
 
     placement: up to this many candidate field blocks are timed and the fastest kept (0 = off, the
     default; bounded by placement_budget_s seconds and by leaving placement_keep_free of the free
-    device memory free -- see GpuSubdomainSolver::place_fields); placement_spacer_gb is held
-    untouched while the candidates are allocated (field blocks >= 2 GB; counted in the bound).
+    device memory free -- see GpuSubdomainSolver::place_fields).
 
     persistent: -1 = auto (latency-bound grids: fp64, one subdomain, fields <= 16 MB (~0.4 M points) run whole
     batches of iterations in one persistent launch, pcg1_persist.hip), 0 = off, 1 = on."""
@@ -106,7 +104,7 @@ def make_session(problem: PoissonEllipse, ranks: int = 1, split: str = "referenc
                      check=check, overlap=overlap, vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b,
                      poison_halos=poison_halos, b_ring=b_ring, placement=placement,
                      placement_budget_s=placement_budget_s, placement_keep_free=placement_keep_free,
-                     persistent=persistent, placement_spacer_gb=placement_spacer_gb)
+                     persistent=persistent)
 
 
 def solve_hip(problem: PoissonEllipse, ranks: int = 1, keep_solution: bool = True, poll_batches: int = 1,

@@ -98,7 +98,7 @@ class DistGpuPCG:
                  overlap: bool = True, vec_b: int = 0, waves_b: int = 0, tile_rows_b: int = -1,
                  b_ring: bool = False, algo: int = -1, init_timeout: float = 90.0, device: int | None = None,
                  placement: int = 0, placement_budget_s: float = 0.5, placement_keep_free: float = 0.5,
-                 phase=None, placement_spacer_gb: float = 0.0):
+                 phase=None):
         """placement: candidate field blocks of the placement probe (0 = off; forced off when ranks share
         a device).  phase(name, seconds): progress-watchdog hook (bench.py's Watch.phase); called with
         "comm-init" before the blocking communicator initialisation, whose own watchdog is
@@ -134,8 +134,7 @@ class DistGpuPCG:
                     ranks=[info.rank], devices=[self.device], rccl_graph=rccl_graph, overlap=overlap,
                     vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b, b_ring=b_ring, algo=algo,
                     defer_connect=True, placement=placement, placement_budget_s=placement_budget_s,
-                    placement_keep_free=placement_keep_free, sharing=sharing,
-                    placement_spacer_gb=0.0 if sharing > 1 else placement_spacer_gb)
+                    placement_keep_free=placement_keep_free, sharing=sharing)
             except Exception as e:  # sizing / allocation: reported collectively below
                 err = e
             agree(info, err is None, f"native solver setup ({err})" if err else "native solver setup",
@@ -162,8 +161,7 @@ class DistGpuPCG:
                     dtype=dtype, exact=exact, graph_batch=graph_batch, ranks=[info.rank], devices=[self.device],
                     overlap=overlap, vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b, b_ring=b_ring,
                     algo=algo, defer_connect=True, placement=placement, placement_budget_s=placement_budget_s,
-                    placement_keep_free=placement_keep_free, sharing=sharing,
-                    placement_spacer_gb=0.0 if sharing > 1 else placement_spacer_gb)
+                    placement_keep_free=placement_keep_free, sharing=sharing)
                 mine = self.session.ipc_export()
             except Exception as e:
                 err, mine = e, b""
