@@ -575,6 +575,16 @@ STUDIES["r4s"] = [
     ("pytest_gpu", 700, f"{PYTEST} tests -m gpu"),
 ]
 
+# (historical: the PMX_PLACEMENT_PERMS knob was removed after r4t -- permutations do not matter)
+# placement: does the assignment of the five fields to the block's slots decide the rate?
+_PP = "--gpus 1 --steps 20 --warmup 5 --no-tol-solve --placement-budget 5"
+STUDIES["r4t"] = [
+    ("perm24_k1_a", 150, "env PMX_PLACEMENT_PERMS=24 " + bench(_PP + " --placement 1")),
+    ("perm24_k1_b", 150, "env PMX_PLACEMENT_PERMS=24 " + bench(_PP + " --placement 1")),
+    ("perm8_k4", 150, "env PMX_PLACEMENT_PERMS=8 " + bench(_PP + " --placement 4")),
+    ("perm24_k1_c", 150, "env PMX_PLACEMENT_PERMS=24 " + bench(_PP + " --placement 1")),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [
