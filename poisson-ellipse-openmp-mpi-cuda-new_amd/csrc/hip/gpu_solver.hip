@@ -286,7 +286,7 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     const int want_rows = std::max(1, (2 * waves + tj - 1) / tj);
     int ti = std::max(2, (sd.nx + want_rows - 1) / want_rows);
     if (const char* e = std::getenv("PMX_PERSIST_ROWS"); e && e[0]) ti = std::max(1, std::atoi(e));
-    tilesP_ = make_pcg1_tiles(G, 2, 1, ti, opt_.pf1 ? opt_.pf1 : 1, int(elem_));
+    tilesP_ = make_pcg1_tiles(G, 2, 1, ti, 1, int(elem_));  // the persistent march prefetches 1 row
     HIP_CHECK(hipMalloc(&tile_order_p_, 4 * size_t(tilesP_.ntiles()) * sizeof(Pcg1Slot)));
     (void)pcg1_build_order(G, tables_, tilesP_, tile_order_p_, true, nullptr);
     HIP_CHECK(hipMalloc(&sched_offs_p_, (size_t(waves) + 1) * sizeof(int)));

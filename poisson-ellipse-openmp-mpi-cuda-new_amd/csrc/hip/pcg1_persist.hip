@@ -12,8 +12,9 @@
 //             k_pcg1, so every point gets bit-identical values for equal scalars);
 //   publish:  the wave sums -> one 5-value partial per workgroup (sc1 stores); the fields are stored
 //             write-through (sc1 buffer stores) and every wave drains them (vmcnt 0) before its
-//             workgroup arrives, so no L2 writeback fence is needed (PMX_PERSIST_WT=0: k_pcg1's
-//             non-temporal stores + one agent-scope release per workgroup instead);
+//             workgroup arrives, so no L2 writeback fence is needed (k_pcg1's non-temporal stores +
+//             one agent-scope release per workgroup measured 57.1 vs 59.6 us at 800x1200, and
+//             prefetch depth 2 45.4 vs 46.6 with an unchanged march: both removed, profiles/r4/persist/);
 //   barrier:  one monotonic arrival counter (relaxed agent-scope add, relaxed polls with s_sleep,
 //             bounded by a wall-clock timeout that stops the solve instead of hanging the GPU);
 //   acquire:  one agent-scope acquire per workgroup, then every workgroup sums the NWG partials in
@@ -70,9 +71,8 @@ __device__ __forceinline__ unsigned long long ld_relaxed(const unsigned long lon
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// WT: field stores write-through (sc1): the publish needs no L2 writeback fence.  Else plain
-// non-temporal stores (k_pcg1's) and one agent release per workgroup and sweep.
-template <typename T, typename C, int PF, bool WT>
+// Field stores write-through (sc1, pcg1_march's WT): the publish needs no L2 writeback fence.
+template <typename T, typename C>
 __global__ void __launch_bounds__(kPersistThreads, kPersistWaves / 4)
 k_pcg1_persist(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1, PcgState* S,
                PersistWs* ws, PersistArgs A) {
@@ -197,7 +197,7 @@ k_pcg1_persist(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T
       const bool use_cls = A.TI + 5 <= 64 / 2;
       double t[kNq] = {0.0, 0.0, 0.0, 0.0, 0.0};
 #define PMX_PMARCH(E, F)                                                                                        \
-  pcg1_march<T, C, VEC, PF, E, F, WT, true>(G, Tb, AF, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, \
+  pcg1_march<T, C, VEC, 1, E, F, true, true>(G, Tb, AF, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, \
                                             c2, t, scol, ocls, use_cls, kring)
 #define PMX_PMARCH_W(F)                  \
   switch (wm) {                          \
@@ -238,12 +238,7 @@ k_pcg1_persist(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T
         for (int wv = 0; wv < kPersistWaves; ++wv) v += s_sum[wv][q];
         st_publish(slot + q, v);
       }
-      if constexpr (!WT) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the XCD L2's dirty field lines
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (ROCm 7.2 may drop the fence's own wait)
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the partial's sc1 stores
-      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the partial's sc1 stores
       __hip_atomic_fetch_add(&ws->arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (tr) A.trace[2 * nwaves + 2 * blockIdx.x] = wall_clock64();
       // ---- grid barrier: every workgroup of sweep `gen` has arrived
@@ -341,19 +336,8 @@ int launch_pcg1_persist(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2
   // every polled word zeroed before EVERY launch (a memset node when captured)
   HIP_CHECK(hipMemsetAsync(ws, 0, kPersistPolled, s));
   static_assert(sizeof(T) == 8, "pcg1p: fp64 storage");
-  static const bool wt = [] {  // PMX_PERSIST_WT=0: non-temporal stores + release fence (A/B)
-    const char* e = std::getenv("PMX_PERSIST_WT");
-    return !(e && e[0] == '0');
-  }();
-#define PMX_PERSIST_LAUNCH(PF, WT)                                                                          \
-  hipLaunchKernelGGL((k_pcg1_persist<T, double, PF, WT>), dim3(nwg), dim3(kPersistThreads), 0, s, G, Tb, w, r, \
-                     r2, p0, p1, S, ws, A)
-  if (tc.pf == 2) {
-    if (wt) PMX_PERSIST_LAUNCH(2, true); else PMX_PERSIST_LAUNCH(2, false);
-  } else {
-    if (wt) PMX_PERSIST_LAUNCH(1, true); else PMX_PERSIST_LAUNCH(1, false);
-  }
-#undef PMX_PERSIST_LAUNCH
+  hipLaunchKernelGGL((k_pcg1_persist<T, double>), dim3(nwg), dim3(kPersistThreads), 0, s, G, Tb, w, r, r2, p0,
+                     p1, S, ws, A);
   HIP_CHECK(hipGetLastError());
   return nwg;
 }
