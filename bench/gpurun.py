@@ -585,6 +585,23 @@ STUDIES["r4t"] = [
     ("perm24_k1_c", 150, "env PMX_PLACEMENT_PERMS=24 " + bench(_PP + " --placement 1")),
 ]
 
+# after stripping the persistent variants: its tests + trace, then the suite
+STUDIES["r4u"] = [
+    ("persist_tests", 200, f"{PYTEST} tests/test_gpu_persist.py -m gpu"),
+    ("persist_trace", 120, "python3 -u bench/probe/persist_trace.py 400x600 800x1200"),
+    ("pytest_gpu", 700, f"{PYTEST} tests -m gpu"),
+]
+
+# block tiles for the latency-bound grids: correctness first, then the rate against the march
+_B8 = "--gpus 1 --M 800 --N 1200 --steps 500 --warmup 50 --no-tol-solve --persistent off"
+_B16 = "--gpus 1 --M 1600 --N 2400 --steps 500 --warmup 50 --no-tol-solve --persistent off"
+_B24 = "--gpus 1 --M 2400 --N 3200 --steps 500 --warmup 50 --no-tol-solve --persistent off"
+_BON = "env PMX_PCG1_BLOCK=1 PMX_PCG1_BLOCK_ROWS="
+STUDIES["r4v"] = [
+    ("block_tests", 300, f"{PYTEST} tests/test_gpu_block.py -m gpu"),
+] + [(f"{g}_{tag}", 60, (f"{_BON}{tag[1:]} " if tag != "m" else "") + bench(a))
+     for g, a in (("g800", _B8), ("g1600", _B16), ("g2400", _B24)) for tag in ("m", "b4", "b8")]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

@@ -65,6 +65,7 @@ py::dict state_dict(const PcgState& st) {
   d["w_pend"] = st.w_pend;
   d["w_pend_n"] = st.w_pend_n;
   d["w_cycle"] = st.w_cycle;
+  d["red_c"] = py::make_tuple(st.red_c[0], st.red_c[1], st.red_c[2], st.red_c[3], st.red_c[4]);
   return d;
 }
 
@@ -588,6 +589,7 @@ PYBIND11_MODULE(_pmx, m) {
           return d;
         };
         py::dict d = one(s.solver(0).tiles());
+        if (s.solver(0).block_tiles()) d["block_tiles"] = true;
         if (!s.solver(0).single_pass()) d["b"] = one(s.solver(0).tiles_b());
         d["algo"] = s.solver(0).single_pass() ? "pcg1" : "pcg2";
         if (s.solver(0).persistent()) {

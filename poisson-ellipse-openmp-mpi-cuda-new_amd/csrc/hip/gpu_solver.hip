@@ -240,6 +240,18 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   tiles_b_.pair_w = tiles_b_.kind == 2 && !opt.exact && opt_.pair_w != 0;
 
   if (pcg1_) {
+    // block tiles (pcg1_block.hip): undecomposed fp64 grids, the three pipeline stages row-parallel
+    // across a workgroup's waves.  Study knob for now: PMX_PCG1_BLOCK=1, PMX_PCG1_BLOCK_ROWS=4|8
+    if (const char* e = std::getenv("PMX_PCG1_BLOCK"); e && e[0] == '1' && G.nb == 0 && elem_ == 8) {
+      int rows = 8;
+      if (const char* er = std::getenv("PMX_PCG1_BLOCK_ROWS"); er && er[0]) rows = std::atoi(er);
+      block1_ = true;
+      opt_.rows1 = rows;
+      opt_.rows1w = rows;
+      opt_.vec1 = 2;
+      opt_.waves1 = 1;
+      opt_.pf1 = opt_.pf1w = 1;
+    }
     tiles1_ = make_pcg1_tiles(G, opt_.vec1, opt_.waves1, opt_.rows1, opt_.pf1, int(elem_));
 #ifdef PMX_WAVE_TRACE
     if (const char* e = std::getenv("PMX_WAVE_TRACE_IT"); e && e[0]) {
@@ -657,6 +669,16 @@ void GpuSubdomainSolver::phase_a_impl(hipStream_t s) {
 
 template <typename T>
 void GpuSubdomainSolver::phase_a_kernel_only(hipStream_t s, int part) {
+  if constexpr (sizeof(T) == 8) {
+    if (block1_) {
+      PMX_CHECK(part == 0, "block tiles run whole sweeps (undecomposed grids)");
+      launch_pcg1_block<T>(geom_, tables_, static_cast<T*>(field_base(0)), static_cast<T*>(field_base(1)),
+                           reinterpret_cast<T*>(r2_ + field_off_ * elem_), static_cast<T*>(field_base(2)),
+                           static_cast<T*>(field_base(3)), partials_, state_, tiles1_for(w_sweep_next()), s,
+                           w_sweep_next());
+      return;
+    }
+  }
   if (pcg1_)
     launch_pcg1<T>(geom_, tables_, static_cast<T*>(field_base(0)), static_cast<T*>(field_base(1)),
                    reinterpret_cast<T*>(r2_ + field_off_ * elem_), static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), partials_, state_,

@@ -1,0 +1,357 @@
+// Small-grid single-pass sweep ("block" tiles): the three pipeline stages of pcg1_march run
+// row-parallel across the waves of a workgroup instead of row-serial inside one wave.
+//
+// Why: at the reference's published grids (800x1200 .. 2400x3200, stage4-mpi+cuda/
+// poisson_mpi_cuda_f.cu:847-943) the launch-per-sweep path is bound by one wave's row march: a
+// 2-row tile marches 6 row steps (its rows plus the stencil halo of the 3-stage pipeline), each
+// ~1.8 us of dependent loads and fp64 arithmetic, and a sweep lasts as long as its slowest tile
+// (profiles/r4/persist/).  Here a workgroup of kBlkWaves waves owns TR rows x 124 columns:
+//
+//   stage A (rows i0-2 .. i1+2):  p^k = D^-1 r^{k-1} + beta p^{k-1}   -> LDS (with r^{k-1}, p^{k-1})
+//   barrier
+//   stage B (rows i0-1 .. i1+1):  A p^k, r^k = r^{k-1} - alpha A p^k, z^k = D^-1 r^k  -> LDS;
+//                                 owned rows store r^k, p^k (and w on the w sweeps)
+//   barrier
+//   stage C (rows i0 .. i1):      A z^k and the five partial sums
+//
+// so a tile costs ~3 row latencies instead of TR + 4.  Every value is computed by the same helper
+// calls in the same order as pcg1_march (coef_c, zdiv_c, apply_c, fma_c, the same roundings to the
+// storage type), so the fields are bit-identical to k_pcg1's; only the partial sums are added in a
+// different order (per workgroup instead of per wave tile), as in the persistent kernel.
+// Undecomposed fp64 grids only (every ghost is a Dirichlet zero); the prologue is k_pcg1's
+// (pcg1_kernels.hip), including the stop test, the breakdown guard and the w-phase check.
+#include <hip/hip_runtime.h>
+
+#include "pcg1_march.hpp"
+
+namespace pmx {
+namespace {
+
+constexpr int kBlkWaves = 8;
+
+template <typename T, int TR, bool WS>
+__global__ void __launch_bounds__(64 * kBlkWaves)
+k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
+             double* __restrict__ partials, PcgState* S, int tiles_j, int ntiles) {
+  using C = double;
+  constexpr int VEC = 2, WO = 64 * VEC - 4, NA = TR + 4, NB = TR + 2;
+  __shared__ double sP[NA][VEC][64];   // p^k of rows i0-2 .. i1+2 (stage A)
+  __shared__ double sPo[NA][VEC][64];  // p^{k-1} of the same rows
+  __shared__ double sRo[NA][VEC][64];  // r^{k-1} of the same rows
+  __shared__ double sZ[NB][VEC][64];   // z^k of rows i0-1 .. i1+1 (stage B)
+  __shared__ double s_col[4 * VEC * 64];
+  __shared__ double s_sum[kBlkWaves][kNq];
+
+  // ---- prologue: k_pcg1's scalars of sweep k (every workgroup computes the same values)
+  typedef const __attribute__((address_space(4))) PcgState CState;
+  const CState* Sc = (const CState*)S;  // NOLINT: address-space cast
+  const int st_done = Sc->done;
+  const long long k = Sc->it;
+  double rc[kNq], al[4], be[4];
+#pragma unroll
+  for (int q = 0; q < kNq; ++q) rc[q] = Sc->red_c[q];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    al[q] = Sc->alpha1[q];
+    be[q] = Sc->beta1[q];
+  }
+  const double zr0 = Sc->zr[0], zr1 = Sc->zr[1];
+  const double s_delta = Sc->delta, s_bd_tol = Sc->bd_tol, s_pmb = Sc->pair_min_beta;
+  const long long s_max_iter = Sc->max_iter;
+  const int s_norm = Sc->norm, cyc = Sc->w_cycle;
+  auto ring4 = [](const double (&v)[4], long long i) {
+    const int j = int(i & 3);
+    return j == 0 ? v[0] : j == 1 ? v[1] : j == 2 ? v[2] : v[3];
+  };
+  if (st_done) return;
+  const bool leader = blockIdx.x == 0 && threadIdx.x == 0;
+  double alpha = 0.0, beta = 0.0, c1 = 0.0, c2 = 0.0;
+  int wm = 0;
+  if (k > 0) {
+    const double rho = rc[0];
+    double diff = 0.0;
+    if (k >= 2) {
+      diff = fabs(ring4(al, k - 1)) * sqrt(rc[4]);
+      const bool bad = !(diff == diff) || !(rho == rho);
+      if (bad || diff < s_delta || k > s_max_iter) {
+        if (leader) {
+          S->diff = diff;
+          S->iters = k - 1;
+          S->status = bad ? int(Status::kBreakdown) : (diff < s_delta ? int(Status::kConverged) : int(Status::kMaxIter));
+          if (bad) S->nan_flag = 1;
+          S->done = 1;
+        }
+        return;
+      }
+      beta = rho / ((k & 1) ? zr1 : zr0);
+    }
+    const double denom = rc[1] + beta * (2.0 * rc[2] + beta * rc[3]);
+    const bool bd = s_norm == int(Norm::kWeighted) ? fabs(denom) < s_bd_tol : denom < s_bd_tol;
+    if (bd || !(denom == denom)) {
+      if (leader) {
+        if (k >= 2) S->diff = diff;
+        S->iters = k;
+        S->status = int(Status::kBreakdown);
+        if (!(denom == denom)) S->nan_flag = 1;
+        S->done = 1;
+      }
+      return;
+    }
+    alpha = rho / denom;
+    const int ph = int(k % cyc);
+    if ((ph == 0) != WS) {  // host and device iteration counters out of step
+      if (leader) {
+        S->iters = k;
+        S->status = int(Status::kBreakdown);
+        S->nan_flag = 1;
+        S->done = 1;
+      }
+      return;
+    }
+    if (ph == 0) {
+      c1 = ring4(al, k - 1);
+      wm = 1;
+      if (cyc == 3) {
+        const double bprev = ring4(be, k - 1);
+        const double a2 = ring4(al, k - 2);
+        if (fabs(bprev) >= s_pmb) { wm = 2; c2 = a2 / bprev; }
+        else { wm = 3; c2 = a2; }
+      }
+    }
+    if (leader) {
+      S->zr[(k - 1) & 1] = rho;
+      S->alpha1[k & 3] = alpha;
+      S->beta1[k & 3] = beta;
+      if (k >= 2) S->diff = diff;
+      S->w_pend = ph ? k : 0;
+      S->w_pend_n = ph;
+    }
+  }
+  if (leader) S->halo_k = k + 1;
+
+  // ---- the tile
+  const int id = xcd_remap(int(blockIdx.x), int(gridDim.x));
+  if (id >= ntiles) return;  // the grid is exactly ntiles workgroups
+  const int ti = id / tiles_j, tj = id - ti * tiles_j;
+  const int i0 = 1 + ti * TR, i1 = min(i0 + TR - 1, G.nx);
+  const int j0 = 1 + tj * WO, j1 = min(j0 + WO - 1, G.ny);
+  T* pnew = (k & 1) ? p1 : p0;
+  const T* pold = (k & 1) ? p0 : p1;
+  const T* rold = (k & 1) ? r2 : r;
+  T* rnew = (k & 1) ? r : r2;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const ArithF AF{float(G.cx), float(G.cy), float(G.dinv_in), float(G.dinv_out), float(G.inv_eps)};
+  const int64_t P = G.pitch;
+  const int c0 = j0 - 2 + lane * VEC;
+  const int cmax = G.ny + 1 + (G.ny & 1);
+  bool colin[VEC], own[VEC];
+  int gj[VEC];
+#pragma unroll
+  for (int u = 0; u < VEC; ++u) {
+    const int c = c0 + u, g = G.gj0 + c;
+    colin[u] = g >= 1 && g <= G.N - 1;
+    own[u] = c >= j0 && c <= j1;
+    gj[u] = min(max(g, 0), G.N);
+  }
+  const bool own_all = own[0] && own[VEC - 1];
+  const bool own_any = own[0] || own[VEC - 1];
+  const int gjlo = max(G.gj0 + j0 - 2, 0), gjhi = min(G.gj0 + j0 - 2 + 64 * VEC - 1, G.N);
+  auto grow = [&](int m) { return min(max(G.gi0 + m, 0), G.M); };
+  auto interior_row = [&](int m) { return G.gi0 + m >= 1 && G.gi0 + m <= G.M - 1; };
+  // column constants of the tile's lanes, for the exact (cut-face) coefficients: one copy per
+  // workgroup, lane-private slots as pcg1_march's park_cols
+  if (wave == 0) {
+#pragma unroll
+    for (int u = 0; u < VEC; ++u) {
+      const ColConst cc = load_col(Tb, gj[u]);
+      s_col[(4 * u) * 64 + lane] = cc.ylo;
+      s_col[(4 * u + 1) * 64 + lane] = cc.yhi;
+      s_col[(4 * u + 2) * 64 + lane] = cc.rh0;
+      s_col[(4 * u + 3) * 64 + lane] = cc.rh1;
+    }
+  }
+  __syncthreads();
+
+  // ---- stage A: p^k of rows i0-2 .. i1+2
+  for (int a = wave; a < NA; a += kBlkWaves) {
+    const int m = i0 - 2 + a;
+    const int mc = min(max(m, -1), G.nx + 2);
+    T rr[VEC], pp[VEC];
+    load_cols<T, VEC>(rold + int64_t(mc) * P, c0, cmax, rr);
+    load_cols<T, VEC>(pold + int64_t(mc) * P, c0, cmax, pp);
+    const bool rowA = interior_row(m);
+    const RowCo cA = row_co(Tb, grow(m), gjlo, gjhi);
+#pragma unroll
+    for (int u = 0; u < VEC; ++u) {
+      const bool in = rowA && colin[u];
+      const C rom = in ? C(rr[u]) : C(0), pom = in ? C(pp[u]) : C(0);
+      C a0, a1, b0, b1;
+      coef_c<C>(cA, Tb, G, AF, s_col, u, lane, gj[u], a0, a1, b0, b1);
+      const C z = zdiv_c<C>(cA.ucls, rom, a0, a1, b0, b1, G, AF);
+      const C v = fma_c(beta, pom, z);
+      sP[a][u][lane] = in ? C(static_cast<T>(v)) : C(0);
+      sPo[a][u][lane] = pom;
+      sRo[a][u][lane] = rom;
+    }
+  }
+  __syncthreads();
+
+  // ---- stage B: A p^k, r^k, z^k of rows i0-1 .. i1+1; stores and three sums on owned rows
+  double acc[kNq] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  auto stage_b = [&](auto wm_c) {
+    constexpr int WM = decltype(wm_c)::value;
+    constexpr bool WUP = WM != 0;
+    for (int b = wave; b < NB; b += kBlkWaves) {
+      const int mb = i0 - 1 + b, a = b + 1;
+      const bool ownB = mb >= i0 && mb <= i1;
+      T wv[VEC] = {}, qv[VEC] = {};
+      if constexpr (WUP) {
+        const int wc = min(max(mb, -1), G.nx + 2);
+        load_cols<T, VEC>(w + int64_t(wc) * P, c0, cmax, wv);
+        // p^{k-2} still sits in the buffer this sweep overwrites with p^k: read before the store
+        if constexpr (WM == 3) load_cols<T, VEC>(pnew + int64_t(wc) * P, c0, cmax, qv);
+      }
+      C Pm1[VEC], Pm2[VEC], Pm[VEC], po1[VEC], po2[VEC], pom[VEC], ro1[VEC];
+#pragma unroll
+      for (int u = 0; u < VEC; ++u) {
+        Pm1[u] = sP[a][u][lane];
+        Pm2[u] = sP[a - 1][u][lane];
+        Pm[u] = sP[a + 1][u][lane];
+        po1[u] = sPo[a][u][lane];
+        po2[u] = sPo[a - 1][u][lane];
+        pom[u] = sPo[a + 1][u][lane];
+        ro1[u] = sRo[a][u][lane];
+      }
+      const bool rowB = interior_row(mb);
+      const RowCo cB = row_co(Tb, grow(mb), gjlo, gjhi);
+      const C left = dpp_shift<kWaveShr1>(Pm1[VEC - 1], C(0));
+      const C right = dpp_shift<kWaveShl1>(Pm1[0], C(0));
+      C oleft = C(0), oright = C(0);
+      if constexpr (WM == 2) {
+        oleft = dpp_shift<kWaveShr1>(po1[VEC - 1], C(0));
+        oright = dpp_shift<kWaveShl1>(po1[0], C(0));
+      }
+      T rs[VEC], ps[VEC], ws[VEC];
+#pragma unroll
+      for (int u = 0; u < VEC; ++u) {
+        C a0, a1, b0, b1;
+        coef_c<C>(cB, Tb, G, AF, s_col, u, lane, gj[u], a0, a1, b0, b1);
+        const C Ap = apply_c<C>(Pm1[u], Pm2[u], Pm[u], u == 0 ? left : Pm1[u - 1],
+                                u == VEC - 1 ? right : Pm1[u + 1], a0, a1, b0, b1, G, AF);
+        const bool in = rowB && colin[u];
+        const C rn = C(static_cast<T>(fma_c(-alpha, Ap, ro1[u])));
+        rs[u] = static_cast<T>(in ? rn : C(0));
+        const C zn = zdiv_c<C>(cB.ucls, rn, a0, a1, b0, b1, G, AF);
+        sZ[b][u][lane] = in ? zn : C(0);
+        ps[u] = static_cast<T>(Pm1[u]);
+        if constexpr (WM == 1) {
+          ws[u] = static_cast<T>(fma_c(C(alpha), Pm1[u], fma_c(C(c1), po1[u], C(wv[u]))));
+        } else if constexpr (WM == 2) {
+          const C Apo = apply_c<C>(po1[u], po2[u], pom[u], u == 0 ? oleft : po1[u - 1],
+                                   u == VEC - 1 ? oright : po1[u + 1], a0, a1, b0, b1, G, AF);
+          const C zo = zdiv_c<C>(cB.ucls, fma_c(C(c1), Apo, ro1[u]), a0, a1, b0, b1, G, AF);
+          const C t = fma_c(C(c2), po1[u] - zo, C(wv[u]));
+          ws[u] = static_cast<T>(fma_c(C(alpha), Pm1[u], fma_c(C(c1), po1[u], t)));
+        } else if constexpr (WM == 3) {
+          const C t = fma_c(C(c2), C(qv[u]), C(wv[u]));
+          ws[u] = static_cast<T>(fma_c(C(alpha), Pm1[u], fma_c(C(c1), po1[u], t)));
+        }
+        if (ownB && own[u]) {
+          acc[0] += double(in ? zn : C(0)) * double(rn);
+          acc[3] += double(Ap) * double(Pm1[u]);
+          acc[4] += double(Pm1[u]) * double(Pm1[u]);
+        }
+      }
+      if (ownB && own_any) {
+        const int64_t o = int64_t(mb) * P;
+        store_cols<T, VEC>(rnew + o, c0, rs, own_all, own);
+        store_cols<T, VEC>(pnew + o, c0, ps, own_all, own);
+        if constexpr (WUP) store_cols<T, VEC>(w + o, c0, ws, own_all, own);
+      }
+    }
+  };
+  if constexpr (!WS) {
+    stage_b(std::integral_constant<int, 0>{});
+  } else {
+    switch (wm) {
+      case 1: stage_b(std::integral_constant<int, 1>{}); break;
+      case 2: stage_b(std::integral_constant<int, 2>{}); break;
+      case 3: stage_b(std::integral_constant<int, 3>{}); break;
+      default: stage_b(std::integral_constant<int, 0>{}); break;  // k = 0: no w step yet
+    }
+  }
+  __syncthreads();
+
+  // ---- stage C: A z^k of the owned rows, (A z, z) and (A z, p)
+  for (int c = wave; c < TR; c += kBlkWaves) {
+    const int mc = i0 + c;
+    if (mc > i1) break;
+    const int b = c + 1;
+    C Zc[VEC], Zm[VEC], Zp[VEC];
+#pragma unroll
+    for (int u = 0; u < VEC; ++u) {
+      Zc[u] = sZ[b][u][lane];
+      Zm[u] = sZ[b - 1][u][lane];
+      Zp[u] = sZ[b + 1][u][lane];
+    }
+    const RowCo cC = row_co(Tb, grow(mc), gjlo, gjhi);
+    const C left = dpp_shift<kWaveShr1>(Zc[VEC - 1], C(0));
+    const C right = dpp_shift<kWaveShl1>(Zc[0], C(0));
+#pragma unroll
+    for (int u = 0; u < VEC; ++u) {
+      C a0, a1, b0, b1;
+      coef_c<C>(cC, Tb, G, AF, s_col, u, lane, gj[u], a0, a1, b0, b1);
+      const C Az = apply_c<C>(Zc[u], Zm[u], Zp[u], u == 0 ? left : Zc[u - 1], u == VEC - 1 ? right : Zc[u + 1],
+                              a0, a1, b0, b1, G, AF);
+      if (own[u]) {
+        acc[1] += double(Az) * double(Zc[u]);
+        acc[2] += double(Az) * double(sP[c + 2][u][lane]);
+      }
+    }
+  }
+
+  // ---- partials: wave sums, then the waves in a fixed order -> one 5-value partial per tile
+  wave_sum2_mfma(acc[0], acc[1]);
+  wave_sum2_mfma(acc[2], acc[3]);
+  acc[4] = wave_sum_mfma(acc[4]);
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < kNq; ++q) s_sum[wave][q] = acc[q];
+  }
+  __syncthreads();
+  if (threadIdx.x < kNq) {
+    double v = 0.0;
+#pragma unroll
+    for (int wv = 0; wv < kBlkWaves; ++wv) v += s_sum[wv][threadIdx.x];
+    partials[int64_t(kNq) * id + threadIdx.x] = v;
+  }
+}
+
+}  // namespace
+
+template <typename T>
+void launch_pcg1_block(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1, double* partials,
+                       PcgState* S, const TileCfg& tc, hipStream_t s, bool wsweep) {
+  static_assert(sizeof(T) == 8, "pcg1 block tiles: fp64 storage");
+  PMX_CHECK(tc.kind == 3 && tc.vec == 2 && G.nb == 0, "pcg1 block tiles: VEC-2 tiling of an undecomposed grid");
+  PMX_CHECK(tc.block == 124 && tc.tiles_j == (G.ny + 123) / 124, "pcg1 block tiles: 124-column tiles");
+  const int n = tc.ntiles();
+#define PMX_BLK(TR)                                                                                                 \
+  if (wsweep)                                                                                                       \
+    hipLaunchKernelGGL((k_pcg1_block<T, TR, true>), dim3(n), dim3(64 * kBlkWaves), 0, s, G, Tb, w, r, r2, p0, p1,   \
+                       partials, S, tc.tiles_j, n);                                                                 \
+  else                                                                                                              \
+    hipLaunchKernelGGL((k_pcg1_block<T, TR, false>), dim3(n), dim3(64 * kBlkWaves), 0, s, G, Tb, w, r, r2, p0, p1,  \
+                       partials, S, tc.tiles_j, n)
+  if (tc.rows == 4) PMX_BLK(4);
+  else if (tc.rows == 8) PMX_BLK(8);
+  else PMX_CHECK(false, "pcg1 block tiles: 4 or 8 rows, got " << tc.rows);
+#undef PMX_BLK
+  HIP_CHECK(hipGetLastError());
+}
+
+template void launch_pcg1_block<double>(const DevGeom&, const DevTables&, double*, double*, double*, double*, double*,
+                                        double*, PcgState*, const TileCfg&, hipStream_t, bool);
+
+}  // namespace pmx

@@ -257,6 +257,7 @@ class GpuSubdomainSolver {
   const Subdomain& sd() const { return sd_; }
   const ProblemSpec& spec() const { return spec_; }
   const GpuOptions& options() const { return opt_; }
+  bool block_tiles() const { return block1_; }  // pcg1 sweeps as block tiles (pcg1_block.hip)
   const DevGeom& geom() const { return geom_; }
   const DevTables& tables() const { return tables_; }
   const TileCfg& tiles() const { return pcg1_ ? tiles1_ : tiles_; }  // pcg_a (or pcg1)
@@ -319,6 +320,7 @@ class GpuSubdomainSolver {
   char* fields_ = nullptr;
   char* r2_ = nullptr;      // pcg1 only: the second r buffer (r is double-buffered there)
   size_t field_stride_ = 0;
+  bool block1_ = false;  // pcg1 sweeps as block tiles (pcg1_block.hip)
   char* field_raw(int f) const { return fields_ + size_t(f) * field_stride_; }
   void place_fields();                // placement probe (see gpu_solver.hip)
   void probe_iterations(hipStream_t s, hipEvent_t e0, hipEvent_t e1);

@@ -119,6 +119,12 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
                  double* partials, PcgState* S, const TileCfg& tc, hipStream_t s, int part = 0,
                  bool wsweep = false);
 
+// pcg1 sweep with block tiles (pcg1_block.hip): one workgroup of 8 waves per tc.rows x 124 tile,
+// the three pipeline stages row-parallel; undecomposed fp64 grids; partial sums per tile as k_pcg1.
+template <typename T>
+void launch_pcg1_block(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1, double* partials,
+                       PcgState* S, const TileCfg& tc, hipStream_t s, bool wsweep);
+
 // pcg1 ghost exchange: pack (unpack=false) the radius-2 edges of the buffers sweep `target` reads
 // (parity of target) into H.send, or unpack H.recv into their ghost cells.
 #ifdef PMX_WAVE_TRACE

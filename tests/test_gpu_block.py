@@ -1,0 +1,61 @@
+"""pcg1 block tiles (csrc/hip/pcg1_block.hip): the three pipeline stages of the single-pass sweep
+row-parallel across a workgroup's waves, for latency-bound undecomposed fp64 grids.  Same per-point
+arithmetic as k_pcg1's march; the partial sums are added per workgroup, so results agree with the
+march path to rounding.  Goldens: the reference's iteration counts (400x600 546 from stage 1,
+800x1200 / 1600x2400 / 2400x3200 989 / 1858 / 2449 from stage4-mpi+cuda, итоговый отчёт p.11)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu(pkg):
+    assert torch.cuda.is_available() and pkg.load_native().device_count() > 0, "no HIP device"
+
+
+def _sess(pkg, monkeypatch, M, N, rows, **kw):
+    if rows:
+        monkeypatch.setenv("PMX_PCG1_BLOCK", "1")
+        monkeypatch.setenv("PMX_PCG1_BLOCK_ROWS", str(rows))
+    else:
+        monkeypatch.delenv("PMX_PCG1_BLOCK", raising=False)
+    kw.setdefault("persistent", 0)
+    return pkg.make_session(pkg.PoissonEllipse(M=M, N=N), **kw)
+
+
+@pytest.mark.parametrize("rows", [4, 8])
+@pytest.mark.parametrize("grid,iters", [((400, 600), 546), ((800, 1200), 989), ((1600, 2400), 1858),
+                                        ((2400, 3200), 2449), ((97, 130), None)])
+def test_block_tiles_goldens_and_march_agreement(pkg, monkeypatch, rows, grid, iters):
+    b = _sess(pkg, monkeypatch, *grid, rows)
+    assert b.tile.get("block_tiles") and b.tile["rows"] == rows
+    rb = b.solve(1)
+    m = _sess(pkg, monkeypatch, *grid, 0)
+    assert not m.tile.get("block_tiles")
+    rm = m.solve(1)
+    assert rb["status"] == rm["status"] == "converged"
+    assert rb["iters"] == rm["iters"]
+    if iters is not None:
+        assert rb["iters"] == iters
+    wb, wm = b.gather_local_w(), m.gather_local_w()
+    assert np.abs(wb - wm).max() <= 1e-10 * np.abs(wm).max()
+
+
+def test_block_tiles_first_sweeps_bitwise(pkg, monkeypatch):
+    """Sweep 0 has alpha = beta = 0 (no sums feed it): its fields must equal the march's bitwise;
+    the next sweeps differ only through the rounding of the sums."""
+    b = _sess(pkg, monkeypatch, 800, 1200, 8, graph_batch=0)
+    m = _sess(pkg, monkeypatch, 800, 1200, 0, graph_batch=0)
+    for s in (b, m):
+        s.init()
+        s.synchronize()
+    assert np.array_equal(b.local_w(0), m.local_w(0))
+    sb, sm = b.state(0), m.state(0)
+    for q in range(5):
+        assert abs(sb["red_c"][q] - sm["red_c"][q]) <= 1e-13 * abs(sm["red_c"][q])
+    for s in (b, m):
+        s.step(7)  # through a w sweep (k = 3, 6)
+        s.synchronize()
+    assert np.abs(b.local_w(0) - m.local_w(0)).max() <= 1e-12 * np.abs(m.local_w(0)).max()
