@@ -602,6 +602,15 @@ STUDIES["r4v"] = [
 ] + [(f"{g}_{tag}", 60, (f"{_BON}{tag[1:]} " if tag != "m" else "") + bench(a))
      for g, a in (("g800", _B8), ("g1600", _B16), ("g2400", _B24)) for tag in ("m", "b4", "b8")]
 
+_VAR = {"m": "", "b8w8": "env PMX_PCG1_BLOCK=1 PMX_PCG1_BLOCK_ROWS=8 PMX_PCG1_BLOCK_WAVES=8 ",
+        "b8w16": "env PMX_PCG1_BLOCK=1 PMX_PCG1_BLOCK_ROWS=8 PMX_PCG1_BLOCK_WAVES=16 ",
+        "b16w8": "env PMX_PCG1_BLOCK=1 PMX_PCG1_BLOCK_ROWS=16 PMX_PCG1_BLOCK_WAVES=8 ",
+        "b16w16": "env PMX_PCG1_BLOCK=1 PMX_PCG1_BLOCK_ROWS=16 PMX_PCG1_BLOCK_WAVES=16 "}
+STUDIES["r4w"] = [
+    ("block_tests", 300, f"{PYTEST} tests/test_gpu_block.py -m gpu"),
+] + [(f"{g}_{tag}", 60, pre + bench(a)) for g, a in (("g800", _B8), ("g1600", _B16), ("g2400", _B24))
+     for tag, pre in _VAR.items()]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

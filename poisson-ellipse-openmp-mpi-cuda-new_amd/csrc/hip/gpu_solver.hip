@@ -246,6 +246,8 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
       int rows = 8;
       if (const char* er = std::getenv("PMX_PCG1_BLOCK_ROWS"); er && er[0]) rows = std::atoi(er);
       block1_ = true;
+      const char* ef = std::getenv("PMX_PCG1_BLOCK_FUSED");
+      block_fused_ = !(ef && ef[0] == '0');
       opt_.rows1 = rows;
       opt_.rows1w = rows;
       opt_.vec1 = 2;
@@ -672,10 +674,15 @@ void GpuSubdomainSolver::phase_a_kernel_only(hipStream_t s, int part) {
   if constexpr (sizeof(T) == 8) {
     if (block1_) {
       PMX_CHECK(part == 0, "block tiles run whole sweeps (undecomposed grids)");
+      const double h = g_.h1h2, wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
+      const double wts[5] = {h, h, h, h, wdiff};
+      // the reduce_n ticket (never in flight together with this sweep: same stream)
+      unsigned* ticket = block_fused_ ? reinterpret_cast<unsigned*>(reduce_ws_ + kReduceNOffset + 8 * kReduceMaxBlocks)
+                                      : nullptr;
       launch_pcg1_block<T>(geom_, tables_, static_cast<T*>(field_base(0)), static_cast<T*>(field_base(1)),
                            reinterpret_cast<T*>(r2_ + field_off_ * elem_), static_cast<T*>(field_base(2)),
                            static_cast<T*>(field_base(3)), partials_, state_, tiles1_for(w_sweep_next()), s,
-                           w_sweep_next());
+                           w_sweep_next(), wts, ticket, progress_dev_);
       return;
     }
   }
@@ -736,6 +743,10 @@ void GpuSubdomainSolver::enqueue_kernel_a_part(hipStream_t s, int part) {
   after_launch(s);
 }
 void GpuSubdomainSolver::enqueue_reduce_a(hipStream_t s) {
+  if (block1_ && block_fused_) {  // the sweep finished its own reduction
+    ++host_k_;
+    return;
+  }
   if (pcg1_) {
     const double h = g_.h1h2, wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
     const double wts[5] = {h, h, h, h, wdiff};

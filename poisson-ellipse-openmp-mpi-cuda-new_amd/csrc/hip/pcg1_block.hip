@@ -22,19 +22,32 @@
 // (pcg1_kernels.hip), including the stop test, the breakdown guard and the w-phase check.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "pcg1_march.hpp"
 
 namespace pmx {
 namespace {
 
-constexpr int kBlkWaves = 8;
+// The reduction of the sweep's partials folded into the sweep (BlockReduce::ticket non-null): every
+// workgroup publishes its partial write-through and takes a ticket; the last one sums all partials
+// in a fixed order and finishes as k_reduce_n does (weights, NaN flag, S->it bump, progress word,
+// ticket re-armed) -- one launch per iteration instead of two.  Hand-off as k_reduce_n's
+// (pcg_device.hpp: st_publish, vmcnt drain, relaxed ticket add, sc1 loads after a barrier).
+struct BlockReduce {
+  double wt[kNq];
+  unsigned* ticket;      // nullptr: plain partials for a separate k_reduce_n
+  long long* progress;   // host-mapped progress words or nullptr
+};
 
-template <typename T, int TR, bool WS>
-__global__ void __launch_bounds__(64 * kBlkWaves)
+template <typename T, int TR, int W, bool WS>
+__global__ void __launch_bounds__(64 * W)
 k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
-             double* __restrict__ partials, PcgState* S, int tiles_j, int ntiles) {
+             double* __restrict__ partials, PcgState* S, int tiles_j, int ntiles, BlockReduce R) {
   using C = double;
   constexpr int VEC = 2, WO = 64 * VEC - 4, NA = TR + 4, NB = TR + 2;
+  constexpr int kBlkWaves = W;
+  constexpr int PA = (NA + W - 1) / W, PB = (NB + W - 1) / W;  // rows per wave in stages A / B
   __shared__ double sP[NA][VEC][64];   // p^k of rows i0-2 .. i1+2 (stage A)
   __shared__ double sPo[NA][VEC][64];  // p^{k-1} of the same rows
   __shared__ double sRo[NA][VEC][64];  // r^{k-1} of the same rows
@@ -173,26 +186,35 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
   }
   __syncthreads();
 
-  // ---- stage A: p^k of rows i0-2 .. i1+2
-  for (int a = wave; a < NA; a += kBlkWaves) {
-    const int m = i0 - 2 + a;
-    const int mc = min(max(m, -1), G.nx + 2);
-    T rr[VEC], pp[VEC];
-    load_cols<T, VEC>(rold + int64_t(mc) * P, c0, cmax, rr);
-    load_cols<T, VEC>(pold + int64_t(mc) * P, c0, cmax, pp);
-    const bool rowA = interior_row(m);
-    const RowCo cA = row_co(Tb, grow(m), gjlo, gjhi);
+  // ---- stage A: p^k of rows i0-2 .. i1+2 (all of a wave's loads first, then its rows)
+  {
+    T rr[PA][VEC], pp[PA][VEC];
 #pragma unroll
-    for (int u = 0; u < VEC; ++u) {
-      const bool in = rowA && colin[u];
-      const C rom = in ? C(rr[u]) : C(0), pom = in ? C(pp[u]) : C(0);
-      C a0, a1, b0, b1;
-      coef_c<C>(cA, Tb, G, AF, s_col, u, lane, gj[u], a0, a1, b0, b1);
-      const C z = zdiv_c<C>(cA.ucls, rom, a0, a1, b0, b1, G, AF);
-      const C v = fma_c(beta, pom, z);
-      sP[a][u][lane] = in ? C(static_cast<T>(v)) : C(0);
-      sPo[a][u][lane] = pom;
-      sRo[a][u][lane] = rom;
+    for (int x = 0; x < PA; ++x) {
+      const int a = min(wave + x * W, NA - 1);  // past the last row: a harmless repeat
+      const int mc = min(max(i0 - 2 + a, -1), G.nx + 2);
+      load_cols<T, VEC>(rold + int64_t(mc) * P, c0, cmax, rr[x]);
+      load_cols<T, VEC>(pold + int64_t(mc) * P, c0, cmax, pp[x]);
+    }
+#pragma unroll
+    for (int x = 0; x < PA; ++x) {
+      const int a = wave + x * W;
+      if (a >= NA) break;
+      const int m = i0 - 2 + a;
+      const bool rowA = interior_row(m);
+      const RowCo cA = row_co(Tb, grow(m), gjlo, gjhi);
+#pragma unroll
+      for (int u = 0; u < VEC; ++u) {
+        const bool in = rowA && colin[u];
+        const C rom = in ? C(rr[x][u]) : C(0), pom = in ? C(pp[x][u]) : C(0);
+        C a0, a1, b0, b1;
+        coef_c<C>(cA, Tb, G, AF, s_col, u, lane, gj[u], a0, a1, b0, b1);
+        const C z = zdiv_c<C>(cA.ucls, rom, a0, a1, b0, b1, G, AF);
+        const C v = fma_c(beta, pom, z);
+        sP[a][u][lane] = in ? C(static_cast<T>(v)) : C(0);
+        sPo[a][u][lane] = pom;
+        sRo[a][u][lane] = rom;
+      }
     }
   }
   __syncthreads();
@@ -202,16 +224,25 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
   auto stage_b = [&](auto wm_c) {
     constexpr int WM = decltype(wm_c)::value;
     constexpr bool WUP = WM != 0;
-    for (int b = wave; b < NB; b += kBlkWaves) {
+    T wvs[PB][VEC] = {}, qvs[PB][VEC] = {};
+    if constexpr (WUP) {
+#pragma unroll
+      for (int x = 0; x < PB; ++x) {
+        const int wc = min(max(i0 - 1 + min(wave + x * W, NB - 1), -1), G.nx + 2);
+        load_cols<T, VEC>(w + int64_t(wc) * P, c0, cmax, wvs[x]);
+        // p^{k-2} still sits in the buffer this sweep overwrites with p^k: read before the store
+        if constexpr (WM == 3) load_cols<T, VEC>(pnew + int64_t(wc) * P, c0, cmax, qvs[x]);
+      }
+    }
+#pragma unroll
+    for (int x = 0; x < PB; ++x) {
+      const int b = wave + x * W;
+      if (b >= NB) break;
       const int mb = i0 - 1 + b, a = b + 1;
       const bool ownB = mb >= i0 && mb <= i1;
-      T wv[VEC] = {}, qv[VEC] = {};
-      if constexpr (WUP) {
-        const int wc = min(max(mb, -1), G.nx + 2);
-        load_cols<T, VEC>(w + int64_t(wc) * P, c0, cmax, wv);
-        // p^{k-2} still sits in the buffer this sweep overwrites with p^k: read before the store
-        if constexpr (WM == 3) load_cols<T, VEC>(pnew + int64_t(wc) * P, c0, cmax, qv);
-      }
+      const T (&wv)[VEC] = wvs[x];
+      const T (&qv)[VEC] = qvs[x];
+      (void)qv;
       C Pm1[VEC], Pm2[VEC], Pm[VEC], po1[VEC], po2[VEC], pom[VEC], ro1[VEC];
 #pragma unroll
       for (int u = 0; u < VEC; ++u) {
@@ -284,7 +315,7 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
   __syncthreads();
 
   // ---- stage C: A z^k of the owned rows, (A z, z) and (A z, p)
-  for (int c = wave; c < TR; c += kBlkWaves) {
+  for (int c = wave; c < TR; c += W) {
     const int mc = i0 + c;
     if (mc > i1) break;
     const int b = c + 1;
@@ -320,11 +351,59 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
     for (int q = 0; q < kNq; ++q) s_sum[wave][q] = acc[q];
   }
   __syncthreads();
-  if (threadIdx.x < kNq) {
-    double v = 0.0;
+  if (!R.ticket) {
+    if (threadIdx.x < kNq) {
+      double v = 0.0;
 #pragma unroll
-    for (int wv = 0; wv < kBlkWaves; ++wv) v += s_sum[wv][threadIdx.x];
-    partials[int64_t(kNq) * id + threadIdx.x] = v;
+      for (int wv = 0; wv < kBlkWaves; ++wv) v += s_sum[wv][threadIdx.x];
+      partials[int64_t(kNq) * id + threadIdx.x] = v;
+    }
+    return;
+  }
+  __shared__ int s_last;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int q = 0; q < kNq; ++q) {
+      double v = 0.0;
+#pragma unroll
+      for (int wv = 0; wv < kBlkWaves; ++wv) v += s_sum[wv][q];
+      st_publish(partials + int64_t(kNq) * id + q, v);
+    }
+    s_last = ticket_arrive_last(R.ticket, ntiles);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // the last workgroup: every wave sums a fixed slice of the partials, then the waves in order
+  double t[kNq];
+#pragma unroll
+  for (int q = 0; q < kNq; ++q) t[q] = 0.0;
+  for (int l = wave * 64 + lane; l < ntiles; l += 64 * W) {
+#pragma unroll
+    for (int q = 0; q < kNq; ++q) t[q] += ld_published(partials + int64_t(kNq) * l + q);
+  }
+  wave_sum2_mfma(t[0], t[1]);
+  wave_sum2_mfma(t[2], t[3]);
+  t[4] = wave_sum_mfma(t[4]);
+  __syncthreads();  // s_sum is reused
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < kNq; ++q) s_sum[wave][q] = t[q];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    bool bad = false;
+#pragma unroll
+    for (int q = 0; q < kNq; ++q) {
+      double v = 0.0;
+#pragma unroll
+      for (int wv = 0; wv < kBlkWaves; ++wv) v += s_sum[wv][q];
+      bad |= !(v == v) || isinf(v);
+      S->red_c[q] = v * R.wt[q];
+    }
+    if (bad) S->nan_flag = 1;
+    S->it = k + 1;
+    if (R.progress) __hip_atomic_store(R.progress, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    *R.ticket = 0u;  // re-arm for the next launch (stream order makes this visible to it)
   }
 }
 
@@ -332,26 +411,39 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
 
 template <typename T>
 void launch_pcg1_block(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1, double* partials,
-                       PcgState* S, const TileCfg& tc, hipStream_t s, bool wsweep) {
+                       PcgState* S, const TileCfg& tc, hipStream_t s, bool wsweep, const double* weights,
+                       unsigned* ticket, long long* progress) {
   static_assert(sizeof(T) == 8, "pcg1 block tiles: fp64 storage");
   PMX_CHECK(tc.kind == 3 && tc.vec == 2 && G.nb == 0, "pcg1 block tiles: VEC-2 tiling of an undecomposed grid");
   PMX_CHECK(tc.block == 124 && tc.tiles_j == (G.ny + 123) / 124, "pcg1 block tiles: 124-column tiles");
   const int n = tc.ntiles();
-#define PMX_BLK(TR)                                                                                                 \
-  if (wsweep)                                                                                                       \
-    hipLaunchKernelGGL((k_pcg1_block<T, TR, true>), dim3(n), dim3(64 * kBlkWaves), 0, s, G, Tb, w, r, r2, p0, p1,   \
-                       partials, S, tc.tiles_j, n);                                                                 \
-  else                                                                                                              \
-    hipLaunchKernelGGL((k_pcg1_block<T, TR, false>), dim3(n), dim3(64 * kBlkWaves), 0, s, G, Tb, w, r, r2, p0, p1,  \
-                       partials, S, tc.tiles_j, n)
-  if (tc.rows == 4) PMX_BLK(4);
-  else if (tc.rows == 8) PMX_BLK(8);
-  else PMX_CHECK(false, "pcg1 block tiles: 4 or 8 rows, got " << tc.rows);
+  BlockReduce R{};
+  for (int q = 0; q < kNq; ++q) R.wt[q] = weights ? weights[q] : 1.0;
+  R.ticket = ticket;
+  R.progress = progress;
+#define PMX_BLK(TR, W)                                                                                             \
+  if (wsweep)                                                                                                      \
+    hipLaunchKernelGGL((k_pcg1_block<T, TR, W, true>), dim3(n), dim3(64 * W), 0, s, G, Tb, w, r, r2, p0, p1,       \
+                       partials, S, tc.tiles_j, n, R);                                                             \
+  else                                                                                                             \
+    hipLaunchKernelGGL((k_pcg1_block<T, TR, W, false>), dim3(n), dim3(64 * W), 0, s, G, Tb, w, r, r2, p0, p1,      \
+                       partials, S, tc.tiles_j, n, R)
+  static const int waves = [] {
+    const char* e = std::getenv("PMX_PCG1_BLOCK_WAVES");
+    return e && e[0] ? std::atoi(e) : 8;
+  }();
+  if (tc.rows == 4 && waves == 8) PMX_BLK(4, 8);
+  else if (tc.rows == 8 && waves == 8) PMX_BLK(8, 8);
+  else if (tc.rows == 8 && waves == 16) PMX_BLK(8, 16);
+  else if (tc.rows == 16 && waves == 8) PMX_BLK(16, 8);
+  else if (tc.rows == 16 && waves == 16) PMX_BLK(16, 16);
+  else PMX_CHECK(false, "pcg1 block tiles: no " << tc.rows << "-row x " << waves << "-wave variant");
 #undef PMX_BLK
   HIP_CHECK(hipGetLastError());
 }
 
 template void launch_pcg1_block<double>(const DevGeom&, const DevTables&, double*, double*, double*, double*, double*,
-                                        double*, PcgState*, const TileCfg&, hipStream_t, bool);
+                                        double*, PcgState*, const TileCfg&, hipStream_t, bool, const double*,
+                                        unsigned*, long long*);
 
 }  // namespace pmx

@@ -320,7 +320,8 @@ class GpuSubdomainSolver {
   char* fields_ = nullptr;
   char* r2_ = nullptr;      // pcg1 only: the second r buffer (r is double-buffered there)
   size_t field_stride_ = 0;
-  bool block1_ = false;  // pcg1 sweeps as block tiles (pcg1_block.hip)
+  bool block1_ = false;       // pcg1 sweeps as block tiles (pcg1_block.hip)
+  bool block_fused_ = false;  // ... which also finish the reduction (no k_reduce_n launch)
   char* field_raw(int f) const { return fields_ + size_t(f) * field_stride_; }
   void place_fields();                // placement probe (see gpu_solver.hip)
   void probe_iterations(hipStream_t s, hipEvent_t e0, hipEvent_t e1);

@@ -119,11 +119,14 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
                  double* partials, PcgState* S, const TileCfg& tc, hipStream_t s, int part = 0,
                  bool wsweep = false);
 
-// pcg1 sweep with block tiles (pcg1_block.hip): one workgroup of 8 waves per tc.rows x 124 tile,
-// the three pipeline stages row-parallel; undecomposed fp64 grids; partial sums per tile as k_pcg1.
+// pcg1 sweep with block tiles (pcg1_block.hip): one workgroup per tc.rows x 124 tile, the three
+// pipeline stages row-parallel; undecomposed fp64 grids; partial sums per tile as k_pcg1.  With a
+// ticket the sweep also finishes the reduction (red_c = sums * weights, S->it + 1, progress[0]),
+// replacing launch_reduce_n.
 template <typename T>
 void launch_pcg1_block(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1, double* partials,
-                       PcgState* S, const TileCfg& tc, hipStream_t s, bool wsweep);
+                       PcgState* S, const TileCfg& tc, hipStream_t s, bool wsweep, const double* weights = nullptr,
+                       unsigned* ticket = nullptr, long long* progress = nullptr);
 
 // pcg1 ghost exchange: pack (unpack=false) the radius-2 edges of the buffers sweep `target` reads
 // (parity of target) into H.send, or unpack H.recv into their ghost cells.
