@@ -611,6 +611,18 @@ STUDIES["r4w"] = [
 ] + [(f"{g}_{tag}", 60, pre + bench(a)) for g, a in (("g800", _B8), ("g1600", _B16), ("g2400", _B24))
      for tag, pre in _VAR.items()]
 
+_G4b = "--gpus 1 --M 400 --N 600 --steps 500 --warmup 50 --no-tol-solve"
+STUDIES["r4x"] = [
+    ("g400_pers", 60, bench(_G4b)),
+    ("g400_block", 60, bench(_G4b + " --persistent off")),
+    ("g400_march", 60, "env PMX_PCG1_BLOCK=0 " + bench(_G4b + " --persistent off")),
+    ("g800_block", 60, bench(_B8)),
+    ("g800_march", 60, "env PMX_PCG1_BLOCK=0 " + bench(_B8)),
+    ("g800_block_unfused", 60, "env PMX_PCG1_BLOCK_FUSED=0 " + bench(_B8)),
+    ("g800_tol", 120, bench("--gpus 1 --M 800 --N 1200 --steps 200 --warmup 20")),
+    ("pytest_gpu_all", 800, f"{PYTEST_ALL} tests -m gpu"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

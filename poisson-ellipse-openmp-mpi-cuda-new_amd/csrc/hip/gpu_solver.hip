@@ -241,8 +241,14 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
 
   if (pcg1_) {
     // block tiles (pcg1_block.hip): undecomposed fp64 grids, the three pipeline stages row-parallel
-    // across a workgroup's waves.  Study knob for now: PMX_PCG1_BLOCK=1, PMX_PCG1_BLOCK_ROWS=4|8
-    if (const char* e = std::getenv("PMX_PCG1_BLOCK"); e && e[0] == '1' && G.nb == 0 && elem_ == 8) {
+    // across a workgroup's waves.  Auto on the grids whose march tiling is latency-bound (fewer than
+    // 4,096 four-row tiles: 800x1200 42.1 -> 34.2 us/iteration; at 1600x2400 the march wins, 61.2
+    // vs 84.3; profiles/r4/block/).  PMX_PCG1_BLOCK=0/1 forces it; PMX_PCG1_BLOCK_ROWS=4|8|16 and
+    // PMX_PCG1_BLOCK_WAVES=8|16 pick the shape (default 8 x 8).
+    int blk = opt_.block1;
+    if (const char* e = std::getenv("PMX_PCG1_BLOCK"); e && e[0]) blk = std::atoi(e);
+    const bool latency_bound = int64_t((G.nx + 3) / 4) * ((G.ny + 123) / 124) < 4096;
+    if (G.nb == 0 && elem_ == 8 && (blk == 1 || (blk == -1 && latency_bound))) {
       int rows = 8;
       if (const char* er = std::getenv("PMX_PCG1_BLOCK_ROWS"); er && er[0]) rows = std::atoi(er);
       block1_ = true;

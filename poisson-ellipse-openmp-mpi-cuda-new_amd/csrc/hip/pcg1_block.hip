@@ -43,7 +43,8 @@ struct BlockReduce {
 template <typename T, int TR, int W, bool WS>
 __global__ void __launch_bounds__(64 * W)
 k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
-             double* __restrict__ partials, PcgState* S, int tiles_j, int ntiles, BlockReduce R) {
+             double* __restrict__ partials, PcgState* S, int tiles_j, int ntiles, BlockReduce R,
+             const Pcg1Slot* __restrict__ order) {
   using C = double;
   constexpr int VEC = 2, WO = 64 * VEC - 4, NA = TR + 4, NB = TR + 2;
   constexpr int kBlkWaves = W;
@@ -142,9 +143,12 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
   }
   if (leader) S->halo_k = k + 1;
 
-  // ---- the tile
-  const int id = xcd_remap(int(blockIdx.x), int(gridDim.x));
-  if (id >= ntiles) return;  // the grid is exactly ntiles workgroups
+  // ---- the tile: dispatch slot -> tile id and its rows' coefficient classes (pcg1_build_order:
+  // the tiles the ellipse cuts first within each XCD's share, so they do not trail the sweep)
+  const int pos = xcd_remap(int(blockIdx.x), int(gridDim.x));
+  if (pos >= ntiles) return;  // the grid is exactly ntiles workgroups
+  const int id = ld_uniform(&order[pos].id, 0);
+  const unsigned long long ocls = ld_uniform(&order[pos].cls, 0);
   const int ti = id / tiles_j, tj = id - ti * tiles_j;
   const int i0 = 1 + ti * TR, i1 = min(i0 + TR - 1, G.nx);
   const int j0 = 1 + tj * WO, j1 = min(j0 + WO - 1, G.ny);
@@ -169,9 +173,10 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
   }
   const bool own_all = own[0] && own[VEC - 1];
   const bool own_any = own[0] || own[VEC - 1];
-  const int gjlo = max(G.gj0 + j0 - 2, 0), gjhi = min(G.gj0 + j0 - 2 + 64 * VEC - 1, G.N);
   auto grow = [&](int m) { return min(max(G.gi0 + m, 0), G.M); };
   auto interior_row = [&](int m) { return G.gi0 + m >= 1 && G.gi0 + m <= G.M - 1; };
+  // row m's class from the slot's 2 bits per row (rows i0-3 .. i1+2; TR + 5 <= 32)
+  auto row_of = [&](int m) { return RowCo{grow(m), int((ocls >> (2 * (m - i0 + 3))) & 3ull)}; };
   // column constants of the tile's lanes, for the exact (cut-face) coefficients: one copy per
   // workgroup, lane-private slots as pcg1_march's park_cols
   if (wave == 0) {
@@ -202,7 +207,7 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
       if (a >= NA) break;
       const int m = i0 - 2 + a;
       const bool rowA = interior_row(m);
-      const RowCo cA = row_co(Tb, grow(m), gjlo, gjhi);
+      const RowCo cA = row_of(m);
 #pragma unroll
       for (int u = 0; u < VEC; ++u) {
         const bool in = rowA && colin[u];
@@ -255,7 +260,7 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
         ro1[u] = sRo[a][u][lane];
       }
       const bool rowB = interior_row(mb);
-      const RowCo cB = row_co(Tb, grow(mb), gjlo, gjhi);
+      const RowCo cB = row_of(mb);
       const C left = dpp_shift<kWaveShr1>(Pm1[VEC - 1], C(0));
       const C right = dpp_shift<kWaveShl1>(Pm1[0], C(0));
       C oleft = C(0), oright = C(0);
@@ -326,7 +331,7 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
       Zm[u] = sZ[b - 1][u][lane];
       Zp[u] = sZ[b + 1][u][lane];
     }
-    const RowCo cC = row_co(Tb, grow(mc), gjlo, gjhi);
+    const RowCo cC = row_of(mc);
     const C left = dpp_shift<kWaveShr1>(Zc[VEC - 1], C(0));
     const C right = dpp_shift<kWaveShl1>(Zc[0], C(0));
 #pragma unroll
@@ -416,6 +421,7 @@ void launch_pcg1_block(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2,
   static_assert(sizeof(T) == 8, "pcg1 block tiles: fp64 storage");
   PMX_CHECK(tc.kind == 3 && tc.vec == 2 && G.nb == 0, "pcg1 block tiles: VEC-2 tiling of an undecomposed grid");
   PMX_CHECK(tc.block == 124 && tc.tiles_j == (G.ny + 123) / 124, "pcg1 block tiles: 124-column tiles");
+  PMX_CHECK(tc.order0 && tc.rows + 5 <= 32, "pcg1 block tiles: a dispatch order with row classes");
   const int n = tc.ntiles();
   BlockReduce R{};
   for (int q = 0; q < kNq; ++q) R.wt[q] = weights ? weights[q] : 1.0;
@@ -424,10 +430,10 @@ void launch_pcg1_block(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2,
 #define PMX_BLK(TR, W)                                                                                             \
   if (wsweep)                                                                                                      \
     hipLaunchKernelGGL((k_pcg1_block<T, TR, W, true>), dim3(n), dim3(64 * W), 0, s, G, Tb, w, r, r2, p0, p1,       \
-                       partials, S, tc.tiles_j, n, R);                                                             \
+                       partials, S, tc.tiles_j, n, R, tc.order0);                                                  \
   else                                                                                                             \
     hipLaunchKernelGGL((k_pcg1_block<T, TR, W, false>), dim3(n), dim3(64 * W), 0, s, G, Tb, w, r, r2, p0, p1,      \
-                       partials, S, tc.tiles_j, n, R)
+                       partials, S, tc.tiles_j, n, R, tc.order0)
   static const int waves = [] {
     const char* e = std::getenv("PMX_PCG1_BLOCK_WAVES");
     return e && e[0] ? std::atoi(e) : 8;

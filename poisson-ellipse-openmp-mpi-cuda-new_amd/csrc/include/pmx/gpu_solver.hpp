@@ -107,6 +107,10 @@ struct GpuOptions {
   // the smallest latency-bound grids, ~0.4 M points), 0 = off, 1 = on where it applies.
   // PMX_PERSISTENT overrides.
   int persistent = -1;
+  // Block tiles for the pcg1 sweep (pcg1_block.hip): -1 = auto (undecomposed fp64 grids with fewer
+  // than 4,096 four-row march tiles), 0 = off, 1 = on for any undecomposed fp64 grid.
+  // PMX_PCG1_BLOCK overrides.
+  int block1 = -1;
   double placement_budget_s = 0.5;
   double placement_keep_free = 0.5;
   bool resolved = false;  // environment overrides already applied (resolve_options)

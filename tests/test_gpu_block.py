@@ -20,7 +20,7 @@ def _sess(pkg, monkeypatch, M, N, rows, **kw):
         monkeypatch.setenv("PMX_PCG1_BLOCK", "1")
         monkeypatch.setenv("PMX_PCG1_BLOCK_ROWS", str(rows))
     else:
-        monkeypatch.delenv("PMX_PCG1_BLOCK", raising=False)
+        monkeypatch.setenv("PMX_PCG1_BLOCK", "0")  # the march (auto picks block tiles on small grids)
     kw.setdefault("persistent", 0)
     return pkg.make_session(pkg.PoissonEllipse(M=M, N=N), **kw)
 
@@ -41,6 +41,15 @@ def test_block_tiles_goldens_and_march_agreement(pkg, monkeypatch, rows, grid, i
         assert rb["iters"] == iters
     wb, wm = b.gather_local_w(), m.gather_local_w()
     assert np.abs(wb - wm).max() <= 1e-10 * np.abs(wm).max()
+
+
+def test_block_tiles_auto_choice(pkg, monkeypatch):
+    monkeypatch.delenv("PMX_PCG1_BLOCK", raising=False)
+    mk = lambda M, N, **kw: pkg.make_session(pkg.PoissonEllipse(M=M, N=N), persistent=0, **kw)  # noqa: E731
+    assert mk(800, 1200).tile.get("block_tiles")           # 2,000 four-row tiles: latency-bound
+    assert not mk(1600, 2400).tile.get("block_tiles")      # 8,000: the march's occupancy wins
+    assert not mk(800, 1200, ranks=2).tile.get("block_tiles")  # decomposed: the march (ghost rows)
+    assert not mk(800, 1200, dtype="fp32").tile.get("block_tiles")
 
 
 def test_block_tiles_first_sweeps_bitwise(pkg, monkeypatch):
