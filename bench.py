@@ -143,8 +143,8 @@ def parse(argv=None):
                     help="placement probe: candidate field blocks timed, the fastest kept (0 = off; "
                          "bounded by --placement-budget and --placement-keep-free; off when ranks share a GPU)")
     ap.add_argument("--persistent", default="auto", choices=["auto", "on", "off"],
-                    help="persistent iteration (one launch per batch, in-kernel grid barrier + reduction): auto = "
-                         "fp64 single-subdomain grids whose fields fit the Infinity Cache (<= 16 MB, ~0.4 M points)")
+                    help="persistent iteration (one launch per batch, in-kernel grid barrier + reduction): on = "
+                         "fp64 single-subdomain grids; auto = off (the block-tile graph replays are faster)")
     ap.add_argument("--loopback-rank", type=int, default=-1,
                     help="timing rehearsal on ONE GPU (valid=false): rank R of the --gpus-rank decomposition "
                          "alone, ghosts filled by device copies of the real sizes (from zeros), all-reduce "

@@ -623,6 +623,16 @@ STUDIES["r4x"] = [
     ("pytest_gpu_all", 800, f"{PYTEST_ALL} tests -m gpu"),
 ]
 
+# block tiles with the cut-first order: shapes x grids against the march
+_SH = {"m": "env PMX_PCG1_BLOCK=0 ", "b4": "env PMX_PCG1_BLOCK=1 PMX_PCG1_BLOCK_ROWS=4 ",
+       "b8": "env PMX_PCG1_BLOCK=1 PMX_PCG1_BLOCK_ROWS=8 ", "b16": "env PMX_PCG1_BLOCK=1 PMX_PCG1_BLOCK_ROWS=16 "}
+STUDIES["r4y"] = [(f"{g}_{tag}", 60, pre + bench(a)) for g, a in
+                  (("g400", _G4b + " --persistent off"), ("g800", _B8), ("g1600", _B16), ("g2400", _B24))
+                  for tag, pre in _SH.items()] + [
+    ("g3200", 60, "env PMX_PCG1_BLOCK=1 " + bench("--gpus 1 --M 3200 --N 4800 --steps 300 --warmup 30 --no-tol-solve")),
+    ("g3200_m", 60, "env PMX_PCG1_BLOCK=0 " + bench("--gpus 1 --M 3200 --N 4800 --steps 300 --warmup 30 --no-tol-solve")),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

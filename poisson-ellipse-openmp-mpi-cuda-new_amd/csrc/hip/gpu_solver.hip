@@ -288,14 +288,13 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   }
 
   if (pcg1_) {
-    // persistent iteration: latency-bound grids whose fields sit in the 256 MB Infinity Cache.  Auto
-    // only up to ~0.4 M points: 400x600 35.3 vs 36.9 us/iter for the graph replays, but 800x1200
-    // 43.8 vs 41.4 (2-row tiles both), 1600x2400 70.6 vs 61.0 -- with one 8-wave workgroup per CU
-    // (LDS) each wave's row march is latency-serial, and once the grid has more tiles than resident
-    // waves the replays' occupancy wins (profiles/r4/persist/)
+    // persistent iteration (one launch per batch, in-kernel grid barrier): on request only.  Its
+    // waves march rows serially; the graph replays of the block-tile sweep (pcg1_block.hip) run the
+    // same latency-bound grids faster -- 400x600 17.0 vs 35.1 us/iteration, 800x1200 26.2 vs 43.8
+    // (profiles/r4/block/, profiles/r4/persist/) -- so auto (-1) no longer picks it
     const bool eligible = G.nb == 0 && elem_ == 8 && !opt.check;
     PMX_CHECK(opt_.persistent != 1 || eligible, "the persistent iteration needs fp64 and an undecomposed grid");
-    persist_ = eligible && (opt_.persistent == 1 || (opt_.persistent == -1 && 5.0 * double(field_bytes_) <= 16e6));
+    persist_ = eligible && opt_.persistent == 1;
   }
   if (persist_) {
     pwg_ = pcg1_persist_max_wg(opt.device);

@@ -103,8 +103,8 @@ struct GpuOptions {
   // bench.py turns it on unless ranks share the device.  PMX_PLACEMENT=K overrides.
   int placement = 0;
   // Persistent iteration (pcg1_persist.hip): one launch runs a whole batch of sweeps with an
-  // in-kernel grid barrier and reduction.  -1 = auto (fp64, undecomposed, five fields <= 16 MB --
-  // the smallest latency-bound grids, ~0.4 M points), 0 = off, 1 = on where it applies.
+  // in-kernel grid barrier and reduction.  1 = on where it applies (fp64, undecomposed); -1 (auto)
+  // and 0 = off: the block-tile sweep's graph replays beat it on every grid measured.
   // PMX_PERSISTENT overrides.
   int persistent = -1;
   // Block tiles for the pcg1 sweep (pcg1_block.hip): -1 = auto (undecomposed fp64 grids with fewer

@@ -95,8 +95,9 @@ def make_session(problem: PoissonEllipse, ranks: int = 1, split: str = "referenc
     default; bounded by placement_budget_s seconds and by leaving placement_keep_free of the free
     device memory free -- see GpuSubdomainSolver::place_fields).
 
-    persistent: -1 = auto (latency-bound grids: fp64, one subdomain, fields <= 16 MB (~0.4 M points) run whole
-    batches of iterations in one persistent launch, pcg1_persist.hip), 0 = off, 1 = on."""
+    persistent: 1 = run whole batches of iterations in one persistent launch (fp64, one subdomain,
+    pcg1_persist.hip); -1 (auto) and 0 = graph replays (on small grids of the block-tile sweep,
+    pcg1_block.hip, which is faster)"""
     n = _native()
     return n.Session(problem.to_native(), world=int(ranks), comm="self" if ranks == 1 else "local",
                      split=getattr(n.Split, split), device=device, kernel=kernel, block=block, vec=vec,

@@ -37,14 +37,15 @@ def test_persistent_goldens(pkg, grid, iters):
 
 
 def test_auto_choice(pkg):
-    assert _sess(pkg, 400, 600, -1).persistent             # 10 MB of fields: one launch per batch
+    assert not _sess(pkg, 400, 600, -1).persistent         # auto: the block-tile graph replays win
     assert not _sess(pkg, 400, 600, 0).persistent
-    assert not _sess(pkg, 400, 600, -1, graph_batch=0).persistent  # individual launches asked for
-    assert not _sess(pkg, 800, 1200, -1).persistent        # 38 MB: the graph replays' occupancy wins
-    assert _sess(pkg, 800, 1200, 1).persistent             # ... but it runs there when asked for
+    assert _sess(pkg, 400, 600, 1).persistent              # on request
+    assert not _sess(pkg, 400, 600, 1, graph_batch=0).persistent  # individual launches asked for
+    assert _sess(pkg, 800, 1200, 1).persistent
     assert not _sess(pkg, 3000, 4000, -1).persistent       # 480 MB of fields: bandwidth-bound, graphs
     assert not _sess(pkg, 400, 600, -1, ranks=4).persistent  # decomposed: LocalComm graphs
-    assert not _sess(pkg, 400, 600, -1, dtype="fp32").persistent
+    with pytest.raises(RuntimeError, match="persistent"):
+        _sess(pkg, 400, 600, 1, dtype="fp32")
 
 
 @pytest.mark.parametrize("grid", [(400, 600), (800, 1200), (97, 130)])
