@@ -633,6 +633,17 @@ STUDIES["r4y"] = [(f"{g}_{tag}", 60, pre + bench(a)) for g, a in
     ("g3200_m", 60, "env PMX_PCG1_BLOCK=0 " + bench("--gpus 1 --M 3200 --N 4800 --steps 300 --warmup 30 --no-tol-solve")),
 ]
 
+# final round-4 validation: suite, smoke, driver bench, the reference grids' full solves
+STUDIES["r4z"] = [
+    ("pytest_gpu_all", 800, f"{PYTEST_ALL} tests -m gpu"),
+    ("smoke", 120, "python -c 'import __graft_entry__ as g; g.smoke()'"),
+    ("bench_driver", 300, bench("--gpus 1 --steps 20 --warmup 5")),
+    ("ref_800", 60, "poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx 800 1200 --json"),
+    ("ref_1600", 60, "poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx 1600 2400 --json"),
+    ("ref_2400", 60, "poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx 2400 3200 --json"),
+    ("phases_800", 120, bench("--gpus 1 --M 800 --N 1200 --steps 200 --warmup 20 --profile-phases 200")),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [
