@@ -644,6 +644,17 @@ STUDIES["r4z"] = [
     ("phases_800", 120, bench("--gpus 1 --M 800 --N 1200 --steps 200 --warmup 20 --profile-phases 200")),
 ]
 
+# block tiles: every global load issued before stage A, column constants only for cut tiles
+STUDIES["r4aa"] = [
+    ("block_tests", 300, f"{PYTEST} tests/test_gpu_block.py -m gpu"),
+    ("g400", 60, bench(_G4b + " --persistent off")),
+    ("g800", 60, bench(_B8)),
+    ("g800_b", 60, bench(_B8)),
+    ("g1600_b16", 60, _SH["b16"] + bench(_B16)),
+    ("g1600_b8", 60, _SH["b8"] + bench(_B16)),
+    ("g1600_m", 60, bench(_B16)),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

@@ -177,30 +177,50 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
   auto interior_row = [&](int m) { return G.gi0 + m >= 1 && G.gi0 + m <= G.M - 1; };
   // row m's class from the slot's 2 bits per row (rows i0-3 .. i1+2; TR + 5 <= 32)
   auto row_of = [&](int m) { return RowCo{grow(m), int((ocls >> (2 * (m - i0 + 3))) & 3ull)}; };
-  // column constants of the tile's lanes, for the exact (cut-face) coefficients: one copy per
-  // workgroup, lane-private slots as pcg1_march's park_cols
-  if (wave == 0) {
+  // does any row of the tile (i0-3 .. i1+2) have cut faces (class 0)?  Only then are the
+  // column constants needed
+  bool tile_cut = false;
 #pragma unroll
-    for (int u = 0; u < VEC; ++u) {
-      const ColConst cc = load_col(Tb, gj[u]);
-      s_col[(4 * u) * 64 + lane] = cc.ylo;
-      s_col[(4 * u + 1) * 64 + lane] = cc.yhi;
-      s_col[(4 * u + 2) * 64 + lane] = cc.rh0;
-      s_col[(4 * u + 3) * 64 + lane] = cc.rh1;
+  for (int q = 0; q < TR + 5; ++q) tile_cut |= ((ocls >> (2 * q)) & 3ull) == 0;
+
+  // ---- every global load of the sweep first: stage A's rows, stage B's w (and p^{k-2}) rows, the
+  // column constants -- one latency for the whole tile
+  T rr[PA][VEC], pp[PA][VEC];
+#pragma unroll
+  for (int x = 0; x < PA; ++x) {
+    const int a = min(wave + x * W, NA - 1);  // past the last row: a harmless repeat
+    const int mc = min(max(i0 - 2 + a, -1), G.nx + 2);
+    load_cols<T, VEC>(rold + int64_t(mc) * P, c0, cmax, rr[x]);
+    load_cols<T, VEC>(pold + int64_t(mc) * P, c0, cmax, pp[x]);
+  }
+  T wvs[PB][VEC] = {}, qvs[PB][VEC] = {};
+  if (WS && wm != 0) {
+#pragma unroll
+    for (int x = 0; x < PB; ++x) {
+      const int wc = min(max(i0 - 1 + min(wave + x * W, NB - 1), -1), G.nx + 2);
+      load_cols<T, VEC>(w + int64_t(wc) * P, c0, cmax, wvs[x]);
+      // p^{k-2} still sits in the buffer this sweep overwrites with p^k: read before the store
+      if (wm == 3) load_cols<T, VEC>(pnew + int64_t(wc) * P, c0, cmax, qvs[x]);
     }
   }
-  __syncthreads();
-
-  // ---- stage A: p^k of rows i0-2 .. i1+2 (all of a wave's loads first, then its rows)
-  {
-    T rr[PA][VEC], pp[PA][VEC];
+  // column constants of the tile's lanes, for the exact (cut-face) coefficients: one copy per
+  // workgroup, lane-private slots as pcg1_march's park_cols
+  if (tile_cut) {
+    if (wave == 0) {
 #pragma unroll
-    for (int x = 0; x < PA; ++x) {
-      const int a = min(wave + x * W, NA - 1);  // past the last row: a harmless repeat
-      const int mc = min(max(i0 - 2 + a, -1), G.nx + 2);
-      load_cols<T, VEC>(rold + int64_t(mc) * P, c0, cmax, rr[x]);
-      load_cols<T, VEC>(pold + int64_t(mc) * P, c0, cmax, pp[x]);
+      for (int u = 0; u < VEC; ++u) {
+        const ColConst cc = load_col(Tb, gj[u]);
+        s_col[(4 * u) * 64 + lane] = cc.ylo;
+        s_col[(4 * u + 1) * 64 + lane] = cc.yhi;
+        s_col[(4 * u + 2) * 64 + lane] = cc.rh0;
+        s_col[(4 * u + 3) * 64 + lane] = cc.rh1;
+      }
     }
+    __syncthreads();
+  }
+
+  // ---- stage A: p^k of rows i0-2 .. i1+2
+  {
 #pragma unroll
     for (int x = 0; x < PA; ++x) {
       const int a = wave + x * W;
@@ -229,16 +249,6 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
   auto stage_b = [&](auto wm_c) {
     constexpr int WM = decltype(wm_c)::value;
     constexpr bool WUP = WM != 0;
-    T wvs[PB][VEC] = {}, qvs[PB][VEC] = {};
-    if constexpr (WUP) {
-#pragma unroll
-      for (int x = 0; x < PB; ++x) {
-        const int wc = min(max(i0 - 1 + min(wave + x * W, NB - 1), -1), G.nx + 2);
-        load_cols<T, VEC>(w + int64_t(wc) * P, c0, cmax, wvs[x]);
-        // p^{k-2} still sits in the buffer this sweep overwrites with p^k: read before the store
-        if constexpr (WM == 3) load_cols<T, VEC>(pnew + int64_t(wc) * P, c0, cmax, qvs[x]);
-      }
-    }
 #pragma unroll
     for (int x = 0; x < PB; ++x) {
       const int b = wave + x * W;
