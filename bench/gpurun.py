@@ -655,6 +655,42 @@ STUDIES["r4aa"] = [
     ("g1600_m", 60, bench(_B16)),
 ]
 
+STUDIES["r4ab"] = [
+    ("g800_b12", 60, "env PMX_PCG1_BLOCK=1 PMX_PCG1_BLOCK_ROWS=12 " + bench(_B8)),
+    ("g800_b8", 60, bench(_B8)),
+    ("g1600_b12", 60, "env PMX_PCG1_BLOCK=1 PMX_PCG1_BLOCK_ROWS=12 " + bench(_B16)),
+    ("g1600_b16", 60, _SH["b16"] + bench(_B16)),
+    ("g1600_m", 60, bench(_B16)),
+    ("g1200", 60, bench("--gpus 1 --M 1200 --N 1800 --steps 500 --warmup 50 --no-tol-solve")),
+    ("g1200_m", 60, "env PMX_PCG1_BLOCK=0 " + bench("--gpus 1 --M 1200 --N 1800 --steps 500 --warmup 50 --no-tol-solve")),
+    ("g1200_b", 60, "env PMX_PCG1_BLOCK=1 " + bench("--gpus 1 --M 1200 --N 1800 --steps 500 --warmup 50 --no-tol-solve")),
+]
+
+_B12 = "env PMX_PCG1_BLOCK=1 PMX_PCG1_BLOCK_ROWS=12 "
+STUDIES["r4ac"] = [
+    ("g400_b12", 60, _B12 + bench(_G4b + " --persistent off")),
+    ("g400_b8", 60, _SH["b8"] + bench(_G4b + " --persistent off")),
+    ("g1200_b12", 60, _B12 + bench("--gpus 1 --M 1200 --N 1800 --steps 500 --warmup 50 --no-tol-solve")),
+    ("g1600_b12", 60, _B12 + bench(_B16)),
+    ("g1600_m", 60, "env PMX_PCG1_BLOCK=0 " + bench(_B16)),
+    ("g2000_b12", 60, _B12 + bench("--gpus 1 --M 2000 --N 3000 --steps 500 --warmup 50 --no-tol-solve")),
+    ("g2000_m", 60, "env PMX_PCG1_BLOCK=0 " + bench("--gpus 1 --M 2000 --N 3000 --steps 500 --warmup 50 --no-tol-solve")),
+    ("g2400_b12", 60, _B12 + bench(_B24)),
+    ("g2400_m", 60, "env PMX_PCG1_BLOCK=0 " + bench(_B24)),
+    ("g800_b12", 60, _B12 + bench(_B8)),
+]
+
+STUDIES["r4ad"] = [
+    ("block_tests", 300, f"{PYTEST} tests/test_gpu_block.py -m gpu"),
+    ("ref_800", 60, "poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx 800 1200 --json"),
+    ("ref_1600", 60, "poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx 1600 2400 --json"),
+    ("ref_2400", 60, "poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx 2400 3200 --json"),
+    ("phases_800", 120, bench("--gpus 1 --M 800 --N 1200 --steps 200 --warmup 20 --profile-phases 200")),
+    ("phases_1600", 120, bench("--gpus 1 --M 1600 --N 2400 --steps 200 --warmup 20 --profile-phases 200")),
+    ("phases_2400", 120, bench("--gpus 1 --M 2400 --N 3200 --steps 200 --warmup 20 --profile-phases 200")),
+    ("pytest_gpu_all", 800, f"{PYTEST_ALL} tests -m gpu"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

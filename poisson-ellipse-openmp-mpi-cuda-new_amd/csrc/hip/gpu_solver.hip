@@ -241,15 +241,16 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
 
   if (pcg1_) {
     // block tiles (pcg1_block.hip): undecomposed fp64 grids, the three pipeline stages row-parallel
-    // across a workgroup's waves.  Auto on the grids whose march tiling is latency-bound (fewer than
-    // 4,096 four-row tiles: 800x1200 42.1 -> 34.2 us/iteration; at 1600x2400 the march wins, 61.2
-    // vs 84.3; profiles/r4/block/).  PMX_PCG1_BLOCK=0/1 forces it; PMX_PCG1_BLOCK_ROWS=4|8|16 and
-    // PMX_PCG1_BLOCK_WAVES=8|16 pick the shape (default 8 x 8).
+    // across a workgroup's 8 waves.  Auto where the march is latency-bound, by its four-row tile
+    // count T4 (study r4ac, profiles/r4/block/, us/iteration block vs march): T4 < 1000 8-row tiles
+    // (400x600 17.3 vs 37.1), T4 < 10000 12-row tiles (800x1200 23.9 vs 42.0, 1200x1800 39.1 vs
+    // 54.1, 1600x2400 59.9 vs 61.2); above, the march (2000x3000 85.7 vs 76.1).  PMX_PCG1_BLOCK=0/1
+    // forces it, PMX_PCG1_BLOCK_ROWS=4|8|12|16 and PMX_PCG1_BLOCK_WAVES=8|16 pick the shape.
     int blk = opt_.block1;
     if (const char* e = std::getenv("PMX_PCG1_BLOCK"); e && e[0]) blk = std::atoi(e);
-    const bool latency_bound = int64_t((G.nx + 3) / 4) * ((G.ny + 123) / 124) < 4096;
-    if (G.nb == 0 && elem_ == 8 && (blk == 1 || (blk == -1 && latency_bound))) {
-      int rows = 8;
+    const int64_t t4 = int64_t((G.nx + 3) / 4) * ((G.ny + 123) / 124);
+    if (G.nb == 0 && elem_ == 8 && (blk == 1 || (blk == -1 && t4 < 10000))) {
+      int rows = t4 < 1000 ? 8 : 12;
       if (const char* er = std::getenv("PMX_PCG1_BLOCK_ROWS"); er && er[0]) rows = std::atoi(er);
       block1_ = true;
       const char* ef = std::getenv("PMX_PCG1_BLOCK_FUSED");

@@ -451,6 +451,7 @@ void launch_pcg1_block(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2,
   if (tc.rows == 4 && waves == 8) PMX_BLK(4, 8);
   else if (tc.rows == 8 && waves == 8) PMX_BLK(8, 8);
   else if (tc.rows == 8 && waves == 16) PMX_BLK(8, 16);
+  else if (tc.rows == 12 && waves == 8) PMX_BLK(12, 8);
   else if (tc.rows == 16 && waves == 8) PMX_BLK(16, 8);
   else if (tc.rows == 16 && waves == 16) PMX_BLK(16, 16);
   else PMX_CHECK(false, "pcg1 block tiles: no " << tc.rows << "-row x " << waves << "-wave variant");

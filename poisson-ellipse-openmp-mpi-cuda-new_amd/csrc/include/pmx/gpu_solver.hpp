@@ -108,7 +108,7 @@ struct GpuOptions {
   // PMX_PERSISTENT overrides.
   int persistent = -1;
   // Block tiles for the pcg1 sweep (pcg1_block.hip): -1 = auto (undecomposed fp64 grids with fewer
-  // than 4,096 four-row march tiles), 0 = off, 1 = on for any undecomposed fp64 grid.
+  // than 10,000 four-row march tiles, ~1600x2400), 0 = off, 1 = on for any undecomposed fp64 grid.
   // PMX_PCG1_BLOCK overrides.
   int block1 = -1;
   double placement_budget_s = 0.5;

@@ -25,7 +25,7 @@ def _sess(pkg, monkeypatch, M, N, rows, **kw):
     return pkg.make_session(pkg.PoissonEllipse(M=M, N=N), **kw)
 
 
-@pytest.mark.parametrize("rows", [4, 8])
+@pytest.mark.parametrize("rows", [4, 8, 12])
 @pytest.mark.parametrize("grid,iters", [((400, 600), 546), ((800, 1200), 989), ((1600, 2400), 1858),
                                         ((2400, 3200), 2449), ((97, 130), None)])
 def test_block_tiles_goldens_and_march_agreement(pkg, monkeypatch, rows, grid, iters):
@@ -46,8 +46,10 @@ def test_block_tiles_goldens_and_march_agreement(pkg, monkeypatch, rows, grid, i
 def test_block_tiles_auto_choice(pkg, monkeypatch):
     monkeypatch.delenv("PMX_PCG1_BLOCK", raising=False)
     mk = lambda M, N, **kw: pkg.make_session(pkg.PoissonEllipse(M=M, N=N), persistent=0, **kw)  # noqa: E731
-    assert mk(800, 1200).tile.get("block_tiles")           # 2,000 four-row tiles: latency-bound
-    assert not mk(1600, 2400).tile.get("block_tiles")      # 8,000: the march's occupancy wins
+    assert mk(400, 600).tile.get("block_tiles") and mk(400, 600).tile["rows"] == 8   # 500 four-row tiles
+    assert mk(800, 1200).tile.get("block_tiles") and mk(800, 1200).tile["rows"] == 12  # 2,000
+    assert mk(1600, 2400).tile.get("block_tiles")          # 8,000: still latency-bound
+    assert not mk(2000, 3000).tile.get("block_tiles")      # 12,500: the march's occupancy wins
     assert not mk(800, 1200, ranks=2).tile.get("block_tiles")  # decomposed: the march (ghost rows)
     assert not mk(800, 1200, dtype="fp32").tile.get("block_tiles")
 
