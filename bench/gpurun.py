@@ -691,6 +691,12 @@ STUDIES["r4ad"] = [
     ("pytest_gpu_all", 800, f"{PYTEST_ALL} tests -m gpu"),
 ]
 
+STUDIES["r4ae"] = [
+    ("phases_800", 120, bench("--gpus 1 --M 800 --N 1200 --steps 200 --warmup 20 --profile-phases 200")),
+    ("phases_1600", 120, bench("--gpus 1 --M 1600 --N 2400 --steps 200 --warmup 20 --profile-phases 200")),
+    ("cli_tests", 300, f"{PYTEST} tests/test_gpu_cli.py tests/test_gpu_block.py -m gpu"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

@@ -1548,7 +1548,7 @@ RunStats PcgDriver::profile_phases(int64_t n) {
     each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_kernel_a(s); });
     mark(kA);
     each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_reduce_a(s); });
-    mark(kRed);
+    if (!local_[0]->reduction_in_sweep()) mark(kRed);  // else the sweep's own tail: compute
     if (ar) {
       comm_->allreduce(local_, single_pass_ ? 2 : 0, streams_);
       mark(kAr);

@@ -262,6 +262,7 @@ class GpuSubdomainSolver {
   const ProblemSpec& spec() const { return spec_; }
   const GpuOptions& options() const { return opt_; }
   bool block_tiles() const { return block1_; }  // pcg1 sweeps as block tiles (pcg1_block.hip)
+  bool reduction_in_sweep() const { return block1_ && block_fused_; }  // no separate reduce launch
   const DevGeom& geom() const { return geom_; }
   const DevTables& tables() const { return tables_; }
   const TileCfg& tiles() const { return pcg1_ ? tiles1_ : tiles_; }  // pcg_a (or pcg1)
