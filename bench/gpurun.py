@@ -697,6 +697,20 @@ STUDIES["r4ae"] = [
     ("cli_tests", 300, f"{PYTEST} tests/test_gpu_cli.py tests/test_gpu_block.py -m gpu"),
 ]
 
+# kernel statistics of the default path on the reference grids (block tiles) and at 16384^2
+STUDIES["r4af"] = [
+    ("stats_800", 120, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4af/stats_800 -o run -- "
+                       "python3 bench.py --gpus 1 --M 800 --N 1200 --steps 500 --warmup 50 --no-tol-solve"),
+    ("stats_1600", 120, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4af/stats_1600 -o run -- "
+                        "python3 bench.py --gpus 1 --M 1600 --N 2400 --steps 500 --warmup 50 --no-tol-solve"),
+    ("tl_800_sum", 60, "python3 bench/loopback_timeline.py gpurun_out/r4af/stats_800"),
+    ("pmc_800_sq", 100, "timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS "
+                        "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_SMEM --output-format csv "
+                        "-d gpurun_out/r4af/pmc_800_sq -o run -- python3 bench.py --gpus 1 --M 800 --N 1200 "
+                        "--steps 30 --warmup 3 --graph-batch 0 --no-tol-solve"),
+    ("pmc_800_sum", 60, "python3 bench/pmc_summary.py gpurun_out/r4af --n 1000 --kernel k_pcg1_block"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [
