@@ -711,6 +711,18 @@ STUDIES["r4af"] = [
     ("pmc_800_sum", 60, "python3 bench/pmc_summary.py gpurun_out/r4af --n 1000 --kernel k_pcg1_block"),
 ]
 
+STUDIES["r4ag"] = [
+    ("block_tests", 300, f"{PYTEST} tests/test_gpu_block.py -m gpu"),
+    ("g400", 60, bench(_G4b + " --persistent off")),
+    ("g800", 60, bench(_B8)),
+    ("g1200", 60, bench("--gpus 1 --M 1200 --N 1800 --steps 500 --warmup 50 --no-tol-solve")),
+    ("g1600", 60, bench(_B16)),
+    ("g2000_b12", 60, _B12 + bench("--gpus 1 --M 2000 --N 3000 --steps 500 --warmup 50 --no-tol-solve")),
+    ("g2000_m", 60, "env PMX_PCG1_BLOCK=0 " + bench("--gpus 1 --M 2000 --N 3000 --steps 500 --warmup 50 --no-tol-solve")),
+    ("stats_1600", 120, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4ag/stats_1600 -o run -- "
+                        "python3 bench.py --gpus 1 --M 1600 --N 2400 --steps 500 --warmup 50 --no-tol-solve"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [
