@@ -142,6 +142,9 @@ def parse(argv=None):
     ap.add_argument("--placement", type=int, default=12,
                     help="placement probe: candidate field blocks timed, the fastest kept (0 = off; "
                          "bounded by --placement-budget and --placement-keep-free; off when ranks share a GPU)")
+    ap.add_argument("--block-tiles", default="auto", choices=["auto", "on", "off"],
+                    help="block-tile sweeps (pcg1_block.hip): auto = undecomposed fp64 grids with < 10,000 "
+                         "four-row march tiles")
     ap.add_argument("--persistent", default="auto", choices=["auto", "on", "off"],
                     help="persistent iteration (one launch per batch, in-kernel grid barrier + reduction): on = "
                          "fp64 single-subdomain grids; auto = off (the block-tile graph replays are faster)")
@@ -579,6 +582,7 @@ def measure(args) -> int:
     elif world == 1:
         models = importlib.import_module(pkg_name + ".models")
         runner = ds.SessionRunner(models.make_session(problem, ranks=1, device=info.local_rank, persistent=persistent,
+                                                      block_tiles={"auto": -1, "on": 1, "off": 0}[args.block_tiles],
                                                       **pkw, **kw), problem, info)
         comm_used = "self"
     elif share and cfg["comm"] == "ipc":

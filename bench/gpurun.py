@@ -723,6 +723,15 @@ STUDIES["r4ag"] = [
                         "python3 bench.py --gpus 1 --M 1600 --N 2400 --steps 500 --warmup 50 --no-tol-solve"),
 ]
 
+STUDIES["r4ah"] = [
+    ("stats_1600_m", 120, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4ah/stats_1600_m -o run -- "
+                          "python3 bench.py --gpus 1 --M 1600 --N 2400 --steps 500 --warmup 50 --no-tol-solve --block-tiles off"),
+    ("stats_1200_m", 120, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4ah/stats_1200_m -o run -- "
+                          "python3 bench.py --gpus 1 --M 1200 --N 1800 --steps 500 --warmup 50 --no-tol-solve --block-tiles off"),
+    ("stats_800_m", 120, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4ah/stats_800_m -o run -- "
+                         "python3 bench.py --gpus 1 --M 800 --N 1200 --steps 500 --warmup 50 --no-tol-solve --block-tiles off"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

@@ -182,9 +182,11 @@ GpuOptions make_options(int device, const std::string& kernel, int block, int ve
                         int tile_rows, const std::string& dtype, bool exact, int graph_batch, bool check,
                         bool overlap = true, int vec_b = 0, int waves_b = 0, int tile_rows_b = -1,
                         bool poison_halos = false, bool b_ring = false, int algo = -1, int placement = 0,
-                        double placement_budget_s = 0.5, double placement_keep_free = 0.5, int persistent = -1) {
+                        double placement_budget_s = 0.5, double placement_keep_free = 0.5, int persistent = -1,
+                        int block1 = -1) {
   GpuOptions o;
   o.persistent = persistent;
+  o.block1 = block1;
   o.placement = placement;
   o.placement_budget_s = placement_budget_s;
   o.placement_keep_free = placement_keep_free;
@@ -449,13 +451,14 @@ PYBIND11_MODULE(_pmx, m) {
                        bool rccl_graph, bool overlap, int vec_b, int waves_b, int tile_rows_b,
                        bool poison_halos, bool b_ring, int algo, bool defer_connect, int threaded,
                        int placement, double placement_budget_s, double placement_keep_free, int sharing,
-                       int persistent) {
+                       int persistent, int block_tiles) {
              SessionConfig c;
              c.sharing = sharing;
              c.spec = s;
              c.opt = make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact,
                                   graph_batch, check, overlap, vec_b, waves_b, tile_rows_b, poison_halos,
-                                  b_ring, algo, placement, placement_budget_s, placement_keep_free, persistent);
+                                  b_ring, algo, placement, placement_budget_s, placement_keep_free, persistent,
+                                  block_tiles);
              c.defer_connect = defer_connect;
              c.threaded = threaded;
              c.split = split;
@@ -483,7 +486,8 @@ PYBIND11_MODULE(_pmx, m) {
            py::arg("waves_b") = 0, py::arg("tile_rows_b") = -1, py::arg("poison_halos") = false,
            py::arg("b_ring") = false, py::arg("algo") = -1, py::arg("defer_connect") = false,
            py::arg("threaded") = -1, py::arg("placement") = 0, py::arg("placement_budget_s") = 0.5,
-           py::arg("placement_keep_free") = 0.5, py::arg("sharing") = 0, py::arg("persistent") = -1)
+           py::arg("placement_keep_free") = 0.5, py::arg("sharing") = 0, py::arg("persistent") = -1,
+           py::arg("block_tiles") = -1)
       .def("ipc_export", [](Session& s) { return py::bytes(s.ipc_export()); },
            "IPC session: this rank's memory handles (pass every rank's to connect_ipc)")
       .def("connect_ipc", [](Session& s, std::vector<py::bytes> ex) {
