@@ -732,6 +732,13 @@ STUDIES["r4ah"] = [
                          "python3 bench.py --gpus 1 --M 800 --N 1200 --steps 500 --warmup 50 --no-tol-solve --block-tiles off"),
 ]
 
+STUDIES["r4ai"] = [
+    ("pytest_gpu_all", 800, f"{PYTEST_ALL} tests -m gpu"),
+    ("smoke", 120, "python -c 'import __graft_entry__ as g; g.smoke()'"),
+    ("bench_driver", 300, bench("--gpus 1 --steps 20 --warmup 5")),
+    ("loopback8", 120, bench(_LB + " --placement 0")),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [
