@@ -739,6 +739,33 @@ STUDIES["r4ai"] = [
     ("loopback8", 120, bench(_LB + " --placement 0")),
 ]
 
+# cross-stream events with a device-scope fence (PMX_EVENT_FENCE) on the loopback rank's split sweep
+_F = lambda f: f"env PMX_EVENT_FENCE={f} "  # noqa: E731
+STUDIES["r4aj"] = [
+    ("lb8_f0", 120, _F(0) + bench(_LB + " --placement 0")),
+    ("lb8_f1", 120, _F(1) + bench(_LB + " --placement 0")),
+    ("lb8_f2", 120, _F(2) + bench(_LB + " --placement 0")),
+    ("lb8_f0b", 120, _F(0) + bench(_LB + " --placement 0")),
+    ("lb8_f1b", 120, _F(1) + bench(_LB + " --placement 0")),
+    ("lb5_f0", 120, _F(0) + bench(_LB5 + " --placement 0")),
+    ("lb5_f1", 120, _F(1) + bench(_LB5 + " --placement 0")),
+    ("tests_f1", 400, "env PMX_EVENT_FENCE=1 " + f"{PYTEST} tests/test_gpu_pcg1.py tests/test_gpu_launch_path.py tests/test_gpu_dist.py -m gpu"),
+]
+
+# march tile height / prefetch on the 8-GPU strip rank (loopback) and on 1600x2400
+_R = lambda r, w=None: f"env PMX_PCG1_ROWS={r} PMX_PCG1_ROWS_W={w or r} "  # noqa: E731
+STUDIES["r4ak"] = [
+    ("lb8_r4", 120, _R(4) + bench(_LB + " --placement 0")),
+    ("lb8_r6", 120, _R(6) + bench(_LB + " --placement 0")),
+    ("lb8_r8", 120, _R(8) + bench(_LB + " --placement 0")),
+    ("lb8_r12", 120, _R(12) + bench(_LB + " --placement 0")),
+    ("lb8_r16", 120, _R(16) + bench(_LB + " --placement 0")),
+    ("lb8_r8_12", 120, _R(8, 12) + bench(_LB + " --placement 0")),
+    ("lb8_r12_8", 120, _R(12, 8) + bench(_LB + " --placement 0")),
+    ("lb8_pf2", 120, "env PMX_PCG1_PF=2 PMX_PCG1_PF_W=2 " + bench(_LB + " --placement 0")),
+    ("lb8_r8b", 120, _R(8) + bench(_LB + " --placement 0")),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [
