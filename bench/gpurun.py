@@ -766,6 +766,27 @@ STUDIES["r4ak"] = [
     ("lb8_r8b", 120, _R(8) + bench(_LB + " --placement 0")),
 ]
 
+# frame tiles on the comm stream ahead of their exchange (PMX_FRAME_ON_COMM): 2 cross-stream edges
+# per iteration instead of 4
+_FC = lambda f: f"env PMX_FRAME_ON_COMM={f} "  # noqa: E731
+STUDIES["r4al"] = [
+    ("lb8_fc0", 120, _FC(0) + bench(_LB + " --placement 0")),
+    ("lb8_fc1", 120, _FC(1) + bench(_LB + " --placement 0")),
+    ("lb8_fc0b", 120, _FC(0) + bench(_LB + " --placement 0")),
+    ("lb8_fc1b", 120, _FC(1) + bench(_LB + " --placement 0")),
+    ("lb8_fc0_d", 120, _FC(0) + _DELAY + bench(_LB + " --placement 0")),
+    ("lb8_fc1_d", 120, _FC(1) + _DELAY + bench(_LB + " --placement 0")),
+    ("lb5_fc0", 120, _FC(0) + bench(_LB5 + " --placement 0")),
+    ("lb5_fc1", 120, _FC(1) + bench(_LB5 + " --placement 0")),
+    ("lb2_fc0", 120, _FC(0) + bench("--gpus 2 --loopback-rank 0 --steps 300 --warmup 30 --placement 0")),
+    ("lb2_fc1", 120, _FC(1) + bench("--gpus 2 --loopback-rank 0 --steps 300 --warmup 30 --placement 0")),
+    ("tl_fc1", 120, "env PMX_FRAME_ON_COMM=1 rocprofv3 --kernel-trace --stats --output-format csv "
+                    "-d gpurun_out/r4al/tl_fc1 -o run -- python3 bench.py " + _LB + " --placement 0"),
+    ("tl_fc1_sum", 60, "python3 bench/loopback_timeline.py gpurun_out/r4al/tl_fc1"),
+    ("tests_fc1", 500, "env PMX_FRAME_ON_COMM=1 " + f"{PYTEST} tests/test_gpu_pcg1.py tests/test_gpu_launch_path.py "
+                       "tests/test_gpu_dist.py tests/test_gpu_solver.py -m gpu"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

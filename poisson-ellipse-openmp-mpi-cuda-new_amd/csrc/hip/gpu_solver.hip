@@ -1083,6 +1083,8 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
       ev(ev_swept_);
     }
     if (same_device) frame_streams_.resize(local_.size(), frame_streams_[0]);
+    const char* fc = std::getenv("PMX_FRAME_ON_COMM");
+    frame_on_comm_ = fc && fc[0] == '1';
   }
 }
 
@@ -1169,21 +1171,32 @@ void PcgDriver::halo_exchange_pcg1(std::vector<hipStream_t>& streams, long long 
 // So the ghost exchange of sweep k runs under the reduction, the all-reduce AND the interior of
 // sweep k+1; only the frame tiles (a few % of the sweep) wait for it.
 void PcgDriver::enqueue_split_iteration() {
+  // frame_on_comm_: F is the comm stream H itself.  The exchange of sweep k reads only edge lines
+  // the frame tiles own (rows / columns 1, 2 and n-1, n: every tile whose march reaches a ghost cell
+  // is a frame tile, pcg1_tiles) and writes only ghost cells, which no interior tile reads; so H
+  // runs frame k -> exchange k -> (wait all-reduce k) frame k+1 in its own order, and the compute
+  // stream joins it once per iteration, before the reduction:
+  //   C: ev_ar -> interior k -> wait ev_fdone -> reduce -> all-reduce k -> ev_ar ...
+  //   H: wait ev_ar -> frame k -> ev_fdone -> pack -> send/recv -> unpack -> ev_halo
+  const bool fc = frame_on_comm_;
+  auto fstream = [&](size_t i) { return fc ? comm_streams_[i] : frame_streams_[i]; };
   for_each_stream([&](size_t i, size_t u) {
     HIP_CHECK(hipEventRecord(ev_ar_[u], streams_[i]));
-    HIP_CHECK(hipStreamWaitEvent(frame_streams_[i], ev_ar_[u], 0));
-    if (halo_pending_) HIP_CHECK(hipStreamWaitEvent(frame_streams_[i], ev_halo_[u], 0));
+    HIP_CHECK(hipStreamWaitEvent(fstream(i), ev_ar_[u], 0));
+    if (halo_pending_ && !fc) HIP_CHECK(hipStreamWaitEvent(frame_streams_[i], ev_halo_[u], 0));
   });
   for (size_t i = 0; i < local_.size(); ++i) {
     HIP_CHECK(hipSetDevice(local_[i]->device()));
     local_[i]->enqueue_kernel_a_part(streams_[i], 1);
-    local_[i]->enqueue_kernel_a_part(frame_streams_[i], 2);
+    local_[i]->enqueue_kernel_a_part(fstream(i), 2);
   }
   for_each_stream([&](size_t i, size_t u) {
-    HIP_CHECK(hipEventRecord(ev_fdone_[u], frame_streams_[i]));
+    HIP_CHECK(hipEventRecord(ev_fdone_[u], fstream(i)));
     HIP_CHECK(hipStreamWaitEvent(streams_[i], ev_fdone_[u], 0));
-    HIP_CHECK(hipEventRecord(ev_swept_[u], streams_[i]));
-    HIP_CHECK(hipStreamWaitEvent(comm_streams_[i], ev_swept_[u], 0));
+    if (!fc) {
+      HIP_CHECK(hipEventRecord(ev_swept_[u], streams_[i]));
+      HIP_CHECK(hipStreamWaitEvent(comm_streams_[i], ev_swept_[u], 0));
+    }
   });
   set_halo_target(local_[0]->host_k() + 1);  // the sweep just enqueued is host_k; the next reads its outputs
   comm_->before_pack(local_, comm_streams_);

@@ -523,6 +523,9 @@ class PcgDriver {
   bool halo_pending_ = false;  // a ghost exchange on the comm stream not yet joined
   std::vector<hipStream_t> frame_streams_;
   std::vector<hipEvent_t> ev_ar_, ev_fdone_, ev_swept_;
+  // frame tiles on the comm stream, ahead of the exchange that reads their edge lines (two
+  // cross-stream edges per iteration instead of four; enqueue_split_iteration)
+  bool frame_on_comm_ = false;
   bool graph_failed_ = false;  // capture is not possible for this driver: eager launches
   std::vector<hipGraph_t> graphs_;
   std::vector<hipGraphExec_t> execs_;
