@@ -1083,8 +1083,11 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
       ev(ev_swept_);
     }
     if (same_device) frame_streams_.resize(local_.size(), frame_streams_[0]);
+    // default on: loopback rank 3 of 8 284.2 / 284.5 vs 288.0 / 286.9 us, 301.8 vs 308.4 with the
+    // 20 / 15-us exchange / all-reduce stand-ins (profiles/r4/loopback/r4al_*); PMX_FRAME_ON_COMM=0
+    // restores the separate frame stream
     const char* fc = std::getenv("PMX_FRAME_ON_COMM");
-    frame_on_comm_ = fc && fc[0] == '1';
+    frame_on_comm_ = !(fc && fc[0] == '0');
   }
 }
 
@@ -1162,7 +1165,8 @@ void PcgDriver::halo_exchange_pcg1(std::vector<hipStream_t>& streams, long long 
   }
 }
 
-// Split sweep k (pcg1, decomposed, overlap on).  Streams C (compute), F (frame), H (comm):
+// Split sweep k (pcg1, decomposed, overlap on).  Default schedule: see frame_on_comm_ below.
+// With PMX_FRAME_ON_COMM=0, streams C (compute), F (frame), H (comm):
 //   C: [all-reduce k-1] -> ev_ar -> interior tiles of sweep k ----------> wait F -> ev_swept ->
 //   F:                     wait ev_ar (+ ev_halo of k-1) -> frame tiles -'
 //   C: reduce -> all-reduce k (no join: see the end of enqueue_split_iteration)
@@ -1171,7 +1175,7 @@ void PcgDriver::halo_exchange_pcg1(std::vector<hipStream_t>& streams, long long 
 // So the ghost exchange of sweep k runs under the reduction, the all-reduce AND the interior of
 // sweep k+1; only the frame tiles (a few % of the sweep) wait for it.
 void PcgDriver::enqueue_split_iteration() {
-  // frame_on_comm_: F is the comm stream H itself.  The exchange of sweep k reads only edge lines
+  // frame_on_comm_ (default): F is the comm stream H itself.  The exchange of sweep k reads only edge lines
   // the frame tiles own (rows / columns 1, 2 and n-1, n: every tile whose march reaches a ghost cell
   // is a frame tile, pcg1_tiles) and writes only ghost cells, which no interior tile reads; so H
   // runs frame k -> exchange k -> (wait all-reduce k) frame k+1 in its own order, and the compute
@@ -1220,7 +1224,7 @@ void PcgDriver::enqueue_split_iteration() {
   // No join of the comm stream here: the exchange (packed or direct rows) reads the edge lines of
   // r_{k+1}, p_{k+1} and writes their ghost cells, with the buffer parity in its launch arguments;
   // sweep k+1 writes the other parity (r_{k+2}, p_{k+2}), its interior tiles read no ghost cell and
-  // its frame tiles wait for ev_halo.  Sweep k+2, the next writer of these buffers, follows the
+  // its frame tiles wait for ev_halo (or follow the exchange on H).  Sweep k+2, the next writer of these buffers, follows the
   // all-reduce of k+1, which follows that frame.  So the next interior starts right after the
   // all-reduce: one cross-queue wait per iteration instead of two (loopback strip 3 of 8: 293 ->
   // 266 us, profiles/r4/loopback/).
