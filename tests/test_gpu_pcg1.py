@@ -106,14 +106,20 @@ def test_pcg1_decomposed_overlap_bitwise(pkg, monkeypatch, graph_batch):
 @pytest.mark.parametrize("graph_batch", [0, 32])
 def test_pcg1_split_sweep_matches_single_subdomain(pkg, monkeypatch, ranks, split, graph_batch):
     """Split sweep (the RCCL default): interior tiles on the compute stream while the previous
-    ghost exchange is in flight on the comm stream, frame tiles on a third stream after it.
+    ghost exchange is in flight; the frame tiles on the comm stream ahead of their own exchange
+    (default) or on a third stream after it (PMX_FRAME_ON_COMM=0) -- bitwise the same.
     Same iteration count and solution as one subdomain, eager and graph-captured."""
     p = pkg.PoissonEllipse(M=400, N=600)
     ref = _solve(pkg, monkeypatch, 1, p)
     monkeypatch.setenv("PMX_PCG1_SPLIT", "1")
-    r = _solve(pkg, monkeypatch, 1, p, ranks=ranks, split=split, graph_batch=graph_batch)
-    assert r.iters == ref.iters == 546
-    assert np.abs(r.w - ref.w).max() < 1e-11
+    out = []
+    for fc in ("1", "0"):
+        monkeypatch.setenv("PMX_FRAME_ON_COMM", fc)
+        r = _solve(pkg, monkeypatch, 1, p, ranks=ranks, split=split, graph_batch=graph_batch)
+        assert r.iters == ref.iters == 546
+        assert np.abs(r.w - ref.w).max() < 1e-11
+        out.append(r.w)
+    assert np.array_equal(out[0], out[1])
 
 
 # ---- w schedule: pairs (PMX_PCG1_WCYCLE=2) vs triples (default in fp64), triples re-reading
