@@ -787,6 +787,26 @@ STUDIES["r4al"] = [
                        "tests/test_gpu_dist.py tests/test_gpu_solver.py -m gpu"),
 ]
 
+# block tiles: two tiles per workgroup (PMX_PCG1_BLOCK_NT=2, both tiles' loads up front, one partial)
+_NT = lambda n: f"env PMX_PCG1_BLOCK_NT={n} "  # noqa: E731
+_G12 = "--gpus 1 --M 1200 --N 1800 --steps 500 --warmup 50 --no-tol-solve"
+_G24 = "--gpus 1 --M 2400 --N 3200 --steps 500 --warmup 50 --no-tol-solve"
+STUDIES["r4am"] = [
+    ("g1600_nt1", 60, _NT(1) + bench(_B16)),
+    ("g1600_nt2", 60, _NT(2) + bench(_B16)),
+    ("g800_nt1", 60, _NT(1) + bench(_B8)),
+    ("g800_nt2", 60, _NT(2) + bench(_B8)),
+    ("g1200_nt1", 60, _NT(1) + bench(_G12)),
+    ("g1200_nt2", 60, _NT(2) + bench(_G12)),
+    ("g2400_b12_nt2", 60, _NT(2) + _B12 + bench(_G24)),
+    ("g2400_m", 60, bench(_G24)),
+    ("g1600_nt2_b", 60, _NT(2) + bench(_B16)),
+    ("g1600_nt1_b", 60, _NT(1) + bench(_B16)),
+    ("ref_800_nt2", 60, _NT(2) + "poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx 800 1200 --json"),
+    ("ref_1600_nt2", 60, _NT(2) + "poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx 1600 2400 --json"),
+    ("block_tests", 300, f"{PYTEST} tests/test_gpu_block.py -m gpu"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [
