@@ -807,6 +807,17 @@ STUDIES["r4am"] = [
     ("block_tests", 300, f"{PYTEST} tests/test_gpu_block.py -m gpu"),
 ]
 
+# block tiles: dispatch slot read in the state's load batch (one round trip fewer per workgroup)
+STUDIES["r4an"] = [
+    ("g1600", 60, bench(_B16)),
+    ("g800", 60, bench(_B8)),
+    ("g1200", 60, bench(_G12)),
+    ("g400", 60, bench(_G4b + " --persistent off")),
+    ("g1600_b", 60, bench(_B16)),
+    ("g800_b", 60, bench(_B8)),
+    ("block_tests", 300, f"{PYTEST} tests/test_gpu_block.py -m gpu"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

@@ -59,6 +59,12 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
   // ---- prologue: k_pcg1's scalars of sweep k (every workgroup computes the same values)
   typedef const __attribute__((address_space(4))) PcgState CState;
   const CState* Sc = (const CState*)S;  // NOLINT: address-space cast
+  // the dispatch slot is read in the same batch as the state (as k_pcg1's prologue): the tile's
+  // loads then wait for one round trip, not for the state's and then the slot's
+  asm volatile("" ::"s"(S), "s"(order), "s"(gridDim.x));  // kernel arguments: one batch
+  const int pos = xcd_remap(int(blockIdx.x), int(gridDim.x));
+  const int id = ld_uniform(&order[pos].id, 0);  // pos < gridDim.x = ntiles (launch_pcg1_block)
+  const unsigned long long ocls = ld_uniform(&order[pos].cls, 0);
   const int st_done = Sc->done;
   const long long k = Sc->it;
   double rc[kNq], al[4], be[4];
@@ -77,6 +83,9 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
     const int j = int(i & 3);
     return j == 0 ? v[0] : j == 1 ? v[1] : j == 2 ? v[2] : v[3];
   };
+  asm volatile("" ::"s"(st_done), "s"(k), "s"(id), "s"(ocls), "s"(rc[0]), "s"(rc[1]), "s"(rc[2]), "s"(rc[3]), "s"(rc[4]),
+               "s"(al[0]), "s"(al[1]), "s"(al[2]), "s"(al[3]), "s"(be[0]), "s"(be[1]), "s"(be[2]), "s"(be[3]),
+               "s"(zr0), "s"(zr1), "s"(s_delta), "s"(s_bd_tol), "s"(s_pmb), "s"(s_max_iter), "s"(s_norm), "s"(cyc));
   if (st_done) return;
   const bool leader = blockIdx.x == 0 && threadIdx.x == 0;
   double alpha = 0.0, beta = 0.0, c1 = 0.0, c2 = 0.0;
@@ -145,10 +154,7 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
 
   // ---- the tile: dispatch slot -> tile id and its rows' coefficient classes (pcg1_build_order:
   // the tiles the ellipse cuts first within each XCD's share, so they do not trail the sweep)
-  const int pos = xcd_remap(int(blockIdx.x), int(gridDim.x));
   if (pos >= ntiles) return;  // the grid is exactly ntiles workgroups
-  const int id = ld_uniform(&order[pos].id, 0);
-  const unsigned long long ocls = ld_uniform(&order[pos].cls, 0);
   const int ti = id / tiles_j, tj = id - ti * tiles_j;
   const int i0 = 1 + ti * TR, i1 = min(i0 + TR - 1, G.nx);
   const int j0 = 1 + tj * WO, j1 = min(j0 + WO - 1, G.ny);
