@@ -818,6 +818,19 @@ STUDIES["r4an"] = [
     ("block_tests", 300, f"{PYTEST} tests/test_gpu_block.py -m gpu"),
 ]
 
+# block tiles: cut tiles' row constants staged in LDS with the tile's loads (no scalar round trip per stage)
+STUDIES["r4ao"] = [
+    ("g800", 60, bench(_B8)),
+    ("g1600", 60, bench(_B16)),
+    ("g1200", 60, bench(_G12)),
+    ("g400", 60, bench(_G4b + " --persistent off")),
+    ("g800_b", 60, bench(_B8)),
+    ("g1600_b", 60, bench(_B16)),
+    ("g1600_unfused", 60, "env PMX_PCG1_BLOCK_FUSED=0 " + bench(_B16)),
+    ("g1200_unfused", 60, "env PMX_PCG1_BLOCK_FUSED=0 " + bench(_G12)),
+    ("block_tests", 300, f"{PYTEST} tests/test_gpu_block.py -m gpu"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

@@ -54,6 +54,7 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
   __shared__ double sRo[NA][VEC][64];  // r^{k-1} of the same rows
   __shared__ double sZ[NB][VEC][64];   // z^k of rows i0-1 .. i1+1 (stage B)
   __shared__ double s_col[4 * VEC * 64];
+  __shared__ RowConst s_row[TR + 5];   // row constants of rows i0-3 .. i1+2 (tiles with cut rows)
   __shared__ double s_sum[kBlkWaves][kNq];
 
   // ---- prologue: k_pcg1's scalars of sweep k (every workgroup computes the same values)
@@ -209,8 +210,9 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
       if (wm == 3) load_cols<T, VEC>(pnew + int64_t(wc) * P, c0, cmax, qvs[x]);
     }
   }
-  // column constants of the tile's lanes, for the exact (cut-face) coefficients: one copy per
-  // workgroup, lane-private slots as pcg1_march's park_cols
+  // column constants of the tile's lanes and row constants of its rows, for the exact (cut-face)
+  // coefficients: one copy per workgroup, lane-private column slots as pcg1_march's park_cols; the
+  // rows' constants come in with the tile's loads instead of a scalar round trip in every stage
   if (tile_cut) {
     if (wave == 0) {
 #pragma unroll
@@ -221,9 +223,36 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
         s_col[(4 * u + 2) * 64 + lane] = cc.rh0;
         s_col[(4 * u + 3) * 64 + lane] = cc.rh1;
       }
+    } else if (wave == 1 && lane < TR + 5) {  // the fields of load_row, one row per lane
+      const int gi = grow(i0 - 3 + lane);
+      RowConst rc;
+      rc.rv0 = Tb.rv[gi];
+      rc.rv1 = Tb.rv[gi + 1];
+      rc.xlo = Tb.xlo[gi];
+      rc.xhi = Tb.xhi[gi];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        rc.ca0[q] = Tb.acls[4 * gi + q];
+        rc.ca1[q] = Tb.acls[4 * (gi + 1) + q];
+        rc.cb[q] = Tb.bcls[4 * gi + q];
+      }
+      s_row[lane] = rc;
     }
     __syncthreads();
   }
+  // coef() with the row's constants from s_row (row m, class c)
+  auto coef_t = [&](const RowCo& c, int m, int u, C& a0, C& a1, C& b0, C& b1) {
+    if (c.ucls != 0) {
+      a0 = a1 = b0 = b1 = c.ucls == 1 ? 1.0 : G.inv_eps;
+    } else {
+      const RowConst rc = s_row[m - i0 + 3];
+      const ColConst cc = col_lds(s_col, u, lane, gj[u]);
+      a0 = face_a0c(cc, rc, G);
+      a1 = face_a1c(cc, rc, G);
+      b0 = face_b0c(cc, rc, G);
+      b1 = face_b1c(cc, rc, G);
+    }
+  };
 
   // ---- stage A: p^k of rows i0-2 .. i1+2
   {
@@ -239,7 +268,7 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
         const bool in = rowA && colin[u];
         const C rom = in ? C(rr[x][u]) : C(0), pom = in ? C(pp[x][u]) : C(0);
         C a0, a1, b0, b1;
-        coef_c<C>(cA, Tb, G, AF, s_col, u, lane, gj[u], a0, a1, b0, b1);
+        coef_t(cA, m, u, a0, a1, b0, b1);
         const C z = zdiv_c<C>(cA.ucls, rom, a0, a1, b0, b1, G, AF);
         const C v = fma_c(beta, pom, z);
         sP[a][u][lane] = in ? C(static_cast<T>(v)) : C(0);
@@ -288,7 +317,7 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
 #pragma unroll
       for (int u = 0; u < VEC; ++u) {
         C a0, a1, b0, b1;
-        coef_c<C>(cB, Tb, G, AF, s_col, u, lane, gj[u], a0, a1, b0, b1);
+        coef_t(cB, mb, u, a0, a1, b0, b1);
         const C Ap = apply_c<C>(Pm1[u], Pm2[u], Pm[u], u == 0 ? left : Pm1[u - 1],
                                 u == VEC - 1 ? right : Pm1[u + 1], a0, a1, b0, b1, G, AF);
         const bool in = rowB && colin[u];
@@ -353,7 +382,7 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
 #pragma unroll
     for (int u = 0; u < VEC; ++u) {
       C a0, a1, b0, b1;
-      coef_c<C>(cC, Tb, G, AF, s_col, u, lane, gj[u], a0, a1, b0, b1);
+      coef_t(cC, mc, u, a0, a1, b0, b1);
       const C Az = apply_c<C>(Zc[u], Zm[u], Zp[u], u == 0 ? left : Zc[u - 1], u == VEC - 1 ? right : Zc[u + 1],
                               a0, a1, b0, b1, G, AF);
       if (own[u]) {
