@@ -831,6 +831,40 @@ STUDIES["r4ao"] = [
     ("block_tests", 300, f"{PYTEST} tests/test_gpu_block.py -m gpu"),
 ]
 
+# block tiles: reduction folded into the sweep (default) vs a separate k_reduce_n, by grid
+_UF = "env PMX_PCG1_BLOCK_FUSED=0 "
+STUDIES["r4ap"] = [
+    ("g800_f", 60, bench(_B8)),
+    ("g800_u", 60, _UF + bench(_B8)),
+    ("g400_f", 60, bench(_G4b + " --persistent off")),
+    ("g400_u", 60, _UF + bench(_G4b + " --persistent off")),
+    ("g1200_f", 60, bench(_G12)),
+    ("g1200_u", 60, _UF + bench(_G12)),
+    ("g1600_f", 60, bench(_B16)),
+    ("g1600_u", 60, _UF + bench(_B16)),
+    ("g800_f2", 60, bench(_B8)),
+    ("g800_u2", 60, _UF + bench(_B8)),
+    ("g2000_u", 60, "env PMX_PCG1_BLOCK=1 PMX_PCG1_BLOCK_ROWS=12 " + _UF +
+     bench("--gpus 1 --M 2000 --N 3000 --steps 500 --warmup 50 --no-tol-solve")),
+    ("g2000_m", 60, bench("--gpus 1 --M 2000 --N 3000 --steps 500 --warmup 50 --no-tol-solve")),
+    ("g2400_u", 60, "env PMX_PCG1_BLOCK=1 PMX_PCG1_BLOCK_ROWS=12 " + _UF + bench(_G24)),
+    ("g2400_m", 60, bench(_G24)),
+]
+
+# the fused/separate reduction rule by tile count; reference grids end to end
+STUDIES["r4aq"] = [
+    ("block_tests", 300, f"{PYTEST} tests/test_gpu_block.py tests/test_gpu_cli.py -m gpu"),
+    ("g1600", 60, bench(_B16)),
+    ("g1200", 60, bench(_G12)),
+    ("g800", 60, bench(_B8)),
+    ("g400", 60, bench(_G4b + " --persistent off")),
+    ("ref_800", 60, "poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx 800 1200 --json"),
+    ("ref_1600", 60, "poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx 1600 2400 --json"),
+    ("ref_2400", 60, "poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx 2400 3200 --json"),
+    ("phases_800", 120, bench("--gpus 1 --M 800 --N 1200 --steps 200 --warmup 20 --profile-phases 200")),
+    ("phases_1600", 120, bench("--gpus 1 --M 1600 --N 2400 --steps 200 --warmup 20 --profile-phases 200")),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

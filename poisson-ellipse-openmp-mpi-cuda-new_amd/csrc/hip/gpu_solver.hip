@@ -253,8 +253,13 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
       int rows = t4 < 1000 ? 8 : 12;
       if (const char* er = std::getenv("PMX_PCG1_BLOCK_ROWS"); er && er[0]) rows = std::atoi(er);
       block1_ = true;
+      // the reduction folded into the sweep costs every workgroup a drain of its stores and a ticket
+      // round trip while it holds its LDS: cheaper than a k_reduce_n launch when the tiles run in
+      // about one round (400x600 16.8 vs 18.3 us, 800x1200 23.3 vs 24.6), dearer over several
+      // (1200x1800 37.5 vs 37.2, 1600x2400 57.3 vs 54.9; study r4ap).  PMX_PCG1_BLOCK_FUSED=0/1 forces it.
+      const int64_t nblk = int64_t((G.nx + rows - 1) / rows) * ((G.ny + 123) / 124);
       const char* ef = std::getenv("PMX_PCG1_BLOCK_FUSED");
-      block_fused_ = !(ef && ef[0] == '0');
+      block_fused_ = ef && ef[0] ? ef[0] != '0' : nblk < 1500;
       opt_.rows1 = rows;
       opt_.rows1w = rows;
       opt_.vec1 = 2;

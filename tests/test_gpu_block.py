@@ -70,3 +70,17 @@ def test_block_tiles_first_sweeps_bitwise(pkg, monkeypatch):
         s.step(7)  # through a w sweep (k = 3, 6)
         s.synchronize()
     assert np.abs(b.local_w(0) - m.local_w(0)).max() <= 1e-12 * np.abs(m.local_w(0)).max()
+
+
+@pytest.mark.parametrize("grid,iters", [((800, 1200), 989), ((1600, 2400), 1858)])
+def test_block_tiles_fused_and_separate_reduction(pkg, monkeypatch, grid, iters):
+    """The reduction finished by the sweep's last workgroup (auto below 1,500 tiles) and by a
+    separate k_reduce_n (auto above): the same goldens, solutions equal to rounding."""
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("PMX_PCG1_BLOCK_FUSED", fused)
+        s = _sess(pkg, monkeypatch, *grid, 12)
+        r = s.solve(1)
+        assert r["status"] == "converged" and r["iters"] == iters
+        out[fused] = s.gather_local_w()
+    assert np.abs(out["1"] - out["0"]).max() <= 1e-10 * np.abs(out["0"]).max()
