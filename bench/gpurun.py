@@ -865,6 +865,29 @@ STUDIES["r4aq"] = [
     ("phases_1600", 120, bench("--gpus 1 --M 1600 --N 2400 --steps 200 --warmup 20 --profile-phases 200")),
 ]
 
+# block-tile shapes again, with the separate reduction above 1,500 tiles
+_BR = lambda r, w=8: f"env PMX_PCG1_BLOCK=1 PMX_PCG1_BLOCK_ROWS={r} PMX_PCG1_BLOCK_WAVES={w} "  # noqa: E731
+STUDIES["r4ar"] = [
+    ("g1600_r12", 60, _BR(12) + bench(_B16)),
+    ("g1600_r16", 60, _BR(16) + bench(_B16)),
+    ("g1600_r16w16", 60, _BR(16, 16) + bench(_B16)),
+    ("g1600_r8", 60, _BR(8) + bench(_B16)),
+    ("g1200_r16", 60, _BR(16) + bench(_G12)),
+    ("g1200_r12", 60, _BR(12) + bench(_G12)),
+    ("g2000_r16", 60, _BR(16) + bench("--gpus 1 --M 2000 --N 3000 --steps 500 --warmup 50 --no-tol-solve")),
+    ("g2000_r12", 60, _BR(12) + bench("--gpus 1 --M 2000 --N 3000 --steps 500 --warmup 50 --no-tol-solve")),
+    ("g2000_m", 60, bench("--gpus 1 --M 2000 --N 3000 --steps 500 --warmup 50 --no-tol-solve")),
+    ("g800_r16", 60, _BR(16) + bench(_B8)),
+]
+
+# final validation after the frame-on-comm schedule and the block-tile changes
+STUDIES["r4as"] = [
+    ("pytest_gpu_all", 800, f"{PYTEST_ALL} tests -m gpu"),
+    ("smoke", 120, "python -c 'import __graft_entry__ as g; g.smoke()'"),
+    ("bench_driver", 300, bench("--gpus 1 --steps 20 --warmup 5")),
+    ("loopback8", 120, bench(_LB + " --placement 0")),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [
