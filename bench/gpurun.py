@@ -888,6 +888,20 @@ STUDIES["r4as"] = [
     ("loopback8", 120, bench(_LB + " --placement 0")),
 ]
 
+# one-workgroup reduction for <= 4096 partials (PMX_REDUCE_ONE) vs the ticketed multi-block k_reduce_n
+_RO = lambda v: f"env PMX_REDUCE_ONE={v} "  # noqa: E731
+STUDIES["r4at"] = [
+    ("g1600_1", 60, _RO(1) + bench(_B16)),
+    ("g1600_0", 60, _RO(0) + bench(_B16)),
+    ("g1200_1", 60, _RO(1) + bench(_G12)),
+    ("g1200_0", 60, _RO(0) + bench(_G12)),
+    ("g800m_1", 60, _RO(1) + bench(_B8 + " --block-tiles off")),
+    ("g800m_0", 60, _RO(0) + bench(_B8 + " --block-tiles off")),
+    ("g1600_1b", 60, _RO(1) + bench(_B16)),
+    ("g1600_0b", 60, _RO(0) + bench(_B16)),
+    ("tests", 400, f"{PYTEST} tests/test_gpu_block.py tests/test_gpu_pcg1.py tests/test_gpu_solver.py -m gpu"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

@@ -427,6 +427,50 @@ k_reduce_n(const double* __restrict__ part, int n, ReduceWeights wt, double* out
   }
 }
 
+// Small n (<= kReduceOneMax partials): ONE workgroup of 1024 threads reads every partial (at most 4
+// per thread, all in flight) and finishes on its own -- no chunk hand-off, no ticket, one memory
+// round trip instead of three.  Same finish as k_reduce_n; the fixed summation order is
+// thread-strided, then waves in order.
+constexpr int kReduceOneMax = 4096;
+
+template <int NQ>
+__global__ void __launch_bounds__(1024)
+k_reduce_1(const double* __restrict__ part, int n, ReduceWeights wt, double* out, PcgState* S, int mode,
+           long long* progress) {
+  __shared__ double lds[NQ][1024 / kWave];
+  if ((mode & kSkipIfDone) && S->done) return;
+  double s[NQ];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) s[q] = 0.0;
+#pragma unroll 4
+  for (int i = int(threadIdx.x); i < n; i += 1024) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) s[q] += part[int64_t(i) * NQ + q];
+  }
+  const int wid = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    s[q] = wave_sum_mfma(s[q]);
+    if (lane == 0) lds[q][wid] = s[q];
+  }
+  __syncthreads();
+  if (threadIdx.x >= kWave) return;  // wave 0 finishes (full EXEC)
+  double t[NQ];
+  bool bad = false;
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    t[q] = wave_sum_mfma(lane < 1024 / kWave ? lds[q][lane] : 0.0);
+    bad |= !(t[q] == t[q]) || isinf(t[q]);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) out[q] = t[q] * wt.w[q];
+    if (bad) S->nan_flag = 1;
+    if (mode & kBumpIter) S->it += 1;
+    if (progress) __hip_atomic_store(progress, S->it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // Per tile: the coefficient class of each row its march visits (rows i0-3 .. i1+2 over the tile's
 // loaded columns, 2 bits per row, see Pcg1Slot) and whether any of them is "cut" (class 0: those
 // rows rebuild every face from the tables, and such a tile takes 3-5x the median tile time,
@@ -635,8 +679,15 @@ void launch_reduce_n(const double* partials, int n, int nq, const double* weight
   unsigned* ticket = reinterpret_cast<unsigned*>(chunk + 8 * kReduceMaxBlocks);
   ReduceWeights wt{};
   for (int q = 0; q < nq; ++q) wt.w[q] = weights[q];
-  hipLaunchKernelGGL(k_reduce_n<kNq>, dim3(nb), dim3(256), 0, s, partials, n, wt, out, S, mode, chunk, ticket,
-                     progress);
+  static const bool one = [] {
+    const char* e = std::getenv("PMX_REDUCE_ONE");
+    return !(e && e[0] == '0');
+  }();
+  if (one && n <= kReduceOneMax)
+    hipLaunchKernelGGL(k_reduce_1<kNq>, dim3(1), dim3(1024), 0, s, partials, n, wt, out, S, mode, progress);
+  else
+    hipLaunchKernelGGL(k_reduce_n<kNq>, dim3(nb), dim3(256), 0, s, partials, n, wt, out, S, mode, chunk, ticket,
+                       progress);
   HIP_CHECK(hipGetLastError());
 }
 
