@@ -427,11 +427,11 @@ k_reduce_n(const double* __restrict__ part, int n, ReduceWeights wt, double* out
   }
 }
 
-// Small n (<= kReduceOneMax partials): ONE workgroup of 1024 threads reads every partial (at most 4
+// Small n (<= kReduceOneMax partials): ONE workgroup of 1024 threads reads every partial (at most 3
 // per thread, all in flight) and finishes on its own -- no chunk hand-off, no ticket, one memory
 // round trip instead of three.  Same finish as k_reduce_n; the fixed summation order is
 // thread-strided, then waves in order.
-constexpr int kReduceOneMax = 4096;
+constexpr int kReduceOneMax = 3072;  // 1200x1800 blocks (2250): 36.3 vs 37.1 us; march 800x1200 (4000): 42.1 vs 41.8
 
 template <int NQ>
 __global__ void __launch_bounds__(1024)
