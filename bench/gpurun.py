@@ -902,6 +902,18 @@ STUDIES["r4at"] = [
     ("tests", 400, f"{PYTEST} tests/test_gpu_block.py tests/test_gpu_pcg1.py tests/test_gpu_solver.py -m gpu"),
 ]
 
+# block tiles: stage B on the rows of the wave's own stage A (r^{k-1}, p^{k-1} from registers, no sRo;
+# sPo only on w sweeps)
+STUDIES["r4au"] = [
+    ("g1600", 60, bench(_B16)),
+    ("g800", 60, bench(_B8)),
+    ("g1200", 60, bench(_G12)),
+    ("g400", 60, bench(_G4b + " --persistent off")),
+    ("g1600_b", 60, bench(_B16)),
+    ("g800_b", 60, bench(_B8)),
+    ("tests", 300, f"{PYTEST} tests/test_gpu_block.py -m gpu"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [
