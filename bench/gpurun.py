@@ -914,6 +914,15 @@ STUDIES["r4au"] = [
     ("tests", 300, f"{PYTEST} tests/test_gpu_block.py -m gpu"),
 ]
 
+# final validation of the round's last state (k_reduce_1 added after r4as)
+STUDIES["r4av"] = [
+    ("pytest_gpu_all", 800, f"{PYTEST_ALL} tests -m gpu"),
+    ("smoke", 120, "python -c 'import __graft_entry__ as g; g.smoke()'"),
+    ("bench_driver", 300, bench("--gpus 1 --steps 20 --warmup 5")),
+    ("loopback8", 120, bench(_LB + " --placement 0")),
+    ("g1600", 60, bench(_B16)),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [
