@@ -139,9 +139,11 @@ def parse(argv=None):
                     help="supervisor: hard limit (s) for one rung's processes (0 = RUNG_CAP per rung)")
     ap.add_argument("--ladder-budget", type=float, default=LADDER_BUDGET,
                     help="supervisor: wall-clock budget (s) of the whole ladder")
-    ap.add_argument("--placement", type=int, default=12,
+    ap.add_argument("--placement", type=int, default=20,
                     help="placement probe: candidate field blocks timed, the fastest kept (0 = off; "
-                         "bounded by --placement-budget and --placement-keep-free; off when ranks share a GPU)")
+                         "bounded by --placement-budget and --placement-keep-free; off when ranks share a GPU). "
+                         "20 with 1/4 of HBM kept free: on boxes whose fast blocks lie past the first half of "
+                         "HBM, 1.804 vs 1.942 ms/step at 16384^2 (profiles/r4/placement/r4aw_*)")
     ap.add_argument("--block-tiles", default="auto", choices=["auto", "on", "off"],
                     help="block-tile sweeps (pcg1_block.hip): auto = undecomposed fp64 grids with < 10,000 "
                          "four-row march tiles")
@@ -153,7 +155,7 @@ def parse(argv=None):
                          "alone, ghosts filled by device copies of the real sizes (from zeros), all-reduce "
                          "skipped -- the real per-rank schedule (split sweep, frame stream, copies) at full speed")
     ap.add_argument("--placement-budget", type=float, default=0.5, help="placement probe: seconds of probing")
-    ap.add_argument("--placement-keep-free", type=float, default=0.5,
+    ap.add_argument("--placement-keep-free", type=float, default=0.25,
                     help="placement probe: fraction of the free device memory left free")
     return ap.parse_args(argv)
 

@@ -923,6 +923,16 @@ STUDIES["r4av"] = [
     ("g1600", 60, bench(_B16)),
 ]
 
+# deeper placement probes on a box whose first half of HBM has no fast block
+_DRV = "--gpus 1 --steps 20 --warmup 5"
+STUDIES["r4aw"] = [
+    ("drv_default", 300, bench(_DRV)),
+    ("drv_p20_q25", 300, bench(_DRV + " --placement 20 --placement-keep-free 0.25")),
+    ("drv_p24_q15", 300, bench(_DRV + " --placement 24 --placement-keep-free 0.15")),
+    ("drv_default_b", 300, bench(_DRV)),
+    ("drv_p20_q25_b", 300, bench(_DRV + " --placement 20 --placement-keep-free 0.25")),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [
