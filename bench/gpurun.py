@@ -933,6 +933,13 @@ STUDIES["r4aw"] = [
     ("drv_p20_q25_b", 300, bench(_DRV + " --placement 20 --placement-keep-free 0.25")),
 ]
 
+# the driver's commands with the new placement defaults
+STUDIES["r4ax"] = [
+    ("bench_driver", 300, bench("--gpus 1 --steps 20 --warmup 5")),
+    ("bench_noflags", 400, "python bench.py"),
+    ("smoke", 120, "python -c 'import __graft_entry__ as g; g.smoke()'"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [
