@@ -940,6 +940,16 @@ STUDIES["r4ax"] = [
     ("smoke", 120, "python -c 'import __graft_entry__ as g; g.smoke()'"),
 ]
 
+# kernel statistics of the final default on the reference grids
+STUDIES["r4ay"] = [
+    ("stats_1600", 120, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4ay/stats_1600 -o run -- "
+                        "python3 bench.py --gpus 1 --M 1600 --N 2400 --steps 500 --warmup 50 --no-tol-solve"),
+    ("stats_800", 120, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4ay/stats_800 -o run -- "
+                       "python3 bench.py --gpus 1 --M 800 --N 1200 --steps 500 --warmup 50 --no-tol-solve"),
+    ("stats_1200", 120, "rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4ay/stats_1200 -o run -- "
+                        "python3 bench.py --gpus 1 --M 1200 --N 1800 --steps 500 --warmup 50 --no-tol-solve"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [
