@@ -950,6 +950,11 @@ STUDIES["r4ay"] = [
                         "python3 bench.py --gpus 1 --M 1200 --N 1800 --steps 500 --warmup 50 --no-tol-solve"),
 ]
 
+# bench-driving GPU tests after the placement default change
+STUDIES["r4az"] = [
+    ("bench_tests", 500, f"{PYTEST} tests/test_gpu_launch_path.py tests/test_gpu_dist.py tests/test_gpu_cli.py -m gpu"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [
