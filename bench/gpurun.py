@@ -955,6 +955,18 @@ STUDIES["r4az"] = [
     ("bench_tests", 500, f"{PYTEST} tests/test_gpu_launch_path.py tests/test_gpu_dist.py tests/test_gpu_cli.py -m gpu"),
 ]
 
+# k_reduce_1 with 256 vs 1024 threads
+_RT = lambda t: f"env PMX_REDUCE_ONE_THREADS={t} "  # noqa: E731
+STUDIES["r4ba"] = [
+    ("g1600_1024", 60, _RT(1024) + bench(_B16)),
+    ("g1600_256", 60, _RT(256) + bench(_B16)),
+    ("g1200_1024", 60, _RT(1024) + bench(_G12)),
+    ("g1200_256", 60, _RT(256) + bench(_G12)),
+    ("g1600_1024b", 60, _RT(1024) + bench(_B16)),
+    ("g1600_256b", 60, _RT(256) + bench(_B16)),
+    ("tests_256", 300, _RT(256) + f"{PYTEST} tests/test_gpu_block.py -m gpu"),
+]
+
 # round 4: the reference's Table 2 buckets at its own grids (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:956-980),
 # BASELINE config 5's per-rank shape in fp32 / mixed (4096x32768 = the 8-rank strip of 32768^2)
 STUDIES["r4b"] = [

@@ -433,17 +433,17 @@ k_reduce_n(const double* __restrict__ part, int n, ReduceWeights wt, double* out
 // thread-strided, then waves in order.
 constexpr int kReduceOneMax = 3072;  // 1200x1800 blocks (2250): 36.3 vs 37.1 us; march 800x1200 (4000): 42.1 vs 41.8
 
-template <int NQ>
-__global__ void __launch_bounds__(1024)
+template <int NQ, int NT>
+__global__ void __launch_bounds__(NT)
 k_reduce_1(const double* __restrict__ part, int n, ReduceWeights wt, double* out, PcgState* S, int mode,
            long long* progress) {
-  __shared__ double lds[NQ][1024 / kWave];
+  __shared__ double lds[NQ][NT / kWave];
   if ((mode & kSkipIfDone) && S->done) return;
   double s[NQ];
 #pragma unroll
   for (int q = 0; q < NQ; ++q) s[q] = 0.0;
 #pragma unroll 4
-  for (int i = int(threadIdx.x); i < n; i += 1024) {
+  for (int i = int(threadIdx.x); i < n; i += NT) {
 #pragma unroll
     for (int q = 0; q < NQ; ++q) s[q] += part[int64_t(i) * NQ + q];
   }
@@ -459,7 +459,7 @@ k_reduce_1(const double* __restrict__ part, int n, ReduceWeights wt, double* out
   bool bad = false;
 #pragma unroll
   for (int q = 0; q < NQ; ++q) {
-    t[q] = wave_sum_mfma(lane < 1024 / kWave ? lds[q][lane] : 0.0);
+    t[q] = wave_sum_mfma(lane < NT / kWave ? lds[q][lane] : 0.0);
     bad |= !(t[q] == t[q]) || isinf(t[q]);
   }
   if (lane == 0) {
@@ -683,8 +683,14 @@ void launch_reduce_n(const double* partials, int n, int nq, const double* weight
     const char* e = std::getenv("PMX_REDUCE_ONE");
     return !(e && e[0] == '0');
   }();
-  if (one && n <= kReduceOneMax)
-    hipLaunchKernelGGL(k_reduce_1<kNq>, dim3(1), dim3(1024), 0, s, partials, n, wt, out, S, mode, progress);
+  static const int one_threads = [] {
+    const char* e = std::getenv("PMX_REDUCE_ONE_THREADS");
+    return e && e[0] ? std::atoi(e) : 1024;
+  }();
+  if (one && n <= kReduceOneMax && one_threads == 256)
+    hipLaunchKernelGGL((k_reduce_1<kNq, 256>), dim3(1), dim3(256), 0, s, partials, n, wt, out, S, mode, progress);
+  else if (one && n <= kReduceOneMax)
+    hipLaunchKernelGGL((k_reduce_1<kNq, 1024>), dim3(1), dim3(1024), 0, s, partials, n, wt, out, S, mode, progress);
   else
     hipLaunchKernelGGL(k_reduce_n<kNq>, dim3(nb), dim3(256), 0, s, partials, n, wt, out, S, mode, chunk, ticket,
                        progress);
