@@ -147,9 +147,6 @@ def parse(argv=None):
     ap.add_argument("--block-tiles", default="auto", choices=["auto", "on", "off"],
                     help="block-tile sweeps (pcg1_block.hip): auto = undecomposed fp64 grids with < 10,000 "
                          "four-row march tiles")
-    ap.add_argument("--persistent", default="auto", choices=["auto", "on", "off"],
-                    help="persistent iteration (one launch per batch, in-kernel grid barrier + reduction): on = "
-                         "fp64 single-subdomain grids; auto = off (the block-tile graph replays are faster)")
     ap.add_argument("--loopback-rank", type=int, default=-1,
                     help="timing rehearsal on ONE GPU (valid=false): rank R of the --gpus-rank decomposition "
                          "alone, ghosts filled by device copies of the real sizes (from zeros), all-reduce "
@@ -570,7 +567,6 @@ def measure(args) -> int:
               waves=args.waves, tile_rows=args.tile_rows, exact=args.exact, graph_batch=args.graph_batch,
               overlap=overlap, vec_b=args.vec_b, tile_rows_b=args.tile_rows_b,
               b_ring=args.b_kernel == "ring")
-    persistent = {"auto": -1, "on": 1, "off": 0}[args.persistent]
     pkw = dict(placement=0 if share else args.placement, placement_budget_s=args.placement_budget,
                placement_keep_free=args.placement_keep_free)
     dkw = dict(kw, **pkw, phase=watch.phase, init_timeout=COMM_INIT_TIMEOUT)
@@ -583,7 +579,7 @@ def measure(args) -> int:
         comm_used = "gloo" if world > 1 else "self"
     elif world == 1:
         models = importlib.import_module(pkg_name + ".models")
-        runner = ds.SessionRunner(models.make_session(problem, ranks=1, device=info.local_rank, persistent=persistent,
+        runner = ds.SessionRunner(models.make_session(problem, ranks=1, device=info.local_rank,
                                                       block_tiles={"auto": -1, "on": 1, "off": 0}[args.block_tiles],
                                                       **pkw, **kw), problem, info)
         comm_used = "self"
@@ -649,14 +645,16 @@ def measure(args) -> int:
         t = torch.tensor([dt], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    pers = path.get("persistent_iters", 0)
-    timed_path = ("persistent" if pers > 0 and path["eager_iters"] == 0 and path["graph_iters"] == 0 else
-                  "graph" if path["eager_iters"] == 0 and path["graph_iters"] > 0 and pers == 0 else
-                  "eager" if path["graph_iters"] == 0 and pers == 0 else "mixed")
+    timed_path = ("graph" if path["eager_iters"] == 0 and path["graph_iters"] > 0 else
+                  "eager" if path["graph_iters"] == 0 else "mixed")
     tile_desc = dict(runner.tile())
     probe = tile_desc.pop("placement_probe_ms", None)
     if probe and isinstance(tile_desc.get("placement"), dict) and len(probe) <= 32:
         tile_desc["placement"] = dict(tile_desc["placement"], probe_ms=[round(float(x), 3) for x in probe])
+    if isinstance(tile_desc.get("placement"), dict):
+        cls = placement_class(tile_desc["placement"].get("kept_ms"), (args.M - 1) * (args.N - 1), args.dtype)
+        if cls:
+            tile_desc["placement"]["class"] = cls
     valid = (not st1["done"]) and (st1["it"] - st0["it"] == args.steps) and not st1["nan"]
     pts = (args.M - 1) * (args.N - 1)
     mlups = pts * args.steps / dt / 1e6
@@ -750,7 +748,6 @@ def measure(args) -> int:
             "timed_graph_lengths": path.get("graph_lengths", []),
             "timed_graph_iters": path["graph_iters"],
             "timed_eager_iters": path["eager_iters"],
-            "timed_persistent_iters": pers,
             "graphs_prepared": bool(prepared),
             "valid": valid and not share,
             "baseline_mlups": BASELINE_MLUPS,
@@ -828,6 +825,25 @@ def measure_loopback(args) -> int:
     }
     print(json.dumps(out), flush=True)
     return 0
+
+
+# Placement classes of a kept field block (GpuSubdomainSolver::place_fields times 6 real iterations
+# per candidate).  At 16384^2 fp64 the blocks fall into ~three rates (profiles/r3/placement/,
+# profiles/r4/placement/): ~10.7 ms per 6 iterations (1.78-1.80 ms/step), ~11.0-11.3, and
+# ~11.55-11.65 (1.92-1.95 ms/step), i.e. ~6.65 / ~6.9 / ~7.2 ps per point and iteration.  The
+# class says which one the timed run got, so a driver record can be read against the others.
+PLACEMENT_CLASS_PS = ((6.80, "fast"), (7.05, "mid"))
+
+
+def placement_class(kept_ms, points, dtype):
+    """'fast' / 'mid' / 'slow' for fp64 grids of >= 8192^2 points (bandwidth-bound), else None."""
+    if not kept_ms or dtype != "fp64" or points < 8192 * 8192:
+        return None
+    ps = float(kept_ms) / 6.0 / points * 1e9
+    for lim, name in PLACEMENT_CLASS_PS:
+        if ps < lim:
+            return name
+    return "slow"
 
 
 def main():

@@ -13,7 +13,7 @@ p = pkg.PoissonEllipse(M=200, N=300)
 for overlap in (True, False):
     s = n.Session(p.to_native(), world=1, comm="rccl", uid=n.rccl_unique_id(), ranks=[0], devices=[0],
                   threaded=1, overlap=overlap)
-    print("overlap", overlap, "persistent", s.persistent, "tile", s.tile.get("persistent"), flush=True)
+    print("overlap", overlap, "tile", s.tile, flush=True)
     d = tempfile.mkdtemp()
     good = os.path.join(d, "ck.bin")
     try:

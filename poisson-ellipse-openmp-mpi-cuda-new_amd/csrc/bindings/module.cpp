@@ -66,6 +66,9 @@ py::dict state_dict(const PcgState& st) {
   d["w_pend_n"] = st.w_pend_n;
   d["w_cycle"] = st.w_cycle;
   d["red_c"] = py::make_tuple(st.red_c[0], st.red_c[1], st.red_c[2], st.red_c[3], st.red_c[4]);
+  d["alpha1"] = py::make_tuple(st.alpha1[0], st.alpha1[1], st.alpha1[2], st.alpha1[3]);
+  d["beta1"] = py::make_tuple(st.beta1[0], st.beta1[1], st.beta1[2], st.beta1[3]);
+  d["halo_k"] = st.halo_k;
   return d;
 }
 
@@ -182,10 +185,8 @@ GpuOptions make_options(int device, const std::string& kernel, int block, int ve
                         int tile_rows, const std::string& dtype, bool exact, int graph_batch, bool check,
                         bool overlap = true, int vec_b = 0, int waves_b = 0, int tile_rows_b = -1,
                         bool poison_halos = false, bool b_ring = false, int algo = -1, int placement = 0,
-                        double placement_budget_s = 0.5, double placement_keep_free = 0.5, int persistent = -1,
-                        int block1 = -1) {
+                        double placement_budget_s = 0.5, double placement_keep_free = 0.5, int block1 = -1) {
   GpuOptions o;
-  o.persistent = persistent;
   o.block1 = block1;
   o.placement = placement;
   o.placement_budget_s = placement_budget_s;
@@ -323,8 +324,6 @@ PYBIND11_MODULE(_pmx, m) {
     HIP_CHECK(hipFree(ws));
     HIP_CHECK(hipFree(st));
   }, py::arg("parts"), py::arg("n"), py::arg("nq"), py::arg("nsets"), py::arg("out"), py::arg("stream") = 0);
-  m.def("persistent_trace", []() { return pcg1_persist_trace(); },
-        "PMX_PERSIST_TRACE=k: wall-clock stamps of sweep k of the last persistent launch (see kernels.hpp)");
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
   // Arena layout for a Python-orchestrated solver (DistGpuPCG comm="torch").  The iteration
   // algorithm is resolved exactly as the solver will (options + environment + device size), so
@@ -451,13 +450,13 @@ PYBIND11_MODULE(_pmx, m) {
                        bool rccl_graph, bool overlap, int vec_b, int waves_b, int tile_rows_b,
                        bool poison_halos, bool b_ring, int algo, bool defer_connect, int threaded,
                        int placement, double placement_budget_s, double placement_keep_free, int sharing,
-                       int persistent, int block_tiles) {
+                       int block_tiles) {
              SessionConfig c;
              c.sharing = sharing;
              c.spec = s;
              c.opt = make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact,
                                   graph_batch, check, overlap, vec_b, waves_b, tile_rows_b, poison_halos,
-                                  b_ring, algo, placement, placement_budget_s, placement_keep_free, persistent,
+                                  b_ring, algo, placement, placement_budget_s, placement_keep_free,
                                   block_tiles);
              c.defer_connect = defer_connect;
              c.threaded = threaded;
@@ -486,8 +485,7 @@ PYBIND11_MODULE(_pmx, m) {
            py::arg("waves_b") = 0, py::arg("tile_rows_b") = -1, py::arg("poison_halos") = false,
            py::arg("b_ring") = false, py::arg("algo") = -1, py::arg("defer_connect") = false,
            py::arg("threaded") = -1, py::arg("placement") = 0, py::arg("placement_budget_s") = 0.5,
-           py::arg("placement_keep_free") = 0.5, py::arg("sharing") = 0, py::arg("persistent") = -1,
-           py::arg("block_tiles") = -1)
+           py::arg("placement_keep_free") = 0.5, py::arg("sharing") = 0, py::arg("block_tiles") = -1)
       .def("ipc_export", [](Session& s) { return py::bytes(s.ipc_export()); },
            "IPC session: this rank's memory handles (pass every rank's to connect_ipc)")
       .def("connect_ipc", [](Session& s, std::vector<py::bytes> ex) {
@@ -547,14 +545,12 @@ PYBIND11_MODULE(_pmx, m) {
              py::dict d;
              d["graph_iters"] = p.graph_iters;
              d["eager_iters"] = p.eager_iters;
-             d["persistent_iters"] = p.persistent_iters;
              d["graph_lengths"] = p.graph_lengths;
              return d;
            })
       .def("reset_path_stats", &Session::reset_path_stats)
       .def_property_readonly("split_sweep", &Session::split_sweep)
       .def_property_readonly("direct_rows", &Session::direct_rows)
-      .def_property_readonly("persistent", &Session::persistent)
       .def("progress", [](Session& s, int i) {
              long long v[3];
              s.progress(i, v);  // host memory only: callable while another thread blocks in the session
@@ -596,12 +592,6 @@ PYBIND11_MODULE(_pmx, m) {
         if (s.solver(0).block_tiles()) d["block_tiles"] = true;
         if (!s.solver(0).single_pass()) d["b"] = one(s.solver(0).tiles_b());
         d["algo"] = s.solver(0).single_pass() ? "pcg1" : "pcg2";
-        if (s.solver(0).persistent()) {
-          py::dict pd = one(s.solver(0).tiles_persistent());
-          pd["workgroups"] = s.solver(0).persistent_workgroups();
-          pd["threads"] = kPersistThreads;
-          d["persistent"] = pd;
-        }
         if (!s.solver(0).placement_ms().empty()) {
           // 3 plain sweeps per candidate field block (rotating field roles), the fastest kept
           std::vector<float> v = s.solver(0).placement_ms();

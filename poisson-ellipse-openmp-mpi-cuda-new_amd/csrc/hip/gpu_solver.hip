@@ -101,7 +101,9 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_PROGRESS", o.progress);
   env_int("PMX_ARITH32", o.arith32);
   env_int("PMX_PLACEMENT", o.placement);
-  env_int("PMX_PERSISTENT", o.persistent);
+  env_int("PMX_PCG1_WPCU", o.wpcu1);
+  env_int("PMX_PCG1_WPCU_W", o.wpcu1w);
+  PMX_CHECK(o.wpcu1 >= 0 && o.wpcu1 <= 32 && o.wpcu1w >= 0 && o.wpcu1w <= 32, "pcg1 waves per CU must be 0..32");
   PMX_CHECK(o.wcycle1 == 2 || o.wcycle1 == 3, "pcg1 w cycle must be 2 or 3");
   PMX_CHECK(o.pair_w >= 0 && o.pair_w <= 2, "pair_w must be 0, 1 or 2");
   PMX_CHECK(o.algo == -1 || o.algo == 1 || o.algo == 2, "algo must be -1, 1 or 2");
@@ -278,6 +280,8 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     tiles1w_ = make_pcg1_tiles(G, opt_.vec1, opt_.waves1, opt_.rows1w ? opt_.rows1w : tiles1_.rows,
                                opt_.pf1w ? opt_.pf1w : tiles1_.pf, int(elem_));
     tiles1w_.arith32 = tiles1_.arith32;
+    tiles1_.lds_pad = pcg1_lds_pad(opt_.wpcu1, tiles1_.waves);
+    tiles1w_.lds_pad = pcg1_lds_pad(opt_.wpcu1w, tiles1w_.waves);
     const bool same_w = tiles1w_.rows == tiles1_.rows;
     // dispatch order tables with the tiles' row classes; order1: the ellipse-cut tiles first
     // within each XCD's share (their 3-5x longer tiles would trail the sweep)
@@ -291,35 +295,6 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
       HIP_CHECK(hipMalloc(&tile_order_w_, 3 * size_t(tiles1w_.ntiles()) * sizeof(Pcg1Slot)));
       (void)pcg1_build_order(G, tables_, tiles1w_, tile_order_w_, opt_.order1 != 0, nullptr);
     }
-  }
-
-  if (pcg1_) {
-    // persistent iteration (one launch per batch, in-kernel grid barrier): on request only.  Its
-    // waves march rows serially; the graph replays of the block-tile sweep (pcg1_block.hip) run the
-    // same latency-bound grids faster -- 400x600 17.0 vs 35.1 us/iteration, 800x1200 26.2 vs 43.8
-    // (profiles/r4/block/, profiles/r4/persist/) -- so auto (-1) no longer picks it
-    const bool eligible = G.nb == 0 && elem_ == 8 && !opt.check;
-    PMX_CHECK(opt_.persistent != 1 || eligible, "the persistent iteration needs fp64 and an undecomposed grid");
-    persist_ = eligible && opt_.persistent == 1;
-  }
-  if (persist_) {
-    pwg_ = pcg1_persist_max_wg(opt.device);
-    // ~2 tiles per resident wave (the static schedule balances cut tiles against plain ones), but
-    // no shorter than 2 rows (a tile marches 4 extra rows; 800x1200: 2 rows 43.2, 4 rows 46.5 us);
-    // PMX_PERSIST_ROWS overrides
-    const int waves = pwg_ * (kPersistThreads / 64), tj = (sd.ny + 123) / 124;
-    const int want_rows = std::max(1, (2 * waves + tj - 1) / tj);
-    int ti = std::max(2, (sd.nx + want_rows - 1) / want_rows);
-    if (const char* e = std::getenv("PMX_PERSIST_ROWS"); e && e[0]) ti = std::max(1, std::atoi(e));
-    tilesP_ = make_pcg1_tiles(G, 2, 1, ti, 1, int(elem_));  // the persistent march prefetches 1 row
-    HIP_CHECK(hipMalloc(&tile_order_p_, 4 * size_t(tilesP_.ntiles()) * sizeof(Pcg1Slot)));
-    (void)pcg1_build_order(G, tables_, tilesP_, tile_order_p_, true, nullptr);
-    HIP_CHECK(hipMalloc(&sched_offs_p_, (size_t(waves) + 1) * sizeof(int)));
-    sched_p_ = tile_order_p_ + 3 * size_t(tilesP_.ntiles());
-    double cut_cost = 2.0;  // a cut row step vs a class-uniform one, with the coefficient carry (NOTES)
-    if (const char* e = std::getenv("PMX_PERSIST_CUT_COST"); e && e[0]) cut_cost = std::atof(e);
-    pcg1_persist_schedule(tilesP_, waves, cut_cost, sched_p_, sched_offs_p_);
-    HIP_CHECK(hipMalloc(&pws_, sizeof(PersistWs)));
   }
 
   init_tiles_ = make_tiles(G, 256, 0);
@@ -495,13 +470,6 @@ void GpuSubdomainSolver::release() noexcept {
   if (fields_) (void)hipFree(fields_);
   if (tile_order_) (void)hipFree(tile_order_);
   if (tile_order_w_) (void)hipFree(tile_order_w_);
-  if (tile_order_p_) (void)hipFree(tile_order_p_);
-  if (sched_offs_p_) (void)hipFree(sched_offs_p_);
-  sched_offs_p_ = nullptr;
-  sched_p_ = nullptr;
-  if (pws_) (void)hipFree(pws_);
-  tile_order_p_ = nullptr;
-  pws_ = nullptr;
   if (tables_buf_) (void)hipFree(tables_buf_);
   if (partials_) (void)hipFree(partials_);
   if (own_arena_ && arena_) (void)hipFree(arena_);
@@ -614,20 +582,6 @@ void GpuSubdomainSolver::halo_impl(hipStream_t s, bool unpack) {
   launch_pcg1_halo<T>(geom_, static_cast<T*>(field_base(1)), reinterpret_cast<T*>(r2_ + field_off_ * elem_),
                       static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(), halo_target_,
                       unpack, s, progress_dev_);
-  after_launch(s);
-}
-
-void GpuSubdomainSolver::enqueue_persistent(hipStream_t s, long long n) {
-  PMX_CHECK(persist_, "persistent iteration not set up for this solver");
-  if (n <= 0) return;
-  HIP_CHECK(hipSetDevice(opt_.device));
-  const double h = g_.h1h2, wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
-  const double wts[5] = {h, h, h, h, wdiff};
-  launch_pcg1_persist<double>(geom_, tables_, static_cast<double*>(field_base(0)), static_cast<double*>(field_base(1)),
-                              reinterpret_cast<double*>(r2_ + field_off_ * elem_), static_cast<double*>(field_base(2)),
-                              static_cast<double*>(field_base(3)), state_, pws_, tilesP_, sched_p_, sched_offs_p_, pwg_,
-                              host_k_ + n - 1, wts, s);
-  host_k_ += n;  // as n reductions would (the device stops early on its own)
   after_launch(s);
 }
 
@@ -1030,9 +984,6 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
   if (const char* d = std::getenv("PMX_DIRECT_ROWS"); d && d[0] == '0') direct = false;
   direct_ = direct;
   for (auto* s : local_) s->set_direct_rows(direct_);
-  // graph_batch 0 asks for individual launches: the persistent path replaces the graph replays only
-  persistent_ = graph_batch_ > 0 && local_.size() == 1 && !any_nb && comm_->world_size() == 1 &&
-                local_[0]->persistent();
   // One hardware queue per process (GPU_MAX_HW_QUEUES=1): every stream lands on it, so forking the
   // halo / frame work onto side streams cannot overlap anything -- and ROCm 7.2 segfaults inside
   // hipGraphLaunch on a captured graph with forked branches in that configuration (traced with
@@ -1433,7 +1384,6 @@ void PcgDriver::note_graph(int len) {
 
 bool PcgDriver::prepare(int64_t n) {
   TraceRange tr("pmx:prepare");
-  if (persistent_) return true;  // nothing to capture: one launch per batch
   const int cyc = graph_period();
   std::vector<long long> k0;
   for (auto* s : local_) k0.push_back(s->host_k());
@@ -1463,15 +1413,6 @@ void PcgDriver::enqueue_eager(int64_t n) {
 
 void PcgDriver::enqueue_iterations(int64_t n) {
   TraceRange tr("pmx:enqueue_iterations");
-  if (persistent_) {
-    // the launch makes no communicator call (world 1), so an aborted one is caught here, as every
-    // other path's first collective would
-    comm_->check_health();
-    HIP_CHECK(hipSetDevice(local_[0]->device()));
-    local_[0]->enqueue_persistent(streams_[0], n);
-    path_.persistent_iters += n;
-    return;
-  }
   const int cyc = graph_period();
   for (auto* s : local_) PMX_CHECK(s->host_k() == local_[0]->host_k(), "local solvers out of step");
   int64_t done = 0;
@@ -1505,10 +1446,7 @@ RunStats PcgDriver::solve(int poll_batches, bool do_init, int64_t ckpt_every,
   if (do_init) init();
   const double t1 = now_s();
   st.init_seconds = t1 - t0;
-  // persistent: the device stops on its own inside a launch, so long launches cost nothing extra --
-  // but no longer than the checkpoint cadence asks for
-  int64_t base = graph_batch_ > 0 ? graph_batch_ : 16;
-  if (persistent_) base = ckpt_every > 0 && on_checkpoint ? std::clamp<int64_t>(ckpt_every, 1, 512) : 512;
+  const int64_t base = graph_batch_ > 0 ? graph_batch_ : 16;
   const int64_t batch = base * std::max(1, poll_batches);
   const int64_t max_iter = local_[0]->spec().effective_max_iter();
   PcgState s = state(0);

@@ -57,101 +57,19 @@ k_pcg1_block(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* 
   __shared__ RowConst s_row[TR + 5];   // row constants of rows i0-3 .. i1+2 (tiles with cut rows)
   __shared__ double s_sum[kBlkWaves][kNq];
 
-  // ---- prologue: k_pcg1's scalars of sweep k (every workgroup computes the same values)
-  typedef const __attribute__((address_space(4))) PcgState CState;
-  const CState* Sc = (const CState*)S;  // NOLINT: address-space cast
-  // the dispatch slot is read in the same batch as the state (as k_pcg1's prologue): the tile's
-  // loads then wait for one round trip, not for the state's and then the slot's
+  // ---- prologue: k_pcg1's (pcg1_march.hpp: one batch of scalar loads, then pcg1_scalars); the
+  // dispatch slot is read in the same batch as the state, so the tile's loads wait for one round trip
   asm volatile("" ::"s"(S), "s"(order), "s"(gridDim.x));  // kernel arguments: one batch
   const int pos = xcd_remap(int(blockIdx.x), int(gridDim.x));
   const int id = ld_uniform(&order[pos].id, 0);  // pos < gridDim.x = ntiles (launch_pcg1_block)
   const unsigned long long ocls = ld_uniform(&order[pos].cls, 0);
-  const int st_done = Sc->done;
-  const long long k = Sc->it;
-  double rc[kNq], al[4], be[4];
-#pragma unroll
-  for (int q = 0; q < kNq; ++q) rc[q] = Sc->red_c[q];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    al[q] = Sc->alpha1[q];
-    be[q] = Sc->beta1[q];
-  }
-  const double zr0 = Sc->zr[0], zr1 = Sc->zr[1];
-  const double s_delta = Sc->delta, s_bd_tol = Sc->bd_tol, s_pmb = Sc->pair_min_beta;
-  const long long s_max_iter = Sc->max_iter;
-  const int s_norm = Sc->norm, cyc = Sc->w_cycle;
-  auto ring4 = [](const double (&v)[4], long long i) {
-    const int j = int(i & 3);
-    return j == 0 ? v[0] : j == 1 ? v[1] : j == 2 ? v[2] : v[3];
-  };
-  asm volatile("" ::"s"(st_done), "s"(k), "s"(id), "s"(ocls), "s"(rc[0]), "s"(rc[1]), "s"(rc[2]), "s"(rc[3]), "s"(rc[4]),
-               "s"(al[0]), "s"(al[1]), "s"(al[2]), "s"(al[3]), "s"(be[0]), "s"(be[1]), "s"(be[2]), "s"(be[3]),
-               "s"(zr0), "s"(zr1), "s"(s_delta), "s"(s_bd_tol), "s"(s_pmb), "s"(s_max_iter), "s"(s_norm), "s"(cyc));
-  if (st_done) return;
-  const bool leader = blockIdx.x == 0 && threadIdx.x == 0;
-  double alpha = 0.0, beta = 0.0, c1 = 0.0, c2 = 0.0;
-  int wm = 0;
-  if (k > 0) {
-    const double rho = rc[0];
-    double diff = 0.0;
-    if (k >= 2) {
-      diff = fabs(ring4(al, k - 1)) * sqrt(rc[4]);
-      const bool bad = !(diff == diff) || !(rho == rho);
-      if (bad || diff < s_delta || k > s_max_iter) {
-        if (leader) {
-          S->diff = diff;
-          S->iters = k - 1;
-          S->status = bad ? int(Status::kBreakdown) : (diff < s_delta ? int(Status::kConverged) : int(Status::kMaxIter));
-          if (bad) S->nan_flag = 1;
-          S->done = 1;
-        }
-        return;
-      }
-      beta = rho / ((k & 1) ? zr1 : zr0);
-    }
-    const double denom = rc[1] + beta * (2.0 * rc[2] + beta * rc[3]);
-    const bool bd = s_norm == int(Norm::kWeighted) ? fabs(denom) < s_bd_tol : denom < s_bd_tol;
-    if (bd || !(denom == denom)) {
-      if (leader) {
-        if (k >= 2) S->diff = diff;
-        S->iters = k;
-        S->status = int(Status::kBreakdown);
-        if (!(denom == denom)) S->nan_flag = 1;
-        S->done = 1;
-      }
-      return;
-    }
-    alpha = rho / denom;
-    const int ph = int(k % cyc);
-    if ((ph == 0) != WS) {  // host and device iteration counters out of step
-      if (leader) {
-        S->iters = k;
-        S->status = int(Status::kBreakdown);
-        S->nan_flag = 1;
-        S->done = 1;
-      }
-      return;
-    }
-    if (ph == 0) {
-      c1 = ring4(al, k - 1);
-      wm = 1;
-      if (cyc == 3) {
-        const double bprev = ring4(be, k - 1);
-        const double a2 = ring4(al, k - 2);
-        if (fabs(bprev) >= s_pmb) { wm = 2; c2 = a2 / bprev; }
-        else { wm = 3; c2 = a2; }
-      }
-    }
-    if (leader) {
-      S->zr[(k - 1) & 1] = rho;
-      S->alpha1[k & 3] = alpha;
-      S->beta1[k & 3] = beta;
-      if (k >= 2) S->diff = diff;
-      S->w_pend = ph ? k : 0;
-      S->w_pend_n = ph;
-    }
-  }
-  if (leader) S->halo_k = k + 1;
+  const Pcg1Pro pro = pcg1_load_state(S);
+  pcg1_batch(pro, id, ocls);
+  Pcg1Sweep sw;
+  if (!pcg1_scalars<WS>(pro, S, blockIdx.x == 0 && threadIdx.x == 0, sw)) return;
+  const long long k = sw.k;
+  const double alpha = sw.alpha, beta = sw.beta, c1 = sw.c1, c2 = sw.c2;
+  const int wm = sw.wm;
 
   // ---- the tile: dispatch slot -> tile id and its rows' coefficient classes (pcg1_build_order:
   // the tiles the ellipse cuts first within each XCD's share, so they do not trail the sweep)

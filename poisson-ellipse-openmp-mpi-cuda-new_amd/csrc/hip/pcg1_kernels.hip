@@ -135,13 +135,9 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
 #ifdef PMX_WAVE_TRACE
   const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
-  // Prologue: ONE batch of independent scalar loads (state through the constant address space,
-  // the tile's dispatch slot), then scalar math.  Read field by field with waits in between, the
-  // state cost ~8 dependent memory round trips, ~7 us of a ~25-us wave (wave traces,
-  // profiles/r2/prologue/).  Every field read here is one this kernel does not write (the rings
-  // alpha1/beta1/zr are written at slot k, read at k-1 / k-2), so the constant view is exact.
-  typedef const __attribute__((address_space(4))) PcgState CState;
-  const CState* Sc = (const CState*)S;  // NOLINT: address-space cast
+  // Prologue: ONE batch of independent scalar loads (kernel arguments; then the state through the
+  // constant address space and the tile's dispatch slot), then the shared control logic
+  // (pcg1_march.hpp: pcg1_scalars -- stop test, breakdown guard, w-phase check, ring writes).
   asm volatile("" ::"s"(S), "s"(part.order), "s"(part.count), "s"(gridDim.x));  // kernel arguments: one batch
   const int pos = xcd_remap(blockIdx.x, gridDim.x) * WAVES + __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   // branch-free: without an order the load reads a valid dummy (the state's first 16 bytes)
@@ -149,106 +145,13 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
   const int oi = part.order ? min(pos, part.count - 1) : 0;
   const int ord = ld_uniform(&obase[oi].id, 0);
   const unsigned long long ocls = ld_uniform(&obase[oi].cls, 0);
-  const int st_done = Sc->done;
-  const long long k = Sc->it;  // 0 = the init sweep (alpha = beta = 0: sums of r^0, z^0 only)
-  double rc[kNq], al[4], be[4];
-#pragma unroll
-  for (int q = 0; q < kNq; ++q) rc[q] = Sc->red_c[q];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    al[q] = Sc->alpha1[q];
-    be[q] = Sc->beta1[q];
-  }
-  const double zr0 = Sc->zr[0], zr1 = Sc->zr[1];
-  const double s_delta = Sc->delta, s_bd_tol = Sc->bd_tol, s_pmb = Sc->pair_min_beta;
-  const long long s_max_iter = Sc->max_iter;
-  const int s_norm = Sc->norm, cyc = Sc->w_cycle;
-  auto ring4 = [](const double (&v)[4], long long i) {
-    const int j = int(i & 3);
-    return j == 0 ? v[0] : j == 1 ? v[1] : j == 2 ? v[2] : v[3];
-  };
-  // every value above is consumed here, so the compiler issues all those loads as one batch
-  // instead of sinking each below the branch that first needs it
-  asm volatile("" ::"s"(st_done), "s"(k), "s"(ord), "s"(ocls), "s"(rc[0]), "s"(rc[1]), "s"(rc[2]), "s"(rc[3]), "s"(rc[4]),
-               "s"(al[0]), "s"(al[1]), "s"(al[2]), "s"(al[3]), "s"(be[0]), "s"(be[1]), "s"(be[2]), "s"(be[3]),
-               "s"(zr0), "s"(zr1), "s"(s_delta), "s"(s_bd_tol), "s"(s_pmb), "s"(s_max_iter), "s"(s_norm), "s"(cyc));
-  if (st_done) return;
-  double alpha = 0.0, beta = 0.0, c1 = 0.0, c2 = 0.0;
-  int wm = 0;
-  if (k > 0) {
-    const double rho = rc[0];  // rho_{k-1} = (z^{k-1}, r^{k-1})
-    double diff = 0.0;
-    if (k >= 2) {
-      // stop test of iteration k-1: ||w^k - w^{k-1}|| = |alpha_{k-1}| ||p^{k-1}||
-      diff = fabs(ring4(al, k - 1)) * sqrt(rc[4]);
-      const bool bad = !(diff == diff) || !(rho == rho);
-      if (bad || diff < s_delta || k > s_max_iter) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-          S->diff = diff;
-          S->iters = k - 1;
-          S->status = bad ? int(Status::kBreakdown)
-                          : (diff < s_delta ? int(Status::kConverged) : int(Status::kMaxIter));
-          if (bad) S->nan_flag = 1;
-          S->done = 1;
-        }
-        return;
-      }
-      beta = rho / ((k & 1) ? zr1 : zr0);  // rho_{k-2} sits in slot k & 1
-    }
-    const double denom = rc[1] + beta * (2.0 * rc[2] + beta * rc[3]);
-    const bool bd = s_norm == int(Norm::kWeighted) ? fabs(denom) < s_bd_tol : denom < s_bd_tol;
-    if (bd || !(denom == denom)) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (k >= 2) S->diff = diff;
-        S->iters = k;
-        S->status = int(Status::kBreakdown);
-        if (!(denom == denom)) S->nan_flag = 1;
-        S->done = 1;
-      }
-      return;
-    }
-    alpha = rho / denom;
-    // w schedule.  Pairs (w_cycle 2): even sweeps add alpha_{k-1} p^{k-1} + alpha_k p^k, p^{k-1}
-    // being the p_old the sweep reads anyway.  Triples (w_cycle 3, default): sweeps k = 0 mod 3
-    // also add alpha_{k-2} p^{k-2}, recovered without reading it: sweep k-1 formed
-    // p^{k-1} = D^-1 r^{k-2} + beta_{k-1} p^{k-2} and r^{k-1} = r^{k-2} - alpha_{k-1} A p^{k-1}, so
-    // p^{k-2} = (p^{k-1} - D^-1 (r^{k-1} + alpha_{k-1} A p^{k-1})) / beta_{k-1} -- one more stencil,
-    // on the p_old this sweep already holds.  Its rounding error grows like eps / |beta_{k-1}|, so
-    // below pair_min_beta the sweep re-reads p^{k-2} from the buffer it is about to overwrite.
-    // w moves on one sweep in three: 37.3 instead of 40 B/pt per iteration.  The stop test uses
-    // |alpha| ||p||, so the schedule changes no iteration count, only w's rounding.
-    const int ph = int(k % cyc);
-    // the host launches the w-sweep kernel (WS) exactly on the sweeps k = 0 mod w_cycle; a
-    // mismatch (host and device iteration counters out of step) must not pass silently
-    if ((ph == 0) != WS) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) {
-        S->iters = k;
-        S->status = int(Status::kBreakdown);
-        S->nan_flag = 1;
-        S->done = 1;
-      }
-      return;
-    }
-    if (ph == 0) {
-      c1 = ring4(al, k - 1);
-      wm = 1;
-      if (cyc == 3) {
-        const double bprev = ring4(be, k - 1);
-        const double a2 = ring4(al, k - 2);
-        if (fabs(bprev) >= s_pmb) { wm = 2; c2 = a2 / bprev; }
-        else { wm = 3; c2 = a2; }
-      }
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      S->zr[(k - 1) & 1] = rho;  // slot of k-1 (read as rho_{k-2} by the next sweep)
-      S->alpha1[k & 3] = alpha;
-      S->beta1[k & 3] = beta;
-      if (k >= 2) S->diff = diff;
-      S->w_pend = ph ? k : 0;
-      S->w_pend_n = ph;
-    }
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) S->halo_k = k + 1;  // the next exchange fills sweep k+1's inputs
+  const Pcg1Pro pro = pcg1_load_state(S);
+  pcg1_batch(pro, ord, ocls);
+  Pcg1Sweep sw;
+  if (!pcg1_scalars<WS>(pro, S, blockIdx.x == 0 && threadIdx.x == 0, sw)) return;
+  const long long k = sw.k;
+  const double alpha = sw.alpha, beta = sw.beta, c1 = sw.c1, c2 = sw.c2;
+  const int wm = sw.wm;
   int ti = 0, tj = 0;
   if (part.order) {  // slow (ellipse-cut) tiles first, so they do not trail the sweep
     if (pos >= part.count) return;
@@ -609,6 +512,13 @@ TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf, 
   return t;
 }
 
+int pcg1_lds_pad(int wpcu, int waves) {
+  if (wpcu <= 0) return 0;
+  constexpr int kLdsPerCu = 160 * 1024;
+  const int per_wg = (kLdsPerCu / std::max(1, wpcu / std::max(1, waves))) & ~511;  // 512-B granules
+  return std::max(0, per_wg - waves * 4096);
+}
+
 template <typename T>
 void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1,
                  double* partials, PcgState* S, const TileCfg& tc, hipStream_t s, int part, bool wsweep) {
@@ -624,10 +534,10 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
 #define PMX_PCG1_C(C, V, WV, PF)                                                                         \
   do {                                                                                                   \
     if (wsweep)                                                                                          \
-      hipLaunchKernelGGL((k_pcg1<T, C, V, WV, PF, true>), dim3(nb), dim3(bs), 0, s, G, Tb, w, r, r2, p0,  \
+      hipLaunchKernelGGL((k_pcg1<T, C, V, WV, PF, true>), dim3(nb), dim3(bs), tc.lds_pad, s, G, Tb, w, r, r2, p0, \
                          p1, partials, S, tc.rows, tc.tiles_j, tc.ntiles(), P);                          \
     else                                                                                                 \
-      hipLaunchKernelGGL((k_pcg1<T, C, V, WV, PF, false>), dim3(nb), dim3(bs), 0, s, G, Tb, w, r, r2, p0, \
+      hipLaunchKernelGGL((k_pcg1<T, C, V, WV, PF, false>), dim3(nb), dim3(bs), tc.lds_pad, s, G, Tb, w, r, r2, p0, \
                          p1, partials, S, tc.rows, tc.tiles_j, tc.ntiles(), P);                          \
   } while (0)
   // fp32 arithmetic: fp32 storage only, the default tile shape (VEC 2, 1 wave) and prefetch 1-3

@@ -1,7 +1,8 @@
 // Device building blocks of the single-pass PCG sweep (pcg1): column loads/stores, coefficient
-// classes, stencil arithmetic in fp64 or fp32, and pcg1_march -- one wave's march over one tile.
-// Shared by the launch-per-sweep kernel k_pcg1 (pcg1_kernels.hip) and the persistent small-grid
-// kernel k_pcg1_persist (pcg1_persist.hip).  See pcg1_kernels.hip's header for the algorithm.
+// classes, stencil arithmetic in fp64 or fp32, the sweep prologue (scalars, stop test, breakdown
+// guard, w schedule) and pcg1_march -- one wave's march over one tile.  Shared by the march kernel
+// k_pcg1 (pcg1_kernels.hip) and the block-tile kernel k_pcg1_block (pcg1_block.hip).  See
+// pcg1_kernels.hip's header for the algorithm.
 #pragma once
 
 #include <type_traits>
@@ -18,6 +19,160 @@ using namespace dev;
 namespace {
 
 constexpr int kNq = 5;  // rho, (Az,z), (Az,p), (Ap,p), |p|^2
+
+// ---- sweep prologue: ONE copy of the pcg1 control logic, used by k_pcg1 and k_pcg1_block --------
+// (the reference's loop control, stage4-mpi+cuda/poisson_mpi_cuda_f.cu:847-943: the stop test, the
+// |denominator| guard, alpha and beta -- here evaluated at the start of the sweep that needs them)
+
+// The PcgState fields a sweep reads.  Every one is a field the sweep does not write (the rings
+// alpha1 / beta1 / zr are written at slot k, read at k-1 / k-2), so the constant address space view
+// is exact and the loads are scalar.
+struct Pcg1Pro {
+  int done, norm, cyc;
+  long long k, max_iter;
+  double rc[kNq], al[4], be[4];
+  double zr0, zr1, delta, bd_tol, pmb;
+};
+
+__device__ __forceinline__ Pcg1Pro pcg1_load_state(const PcgState* S) {
+  typedef const __attribute__((address_space(4))) PcgState CState;
+  const CState* Sc = (const CState*)S;  // NOLINT: address-space cast
+  Pcg1Pro v;
+  v.done = Sc->done;
+  v.k = Sc->it;  // 0 = the init sweep (alpha = beta = 0: sums of r^0, z^0 only)
+#pragma unroll
+  for (int q = 0; q < kNq; ++q) v.rc[q] = Sc->red_c[q];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    v.al[q] = Sc->alpha1[q];
+    v.be[q] = Sc->beta1[q];
+  }
+  v.zr0 = Sc->zr[0];
+  v.zr1 = Sc->zr[1];
+  v.delta = Sc->delta;
+  v.bd_tol = Sc->bd_tol;
+  v.pmb = Sc->pair_min_beta;
+  v.max_iter = Sc->max_iter;
+  v.norm = Sc->norm;
+  v.cyc = Sc->w_cycle;
+  return v;
+}
+
+// Every state value (and the tile's dispatch slot, id / cls) consumed by one empty asm, so the
+// compiler issues all those scalar loads as ONE batch instead of sinking each below the branch that
+// first needs it: read field by field with waits in between, the state cost ~8 dependent memory round
+// trips, ~7 us of a ~25-us wave (wave traces, profiles/r2/prologue/).
+__device__ __forceinline__ void pcg1_batch(const Pcg1Pro& v, int id, unsigned long long cls) {
+  asm volatile("" ::"s"(v.done), "s"(v.k), "s"(id), "s"(cls), "s"(v.rc[0]), "s"(v.rc[1]), "s"(v.rc[2]), "s"(v.rc[3]),
+               "s"(v.rc[4]), "s"(v.al[0]), "s"(v.al[1]), "s"(v.al[2]), "s"(v.al[3]), "s"(v.be[0]), "s"(v.be[1]),
+               "s"(v.be[2]), "s"(v.be[3]), "s"(v.zr0), "s"(v.zr1), "s"(v.delta), "s"(v.bd_tol), "s"(v.pmb),
+               "s"(v.max_iter), "s"(v.norm), "s"(v.cyc));
+}
+
+// What sweep k runs with.  wm: the w schedule of this sweep (0 = w untouched; 1 = pairs; 2 = triples
+// with p^{k-2} recovered; 3 = triples re-reading p^{k-2}; see pcg1_march's WM).
+struct Pcg1Sweep {
+  long long k;
+  double alpha, beta, c1, c2;
+  int wm;
+};
+
+__device__ __forceinline__ double pcg1_ring4(const double (&v)[4], long long i) {
+  const int j = int(i & 3);
+  return j == 0 ? v[0] : j == 1 ? v[1] : j == 2 ? v[2] : v[3];
+}
+
+// The scalars of sweep k from the reduced sums of sweep k-1 (every workgroup computes the same
+// values).  Returns false when the sweep must not run: the solve is done, iteration k-1 met the stop
+// test or max_iter, alpha's denominator broke down, or the host launched the w kernel (WS) on the
+// wrong phase.  `leader` (one lane of the whole launch) records the outcome and the rings in S.
+template <bool WS>
+__device__ __forceinline__ bool pcg1_scalars(const Pcg1Pro& v, PcgState* S, bool leader, Pcg1Sweep& o) {
+  o = Pcg1Sweep{v.k, 0.0, 0.0, 0.0, 0.0, 0};
+  if (v.done) return false;
+  const long long k = v.k;
+  if (k > 0) {
+    const double rho = v.rc[0];  // rho_{k-1} = (z^{k-1}, r^{k-1})
+    double diff = 0.0;
+    if (k >= 2) {
+      // stop test of iteration k-1: ||w^k - w^{k-1}|| = |alpha_{k-1}| ||p^{k-1}||
+      diff = fabs(pcg1_ring4(v.al, k - 1)) * sqrt(v.rc[4]);
+      const bool bad = !(diff == diff) || !(rho == rho);
+      if (bad || diff < v.delta || k > v.max_iter) {
+        if (leader) {
+          S->diff = diff;
+          S->iters = k - 1;
+          S->status = bad ? int(Status::kBreakdown) : (diff < v.delta ? int(Status::kConverged) : int(Status::kMaxIter));
+          if (bad) S->nan_flag = 1;
+          S->done = 1;
+        }
+        return false;
+      }
+      o.beta = rho / ((k & 1) ? v.zr1 : v.zr0);  // rho_{k-2} sits in slot k & 1
+    }
+    // (A p^k, p^k) expanded from sweep k-1's sums (see pcg1_kernels.hip's header)
+    const double beta = o.beta;
+    const double denom = v.rc[1] + beta * (2.0 * v.rc[2] + beta * v.rc[3]);
+    const bool bd = v.norm == int(Norm::kWeighted) ? fabs(denom) < v.bd_tol : denom < v.bd_tol;
+    if (bd || !(denom == denom)) {
+      if (leader) {
+        if (k >= 2) S->diff = diff;
+        S->iters = k;
+        S->status = int(Status::kBreakdown);
+        if (!(denom == denom)) S->nan_flag = 1;
+        S->done = 1;
+      }
+      return false;
+    }
+    o.alpha = rho / denom;
+    // w schedule.  Pairs (w_cycle 2): even sweeps add alpha_{k-1} p^{k-1} + alpha_k p^k, p^{k-1}
+    // being the p_old the sweep reads anyway.  Triples (w_cycle 3, default): sweeps k = 0 mod 3
+    // also add alpha_{k-2} p^{k-2}, recovered without reading it: sweep k-1 formed
+    // p^{k-1} = D^-1 r^{k-2} + beta_{k-1} p^{k-2} and r^{k-1} = r^{k-2} - alpha_{k-1} A p^{k-1}, so
+    // p^{k-2} = (p^{k-1} - D^-1 (r^{k-1} + alpha_{k-1} A p^{k-1})) / beta_{k-1} -- one more stencil,
+    // on the p_old this sweep already holds.  Its rounding error grows like eps / |beta_{k-1}|, so
+    // below pair_min_beta the sweep re-reads p^{k-2} from the buffer it is about to overwrite.
+    // w moves on one sweep in three: 37.3 instead of 40 B/pt per iteration.  The stop test uses
+    // |alpha| ||p||, so the schedule changes no iteration count, only w's rounding.
+    const int ph = int(k % v.cyc);
+    // the host launches the w-sweep kernel (WS) exactly on the sweeps k = 0 mod w_cycle; a
+    // mismatch (host and device iteration counters out of step) must not pass silently
+    if ((ph == 0) != WS) {
+      if (leader) {
+        S->iters = k;
+        S->status = int(Status::kBreakdown);
+        S->nan_flag = 1;
+        S->done = 1;
+      }
+      return false;
+    }
+    if (ph == 0) {
+      o.c1 = pcg1_ring4(v.al, k - 1);
+      o.wm = 1;
+      if (v.cyc == 3) {
+        const double bprev = pcg1_ring4(v.be, k - 1);
+        const double a2 = pcg1_ring4(v.al, k - 2);
+        if (fabs(bprev) >= v.pmb) {
+          o.wm = 2;
+          o.c2 = a2 / bprev;
+        } else {
+          o.wm = 3;
+          o.c2 = a2;
+        }
+      }
+    }
+    if (leader) {
+      S->zr[(k - 1) & 1] = rho;  // slot of k-1 (read as rho_{k-2} by the next sweep)
+      S->alpha1[k & 3] = o.alpha;
+      S->beta1[k & 3] = o.beta;
+      if (k >= 2) S->diff = diff;
+      S->w_pend = ph ? k : 0;
+      S->w_pend_n = ph;
+    }
+  }
+  if (leader) S->halo_k = k + 1;  // the next exchange fills sweep k+1's inputs
+  return true;
+}
 
 // VEC columns from c0 (c0 - 1 even, so every 2-column chunk is 2-element aligned); chunks are
 // clamped to start <= cmax (cmax - 1 even, cmax + 1 inside the padded row).
@@ -64,46 +219,6 @@ __device__ __forceinline__ void store_cols(T* row, int c0, const T (&in)[VEC], b
 #pragma unroll
     for (int u = 0; u < VEC; ++u)
       if (own[u]) __builtin_nontemporal_store(in[u], col_ptr(row, c0 + u));
-  }
-}
-
-// Write-through variant (WT, the persistent kernel): buffer stores with the sc1 bit, so the bytes
-// leave the XCD L2 at once and a consumer in another workgroup of the same launch sees them after
-// the producer's vmcnt drain and its own agent acquire -- no L2 writeback fence per sweep
-// (MI355X_MICROARCH.md, publish-large: write-through wins for tens of KB per workgroup).  The row
-// pointer is wave-uniform (an SGPR resource), the column offset per lane; byte offsets stay below
-// 2 GB (persistent grids are <= 192 MB of fields).
-template <typename T, int VEC>
-__device__ __forceinline__ void store_cols_wt(T* row, int c0, const T (&in)[VEC], bool all, const bool (&own)[VEC]) {
-  constexpr int kSc1 = 16;  // aux bits: sc1
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(row - 2, 0, 0x7fffffff, 0x00020000);
-  if (all) {
-#pragma unroll
-    for (int q = 0; q < VEC / 2; ++q) {
-      const unsigned off = unsigned(c0 + 2 * q + 2) * unsigned(sizeof(T));
-      if constexpr (sizeof(T) == 8) {
-        typedef double d2 __attribute__((ext_vector_type(2)));
-        typedef unsigned u4 __attribute__((ext_vector_type(4)));
-        const d2 v = {in[2 * q], in[2 * q + 1]};
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), rs, off, 0, kSc1);
-      } else {
-        typedef float f2 __attribute__((ext_vector_type(2)));
-        typedef unsigned u2 __attribute__((ext_vector_type(2)));
-        const f2 v = {in[2 * q], in[2 * q + 1]};
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), rs, off, 0, kSc1);
-      }
-    }
-  } else {
-#pragma unroll
-    for (int u = 0; u < VEC; ++u)
-      if (own[u]) {
-        const unsigned off = unsigned(c0 + u + 2) * unsigned(sizeof(T));
-        typedef unsigned u2 __attribute__((ext_vector_type(2)));
-        if constexpr (sizeof(T) == 8)
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, in[u]), rs, off, 0, kSc1);
-        else
-          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, in[u]), rs, off, 0, kSc1);
-      }
   }
 }
 
@@ -255,20 +370,14 @@ struct Pcg1Row {
 // The tile marches top-down, rows i0-2 .. i1+2.  (Bottom-up and alternating marches, super-row and
 // banded dispatch orders were tried to make vertically adjacent tiles share their halo rows in L2:
 // all slower, NOTES #30, #46-48.)
-// CC (coefficient carry, the persistent kernel): a row the ellipse cuts has its face coefficients
-// evaluated ONCE, in stage A, and parked in a lane-private LDS ring (kring: 3 rows x VEC x 4 values
-// per lane) for stages B and C, instead of three evaluations per row -- on cut rows the exact face
-// formulas (fp64 divisions at quarter rate, executed by the whole wave for the few cut lanes) are
-// what makes a cut tile 3-5x slower than its neighbours, and at the reference's small grids the
-// slowest tile is the sweep.  Class-uniform rows never touch the ring.  Same values, same results.
-template <typename T, typename C, int VEC, int PF, int WM, bool FAST, bool WT = false, bool CC = false>
+template <typename T, typename C, int VEC, int PF, int WM, bool FAST>
 __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb, const ArithF& F, T* __restrict__ w,
                                            const T* __restrict__ rold, T* __restrict__ rnew,
                                            const T* __restrict__ pold,
                                            T* pnew, int i0, int i1, int j0, int j1,
                                            double alpha_d, double beta_d, double c1_d, double c2_d,
                                            double (&acc)[kNq], double* __restrict__ scol,
-                                           unsigned long long cls, bool use_cls, double* __restrict__ kring = nullptr) {
+                                           unsigned long long cls, bool use_cls) {
   constexpr bool WUP = WM != 0;
   constexpr bool PK = std::is_same_v<C, float> && VEC == 2;  // packed fp32 stencils (apply_row)
   const C alpha = C(alpha_d), beta = C(beta_d), c1 = C(c1_d), c2 = C(c2_d);
@@ -299,16 +408,9 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     return row_co(Tb, grow(m), gjlo, gjhi);
   };
   auto interior_row = [&](int m) { return G.gi0 + m >= 1 && G.gi0 + m <= G.M - 1; };
-  // CC ring slot of row m (m >= -3), value q in {a0, a1, b0, b1} of column u
-  auto ring = [&](int m, int u, int q) -> double& { return kring[(((m + 3) % 3 * VEC + u) * 4 + q) * 64 + lane]; };
-  // coefficients of a row in stage B / C: from the ring when CC carries them, else rebuilt
+  // coefficients of a row in stage B / C, rebuilt (class fast path or the exact face formulas)
   auto coef_at = [&](const RowCo& c, int m, int u, C& a0, C& a1, C& b0, C& b1) {
-    if constexpr (CC) {
-      if (c.ucls == 0) {
-        a0 = C(ring(m, u, 0)); a1 = C(ring(m, u, 1)); b0 = C(ring(m, u, 2)); b1 = C(ring(m, u, 3));
-        return;
-      }
-    }
+    (void)m;
     coef_c<C>(c, Tb, G, F, scol, u, lane, gj[u], a0, a1, b0, b1);
   };
 
@@ -344,17 +446,6 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     parked = true;
   };
   if (cB.ucls == 0) park_cols();
-  if constexpr (CC) {  // row i0-3 enters stage B at the first step without passing stage A
-    if (cB.ucls == 0) {
-#pragma unroll
-      for (int u = 0; u < VEC; ++u) {
-        C a0, a1, b0, b1;
-        coef_c<C>(cB, Tb, G, F, scol, u, lane, gj[u], a0, a1, b0, b1);
-        ring(i0 - 3, u, 0) = double(a0); ring(i0 - 3, u, 1) = double(a1);
-        ring(i0 - 3, u, 2) = double(b0); ring(i0 - 3, u, 3) = double(b1);
-      }
-    }
-  }
 
   const int mfirst = i0 - 2, mlast = i1 + 2;
   auto step = [&](int m, const Pcg1Row<T, VEC>& cur, Pcg1Row<T, VEC>& nxt) {
@@ -373,12 +464,6 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
       pom[u] = in ? C(cur.p[u]) : C(0);
       C a0, a1, b0, b1;
       coef_c<C>(cA, Tb, G, F, scol, u, lane, gj[u], a0, a1, b0, b1);
-      if constexpr (CC) {
-        if (cA.ucls == 0) {
-          ring(m, u, 0) = double(a0); ring(m, u, 1) = double(a1);
-          ring(m, u, 2) = double(b0); ring(m, u, 3) = double(b1);
-        }
-      }
       const C z = zdiv_c<C>(cA.ucls, rom[u], a0, a1, b0, b1, G, F);
       const C v = fma_c(beta, pom[u], z);
       Pm[u] = in ? C(static_cast<T>(v)) : C(0);  // the stored (rounded) p^k is the one used
@@ -446,15 +531,9 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     }
     if (ownB && (FAST ? own_all : own_any)) {
       const int64_t o = int64_t(mb) * P;
-      if constexpr (WT) {
-        store_cols_wt<T, VEC>(rnew + o, c0, rs, FAST || own_all, own);
-        store_cols_wt<T, VEC>(pnew + o, c0, ps, FAST || own_all, own);
-        if constexpr (WUP) store_cols_wt<T, VEC>(w + o, c0, ws, FAST || own_all, own);
-      } else {
-        store_cols<T, VEC>(rnew + o, c0, rs, FAST || own_all, own);
-        store_cols<T, VEC>(pnew + o, c0, ps, FAST || own_all, own);
-        if constexpr (WUP) store_cols<T, VEC>(w + o, c0, ws, FAST || own_all, own);
-      }
+      store_cols<T, VEC>(rnew + o, c0, rs, FAST || own_all, own);
+      store_cols<T, VEC>(pnew + o, c0, ps, FAST || own_all, own);
+      if constexpr (WUP) store_cols<T, VEC>(w + o, c0, ws, FAST || own_all, own);
     }
     // ---- stage C: A z^k of row m-2
     const int mcr = m - 2;

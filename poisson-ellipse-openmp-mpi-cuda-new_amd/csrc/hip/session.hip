@@ -163,8 +163,7 @@ PcgDriver::PathStats Session::path_stats() const {
   require_connected();
   PcgDriver::PathStats p = drivers_[0]->path_stats();
   for (auto& d : drivers_)
-    PMX_CHECK(d->path_stats().graph_iters == p.graph_iters && d->path_stats().eager_iters == p.eager_iters &&
-                  d->path_stats().persistent_iters == p.persistent_iters,
+    PMX_CHECK(d->path_stats().graph_iters == p.graph_iters && d->path_stats().eager_iters == p.eager_iters,
               "drivers disagree on the launch path");
   return p;
 }
@@ -176,11 +175,6 @@ void Session::reset_path_stats() {
 bool Session::split_sweep() const {
   require_connected();
   return drivers_[0]->split_sweep();
-}
-
-bool Session::persistent() const {
-  require_connected();
-  return drivers_[0]->persistent();
 }
 
 bool Session::direct_rows() const {

@@ -102,15 +102,15 @@ struct GpuOptions {
   // placement_budget_s of probing and by keeping placement_keep_free of the free memory free.
   // bench.py turns it on unless ranks share the device.  PMX_PLACEMENT=K overrides.
   int placement = 0;
-  // Persistent iteration (pcg1_persist.hip): one launch runs a whole batch of sweeps with an
-  // in-kernel grid barrier and reduction.  1 = on where it applies (fp64, undecomposed); -1 (auto)
-  // and 0 = off: the block-tile sweep's graph replays beat it on every grid measured.
-  // PMX_PERSISTENT overrides.
-  int persistent = -1;
   // Block tiles for the pcg1 sweep (pcg1_block.hip): -1 = auto (undecomposed fp64 grids with fewer
   // than 10,000 four-row march tiles, ~1600x2400), 0 = off, 1 = on for any undecomposed fp64 grid.
   // PMX_PCG1_BLOCK overrides.
   int block1 = -1;
+  // pcg1 march sweeps: resident waves per CU (0 = as many as the registers allow: 16 for the plain
+  // sweep, 12 for the w sweep).  A cap is enforced with padding LDS per workgroup.  Fewer streams
+  // in flight keep more DRAM rows open per access (bench/probe/dma_march.hip).
+  // PMX_PCG1_WPCU / PMX_PCG1_WPCU_W override.
+  int wpcu1 = 0, wpcu1w = 0;
   double placement_budget_s = 0.5;
   double placement_keep_free = 0.5;
   bool resolved = false;  // environment overrides already applied (resolve_options)
@@ -190,11 +190,6 @@ class GpuSubdomainSolver {
   // pcg1 only: the interior (part 1) or frame (part 2) tiles of the sweep, see launch_pcg1
   void enqueue_kernel_a_part(hipStream_t s, int part);
   bool has_interior_split() const { return pcg1_ && geom_.nb != 0; }
-  // persistent iteration (GpuOptions::persistent): sweeps host_k .. host_k + n - 1 in ONE launch
-  bool persistent() const { return persist_; }
-  void enqueue_persistent(hipStream_t s, long long n);
-  const TileCfg& tiles_persistent() const { return tilesP_; }
-  int persistent_workgroups() const { return pwg_; }
   void enqueue_reduce_a(hipStream_t s);
   void enqueue_kernel_b(hipStream_t s, bool pack);
   void enqueue_reduce_b(hipStream_t s);
@@ -310,13 +305,6 @@ class GpuSubdomainSolver {
   long long host_k_ = 0;
   bool direct_rows_ = false;
   long long halo_target_ = 0;
-  bool persist_ = false;
-  TileCfg tilesP_{};
-  Pcg1Slot* tile_order_p_ = nullptr;
-  Pcg1Slot* sched_p_ = nullptr;  // the persistent kernel's static schedule (inside tile_order_p_)
-  int* sched_offs_p_ = nullptr;
-  PersistWs* pws_ = nullptr;
-  int pwg_ = 0;
   TileCfg init_tiles_{};
   CommLayout layout_{};
   size_t elem_ = 8, field_bytes_ = 0, field_off_ = 0;
@@ -468,12 +456,11 @@ class PcgDriver {
   // pcg1 split sweep in use (interior tiles overlap the previous exchange, see enqueue_split_iteration)
   bool split_sweep() const { return split_; }
   bool direct_rows() const { return direct_; }
-  bool persistent() const { return persistent_; }
 
   // Which path ran: iterations replayed from captured graphs / enqueued as individual launches
   // since the last reset, and the graph lengths used (bench.py reports them for its timed region).
   struct PathStats {
-    int64_t graph_iters = 0, eager_iters = 0, persistent_iters = 0;
+    int64_t graph_iters = 0, eager_iters = 0;
     std::vector<int> graph_lengths;  // distinct lengths, in first-use order
   };
   const PathStats& path_stats() const { return path_; }
@@ -515,7 +502,6 @@ class PcgDriver {
   bool single_pass_ = false;
   bool any_nb_ = false;
   bool direct_ = false;  // direct-row ghost exchange (GpuSubdomainSolver::set_direct_rows)
-  bool persistent_ = false;  // one local undecomposed solver running persistent launches
   std::vector<hipStream_t> comm_streams_;
   std::vector<hipEvent_t> ev_packed_, ev_halo_;
   // split sweep (pcg1 with neighbours and overlap): the frame tiles run on their own stream

@@ -51,6 +51,7 @@ struct TileCfg {
   const Pcg1Slot* order1 = nullptr;
   const Pcg1Slot* order2 = nullptr;  // the frame tiles
   int arith32 = 0;  // kind 3 with fp32 storage: 1 = fp32 stencil arithmetic (GpuOptions::arith32)
+  int lds_pad = 0;  // kind 3: dynamic LDS bytes per workgroup that cap the resident waves per CU
   int interior_tiles() const { return (ti_hi - ti_lo) * (tj_hi - tj_lo); }
   int ntiles() const { return tiles_i * tiles_j; }
 };
@@ -63,6 +64,9 @@ TileCfg make_wave_tiles(const DevGeom& G, int vec, int waves, int rows, int max_
 TileCfg make_row_tiles(const DevGeom& G, int vec, int waves, int rows);
 // kind 3 tiles for k_pcg1: 64*vec - 4 owned columns, rows = 0: auto
 TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf = 0, int elem = 8);
+// padding LDS (bytes per workgroup) that lets at most wpcu workgroups of k_pcg1 (static LDS: 4 KiB
+// per wave) share a CU; 0 for no cap
+int pcg1_lds_pad(int wpcu, int waves);
 
 enum ReduceMode : int { kSkipIfDone = 1, kBumpIter = 2 };
 
@@ -160,34 +164,6 @@ void launch_reduce(const double* partials, int n, int nq, double w0, double w1, 
 // bump; launch_pcg1_halo counts [1] (exchanges packed) and [2] (exchanges unpacked).
 void launch_reduce_n(const double* partials, int n, int nq, const double* weights, double* out,
                      PcgState* S, int mode, double* ws, hipStream_t s, long long* progress = nullptr);
-
-// Persistent single-pass iteration (pcg1_persist.hip): nwg workgroups of kPersistThreads stay
-// resident and run sweeps host_k .. k_end with an in-kernel grid barrier and reduction, leaving
-// PcgState exactly as the launch-per-sweep path would (undecomposed grids; see the file header).
-// `ws` holds the polled words (the first kPersistPolled bytes, zeroed before every launch) and the
-// per-workgroup partials; weights: the 5 sums' weights as for launch_reduce_n.
-constexpr int kPersistMaxWg = 1024;
-constexpr int kPersistThreads = 512;  // 8 waves per workgroup (2 per SIMD), one workgroup per CU
-struct PersistWs {
-  unsigned long long arrive;  // grid barrier arrivals (monotonic within a launch)
-  unsigned long long err;     // 1: a barrier wait timed out (the solve is stopped)
-  unsigned long long pad[6];
-  double part[2][5 * kPersistMaxWg];  // per-workgroup partial sums, by barrier parity
-};
-constexpr size_t kPersistPolled = 64;
-template <typename T>
-int launch_pcg1_persist(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1, PcgState* S,
-                        PersistWs* ws, const TileCfg& tc, const Pcg1Slot* sched, const int* offs, int nwg,
-                        long long k_end, const double* weights, hipStream_t s);
-// The persistent kernel's static schedule: tc's tiles (tc.order0, with their row classes) onto
-// `nwaves` waves, longest first onto the least loaded wave, a cut row costing cut_row_cost row steps
-// more; d_sched (tc.ntiles() slots) lists wave 0's tiles, then wave 1's ..., d_offs (nwaves + 1)
-// where each wave's list starts.
-void pcg1_persist_schedule(const TileCfg& tc, int nwaves, double cut_row_cost, Pcg1Slot* d_sched, int* d_offs);
-int pcg1_persist_max_wg(int device);  // workgroups that are always co-resident (one per CU)
-// PMX_PERSIST_TRACE=k: stamps of sweep k of the last launch -- 2 per wave (march start, end), then 2
-// per workgroup (barrier arrival, exit); wall_clock64 ticks (100 MHz)
-std::vector<unsigned long long> pcg1_persist_trace();
 
 // Deterministic in-process "all-reduce" across P subdomains on one device (LocalComm):
 // out_k[q] = sum_r in_r[q] for every k, summed in rank order.

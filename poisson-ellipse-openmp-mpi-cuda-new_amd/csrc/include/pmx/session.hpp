@@ -71,7 +71,6 @@ class Session {
   void reset_path_stats();
   bool split_sweep() const;
   bool direct_rows() const;
-  bool persistent() const;  // batches run as persistent launches (GpuOptions::persistent)
   // host-mapped device progress of owned rank i (GpuSubdomainSolver::progress); no HIP call
   void progress(int i, long long out[3]) const;
   // error vs the analytic solution over the owned subdomains (sum of e^2, max |e|, max w)

@@ -81,8 +81,7 @@ def make_session(problem: PoissonEllipse, ranks: int = 1, split: str = "referenc
                  tile_rows: int = 0, exact: bool = False, graph_batch: int = 32, check: bool = False,
                  overlap: bool = True, vec_b: int = 0, waves_b: int = 0, tile_rows_b: int = -1,
                  poison_halos: bool = False, b_ring: bool = False, placement: int = 0,
-                 placement_budget_s: float = 0.5, placement_keep_free: float = 0.5, persistent: int = -1,
-                 block_tiles: int = -1):
+                 placement_budget_s: float = 0.5, placement_keep_free: float = 0.5, block_tiles: int = -1):
     """Native GPU session with `ranks` subdomains on one device (LocalComm when ranks > 1).
 
     overlap: ghost exchange on a second stream concurrent with pcg_b (only matters for ranks > 1).
@@ -96,9 +95,6 @@ def make_session(problem: PoissonEllipse, ranks: int = 1, split: str = "referenc
     default; bounded by placement_budget_s seconds and by leaving placement_keep_free of the free
     device memory free -- see GpuSubdomainSolver::place_fields).
 
-    persistent: 1 = run whole batches of iterations in one persistent launch (fp64, one subdomain,
-    pcg1_persist.hip); -1 (auto) and 0 = graph replays (on small grids of the block-tile sweep,
-    pcg1_block.hip, which is faster)
     block_tiles: -1 = auto (block-tile sweeps, pcg1_block.hip, on small undecomposed fp64 grids), 0 = off,
     1 = on for any undecomposed fp64 grid."""
     n = _native()
@@ -108,7 +104,7 @@ def make_session(problem: PoissonEllipse, ranks: int = 1, split: str = "referenc
                      check=check, overlap=overlap, vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b,
                      poison_halos=poison_halos, b_ring=b_ring, placement=placement,
                      placement_budget_s=placement_budget_s, placement_keep_free=placement_keep_free,
-                     persistent=persistent, block_tiles=block_tiles)
+                     block_tiles=block_tiles)
 
 
 def solve_hip(problem: PoissonEllipse, ranks: int = 1, keep_solution: bool = True, poll_batches: int = 1,

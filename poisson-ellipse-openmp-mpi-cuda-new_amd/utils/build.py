@@ -35,7 +35,6 @@ HIP_SOURCES = [
     "hip/pcg_kernels.hip",
     "hip/pcg_kernels_dpp.hip",
     "hip/pcg1_kernels.hip",
-    "hip/pcg1_persist.hip",
     "hip/pcg1_block.hip",
     "hip/ops_kernels.hip",
     "hip/gpu_solver.hip",

@@ -21,7 +21,6 @@ def _sess(pkg, monkeypatch, M, N, rows, **kw):
         monkeypatch.setenv("PMX_PCG1_BLOCK_ROWS", str(rows))
     else:
         monkeypatch.setenv("PMX_PCG1_BLOCK", "0")  # the march (auto picks block tiles on small grids)
-    kw.setdefault("persistent", 0)
     return pkg.make_session(pkg.PoissonEllipse(M=M, N=N), **kw)
 
 
@@ -45,7 +44,7 @@ def test_block_tiles_goldens_and_march_agreement(pkg, monkeypatch, rows, grid, i
 
 def test_block_tiles_auto_choice(pkg, monkeypatch):
     monkeypatch.delenv("PMX_PCG1_BLOCK", raising=False)
-    mk = lambda M, N, **kw: pkg.make_session(pkg.PoissonEllipse(M=M, N=N), persistent=0, **kw)  # noqa: E731
+    mk = lambda M, N, **kw: pkg.make_session(pkg.PoissonEllipse(M=M, N=N), **kw)  # noqa: E731
     assert mk(400, 600).tile.get("block_tiles") and mk(400, 600).tile["rows"] == 8   # 500 four-row tiles
     assert mk(800, 1200).tile.get("block_tiles") and mk(800, 1200).tile["rows"] == 12  # 2,000
     assert mk(1600, 2400).tile.get("block_tiles")          # 8,000: still latency-bound
@@ -84,3 +83,33 @@ def test_block_tiles_fused_and_separate_reduction(pkg, monkeypatch, grid, iters)
         assert r["status"] == "converged" and r["iters"] == iters
         out[fused] = s.gather_local_w()
     assert np.abs(out["1"] - out["0"]).max() <= 1e-10 * np.abs(out["0"]).max()
+
+
+@pytest.mark.parametrize("grid", [(40, 40), (400, 600)])
+def test_block_and_march_share_the_control_logic(pkg, monkeypatch, grid):
+    """k_pcg1 and k_pcg1_block run ONE copy of the sweep prologue (pcg1_march.hpp: pcg1_scalars --
+    stop test, breakdown guard, w-phase check, ring writes, halo_k).  Stepped one sweep at a time,
+    both paths must agree on every integer state field after every sweep (the iteration counter,
+    the deferred-w bookkeeping, done / status at the stop) and on the scalars to rounding (the two
+    paths add the partial sums in different orders)."""
+    b = _sess(pkg, monkeypatch, *grid, 8, graph_batch=0)
+    m = _sess(pkg, monkeypatch, *grid, 0, graph_batch=0)
+    assert b.tile.get("block_tiles") and not m.tile.get("block_tiles")
+    for s in (b, m):
+        s.init()
+    limit = 60 if grid == (40, 40) else 7
+    for k in range(limit):
+        for s in (b, m):
+            s.step(1)
+            s.synchronize()
+        sb, sm = b.state(0), m.state(0)
+        for f in ("it", "iters", "done", "status", "nan", "w_pend", "w_pend_n", "w_cycle", "halo_k"):
+            assert sb[f] == sm[f], (k, f, sb[f], sm[f])
+        for f in ("alpha1", "beta1", "zr"):
+            for x, y in zip(sb[f], sm[f]):
+                assert abs(x - y) <= 1e-12 * max(abs(y), 1e-300), (k, f, x, y)
+        assert abs(sb["diff"] - sm["diff"]) <= 1e-11 * max(abs(sm["diff"]), 1e-300)
+        if sm["done"]:
+            break
+    if grid == (40, 40):
+        assert sm["done"] and sm["status"] == "converged" and sm["iters"] == 50

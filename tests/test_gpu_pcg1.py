@@ -236,7 +236,7 @@ def test_pcg1_graph_phases_match_eager(pkg, monkeypatch, ranks):
     p = pkg.PoissonEllipse(M=400, N=600)
     out = {}
     for gb in (0, 32):
-        s = sub("models").make_session(p, ranks=ranks, graph_batch=gb, persistent=0)
+        s = sub("models").make_session(p, ranks=ranks, graph_batch=gb)
         s.init()
         for n in (5, 64, 7, 32, 33, 1, 32):
             s.step(n)

@@ -79,27 +79,25 @@ def test_poisoned_halo_without_exchange_raises_nan_flag(pkg, native, algo):
     assert st["nan"]
 
 
-@pytest.mark.parametrize("persistent", [0, 1])
 @pytest.mark.parametrize("steps", [7, 8])
-def test_resume_with_pending_w_step_is_bitwise(pkg, tmp_path, steps, persistent):
+def test_resume_with_pending_w_step_is_bitwise(pkg, tmp_path, steps):
     """A checkpoint taken mid-cycle holds deferred w steps (pcg1 fp64 moves w on one sweep in
     three: 1 or 2 steps pending); the resumed solve -- whose host iteration counter comes from the
     checkpoint and picks the plain / w sweep kernels and graph phase -- must apply them exactly like
-    the uninterrupted one.  Each launch path against itself: the persistent kernel sums its partials
-    per workgroup, the graph path per tile, so the two agree to rounding, not bitwise."""
+    the uninterrupted one."""
     models = sub("models")
     p = pkg.PoissonEllipse(M=400, N=600)
     path = str(tmp_path / "ck.bin")
-    ref = models.make_session(p, persistent=persistent)
+    ref = models.make_session(p)
     rr = ref.solve_checkpointed(str(tmp_path / "unused.bin"), every=0)
-    # stop at exactly `steps`: eager launches, or one persistent launch of `steps` iterations
-    a = models.make_session(p, graph_batch=0) if not persistent else models.make_session(p, persistent=1)
+    # stop at exactly `steps`: eager launches
+    a = models.make_session(p, graph_batch=0)
     a.init()
     a.step(steps)
     a.synchronize()
     assert a.state()["w_pend"] == steps and a.state()["w_pend_n"] == steps % 3
     a.save_checkpoint(path)
-    b = models.make_session(p, persistent=persistent)
+    b = models.make_session(p)
     rb = b.solve_checkpointed(path, every=0, resume=True)
     assert rb["iters"] == rr["iters"] == 546
     assert np.array_equal(b.gather_local_w(), ref.gather_local_w())

@@ -108,7 +108,7 @@ def test_wave_kernels_decomposed(pkg, ranks):
 def test_graph_vs_eager(pkg):
     p = pkg.PoissonEllipse(M=400, N=600)
     a = pkg.solve(p, "hip", graph_batch=0)
-    b = pkg.solve(p, "hip", graph_batch=16, persistent=0)  # graph replays, not the persistent launch
+    b = pkg.solve(p, "hip", graph_batch=16)
     assert a.iters == b.iters == 546
     assert np.array_equal(a.w, b.w)
 
@@ -180,8 +180,7 @@ def test_native_rccl_world1(pkg, rccl_graph):
     r = s.solve()
     assert r.iters == 546 and r.status == "converged"
     assert s.session.comm_name == "rccl"
-    # the same launch path on one GPU (the persistent kernel sums per workgroup, graphs per tile)
-    ref = pkg.solve(p, "hip", persistent=1 if s.session.persistent else 0)
+    ref = pkg.solve(p, "hip")
     assert np.array_equal(r.w, ref.w)
 
 
