@@ -1001,6 +1001,31 @@ def script(name: str, steps) -> str:
     return "\n".join(lines) + "\n"
 
 
+# round 5: march occupancy / prefetch depth (bench/probe/dma_march.hip showed the access pattern
+# runs 9% faster at 8-10 than at 16 waves per CU); the shared-prologue tests
+_AB5 = "python -u bench/ab_env.py --fresh --shape 16384x16384 --rounds 2 --iters 200 "
+STUDIES["r5a"] = [
+    ("probe", 240, "bench/probe/dma_march 16384 3 10"),
+    ("tests_block", 400, f"{PYTEST} tests/test_gpu_block.py"),
+    ("ab_pf", 900, _AB5 + "--cfg base: --cfg pf2:PMX_PCG1_PF=2,PMX_PCG1_PF_W=1 "
+                    "--cfg pf2w12:PMX_PCG1_PF=2,PMX_PCG1_PF_W=1,PMX_PCG1_WPCU=12 "
+                    "--cfg pf2w10:PMX_PCG1_PF=2,PMX_PCG1_PF_W=1,PMX_PCG1_WPCU=10 "
+                    "--cfg pf3w12:PMX_PCG1_PF=3,PMX_PCG1_PF_W=1,PMX_PCG1_WPCU=12 "
+                    "--cfg pf3w10:PMX_PCG1_PF=3,PMX_PCG1_PF_W=1,PMX_PCG1_WPCU=10 "
+                    "--cfg wpf2w10:PMX_PCG1_PF_W=2,PMX_PCG1_WPCU_W=10"),
+]
+
+
+STUDIES["r5c"] = [
+    ("tests_dma", 600, f"{PYTEST} tests/test_gpu_pcg1.py -k 'dma or goldens'"),
+    ("ab_dma", 900, _AB5 + "--cfg base: --cfg d2:PMX_PCG1_DMA=2 --cfg d3:PMX_PCG1_DMA=3 "
+                    "--cfg d2w12:PMX_PCG1_DMA=2,PMX_PCG1_WPCU=12,PMX_PCG1_WPCU_W=10 "
+                    "--cfg d3w12:PMX_PCG1_DMA=3,PMX_PCG1_WPCU=12,PMX_PCG1_WPCU_W=10 "
+                    "--cfg d2w10:PMX_PCG1_DMA=2,PMX_PCG1_WPCU=10,PMX_PCG1_WPCU_W=8 "
+                    "--cfg d2p:PMX_PCG1_DMA=2,PMX_PCG1_DMA_W=0"),
+]
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("study", choices=sorted(STUDIES) + sorted(PARAMETRISED))

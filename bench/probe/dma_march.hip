@@ -56,10 +56,11 @@ typedef double d2v __attribute__((ext_vector_type(2)));
 
 struct Geo {
   int n, pitch, TI, tiles_i, tiles_j, halo;  // halo 0: march rows i0 .. i1+1 only (one extra row)
+  int order;  // 0: XCD bands of tile rows (xcd_remap, as k_pcg1); 1: block b = tile b (XCDs interleaved)
 };
 
 __device__ __forceinline__ void tile_of(const Geo& g, int& i0, int& i1, int& c0) {
-  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int id = g.order == 0 ? xcd_remap(blockIdx.x, gridDim.x) : int(blockIdx.x);
   const int ti = id / g.tiles_j, tj = id - ti * g.tiles_j;
   i0 = 2 + ti * g.TI;
   i1 = min(i0 + g.TI - 1, g.n - 3);
@@ -149,6 +150,68 @@ __global__ void __launch_bounds__(64) k_il(Geo g, const double* __restrict__ rp,
     }
   }
 done:
+  if (acc == 12345.678) sink[0] = acc + cap[0];
+}
+
+// Register prefetch (PF 1) like k_reg, but the march split into phases (3 steps without stores, a
+// steady loop whose every step stores, one last step without) and the stores issued for all 64
+// lanes as buffer stores whose non-owned lanes get an out-of-range offset (dropped by the range
+// check): no store is conditional, so the compiler's vmcnt wait for the prefetched row counts the
+// previous step's stores as younger ops instead of waiting for their acknowledgement.
+__device__ __forceinline__ void st_rows(const double* base, unsigned voff, d2v v) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), 0, 0x7fffffff, 0x00020000);
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), rs, voff, 0, 2);  // aux 2: nt
+}
+
+template <int WORK>
+__global__ void __launch_bounds__(64) k_regp(Geo g, const double* __restrict__ r, const double* __restrict__ p,
+                                             double* __restrict__ rn, double* __restrict__ pn, double a,
+                                             double* sink) {
+  extern __shared__ double cap[];
+  int i0, i1, c0;
+  tile_of(g, i0, i1, c0);
+  const int lane = threadIdx.x & 63;
+  const bool own = lane >= 1 && lane <= 62 && c0 + 1 < g.n;
+  const unsigned soff = own ? unsigned(c0) * 8u : 0x80000000u;  // dropped lanes: out of range
+  const int mfirst = i0 - 2, mlast = i1 + 2;
+  const int h = i1 - i0 + 1;
+  double2 br[2], bp[2];
+  auto fetch = [&](int m, double2& x, double2& y) {
+    m = min(m, mlast);
+    x = *reinterpret_cast<const double2*>(r + size_t(m) * g.pitch + c0);
+    y = *reinterpret_cast<const double2*>(p + size_t(m) * g.pitch + c0);
+  };
+  double acc = 0.0;
+  double x[2] = {0, 0}, y[2] = {0, 0};
+  auto body = [&](int t, const double2& cr, const double2& cp, bool store) {
+    x[0] += cr.x; x[1] += cr.y; y[0] += cp.x; y[1] += cp.y;
+    work<WORK>(x, y, a);
+    x[0] += shl(y[1]);
+    if (store) {
+      const size_t o = size_t(mfirst + t - 1) * g.pitch;
+      st_rows(rn + o, soff, (d2v){x[0], x[1]});
+      st_rows(pn + o, soff, (d2v){y[0], y[1]});
+    }
+    acc += x[0] * y[1];
+  };
+  fetch(mfirst, br[0], bp[0]);
+  // steps 0 .. 2: no stores
+  fetch(mfirst + 1, br[1], bp[1]); body(0, br[0], bp[0], false);
+  fetch(mfirst + 2, br[0], bp[0]); body(1, br[1], bp[1], false);
+  fetch(mfirst + 3, br[1], bp[1]); body(2, br[0], bp[0], false);
+  // steps 3 .. h+2: every step stores (two steps per trip, so the ring needs no copies)
+  int t = 3;
+  for (; t + 1 <= h + 2; t += 2) {
+    fetch(mfirst + t + 1, br[0], bp[0]); body(t, br[1], bp[1], true);
+    fetch(mfirst + t + 2, br[1], bp[1]); body(t + 1, br[0], bp[0], true);
+  }
+  if (t <= h + 2) {
+    fetch(mfirst + t + 1, br[0], bp[0]); body(t, br[1], bp[1], true);
+    body(t + 1, br[0], bp[0], false);  // the last step (t + 1 = h + 3)
+  } else {
+    body(t, br[1], bp[1], false);
+  }
   if (acc == 12345.678) sink[0] = acc + cap[0];
 }
 
@@ -286,24 +349,22 @@ int main(int argc, char** argv) {
     int pf, dma;
   };
   const V vars[] = {
-      {"reg1", k_reg<1, 6>, 1, 0}, {"il1", k_il<1, 6>, 1, 0}, {"one", k_one<6>, 1, 0},
+      {"reg1", k_reg<1, 6>, 1, 0}, {"reg1w", k_reg<1, 30>, 1, 0},
   };
-  const int tis[] = {8};
-  const int wpcu[] = {8, 10, 12, 16};
+  const int tis[] = {4, 6, 8};
+  const int wpcu[] = {8, 12, 16};
   printf("n=%d pitch=%d candidates=%d reps=%d (ms per sweep; GB/s at 32 B/pt)\n", n, pitch, ncand, reps);
-  for (int halo = 1; halo >= 1; --halo)
+  for (int order = 0; order <= 1; ++order)
   for (int TI : tis) {
-    Geo g{n, pitch, TI, (n - 4 + TI - 1) / TI, (n - 4 + 123) / 124, halo};
+    Geo g{n, pitch, TI, (n - 4 + TI - 1) / TI, (n - 4 + 123) / 124, 1, order};
     const int nb = g.tiles_i * g.tiles_j;
     for (int wc : wpcu) {
       for (const V& v : vars) {
-        if (!halo && v.dma) continue;
-        if (v.dma && wc < 12) continue;
         const size_t ring = v.dma ? size_t(v.pf) * 2048 : 0;
         const size_t lds = std::max(ring, size_t(163840 / wc) & ~size_t(255));
         CK(hipFuncSetAttribute(reinterpret_cast<const void*>(v.k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                int(lds)));
-        printf("halo=%d TI=%2d waves/CU=%2d %-5s:", halo, TI, wc, v.name);
+        printf("order=%d TI=%2d waves/CU=%2d %-5s:", order, TI, wc, v.name);
         std::vector<float> ms;
         for (int c = 0; c < ncand; ++c) {
           double* b = blocks[c];
@@ -332,7 +393,7 @@ int main(int argc, char** argv) {
   }
   // correctness of the DMA ring: the two kernels must store identical rn/pn
   {
-    Geo g{n, pitch, 8, (n - 4 + 7) / 8, (n - 4 + 123) / 124, 1};
+    Geo g{n, pitch, 8, (n - 4 + 7) / 8, (n - 4 + 123) / 124, 1, 0};
     const int nb = g.tiles_i * g.tiles_j;
     double* b = blocks[0];
     double *r = b, *p = b + fb / 8, *rn = b + 2 * (fb / 8), *pn = b + 3 * (fb / 8);

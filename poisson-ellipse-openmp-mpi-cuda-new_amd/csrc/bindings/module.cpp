@@ -504,6 +504,11 @@ PYBIND11_MODULE(_pmx, m) {
              { py::gil_scoped_release g; w = s.local_w(i); }
              return to_numpy(w, {s.solver(i).sd().nx, s.solver(i).sd().ny});
            }, py::arg("i") = 0)
+      .def("partials", [](Session& s, int i) {
+             std::vector<double> v;
+             { py::gil_scoped_release g; v = s.partials(i); }
+             return to_numpy(v, {py::ssize_t(v.size() / 5), 5});
+           }, py::arg("i") = 0, "per-tile partial sums of the last sweep (tests of the reduction hand-off)")
       .def("init", [](Session& s) { py::gil_scoped_release g; s.init(); })
       .def("step", [](Session& s, int64_t n) { py::gil_scoped_release g; s.step(n); })
       .def("synchronize", [](Session& s) { py::gil_scoped_release g; s.synchronize(); })
@@ -586,6 +591,8 @@ PYBIND11_MODULE(_pmx, m) {
           d["block"] = t.block; d["rows"] = t.rows;
           d["vec"] = t.vec; d["waves"] = t.waves; d["tiles_i"] = t.tiles_i; d["tiles_j"] = t.tiles_j;
           if (t.kind == 3) d["pf"] = t.pf;
+          if (t.kind == 3 && t.dpf) d["dpf"] = t.dpf;
+          if (t.kind == 3 && t.lds_pad) d["lds_pad"] = t.lds_pad;
           return d;
         };
         py::dict d = one(s.solver(0).tiles());

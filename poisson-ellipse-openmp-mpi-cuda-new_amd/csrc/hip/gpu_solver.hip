@@ -103,6 +103,11 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_PLACEMENT", o.placement);
   env_int("PMX_PCG1_WPCU", o.wpcu1);
   env_int("PMX_PCG1_WPCU_W", o.wpcu1w);
+  env_int("PMX_PCG1_DMA", o.dma1);
+  env_int("PMX_PCG1_DMA_W", o.dma1w);
+  PMX_CHECK(o.dma1 == 0 || o.dma1 == 2 || o.dma1 == 3, "pcg1 LDS-DMA prefetch depth must be 0, 2 or 3");
+  PMX_CHECK(o.dma1w == -1 || o.dma1w == 0 || o.dma1w == 2 || o.dma1w == 3,
+            "pcg1 w-sweep LDS-DMA prefetch depth must be -1, 0, 2 or 3");
   PMX_CHECK(o.wpcu1 >= 0 && o.wpcu1 <= 32 && o.wpcu1w >= 0 && o.wpcu1w <= 32, "pcg1 waves per CU must be 0..32");
   PMX_CHECK(o.wcycle1 == 2 || o.wcycle1 == 3, "pcg1 w cycle must be 2 or 3");
   PMX_CHECK(o.pair_w >= 0 && o.pair_w <= 2, "pair_w must be 0, 1 or 2");
@@ -282,6 +287,10 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     tiles1w_.arith32 = tiles1_.arith32;
     tiles1_.lds_pad = pcg1_lds_pad(opt_.wpcu1, tiles1_.waves);
     tiles1w_.lds_pad = pcg1_lds_pad(opt_.wpcu1w, tiles1w_.waves);
+    // the LDS-DMA march: fp64 with the default shape only (VEC 2, 1 wave, register prefetch 1)
+    auto dma_ok = [&](const TileCfg& t) { return elem_ == 8 && t.vec == 2 && t.waves == 1 && t.pf == 1; };
+    if (dma_ok(tiles1_)) tiles1_.dpf = opt_.dma1;
+    if (dma_ok(tiles1w_)) tiles1w_.dpf = opt_.dma1w >= 0 ? opt_.dma1w : opt_.dma1;
     const bool same_w = tiles1w_.rows == tiles1_.rows;
     // dispatch order tables with the tiles' row classes; order1: the ellipse-cut tiles first
     // within each XCD's share (their 3-5x longer tiles would trail the sweep)
@@ -901,6 +910,14 @@ PcgState GpuSubdomainSolver::read_state(hipStream_t s) const {
   HIP_CHECK(hipMemcpyAsync(&host_state_[0], state_, sizeof(PcgState), hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
   return host_state_[0];
+}
+
+std::vector<double> GpuSubdomainSolver::read_partials(hipStream_t s) const {
+  HIP_CHECK(hipSetDevice(opt_.device));
+  std::vector<double> h(npart_ * 5);
+  HIP_CHECK(hipMemcpyAsync(h.data(), partials_, h.size() * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  return h;
 }
 
 std::vector<double> GpuSubdomainSolver::download_field(int which, hipStream_t s) const {

@@ -127,7 +127,7 @@ __host__ __device__ inline bool pcg1_tile(int k, const Pcg1Part& P, int tiles_j,
   return false;
 }
 
-template <typename T, typename C, int VEC, int WAVES, int PF, bool WS>
+template <typename T, typename C, int VEC, int WAVES, int PF, bool WS, int DPF = 0>
 __global__ void __launch_bounds__(64 * WAVES, (pcg1_min_waves<T, C, VEC, WAVES, PF, WS>()))
 k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
        double* __restrict__ partials, PcgState* S, int TI, int tiles_j, int ntiles, Pcg1Part part) {
@@ -183,6 +183,14 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
 #define PMX_MARCH(E, F)                                                                                       \
   pcg1_march<T, C, VEC, PF, E, F>(G, Tb, AF, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, acc, \
                                   scol, ocls, use_cls)
+  // LDS-DMA ring of the FAST march (pcg1_march's DPF mode): DPF slots of r, p (, w) rows per wave
+  constexpr int kRingDoubles = DPF > 0 ? DPF * (WS ? 3 : 2) * 128 : 2;
+  __shared__ double s_ring[WAVES * kRingDoubles];
+  double* dring = s_ring + __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)) * kRingDoubles;
+  (void)dring;
+#define PMX_MARCH_D(E)                                                                                            \
+  pcg1_march<T, C, VEC, PF, E, true, DPF>(G, Tb, AF, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, \
+                                          acc, scol, ocls, use_cls, dring)
 #define PMX_MARCH_W(F)                                     \
   if constexpr (!WS) {                                     \
     PMX_MARCH(0, F);                                       \
@@ -193,11 +201,24 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
       default: PMX_MARCH(3, F); break;                     \
     }                                                      \
   }
+  if constexpr (DPF > 0 && sizeof(T) == 8 && VEC == 2) {
+    if (fast && i1 - i0 + 1 >= DPF && (!WS || wm == 1 || wm == 2)) {
+      if constexpr (!WS) {
+        PMX_MARCH_D(0);
+      } else {
+        if (wm == 1) PMX_MARCH_D(1);
+        else PMX_MARCH_D(2);
+      }
+      goto marched;
+    }
+  }
   if (fast) {
     PMX_MARCH_W(true)
   } else {
     PMX_MARCH_W(false)
   }
+marched:
+#undef PMX_MARCH_D
 #undef PMX_MARCH_W
 #undef PMX_MARCH
   wave_sum2_mfma(acc[0], acc[1]);
@@ -531,14 +552,24 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
   PMX_CHECK(G.nb == 0 || (G.nx >= 2 && G.ny >= 2), "pcg1 on a decomposed grid needs subdomains >= 2 x 2");
   const int nb = (count + tc.waves - 1) / tc.waves;
   const int bs = 64 * tc.waves;
-#define PMX_PCG1_C(C, V, WV, PF)                                                                         \
+#define PMX_PCG1_CD(C, V, WV, PF, D)                                                                     \
   do {                                                                                                   \
     if (wsweep)                                                                                          \
-      hipLaunchKernelGGL((k_pcg1<T, C, V, WV, PF, true>), dim3(nb), dim3(bs), tc.lds_pad, s, G, Tb, w, r, r2, p0, \
-                         p1, partials, S, tc.rows, tc.tiles_j, tc.ntiles(), P);                          \
+      hipLaunchKernelGGL((k_pcg1<T, C, V, WV, PF, true, D>), dim3(nb), dim3(bs), tc.lds_pad, s, G, Tb, w, r, r2, \
+                         p0, p1, partials, S, tc.rows, tc.tiles_j, tc.ntiles(), P);                      \
     else                                                                                                 \
-      hipLaunchKernelGGL((k_pcg1<T, C, V, WV, PF, false>), dim3(nb), dim3(bs), tc.lds_pad, s, G, Tb, w, r, r2, p0, \
-                         p1, partials, S, tc.rows, tc.tiles_j, tc.ntiles(), P);                          \
+      hipLaunchKernelGGL((k_pcg1<T, C, V, WV, PF, false, D>), dim3(nb), dim3(bs), tc.lds_pad, s, G, Tb, w, r, r2, \
+                         p0, p1, partials, S, tc.rows, tc.tiles_j, tc.ntiles(), P);                      \
+  } while (0)
+  // the LDS-DMA march (tc.dpf rows ahead): fp64 storage and arithmetic, the default tile shape
+#define PMX_PCG1_C(C, V, WV, PF)                                                                         \
+  do {                                                                                                   \
+    if constexpr (sizeof(T) == 8 && std::is_same_v<C, double> && V == 2 && WV == 1 && PF == 1) {        \
+      if (tc.dpf == 2) { PMX_PCG1_CD(C, V, WV, PF, 2); break; }                                          \
+      if (tc.dpf == 3) { PMX_PCG1_CD(C, V, WV, PF, 3); break; }                                          \
+    }                                                                                                    \
+    PMX_CHECK(tc.dpf == 0, "pcg1: the LDS-DMA march needs fp64, VEC 2 x 1 wave, prefetch 1 and dpf 2 or 3"); \
+    PMX_PCG1_CD(C, V, WV, PF, 0);                                                                        \
   } while (0)
   // fp32 arithmetic: fp32 storage only, the default tile shape (VEC 2, 1 wave) and prefetch 1-3
 #define PMX_PCG1(V, WV, PF)                                                                              \
@@ -566,6 +597,7 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
 #endif
 #undef PMX_PCG1
 #undef PMX_PCG1_C
+#undef PMX_PCG1_CD
   HIP_CHECK(hipGetLastError());
 }
 

@@ -352,6 +352,24 @@ __device__ __forceinline__ bool static_for_while(F&& f) {
   return static_for_while_impl(f, std::make_integer_sequence<int, N>{});
 }
 
+// ---- LDS-DMA row prefetch (pcg1_march's DPF mode) ----
+// global_load_lds_dwordx4: 16 B per lane from base + voff into LDS at lds + 16 * lane, no VGPR
+// destination.  Inline asm on purpose: hipcc does not see the load, so it emits no wait for it --
+// the march counts vmcnt itself (wait_vmcnt), exactly, stores included.  M0 (the LDS base) is
+// saved and restored inside the statement (cdna_hip_programming.md: M0 is compiler-reserved).
+__device__ __forceinline__ void dma16(const void* base, unsigned voff, unsigned lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(base), "s"(lds)
+               : "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
 template <typename T, int VEC>
 struct Pcg1Row {
   T r[VEC], p[VEC], w[VEC], q[VEC];  // q: p^{k-2} (WM 3 only)
@@ -370,15 +388,26 @@ struct Pcg1Row {
 // The tile marches top-down, rows i0-2 .. i1+2.  (Bottom-up and alternating marches, super-row and
 // banded dispatch orders were tried to make vertically adjacent tiles share their halo rows in L2:
 // all slower, NOTES #30, #46-48.)
-template <typename T, typename C, int VEC, int PF, int WM, bool FAST>
+//
+// DPF > 0 (FAST tiles of fp64 storage, VEC 2, WM 0-2, at least DPF rows): the rows are prefetched
+// DPF ahead by LDS-DMA into a per-wave ring `dring` (DPF slots of r, p [, w] rows, 1 KiB each)
+// instead of registers.  Why: with compiler-visible loads the march waits, every row, for the
+// previous row's STORES -- the stores sit in a branch (owned rows only), so at the merge hipcc
+// cannot count them and its vmcnt wait for the prefetched row covers them too: a full store round
+// trip per row per wave (bench/probe/dma_march.hip, isa of k_reg).  Here hipcc sees no load at all
+// and the march waits with exact counts: the loop is split into 3 steps without stores, DPF ramp
+// steps and a steady loop whose every step stores, so each wait's number of younger operations
+// (later DMAs and stores) is a compile-time constant.  Same arithmetic, bit-identical fields.
+template <typename T, typename C, int VEC, int PF, int WM, bool FAST, int DPF = 0>
 __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb, const ArithF& F, T* __restrict__ w,
                                            const T* __restrict__ rold, T* __restrict__ rnew,
                                            const T* __restrict__ pold,
                                            T* pnew, int i0, int i1, int j0, int j1,
                                            double alpha_d, double beta_d, double c1_d, double c2_d,
                                            double (&acc)[kNq], double* __restrict__ scol,
-                                           unsigned long long cls, bool use_cls) {
+                                           unsigned long long cls, bool use_cls, double* dring = nullptr) {
   constexpr bool WUP = WM != 0;
+  static_assert(DPF == 0 || (FAST && VEC == 2 && sizeof(T) == 8 && WM <= 2), "LDS-DMA march: fp64 FAST tiles, WM 0-2");
   constexpr bool PK = std::is_same_v<C, float> && VEC == 2;  // packed fp32 stencils (apply_row)
   const C alpha = C(alpha_d), beta = C(beta_d), c1 = C(c1_d), c2 = C(c2_d);
   const int64_t P = G.pitch;
@@ -448,10 +477,8 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
   if (cB.ucls == 0) park_cols();
 
   const int mfirst = i0 - 2, mlast = i1 + 2;
-  auto step = [&](int m, const Pcg1Row<T, VEC>& cur, Pcg1Row<T, VEC>& nxt) {
-    // PF rows ahead, unconditional (a branch around loads forces vmcnt(0)); past the tile's last
-    // row re-read that row (a cache hit) instead of the next tile's rows
-    fetch(min(m + PF, mlast), nxt);
+  // one row step of the 3-stage pipeline on row m's loaded values
+  auto core = [&](int m, const Pcg1Row<T, VEC>& cur) {
     // ---- stage A: p^k of row m
     const bool rowA = FAST || interior_row(m);
     const RowCo cA = row_of(m);
@@ -572,19 +599,76 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
     cB = cA;
   };
 
-  // ring of PF + 1 row buffers, unrolled by its size so no buffer is ever copied: step m reads
-  // slot q and refills the slot step m - 1 consumed
-  Pcg1Row<T, VEC> buf[PF + 1];
+  if constexpr (DPF > 0) {
+    // ---- LDS-DMA ring (see the template comment).  Row mfirst + t sits in slot t % DPF.
+    constexpr int ND = WUP ? 3 : 2;  // DMAs per row: r, p (, w of the row above)
+    constexpr int NS = WUP ? 3 : 2;  // stores per storing step: r, p (, w)
+    const unsigned voff = unsigned(c0 + 2) * 8u;  // bytes from row - 2 (col_ptr's unsigned form)
+    const unsigned lds0 = unsigned(reinterpret_cast<uintptr_t>(dring));
+    auto dma_row = [&](int m, int slot) {
+      const unsigned l = lds0 + unsigned(slot) * (ND * 1024u);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's previous ds_reads have returned
+      dma16(rold + int64_t(m) * P - 2, voff, l);
+      dma16(pold + int64_t(m) * P - 2, voff, l + 1024u);
+      if constexpr (WUP) dma16(w + int64_t(m - 1) * P - 2, voff, l + 2048u);
+    };
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const int h = i1 - i0 + 1;  // rows stored: steps t = 3 .. h + 2 (the caller guarantees h >= DPF)
+    int slot = 0;
+    // step t: wait for its row (younger: the later rows' DMAs and KS steps' stores), read it from
+    // the ring, refill the slot DPF rows ahead (the last row again past the end: a cache hit), run
+    // the pipeline
+    auto dstep = [&](int t, auto ks) {
+      constexpr int KS = decltype(ks)::value;
+      wait_vmcnt<(DPF - 1) * ND + KS * NS>();
+      const double* sl = dring + slot * (ND * 128);
+      Pcg1Row<T, VEC> cur;
+      const d2 rv = *reinterpret_cast<const d2*>(sl + 2 * lane);
+      const d2 pv = *reinterpret_cast<const d2*>(sl + 128 + 2 * lane);
+      cur.r[0] = rv.x; cur.r[1] = rv.y;
+      cur.p[0] = pv.x; cur.p[1] = pv.y;
+      if constexpr (WUP) {
+        const d2 wv = *reinterpret_cast<const d2*>(sl + 256 + 2 * lane);
+        cur.w[0] = wv.x; cur.w[1] = wv.y;
+      }
+      dma_row(min(mfirst + t + DPF, mlast), slot);
+      slot = slot + 1 == DPF ? 0 : slot + 1;
+      core(mfirst + t, cur);
+    };
 #pragma unroll
-  for (int q = 0; q < PF; ++q) fetch(min(mfirst + q, mlast), buf[q]);
-  for (int m = mfirst; m <= mlast; m += PF + 1) {
+    for (int q = 0; q < DPF; ++q) dma_row(mfirst + q, q);
+    using K0 = std::integral_constant<int, 0>;
+    dstep(0, K0{});
+    dstep(1, K0{});
+    dstep(2, K0{});
+    // ramp: step 3 + K has the stores of K steps behind its row's DMA
+    static_for_while<DPF>([&](auto k) {
+      dstep(3 + decltype(k)::value, k);
+      return true;
+    });
+    for (int t = 3 + DPF; t <= h + 3; ++t) dstep(t, std::integral_constant<int, DPF>{});
+    wait_vmcnt<0>();  // no DMA may land after the wave has moved on (its LDS is the next tile's)
+  } else {
+    // ring of PF + 1 row buffers, unrolled by its size so no buffer is ever copied: step m reads
+    // slot q and refills the slot step m - 1 consumed
+    Pcg1Row<T, VEC> buf[PF + 1];
 #pragma unroll
-    for (int q = 0; q <= PF; ++q) {
-      if (m + q > mlast) goto done;
-      step(m + q, buf[q], buf[(q + PF) % (PF + 1)]);
+    for (int q = 0; q < PF; ++q) fetch(min(mfirst + q, mlast), buf[q]);
+    bool more = true;
+    for (int m = mfirst; more && m <= mlast; m += PF + 1) {
+#pragma unroll
+      for (int q = 0; q <= PF; ++q) {
+        if (m + q > mlast) {
+          more = false;
+          break;
+        }
+        // PF rows ahead, unconditional (a branch around loads forces vmcnt(0)); past the tile's
+        // last row re-read that row (a cache hit) instead of the next tile's rows
+        fetch(min(m + q + PF, mlast), buf[(q + PF) % (PF + 1)]);
+        core(m + q, buf[q]);
+      }
     }
   }
-done:
   if constexpr (FAST) {  // lanes 0 and 63 own no column
 #pragma unroll
     for (int q = 0; q < kNq; ++q) acc[q] = own_all ? acc[q] : 0.0;

@@ -271,6 +271,11 @@ std::vector<double> Session::local_w(int i) {
   return solvers_.at(size_t(i))->download_w(stream_of(i));
 }
 
+std::vector<double> Session::partials(int i) {
+  synchronize();
+  return solvers_.at(size_t(i))->read_partials(stream_of(i));
+}
+
 std::vector<double> Session::gather_local_w() {
   const int M = cfg_.spec.M, N = cfg_.spec.N;
   std::vector<double> g(size_t(M + 1) * (N + 1), 0.0);

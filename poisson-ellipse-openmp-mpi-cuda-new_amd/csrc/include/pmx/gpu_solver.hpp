@@ -111,6 +111,10 @@ struct GpuOptions {
   // in flight keep more DRAM rows open per access (bench/probe/dma_march.hip).
   // PMX_PCG1_WPCU / PMX_PCG1_WPCU_W override.
   int wpcu1 = 0, wpcu1w = 0;
+  // pcg1 march, interior (FAST) tiles in fp64: rows prefetched dma1 ahead by LDS-DMA into a per-wave
+  // LDS ring with exact vmcnt counting (2 or 3), 0 = register prefetch.  dma1w: the w sweep (-1 = as
+  // dma1).  PMX_PCG1_DMA / PMX_PCG1_DMA_W override.
+  int dma1 = 0, dma1w = -1;
   double placement_budget_s = 0.5;
   double placement_keep_free = 0.5;
   bool resolved = false;  // environment overrides already applied (resolve_options)
@@ -225,6 +229,7 @@ class GpuSubdomainSolver {
   void load_checkpoint(std::istream& is, hipStream_t s);
 
   PcgState read_state(hipStream_t s) const;  // synchronous D2H of the scalars
+  std::vector<double> read_partials(hipStream_t s) const;  // the partials buffer (5 per tile slot)
   // device-side error norms of the current w (pending steps applied); synchronous
   ErrorStats error_norms(hipStream_t s) const;
   // host-mapped progress counters (GpuOptions::progress): sweeps reduced, ghost exchanges packed,

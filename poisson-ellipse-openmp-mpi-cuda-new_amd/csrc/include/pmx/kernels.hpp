@@ -52,6 +52,7 @@ struct TileCfg {
   const Pcg1Slot* order2 = nullptr;  // the frame tiles
   int arith32 = 0;  // kind 3 with fp32 storage: 1 = fp32 stencil arithmetic (GpuOptions::arith32)
   int lds_pad = 0;  // kind 3: dynamic LDS bytes per workgroup that cap the resident waves per CU
+  int dpf = 0;      // kind 3: FAST tiles prefetch their rows dpf ahead by LDS-DMA (0 = registers)
   int interior_tiles() const { return (ti_hi - ti_lo) * (tj_hi - tj_lo); }
   int ntiles() const { return tiles_i * tiles_j; }
 };

@@ -87,6 +87,8 @@ class Session {
   std::vector<double> gather_local_w();
   // local interior (nx x ny, row-major) of owned subdomain i
   std::vector<double> local_w(int i = 0);
+  // the per-tile partial sums (5 per tile slot) the last sweep wrote (tests of the reduction hand-off)
+  std::vector<double> partials(int i = 0);
 
  private:
   void require_connected() const {

@@ -113,3 +113,33 @@ def test_block_and_march_share_the_control_logic(pkg, monkeypatch, grid):
             break
     if grid == (40, 40):
         assert sm["done"] and sm["status"] == "converged" and sm["iters"] == 50
+
+
+@pytest.mark.parametrize("grid,rows", [((800, 1200), 12), ((400, 600), 8), ((1200, 1800), 12)])
+def test_fused_block_reduction_handoff_stress(pkg, monkeypatch, grid, rows):
+    """The reduction folded into the block-tile sweep (every workgroup publishes its five partials
+    write-through and takes a ticket; the last one sums them all) runs with 2 workgroups per CU and
+    up to ~2,250 workgroups.  After every one of 300 sweeps the device's red_c must equal the
+    weighted, exactly rounded sum of the partials that sweep wrote: a stale partial (a hand-off that
+    missed one workgroup's stores) would be off by a whole tile's share, ~1/ntiles of the total."""
+    import math
+    monkeypatch.setenv("PMX_PCG1_BLOCK_FUSED", "1")
+    s = _sess(pkg, monkeypatch, *grid, rows, graph_batch=0)
+    assert s.tile.get("block_tiles")
+    ntiles = s.tile["tiles_i"] * s.tile["tiles_j"]
+    M, N = grid
+    h = (2.0 / M) * (1.2 / N)  # weighted norm: every sum carries h1 h2
+    s.init()
+    checked = 0
+    for _ in range(300):
+        s.step(1)
+        st = s.state(0)
+        if st["done"]:
+            break
+        P = s.partials(0)[:ntiles]
+        for q in range(5):
+            exact = math.fsum(P[:, q]) * h
+            scale = math.fsum(abs(x) for x in P[:, q]) * h
+            assert abs(st["red_c"][q] - exact) <= 1e-12 * scale, (checked, q, st["red_c"][q], exact)
+        checked += 1
+    assert checked >= 250

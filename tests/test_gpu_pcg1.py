@@ -322,3 +322,26 @@ def test_loopback_rank_runs_the_real_schedule(pkg, native, rank, split):
     s.synchronize()
     st = s.state(0)
     assert s.path_stats()["graph_iters"] == 48 and st["it"] - st0["it"] == 48 and not st["done"], st
+
+
+@pytest.mark.parametrize("dma", [2, 3])
+@pytest.mark.parametrize("grid,ranks", [((1600, 2400), 1), ((1000, 1400), 3), ((700, 900), 1)])
+def test_pcg1_lds_dma_march_bitwise(pkg, monkeypatch, dma, grid, ranks):
+    """The LDS-DMA march (interior tiles prefetch their rows through a per-wave LDS ring, exact vmcnt
+    counts; pcg1_march's DPF mode) computes the same values in the same order as the register
+    march: w, the sums and the iteration count are bitwise equal, plain and w sweeps alike (and the
+    reference's 1858 at 1600x2400 with the march forced instead of block tiles)."""
+    monkeypatch.setenv("PMX_PCG1_BLOCK", "0")
+    p = pkg.PoissonEllipse(M=grid[0], N=grid[1])
+    out = {}
+    for d in (0, dma):
+        monkeypatch.setenv("PMX_PCG1_DMA", str(d))
+        s = pkg.make_session(p, ranks=ranks, graph_batch=16)
+        assert s.tile.get("dpf", 0) == d
+        r = s.solve(1)
+        out[d] = (r["iters"], s.gather_local_w(), s.state(0)["red_c"])
+    assert out[0][0] == out[dma][0]
+    assert np.array_equal(out[0][1], out[dma][1])
+    assert out[0][2] == out[dma][2]
+    if grid == (1600, 2400):
+        assert out[dma][0] == 1858
