@@ -1026,6 +1026,16 @@ STUDIES["r5c"] = [
 ]
 
 
+STUDIES["r5e"] = [
+    ("tests_loop", 600, f"{PYTEST} tests/test_gpu_block.py -k 'looping or goldens'"),
+    ("ab_loop", 600, "python -u bench/ab_env.py --shape 800x1200 --shape 1200x1800 --shape 1600x2400 "
+                     "--shape 2400x3200 --rounds 3 --iters 600 --warmup 50 --cfg base: --cfg b0:PMX_PCG1_BLOCK=1 "
+                     "--cfg l1:PMX_PCG1_BLOCK=1,PMX_PCG1_BLOCK_LOOP=1 --cfg l2:PMX_PCG1_BLOCK=1,PMX_PCG1_BLOCK_LOOP=2 "
+                     "--cfg l2f:PMX_PCG1_BLOCK=1,PMX_PCG1_BLOCK_LOOP=2,PMX_PCG1_BLOCK_FUSED=1 "
+                     "--cfg l3:PMX_PCG1_BLOCK=1,PMX_PCG1_BLOCK_LOOP=3"),
+]
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("study", choices=sorted(STUDIES) + sorted(PARAMETRISED))

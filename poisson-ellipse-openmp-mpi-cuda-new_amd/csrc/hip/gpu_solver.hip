@@ -103,6 +103,15 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_PLACEMENT", o.placement);
   env_int("PMX_PCG1_WPCU", o.wpcu1);
   env_int("PMX_PCG1_WPCU_W", o.wpcu1w);
+  env_int("PMX_PCG1_BLOCK", o.block1);
+  env_int("PMX_PCG1_BLOCK_ROWS", o.block_rows1);
+  env_int("PMX_PCG1_BLOCK_WAVES", o.block_waves1);
+  env_int("PMX_PCG1_BLOCK_FUSED", o.block_fused1);
+  PMX_CHECK(o.block1 >= -1 && o.block1 <= 1, "block tiles must be -1 (auto), 0 or 1");
+  PMX_CHECK(o.block_rows1 == 0 || pcg1_block_shape_ok(o.block_rows1, o.block_waves1),
+            "block tiles: no " << o.block_rows1 << "-row x " << o.block_waves1 << "-wave variant (4/8/12/16 x 8, 8/16 x 16)");
+  PMX_CHECK(o.block_waves1 == 8 || o.block_waves1 == 16, "block tiles: 8 or 16 waves per workgroup");
+  PMX_CHECK(o.block_fused1 >= -1 && o.block_fused1 <= 1, "block-tile fused reduction must be -1 (auto), 0 or 1");
   env_int("PMX_PCG1_DMA", o.dma1);
   env_int("PMX_PCG1_DMA_W", o.dma1w);
   PMX_CHECK(o.dma1 == 0 || o.dma1 == 2 || o.dma1 == 3, "pcg1 LDS-DMA prefetch depth must be 0, 2 or 3");
@@ -253,20 +262,19 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     // (400x600 17.3 vs 37.1), T4 < 10000 12-row tiles (800x1200 23.9 vs 42.0, 1200x1800 39.1 vs
     // 54.1, 1600x2400 59.9 vs 61.2); above, the march (2000x3000 85.7 vs 76.1).  PMX_PCG1_BLOCK=0/1
     // forces it, PMX_PCG1_BLOCK_ROWS=4|8|12|16 and PMX_PCG1_BLOCK_WAVES=8|16 pick the shape.
-    int blk = opt_.block1;
-    if (const char* e = std::getenv("PMX_PCG1_BLOCK"); e && e[0]) blk = std::atoi(e);
+    const int blk = opt_.block1;
     const int64_t t4 = int64_t((G.nx + 3) / 4) * ((G.ny + 123) / 124);
     if (G.nb == 0 && elem_ == 8 && (blk == 1 || (blk == -1 && t4 < 10000))) {
-      int rows = t4 < 1000 ? 8 : 12;
-      if (const char* er = std::getenv("PMX_PCG1_BLOCK_ROWS"); er && er[0]) rows = std::atoi(er);
+      const int rows = opt_.block_rows1 ? opt_.block_rows1 : t4 < 1000 ? 8 : 12;
+      PMX_CHECK(pcg1_block_shape_ok(rows, opt_.block_waves1),
+                "block tiles: no " << rows << "-row x " << opt_.block_waves1 << "-wave variant");
       block1_ = true;
       // the reduction folded into the sweep costs every workgroup a drain of its stores and a ticket
       // round trip while it holds its LDS: cheaper than a k_reduce_n launch when the tiles run in
       // about one round (400x600 16.8 vs 18.3 us, 800x1200 23.3 vs 24.6), dearer over several
       // (1200x1800 37.5 vs 37.2, 1600x2400 57.3 vs 54.9; study r4ap).  PMX_PCG1_BLOCK_FUSED=0/1 forces it.
       const int64_t nblk = int64_t((G.nx + rows - 1) / rows) * ((G.ny + 123) / 124);
-      const char* ef = std::getenv("PMX_PCG1_BLOCK_FUSED");
-      block_fused_ = ef && ef[0] ? ef[0] != '0' : nblk < 1500;
+      block_fused_ = opt_.block_fused1 >= 0 ? opt_.block_fused1 == 1 : nblk < 1500;
       opt_.rows1 = rows;
       opt_.rows1w = rows;
       opt_.vec1 = 2;
@@ -287,6 +295,7 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     tiles1w_.arith32 = tiles1_.arith32;
     tiles1_.lds_pad = pcg1_lds_pad(opt_.wpcu1, tiles1_.waves);
     tiles1w_.lds_pad = pcg1_lds_pad(opt_.wpcu1w, tiles1w_.waves);
+    if (block1_) tiles1_.bwaves = tiles1w_.bwaves = opt_.block_waves1;
     // the LDS-DMA march: fp64 with the default shape only (VEC 2, 1 wave, register prefetch 1)
     auto dma_ok = [&](const TileCfg& t) { return elem_ == 8 && t.vec == 2 && t.waves == 1 && t.pf == 1; };
     if (dma_ok(tiles1_)) tiles1_.dpf = opt_.dma1;

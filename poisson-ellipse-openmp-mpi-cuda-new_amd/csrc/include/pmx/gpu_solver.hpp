@@ -106,6 +106,10 @@ struct GpuOptions {
   // than 10,000 four-row march tiles, ~1600x2400), 0 = off, 1 = on for any undecomposed fp64 grid.
   // PMX_PCG1_BLOCK overrides.
   int block1 = -1;
+  // block-tile shape and reduction: rows per tile (0 = auto: 8 below 1,000 four-row tiles, else 12),
+  // waves per workgroup (8 or 16), the reduction folded into the sweep (-1 = auto: below 1,500
+  // tiles).  PMX_PCG1_BLOCK_ROWS / _WAVES / _FUSED.
+  int block_rows1 = 0, block_waves1 = 8, block_fused1 = -1;
   // pcg1 march sweeps: resident waves per CU (0 = as many as the registers allow: 16 for the plain
   // sweep, 12 for the w sweep).  A cap is enforced with padding LDS per workgroup.  Fewer streams
   // in flight keep more DRAM rows open per access (bench/probe/dma_march.hip).

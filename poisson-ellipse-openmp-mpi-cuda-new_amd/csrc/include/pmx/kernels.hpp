@@ -53,6 +53,7 @@ struct TileCfg {
   int arith32 = 0;  // kind 3 with fp32 storage: 1 = fp32 stencil arithmetic (GpuOptions::arith32)
   int lds_pad = 0;  // kind 3: dynamic LDS bytes per workgroup that cap the resident waves per CU
   int dpf = 0;      // kind 3: FAST tiles prefetch their rows dpf ahead by LDS-DMA (0 = registers)
+  int bwaves = 8;   // kind 3 block tiles (pcg1_block.hip): waves per workgroup
   int interior_tiles() const { return (ti_hi - ti_lo) * (tj_hi - tj_lo); }
   int ntiles() const { return tiles_i * tiles_j; }
 };
@@ -125,9 +126,9 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
                  bool wsweep = false);
 
 // pcg1 sweep with block tiles (pcg1_block.hip): one workgroup per tc.rows x 124 tile, the three
-// pipeline stages row-parallel; undecomposed fp64 grids; partial sums per tile as k_pcg1.  With a
-// ticket the sweep also finishes the reduction (red_c = sums * weights, S->it + 1, progress[0]),
-// replacing launch_reduce_n.
+// pipeline stages row-parallel; undecomposed fp64 grids; partial sums per tile as k_pcg1.  With a ticket the sweep also finishes the reduction (red_c =
+// sums * weights, S->it + 1, progress[0]), replacing launch_reduce_n.
+bool pcg1_block_shape_ok(int rows, int waves);  // an instantiated (rows, waves per workgroup) variant
 template <typename T>
 void launch_pcg1_block(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1, double* partials,
                        PcgState* S, const TileCfg& tc, hipStream_t s, bool wsweep, const double* weights = nullptr,
