@@ -1036,6 +1036,40 @@ STUDIES["r5e"] = [
 ]
 
 
+STUDIES["r5f"] = [
+    ("tests_lock", 600, f"{PYTEST} tests/test_gpu_pcg1.py -k 'lockstep or goldens'"),
+    ("ab_lock", 900, _AB5 + "--shape 2048x16384 --cfg base: --cfg w8:PMX_PCG1_WAVES=8 "
+                     "--cfg w8w8:PMX_PCG1_WAVES=8,PMX_PCG1_WAVES_W=8 --cfg w4:PMX_PCG1_WAVES=4 "
+                     "--cfg w8r4:PMX_PCG1_WAVES=8,PMX_PCG1_ROWS=4 --cfg w8r12:PMX_PCG1_WAVES=8,PMX_PCG1_ROWS=12"),
+]
+
+
+STUDIES["r5g"] = [
+    ("ab_lock2", 900, _AB5 + "--cfg base: --cfg w4r12:PMX_PCG1_WAVES=4,PMX_PCG1_ROWS=12 "
+                      "--cfg w8r16:PMX_PCG1_WAVES=8,PMX_PCG1_ROWS=16 --cfg w4r16:PMX_PCG1_WAVES=4,PMX_PCG1_ROWS=16 "
+                      "--cfg r12:PMX_PCG1_ROWS=12"),
+]
+
+
+STUDIES["r5h"] = [
+    ("ab_rows", 1100, "python -u bench/ab_env.py --fresh --shape 16384x16384 --rounds 3 --iters 200 "
+                      "--cfg base: --cfg r12:PMX_PCG1_ROWS=12 --cfg w4r12:PMX_PCG1_WAVES=4,PMX_PCG1_ROWS=12 "
+                      "--cfg w4r12w1:PMX_PCG1_WAVES=4,PMX_PCG1_ROWS=12,PMX_PCG1_WAVES_W=1 "
+                      "--cfg w4r10:PMX_PCG1_WAVES=4,PMX_PCG1_ROWS=10 --cfg w4r14:PMX_PCG1_WAVES=4,PMX_PCG1_ROWS=14 "
+                      "--cfg r14:PMX_PCG1_ROWS=14"),
+]
+
+
+STUDIES["r5i"] = [
+    ("ab_rows_probe", 1100, "python -u bench/ab_env.py --fresh --shape 16384x16384 --shape 2048x16384 --rounds 2 "
+                            "--iters 200 --cfg base:PMX_PLACEMENT=20 --cfg r12:PMX_PLACEMENT=20,PMX_PCG1_ROWS=12 "
+                            "--cfg w4r12:PMX_PLACEMENT=20,PMX_PCG1_WAVES=4,PMX_PCG1_ROWS=12 "
+                            "--cfg w4r14:PMX_PLACEMENT=20,PMX_PCG1_WAVES=4,PMX_PCG1_ROWS=14"),
+    ("bench_w4r12", 300, "env PMX_PCG1_WAVES=4 PMX_PCG1_ROWS=12 " + bench("--gpus 1 --steps 20 --warmup 5")),
+    ("bench_base", 300, bench("--gpus 1 --steps 20 --warmup 5")),
+]
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("study", choices=sorted(STUDIES) + sorted(PARAMETRISED))

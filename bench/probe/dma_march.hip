@@ -215,6 +215,54 @@ __global__ void __launch_bounds__(64) k_regp(Geo g, const double* __restrict__ r
   if (acc == 12345.678) sink[0] = acc + cap[0];
 }
 
+// NW waves per workgroup march NW side-by-side column tiles of one tile row in lockstep (an
+// s_barrier per row step): each row step of the workgroup reads NW KiB contiguous per field.
+template <int NW, int WORK>
+__global__ void __launch_bounds__(64 * NW) k_lock(Geo g, const double* __restrict__ r, const double* __restrict__ p,
+                                                 double* __restrict__ rn, double* __restrict__ pn, double a,
+                                                 double* sink) {
+  extern __shared__ double cap[];
+  const int wid = int(threadIdx.x >> 6);
+  const int gtj = (g.tiles_j + NW - 1) / NW;  // workgroup tiles per tile row
+  const int id = g.order == 0 ? xcd_remap(blockIdx.x, gridDim.x) : int(blockIdx.x);
+  const int ti = id / gtj, tjg = id - ti * gtj;
+  const int tj = min(tjg * NW + wid, g.tiles_j - 1);
+  const int i0 = 2 + ti * g.TI, i1 = min(i0 + g.TI - 1, g.n - 3);
+  const int lane = threadIdx.x & 63;
+  const int c0 = tj * 124 + 2 * lane;
+  const bool own = lane >= 1 && lane <= 62 && c0 + 1 < g.n && tjg * NW + wid < g.tiles_j;
+  const int mfirst = i0 - 2, mlast = i1 + 2;
+  double2 br[2], bp[2];
+  auto fetch = [&](int m, double2& x, double2& y) {
+    m = min(m, mlast);
+    x = *reinterpret_cast<const double2*>(r + size_t(m) * g.pitch + c0);
+    y = *reinterpret_cast<const double2*>(p + size_t(m) * g.pitch + c0);
+  };
+  fetch(mfirst, br[0], bp[0]);
+  double acc = 0.0;
+  double x[2] = {0, 0}, y[2] = {0, 0};
+  for (int m = mfirst; m <= mlast; m += 2) {
+#pragma unroll
+    for (int q = 0; q <= 1; ++q) {
+      const int mm = m + q;
+      if (mm > mlast) goto done;
+      fetch(mm + 1, br[q ^ 1], bp[q ^ 1]);
+      x[0] += br[q].x; x[1] += br[q].y; y[0] += bp[q].x; y[1] += bp[q].y;
+      work<WORK>(x, y, a);
+      x[0] += shl(y[1]);
+      if (mm - 1 >= i0 && mm - 1 <= i1 && own) {
+        const size_t o = size_t(mm - 1) * g.pitch + c0;
+        __builtin_nontemporal_store((d2v){x[0], x[1]}, reinterpret_cast<d2v*>(rn + o));
+        __builtin_nontemporal_store((d2v){y[0], y[1]}, reinterpret_cast<d2v*>(pn + o));
+      }
+      acc += x[0] * y[1];
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+done:
+  if (acc == 12345.678) sink[0] = acc + cap[0];
+}
+
 // one field only (r read, rn written): half the concurrent streams of k_reg
 template <int WORK>
 __global__ void __launch_bounds__(64) k_one(Geo g, const double* __restrict__ r, const double* __restrict__ p,
@@ -349,19 +397,24 @@ int main(int argc, char** argv) {
     int pf, dma;
   };
   const V vars[] = {
-      {"reg1", k_reg<1, 6>, 1, 0}, {"reg1w", k_reg<1, 30>, 1, 0},
+      {"reg1", k_reg<1, 6>, 1, 0}, {"lock2", k_lock<2, 6>, 1, 2}, {"lock4", k_lock<4, 6>, 1, 4},
+      {"lock8", k_lock<8, 6>, 1, 8},
   };
-  const int tis[] = {4, 6, 8};
+  const int tis[] = {4, 8};
   const int wpcu[] = {8, 12, 16};
   printf("n=%d pitch=%d candidates=%d reps=%d (ms per sweep; GB/s at 32 B/pt)\n", n, pitch, ncand, reps);
-  for (int order = 0; order <= 1; ++order)
+  for (int order = 0; order <= 0; ++order)
   for (int TI : tis) {
     Geo g{n, pitch, TI, (n - 4 + TI - 1) / TI, (n - 4 + 123) / 124, 1, order};
-    const int nb = g.tiles_i * g.tiles_j;
     for (int wc : wpcu) {
       for (const V& v : vars) {
-        const size_t ring = v.dma ? size_t(v.pf) * 2048 : 0;
-        const size_t lds = std::max(ring, size_t(163840 / wc) & ~size_t(255));
+        // lock variants: v.dma = waves per workgroup (side-by-side column tiles)
+        const bool lock = v.name[0] == 'l';
+        const int nw = lock ? v.dma : 1;
+        const int nb = lock ? g.tiles_i * ((g.tiles_j + nw - 1) / nw) : g.tiles_i * g.tiles_j;
+        const int bs = 64 * nw;
+        const size_t ring = (v.dma && !lock) ? size_t(v.pf) * 2048 : 0;
+        const size_t lds = std::min(size_t(163840), std::max(ring, (size_t(163840 / wc) * nw) & ~size_t(255)));
         CK(hipFuncSetAttribute(reinterpret_cast<const void*>(v.k), hipFuncAttributeMaxDynamicSharedMemorySize,
                                int(lds)));
         printf("order=%d TI=%2d waves/CU=%2d %-5s:", order, TI, wc, v.name);
@@ -369,13 +422,13 @@ int main(int argc, char** argv) {
         for (int c = 0; c < ncand; ++c) {
           double* b = blocks[c];
           double *r = b, *p = b + fb / 8, *rn = b + 2 * (fb / 8), *pn = b + 3 * (fb / 8);
-          hipLaunchKernelGGL(v.k, dim3(nb), dim3(64), lds, 0, g, r, p, rn, pn, 1e-3, sink);
+          hipLaunchKernelGGL(v.k, dim3(nb), dim3(bs), lds, 0, g, r, p, rn, pn, 1e-3, sink);
           CK(hipEventRecord(e0));
           for (int k = 0; k < reps; ++k) {
             if (k & 1)
-              hipLaunchKernelGGL(v.k, dim3(nb), dim3(64), lds, 0, g, rn, pn, r, p, 1e-3, sink);
+              hipLaunchKernelGGL(v.k, dim3(nb), dim3(bs), lds, 0, g, rn, pn, r, p, 1e-3, sink);
             else
-              hipLaunchKernelGGL(v.k, dim3(nb), dim3(64), lds, 0, g, r, p, rn, pn, 1e-3, sink);
+              hipLaunchKernelGGL(v.k, dim3(nb), dim3(bs), lds, 0, g, r, p, rn, pn, 1e-3, sink);
           }
           CK(hipEventRecord(e1));
           CK(hipEventSynchronize(e1));

@@ -95,6 +95,7 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_PCG1_ROWS_W", o.rows1w);
   env_int("PMX_PCG1_PF_W", o.pf1w);
   env_int("PMX_PCG1_WAVES", o.waves1);
+  env_int("PMX_PCG1_WAVES_W", o.waves1w);
   env_int("PMX_PCG1_PF", o.pf1);
   env_int("PMX_PCG1_ORDER", o.order1);
   env_int("PMX_PCG1_WCYCLE", o.wcycle1);
@@ -279,6 +280,7 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
       opt_.rows1w = rows;
       opt_.vec1 = 2;
       opt_.waves1 = 1;
+      opt_.waves1w = 1;
       opt_.pf1 = opt_.pf1w = 1;
     }
     tiles1_ = make_pcg1_tiles(G, opt_.vec1, opt_.waves1, opt_.rows1, opt_.pf1, int(elem_));
@@ -290,7 +292,8 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
 #endif
     r2_ = field_raw(4);
     tiles1_.arith32 = elem_ == 4 && opt_.arith32 ? 1 : 0;
-    tiles1w_ = make_pcg1_tiles(G, opt_.vec1, opt_.waves1, opt_.rows1w ? opt_.rows1w : tiles1_.rows,
+    const int waves_w = opt_.waves1w ? opt_.waves1w : (opt_.waves1 == 8 ? 4 : opt_.waves1);
+    tiles1w_ = make_pcg1_tiles(G, opt_.vec1, waves_w, opt_.rows1w ? opt_.rows1w : tiles1_.rows,
                                opt_.pf1w ? opt_.pf1w : tiles1_.pf, int(elem_));
     tiles1w_.arith32 = tiles1_.arith32;
     tiles1_.lds_pad = pcg1_lds_pad(opt_.wpcu1, tiles1_.waves);
@@ -300,17 +303,18 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     auto dma_ok = [&](const TileCfg& t) { return elem_ == 8 && t.vec == 2 && t.waves == 1 && t.pf == 1; };
     if (dma_ok(tiles1_)) tiles1_.dpf = opt_.dma1;
     if (dma_ok(tiles1w_)) tiles1w_.dpf = opt_.dma1w >= 0 ? opt_.dma1w : opt_.dma1;
-    const bool same_w = tiles1w_.rows == tiles1_.rows;
+    const bool same_w = tiles1w_.rows == tiles1_.rows && tiles1w_.waves == tiles1_.waves;
     // dispatch order tables with the tiles' row classes; order1: the ellipse-cut tiles first
     // within each XCD's share (their 3-5x longer tiles would trail the sweep)
-    HIP_CHECK(hipMalloc(&tile_order_, 3 * size_t(tiles1_.ntiles()) * sizeof(Pcg1Slot)));
+    HIP_CHECK(hipMalloc(&tile_order_, pcg1_order_slots(tiles1_) * sizeof(Pcg1Slot)));
     slow_tiles_ = pcg1_build_order(G, tables_, tiles1_, tile_order_, opt_.order1 != 0, nullptr);
     if (same_w) {
       tiles1w_.order0 = tiles1_.order0;
       tiles1w_.order1 = tiles1_.order1;
       tiles1w_.order2 = tiles1_.order2;
+      for (int q = 0; q < 3; ++q) tiles1w_.groups[q] = tiles1_.groups[q];
     } else {
-      HIP_CHECK(hipMalloc(&tile_order_w_, 3 * size_t(tiles1w_.ntiles()) * sizeof(Pcg1Slot)));
+      HIP_CHECK(hipMalloc(&tile_order_w_, pcg1_order_slots(tiles1w_) * sizeof(Pcg1Slot)));
       (void)pcg1_build_order(G, tables_, tiles1w_, tile_order_w_, opt_.order1 != 0, nullptr);
     }
   }

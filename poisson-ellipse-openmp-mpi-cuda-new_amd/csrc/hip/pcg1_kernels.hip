@@ -84,6 +84,10 @@ __device__ long long g_wtrace_it = -1;
 //    allocator picks at the 4-wave bound of the plain sweep (see kPcg1F32Waves).
 template <typename T, typename C, int VEC, int WAVES, int PF, bool WS>
 constexpr int pcg1_min_waves() {
+  // lockstep workgroups (WAVES 4 / 8, fp64, prefetch 1): the plain sweep at 4 waves per SIMD (2
+  // eight-wave or 4 four-wave workgroups per CU), the w sweep at 3 with four-wave workgroups
+  if (VEC == 2 && (WAVES == 4 || WAVES == 8) && PF == 1 && std::is_same_v<C, double>)
+    return WS ? (WAVES == 4 ? 3 : 2) : 4;
   if (VEC != 2 || WAVES != 1) return 1;
   if (std::is_same_v<C, float>) return WS ? kPcg1F32WavesW : kPcg1F32Waves;
   if (!WS && (PF == 1 || (sizeof(T) == 4 && PF <= 3) || (sizeof(T) == 8 && PF == 2))) return 4;
@@ -154,7 +158,7 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
   const int wm = sw.wm;
   int ti = 0, tj = 0;
   if (part.order) {  // slow (ellipse-cut) tiles first, so they do not trail the sweep
-    if (pos >= part.count) return;
+    if (pos >= part.count || ord < 0) return;  // ord -1: an unused slot of a lockstep group
     ti = ord / tiles_j;
     tj = ord - ti * tiles_j;
   } else if (!pcg1_tile(pos, part, tiles_j, ti, tj)) {
@@ -181,8 +185,8 @@ k_pcg1(DevGeom G, DevTables Tb, T* __restrict__ w, T* r, T* r2, T* p0, T* p1,
   const bool use_cls = part.order != nullptr && TI + 5 <= 64 / 2;  // 2 bits for each of the TI+5 rows
   const ArithF AF{float(G.cx), float(G.cy), float(G.dinv_in), float(G.dinv_out), float(G.inv_eps)};
 #define PMX_MARCH(E, F)                                                                                       \
-  pcg1_march<T, C, VEC, PF, E, F>(G, Tb, AF, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, c1, c2, acc, \
-                                  scol, ocls, use_cls)
+  pcg1_march<T, C, VEC, PF, E, F, 0, (WAVES > 1)>(G, Tb, AF, w, rold, rnew, pold, pnew, i0, i1, j0, j1, alpha, beta, \
+                                                c1, c2, acc, scol, ocls, use_cls)
   // LDS-DMA ring of the FAST march (pcg1_march's DPF mode): DPF slots of r, p (, w) rows per wave
   constexpr int kRingDoubles = DPF > 0 ? DPF * (WS ? 3 : 2) * 128 : 2;
   __shared__ double s_ring[WAVES * kRingDoubles];
@@ -429,11 +433,19 @@ __global__ void k_pcg1_tile_classes(DevGeom G, DevTables Tb, int TI, int tiles_i
 
 }  // namespace
 
+size_t pcg1_order_slots(const TileCfg& tc) {
+  // one group per tc.waves tiles of a tile row at most: per part ntiles + tiles_i * (waves - 1) slots
+  const size_t per = size_t(tc.ntiles()) + size_t(tc.tiles_i + 2) * size_t(tc.waves);
+  return 3 * per;
+}
+
 int pcg1_build_order(const DevGeom& G, const DevTables& Tb, TileCfg& tc, Pcg1Slot* d_order, bool slow_first,
                      hipStream_t s) {
   tc.order0 = tc.order1 = tc.order2 = nullptr;
+  tc.groups[0] = tc.groups[1] = tc.groups[2] = 0;
   const int n = tc.ntiles();
-  if (tc.waves != 1 || n == 0) return 0;
+  if (n == 0) return 0;
+  const int gw = tc.waves;  // slots per group (1: every tile its own workgroup)
   unsigned char* d_cut = nullptr;
   unsigned long long* d_cls = nullptr;
   HIP_CHECK(hipMalloc(&d_cut, size_t(n)));
@@ -448,30 +460,44 @@ int pcg1_build_order(const DevGeom& G, const DevTables& Tb, TileCfg& tc, Pcg1Slo
   HIP_CHECK(hipStreamSynchronize(s));
   HIP_CHECK(hipFree(d_cut));
   HIP_CHECK(hipFree(d_cls));
-  std::vector<Pcg1Slot> order(3 * size_t(n), Pcg1Slot{0, 0, 0ull});
+  const size_t per = pcg1_order_slots(tc) / 3;
+  std::vector<Pcg1Slot> order(3 * per, Pcg1Slot{-1, 0, 0ull});
   int nslow = 0;
   for (int part = 0; part <= 2; ++part) {
     const Pcg1Part P{part, tc.tiles_i, tc.ti_lo, tc.ti_hi, tc.tj_lo, tc.tj_hi, nullptr, 0};
     const int count = part == 0 ? n : part == 1 ? tc.interior_tiles() : n - tc.interior_tiles();
-    Pcg1Slot* o = order.data() + size_t(part) * n;
-    // positions of XCD x (xcd_remap with one wave per workgroup): [x (q+1), ...) as in xcd_remap
-    const int q = count / 8, r = count % 8;
-    std::vector<int> ids;
+    // groups: runs of up to gw consecutive tiles of the part's enumeration within one tile row
+    std::vector<std::vector<int>> groups;
+    for (int k = 0, last_ti = -1; k < count; ++k) {
+      int ti = 0, tj = 0;
+      PMX_CHECK(pcg1_tile(k, P, tc.tiles_j, ti, tj), "pcg1_build_order: tile enumeration");
+      if (groups.empty() || ti != last_ti || int(groups.back().size()) == gw) groups.emplace_back();
+      groups.back().push_back(ti * tc.tiles_j + tj);
+      last_ti = ti;
+    }
+    const int ng = int(groups.size());
+    PMX_CHECK(size_t(ng) * size_t(gw) <= per, "pcg1_build_order: order capacity");
+    tc.groups[part] = gw > 1 ? ng : 0;
+    Pcg1Slot* o = order.data() + size_t(part) * per;
+    auto has_cut = [&](const std::vector<int>& g) {
+      for (int id : g)
+        if (cut[size_t(id)]) return true;
+      return false;
+    };
+    // the groups of XCD x (xcd_remap over ng workgroups): [x (q+1), ...) as in xcd_remap
+    const int q = ng / 8, r = ng % 8;
     for (int x = 0, start = 0; x < 8; ++x) {
       const int len = q + (x < r ? 1 : 0);
-      // this XCD's tiles (a band of tile rows), row-major
-      ids.clear();
-      for (int k = start; k < start + len; ++k) {
-        int ti = 0, tj = 0;
-        PMX_CHECK(pcg1_tile(k, P, tc.tiles_j, ti, tj), "pcg1_build_order: tile enumeration");
-        ids.push_back(ti * tc.tiles_j + tj);
-      }
       int w = start;
-      for (int pass = 0; pass < (slow_first ? 2 : 1); ++pass)  // slow tiles first, then the rest
-        for (int id : ids)
-          if (!slow_first || (cut[size_t(id)] != 0) == (pass == 0)) {
-            o[w++] = Pcg1Slot{id, 0, cls[size_t(id)]};
-            if (slow_first && pass == 0 && part == 0) ++nslow;
+      for (int pass = 0; pass < (slow_first ? 2 : 1); ++pass)  // slow groups first, then the rest
+        for (int g = start; g < start + len; ++g)
+          if (!slow_first || has_cut(groups[size_t(g)]) == (pass == 0)) {
+            for (size_t u = 0; u < groups[size_t(g)].size(); ++u) {
+              const int id = groups[size_t(g)][u];
+              o[size_t(w) * gw + u] = Pcg1Slot{id, 0, cls[size_t(id)]};
+              if (slow_first && pass == 0 && part == 0 && cut[size_t(id)]) ++nslow;
+            }
+            ++w;
           }
       start += len;
     }
@@ -479,8 +505,8 @@ int pcg1_build_order(const DevGeom& G, const DevTables& Tb, TileCfg& tc, Pcg1Slo
   HIP_CHECK(hipMemcpyAsync(d_order, order.data(), order.size() * sizeof(Pcg1Slot), hipMemcpyHostToDevice, s));
   HIP_CHECK(hipStreamSynchronize(s));
   tc.order0 = d_order;
-  tc.order1 = d_order + n;
-  tc.order2 = d_order + 2 * size_t(n);
+  tc.order1 = d_order + per;
+  tc.order2 = d_order + 2 * per;
   return nslow;
 }
 
@@ -488,7 +514,7 @@ TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf, 
   PMX_CHECK(vec == 2 || vec == 4, "pcg1: vec must be 2 or 4");
   PMX_CHECK(pf >= 0 && pf <= 4, "pcg1: prefetch depth must be 0 (auto) or 1..4");
   PMX_CHECK(pf <= 1 || (vec == 2 && waves == 1), "pcg1: prefetch depth > 1 needs vec 2 x 1 wave");
-  PMX_CHECK(waves == 1 || waves == 2 || waves == 4, "pcg1: waves must be 1, 2 or 4");
+  PMX_CHECK(waves == 1 || waves == 2 || waves == 4 || waves == 8, "pcg1: waves must be 1, 2, 4 or 8");
   PMX_CHECK(vec == 2 || waves == 1, "pcg1: VEC 4 runs 1 wave per workgroup");
   TileCfg t;
   t.kind = 3;
@@ -510,6 +536,10 @@ TileCfg make_pcg1_tiles(const DevGeom& G, int vec, int waves, int rows, int pf, 
     // keep fewer DRAM rows in flight and win despite the 4 extra marched rows.
     rows = fp32 ? 24 : 8;
     while (rows > 4 && int64_t((G.nx + rows - 1) / rows) * t.tiles_j < 8192) rows /= 2;
+    // (round 5) fp64 grids with >= 16K twelve-row tiles: 12 rows.  Fresh-process A/B, 3 rounds:
+    // 16384^2 2093.8 -> 2060.7 us (-1.6%) without the probe, 1939.3 -> 1903.5 (-1.8%) with it;
+    // 2048x16384 (the 8-GPU strip) 261.6 either way (studies r5h, r5i; NOTES #101)
+    if (!fp32 && int64_t((G.nx + 11) / 12) * t.tiles_j >= 16384) rows = 12;
     // the reference's smallest grid (800x1200: 2000 tiles of 4 rows, ~2 waves per SIMD) is bound by
     // one wave's serial row march: 2-row tiles double the waves and cut the march from 8 row steps
     // to 6 -- 50.1 -> 41.6 us/iteration; 1 row (5 steps, 4x the rows marched) 47.1; at 1600x2400
@@ -545,12 +575,16 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
                  double* partials, PcgState* S, const TileCfg& tc, hipStream_t s, int part, bool wsweep) {
   PMX_CHECK(tc.kind == 3, "launch_pcg1 needs make_pcg1_tiles");
   PMX_CHECK(part >= 0 && part <= 2, "launch_pcg1: part must be 0, 1 or 2");
-  const int count = part == 0 ? tc.ntiles() : part == 1 ? tc.interior_tiles() : tc.ntiles() - tc.interior_tiles();
-  const Pcg1Part P{part, tc.tiles_i, tc.ti_lo, tc.ti_hi, tc.tj_lo, tc.tj_hi,
-                   tc.waves == 1 ? (part == 0 ? tc.order0 : part == 1 ? tc.order1 : tc.order2) : nullptr, count};
-  if (count == 0) return;
+  const int tiles = part == 0 ? tc.ntiles() : part == 1 ? tc.interior_tiles() : tc.ntiles() - tc.interior_tiles();
+  const Pcg1Slot* ord = part == 0 ? tc.order0 : part == 1 ? tc.order1 : tc.order2;
+  // lockstep workgroups: one per group of the order (tc.groups), tc.waves slots each
+  const bool grouped = tc.waves > 1 && ord != nullptr;
+  PMX_CHECK(tc.waves == 1 || grouped, "pcg1: workgroups of several waves need the grouped dispatch order");
+  const int nb = grouped ? tc.groups[part] : tiles;
+  const int count = grouped ? nb * tc.waves : tiles;
+  const Pcg1Part P{part, tc.tiles_i, tc.ti_lo, tc.ti_hi, tc.tj_lo, tc.tj_hi, ord, count};
+  if (tiles == 0) return;
   PMX_CHECK(G.nb == 0 || (G.nx >= 2 && G.ny >= 2), "pcg1 on a decomposed grid needs subdomains >= 2 x 2");
-  const int nb = (count + tc.waves - 1) / tc.waves;
   const int bs = 64 * tc.waves;
 #define PMX_PCG1_CD(C, V, WV, PF, D)                                                                     \
   do {                                                                                                   \
@@ -586,9 +620,10 @@ void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0
   if (tc.vec == 2 && tc.waves == 1 && tc.pf == 1) PMX_PCG1(2, 1, 1);
   else if (tc.vec == 2 && tc.waves == 1 && tc.pf == 2) PMX_PCG1(2, 1, 2);
   else if (tc.vec == 2 && tc.waves == 1 && tc.pf == 3) PMX_PCG1(2, 1, 3);
+  else if (tc.vec == 2 && tc.waves == 8 && tc.pf == 1) PMX_PCG1(2, 8, 1);
+  else if (tc.vec == 2 && tc.waves == 4 && tc.pf == 1) PMX_PCG1(2, 4, 1);
 #ifdef PMX_PCG1_ALL_SHAPES
   else if (tc.vec == 2 && tc.waves == 1) PMX_PCG1(2, 1, 4);
-  else if (tc.vec == 2 && tc.waves == 4) PMX_PCG1(2, 4, 1);
   else if (tc.vec == 2 && tc.waves == 2) PMX_PCG1(2, 2, 1);
   else PMX_PCG1(4, 1, 1);
 #else

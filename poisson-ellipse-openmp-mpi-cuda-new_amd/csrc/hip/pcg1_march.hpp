@@ -398,7 +398,14 @@ struct Pcg1Row {
 // and the march waits with exact counts: the loop is split into 3 steps without stores, DPF ramp
 // steps and a steady loop whose every step stores, so each wait's number of younger operations
 // (later DMAs and stores) is a compile-time constant.  Same arithmetic, bit-identical fields.
-template <typename T, typename C, int VEC, int PF, int WM, bool FAST, int DPF = 0>
+//
+// LOCK (lockstep workgroups, k_pcg1 with several waves): the waves of a workgroup march side-by-side
+// tiles of one tile row and meet at an s_barrier after every row step, so the workgroup reads and
+// writes each row as ONE contiguous span of 8 x 1 KiB per field instead of as independent 1-KiB
+// pieces at different times (bench/probe/dma_march.hip k_lock: 16384^2, 16 waves per CU, 1.846 ->
+// 1.688 ms per sweep).  Pure pacing: no data passes between the waves, every wave of a workgroup
+// marches the same number of rows (one tile row), and a wave that has left no longer counts.
+template <typename T, typename C, int VEC, int PF, int WM, bool FAST, int DPF = 0, bool LOCK = false>
 __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb, const ArithF& F, T* __restrict__ w,
                                            const T* __restrict__ rold, T* __restrict__ rnew,
                                            const T* __restrict__ pold,
@@ -666,6 +673,7 @@ __device__ __forceinline__ void pcg1_march(const DevGeom& G, const DevTables& Tb
         // last row re-read that row (a cache hit) instead of the next tile's rows
         fetch(min(m + q + PF, mlast), buf[(q + PF) % (PF + 1)]);
         core(m + q, buf[q]);
+        if constexpr (LOCK) __builtin_amdgcn_s_barrier();
       }
     }
   }

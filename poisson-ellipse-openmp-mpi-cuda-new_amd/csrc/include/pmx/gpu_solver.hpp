@@ -75,6 +75,9 @@ struct GpuOptions {
   // pcg1 tile shape (rows1 = 0: auto).  VEC=2 x 1 wave/workgroup won the 16384^2 sweeps
   // (bench/gpu_pcg1_sweep.sh; VEC=4 needs 256 VGPRs and is 35% slower).
   int vec1 = 2, waves1 = 1, rows1 = 0;
+  // waves per workgroup of the w sweep (0 = as waves1, but 4 where waves1 is 8: the w sweep's
+  // registers allow 3 waves per SIMD, i.e. one 8-wave workgroup per CU).  PMX_PCG1_WAVES_W.
+  int waves1w = 0;
   // the w-moving sweep (one in w_cycle, a kernel of its own at 3 waves/SIMD) may use its own tile
   // height and prefetch depth: 0 = as the plain sweep (PMX_PCG1_ROWS_W, PMX_PCG1_PF_W)
   int rows1w = 0, pf1w = 0;

@@ -50,6 +50,7 @@ struct TileCfg {
   const Pcg1Slot* order0 = nullptr;
   const Pcg1Slot* order1 = nullptr;
   const Pcg1Slot* order2 = nullptr;  // the frame tiles
+  int groups[3] = {0, 0, 0};  // waves > 1: workgroups of each part (lockstep groups, pcg1_build_order)
   int arith32 = 0;  // kind 3 with fp32 storage: 1 = fp32 stencil arithmetic (GpuOptions::arith32)
   int lds_pad = 0;  // kind 3: dynamic LDS bytes per workgroup that cap the resident waves per CU
   int dpf = 0;      // kind 3: FAST tiles prefetch their rows dpf ahead by LDS-DMA (0 = registers)
@@ -114,11 +115,16 @@ void launch_pcg_b_wave(const DevGeom& G, const DevTables& Tb, T* w, T* r, const 
 // wsweep: launch the kernel that moves w; it must be set exactly on the sweeps k >= 1 with
 // k % S->w_cycle == 0 (the caller mirrors the device iteration counter; a mismatch stops the solve
 // with status breakdown and the NaN flag).
-// Builds tc.order0/order1/order2 in d_order (3 * tc.ntiles() slots): per launch part, the tiles of
-// each XCD's share of the positions with their row classes; slow_first: the tiles with cut
-// (slow-path) rows go first within each share.  Returns the number of such tiles.
+// Builds tc.order0/order1/order2 in d_order (pcg1_order_slots(tc) slots): per launch part, the
+// tiles of each XCD's share of the positions with their row classes; slow_first: the tiles with
+// cut (slow-path) rows go first within each share.  Returns the number of such tiles.
+// tc.waves > 1 (lockstep workgroups): the positions come in groups of tc.waves -- up to tc.waves
+// adjacent tiles of ONE tile row, marched side by side by the waves of one workgroup; unused slots
+// hold id -1; tc.groups[part] = the workgroups of each part, the XCD shares and the cut-first
+// ordering are per group.
 int pcg1_build_order(const DevGeom& G, const DevTables& Tb, TileCfg& tc, Pcg1Slot* d_order, bool slow_first,
                      hipStream_t s);
+size_t pcg1_order_slots(const TileCfg& tc);  // d_order capacity pcg1_build_order needs
 
 template <typename T>
 void launch_pcg1(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2, T* p0, T* p1,

@@ -345,3 +345,29 @@ def test_pcg1_lds_dma_march_bitwise(pkg, monkeypatch, dma, grid, ranks):
     assert out[0][2] == out[dma][2]
     if grid == (1600, 2400):
         assert out[dma][0] == 1858
+
+
+@pytest.mark.parametrize("waves,waves_w", [(8, 0), (4, 4), (8, 8)])
+@pytest.mark.parametrize("grid,ranks,split", [((1600, 2400), 1, "auto"), ((1000, 1400), 3, "auto"),
+                                              ((900, 1300), 4, "reference"), ((2000, 3000), 1, "auto")])
+def test_pcg1_lockstep_workgroups_bitwise(pkg, monkeypatch, waves, waves_w, grid, ranks, split):
+    """Lockstep workgroups (the waves of a workgroup march side-by-side tiles of one tile row, an
+    s_barrier per row step; grouped dispatch order with idle slots) change only the pacing: every
+    tile computes the same values and writes its partials to its own slot, so w, the sums and the
+    iteration count are bitwise those of one wave per workgroup, on one subdomain and decomposed
+    (split sweep: interior and frame parts grouped separately)."""
+    monkeypatch.setenv("PMX_PCG1_BLOCK", "0")
+    p = pkg.PoissonEllipse(M=grid[0], N=grid[1])
+    out = {}
+    for wv in (1, waves):
+        monkeypatch.setenv("PMX_PCG1_WAVES", str(wv))
+        monkeypatch.setenv("PMX_PCG1_WAVES_W", str(waves_w if wv > 1 else 0))
+        s = pkg.make_session(p, ranks=ranks, split=split, graph_batch=16)
+        assert s.tile["waves"] == wv
+        r = s.solve(1)
+        out[wv] = (r["iters"], s.gather_local_w(), s.state(0)["red_c"])
+    assert out[1][0] == out[waves][0]
+    assert np.array_equal(out[1][1], out[waves][1])
+    assert out[1][2] == out[waves][2]
+    if grid == (1600, 2400):
+        assert out[waves][0] == 1858
