@@ -102,9 +102,9 @@ def parse(argv=None):
                     help="process grid: auto = row strips while every strip keeps >= 128 rows, else the "
                          "least ghost perimeter (16384^2: 2x1, 4x1, 8x1 for 2/4/8 ranks); reference = the "
                          "reference's choose_process_grid (1x2, 2x2, 2x4)")
-    ap.add_argument("--kernel", default="wave", choices=["wave", "lds"],
-                    help="wave: wave-tile kernels with DPP lane shifts; lds: workgroup tiles + LDS row ring")
-    ap.add_argument("--block", type=int, default=256, help="lds kernels: tile width")
+    ap.add_argument("--kernel", default="wave", choices=["wave"],
+                    help="wave: wave-tile kernels with DPP lane shifts (the round-1 lds kernels are retired)")
+    ap.add_argument("--block", type=int, default=256, help="unused (the retired lds kernels' tile width)")
     ap.add_argument("--vec", type=int, default=0, help="wave kernels: columns per lane (0 = per-kernel best)")
     ap.add_argument("--vec-b", type=int, default=0, help="pcg_b columns per lane (0 = follow --vec / auto)")
     ap.add_argument("--tile-rows-b", type=int, default=-1, help="pcg_b tile height (-1 = auto)")

@@ -8,7 +8,7 @@
 //       [--breakdown-tol 1e-15]
 //       [--backend cpu|omp|hip] [--threads T] [--ranks P] [--gpus G] [--comm self|local|rccl]
 //       [--split reference|auto|rows|cols] [--dtype fp64|fp32|mixed] [--norm weighted|unweighted]
-//       [--exact] [--graph-batch 32] [--tile-rows 0] [--kernel wave|lds] [--vec 2] [--waves 4]
+//       [--exact] [--graph-batch 32] [--tile-rows 0] [--kernel wave] [--vec 2] [--waves 4]
 //       [--block 256] [--device D] [--vec-b V] [--waves-b W] [--tile-rows-b R] [--b-kernel rows|ring]
 //       [--dump sol.txt] [--dump-stride s] [--json] [--banner stage0..stage4]
 //       [--profile-phases N] [--check] [--overlap on|off] [--poison-halos]
@@ -55,7 +55,7 @@ struct Cli {
                "           [--backend cpu|omp|hip] [--threads T] [--ranks P] [--gpus G]\n"
                "           [--comm self|local|rccl] [--split reference|auto|rows|cols]\n"
                "           [--dtype fp64|fp32|mixed] [--norm weighted|unweighted] [--exact]\n"
-               "           [--graph-batch N] [--tile-rows R] [--kernel wave|lds] [--vec V]\n"
+               "           [--graph-batch N] [--tile-rows R] [--kernel wave] [--vec V]\n"
                "           [--waves W] [--block B] [--device D] [--vec-b V] [--waves-b W] [--tile-rows-b R]\n"
                "           [--b-kernel rows|ring] [--pair-w 0|1|2]\n"
                "           [--dump FILE] [--dump-stride S] [--json] [--banner stage0..stage4]\n"
@@ -127,8 +127,8 @@ Cli parse(int argc, char** argv) {
     else if (a == "--pair-w") c.opt.pair_w = std::atoi(val().c_str());
     else if (a == "--kernel") {
       const std::string v = val();
-      if (v != "wave" && v != "lds") usage("--kernel wave|lds");
-      c.opt.kernel = v == "lds" ? 0 : 1;
+      if (v != "wave") usage("--kernel wave (the round-1 lds kernels are retired)");
+      c.opt.kernel = 1;
     }
     else if (a == "--device") c.device = std::atoi(val().c_str());
     else if (a == "--dump") c.dump = val();

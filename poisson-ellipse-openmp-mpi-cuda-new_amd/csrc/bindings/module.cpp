@@ -193,8 +193,8 @@ GpuOptions make_options(int device, const std::string& kernel, int block, int ve
   o.placement_keep_free = placement_keep_free;
   o.algo = algo;
   o.device = device;
-  PMX_CHECK(kernel == "lds" || kernel == "wave", "kernel must be lds or wave, got " << kernel);
-  o.kernel = kernel == "lds" ? 0 : 1;
+  PMX_CHECK(kernel == "wave", "kernel must be wave (the round-1 lds kernels are retired, bench/RETIRED.md), got " << kernel);
+  o.kernel = 1;
   o.vec = vec;
   o.waves = waves;
   o.block = block;

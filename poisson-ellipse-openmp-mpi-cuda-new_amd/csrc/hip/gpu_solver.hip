@@ -237,7 +237,7 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   // 1D face tables
   tables_ = upload_tables(spec, &tables_buf_);
 
-  PMX_CHECK(opt.kernel == 0 || opt.kernel == 1, "kernel must be 0 (lds) or 1 (wave/dpp)");
+  PMX_CHECK(opt.kernel == 1, "kernel must be 1 (wave tiles); the round-1 LDS-ring kernels are retired (bench/RETIRED.md)");
   // tile shapes per kernel (profiles/tile_counters_16384_fp64.md: pcg_a is fastest with 4
   // columns/lane, pcg_b with 2 in fp64; fp32 moves 16 B with 4 columns)
   const bool fp64 = opt.dtype == DType::kFp64;
@@ -246,11 +246,8 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   const int waves_b = opt.waves_b ? opt.waves_b : opt.waves;
   const int rows_b = opt.tile_rows_b >= 0 ? opt.tile_rows_b : opt.tile_rows;
   // auto tile heights (caps and tile-count targets from bench/tile_sweep.py, see make_wave_tiles)
-  tiles_ = opt.kernel == 0 ? make_tiles(G, opt.block, opt.tile_rows)
-                           : make_wave_tiles(G, vec_a, opt.waves, opt.tile_rows, 32, 22000);
-  if (opt.kernel == 0)
-    tiles_b_ = make_tiles(G, opt.block, rows_b);
-  else if (opt.b_ring)
+  tiles_ = make_wave_tiles(G, vec_a, opt.waves, opt.tile_rows, 32, 22000);
+  if (opt.b_ring)
     tiles_b_ = make_wave_tiles(G, vec_b, waves_b, rows_b, 24, 66000);
   else  // default: ring-free 2-row tiles, independent of the pcg_a height
     tiles_b_ = make_row_tiles(G, vec_b, waves_b, opt.tile_rows_b >= 0 ? opt.tile_rows_b : 0);
@@ -677,14 +674,10 @@ void GpuSubdomainSolver::phase_a_kernel_only(hipStream_t s, int part) {
     launch_pcg1<T>(geom_, tables_, static_cast<T*>(field_base(0)), static_cast<T*>(field_base(1)),
                    reinterpret_cast<T*>(r2_ + field_off_ * elem_), static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), partials_, state_,
                    tiles1_for(w_sweep_next()), s, part, w_sweep_next());
-  else if (tiles_.kind == 1)
+  else
     launch_pcg_a_wave<T>(geom_, tables_, static_cast<const T*>(field_base(1)),
                          static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(),
                          partials_, state_, tiles_, opt_.exact, s);
-  else
-    launch_pcg_a<T>(geom_, tables_, static_cast<const T*>(field_base(1)),
-                    static_cast<T*>(field_base(2)), static_cast<T*>(field_base(3)), halo<T>(),
-                    partials_, state_, tiles_, opt_.exact, s);
 }
 
 template <typename T>
@@ -699,15 +692,10 @@ void GpuSubdomainSolver::phase_b_kernel_only(hipStream_t s, bool pack) {
   // pcg_b reads G.nb only to pack the send buffers: clearing it skips the packing
   DevGeom G = geom_;
   if (!pack) G.nb = 0;
-  if (tiles_b_.kind != 0)
-    launch_pcg_b_wave<T>(G, tables_, static_cast<T*>(field_base(0)),
-                         static_cast<T*>(field_base(1)), static_cast<const T*>(field_base(2)),
-                         static_cast<const T*>(field_base(3)), halo<T>(), partials_, state_, tiles_b_,
-                         opt_.exact, s);
-  else
-    launch_pcg_b<T>(G, tables_, static_cast<T*>(field_base(0)), static_cast<T*>(field_base(1)),
-                    static_cast<const T*>(field_base(2)), static_cast<const T*>(field_base(3)),
-                    halo<T>(), partials_, state_, tiles_b_, opt_.exact, s);
+  launch_pcg_b_wave<T>(G, tables_, static_cast<T*>(field_base(0)),
+                       static_cast<T*>(field_base(1)), static_cast<const T*>(field_base(2)),
+                       static_cast<const T*>(field_base(3)), halo<T>(), partials_, state_, tiles_b_,
+                       opt_.exact, s);
 }
 
 void GpuSubdomainSolver::enqueue_init(hipStream_t s) {

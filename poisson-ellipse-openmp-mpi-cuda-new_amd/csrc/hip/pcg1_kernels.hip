@@ -656,17 +656,7 @@ void launch_reduce_n(const double* partials, int n, int nq, const double* weight
   unsigned* ticket = reinterpret_cast<unsigned*>(chunk + 8 * kReduceMaxBlocks);
   ReduceWeights wt{};
   for (int q = 0; q < nq; ++q) wt.w[q] = weights[q];
-  static const bool one = [] {
-    const char* e = std::getenv("PMX_REDUCE_ONE");
-    return !(e && e[0] == '0');
-  }();
-  static const int one_threads = [] {
-    const char* e = std::getenv("PMX_REDUCE_ONE_THREADS");
-    return e && e[0] ? std::atoi(e) : 1024;
-  }();
-  if (one && n <= kReduceOneMax && one_threads == 256)
-    hipLaunchKernelGGL((k_reduce_1<kNq, 256>), dim3(1), dim3(256), 0, s, partials, n, wt, out, S, mode, progress);
-  else if (one && n <= kReduceOneMax)
+  if (n <= kReduceOneMax)
     hipLaunchKernelGGL((k_reduce_1<kNq, 1024>), dim3(1), dim3(1024), 0, s, partials, n, wt, out, S, mode, progress);
   else
     hipLaunchKernelGGL(k_reduce_n<kNq>, dim3(nb), dim3(256), 0, s, partials, n, wt, out, S, mode, chunk, ticket,

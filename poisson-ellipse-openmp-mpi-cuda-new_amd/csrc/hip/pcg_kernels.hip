@@ -1,15 +1,13 @@
-// Fused PCG kernels for CDNA4 (gfx950).  See pmx/kernels.hpp for the dataflow.
-//
-// Replaces the reference's per-op CUDA kernels (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:507-676):
-//   apply_A_kernel + dot_kernel(Ap,p) + update_p_kernel       -> k_pcg_a
-//   update_w_r_kernel + apply_Dinv_kernel + dot_kernel(z,r)   -> k_pcg_b
-//   host partial-sum loops dot_gpu/reduce_diff (:772-797)     -> k_reduce (device, deterministic)
-//   CPU fic_reg + H2D copies (:713-760)                       -> k_init + on-the-fly coefficients
-//
-// Mapping: one workgroup = one tile of `rows` x BLOCK nodes; thread t owns column j0+t (the
-// contiguous axis, so every wave64 load/store is one coalesced 512-B (fp64) segment) and
-// marches down the rows.  The i-neighbours of the stencil live in registers, the j-neighbours
-// of the freshly computed p row in a 3-slot LDS ring (one barrier per row).
+// Setup and reduction kernels shared by both iterations (pcg1, pcg2) on CDNA4 (gfx950):
+//   CPU fic_reg + H2D copies (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:713-760) -> k_init (w = 0,
+//     r = B, z^0 partials, coefficients rebuilt on the fly from the 1-D face tables)
+//   host partial-sum loops dot_gpu / reduce_diff (:772-797)                 -> k_reduce (device,
+//     deterministic, ticketed multi-block finish)
+//   k_edge_r (pcg2 with a second stream: the edge lines of r a neighbour needs, packed ahead of
+//     the sweep), k_local_allreduce (LocalComm's in-process "all-reduce").
+// Tiles: one workgroup = `rows` x BLOCK nodes, thread t owns column j0+t (the contiguous axis: every
+// wave64 access is one coalesced segment).  The round-1 LDS-ring iteration kernels (k_pcg_a /
+// k_pcg_b, `--kernel lds`) are retired (bench/RETIRED.md): the wave kernels replaced them.
 #include <algorithm>
 #include <cmath>
 
@@ -82,217 +80,6 @@ k_init(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, HaloBufs<T
   if (threadIdx.x == 0) {
     partials[2 * t.id] = 0.0;
     partials[2 * t.id + 1] = acc;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// k_pcg_a: scalar prologue (stop test, beta), p^k = z + beta p^{k-1}, (A p^k, p^k) partial
-// ---------------------------------------------------------------------------
-template <typename T, int BLOCK, bool EXACT>
-__global__ void __launch_bounds__(BLOCK)
-k_pcg_a(DevGeom G, DevTables Tb, const T* __restrict__ r, T* p0, T* p1, HaloBufs<T> H,
-        double* __restrict__ partials, PcgState* S, int TI, int tiles_j) {
-  __shared__ double ring[3][BLOCK + 2];
-  __shared__ double halo[2][kMaxRows];
-  __shared__ double lds[2 * BLOCK / kWave];
-
-  if (S->done) return;
-  const long long k = S->it;
-  const bool first = (k == 1);
-  const double zr_prev = S->red_b[1];  // zr_{k-1}
-  double beta = 0.0;
-  if (!first) {
-    // stop rule of iteration k-1 (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:890-906)
-    const double diff = sqrt(S->red_b[0]);
-    const bool bad = !(diff == diff) || !(zr_prev == zr_prev);
-    if (bad || diff < S->delta || k > S->max_iter) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) {
-        S->diff = diff;
-        S->iters = k - 1;
-        S->status = bad ? int(Status::kBreakdown)
-                        : (diff < S->delta ? int(Status::kConverged) : int(Status::kMaxIter));
-        if (bad) S->nan_flag = 1;
-        S->done = 1;
-      }
-      return;
-    }
-    beta = zr_prev / S->zr[k & 1];  // zr_{k-1} / zr_{k-2}
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    S->zr[(k - 1) & 1] = zr_prev;
-    if (!first) S->diff = sqrt(S->red_b[0]);
-  }
-
-  T* pnew = (k & 1) ? p1 : p0;  // p^k lives in buffer k & 1
-  const T* pold = (k & 1) ? p0 : p1;
-  const Tile t = tile_of(blockIdx.x, tiles_j, TI, BLOCK, G);
-  const int nrows = t.iend - t.i0 + 1;
-  const int64_t P = G.pitch;
-
-  // (1) p^k on the two halo columns j0-1 / jend+1 (ghost columns come from the recv buffers)
-  for (int idx = threadIdx.x; idx < 2 * nrows; idx += BLOCK) {
-    const int side = idx >= nrows ? 1 : 0;
-    const int ii = t.i0 + (side ? idx - nrows : idx);
-    const int jj = side ? t.jend + 1 : t.j0 - 1;
-    const int gi = G.gi0 + ii, gj = G.gj0 + jj;
-    double v = 0.0;
-    if (!dirichlet(G, gi, gj)) {
-      double rv;
-      if (jj == 0) rv = H.recv[2][ii - 1];
-      else if (jj == G.ny + 1) rv = H.recv[3][ii - 1];
-      else rv = r[int64_t(ii) * P + jj];
-      const double a0 = coef_a(Tb, G, gi, gj), a1 = coef_a(Tb, G, gi + 1, gj);
-      const double b0 = coef_b(Tb, G, gi, gj), b1 = coef_b(Tb, G, gi, gj + 1);
-      const double z = zdiv<EXACT>(rv, a0, a1, b0, b1, G);
-      v = first ? z : z + beta * double(pold[int64_t(ii) * P + jj]);
-      if ((jj == 0 && (G.nb & kNbYlo)) || (jj == G.ny + 1 && (G.nb & kNbYhi)))
-        pnew[int64_t(ii) * P + jj] = static_cast<T>(v);
-    }
-    halo[side][ii - t.i0] = v;
-  }
-  __syncthreads();
-
-  // (2) march down the rows.  Row i+1's loads (r, p^{k-1}, row tables) are issued before row
-  // i is computed, so every wave keeps two rows of HBM traffic in flight across the barrier.
-  const int tid = threadIdx.x;
-  const int j = t.j0 + tid;
-  const bool valid = j <= t.jend;
-  const int gj = G.gj0 + (valid ? j : t.jend);
-  const ColConst cc = load_col(Tb, gj);
-  const int rpos = t.jend - t.j0 + 2;  // LDS ring index of the right halo column
-  const int ilast = t.iend + 1;
-  auto fetch = [&](int i, double& rv, double& po) {
-    rv = 0.0;
-    po = 0.0;
-    const int gi = G.gi0 + i;
-    if (valid && i <= ilast && gi > 0 && gi < G.M) {
-      rv = (i == 0) ? double(H.recv[0][j - 1])
-                    : (i == G.nx + 1) ? double(H.recv[1][j - 1]) : double(r[int64_t(i) * P + j]);
-      if (!first) po = double(pold[int64_t(i) * P + j]);
-    }
-  };
-  double pm2 = 0.0, pm1 = 0.0;         // p^k at rows i-2, i-1
-  double qa0 = 0.0, qa1 = 0.0, qb0 = 0.0, qb1 = 0.0;  // coefficients of row i-1
-  double acc = 0.0;
-  double rv_c, po_c;
-  fetch(t.i0 - 1, rv_c, po_c);
-  RowConst rc = load_row(Tb, G.gi0 + t.i0 - 1);
-  for (int i = t.i0 - 1; i <= ilast; ++i) {
-    double rv_n, po_n;
-    fetch(i + 1, rv_n, po_n);
-    const RowConst rc_n = load_row(Tb, G.gi0 + min(i + 1, ilast));
-    const int gi = G.gi0 + i;
-    const double a0 = face_a0c(cc, rc, G), a1 = face_a1c(cc, rc, G);
-    const double b0 = face_b0c(cc, rc, G), b1 = face_b1c(cc, rc, G);
-    double pc = 0.0;
-    const int slot = (i - t.i0 + 1) % 3;
-    if (valid) {
-      if (gi > 0 && gi < G.M) {
-        const double z = zdiv<EXACT>(rv_c, a0, a1, b0, b1, G);
-        pc = first ? z : z + beta * po_c;
-        const bool own = i >= t.i0 && i <= t.iend;
-        const bool ghost = (i == 0 && (G.nb & kNbXlo)) || (i == G.nx + 1 && (G.nb & kNbXhi));
-        if (own || ghost) pnew[int64_t(i) * P + j] = static_cast<T>(pc);
-      }
-      pc = double(static_cast<T>(pc));  // use the stored precision in A p (fp32 mode)
-      ring[slot][tid + 1] = pc;
-    }
-    if (tid == 0 && i >= t.i0 && i <= t.iend) {
-      ring[slot][0] = halo[0][i - t.i0];
-      ring[slot][rpos] = halo[1][i - t.i0];
-    }
-    __syncthreads();
-    if (valid && i - 1 >= t.i0) {
-      const int sm = (i - t.i0) % 3;  // slot of row i-1
-      const double pjm = ring[sm][tid], pjp = ring[sm][tid + 2];
-      const double Ap = apply_a<EXACT>(pm1, pm2, pc, pjm, pjp, qa0, qa1, qb0, qb1, G);
-      acc += Ap * pm1;
-    }
-    pm2 = pm1; pm1 = pc;
-    qa0 = a0; qa1 = a1; qb0 = b0; qb1 = b1;
-    rv_c = rv_n; po_c = po_n; rc = rc_n;
-  }
-  double unused = 0.0;
-  block_sum2<BLOCK>(acc, unused, lds);
-  if (threadIdx.x == 0) partials[t.id] = acc;
-}
-
-// ---------------------------------------------------------------------------
-// k_pcg_b: alpha, A p (recomputed), w/r update, sum dw^2, (z, r), halo pack of r
-// ---------------------------------------------------------------------------
-template <typename T, int BLOCK, bool EXACT>
-__global__ void __launch_bounds__(BLOCK)
-k_pcg_b(DevGeom G, DevTables Tb, T* __restrict__ w, T* __restrict__ r, const T* p0, const T* p1,
-        HaloBufs<T> H, double* __restrict__ partials, PcgState* S, int TI, int tiles_j) {
-  __shared__ double lds[2 * BLOCK / kWave];
-  if (S->done) return;
-  const long long k = S->it;
-  const double denom = S->red_a[0];
-  // breakdown guard: |denom| < tol (stages 2-4) or denom < tol (stage 0), tol = 1e-15 by default
-  const bool bd = S->norm == int(Norm::kWeighted) ? fabs(denom) < S->bd_tol : denom < S->bd_tol;
-  if (bd || !(denom == denom)) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      S->iters = k;
-      S->status = int(Status::kBreakdown);
-      if (!(denom == denom)) S->nan_flag = 1;
-      S->done = 1;
-    }
-    return;
-  }
-  const double alpha = S->zr[(k - 1) & 1] / denom;
-  const T* pn = (k & 1) ? p1 : p0;
-  const Tile t = tile_of(blockIdx.x, tiles_j, TI, BLOCK, G);
-  const int j = t.j0 + threadIdx.x;
-  double dacc = 0.0, zacc = 0.0;
-  if (j <= t.jend) {
-    // software-pipelined march: row i+1's five loads are in flight while row i is computed
-    const int64_t P = G.pitch;
-    const int gj = G.gj0 + j;
-    const ColConst cc = load_col(Tb, gj);
-    double pm = double(pn[int64_t(t.i0 - 1) * P + j]);
-    int64_t c = int64_t(t.i0) * P + j;
-    double pc = double(pn[c]);
-    double pp = double(pn[c + P]), pjm = double(pn[c - 1]), pjp = double(pn[c + 1]);
-    double wo = double(w[c]), ro = double(r[c]);
-    RowConst rc = load_row(Tb, G.gi0 + t.i0);
-    double acur = face_a0c(cc, rc, G);
-    for (int i = t.i0; i <= t.iend; ++i) {
-      const int64_t cn = c + P;
-      const bool more = i < t.iend;
-      double pp_n = 0.0, pjm_n = 0.0, pjp_n = 0.0, wo_n = 0.0, ro_n = 0.0;
-      if (more) {
-        pp_n = double(pn[cn + P]);
-        pjm_n = double(pn[cn - 1]);
-        pjp_n = double(pn[cn + 1]);
-        wo_n = double(w[cn]);
-        ro_n = double(r[cn]);
-      }
-      const RowConst rc_n = load_row(Tb, G.gi0 + (more ? i + 1 : i));
-      const double a0 = acur, a1 = face_a1c(cc, rc, G);
-      const double b0 = face_b0c(cc, rc, G), b1 = face_b1c(cc, rc, G);
-      const double Ap = apply_a<EXACT>(pc, pm, pp, pjm, pjp, a0, a1, b0, b1, G);
-      const T ws = static_cast<T>(upd_w<EXACT>(wo, alpha, pc));
-      const T rs = static_cast<T>(upd_r<EXACT>(ro, alpha, Ap));
-      const double dw = double(ws) - wo;
-      dacc += dw * dw;
-      const double rq = double(rs);
-      const double z = zdiv<EXACT>(rq, a0, a1, b0, b1, G);
-      zacc += z * rq;
-      w[c] = ws;
-      r[c] = rs;
-      if (i == 1 && (G.nb & kNbXlo)) H.send[0][j - 1] = rs;
-      if (i == G.nx && (G.nb & kNbXhi)) H.send[1][j - 1] = rs;
-      if (j == 1 && (G.nb & kNbYlo)) H.send[2][i - 1] = rs;
-      if (j == G.ny && (G.nb & kNbYhi)) H.send[3][i - 1] = rs;
-      pm = pc; pc = pp; acur = a1;
-      pp = pp_n; pjm = pjm_n; pjp = pjp_n; wo = wo_n; ro = ro_n; rc = rc_n;
-      c = cn;
-    }
-  }
-  block_sum2<BLOCK>(dacc, zacc, lds);
-  if (threadIdx.x == 0) {
-    partials[2 * t.id] = dacc;
-    partials[2 * t.id + 1] = zacc;
   }
 }
 
@@ -417,37 +204,6 @@ void launch_init(const DevGeom& G, const DevTables& Tb, T* w, T* r, HaloBufs<T> 
 }
 
 template <typename T>
-void launch_pcg_a(const DevGeom& G, const DevTables& Tb, const T* r, T* p0, T* p1, HaloBufs<T> H,
-                  double* partials, PcgState* S, const TileCfg& tc, bool exact, hipStream_t s) {
-  if (exact) {
-    PMX_BLOCK_DISPATCH(tc.block,
-        hipLaunchKernelGGL((k_pcg_a<T, B, true>), dim3(tc.ntiles()), dim3(B), 0, s, G, Tb, r, p0,
-                           p1, H, partials, S, tc.rows, tc.tiles_j));
-  } else {
-    PMX_BLOCK_DISPATCH(tc.block,
-        hipLaunchKernelGGL((k_pcg_a<T, B, false>), dim3(tc.ntiles()), dim3(B), 0, s, G, Tb, r, p0,
-                           p1, H, partials, S, tc.rows, tc.tiles_j));
-  }
-  HIP_CHECK(hipGetLastError());
-}
-
-template <typename T>
-void launch_pcg_b(const DevGeom& G, const DevTables& Tb, T* w, T* r, const T* p0, const T* p1,
-                  HaloBufs<T> H, double* partials, PcgState* S, const TileCfg& tc, bool exact,
-                  hipStream_t s) {
-  if (exact) {
-    PMX_BLOCK_DISPATCH(tc.block,
-        hipLaunchKernelGGL((k_pcg_b<T, B, true>), dim3(tc.ntiles()), dim3(B), 0, s, G, Tb, w, r,
-                           p0, p1, H, partials, S, tc.rows, tc.tiles_j));
-  } else {
-    PMX_BLOCK_DISPATCH(tc.block,
-        hipLaunchKernelGGL((k_pcg_b<T, B, false>), dim3(tc.ntiles()), dim3(B), 0, s, G, Tb, w, r,
-                           p0, p1, H, partials, S, tc.rows, tc.tiles_j));
-  }
-  HIP_CHECK(hipGetLastError());
-}
-
-template <typename T>
 void launch_edge_r(const DevGeom& G, const DevTables& Tb, const T* r, const T* p0, const T* p1,
                    HaloBufs<T> H, const PcgState* S, bool exact, hipStream_t s) {
   const int n = 2 * G.nx + 2 * G.ny;
@@ -478,11 +234,6 @@ void launch_local_allreduce(double* const* bufs, int nranks, int nq, hipStream_t
 #define PMX_INST(T)                                                                              \
   template void launch_init<T>(const DevGeom&, const DevTables&, T*, T*, HaloBufs<T>, double*,  \
                                const TileCfg&, hipStream_t);                                     \
-  template void launch_pcg_a<T>(const DevGeom&, const DevTables&, const T*, T*, T*, HaloBufs<T>, \
-                                double*, PcgState*, const TileCfg&, bool, hipStream_t);          \
-  template void launch_pcg_b<T>(const DevGeom&, const DevTables&, T*, T*, const T*, const T*,    \
-                                HaloBufs<T>, double*, PcgState*, const TileCfg&, bool,           \
-                                hipStream_t);                                                    \
   template void launch_edge_r<T>(const DevGeom&, const DevTables&, const T*, const T*, const T*, \
                                  HaloBufs<T>, const PcgState*, bool, hipStream_t);
 PMX_INST(double)

@@ -87,15 +87,6 @@ void launch_init(const DevGeom& G, const DevTables& Tb, T* w, T* r, HaloBufs<T> 
                  double* partials, const TileCfg& tc, hipStream_t s);
 
 template <typename T>
-void launch_pcg_a(const DevGeom& G, const DevTables& Tb, const T* r, T* p0, T* p1, HaloBufs<T> H,
-                  double* partials, PcgState* S, const TileCfg& tc, bool exact, hipStream_t s);
-
-template <typename T>
-void launch_pcg_b(const DevGeom& G, const DevTables& Tb, T* w, T* r, const T* p0, const T* p1,
-                  HaloBufs<T> H, double* partials, PcgState* S, const TileCfg& tc, bool exact,
-                  hipStream_t s);
-
-template <typename T>
 void launch_pcg_a_wave(const DevGeom& G, const DevTables& Tb, const T* r, T* p0, T* p1,
                        HaloBufs<T> H, double* partials, PcgState* S, const TileCfg& tc, bool exact,
                        hipStream_t s);

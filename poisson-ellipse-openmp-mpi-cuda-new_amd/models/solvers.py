@@ -87,8 +87,8 @@ def make_session(problem: PoissonEllipse, ranks: int = 1, split: str = "referenc
     overlap: ghost exchange on a second stream concurrent with pcg_b (only matters for ranks > 1).
 
     kernel="wave": wave-tile kernels with DPP neighbour shifts (vec columns/lane, `waves` tiles per
-    workgroup); kernel="lds": workgroup tiles with an LDS row ring (`block` columns).  vec=0 picks
-    the measured best per kernel (pcg_a 4, pcg_b 2 in fp64); *_b override pcg_b's shape alone.
+    workgroup; the round-1 "lds" kernels are retired, bench/RETIRED.md).  vec=0 picks the measured
+    best per kernel (pcg_a 4, pcg_b 2 in fp64); *_b override pcg_b's shape alone.
     pcg_b runs the ring-free 2-row kernel by default; b_ring=True selects the pipelined one.
 
     placement: up to this many candidate field blocks are timed and the fastest kept (0 = off, the

@@ -58,7 +58,7 @@ def test_pcg1_matches_cpu_oracle(pkg, monkeypatch):
     (2, {}, "pcg1"),                  # decomposed: radius-2 halo
     (8, {}, "pcg1"),
     (2, {"dtype": "fp32"}, "pcg1"),
-    (2, {"kernel": "lds"}, "pcg2"),
+    (2, {"exact": True}, "pcg2"),
 ])
 def test_auto_algorithm_selection(pkg, monkeypatch, ranks, kw, algo):
     monkeypatch.delenv("PMX_ALGO", raising=False)

@@ -60,18 +60,9 @@ def test_local_comm_decomposition(pkg, ranks):
 def test_local_comm_splits_and_tiles(pkg, split):
     p = pkg.PoissonEllipse(M=300, N=700)
     ref = pkg.solve(p, "cpu")
-    r = pkg.solve(p, "hip", ranks=6, split=split, tile_rows=17, kernel="lds", block=128)
+    r = pkg.solve(p, "hip", ranks=6, split=split, tile_rows=17)
     assert r.iters == ref.iters
     assert np.abs(r.w - ref.w).max() < 1e-10
-
-
-@pytest.mark.parametrize("block,rows", [(128, 1), (256, 64), (512, 256), (256, 7)])
-def test_lds_tile_shapes(pkg, block, rows):
-    p = pkg.PoissonEllipse(M=211, N=1031)
-    ref = pkg.solve(p, "hip")
-    r = pkg.solve(p, "hip", kernel="lds", block=block, tile_rows=rows)
-    assert r.iters == ref.iters
-    assert np.abs(r.w - ref.w).max() < 1e-12
 
 
 @pytest.mark.parametrize("vec,waves,rows", [(1, 4, 1), (2, 4, 64), (2, 1, 5), (2, 8, 33), (1, 4, 0), (2, 4, 0), (4, 4, 0), (4, 4, 7)])
@@ -81,16 +72,16 @@ def test_wave_tile_shapes(pkg, vec, waves, rows, grid, b_ring):
     """Wave-tile kernels on full and partial tiles (odd widths leave half-filled lanes); pcg_b as
     the ring-free row kernel (rows = its tile height) or the pipelined ring kernel."""
     p = pkg.PoissonEllipse(M=grid[0], N=grid[1])
-    ref = pkg.solve(p, "hip", kernel="lds")
+    ref = pkg.solve(p, "cpu")
     r = pkg.solve(p, "hip", kernel="wave", vec=vec, waves=waves, tile_rows=rows, b_ring=b_ring,
                   tile_rows_b=-1 if b_ring else rows)
     assert r.iters == ref.iters
-    assert np.abs(r.w - ref.w).max() < 1e-12
+    assert np.abs(r.w - ref.w).max() < 1e-11
 
 
 def test_wave_fp32_vec4(pkg):
     p = pkg.PoissonEllipse(M=400, N=600)
-    a = pkg.solve(p, "hip", kernel="lds", dtype="fp32")
+    a = pkg.solve(p, "hip", dtype="fp32")
     b = pkg.solve(p, "hip", kernel="wave", vec=4, dtype="fp32")
     assert abs(a.iters - b.iters) <= 3
     assert np.abs(a.w - b.w).max() < 1e-5
@@ -99,7 +90,7 @@ def test_wave_fp32_vec4(pkg):
 @pytest.mark.parametrize("ranks", [2, 4, 7])
 def test_wave_kernels_decomposed(pkg, ranks):
     p = pkg.PoissonEllipse(M=260, N=390)
-    ref = pkg.solve(p, "hip", kernel="lds")
+    ref = pkg.solve(p, "cpu")
     r = pkg.solve(p, "hip", kernel="wave", ranks=ranks)
     assert r.iters == ref.iters
     assert np.abs(r.w - ref.w).max() < 1e-11
@@ -113,7 +104,7 @@ def test_graph_vs_eager(pkg):
     assert np.array_equal(a.w, b.w)
 
 
-@pytest.mark.parametrize("kernel", ["wave", "lds"])
+@pytest.mark.parametrize("kernel", ["wave"])
 @pytest.mark.parametrize("ranks,split", [(2, "reference"), (4, "reference"), (7, "auto"), (3, "cols")])
 def test_overlap_matches_serial_halo(pkg, kernel, ranks, split):
     """Halo on a second stream (edges packed by k_edge_r) is bit-identical to the in-order path."""
@@ -198,7 +189,7 @@ def test_bench_session_steps(pkg):
     assert not st1["done"] and st1["it"] - st0["it"] == 70
 
 
-@pytest.mark.parametrize("kernel", ["wave", "lds"])
+@pytest.mark.parametrize("kernel", ["wave"])
 def test_breakdown_tolerance_parameter_gpu(pkg, kernel):
     r = pkg.solve(pkg.PoissonEllipse(M=40, N=40, breakdown_tol=1e3), "hip", kernel=kernel)
     assert r.status == "breakdown" and r.iters == 1
