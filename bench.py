@@ -112,6 +112,9 @@ def parse(argv=None):
                     help="pcg_b: ring-free 2-row tiles (default) or the software-pipelined ring kernel")
     ap.add_argument("--waves", type=int, default=4, help="wave kernels: wave tiles per workgroup")
     ap.add_argument("--tile-rows", type=int, default=0, help="tile height (0 = auto)")
+    ap.add_argument("--algo", default="auto", choices=["auto", "pcg1", "pcg2", "ca"],
+                    help="iteration algorithm: auto (pcg1 / pcg2), or ca = s-step PCG (one GPU, ca_kernels.hip)")
+    ap.add_argument("--ca-s", type=int, default=3, choices=[2, 3], help="s-step PCG: iterations per block")
     ap.add_argument("--graph-batch", type=int, default=32,
                     help="iterations per captured hipGraph; the timed region replays graphs for any --steps "
                          "(full batches plus one remainder graph, all captured during warmup)")
@@ -581,7 +584,7 @@ def measure(args) -> int:
         models = importlib.import_module(pkg_name + ".models")
         runner = ds.SessionRunner(models.make_session(problem, ranks=1, device=info.local_rank,
                                                       block_tiles={"auto": -1, "on": 1, "off": 0}[args.block_tiles],
-                                                      **pkw, **kw), problem, info)
+                                                      algo=args.algo, ca_s=args.ca_s, **pkw, **kw), problem, info)
         comm_used = "self"
     elif share and cfg["comm"] == "ipc":
         runner = ds.DistGpuPCG(problem, info, comm="ipc", device=0, **dkw)

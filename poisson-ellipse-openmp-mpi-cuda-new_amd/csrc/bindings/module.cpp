@@ -185,8 +185,10 @@ GpuOptions make_options(int device, const std::string& kernel, int block, int ve
                         int tile_rows, const std::string& dtype, bool exact, int graph_batch, bool check,
                         bool overlap = true, int vec_b = 0, int waves_b = 0, int tile_rows_b = -1,
                         bool poison_halos = false, bool b_ring = false, int algo = -1, int placement = 0,
-                        double placement_budget_s = 0.5, double placement_keep_free = 0.5, int block1 = -1) {
+                        double placement_budget_s = 0.5, double placement_keep_free = 0.5, int block1 = -1,
+                        int ca_s = 3) {
   GpuOptions o;
+  o.ca_s = ca_s;
   o.block1 = block1;
   o.placement = placement;
   o.placement_budget_s = placement_budget_s;
@@ -450,14 +452,14 @@ PYBIND11_MODULE(_pmx, m) {
                        bool rccl_graph, bool overlap, int vec_b, int waves_b, int tile_rows_b,
                        bool poison_halos, bool b_ring, int algo, bool defer_connect, int threaded,
                        int placement, double placement_budget_s, double placement_keep_free, int sharing,
-                       int block_tiles) {
+                       int block_tiles, int ca_s) {
              SessionConfig c;
              c.sharing = sharing;
              c.spec = s;
              c.opt = make_options(device, kernel, block, vec, waves, tile_rows, dtype, exact,
                                   graph_batch, check, overlap, vec_b, waves_b, tile_rows_b, poison_halos,
                                   b_ring, algo, placement, placement_budget_s, placement_keep_free,
-                                  block_tiles);
+                                  block_tiles, ca_s);
              c.defer_connect = defer_connect;
              c.threaded = threaded;
              c.split = split;
@@ -485,7 +487,8 @@ PYBIND11_MODULE(_pmx, m) {
            py::arg("waves_b") = 0, py::arg("tile_rows_b") = -1, py::arg("poison_halos") = false,
            py::arg("b_ring") = false, py::arg("algo") = -1, py::arg("defer_connect") = false,
            py::arg("threaded") = -1, py::arg("placement") = 0, py::arg("placement_budget_s") = 0.5,
-           py::arg("placement_keep_free") = 0.5, py::arg("sharing") = 0, py::arg("block_tiles") = -1)
+           py::arg("placement_keep_free") = 0.5, py::arg("sharing") = 0, py::arg("block_tiles") = -1,
+           py::arg("ca_s") = 3)
       .def("ipc_export", [](Session& s) { return py::bytes(s.ipc_export()); },
            "IPC session: this rank's memory handles (pass every rank's to connect_ipc)")
       .def("connect_ipc", [](Session& s, std::vector<py::bytes> ex) {
@@ -583,7 +586,9 @@ PYBIND11_MODULE(_pmx, m) {
       .def_property_readonly("poisoned", [](Session& s) { return s.poisoned(); })
       .def_property_readonly("device_bytes", &Session::device_bytes)
       .def_property_readonly("grid", [](Session& s) { return py::make_tuple(s.grid().Px, s.grid().Py); })
-      .def_property_readonly("ntiles", [](Session& s) { return s.solver(0).tiles().ntiles(); })
+      .def_property_readonly("ntiles", [](Session& s) {
+        return s.solver(0).ca() ? s.solver(0).ca_tiles().ntiles() : s.solver(0).tiles().ntiles();
+      })
       .def_property_readonly("tile", [](Session& s) {
         auto one = [](const TileCfg& t) {
           py::dict d;
@@ -597,8 +602,22 @@ PYBIND11_MODULE(_pmx, m) {
         };
         py::dict d = one(s.solver(0).tiles());
         if (s.solver(0).block_tiles()) d["block_tiles"] = true;
-        if (!s.solver(0).single_pass()) d["b"] = one(s.solver(0).tiles_b());
-        d["algo"] = s.solver(0).single_pass() ? "pcg1" : "pcg2";
+        if (s.solver(0).ca()) {  // s-step PCG: its own wave tiles
+          const CaTiles& c = s.solver(0).ca_tiles();
+          d = py::dict();
+          d["kind"] = "ca";
+          d["s"] = c.s;
+          d["block"] = c.wo;
+          d["rows"] = c.rows;
+          d["vec"] = 2;
+          d["waves"] = 1;
+          d["tiles_i"] = c.tiles_i;
+          d["tiles_j"] = c.tiles_j;
+          d["algo"] = "ca";
+        } else {
+          if (!s.solver(0).single_pass()) d["b"] = one(s.solver(0).tiles_b());
+          d["algo"] = s.solver(0).single_pass() ? "pcg1" : "pcg2";
+        }
         if (!s.solver(0).placement_ms().empty()) {
           // 3 plain sweeps per candidate field block (rotating field roles), the fastest kept
           std::vector<float> v = s.solver(0).placement_ms();

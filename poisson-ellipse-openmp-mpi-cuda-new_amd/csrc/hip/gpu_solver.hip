@@ -113,6 +113,10 @@ GpuOptions resolve_options(const GpuOptions& in) {
             "block tiles: no " << o.block_rows1 << "-row x " << o.block_waves1 << "-wave variant (4/8/12/16 x 8, 8/16 x 16)");
   PMX_CHECK(o.block_waves1 == 8 || o.block_waves1 == 16, "block tiles: 8 or 16 waves per workgroup");
   PMX_CHECK(o.block_fused1 >= -1 && o.block_fused1 <= 1, "block-tile fused reduction must be -1 (auto), 0 or 1");
+  env_int("PMX_CA_S", o.ca_s);
+  env_int("PMX_CA_ROWS", o.ca_rows);
+  PMX_CHECK(o.ca_s == 2 || o.ca_s == 3, "s-step PCG: s must be 2 or 3");
+  PMX_CHECK(o.ca_rows >= 0 && o.ca_rows <= 4096, "s-step PCG: tile rows must be 0 (auto) .. 4096");
   env_int("PMX_PCG1_DMA", o.dma1);
   env_int("PMX_PCG1_DMA_W", o.dma1w);
   PMX_CHECK(o.dma1 == 0 || o.dma1 == 2 || o.dma1 == 3, "pcg1 LDS-DMA prefetch depth must be 0, 2 or 3");
@@ -121,7 +125,7 @@ GpuOptions resolve_options(const GpuOptions& in) {
   PMX_CHECK(o.wpcu1 >= 0 && o.wpcu1 <= 32 && o.wpcu1w >= 0 && o.wpcu1w <= 32, "pcg1 waves per CU must be 0..32");
   PMX_CHECK(o.wcycle1 == 2 || o.wcycle1 == 3, "pcg1 w cycle must be 2 or 3");
   PMX_CHECK(o.pair_w >= 0 && o.pair_w <= 2, "pair_w must be 0, 1 or 2");
-  PMX_CHECK(o.algo == -1 || o.algo == 1 || o.algo == 2, "algo must be -1, 1 or 2");
+  PMX_CHECK(o.algo >= -1 && o.algo <= 3 && o.algo != 0, "algo must be -1, 1, 2 or 3");
   o.resolved = true;
   return o;
 }
@@ -129,7 +133,7 @@ GpuOptions resolve_options(const GpuOptions& in) {
 bool choose_single_pass(const ProblemSpec& spec, const ProcGrid& grid, const GpuOptions& o,
                         double device_total_bytes, int subdomains_per_device) {
   PMX_CHECK(o.resolved, "choose_single_pass needs resolve_options()");
-  if (o.algo == 2) return false;
+  if (o.algo == 2 || o.algo == 3) return false;
   // the radius-2 halo takes two owned lines from every neighbour: each block needs >= 2 x 2
   const bool thick = grid.size() == 1 || ((spec.M - 1) / grid.Px >= 2 && (spec.N - 1) / grid.Py >= 2);
   const bool ok = !o.exact && o.kernel == 1 && thick;
@@ -201,6 +205,9 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   // iteration algorithm (see GpuOptions::algo); a Session resolves it once for all its solvers
   if (opt_.algo == -1) opt_.algo = choose_single_pass(spec, sd.grid, opt_, double(total_b), 1) ? 1 : 2;
   pcg1_ = opt_.algo == 1;
+  ca_ = opt_.algo == 3;
+  PMX_CHECK(!ca_ || (opt.dtype == DType::kFp64 && !opt.exact && sd.grid.size() == 1),
+            "s-step PCG (algo 3) runs undecomposed fp64 grids with the fast arithmetic");
   PMX_CHECK(!pcg1_ || (!opt.exact && opt.kernel == 1 && (sd.grid.size() == 1 || (sd.nx >= 2 && sd.ny >= 2))),
             "pcg1 needs the wave kernels, the fast arithmetic and a subdomain of at least 2 x 2 nodes");
 
@@ -214,7 +221,7 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   field_off_ = size_t(G.pitch) + align_elems - 1;
   field_bytes_ = round_up((align_elems - 1 + size_t(sd.nx + 4) * G.pitch) * elem_, 256);
   {  // fail with a sizing message instead of a bare hipErrorOutOfMemory
-    const size_t need = estimate_device_bytes(spec, sd, opt.dtype, pcg1_);
+    const size_t need = estimate_device_bytes(spec, sd, opt.dtype, pcg1_ || ca_);
     PMX_CHECK(need <= free_b,
               "subdomain " << sd.nx << "x" << sd.ny << " (" << (pcg1_ ? "pcg1, 5" : "pcg2, 4")
                            << " fields) needs " << need / 1e9 << " GB on device " << opt.device
@@ -227,7 +234,7 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   // fields (0 ... 8 MiB of stagger) and physically contiguous memory were measured: no gain
   // (profiles/r3/placement/stagger.log); where the block lands is what matters (place_fields).
   field_stride_ = field_bytes_;
-  const int nfields = pcg1_ ? 5 : 4;
+  const int nfields = pcg1_ || ca_ ? 5 : 4;
   HIP_CHECK(hipMalloc(&fields_, size_t(nfields) * field_stride_));
   if (const char* e = std::getenv("PMX_DEBUG_ALLOC"); e && e[0] == '1')
     std::fprintf(stderr, "pmx alloc: fields %p (%zu B, mod 1G %zu, mod 2M %zu)\n", static_cast<void*>(fields_),
@@ -316,9 +323,22 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     }
   }
 
+  if (ca_) {
+    r2_ = field_raw(4);  // the second z buffer
+    ca_tiles_ = make_ca_tiles(G, opt_.ca_s, opt_.ca_rows);
+    HIP_CHECK(hipMalloc(&ca_tbl_, size_t(ca_tiles_.tiles_j) * ca_tiles_.cwords * sizeof(unsigned)));
+    ca_tiles_.tbl = ca_tbl_;
+    ca_build_classes(G, tables_, ca_tiles_, ca_tbl_, nullptr);
+    HIP_CHECK(hipStreamSynchronize(nullptr));
+    HIP_CHECK(hipMalloc(&ca_state_, sizeof(CaState)));
+    HIP_CHECK(hipMemset(ca_state_, 0, sizeof(CaState)));
+    HIP_CHECK(hipMalloc(&ca_chunk_, size_t(kReduceMaxBlocks) * ca_nq(ca_tiles_.s) * sizeof(double)));
+  }
   init_tiles_ = make_tiles(G, 256, 0);
+  // partials: 5 doubles per slot (the s-step Gram partials take ca_nq per tile)
+  const int ca_slots = ca_ ? (ca_tiles_.ntiles() * ca_nq(ca_tiles_.s) + 4) / 5 : 0;
   const size_t npart = size_t(std::max({tiles_.ntiles(), tiles_b_.ntiles(), init_tiles_.ntiles(),
-                                        pcg1_ ? std::max(tiles1_.ntiles(), tiles1w_.ntiles()) : 0}));
+                                        pcg1_ ? std::max(tiles1_.ntiles(), tiles1w_.ntiles()) : 0, ca_slots}));
   npart_ = npart;
   HIP_CHECK(hipMalloc(&partials_, (npart * 5 + kReduceWsDoubles) * sizeof(double)));
   reduce_ws_ = partials_ + npart * 5;
@@ -343,7 +363,7 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     HIP_CHECK(hipHostGetDevicePointer(&d, progress_host_, 0));
     progress_dev_ = static_cast<long long*>(d);
   }
-  if (pcg1_) place_fields();
+  if (pcg1_ || ca_) place_fields();
 }
 
 // Field placement probe.  On MI355X the same sweep runs at one of (at least) three rates depending
@@ -364,6 +384,13 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
 // (profiles/r4/placement/).  No ghost exchange (timing only); the driver's init() resets everything.
 void GpuSubdomainSolver::probe_iterations(hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   enqueue_init(s);
+  if (ca_) {  // s-step: one untimed block, then two (2 s iterations)
+    enqueue_ca_block(s, ca_tiles_.s);
+    HIP_CHECK(hipEventRecord(e0, s));
+    for (int k = 0; k < 2; ++k) enqueue_ca_block(s, ca_tiles_.s);
+    HIP_CHECK(hipEventRecord(e1, s));
+    return;
+  }
   for (int k = 0; k < 2; ++k) enqueue_phase_a(s);
   HIP_CHECK(hipEventRecord(e0, s));
   for (int k = 0; k < 6; ++k) enqueue_phase_a(s);
@@ -489,6 +516,12 @@ void GpuSubdomainSolver::release() noexcept {
   if (fields_) (void)hipFree(fields_);
   if (tile_order_) (void)hipFree(tile_order_);
   if (tile_order_w_) (void)hipFree(tile_order_w_);
+  if (ca_tbl_) (void)hipFree(ca_tbl_);
+  if (ca_state_) (void)hipFree(ca_state_);
+  if (ca_chunk_) (void)hipFree(ca_chunk_);
+  ca_tbl_ = nullptr;
+  ca_state_ = nullptr;
+  ca_chunk_ = nullptr;
   if (tables_buf_) (void)hipFree(tables_buf_);
   if (partials_) (void)hipFree(partials_);
   if (own_arena_ && arena_) (void)hipFree(arena_);
@@ -573,7 +606,7 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
   std::memset(&st, 0, sizeof(st));
   st.delta = spec_.delta;
   st.bd_tol = spec_.breakdown_tol;
-  st.it = pcg1_ ? 0 : 1;  // pcg1: sweep 0 (enqueued by the driver) forms (z^0, r^0), (A z^0, z^0)
+  st.it = pcg1_ || ca_ ? 0 : 1;  // pcg1: sweep 0 (enqueued by the driver) forms (z^0, r^0), (A z^0, z^0)
   st.halo_k = 0;          // pcg1: the first ghost exchange fills sweep 0's inputs
   st.max_iter = spec_.effective_max_iter();
   st.norm = int(spec_.norm);
@@ -594,6 +627,31 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
   after_launch(s);
   launch_reduce(partials_, init_tiles_.ntiles(), 2, 0.0, g_.h1h2, state_->red_b, state_, 0, reduce_ws_, s);
   after_launch(s);
+  if (ca_) {  // set 0: z^0 = D^-1 r^0 (in r's buffer), p^0 = z^0; block counter 0
+    if constexpr (sizeof(T) == 8) {
+      HIP_CHECK(hipMemsetAsync(ca_state_, 0, sizeof(CaState), s));
+      launch_ca_init<double>(geom_, tables_, static_cast<double*>(field_base(1)), static_cast<double*>(field_base(2)), s);
+      after_launch(s);
+    }
+  }
+}
+
+void GpuSubdomainSolver::enqueue_ca_block(hipStream_t s, int n) {
+  PMX_CHECK(ca_ && elem_ == 8, "enqueue_ca_block: not an s-step solver");
+  double* w = static_cast<double*>(field_base(0));
+  double* z0 = static_cast<double*>(field_base(1));
+  double* z1 = reinterpret_cast<double*>(r2_ + field_off_ * elem_);
+  double* p0 = static_cast<double*>(field_base(2));
+  double* p1 = static_cast<double*>(field_base(3));
+  const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
+  launch_ca_sweep<double>(geom_, tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, false, s);
+  after_launch(s);
+  launch_ca_reduce(partials_, ca_tiles_.ntiles(), ca_tiles_.s, g_.h1h2, wdiff, n, state_, ca_state_, ca_chunk_, s,
+                   progress_dev_);
+  after_launch(s);
+  launch_ca_sweep<double>(geom_, tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, true, s);
+  after_launch(s);
+  host_k_ += n;
 }
 
 template <typename T>
@@ -779,6 +837,7 @@ constexpr char kCkptMagic[8] = {'P', 'M', 'X', 'C', 'K', 'P', 'T', '1'};
 }  // namespace
 
 void GpuSubdomainSolver::save_checkpoint(std::ostream& os, hipStream_t s) const {
+  PMX_CHECK(!ca_, "not available for the s-step solver");
   HIP_CHECK(hipSetDevice(opt_.device));
   HIP_CHECK(hipStreamSynchronize(s));
   CkptHeader h{};
@@ -803,6 +862,7 @@ void GpuSubdomainSolver::save_checkpoint(std::ostream& os, hipStream_t s) const 
 }
 
 void GpuSubdomainSolver::load_checkpoint(std::istream& is, hipStream_t s) {
+  PMX_CHECK(!ca_, "not available for the s-step solver");
   HIP_CHECK(hipSetDevice(opt_.device));
   CkptHeader h{};
   is.read(reinterpret_cast<char*>(&h), sizeof(h));
@@ -846,6 +906,7 @@ void GpuSubdomainSolver::enqueue_pack(hipStream_t s) {
 }
 
 double GpuSubdomainSolver::bench_kernel(int which, int abl, int reps, hipStream_t s) {
+  PMX_CHECK(!ca_, "not available for the s-step solver");
   HIP_CHECK(hipSetDevice(opt_.device));
   PcgState& st = host_state_[1];
   std::memset(&st, 0, sizeof(st));
@@ -992,8 +1053,12 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
   for (auto* s : local_) any_nb |= s->geom().nb != 0;
   any_nb_ = any_nb;
   single_pass_ = local_[0]->single_pass();
+  ca_ = local_[0]->ca();
   for (auto* s : local_)
-    PMX_CHECK(s->single_pass() == single_pass_, "local subdomains disagree on the iteration algorithm");
+    PMX_CHECK(s->single_pass() == single_pass_ && s->ca() == ca_,
+              "local subdomains disagree on the iteration algorithm");
+  PMX_CHECK(!ca_ || (local_.size() == 1 && !any_nb && comm_->world_size() == 1),
+            "s-step PCG runs one undecomposed subdomain");
   overlap_ = any_nb && local_[0]->options().overlap;
   // Direct-row ghost exchange (row strips): no pack/unpack launches; PMX_DIRECT_ROWS=0 turns it off
   // (A/B).  Every local solver must qualify (they exchange with each other under LocalComm).
@@ -1091,6 +1156,11 @@ void PcgDriver::synchronize() {
 
 void PcgDriver::init() {
   TraceRange tr("pmx:init");
+  if (ca_) {  // fields, state and set 0 of the first block
+    local_[0]->enqueue_init(streams_[0]);
+    synchronize();
+    return;
+  }
   // pcg2's k_init packs r^0 into the send slots
   if (!single_pass_ && any_nb_) comm_->before_pack(local_, streams_);
   for (size_t i = 0; i < local_.size(); ++i) local_[i]->enqueue_init(streams_[i]);
@@ -1210,7 +1280,27 @@ void PcgDriver::join_halo() {
   halo_pending_ = false;
 }
 
+int PcgDriver::ca_batch() const {
+  const int s = local_[0]->ca_s();
+  const int b = graph_batch_ > 0 ? graph_batch_ : 16;
+  return (b + s - 1) / s * s;  // whole blocks per captured batch
+}
+
+void PcgDriver::enqueue_ca(int64_t n) {
+  const int s = local_[0]->ca_s();
+  HIP_CHECK(hipSetDevice(local_[0]->device()));
+  while (n > 0) {
+    const int m = int(std::min<int64_t>(s, n));
+    local_[0]->enqueue_ca_block(streams_[0], m);
+    n -= m;
+  }
+}
+
 void PcgDriver::enqueue_one_iteration() {
+  if (ca_) {
+    enqueue_ca(1);
+    return;
+  }
   if (split_) {
     enqueue_split_iteration();
     return;
@@ -1346,7 +1436,8 @@ hipGraphExec_t PcgDriver::build_graph(int phase, int len) {
   PMX_CHECK(!halo_pending_, "graph capture with an unjoined ghost exchange");
   PMX_GDBG("capture begun");
   try {
-    for (int k = 0; k < len; ++k) enqueue_one_iteration();
+    if (ca_) enqueue_ca(len);
+    else for (int k = 0; k < len; ++k) enqueue_one_iteration();
     join_halo();  // a captured batch is self-contained: every forked stream rejoins
   } catch (...) {  // e.g. an aborted communicator: end the capture so the stream stays usable
     halo_pending_ = false;
@@ -1406,14 +1497,15 @@ bool PcgDriver::prepare(int64_t n) {
   std::vector<long long> k0;
   for (auto* s : local_) k0.push_back(s->host_k());
   bool ok = graph_batch_ > 0 && !graph_failed_;
+  const int gb = ca_ ? ca_batch() : graph_batch_;
   int64_t done = 0;
   auto at = [&](int64_t off) {  // host counters as they will be `off` iterations from now
     for (size_t i = 0; i < local_.size(); ++i) local_[i]->set_host_k(k0[i] + off);
   };
-  while (ok && done + graph_batch_ <= n) {
+  while (ok && done + gb <= n) {
     at(done);
-    ok = graph_for(int((k0[0] + done) % cyc), graph_batch_) != nullptr;
-    done += graph_batch_;
+    ok = graph_for(int((k0[0] + done) % cyc), gb) != nullptr;
+    done += gb;
   }
   if (ok && done < n) {
     at(done);
@@ -1424,7 +1516,8 @@ bool PcgDriver::prepare(int64_t n) {
 }
 
 void PcgDriver::enqueue_eager(int64_t n) {
-  for (int64_t k = 0; k < n; ++k) enqueue_one_iteration();
+  if (ca_) enqueue_ca(n);
+  else for (int64_t k = 0; k < n; ++k) enqueue_one_iteration();
   path_.eager_iters += n;
   join_halo();
 }
@@ -1434,8 +1527,9 @@ void PcgDriver::enqueue_iterations(int64_t n) {
   const int cyc = graph_period();
   for (auto* s : local_) PMX_CHECK(s->host_k() == local_[0]->host_k(), "local solvers out of step");
   int64_t done = 0;
+  const int gb = ca_ ? ca_batch() : graph_batch_;
   while (done < n) {
-    const int len = int(std::min<int64_t>(graph_batch_, n - done));
+    const int len = int(std::min<int64_t>(gb, n - done));
     hipGraphExec_t e = len > 0 ? graph_for(int(local_[0]->host_k() % cyc), len) : nullptr;
     if (!e) break;
     PMX_GDBG("launch len %d", len);
@@ -1445,7 +1539,8 @@ void PcgDriver::enqueue_iterations(int64_t n) {
     note_graph(len);
     done += len;
   }
-  for (int64_t k = done; k < n; ++k) enqueue_one_iteration();
+  if (ca_) enqueue_ca(n - done);
+  else for (int64_t k = done; k < n; ++k) enqueue_one_iteration();
   path_.eager_iters += n - done;
   join_halo();
 }
@@ -1464,7 +1559,7 @@ RunStats PcgDriver::solve(int poll_batches, bool do_init, int64_t ckpt_every,
   if (do_init) init();
   const double t1 = now_s();
   st.init_seconds = t1 - t0;
-  const int64_t base = graph_batch_ > 0 ? graph_batch_ : 16;
+  const int64_t base = ca_ ? ca_batch() : graph_batch_ > 0 ? graph_batch_ : 16;
   const int64_t batch = base * std::max(1, poll_batches);
   const int64_t max_iter = local_[0]->spec().effective_max_iter();
   PcgState s = state(0);
@@ -1502,6 +1597,7 @@ RunStats PcgDriver::profile_phases(int64_t n) {
   // exchange of an undecomposed grid, pcg2's second half in pcg1) records no event: two back-to-back
   // timing events cost ~5 us of marker latency, which would otherwise show up as that bucket's time.
   RunStats st;
+  PMX_CHECK(!ca_, "profile_phases: not available for the s-step solver (rocprofv3 --kernel-trace times its passes)");
   HIP_CHECK(hipSetDevice(local_[0]->device()));
   hipStream_t s0 = streams_[0];
   enum Bucket { kA, kB, kRed, kAr, kHalo };

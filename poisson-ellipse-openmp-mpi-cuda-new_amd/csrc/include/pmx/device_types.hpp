@@ -90,6 +90,20 @@ struct alignas(64) PcgState {
   int w_pend_n;
 };
 
+// s-step PCG (ca_kernels.hip): the per-block scalars next to PcgState.  Basis of a block: Chebyshev
+// polynomials of L = D^-1 A in p and z, Y = [P_0..P_s, Z_0..Z_{s-1}] (2s+1 vectors); p, z and w - w_k
+// after j iterations are Y a_j, Y b_j, Y c_j.
+constexpr int kCaMaxS = 3;
+constexpr int kCaMaxNb = 2 * kCaMaxS + 1;
+struct alignas(64) CaState {
+  double coef[3][kCaMaxNb];  // a_n, b_n, c_n of the block's last applied iteration n (pass 2 reads)
+  long long blk;   // blocks applied: pass 1 reads (p, z) from set blk & 1, pass 2 writes set (blk & 1)
+  int nupd;        // iterations the current block applies (0: nothing, the solve had stopped)
+  int s;           // block size (basis degree)
+  unsigned ticket; // the reduction's last-block ticket (re-armed by the finishing block)
+  int pad;
+};
+
 // Pointers for the halo ("ghost") exchange, one per slot (see kHaloSlots).  Two-sweep iteration:
 // slots 0-3 hold one line of r (ny values for x sides, nx for y sides).  Single-pass iteration:
 // two lines of r and of p per side (4 ny / 4 nx values) and one (r, p) pair per corner.

@@ -71,7 +71,11 @@ struct GpuOptions {
   // options, device size), so every rank of a distributed run makes the same one.
   // PMX_ALGO=-1|1|2 overrides.  pcg1 matches the reference iteration counts and pcg2's solution
   // (tests/test_gpu_pcg1.py) and moves 40 instead of 56 B/pt per iteration.
+  // 3 = s-step PCG (ca_kernels.hip: s iterations per two passes and one reduction, 21.3 B/pt per
+  // iteration at s = 3; undecomposed fp64 grids), never chosen by auto.
   int algo = -1;
+  // s-step PCG: block size (2 or 3) and tile height (0 = auto).  PMX_CA_S / PMX_CA_ROWS.
+  int ca_s = 3, ca_rows = 0;
   // pcg1 tile shape (rows1 = 0: auto).  VEC=2 x 1 wave/workgroup won the 16384^2 sweeps
   // (bench/gpu_pcg1_sweep.sh; VEC=4 needs 256 VGPRs and is 35% slower).
   int vec1 = 2, waves1 = 1, rows1 = 0;
@@ -274,6 +278,12 @@ class GpuSubdomainSolver {
   const DevTables& tables() const { return tables_; }
   const TileCfg& tiles() const { return pcg1_ ? tiles1_ : tiles_; }  // pcg_a (or pcg1)
   bool single_pass() const { return pcg1_; }
+  // s-step PCG (GpuOptions::algo 3): a block of n <= ca_s() iterations is pass 1 -> reduction (+ the
+  // block's scalars) -> pass 2; host_k() counts iterations enqueued
+  bool ca() const { return ca_; }
+  int ca_s() const { return ca_ ? ca_tiles_.s : 0; }
+  const CaTiles& ca_tiles() const { return ca_tiles_; }
+  void enqueue_ca_block(hipStream_t s, int n);
   // pcg1: host mirror of the device iteration counter S->it -- the index of the next sweep this
   // solver enqueues.  init sets it to 0, every enqueued reduction (which bumps S->it on the
   // device) advances it, load_checkpoint reads it from the checkpoint.  It picks the plain or the
@@ -314,6 +324,11 @@ class GpuSubdomainSolver {
   TileCfg tiles1w_{};  // pcg1, the w-moving sweeps (GpuOptions::rows1w / pf1w)
   const TileCfg& tiles1_for(bool wsweep) const { return wsweep ? tiles1w_ : tiles1_; }
   bool pcg1_ = false;
+  bool ca_ = false;             // s-step PCG
+  CaTiles ca_tiles_{};
+  unsigned* ca_tbl_ = nullptr;  // its row-class table
+  CaState* ca_state_ = nullptr;
+  double* ca_chunk_ = nullptr;  // its reduction's chunk sums
   long long host_k_ = 0;
   bool direct_rows_ = false;
   long long halo_target_ = 0;
@@ -487,6 +502,9 @@ class PcgDriver {
 
  private:
   void enqueue_one_iteration();
+  // s-step PCG: n iterations as blocks of ca_s() (the last one shorter), graphs of ca_batch()
+  void enqueue_ca(int64_t n);
+  int ca_batch() const;
   // pack -> comm -> unpack, filling the inputs of sweep `target` (direct rows: comm only)
   void halo_exchange_pcg1(std::vector<hipStream_t>& streams, long long target);
   void set_halo_target(long long k);
@@ -494,7 +512,7 @@ class PcgDriver {
   // its parity (the exchanged spans alternate between the double buffers)
   // pcg1 with neighbours: every exchange names its target sweep's buffer parity in its launch
   // arguments (direct spans or pack/unpack), so a captured batch is only valid at its parity
-  int graph_period() const { return local_[0]->w_cycle() * (single_pass_ && any_nb_ ? 2 : 1); }
+  int graph_period() const { return ca_ ? 1 : local_[0]->w_cycle() * (single_pass_ && any_nb_ ? 2 : 1); }
   void enqueue_split_iteration();  // pcg1, decomposed, overlap: interior/frame sweep split
   void join_halo();                // compute stream waits for a pending ghost exchange
   // captured batch of `len` iterations starting at w-cycle phase `phase`, built on first use;
@@ -512,6 +530,7 @@ class PcgDriver {
   bool overlap_ = false;
   bool poison_ = false;
   bool single_pass_ = false;
+  bool ca_ = false;  // s-step PCG (one undecomposed subdomain)
   bool any_nb_ = false;
   bool direct_ = false;  // direct-row ghost exchange (GpuSubdomainSolver::set_direct_rows)
   std::vector<hipStream_t> comm_streams_;

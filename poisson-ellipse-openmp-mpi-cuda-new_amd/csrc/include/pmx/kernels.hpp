@@ -131,6 +131,32 @@ void launch_pcg1_block(const DevGeom& G, const DevTables& Tb, T* w, T* r, T* r2,
                        PcgState* S, const TileCfg& tc, hipStream_t s, bool wsweep, const double* weights = nullptr,
                        unsigned* ticket = nullptr, long long* progress = nullptr);
 
+// s-step PCG (ca_kernels.hip): s iterations per block of pass 1 (basis + Gram partials), one
+// reduction that also runs the block's scalar recurrences, and pass 2 (p, z, w updated).
+// Undecomposed fp64 grids; fields w and two (z, p) sets, the set read by a block in CaState::blk.
+struct CaTiles {
+  int s = 3;        // block size = basis degree (2 or 3)
+  int he = 4;       // extra columns loaded per side ((s + 1) & ~1)
+  int wo = 120;     // owned columns per wave tile (128 - 2 he)
+  int rows = 0;     // rows per tile
+  int tiles_i = 0, tiles_j = 0;
+  int cwords = 0;   // row-class words per tile column (16 rows each)
+  unsigned* tbl = nullptr;  // row classes (ca_build_classes), tiles_j * cwords words, owned by the caller
+  int ntiles() const { return tiles_i * tiles_j; }
+};
+CaTiles make_ca_tiles(const DevGeom& G, int s, int rows);
+int ca_nq(int s);  // Gram partials per tile
+void ca_build_classes(const DevGeom& G, const DevTables& Tb, const CaTiles& t, unsigned* tbl, hipStream_t s);
+// z = D^-1 r in place, p = z (the first block's set 0)
+template <typename T>
+void launch_ca_init(const DevGeom& G, const DevTables& Tb, T* z, T* p, hipStream_t s);
+template <typename T>
+void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, T* p0, T* p1, double* partials,
+                     const PcgState* S, const CaState* C, const CaTiles& t, bool upd, hipStream_t s);
+// chunk: kReduceMaxBlocks * ca_nq(s) doubles of workspace; nmax: iterations this block may run
+void launch_ca_reduce(const double* partials, int n, int s_, double h, double wdiff, int nmax, PcgState* S,
+                      CaState* C, double* chunk, hipStream_t s, long long* progress = nullptr);
+
 // pcg1 ghost exchange: pack (unpack=false) the radius-2 edges of the buffers sweep `target` reads
 // (parity of target) into H.send, or unpack H.recv into their ghost cells.
 #ifdef PMX_WAVE_TRACE

@@ -81,7 +81,8 @@ def make_session(problem: PoissonEllipse, ranks: int = 1, split: str = "referenc
                  tile_rows: int = 0, exact: bool = False, graph_batch: int = 32, check: bool = False,
                  overlap: bool = True, vec_b: int = 0, waves_b: int = 0, tile_rows_b: int = -1,
                  poison_halos: bool = False, b_ring: bool = False, placement: int = 0,
-                 placement_budget_s: float = 0.5, placement_keep_free: float = 0.5, block_tiles: int = -1):
+                 placement_budget_s: float = 0.5, placement_keep_free: float = 0.5, block_tiles: int = -1,
+                 algo: str | int = -1, ca_s: int = 3):
     """Native GPU session with `ranks` subdomains on one device (LocalComm when ranks > 1).
 
     overlap: ghost exchange on a second stream concurrent with pcg_b (only matters for ranks > 1).
@@ -96,15 +97,19 @@ def make_session(problem: PoissonEllipse, ranks: int = 1, split: str = "referenc
     device memory free -- see GpuSubdomainSolver::place_fields).
 
     block_tiles: -1 = auto (block-tile sweeps, pcg1_block.hip, on small undecomposed fp64 grids), 0 = off,
-    1 = on for any undecomposed fp64 grid."""
+    1 = on for any undecomposed fp64 grid.
+
+    algo: -1 = auto (pcg1 / pcg2), "pcg1" / 1, "pcg2" / 2, or "ca" / 3 -- the s-step PCG
+    (ca_kernels.hip: ca_s = 2 or 3 iterations per two passes and one reduction; undecomposed fp64)."""
     n = _native()
+    algo = {"auto": -1, "pcg1": 1, "pcg2": 2, "ca": 3}.get(algo, algo) if isinstance(algo, str) else algo
     return n.Session(problem.to_native(), world=int(ranks), comm="self" if ranks == 1 else "local",
                      split=getattr(n.Split, split), device=device, kernel=kernel, block=block, vec=vec,
                      waves=waves, tile_rows=tile_rows, dtype=dtype, exact=exact, graph_batch=graph_batch,
                      check=check, overlap=overlap, vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b,
                      poison_halos=poison_halos, b_ring=b_ring, placement=placement,
                      placement_budget_s=placement_budget_s, placement_keep_free=placement_keep_free,
-                     block_tiles=block_tiles)
+                     block_tiles=block_tiles, algo=int(algo), ca_s=int(ca_s))
 
 
 def solve_hip(problem: PoissonEllipse, ranks: int = 1, keep_solution: bool = True, poll_batches: int = 1,

@@ -36,6 +36,7 @@ HIP_SOURCES = [
     "hip/pcg_kernels_dpp.hip",
     "hip/pcg1_kernels.hip",
     "hip/pcg1_block.hip",
+    "hip/ca_kernels.hip",
     "hip/ops_kernels.hip",
     "hip/gpu_solver.hip",
     "hip/session.hip",
