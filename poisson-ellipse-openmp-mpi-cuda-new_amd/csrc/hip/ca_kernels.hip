@@ -4,28 +4,35 @@
 // Same iteration as the reference (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:847-943; z = D^-1 r,
 // alpha = (r, z) / (A p, p), w += alpha p, r -= alpha A p, beta = (r', z') / (r, z), p = z' + beta p,
 // stop when ||w^{k+1} - w^k|| = |alpha| ||p|| < delta), regrouped by blocks of s iterations.  In
-// the D-inner product <x, y> = x^T D y the preconditioned operator L = D^-1 A is self-adjoint, and
+// the D-inner product <x, y>_D = x^T D y the preconditioned operator L = D^-1 A is self-adjoint, and
 // after j < s iterations of a block p, z = D^-1 r and w - w_k lie in the span of the Krylov basis
-//   Y = [P_0 .. P_s, Z_0 .. Z_{s-1}],  P_i = T_i(L - I) p_k,  Z_i = T_i(L - I) z_k
-// (Chebyshev polynomials T_i: L - I has its spectrum in (-1, 1) -- Gershgorin on the M-matrix A --
-// so the basis stays well conditioned; a monomial basis would not).  With p = Y a, z = Y b,
+//   Y = [P_0 .. P_s, Z_0 .. Z_{s-1}],  P_i = T_i(L~) p_k,  Z_i = T_i(L~) z_k,  L~ = L - I
+// (Chebyshev polynomials T_i: L~ has its spectrum in (-1, 1) -- Gershgorin on the M-matrix A -- so
+// the basis stays well conditioned; a monomial basis would not).  With p = Y a, z = Y b,
 // w - w_k = Y c and L Y = Y T (T: the Chebyshev three-term recurrence, exact in the columns that stay
-// in the basis), every scalar of the s iterations comes from two small Gram matrices:
-//   (r, z) = b^T G_D b,   (A p, p) = a^T G_D T a,   ||p||^2 = a^T G_0 a,
-//   G_D = Y^T D Y (all 2s+1 vectors),  G_0 = Y^T Y (the 2s-1 vectors p can use, P_0..P_{s-1}, Z_0..Z_{s-2}).
-// So a block is:
-//   pass 1 (k_ca_sweep<.., false>): per tile, the basis on the fly from p_k, z_k (radius s) and
-//          the (2s+1)(2s+2)/2 + (2s-1)2s/2 Gram partials (s = 3: 28 + 15);
-//   reduce (k_ca_reduce): the partials summed in a fixed order, then ONE lane runs the s iterations
-//          on the coefficient vectors (alpha, beta, the breakdown guard and the stop test of every
-//          iteration, exactly where the classic loop has them) and leaves a_n, b_n, c_n in CaState;
-//   pass 2 (k_ca_sweep<.., true>): the basis again, p = Y a_n, z = Y b_n, w += Y c_n.
+// in the basis), alpha's numerator and denominator come from one Gram matrix:
+//   (r, z) = b^T G b,   (A p, p) = a^T G T a,   G = Y^T D Y,
+// and G itself from 6s products: the Chebyshev product rule T_a T_b = (T_{a+b} + T_{|a-b|}) / 2 and
+// the D-self-adjointness of L~ give <P_a, P_b>_D = (mu_{a+b} + mu_{|a-b|}) / 2 with
+// mu_m = <T_m(L~) p, p>_D (likewise nu for z, rho for <T_m p, z>_D); mu_0..mu_s are products with P_0,
+// the higher moments come from <P_i, P_j> with i + j = m (s = 3: 18 products for 28 entries).
+// The stop test needs the plain norm ||p_{k+j}||, which has no such symmetry: pass 2 forms
+// p_{k+j} = Y a_j explicitly and sums its squares, and the test of a block's iterations runs in the
+// NEXT reduction (or in a check after the last block of a batch).  A stop at iteration j < n of a
+// block rewinds w to w_k + Y c_{j+1} with one more pass over the block's inputs, which are still intact
+// (the next pass 2 has not overwritten that set).  So a block is:
+//   pass 1 (k_ca_sweep<.., false>): per tile, the basis on the fly from p_k, z_k (radius s) and the
+//          6s Gram products;
+//   reduce (k_ca_reduce): the partials summed in a fixed order, then ONE lane runs the pending stop
+//          test of the previous block and the s iterations of this one on the coefficient vectors
+//          (alpha, beta, the breakdown guard, max_iter) and leaves a_n, b_n, c_n in CaState;
+//   pass 2 (k_ca_sweep<.., true>): the basis again, p = Y a_n, z = Y b_n, w += Y c_n, ||Y a_j||^2.
 // HBM traffic per block: pass 1 reads p, z (16 B/pt), pass 2 reads p, z, w and writes them (48 B/pt):
 // 64 B/pt for s iterations -- 21.3 B/pt/iteration at s = 3 against pcg1's 37.3.  The price is
-// arithmetic: 2 x (2s - 1) stencils and ~50 Gram FMAs per point and block.
+// arithmetic: 2 x (2s - 1) stencils and ~6s Gram FMAs per point and block.
 // The iterates equal the classic loop's in exact arithmetic; in fp64 the Gram-based scalars differ
 // at rounding level, and every reference iteration count (546 / 989 / 1858 / 2449) and 16384^2's
-// 10,363 is reproduced (tests/test_gpu_ca.py, bench/probe/ca_pcg_proto.py).
+// 10,363 is reproduced (tests/test_gpu_ca.py; models/sstep_pcg.py is the PyTorch statement).
 //
 // Mapping (CDNA4): one wave64 marches a tile of TI rows x WO owned columns, 2 columns per lane.  The
 // dependency radius is s in both directions: the tile loads HE >= s extra columns per side (HE even,
@@ -58,20 +65,33 @@ namespace {
 
 template <int S>
 struct CaShape {
-  static constexpr int NB = 2 * S + 1;           // basis vectors
-  static constexpr int NGD = NB * (NB + 1) / 2;  // G_D upper triangle
-  static constexpr int N0 = 2 * S - 1;           // vectors of G_0: P_0..P_{S-1}, Z_0..Z_{S-2}
-  static constexpr int NG0 = N0 * (N0 + 1) / 2;
-  static constexpr int NQ = NGD + NG0;           // partials per tile
-  static constexpr int HE = (S + 1) & ~1;        // extra columns per side (even: aligned chunks)
-  static constexpr int WO = 128 - 2 * HE;        // owned columns per wave tile (2 per lane)
+  static constexpr int NB = 2 * S + 1;     // basis vectors
+  static constexpr int NQ = 6 * S;         // Gram products per tile (pass 1)
+  static constexpr int NN = S;             // ||p_{k+j}||^2 partials per tile (pass 2)
+  static constexpr int HE = (S + 1) & ~1;  // extra columns per side (even: aligned chunks)
+  static constexpr int WO = 128 - 2 * HE;  // owned columns per wave tile (2 per lane)
   static constexpr int AGES = S + 1 > 3 ? S + 1 : 3;  // rows of every level kept in the window
 };
 
-// G_0 position of basis vector i (-1: not in G_0)
+// Gram product q = <Y_i, Y_j>_D (basis index: P_m = m, Z_m = S + 1 + m), in the order
+//   mu:  <P_m, P_0> m = 0..S, then <P_{(m+1)/2}, P_{m/2}> m = S+1..2S
+//   nu:  <Z_m, Z_0> m = 0..S-1, then <Z_{(m+1)/2}, Z_{m/2}> m = S..2S-2
+//   rho: <P_m, Z_0> m = 0..S, then <P_S, Z_b> b = 1..S-1
 template <int S>
-__host__ __device__ constexpr int ca_g0_pos(int i) {
-  return i < S ? i : (i > S && i < 2 * S) ? i - 1 : -1;
+__host__ __device__ constexpr int ca_prod_i(int q) {
+  if (q <= 2 * S) return q <= S ? q : (q + 1) / 2;
+  q -= 2 * S + 1;
+  if (q <= 2 * S - 2) return S + 1 + (q <= S - 1 ? q : (q + 1) / 2);
+  q -= 2 * S - 1;
+  return q <= S ? q : S;
+}
+template <int S>
+__host__ __device__ constexpr int ca_prod_j(int q) {
+  if (q <= 2 * S) return q <= S ? 0 : q / 2;
+  q -= 2 * S + 1;
+  if (q <= 2 * S - 2) return S + 1 + (q <= S - 1 ? 0 : q / 2);
+  q -= 2 * S - 1;
+  return q <= S ? S + 1 : S + 1 + (q - S);
 }
 
 // Per-wave constants of the uniform-stencil formula: at a point whose four faces are equal,
@@ -173,20 +193,31 @@ __device__ __forceinline__ void ca_diag(int ucls, int gi, const CaK& K, const De
   }
 }
 
+// Wave lane shift of a double with zero fill at the edge lane (DPP bound_ctrl: no old value to set up)
+template <int CTRL>
+__device__ __forceinline__ double dpp_shift0(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp(int(b), CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(int(b >> 32), CTRL, 0xf, 0xf, true);
+  return __longlong_as_double((long long)(unsigned)lo | ((long long)hi << 32));
+}
+
 template <typename T, int S, bool UPD>
 struct CaRow {
   T p[2], z[2], w[2];
 };
 
-// One wave's march over one tile (see the header).  UPD = false: Gram partials into acc; true:
-// p, z, w updated with the block's coefficient vectors ca / cb / cc.
-template <typename T, int S, bool UPD, bool FAST>
+// One wave's march over one tile (see the header).  UPD = false: the Gram products into acc; true:
+// p, z, w updated with the block's coefficient vectors ca / cb / cc and ||Y pa_j||^2 into acc
+// (REW: w += Y cc only).
+template <typename T, int S, bool UPD, bool FAST, int PF, bool REW>
 __device__ __forceinline__ void ca_march(const DevGeom& G, const DevTables& Tb, const CaK& K,
                                          const T* __restrict__ pin, const T* __restrict__ zin, T* __restrict__ pout,
                                          T* __restrict__ zout, T* __restrict__ w, int i0, int i1, int j0, int j1,
                                          const unsigned* __restrict__ ctbl, const double* scol,
                                          double (&acc)[CaShape<S>::NQ], const double (&ca)[CaShape<S>::NB],
-                                         const double (&cb)[CaShape<S>::NB], const double (&cc)[CaShape<S>::NB]) {
+                                         const double (&cb)[CaShape<S>::NB], const double (&cc)[CaShape<S>::NB],
+                                         const double (&pa)[S][CaShape<S>::NB]) {
   using Sh = CaShape<S>;
   constexpr int NB = Sh::NB, A = Sh::AGES;
   const int64_t P = G.pitch;
@@ -217,106 +248,85 @@ __device__ __forceinline__ void ca_march(const DevGeom& G, const DevTables& Tb, 
     }
   };
 
-  // windows: X[l][a] = level l at row (m - l - a) after step m
-  double XP[S + 1][A][2], XZ[S][A][2];
+  // windows: level l at row r sits in slot (r - mfirst) & 3 of X[l] (every level keeps at most 4
+  // consecutive rows alive), and the march is unrolled by 4, so every slot index is a compile-time
+  // constant and no row is ever moved between registers
+  static_assert(Sh::AGES <= 4, "ca_march: window deeper than 4 rows");
+  double XP[S + 1][4][2], XZ[S][4][2];
 #pragma unroll
   for (int l = 0; l <= S; ++l)
 #pragma unroll
-    for (int a = 0; a < A; ++a) XP[l][a][0] = XP[l][a][1] = 0.0;
+    for (int a = 0; a < 4; ++a) XP[l][a][0] = XP[l][a][1] = 0.0;
 #pragma unroll
   for (int l = 0; l < S; ++l)
 #pragma unroll
-    for (int a = 0; a < A; ++a) XZ[l][a][0] = XZ[l][a][1] = 0.0;
-  int ch[S + 1];  // class of rows m, m-1, .., m-S
-#pragma unroll
-  for (int a = 0; a <= S; ++a) ch[a] = 0;
+    for (int a = 0; a < 4; ++a) XZ[l][a][0] = XZ[l][a][1] = 0.0;
+  int ch[4] = {0, 0, 0, 0};  // row classes, same slots
 
   const int mfirst = i0 - S, mlast = i1 + S;
-  // one level of a chain: X[l][0] (row m - l) from X[l-1] rows m-l-1 .. m-l+1 and X[l-2] row m-l
-  auto level = [&](auto& X, int l, int m) {
+  // one level of a chain at step m (slot q = (m - mfirst) & 3): level l at row m - l from level l-1
+  // at rows m-l-1 .. m-l+1 and level l-2 at row m-l
+  auto level = [&](auto& X, auto lc, auto qc, int m) {
+    constexpr int l = decltype(lc)::value, q = decltype(qc)::value;
+    constexpr int sc = (q - l) & 3, sm = (q - l - 1) & 3, sp = (q - l + 1) & 3;
     const int r = m - l;
-    const double(&ctr)[2] = X[l - 1][1];
-    const double left = dpp_shift<kWaveShr1>(ctr[1], 0.0);
-    const double right = dpp_shift<kWaveShl1>(ctr[0], 0.0);
+    const double(&ctr)[2] = X[l - 1][sc];
+    const double left = dpp_shift0<kWaveShr1>(ctr[1]);
+    const double right = dpp_shift0<kWaveShl1>(ctr[0]);
     double lt[2];
-    ca_lt(ch[l], grow(r), ctr, X[l - 1][2], X[l - 1][0], left, right, K, G, Tb, scol, lane, gj, lt);
+    ca_lt(ch[sc], grow(r), ctr, X[l - 1][sm], X[l - 1][sp], left, right, K, G, Tb, scol, lane, gj, lt);
     const bool rin = FAST || interior_row(r);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const double v = l == 1 ? lt[u] : __builtin_fma(2.0, lt[u], -X[l >= 2 ? l - 2 : 0][2][u]);
-      X[l][0][u] = (FAST || (rin && colin[u])) ? v : 0.0;
+      double v;
+      if constexpr (l == 1) v = lt[u];
+      else v = __builtin_fma(2.0, lt[u], -X[l - 2][sc][u]);
+      X[l][sc][u] = (FAST || (rin && colin[u])) ? v : 0.0;
     }
   };
 
-  auto core = [&](int m, const CaRow<T, S, UPD>& cur) {
-    // shift the windows and the class history
-#pragma unroll
-    for (int a = A - 1; a >= 1; --a) {
-#pragma unroll
-      for (int l = 0; l <= S; ++l) {
-        XP[l][a][0] = XP[l][a - 1][0];
-        XP[l][a][1] = XP[l][a - 1][1];
-      }
-#pragma unroll
-      for (int l = 0; l < S; ++l) {
-        XZ[l][a][0] = XZ[l][a - 1][0];
-        XZ[l][a][1] = XZ[l][a - 1][1];
-      }
-    }
-#pragma unroll
-    for (int a = S; a >= 1; --a) ch[a] = ch[a - 1];
-    ch[0] = ca_row_cls(ctbl, m);
+  auto core = [&](auto qc, int m, const CaRow<T, S, UPD>& cur) {
+    constexpr int q = decltype(qc)::value;
+    ch[q] = ca_row_cls(ctbl, m);
     const bool rin = FAST || interior_row(m);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const bool in = FAST || (rin && colin[u]);
-      XP[0][0][u] = in ? double(cur.p[u]) : 0.0;
-      XZ[0][0][u] = in ? double(cur.z[u]) : 0.0;
+      XP[0][q][u] = in ? double(cur.p[u]) : 0.0;
+      XZ[0][q][u] = in ? double(cur.z[u]) : 0.0;
     }
-#pragma unroll
-    for (int l = 1; l <= S; ++l) level(XP, l, m);
-#pragma unroll
-    for (int l = 1; l < S; ++l) level(XZ, l, m);
+    static_for_while<S>([&](auto l1) {
+      level(XP, std::integral_constant<int, decltype(l1)::value + 1>{}, qc, m);
+      return true;
+    });
+    static_for_while<S - 1>([&](auto l1) {
+      level(XZ, std::integral_constant<int, decltype(l1)::value + 1>{}, qc, m);
+      return true;
+    });
     // row g = m - S: every level of both chains
     const int g = m - S;
     if (g < i0 || g > i1) return;
+    constexpr int sg = (q - S) & 3;
     double Y[NB][2];
 #pragma unroll
     for (int l = 0; l <= S; ++l) {
-      Y[l][0] = XP[l][S - l][0];
-      Y[l][1] = XP[l][S - l][1];
+      Y[l][0] = XP[l][sg][0];
+      Y[l][1] = XP[l][sg][1];
     }
 #pragma unroll
     for (int l = 0; l < S; ++l) {
-      Y[S + 1 + l][0] = XZ[l][S - l][0];
-      Y[S + 1 + l][1] = XZ[l][S - l][1];
+      Y[S + 1 + l][0] = XZ[l][sg][0];
+      Y[S + 1 + l][1] = XZ[l][sg][1];
     }
     if constexpr (!UPD) {
       double d[2];
-      ca_diag(ch[S], grow(g), K, G, Tb, scol, lane, gj, d);
+      ca_diag(ch[sg], grow(g), K, G, Tb, scol, lane, gj, d);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         if (!(FAST || own[u])) continue;
-        int q = 0;
 #pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          const double dy = d[u] * Y[j][u];
-#pragma unroll
-          for (int i = 0; i <= j; ++i) {
-            acc[q] = __builtin_fma(Y[i][u], dy, acc[q]);
-            ++q;
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          if (ca_g0_pos<S>(j) < 0) continue;
-#pragma unroll
-          for (int i = 0; i <= j; ++i) {
-            if (ca_g0_pos<S>(i) < 0) continue;
-            acc[q] = __builtin_fma(Y[i][u], Y[j][u], acc[q]);
-            ++q;
-          }
-        }
+        for (int q = 0; q < Sh::NQ; ++q)  // the compiler shares d * Y_j between products
+          acc[q] = __builtin_fma(Y[ca_prod_i<S>(q)][u], d[u] * Y[ca_prod_j<S>(q)][u], acc[q]);
       }
     } else {
       T pn[2], zn[2], wn[2];
@@ -325,39 +335,73 @@ __device__ __forceinline__ void ca_march(const DevGeom& G, const DevTables& Tb, 
         double sp = 0.0, sz = 0.0, sw = double(cur.w[u]);
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
-          sp = __builtin_fma(ca[i], Y[i][u], sp);
-          sz = __builtin_fma(cb[i], Y[i][u], sz);
+          if constexpr (!REW) {
+            sp = __builtin_fma(ca[i], Y[i][u], sp);
+            sz = __builtin_fma(cb[i], Y[i][u], sz);
+          }
           sw = __builtin_fma(cc[i], Y[i][u], sw);
         }
         pn[u] = static_cast<T>(sp);
         zn[u] = static_cast<T>(sz);
         wn[u] = static_cast<T>(sw);
+        if constexpr (!REW) {
+          // ||p_{k+j}||^2, p_{k+j} = Y a_j: a_j lives on P_0..P_j, Z_0..Z_{j-1} (a_0 = e_0)
+          if (FAST || own[u]) {
+            acc[0] = __builtin_fma(Y[0][u], Y[0][u], acc[0]);
+#pragma unroll
+            for (int j = 1; j < S; ++j) {
+              double v = 0.0;
+#pragma unroll
+              for (int i = 0; i <= j; ++i) v = __builtin_fma(pa[j][i], Y[i][u], v);
+#pragma unroll
+              for (int i = 0; i < j; ++i) v = __builtin_fma(pa[j][S + 1 + i], Y[S + 1 + i][u], v);
+              acc[j] = __builtin_fma(v, v, acc[j]);
+            }
+          }
+        }
       }
       if (FAST ? own_all : own_any) {
         const int64_t o = int64_t(g) * P;
-        ca_store2<T>(pout + o, c0, pn, FAST || own_all, own);
-        ca_store2<T>(zout + o, c0, zn, FAST || own_all, own);
+        if constexpr (!REW) {
+          ca_store2<T>(pout + o, c0, pn, FAST || own_all, own);
+          ca_store2<T>(zout + o, c0, zn, FAST || own_all, own);
+        }
         ca_store2<T>(w + o, c0, wn, FAST || own_all, own);
       }
     }
   };
 
-  // two row buffers: step m reads one and refills the other one row ahead (unconditional loads,
-  // the last row re-read past the end)
-  CaRow<T, S, UPD> buf[2];
-  fetch(mfirst, buf[0]);
-  for (int m = mfirst; m <= mlast; m += 2) {
-    fetch(min(m + 1, mlast), buf[1]);
-    core(m, buf[0]);
-    if (m + 1 > mlast) break;
-    fetch(min(m + 2, mlast), buf[0]);
-    core(m + 1, buf[1]);
+  // PF + 1 row buffers: step m reads one and refills the one step m - 1 consumed with row m + PF
+  // (unconditional loads, the last row re-read past the end).  Unrolled by 4 = the window depth
+  // (and a multiple of PF + 1), so the window shifts and the ring are register renames, not moves.
+  static_assert(PF == 1 || PF == 3, "ca_march: prefetch depth 1 or 3");
+  constexpr int NBUF = PF + 1;
+  CaRow<T, S, UPD> buf[NBUF];
+#pragma unroll
+  for (int q = 0; q < PF; ++q) fetch(min(mfirst + q, mlast), buf[q]);
+  bool more = true;
+  for (int m = mfirst; more && m <= mlast; m += 4) {
+    more = static_for_while<4>([&](auto qc) {
+      constexpr int q = decltype(qc)::value;
+      if (m + q > mlast) return false;
+      fetch(min(m + q + PF, mlast), buf[(q + PF) % NBUF]);
+      core(qc, m + q, buf[q % NBUF]);
+      return true;
+    });
   }
-  if constexpr (FAST && !UPD) {  // only the lanes that own both columns summed
+  if constexpr (FAST) {  // only the lanes that own both columns summed
 #pragma unroll
     for (int q = 0; q < Sh::NQ; ++q) acc[q] = own_all ? acc[q] : 0.0;
   }
 }
+
+#ifndef PMX_CA_PF_GRAM
+#define PMX_CA_PF_GRAM 3
+#endif
+#ifndef PMX_CA_PF_UPD
+#define PMX_CA_PF_UPD 1
+#endif
+constexpr int kCaPfGram = PMX_CA_PF_GRAM, kCaPfUpd = PMX_CA_PF_UPD;
 
 template <int S, bool UPD>
 constexpr int ca_min_waves() {
@@ -376,19 +420,23 @@ k_ca_sweep(DevGeom G, DevTables Tb, T* w, T* z0, T* z1, T* p0, T* p1, double* __
   const int done = ((CPS*)St)->done;    // NOLINT
   const long long blk = ((CCS*)C)->blk;  // NOLINT
   const int nupd = ((CCS*)C)->nupd;      // NOLINT
-  double ca[NB], cb[NB], cc[NB];
+  double ca[NB], cb[NB], cc[NB], pa[S][NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) {
     ca[i] = UPD ? ((CCS*)C)->coef[0][i] : 0.0;  // NOLINT
     cb[i] = UPD ? ((CCS*)C)->coef[1][i] : 0.0;  // NOLINT
     cc[i] = UPD ? ((CCS*)C)->coef[2][i] : 0.0;  // NOLINT
+#pragma unroll
+    for (int j = 0; j < S; ++j) pa[j][i] = UPD ? ((CCS*)C)->pa[j][i] : 0.0;  // NOLINT
   }
   if (UPD ? nupd == 0 : done != 0) return;
+  const int ntiles = int(gridDim.x);
   const int id = xcd_remap(blockIdx.x, gridDim.x);
   const int ti = id / tiles_j, tj = id - ti * tiles_j;
   const int i0 = 1 + ti * TI, i1 = min(i0 + TI - 1, G.nx);
   const int j0 = 1 + tj * Sh::WO, j1 = min(j0 + Sh::WO - 1, G.ny);
   // pass 1 reads set blk & 1; pass 2 runs after the reduction advanced blk: reads set (blk - 1) & 1
+  // (a rewind leaves blk alone: the set the stopped block read)
   const int in = int((UPD ? blk - 1 : blk) & 1);
   const T* pin = in ? p1 : p0;
   const T* zin = in ? z1 : z0;
@@ -415,18 +463,30 @@ k_ca_sweep(DevGeom G, DevTables Tb, T* w, T* z0, T* z1, T* p0, T* p1, double* __
   double acc[Sh::NQ];
 #pragma unroll
   for (int q = 0; q < Sh::NQ; ++q) acc[q] = 0.0;
-  if (fast)
-    ca_march<T, S, UPD, true>(G, Tb, K, pin, zin, pout, zout, w, i0, i1, j0, j1, tbl, scol, acc, ca, cb, cc);
-  else
-    ca_march<T, S, UPD, false>(G, Tb, K, pin, zin, pout, zout, w, i0, i1, j0, j1, tbl, scol, acc, ca, cb, cc);
-  if constexpr (!UPD) {
-#pragma unroll
-    for (int q = 0; q + 1 < Sh::NQ; q += 2) wave_sum2_mfma(acc[q], acc[q + 1]);
-    if constexpr (Sh::NQ & 1) acc[Sh::NQ - 1] = wave_sum_mfma(acc[Sh::NQ - 1]);
-    if (lane == 0) {
-#pragma unroll
-      for (int q = 0; q < Sh::NQ; ++q) partials[int64_t(Sh::NQ) * id + q] = acc[q];
+  // rows in flight: pass 1 (2 fields, compute-heavy) 3 rows ahead; pass 2 (3 fields) 1
+  constexpr int PF = UPD ? kCaPfUpd : kCaPfGram;
+#define PMX_CA_MARCH(F, R) \
+  ca_march<T, S, UPD, F, PF, R>(G, Tb, K, pin, zin, pout, zout, w, i0, i1, j0, j1, tbl, scol, acc, ca, cb, cc, pa)
+  if constexpr (UPD) {
+    if (nupd < 0) {  // rewind: w only
+      if (fast) PMX_CA_MARCH(true, true);
+      else PMX_CA_MARCH(false, true);
+      return;
     }
+  }
+  if (fast) PMX_CA_MARCH(true, false);
+  else PMX_CA_MARCH(false, false);
+#undef PMX_CA_MARCH
+  // partials, one array per quantity: Gram products q (pass 1) at [q][tile], norms j (pass 2) at
+  // [NQ + j][tile]
+  constexpr int NOUT = UPD ? Sh::NN : Sh::NQ;
+  constexpr int OFF = UPD ? Sh::NQ : 0;
+#pragma unroll
+  for (int q = 0; q + 1 < NOUT; q += 2) wave_sum2_mfma(acc[q], acc[q + 1]);
+  if constexpr (NOUT & 1) acc[NOUT - 1] = wave_sum_mfma(acc[NOUT - 1]);
+  if (lane == 0) {
+#pragma unroll
+    for (int q = 0; q < NOUT; ++q) partials[int64_t(OFF + q) * ntiles + id] = acc[q];
   }
 }
 
@@ -468,41 +528,88 @@ __global__ void __launch_bounds__(256) k_ca_init(DevGeom G, DevTables Tb, T* z, 
   p[o] = static_cast<T>(v);
 }
 
-// The block's scalars from the reduced Gram sums t (raw): the s iterations of the classic loop on
-// the coefficient vectors, in the classic order of tests (max_iter, breakdown guard, stop test).
+// The scalars of one reduction: first the pending stop test of the previous block (its ||p_{k+j}||^2
+// sums u, its alpha_j from CaState), then -- unless the solve ended there or check_only -- the s
+// iterations of this block on the coefficient vectors, from the Gram products t (raw sums), in the
+// classic loop's order of tests (max_iter, the |denominator| guard; the stop test follows in the next
+// reduction).  One lane; writes CaState (pass 2's coefficients and mode) and the PcgState outcome.
 template <int S>
-__device__ void ca_finish(const double* t, double h, double wdiff, int nmax, PcgState* St, CaState* C) {
+__device__ void ca_finish(const double* t, const double* u, double h, double wdiff, int nmax, bool check_only,
+                          PcgState* St, CaState* C) {
   using Sh = CaShape<S>;
   constexpr int NB = Sh::NB;
-  if (St->done) {
-    C->nupd = 0;
+  C->nupd = 0;
+  if (St->done) return;
+  // ---- (i) the pending stop test: ||w^{k+j+1} - w^{k+j}|| = |alpha_j| ||p_{k+j}||
+  if (C->pend_n > 0) {
+    const int n = C->pend_n;
+    double diff = 0.0;
+    for (int j = 0; j < n; ++j) {
+      diff = fabs(C->alpha[j]) * sqrt(u[j] * wdiff);
+      const bool bad = !(diff == diff);
+      if (bad || diff < St->delta) {
+        const long long kk = C->pend_k + j + 1;
+        if (j + 1 < n) {  // w went past the stop: back to w_k + Y c_{j+1}
+          for (int i = 0; i < NB; ++i) C->coef[2][i] = C->pc[j][i] - C->pc[n - 1][i];
+          C->nupd = -1;
+        }
+        St->it = kk;
+        St->iters = kk;
+        St->diff = diff;
+        St->status = bad ? int(Status::kBreakdown) : int(Status::kConverged);
+        if (bad) St->nan_flag = 1;
+        St->done = 1;
+        C->pend_n = 0;
+        return;
+      }
+    }
+    St->diff = diff;
+    C->pend_n = 0;
+    if (C->after_status != 0) {  // the pending block ended at a breakdown or at max_iter
+      St->iters = C->after_iters;
+      St->status = C->after_status;
+      St->done = 1;
+      C->after_status = 0;
+      return;
+    }
+  }
+  if (check_only) return;
+  // ---- (ii) this block's iterations
+  const long long k = St->it;
+  const long long left = St->max_iter - k;
+  if (left <= 0) {
+    St->iters = k;
+    St->status = int(Status::kMaxIter);
+    St->done = 1;
     return;
   }
-  double GD[NB][NB], G0[NB][NB];
-  {
-    int q = 0;
-    for (int j = 0; j < NB; ++j)
-      for (int i = 0; i <= j; ++i) {
-        GD[i][j] = GD[j][i] = t[q++] * h;
-      }
-    for (int j = 0; j < NB; ++j)
-      for (int i = 0; i < NB; ++i) G0[i][j] = 0.0;
-    for (int j = 0; j < NB; ++j) {
-      if (ca_g0_pos<S>(j) < 0) continue;
-      for (int i = 0; i <= j; ++i) {
-        if (ca_g0_pos<S>(i) < 0) continue;
-        G0[i][j] = G0[j][i] = t[q++] * wdiff;
-      }
-    }
+  const int nm = int(left < nmax ? left : nmax);
+  // G = Y^T D Y from the moments (see the header)
+  double mu[2 * S + 1], nu[2 * S - 1], rho[2 * S];
+  bool nan = false;
+  for (int q = 0; q < Sh::NQ; ++q) nan |= !(t[q] == t[q]) || isinf(t[q]);
+  for (int m = 0; m <= S; ++m) mu[m] = t[m] * h;
+  for (int m = S + 1; m <= 2 * S; ++m) mu[m] = 2.0 * t[m] * h - mu[m & 1];
+  for (int m = 0; m < S; ++m) nu[m] = t[2 * S + 1 + m] * h;
+  for (int m = S; m <= 2 * S - 2; ++m) nu[m] = 2.0 * t[2 * S + 1 + m] * h - nu[m & 1];
+  for (int m = 0; m <= S; ++m) rho[m] = t[4 * S + m] * h;
+  for (int b = 1; b < S; ++b) rho[S + b] = 2.0 * t[5 * S + b] * h - rho[S - b];
+  double Gm[NB][NB];
+  for (int a = 0; a <= S; ++a) {
+    for (int b = 0; b <= S; ++b) Gm[a][b] = 0.5 * (mu[a + b] + mu[a > b ? a - b : b - a]);
+    for (int b = 0; b < S; ++b)
+      Gm[a][S + 1 + b] = Gm[S + 1 + b][a] = 0.5 * (rho[a + b] + rho[a > b ? a - b : b - a]);
   }
-  auto quad = [&](const double (&M)[NB][NB], const double* x, const double* y) {
-    double s = 0.0;
+  for (int a = 0; a < S; ++a)
+    for (int b = 0; b < S; ++b) Gm[S + 1 + a][S + 1 + b] = 0.5 * (nu[a + b] + nu[a > b ? a - b : b - a]);
+  auto quad = [&](const double* x, const double* y) {
+    double r = 0.0;
     for (int i = 0; i < NB; ++i) {
-      double r = 0.0;
-      for (int j = 0; j < NB; ++j) r = __builtin_fma(M[i][j], y[j], r);
-      s = __builtin_fma(x[i], r, s);
+      double v = 0.0;
+      for (int j = 0; j < NB; ++j) v = __builtin_fma(Gm[i][j], y[j], v);
+      r = __builtin_fma(x[i], v, r);
     }
-    return s;
+    return r;
   };
   // L Y = Y T: L P_0 = P_0 + P_1, L P_i = P_i + (P_{i-1} + P_{i+1}) / 2; the same for Z
   auto shiftT = [&](const double* x, double* y) {
@@ -520,132 +627,126 @@ __device__ void ca_finish(const double* t, double h, double wdiff, int nmax, Pcg
   for (int i = 0; i < NB; ++i) a[i] = b[i] = c[i] = 0.0;
   a[0] = 1.0;
   b[S + 1] = 1.0;
-  double g = GD[S + 1][S + 1];
-  const long long k = St->it;
+  double g = Gm[S + 1][S + 1];
   const bool weighted = St->norm == int(Norm::kWeighted);
-  int nupd = 0, status = -1;
-  long long iters = 0;
-  bool nan = !(g == g);
-  double diff = St->diff;
-  for (int j = 0; j < S && j < nmax; ++j) {
-    const long long kk = k + j + 1;
-    if (nan) {
-      status = int(Status::kBreakdown);
-      iters = kk;
-      break;
-    }
-    if (kk > St->max_iter) {
-      status = int(Status::kMaxIter);
-      iters = kk - 1;
-      break;
-    }
+  int n = 0;
+  for (int j = 0; j < nm; ++j) {
     shiftT(a, Ta);
-    const double den = quad(GD, a, Ta);
-    if (!(den == den) || (weighted ? fabs(den) < St->bd_tol : den < St->bd_tol)) {
-      status = int(Status::kBreakdown);
-      iters = kk;
-      nan = !(den == den);
+    const double den = quad(a, Ta);
+    if (nan || !(den == den) || !(g == g) || (weighted ? fabs(den) < St->bd_tol : den < St->bd_tol)) {
+      C->after_status = int(Status::kBreakdown);
+      C->after_iters = k + j + 1;
+      if (nan || !(den == den) || !(g == g)) St->nan_flag = 1;
       break;
     }
     const double alpha = g / den;
-    for (int i = 0; i < NB; ++i) c[i] = __builtin_fma(alpha, a[i], c[i]);
-    nupd = j + 1;
-    const double pp = quad(G0, a, a);
-    diff = fabs(alpha) * sqrt(pp);
-    if (!(diff == diff)) {
-      status = int(Status::kBreakdown);
-      iters = kk;
-      nan = true;
-      break;
+    for (int i = 0; i < NB; ++i) {
+      C->pa[j][i] = a[i];
+      c[i] = __builtin_fma(alpha, a[i], c[i]);
+      C->pc[j][i] = c[i];
     }
-    if (diff < St->delta) {
-      status = int(Status::kConverged);
-      iters = kk;
-      break;
-    }
+    C->alpha[j] = alpha;
+    n = j + 1;
     for (int i = 0; i < NB; ++i) b[i] = __builtin_fma(-alpha, Ta[i], b[i]);
-    const double gn = quad(GD, b, b);
+    const double gn = quad(b, b);
     const double beta = gn / g;
     for (int i = 0; i < NB; ++i) a[i] = __builtin_fma(beta, a[i], b[i]);
     g = gn;
-    nan = !(g == g);
+  }
+  if (n == 0) {  // breakdown in the block's first iteration: nothing to apply or to test
+    St->iters = C->after_iters;
+    St->status = C->after_status;
+    St->done = 1;
+    C->after_status = 0;
+    return;
+  }
+  if (C->after_status == 0 && k + n >= St->max_iter) {
+    C->after_status = int(Status::kMaxIter);
+    C->after_iters = St->max_iter;
   }
   for (int i = 0; i < NB; ++i) {
     C->coef[0][i] = a[i];
     C->coef[1][i] = b[i];
     C->coef[2][i] = c[i];
   }
-  C->nupd = nupd;
-  if (nupd > 0) C->blk += 1;
-  St->it = k + nupd;
-  St->diff = diff;
-  if (status >= 0) {
-    St->iters = iters;
-    St->status = status;
-    if (nan) St->nan_flag = 1;
-    St->done = 1;
-  }
+  C->nupd = n;
+  C->blk += 1;
+  C->pend_n = n;
+  C->pend_k = k;
+  St->it = k + n;
 }
 
-// Deterministic reduction of the pass-1 partials (n tiles x NQ) + the scalar finish: blocks sum
-// contiguous tile ranges (thread-strided, then waves in order), publish NQ chunk sums, and the last
-// block to arrive (ticket) sums the chunks in block order and runs ca_finish.  Hand-off as k_reduce_n.
+// Deterministic reduction of the partials (one array of n tile values per quantity: the Gram
+// products of pass 1, then the norms of the previous pass 2) + ca_finish.  Blocks sum contiguous tile
+// ranges (thread-strided, then waves in order) and publish their chunk sums; the last block to arrive
+// (ticket) sums the chunks in block order, one quantity per lane.  check_only: the norms alone (the
+// pending test after a batch's last block).  Hand-off as k_reduce_n (pcg_device.hpp).
 template <int S>
 __global__ void __launch_bounds__(256)
-k_ca_reduce(const double* __restrict__ part, int n, double h, double wdiff, int nmax, PcgState* St, CaState* C,
-            double* chunk, long long* progress) {
-  constexpr int NQ = CaShape<S>::NQ;
-  __shared__ double lds[NQ][256 / kWave];
-  __shared__ double tot[NQ];
+k_ca_reduce(const double* __restrict__ part, int n, double h, double wdiff, int nmax, int check_only,
+            PcgState* St, CaState* C, double* chunk, long long* progress) {
+  using Sh = CaShape<S>;
+  constexpr int NT = Sh::NQ + Sh::NN;
+  __shared__ double lds[NT][256 / kWave];
+  __shared__ double tot[NT];
   __shared__ int last;
   if (St->done) {
     if (blockIdx.x == 0 && threadIdx.x == 0) C->nupd = 0;
     return;
   }
+  const int q0 = check_only ? Sh::NQ : 0;  // first quantity summed
   const int nb = int(gridDim.x);
   const int lo = int(int64_t(n) * blockIdx.x / nb);
   const int hi = int(int64_t(n) * (blockIdx.x + 1) / nb);
-  double s[NQ];
+  double s[NT];
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) s[q] = 0.0;
+  for (int q = 0; q < NT; ++q) s[q] = 0.0;
   for (int i = lo + int(threadIdx.x); i < hi; i += 256) {
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) s[q] += part[int64_t(i) * NQ + q];
+    for (int q = 0; q < NT; ++q)
+      if (q >= q0) s[q] += part[int64_t(q) * n + i];
   }
   const int wid = threadIdx.x / kWave, lane = threadIdx.x % kWave;
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) {
+  for (int q = 0; q < NT; ++q) {
     s[q] = wave_sum_mfma(s[q]);
     if (lane == 0) lds[q][wid] = s[q];
   }
   __syncthreads();
-  if (nb == 1) {
+  if (nb > 1) {
     if (threadIdx.x == 0) {
-      for (int q = 0; q < NQ; ++q) tot[q] = (lds[q][0] + lds[q][1]) + (lds[q][2] + lds[q][3]);
-      ca_finish<S>(tot, h, wdiff, nmax, St, C);
-      if (progress) __hip_atomic_store(progress, St->it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+      for (int q = 0; q < NT; ++q)
+        st_publish(chunk + NT * blockIdx.x + q, (lds[q][0] + lds[q][1]) + (lds[q][2] + lds[q][3]));
+      last = ticket_arrive_last(&C->ticket, nb);
     }
-    return;
-  }
-  if (threadIdx.x == 0) {
+    __syncthreads();
+    if (!last || threadIdx.x >= kWave) return;  // wave 0 of the last block finishes (full EXEC)
+    // lane l sums chunks l, l + 64, .. (all NT loads of a round in flight together), then the wave
+    double t[NT];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q)
-      st_publish(chunk + NQ * blockIdx.x + q, (lds[q][0] + lds[q][1]) + (lds[q][2] + lds[q][3]));
-    last = ticket_arrive_last(&C->ticket, nb);
-  }
-  __syncthreads();
-  if (!last || threadIdx.x >= kWave) return;  // wave 0 of the last block finishes (full EXEC)
-  const int l = int(threadIdx.x);
+    for (int q = 0; q < NT; ++q) t[q] = 0.0;
+    for (int r = 0; r < (nb + kWave - 1) / kWave; ++r) {
+      const int c = lane + kWave * r;
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const double v = l < nb ? ld_published(chunk + NQ * l + q) : 0.0;
-    const double sum = wave_sum_mfma(v);
-    if (l == 0) tot[q] = sum;
+      for (int q = 0; q < NT; ++q)
+        if (q >= q0) t[q] += c < nb ? ld_published(chunk + NT * c + q) : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < NT; ++q) {
+      t[q] = wave_sum_mfma(t[q]);
+      if (lane == 0) tot[q] = t[q];
+    }
+  } else {
+    if (threadIdx.x >= kWave) return;
+    if (lane < NT) tot[lane] = (lds[lane][0] + lds[lane][1]) + (lds[lane][2] + lds[lane][3]);
   }
-  if (l == 0) {
-    ca_finish<S>(tot, h, wdiff, nmax, St, C);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  if (lane == 0) {
+    ca_finish<S>(tot, tot + Sh::NQ, h, wdiff, nmax, check_only != 0, St, C);
     if (progress) __hip_atomic_store(progress, St->it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    C->ticket = 0u;  // re-arm for the next launch (stream order makes this visible to it)
+    if (nb > 1) C->ticket = 0u;  // re-arm for the next launch (stream order makes this visible to it)
   }
 }
 
@@ -671,7 +772,7 @@ CaTiles make_ca_tiles(const DevGeom& G, int s, int rows) {
   return t;
 }
 
-int ca_nq(int s) { return s == 2 ? CaShape<2>::NQ : CaShape<3>::NQ; }
+int ca_nq(int s) { return s == 2 ? CaShape<2>::NQ + CaShape<2>::NN : CaShape<3>::NQ + CaShape<3>::NN; }
 
 void ca_build_classes(const DevGeom& G, const DevTables& Tb, const CaTiles& t, unsigned* tbl, hipStream_t s) {
   const int n = t.tiles_j * t.cwords;
@@ -708,14 +809,17 @@ void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, 
   HIP_CHECK(hipGetLastError());
 }
 
-void launch_ca_reduce(const double* partials, int n, int s_, double h, double wdiff, int nmax, PcgState* S,
-                      CaState* C, double* chunk, hipStream_t s, long long* progress) {
+void launch_ca_reduce(const double* partials, int n, int s_, double h, double wdiff, int nmax, bool check_only,
+                      PcgState* S, CaState* C, double* chunk, hipStream_t s, long long* progress) {
   PMX_CHECK(nmax >= 1 && nmax <= s_, "s-step PCG: a block runs 1..s iterations");
-  const int nb = std::max(1, std::min(kReduceMaxBlocks, n / 256));
+  const int nb = std::max(1, std::min(kCaReduceMaxBlocks, n / 512));
+  const int co = check_only ? 1 : 0;
   if (s_ == 2)
-    hipLaunchKernelGGL(k_ca_reduce<2>, dim3(nb), dim3(256), 0, s, partials, n, h, wdiff, nmax, S, C, chunk, progress);
+    hipLaunchKernelGGL(k_ca_reduce<2>, dim3(nb), dim3(256), 0, s, partials, n, h, wdiff, nmax, co, S, C, chunk,
+                       progress);
   else
-    hipLaunchKernelGGL(k_ca_reduce<3>, dim3(nb), dim3(256), 0, s, partials, n, h, wdiff, nmax, S, C, chunk, progress);
+    hipLaunchKernelGGL(k_ca_reduce<3>, dim3(nb), dim3(256), 0, s, partials, n, h, wdiff, nmax, co, S, C, chunk,
+                       progress);
   HIP_CHECK(hipGetLastError());
 }
 

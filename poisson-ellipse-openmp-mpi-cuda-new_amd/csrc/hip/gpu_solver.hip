@@ -332,7 +332,7 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     HIP_CHECK(hipStreamSynchronize(nullptr));
     HIP_CHECK(hipMalloc(&ca_state_, sizeof(CaState)));
     HIP_CHECK(hipMemset(ca_state_, 0, sizeof(CaState)));
-    HIP_CHECK(hipMalloc(&ca_chunk_, size_t(kReduceMaxBlocks) * ca_nq(ca_tiles_.s) * sizeof(double)));
+    HIP_CHECK(hipMalloc(&ca_chunk_, size_t(kCaReduceMaxBlocks) * ca_nq(ca_tiles_.s) * sizeof(double)));
   }
   init_tiles_ = make_tiles(G, 256, 0);
   // partials: 5 doubles per slot (the s-step Gram partials take ca_nq per tile)
@@ -646,12 +646,28 @@ void GpuSubdomainSolver::enqueue_ca_block(hipStream_t s, int n) {
   const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
   launch_ca_sweep<double>(geom_, tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, false, s);
   after_launch(s);
-  launch_ca_reduce(partials_, ca_tiles_.ntiles(), ca_tiles_.s, g_.h1h2, wdiff, n, state_, ca_state_, ca_chunk_, s,
-                   progress_dev_);
+  launch_ca_reduce(partials_, ca_tiles_.ntiles(), ca_tiles_.s, g_.h1h2, wdiff, n, false, state_, ca_state_,
+                   ca_chunk_, s, progress_dev_);
   after_launch(s);
   launch_ca_sweep<double>(geom_, tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, true, s);
   after_launch(s);
   host_k_ += n;
+}
+
+void GpuSubdomainSolver::enqueue_ca_check(hipStream_t s) {
+  PMX_CHECK(ca_ && elem_ == 8, "enqueue_ca_check: not an s-step solver");
+  double* w = static_cast<double*>(field_base(0));
+  double* z0 = static_cast<double*>(field_base(1));
+  double* z1 = reinterpret_cast<double*>(r2_ + field_off_ * elem_);
+  double* p0 = static_cast<double*>(field_base(2));
+  double* p1 = static_cast<double*>(field_base(3));
+  const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
+  launch_ca_reduce(partials_, ca_tiles_.ntiles(), ca_tiles_.s, g_.h1h2, wdiff, 1, true, state_, ca_state_, ca_chunk_,
+                   s, progress_dev_);
+  after_launch(s);
+  // a stop inside the last block rewinds w (every workgroup returns at once otherwise)
+  launch_ca_sweep<double>(geom_, tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, true, s);
+  after_launch(s);
 }
 
 template <typename T>
@@ -1289,11 +1305,14 @@ int PcgDriver::ca_batch() const {
 void PcgDriver::enqueue_ca(int64_t n) {
   const int s = local_[0]->ca_s();
   HIP_CHECK(hipSetDevice(local_[0]->device()));
+  if (n <= 0) return;
   while (n > 0) {
     const int m = int(std::min<int64_t>(s, n));
     local_[0]->enqueue_ca_block(streams_[0], m);
     n -= m;
   }
+  // the last block's stop test (and its rewind): the state is exact at every batch boundary
+  local_[0]->enqueue_ca_check(streams_[0]);
 }
 
 void PcgDriver::enqueue_one_iteration() {

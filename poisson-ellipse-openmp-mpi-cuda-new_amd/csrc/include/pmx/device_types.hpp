@@ -92,15 +92,24 @@ struct alignas(64) PcgState {
 
 // s-step PCG (ca_kernels.hip): the per-block scalars next to PcgState.  Basis of a block: Chebyshev
 // polynomials of L = D^-1 A in p and z, Y = [P_0..P_s, Z_0..Z_{s-1}] (2s+1 vectors); p, z and w - w_k
-// after j iterations are Y a_j, Y b_j, Y c_j.
+// after j iterations are Y a_j, Y b_j, Y c_j.  The stop test of a block's iterations needs ||p_{k+j}||,
+// which pass 2 forms explicitly: it is checked one reduction later ("pending"), and a stop inside the
+// block rewinds w to c_{j+1} with one more pass over the block's (still intact) inputs.
 constexpr int kCaMaxS = 3;
 constexpr int kCaMaxNb = 2 * kCaMaxS + 1;
 struct alignas(64) CaState {
-  double coef[3][kCaMaxNb];  // a_n, b_n, c_n of the block's last applied iteration n (pass 2 reads)
-  long long blk;   // blocks applied: pass 1 reads (p, z) from set blk & 1, pass 2 writes set (blk & 1)
-  int nupd;        // iterations the current block applies (0: nothing, the solve had stopped)
-  int s;           // block size (basis degree)
-  unsigned ticket; // the reduction's last-block ticket (re-armed by the finishing block)
+  double coef[3][kCaMaxNb];     // pass 2: a_n, b_n, c_n (rewind: w += Y coef[2])
+  double pa[kCaMaxS][kCaMaxNb];  // a_j (p_{k+j} = Y a_j) of the block's iterations: pass 2's norms
+  double pc[kCaMaxS][kCaMaxNb];  // c_{j+1} of the pending block (the rewind target)
+  double alpha[kCaMaxS];         // alpha_j of the pending block
+  long long blk;          // blocks applied: pass 1 reads (p, z) from set blk & 1, pass 2 writes set (blk & 1)
+  long long pend_k;       // iterations done before the pending block
+  long long after_iters;  // iteration count reported with after_status
+  int nupd;               // pass 2: n > 0 apply n iterations, 0 nothing, -1 rewind w only
+  int pend_n;             // iterations of the block whose stop test is pending (0: none)
+  int after_status;       // 0, or the status (breakdown / max_iter) that ends the solve once the pending test passes
+  int s;                  // block size (basis degree)
+  unsigned ticket;        // the reduction's last-block ticket (re-armed by the finishing block)
   int pad;
 };
 

@@ -284,6 +284,8 @@ class GpuSubdomainSolver {
   int ca_s() const { return ca_ ? ca_tiles_.s : 0; }
   const CaTiles& ca_tiles() const { return ca_tiles_; }
   void enqueue_ca_block(hipStream_t s, int n);
+  // the pending stop test of the last block, and pass 2 rewinding w if it stopped inside that block
+  void enqueue_ca_check(hipStream_t s);
   // pcg1: host mirror of the device iteration counter S->it -- the index of the next sweep this
   // solver enqueues.  init sets it to 0, every enqueued reduction (which bumps S->it on the
   // device) advances it, load_checkpoint reads it from the checkpoint.  It picks the plain or the

@@ -145,7 +145,7 @@ struct CaTiles {
   int ntiles() const { return tiles_i * tiles_j; }
 };
 CaTiles make_ca_tiles(const DevGeom& G, int s, int rows);
-int ca_nq(int s);  // Gram partials per tile
+int ca_nq(int s);  // partials per tile (pass 1's Gram products + pass 2's norms)
 void ca_build_classes(const DevGeom& G, const DevTables& Tb, const CaTiles& t, unsigned* tbl, hipStream_t s);
 // z = D^-1 r in place, p = z (the first block's set 0)
 template <typename T>
@@ -153,9 +153,12 @@ void launch_ca_init(const DevGeom& G, const DevTables& Tb, T* z, T* p, hipStream
 template <typename T>
 void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, T* p0, T* p1, double* partials,
                      const PcgState* S, const CaState* C, const CaTiles& t, bool upd, hipStream_t s);
-// chunk: kReduceMaxBlocks * ca_nq(s) doubles of workspace; nmax: iterations this block may run
-void launch_ca_reduce(const double* partials, int n, int s_, double h, double wdiff, int nmax, PcgState* S,
-                      CaState* C, double* chunk, hipStream_t s, long long* progress = nullptr);
+// chunk: kCaReduceMaxBlocks * ca_nq(s) doubles of workspace; nmax: iterations this block may run
+constexpr int kCaReduceMaxBlocks = 256;
+// check_only: the pending stop test alone (after the last block of a batch; pass 2 then rewinds w if
+// the test stopped inside that block)
+void launch_ca_reduce(const double* partials, int n, int s_, double h, double wdiff, int nmax, bool check_only,
+                      PcgState* S, CaState* C, double* chunk, hipStream_t s, long long* progress = nullptr);
 
 // pcg1 ghost exchange: pack (unpack=false) the radius-2 edges of the buffers sweep `target` reads
 // (parity of target) into H.send, or unpack H.recv into their ghost cells.
