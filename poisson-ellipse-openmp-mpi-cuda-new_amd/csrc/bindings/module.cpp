@@ -609,6 +609,7 @@ PYBIND11_MODULE(_pmx, m) {
           d["s"] = c.s;
           d["block"] = c.wo;
           d["rows"] = c.rows;
+          d["rows_upd"] = c.rows2;
           d["vec"] = 2;
           d["waves"] = 1;
           d["tiles_i"] = c.tiles_i;

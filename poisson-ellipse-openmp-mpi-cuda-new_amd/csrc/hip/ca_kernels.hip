@@ -210,14 +210,14 @@ struct CaRow {
 // One wave's march over one tile (see the header).  UPD = false: the Gram products into acc; true:
 // p, z, w updated with the block's coefficient vectors ca / cb / cc and ||Y pa_j||^2 into acc
 // (REW: w += Y cc only).
-template <typename T, int S, bool UPD, bool FAST, int PF, bool REW>
+template <typename T, int S, bool UPD, bool FAST, int PF, bool REW, int DPF = 0>
 __device__ __forceinline__ void ca_march(const DevGeom& G, const DevTables& Tb, const CaK& K,
                                          const T* __restrict__ pin, const T* __restrict__ zin, T* __restrict__ pout,
                                          T* __restrict__ zout, T* __restrict__ w, int i0, int i1, int j0, int j1,
                                          const unsigned* __restrict__ ctbl, const double* scol,
                                          double (&acc)[CaShape<S>::NQ], const double (&ca)[CaShape<S>::NB],
                                          const double (&cb)[CaShape<S>::NB], const double (&cc)[CaShape<S>::NB],
-                                         const double (&pa)[S][CaShape<S>::NB]) {
+                                         const double (&pa)[S][CaShape<S>::NB], double* dring = nullptr) {
   using Sh = CaShape<S>;
   constexpr int NB = Sh::NB, A = Sh::AGES;
   const int64_t P = G.pitch;
@@ -375,6 +375,50 @@ __device__ __forceinline__ void ca_march(const DevGeom& G, const DevTables& Tb, 
   // (unconditional loads, the last row re-read past the end).  Unrolled by 4 = the window depth
   // (and a multiple of PF + 1), so the window shifts and the ring are register renames, not moves.
   static_assert(PF == 1 || PF == 3, "ca_march: prefetch depth 1 or 3");
+  if constexpr (DPF > 0) {
+    // LDS-DMA ring (pass 1 of fp64 FAST tiles): row mfirst + t in slot t & 3, DPF = 4 rows ahead, no
+    // VGPR buffers.  global_load_lds_dwordx4 is invisible to hipcc (pcg1_march.hpp: dma16), so the
+    // march counts vmcnt itself: pass 1 issues no other vector memory operation in the loop (row
+    // classes and cut-row constants are scalar / LDS loads), so before reading row m exactly the
+    // DMAs of rows m+1 .. m+3 may still be in flight.
+    static_assert(DPF == 4 && !UPD && FAST && sizeof(T) == 8, "ca_march: LDS-DMA for pass 1 FAST tiles, 4 rows");
+    const unsigned voff = unsigned(c0 + 4) * 8u;  // bytes from row - 4 (ca_col's unsigned form)
+    const unsigned lds0 = unsigned(reinterpret_cast<uintptr_t>(dring));
+    auto dma_row = [&](int m, int slot) {
+      const unsigned l = lds0 + unsigned(slot) * 2048u;
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's previous ds_reads have returned
+      dma16(pin + int64_t(m) * P - 4, voff, l);
+      dma16(zin + int64_t(m) * P - 4, voff, l + 1024u);
+    };
+    typedef double d2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int q = 0; q < DPF; ++q) dma_row(min(mfirst + q, mlast), q);
+    bool more = true;
+    for (int m = mfirst; more && m <= mlast; m += 4) {
+      more = static_for_while<4>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        if (m + q > mlast) return false;
+        wait_vmcnt<(DPF - 1) * 2>();
+        const double* sl = dring + q * 256;
+        CaRow<T, S, UPD> cur;
+        const d2 pv = *reinterpret_cast<const d2*>(sl + 2 * lane);
+        const d2 zv = *reinterpret_cast<const d2*>(sl + 128 + 2 * lane);
+        cur.p[0] = pv.x;
+        cur.p[1] = pv.y;
+        cur.z[0] = zv.x;
+        cur.z[1] = zv.y;
+        dma_row(min(m + q + DPF, mlast), q);
+        core(qc, m + q, cur);
+        return true;
+      });
+    }
+    wait_vmcnt<0>();  // no DMA may land after the wave has moved on
+    if constexpr (FAST) {
+#pragma unroll
+      for (int q = 0; q < Sh::NQ; ++q) acc[q] = own_all ? acc[q] : 0.0;
+    }
+    return;
+  }
   constexpr int NBUF = PF + 1;
   CaRow<T, S, UPD> buf[NBUF];
 #pragma unroll
@@ -386,6 +430,9 @@ __device__ __forceinline__ void ca_march(const DevGeom& G, const DevTables& Tb, 
       if (m + q > mlast) return false;
       fetch(min(m + q + PF, mlast), buf[(q + PF) % NBUF]);
       core(qc, m + q, buf[q % NBUF]);
+#ifdef PMX_CA_SCHED_BARRIER
+      __builtin_amdgcn_sched_barrier(0);  // one row step at a time: bounded live ranges
+#endif
       return true;
     });
   }
@@ -403,16 +450,14 @@ __device__ __forceinline__ void ca_march(const DevGeom& G, const DevTables& Tb, 
 #endif
 constexpr int kCaPfGram = PMX_CA_PF_GRAM, kCaPfUpd = PMX_CA_PF_UPD;
 
-template <int S, bool UPD>
-constexpr int ca_min_waves() {
-  return UPD ? 3 : 2;
-}
 
-template <typename T, int S, bool UPD>
-__global__ void __launch_bounds__(64, (ca_min_waves<S, UPD>()))
+// MW: waves per SIMD the register allocation must allow; DMA: pass 1's interior tiles prefetch by
+// LDS-DMA (4 rows ahead) instead of registers.  The launcher picks the variant from CaTiles.
+template <typename T, int S, bool UPD, int MW, bool DMA>
+__global__ void __launch_bounds__(64, MW)
 k_ca_sweep(DevGeom G, DevTables Tb, T* w, T* z0, T* z1, T* p0, T* p1, double* __restrict__ partials,
            const PcgState* St, const CaState* C, int TI, int tiles_j, const unsigned* __restrict__ ctbl,
-           int cwords) {
+           int cwords, int64_t pbase) {
   using Sh = CaShape<S>;
   constexpr int NB = Sh::NB;
   typedef const __attribute__((address_space(4))) PcgState CPS;
@@ -446,6 +491,8 @@ k_ca_sweep(DevGeom G, DevTables Tb, T* w, T* z0, T* z1, T* p0, T* p1, double* __
   const int lane = threadIdx.x & 63;
   // column constants of the lane's columns for the cut rows (coef's LDS slots)
   __shared__ double scol[4 * 2 * 64];
+  // pass 1's LDS-DMA row ring (4 slots of p, z rows, 2 KiB each)
+  __shared__ double s_ring[(!UPD && DMA) ? 4 * 256 : 2];
   {
     const int c0 = j0 - Sh::HE + 2 * lane;
 #pragma unroll
@@ -474,19 +521,26 @@ k_ca_sweep(DevGeom G, DevTables Tb, T* w, T* z0, T* z1, T* p0, T* p1, double* __
       return;
     }
   }
+  if constexpr (!UPD && DMA && sizeof(T) == 8) {
+    if (fast) {  // pass 1, interior tiles: rows prefetched by LDS-DMA
+      ca_march<T, S, UPD, true, PF, false, 4>(G, Tb, K, pin, zin, pout, zout, w, i0, i1, j0, j1, tbl, scol, acc, ca,
+                                              cb, cc, pa, s_ring);
+      goto marched;
+    }
+  }
   if (fast) PMX_CA_MARCH(true, false);
   else PMX_CA_MARCH(false, false);
+marched:
 #undef PMX_CA_MARCH
-  // partials, one array per quantity: Gram products q (pass 1) at [q][tile], norms j (pass 2) at
-  // [NQ + j][tile]
+  // partials, one array per quantity: Gram products q (pass 1, n1 tiles) at [q][tile], norms j (pass
+  // 2, its own n2 tiles) at pbase + [j][tile], pbase = NQ n1
   constexpr int NOUT = UPD ? Sh::NN : Sh::NQ;
-  constexpr int OFF = UPD ? Sh::NQ : 0;
 #pragma unroll
   for (int q = 0; q + 1 < NOUT; q += 2) wave_sum2_mfma(acc[q], acc[q + 1]);
   if constexpr (NOUT & 1) acc[NOUT - 1] = wave_sum_mfma(acc[NOUT - 1]);
   if (lane == 0) {
 #pragma unroll
-    for (int q = 0; q < NOUT; ++q) partials[int64_t(OFF + q) * ntiles + id] = acc[q];
+    for (int q = 0; q < NOUT; ++q) partials[pbase + int64_t(q) * ntiles + id] = acc[q];
   }
 }
 
@@ -683,7 +737,7 @@ __device__ void ca_finish(const double* t, const double* u, double h, double wdi
 // pending test after a batch's last block).  Hand-off as k_reduce_n (pcg_device.hpp).
 template <int S>
 __global__ void __launch_bounds__(256)
-k_ca_reduce(const double* __restrict__ part, int n, double h, double wdiff, int nmax, int check_only,
+k_ca_reduce(const double* __restrict__ part, int n, int n2, double h, double wdiff, int nmax, int check_only,
             PcgState* St, CaState* C, double* chunk, long long* progress) {
   using Sh = CaShape<S>;
   constexpr int NT = Sh::NQ + Sh::NN;
@@ -696,15 +750,23 @@ k_ca_reduce(const double* __restrict__ part, int n, double h, double wdiff, int 
   }
   const int q0 = check_only ? Sh::NQ : 0;  // first quantity summed
   const int nb = int(gridDim.x);
-  const int lo = int(int64_t(n) * blockIdx.x / nb);
-  const int hi = int(int64_t(n) * (blockIdx.x + 1) / nb);
   double s[NT];
 #pragma unroll
   for (int q = 0; q < NT; ++q) s[q] = 0.0;
-  for (int i = lo + int(threadIdx.x); i < hi; i += 256) {
+  if (!check_only) {  // the Gram products of pass 1's n tiles
+    const int lo = int(int64_t(n) * blockIdx.x / nb), hi = int(int64_t(n) * (blockIdx.x + 1) / nb);
+    for (int i = lo + int(threadIdx.x); i < hi; i += 256) {
 #pragma unroll
-    for (int q = 0; q < NT; ++q)
-      if (q >= q0) s[q] += part[int64_t(q) * n + i];
+      for (int q = 0; q < Sh::NQ; ++q) s[q] += part[int64_t(q) * n + i];
+    }
+  }
+  {  // the norms of pass 2's n2 tiles
+    const double* p2 = part + int64_t(Sh::NQ) * n;
+    const int lo = int(int64_t(n2) * blockIdx.x / nb), hi = int(int64_t(n2) * (blockIdx.x + 1) / nb);
+    for (int i = lo + int(threadIdx.x); i < hi; i += 256) {
+#pragma unroll
+      for (int q = Sh::NQ; q < NT; ++q) s[q] += p2[int64_t(q - Sh::NQ) * n2 + i];
+    }
   }
   const int wid = threadIdx.x / kWave, lane = threadIdx.x % kWave;
 #pragma unroll
@@ -752,7 +814,7 @@ k_ca_reduce(const double* __restrict__ part, int n, double h, double wdiff, int 
 
 }  // namespace
 
-CaTiles make_ca_tiles(const DevGeom& G, int s, int rows) {
+CaTiles make_ca_tiles(const DevGeom& G, int s, int rows, int rows2) {
   PMX_CHECK(s == 2 || s == 3, "s-step PCG: s must be 2 or 3");
   CaTiles t;
   t.s = s;
@@ -768,6 +830,13 @@ CaTiles make_ca_tiles(const DevGeom& G, int s, int rows) {
   PMX_CHECK(rows >= 1 && rows <= 4096, "s-step PCG: tile rows must be in [1, 4096]");
   t.rows = rows;
   t.tiles_i = (G.nx + rows - 1) / rows;
+  // pass 2 (memory-bound, no Gram) marches shorter tiles: fewer DRAM rows in flight per wave and a
+  // finer load balance win over the extra halo rows (16384^2: pass 2 2.87 ms at 32 rows, 2.66 at 16;
+  // pass 1 1.78 at 32, 1.77 at 64, 2.17 at 16 -- profiles/r5/ca/)
+  if (rows2 <= 0) rows2 = std::max(8, rows / 4);
+  PMX_CHECK(rows2 >= 1 && rows2 <= 4096, "s-step PCG: pass-2 tile rows must be in [1, 4096]");
+  t.rows2 = rows2;
+  t.tiles_i2 = (G.nx + rows2 - 1) / rows2;
   t.cwords = (G.nx + 2 * s + 2 * kCaRowOff + 15) / 16 + 1;
   return t;
 }
@@ -793,32 +862,43 @@ void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, 
                      const PcgState* S, const CaState* C, const CaTiles& t, bool upd, hipStream_t s) {
   PMX_CHECK(G.nb == 0, "s-step PCG runs undecomposed grids");
   PMX_CHECK(t.tbl != nullptr, "s-step PCG: row-class table missing");
-  const int n = t.ntiles();
+  const int n = upd ? t.ntiles2() : t.ntiles();
+  const int rows = upd ? t.rows2 : t.rows;
+  const int64_t pbase = upd ? int64_t(ca_nq(t.s) - t.s) * t.ntiles() : 0;  // norms after the Gram products
+#define PMX_CA_K(SS, U, MW, D)                                                                                \
+  hipLaunchKernelGGL((k_ca_sweep<T, SS, U, MW, D>), dim3(n), dim3(64), 0, s, G, Tb, w, z0, z1, p0, p1, partials, S, C, \
+                     rows, t.tiles_j, t.tbl, t.cwords, pbase)
 #define PMX_CA(SS)                                                                                              \
   do {                                                                                                          \
-    if (upd)                                                                                                    \
-      hipLaunchKernelGGL((k_ca_sweep<T, SS, true>), dim3(n), dim3(64), 0, s, G, Tb, w, z0, z1, p0, p1, partials, \
-                         S, C, t.rows, t.tiles_j, t.tbl, t.cwords);                                             \
-    else                                                                                                        \
-      hipLaunchKernelGGL((k_ca_sweep<T, SS, false>), dim3(n), dim3(64), 0, s, G, Tb, w, z0, z1, p0, p1,         \
-                         partials, S, C, t.rows, t.tiles_j, t.tbl, t.cwords);                                   \
+    if (upd) {                                                                                                  \
+      if (t.waves_upd == 2) PMX_CA_K(SS, true, 2, false);                                                       \
+      else PMX_CA_K(SS, true, 3, false);                                                                        \
+    } else if (t.dma) {                                                                                         \
+      if (t.waves_gram == 3) PMX_CA_K(SS, false, 3, true);                                                      \
+      else PMX_CA_K(SS, false, 2, true);                                                                        \
+    } else {                                                                                                    \
+      if (t.waves_gram == 3) PMX_CA_K(SS, false, 3, false);                                                     \
+      else PMX_CA_K(SS, false, 2, false);                                                                       \
+    }                                                                                                           \
   } while (0)
+  PMX_CHECK(sizeof(T) == 8 || !t.dma, "s-step PCG: LDS-DMA rows need fp64");
   if (t.s == 2) PMX_CA(2);
   else PMX_CA(3);
+#undef PMX_CA_K
 #undef PMX_CA
   HIP_CHECK(hipGetLastError());
 }
 
-void launch_ca_reduce(const double* partials, int n, int s_, double h, double wdiff, int nmax, bool check_only,
-                      PcgState* S, CaState* C, double* chunk, hipStream_t s, long long* progress) {
+void launch_ca_reduce(const double* partials, int n, int n2, int s_, double h, double wdiff, int nmax,
+                      bool check_only, PcgState* S, CaState* C, double* chunk, hipStream_t s, long long* progress) {
   PMX_CHECK(nmax >= 1 && nmax <= s_, "s-step PCG: a block runs 1..s iterations");
-  const int nb = std::max(1, std::min(kCaReduceMaxBlocks, n / 512));
+  const int nb = std::max(1, std::min(kCaReduceMaxBlocks, std::max(n, n2) / 512));
   const int co = check_only ? 1 : 0;
   if (s_ == 2)
-    hipLaunchKernelGGL(k_ca_reduce<2>, dim3(nb), dim3(256), 0, s, partials, n, h, wdiff, nmax, co, S, C, chunk,
+    hipLaunchKernelGGL(k_ca_reduce<2>, dim3(nb), dim3(256), 0, s, partials, n, n2, h, wdiff, nmax, co, S, C, chunk,
                        progress);
   else
-    hipLaunchKernelGGL(k_ca_reduce<3>, dim3(nb), dim3(256), 0, s, partials, n, h, wdiff, nmax, co, S, C, chunk,
+    hipLaunchKernelGGL(k_ca_reduce<3>, dim3(nb), dim3(256), 0, s, partials, n, n2, h, wdiff, nmax, co, S, C, chunk,
                        progress);
   HIP_CHECK(hipGetLastError());
 }

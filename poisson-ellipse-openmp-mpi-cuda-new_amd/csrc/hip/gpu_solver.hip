@@ -115,8 +115,15 @@ GpuOptions resolve_options(const GpuOptions& in) {
   PMX_CHECK(o.block_fused1 >= -1 && o.block_fused1 <= 1, "block-tile fused reduction must be -1 (auto), 0 or 1");
   env_int("PMX_CA_S", o.ca_s);
   env_int("PMX_CA_ROWS", o.ca_rows);
+  env_int("PMX_CA_ROWS_UPD", o.ca_rows2);
   PMX_CHECK(o.ca_s == 2 || o.ca_s == 3, "s-step PCG: s must be 2 or 3");
   PMX_CHECK(o.ca_rows >= 0 && o.ca_rows <= 4096, "s-step PCG: tile rows must be 0 (auto) .. 4096");
+  env_int("PMX_CA_DMA", o.ca_dma);
+  env_int("PMX_CA_WAVES_GRAM", o.ca_waves_gram);
+  env_int("PMX_CA_WAVES_UPD", o.ca_waves_upd);
+  PMX_CHECK(o.ca_dma == 0 || o.ca_dma == 1, "s-step PCG: ca_dma must be 0 or 1");
+  PMX_CHECK((o.ca_waves_gram == 2 || o.ca_waves_gram == 3) && (o.ca_waves_upd == 2 || o.ca_waves_upd == 3),
+            "s-step PCG: waves per SIMD must be 2 or 3");
   env_int("PMX_PCG1_DMA", o.dma1);
   env_int("PMX_PCG1_DMA_W", o.dma1w);
   PMX_CHECK(o.dma1 == 0 || o.dma1 == 2 || o.dma1 == 3, "pcg1 LDS-DMA prefetch depth must be 0, 2 or 3");
@@ -325,7 +332,10 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
 
   if (ca_) {
     r2_ = field_raw(4);  // the second z buffer
-    ca_tiles_ = make_ca_tiles(G, opt_.ca_s, opt_.ca_rows);
+    ca_tiles_ = make_ca_tiles(G, opt_.ca_s, opt_.ca_rows, opt_.ca_rows2);
+    ca_tiles_.dma = opt_.ca_dma;
+    ca_tiles_.waves_gram = opt_.ca_waves_gram;
+    ca_tiles_.waves_upd = opt_.ca_waves_upd;
     HIP_CHECK(hipMalloc(&ca_tbl_, size_t(ca_tiles_.tiles_j) * ca_tiles_.cwords * sizeof(unsigned)));
     ca_tiles_.tbl = ca_tbl_;
     ca_build_classes(G, tables_, ca_tiles_, ca_tbl_, nullptr);
@@ -336,7 +346,10 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   }
   init_tiles_ = make_tiles(G, 256, 0);
   // partials: 5 doubles per slot (the s-step Gram partials take ca_nq per tile)
-  const int ca_slots = ca_ ? (ca_tiles_.ntiles() * ca_nq(ca_tiles_.s) + 4) / 5 : 0;
+  const int ca_slots =
+      ca_ ? int((int64_t(ca_tiles_.ntiles()) * (ca_nq(ca_tiles_.s) - ca_tiles_.s) +
+                 int64_t(ca_tiles_.ntiles2()) * ca_tiles_.s + 4) / 5)
+          : 0;
   const size_t npart = size_t(std::max({tiles_.ntiles(), tiles_b_.ntiles(), init_tiles_.ntiles(),
                                         pcg1_ ? std::max(tiles1_.ntiles(), tiles1w_.ntiles()) : 0, ca_slots}));
   npart_ = npart;
@@ -646,7 +659,7 @@ void GpuSubdomainSolver::enqueue_ca_block(hipStream_t s, int n) {
   const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
   launch_ca_sweep<double>(geom_, tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, false, s);
   after_launch(s);
-  launch_ca_reduce(partials_, ca_tiles_.ntiles(), ca_tiles_.s, g_.h1h2, wdiff, n, false, state_, ca_state_,
+  launch_ca_reduce(partials_, ca_tiles_.ntiles(), ca_tiles_.ntiles2(), ca_tiles_.s, g_.h1h2, wdiff, n, false, state_, ca_state_,
                    ca_chunk_, s, progress_dev_);
   after_launch(s);
   launch_ca_sweep<double>(geom_, tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, true, s);
@@ -662,7 +675,7 @@ void GpuSubdomainSolver::enqueue_ca_check(hipStream_t s) {
   double* p0 = static_cast<double*>(field_base(2));
   double* p1 = static_cast<double*>(field_base(3));
   const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
-  launch_ca_reduce(partials_, ca_tiles_.ntiles(), ca_tiles_.s, g_.h1h2, wdiff, 1, true, state_, ca_state_, ca_chunk_,
+  launch_ca_reduce(partials_, ca_tiles_.ntiles(), ca_tiles_.ntiles2(), ca_tiles_.s, g_.h1h2, wdiff, 1, true, state_, ca_state_, ca_chunk_,
                    s, progress_dev_);
   after_launch(s);
   // a stop inside the last block rewinds w (every workgroup returns at once otherwise)

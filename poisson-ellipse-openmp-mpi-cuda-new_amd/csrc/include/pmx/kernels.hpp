@@ -138,13 +138,18 @@ struct CaTiles {
   int s = 3;        // block size = basis degree (2 or 3)
   int he = 4;       // extra columns loaded per side ((s + 1) & ~1)
   int wo = 120;     // owned columns per wave tile (128 - 2 he)
-  int rows = 0;     // rows per tile
+  int rows = 0;     // rows per tile (pass 1)
   int tiles_i = 0, tiles_j = 0;
+  int rows2 = 0, tiles_i2 = 0;  // pass 2's tile rows (same columns)
   int cwords = 0;   // row-class words per tile column (16 rows each)
   unsigned* tbl = nullptr;  // row classes (ca_build_classes), tiles_j * cwords words, owned by the caller
+  int dma = 1;         // pass 1: interior tiles prefetch their rows by LDS-DMA (0: registers)
+  int waves_gram = 2;  // waves per SIMD the pass-1 registers must allow (2 or 3)
+  int waves_upd = 3;   // ... pass 2 (2 or 3)
   int ntiles() const { return tiles_i * tiles_j; }
+  int ntiles2() const { return tiles_i2 * tiles_j; }
 };
-CaTiles make_ca_tiles(const DevGeom& G, int s, int rows);
+CaTiles make_ca_tiles(const DevGeom& G, int s, int rows, int rows2 = 0);
 int ca_nq(int s);  // partials per tile (pass 1's Gram products + pass 2's norms)
 void ca_build_classes(const DevGeom& G, const DevTables& Tb, const CaTiles& t, unsigned* tbl, hipStream_t s);
 // z = D^-1 r in place, p = z (the first block's set 0)
@@ -157,8 +162,10 @@ void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, 
 constexpr int kCaReduceMaxBlocks = 256;
 // check_only: the pending stop test alone (after the last block of a batch; pass 2 then rewinds w if
 // the test stopped inside that block)
-void launch_ca_reduce(const double* partials, int n, int s_, double h, double wdiff, int nmax, bool check_only,
-                      PcgState* S, CaState* C, double* chunk, hipStream_t s, long long* progress = nullptr);
+// n / n2: pass 1 / pass 2 tiles (the partials of each)
+void launch_ca_reduce(const double* partials, int n, int n2, int s_, double h, double wdiff, int nmax,
+                      bool check_only, PcgState* S, CaState* C, double* chunk, hipStream_t s,
+                      long long* progress = nullptr);
 
 // pcg1 ghost exchange: pack (unpack=false) the radius-2 edges of the buffers sweep `target` reads
 // (parity of target) into H.send, or unpack H.recv into their ghost cells.
