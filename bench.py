@@ -549,6 +549,8 @@ def measure(args) -> int:
     info = launch.init_distributed(backend=backend if env.world > 1 else None,
                                    device_type="cpu" if (dry or share or backend == "gloo") else None)
     world = info.world
+    if args.algo == "ca" and world > 1:
+        raise SystemExit("[bench] --algo ca (the s-step PCG) runs undecomposed grids on one GPU; use auto / pcg1")
     device = 0 if share else info.local_rank
     if not dry:
         if not torch.cuda.is_available():
@@ -582,9 +584,14 @@ def measure(args) -> int:
         comm_used = "gloo" if world > 1 else "self"
     elif world == 1:
         models = importlib.import_module(pkg_name + ".models")
+        # auto on one GPU: the s-step PCG (ca_kernels.hip) where it applies -- fp64, fast arithmetic
+        # (same iteration counts, 64 instead of 3 x 37.3 B/pt per 3 iterations); else pcg1 / pcg2
+        algo = args.algo
+        if algo == "auto" and args.dtype == "fp64" and not args.exact:
+            algo = "ca"
         runner = ds.SessionRunner(models.make_session(problem, ranks=1, device=info.local_rank,
                                                       block_tiles={"auto": -1, "on": 1, "off": 0}[args.block_tiles],
-                                                      algo=args.algo, ca_s=args.ca_s, **pkw, **kw), problem, info)
+                                                      algo=algo, ca_s=args.ca_s, **pkw, **kw), problem, info)
         comm_used = "self"
     elif share and cfg["comm"] == "ipc":
         runner = ds.DistGpuPCG(problem, info, comm="ipc", device=0, **dkw)
@@ -655,7 +662,8 @@ def measure(args) -> int:
     if probe and isinstance(tile_desc.get("placement"), dict) and len(probe) <= 32:
         tile_desc["placement"] = dict(tile_desc["placement"], probe_ms=[round(float(x), 3) for x in probe])
     if isinstance(tile_desc.get("placement"), dict):
-        cls = placement_class(tile_desc["placement"].get("kept_ms"), (args.M - 1) * (args.N - 1), args.dtype)
+        cls = placement_class(tile_desc["placement"].get("kept_ms"), (args.M - 1) * (args.N - 1), args.dtype,
+                              tile_desc.get("algo", "pcg1"))
         if cls:
             tile_desc["placement"]["class"] = cls
     valid = (not st1["done"]) and (st1["it"] - st0["it"] == args.steps) and not st1["nan"]
@@ -836,14 +844,17 @@ def measure_loopback(args) -> int:
 # ~11.55-11.65 (1.92-1.95 ms/step), i.e. ~6.65 / ~6.9 / ~7.2 ps per point and iteration.  The
 # class says which one the timed run got, so a driver record can be read against the others.
 PLACEMENT_CLASS_PS = ((6.80, "fast"), (7.05, "mid"))
+# s-step PCG (6 iterations = 2 blocks per candidate): provisional limits from the round-5 boxes
+# (kept 8.61 / 8.80 / 9.03 / 9.45 ms at 16384^2 = 5.35 / 5.47 / 5.61 / 5.87 ps per point and iteration)
+PLACEMENT_CLASS_PS_CA = ((5.50, "fast"), (5.70, "mid"))
 
 
-def placement_class(kept_ms, points, dtype):
+def placement_class(kept_ms, points, dtype, algo="pcg1"):
     """'fast' / 'mid' / 'slow' for fp64 grids of >= 8192^2 points (bandwidth-bound), else None."""
     if not kept_ms or dtype != "fp64" or points < 8192 * 8192:
         return None
     ps = float(kept_ms) / 6.0 / points * 1e9
-    for lim, name in PLACEMENT_CLASS_PS:
+    for lim, name in (PLACEMENT_CLASS_PS_CA if algo == "ca" else PLACEMENT_CLASS_PS):
         if ps < lim:
             return name
     return "slow"

@@ -77,8 +77,10 @@ struct GpuOptions {
   // s-step PCG: block size (2 or 3) and tile height (0 = auto).  PMX_CA_S / PMX_CA_ROWS.
   int ca_s = 3, ca_rows = 0, ca_rows2 = 0;  // (ca_rows2: pass 2's tile rows, PMX_CA_ROWS_UPD)
   // s-step pass shapes: pass 1 rows by LDS-DMA (1) or registers (0); waves per SIMD each pass's
-  // registers must allow (2 or 3).  PMX_CA_DMA / PMX_CA_WAVES_GRAM / PMX_CA_WAVES_UPD.
-  int ca_dma = 1, ca_waves_gram = 2, ca_waves_upd = 3;
+  // registers must allow (2 or 3).  PMX_CA_DMA / PMX_CA_WAVES_GRAM / PMX_CA_WAVES_UPD.  Same-process
+  // A/B at 16384^2 (profiles/r5/ca/): pass 1 1712 us with registers vs 1815 with LDS-DMA, 2407 at 3
+  // waves (spills); pass 2 3025 at 2 waves vs 3105 at 3 (56 B of spills) -- within noise
+  int ca_dma = 0, ca_waves_gram = 2, ca_waves_upd = 3;
   // pcg1 tile shape (rows1 = 0: auto).  VEC=2 x 1 wave/workgroup won the 16384^2 sweeps
   // (bench/gpu_pcg1_sweep.sh; VEC=4 needs 256 VGPRs and is 35% slower).
   int vec1 = 2, waves1 = 1, rows1 = 0;

@@ -143,7 +143,7 @@ struct CaTiles {
   int rows2 = 0, tiles_i2 = 0;  // pass 2's tile rows (same columns)
   int cwords = 0;   // row-class words per tile column (16 rows each)
   unsigned* tbl = nullptr;  // row classes (ca_build_classes), tiles_j * cwords words, owned by the caller
-  int dma = 1;         // pass 1: interior tiles prefetch their rows by LDS-DMA (0: registers)
+  int dma = 0;         // pass 1: interior tiles prefetch their rows by LDS-DMA (0: registers)
   int waves_gram = 2;  // waves per SIMD the pass-1 registers must allow (2 or 3)
   int waves_upd = 3;   // ... pass 2 (2 or 3)
   int ntiles() const { return tiles_i * tiles_j; }
