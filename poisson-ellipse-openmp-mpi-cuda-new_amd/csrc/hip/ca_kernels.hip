@@ -151,46 +151,64 @@ __device__ __forceinline__ int ca_row_cls(const unsigned* tbl, int m) {
   return int((wd >> (2 * (r & 15))) & 3u);
 }
 
+// Face coefficients of the rows the ellipse cuts come from two precomputed fields (k_ca_faces:
+// fa = a(gi, gj), fb = b(gi, gj) at every local node, pitch as the solution fields): four vector loads
+// per lane instead of rebuilding the faces from the 1D tables, which would keep the row constants
+// and the clip arithmetic live next to the register windows (the kernel spilled with it).
+struct CaFaces {
+  const double* a;
+  const double* b;
+};
+
+// the coefficients of a lane's 2 columns at local row r (clamped into the allocated rows; rows
+// outside the grid only feed masked values)
+__device__ __forceinline__ void ca_faces(const CaFaces& F, const DevGeom& G, int r, int c0, int cmax,
+                                         double (&a0)[2], double (&a1)[2], double (&b0)[2], double (&b1)[2]) {
+  const int rc = min(max(r, -1), G.nx + 1);
+  const double* ra = F.a + int64_t(rc) * G.pitch;
+  const double* rb = F.b + int64_t(rc) * G.pitch;
+  vload<double, 2>(ca_col(ra, min(c0, cmax)), a0);
+  vload<double, 2>(ca_col(ra + G.pitch, min(c0, cmax)), a1);
+  vload<double, 2>(ca_col(rb, min(c0, cmax)), b0);
+  b1[0] = b0[1];
+  b1[1] = *ca_col(rb, min(c0 + 2, cmax + 1));
+}
+
 // L~ v on a lane's 2 columns at one row: centre c, rows above / below im / ip, lane neighbours'
 // edge columns left / right.  ucls: the row's class (!= 0: every point of the row is uniform).
-__device__ __forceinline__ void ca_lt(int ucls, int gi, const double (&c)[2], const double (&im)[2],
+__device__ __forceinline__ void ca_lt(int ucls, int r, const double (&c)[2], const double (&im)[2],
                                       const double (&ip)[2], double left, double right, const CaK& K,
-                                      const DevGeom& G, const DevTables& Tb, const double* scol, int lane,
-                                      const int (&gj)[2], double (&out)[2]) {
+                                      const DevGeom& G, const CaFaces& F, int c0, int cmax, double (&out)[2]) {
   const double jm[2] = {left, c[0]}, jp[2] = {c[1], right};
   if (ucls != 0) {
 #pragma unroll
     for (int u = 0; u < 2; ++u) out[u] = -__builtin_fma(K.cyh, jm[u] + jp[u], K.cxh * (im[u] + ip[u]));
     return;
   }
-  const RowCo rc{gi, 0};
+  double a0[2], a1[2], b0[2], b1[2];
+  ca_faces(F, G, r, c0, cmax, a0, a1, b0, b1);
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
-    double a0, a1, b0, b1;
-    coef(rc, Tb, G, scol, u, lane, gj[u], a0, a1, b0, b1);
-    if (a0 == a1 && a0 == b0 && a0 == b1) {
+    if (a0[u] == a1[u] && a0[u] == b0[u] && a0[u] == b1[u]) {
       out[u] = -__builtin_fma(K.cyh, jm[u] + jp[u], K.cxh * (im[u] + ip[u]));
     } else {
-      const double av = apply_a<false>(c[u], im[u], ip[u], jm[u], jp[u], a0, a1, b0, b1, G);
-      out[u] = av / diag<false>(a0, a1, b0, b1, G) - c[u];
+      const double av = apply_a<false>(c[u], im[u], ip[u], jm[u], jp[u], a0[u], a1[u], b0[u], b1[u], G);
+      out[u] = av / diag<false>(a0[u], a1[u], b0[u], b1[u], G) - c[u];
     }
   }
 }
 
 // D at a lane's 2 columns of a row (the Gram weight)
-__device__ __forceinline__ void ca_diag(int ucls, int gi, const CaK& K, const DevGeom& G, const DevTables& Tb,
-                                        const double* scol, int lane, const int (&gj)[2], double (&d)[2]) {
+__device__ __forceinline__ void ca_diag(int ucls, int r, const CaK& K, const DevGeom& G, const CaFaces& F, int c0,
+                                        int cmax, double (&d)[2]) {
   if (ucls != 0) {
     d[0] = d[1] = ucls == 1 ? K.d_in : K.d_out;
     return;
   }
-  const RowCo rc{gi, 0};
+  double a0[2], a1[2], b0[2], b1[2];
+  ca_faces(F, G, r, c0, cmax, a0, a1, b0, b1);
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    double a0, a1, b0, b1;
-    coef(rc, Tb, G, scol, u, lane, gj[u], a0, a1, b0, b1);
-    d[u] = diag<false>(a0, a1, b0, b1, G);
-  }
+  for (int u = 0; u < 2; ++u) d[u] = diag<false>(a0[u], a1[u], b0[u], b1[u], G);
 }
 
 // Wave lane shift of a double with zero fill at the edge lane (DPP bound_ctrl: no old value to set up)
@@ -214,7 +232,7 @@ template <typename T, int S, bool UPD, bool FAST, int PF, bool REW, int DPF = 0>
 __device__ __forceinline__ void ca_march(const DevGeom& G, const DevTables& Tb, const CaK& K,
                                          const T* __restrict__ pin, const T* __restrict__ zin, T* __restrict__ pout,
                                          T* __restrict__ zout, T* __restrict__ w, int i0, int i1, int j0, int j1,
-                                         const unsigned* __restrict__ ctbl, const double* scol,
+                                         const unsigned* __restrict__ ctbl, const CaFaces& F,
                                          double (&acc)[CaShape<S>::NQ], const double (&ca)[CaShape<S>::NB],
                                          const double (&cb)[CaShape<S>::NB], const double (&cc)[CaShape<S>::NB],
                                          const double (&pa)[S][CaShape<S>::NB], double* dring = nullptr) {
@@ -274,7 +292,7 @@ __device__ __forceinline__ void ca_march(const DevGeom& G, const DevTables& Tb, 
     const double left = dpp_shift0<kWaveShr1>(ctr[1]);
     const double right = dpp_shift0<kWaveShl1>(ctr[0]);
     double lt[2];
-    ca_lt(ch[sc], grow(r), ctr, X[l - 1][sm], X[l - 1][sp], left, right, K, G, Tb, scol, lane, gj, lt);
+    ca_lt(ch[sc], r, ctr, X[l - 1][sm], X[l - 1][sp], left, right, K, G, F, c0, cmax, lt);
     const bool rin = FAST || interior_row(r);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -320,7 +338,7 @@ __device__ __forceinline__ void ca_march(const DevGeom& G, const DevTables& Tb, 
     }
     if constexpr (!UPD) {
       double d[2];
-      ca_diag(ch[sg], grow(g), K, G, Tb, scol, lane, gj, d);
+      ca_diag(ch[sg], g, K, G, F, c0, cmax, d);
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         if (!(FAST || own[u])) continue;
@@ -451,13 +469,49 @@ __device__ __forceinline__ void ca_march(const DevGeom& G, const DevTables& Tb, 
 constexpr int kCaPfGram = PMX_CA_PF_GRAM, kCaPfUpd = PMX_CA_PF_UPD;
 
 
+// Which tiles a launch covers: the interior rectangle [ti_lo, ti_hi) x [tj_lo, tj_hi) of a pass's
+// tiling (every tile there is "fast": no Dirichlet node or partial width in reach), or the frame
+// around it.  Part 0 (all tiles) is the general kernel over the whole tiling.
+struct CaPart {
+  int part;  // 0 all, 1 interior, 2 frame
+  int tiles_i, ti_lo, ti_hi, tj_lo, tj_hi;
+};
+
+// k-th tile of a part -> (ti, tj); the frame: tile rows above the rectangle, below it, then the
+// columns left and right of it
+__device__ __forceinline__ void ca_part_tile(int k, const CaPart& P, int tiles_j, int& ti, int& tj) {
+  if (P.part == 0) {
+    ti = k / tiles_j;
+    tj = k - ti * tiles_j;
+    return;
+  }
+  const int h = P.ti_hi - P.ti_lo, wj = P.tj_hi - P.tj_lo;
+  if (P.part == 1) {
+    ti = P.ti_lo + k / wj;
+    tj = P.tj_lo + k % wj;
+    return;
+  }
+  const int ntop = P.ti_lo * tiles_j;
+  if (k < ntop) { ti = k / tiles_j; tj = k % tiles_j; return; }
+  k -= ntop;
+  const int nbot = (P.tiles_i - P.ti_hi) * tiles_j;
+  if (k < nbot) { ti = P.ti_hi + k / tiles_j; tj = k % tiles_j; return; }
+  k -= nbot;
+  if (k < h * P.tj_lo) { ti = P.ti_lo + k / P.tj_lo; tj = k % P.tj_lo; return; }
+  k -= h * P.tj_lo;
+  const int wr = tiles_j - P.tj_hi;
+  ti = P.ti_lo + k / wr;
+  tj = P.tj_hi + k % wr;
+}
+
 // MW: waves per SIMD the register allocation must allow; DMA: pass 1's interior tiles prefetch by
-// LDS-DMA (4 rows ahead) instead of registers.  The launcher picks the variant from CaTiles.
-template <typename T, int S, bool UPD, int MW, bool DMA>
+// LDS-DMA (4 rows ahead) instead of registers; PART 1: the interior tiles only, compiled without the
+// Dirichlet / partial-tile paths (whose registers would otherwise cap every tile's occupancy).
+template <typename T, int S, bool UPD, int MW, bool DMA, int PART>
 __global__ void __launch_bounds__(64, MW)
 k_ca_sweep(DevGeom G, DevTables Tb, T* w, T* z0, T* z1, T* p0, T* p1, double* __restrict__ partials,
            const PcgState* St, const CaState* C, int TI, int tiles_j, const unsigned* __restrict__ ctbl,
-           int cwords, int64_t pbase) {
+           int cwords, int64_t pbase, CaFaces faces, CaPart part, int ntiles) {
   using Sh = CaShape<S>;
   constexpr int NB = Sh::NB;
   typedef const __attribute__((address_space(4))) PcgState CPS;
@@ -475,9 +529,9 @@ k_ca_sweep(DevGeom G, DevTables Tb, T* w, T* z0, T* z1, T* p0, T* p1, double* __
     for (int j = 0; j < S; ++j) pa[j][i] = UPD ? ((CCS*)C)->pa[j][i] : 0.0;  // NOLINT
   }
   if (UPD ? nupd == 0 : done != 0) return;
-  const int ntiles = int(gridDim.x);
-  const int id = xcd_remap(blockIdx.x, gridDim.x);
-  const int ti = id / tiles_j, tj = id - ti * tiles_j;
+  int ti = 0, tj = 0;
+  ca_part_tile(xcd_remap(blockIdx.x, gridDim.x), part, tiles_j, ti, tj);
+  const int id = ti * tiles_j + tj;  // the tile's partials slot, whichever launch covers it
   const int i0 = 1 + ti * TI, i1 = min(i0 + TI - 1, G.nx);
   const int j0 = 1 + tj * Sh::WO, j1 = min(j0 + Sh::WO - 1, G.ny);
   // pass 1 reads set blk & 1; pass 2 runs after the reduction advanced blk: reads set (blk - 1) & 1
@@ -489,41 +543,37 @@ k_ca_sweep(DevGeom G, DevTables Tb, T* w, T* z0, T* z1, T* p0, T* p1, double* __
   T* zout = in ? z0 : z1;
   const CaK K = ca_consts(G);
   const int lane = threadIdx.x & 63;
-  // column constants of the lane's columns for the cut rows (coef's LDS slots)
-  __shared__ double scol[4 * 2 * 64];
   // pass 1's LDS-DMA row ring (4 slots of p, z rows, 2 KiB each)
   __shared__ double s_ring[(!UPD && DMA) ? 4 * 256 : 2];
-  {
-    const int c0 = j0 - Sh::HE + 2 * lane;
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const ColConst cc0 = load_col(Tb, min(max(G.gj0 + c0 + u, 0), G.N));
-      scol[(4 * u) * 64 + lane] = cc0.ylo;
-      scol[(4 * u + 1) * 64 + lane] = cc0.yhi;
-      scol[(4 * u + 2) * 64 + lane] = cc0.rh0;
-      scol[(4 * u + 3) * 64 + lane] = cc0.rh1;
-    }
-  }
   const unsigned* tbl = ctbl + int64_t(tj) * cwords;
-  const bool fast = j1 == j0 + Sh::WO - 1 && G.gi0 + i0 - S >= 1 && G.gi0 + i1 + S <= G.M - 1 &&
-                    G.gj0 + j0 - Sh::HE >= 1 && G.gj0 + j0 - Sh::HE + 127 <= G.N - 1;
+  const bool fast = PART == 1 || (j1 == j0 + Sh::WO - 1 && G.gi0 + i0 - S >= 1 && G.gi0 + i1 + S <= G.M - 1 &&
+                                   G.gj0 + j0 - Sh::HE >= 1 && G.gj0 + j0 - Sh::HE + 127 <= G.N - 1);
   double acc[Sh::NQ];
 #pragma unroll
   for (int q = 0; q < Sh::NQ; ++q) acc[q] = 0.0;
   // rows in flight: pass 1 (2 fields, compute-heavy) 3 rows ahead; pass 2 (3 fields) 1
   constexpr int PF = UPD ? kCaPfUpd : kCaPfGram;
 #define PMX_CA_MARCH(F, R) \
-  ca_march<T, S, UPD, F, PF, R>(G, Tb, K, pin, zin, pout, zout, w, i0, i1, j0, j1, tbl, scol, acc, ca, cb, cc, pa)
+  ca_march<T, S, UPD, F, PF, R>(G, Tb, K, pin, zin, pout, zout, w, i0, i1, j0, j1, tbl, faces, acc, ca, cb, cc, pa)
   if constexpr (UPD) {
     if (nupd < 0) {  // rewind: w only
-      if (fast) PMX_CA_MARCH(true, true);
+      if constexpr (PART == 1) PMX_CA_MARCH(true, true);
+      else if (fast) PMX_CA_MARCH(true, true);
       else PMX_CA_MARCH(false, true);
       return;
     }
   }
+  if constexpr (PART == 1) {
+    if constexpr (!UPD && DMA && sizeof(T) == 8)  // pass 1: rows prefetched by LDS-DMA
+      ca_march<T, S, UPD, true, PF, false, 4>(G, Tb, K, pin, zin, pout, zout, w, i0, i1, j0, j1, tbl, faces, acc, ca,
+                                              cb, cc, pa, s_ring);
+    else
+      PMX_CA_MARCH(true, false);
+    goto marched;
+  }
   if constexpr (!UPD && DMA && sizeof(T) == 8) {
     if (fast) {  // pass 1, interior tiles: rows prefetched by LDS-DMA
-      ca_march<T, S, UPD, true, PF, false, 4>(G, Tb, K, pin, zin, pout, zout, w, i0, i1, j0, j1, tbl, scol, acc, ca,
+      ca_march<T, S, UPD, true, PF, false, 4>(G, Tb, K, pin, zin, pout, zout, w, i0, i1, j0, j1, tbl, faces, acc, ca,
                                               cb, cc, pa, s_ring);
       goto marched;
     }
@@ -565,6 +615,18 @@ __global__ void k_ca_row_classes(DevGeom G, DevTables Tb, int he, int wo, int ti
     bits |= unsigned(row_class(rc, gjlo, gjhi)) << (2 * q);
   }
   out[t] = bits;
+}
+
+// The face coefficients of every local node (rows -1 .. nx+2, columns -1 .. ny+2): a(gi, gj) and
+// b(gi, gj) by the exact formula (the class fast values are bit-identical to it).
+__global__ void __launch_bounds__(256) k_ca_faces(DevGeom G, DevTables Tb, double* fa, double* fb) {
+  const int lj = -1 + int(blockIdx.x * blockDim.x + threadIdx.x);
+  const int li = -1 + int(blockIdx.y);
+  if (lj > G.ny + 2) return;
+  const int gi = min(max(G.gi0 + li, 0), G.M), gj = min(max(G.gj0 + lj, 0), G.N);
+  const int64_t o = int64_t(li) * G.pitch + lj;
+  fa[o] = coef_a(Tb, G, gi, gj);
+  fb[o] = coef_b(Tb, G, gi, gj);
 }
 
 // z^0 = D^-1 r^0 in place and p^0 = z^0 (set 0): the state the first block starts from.
@@ -837,6 +899,30 @@ CaTiles make_ca_tiles(const DevGeom& G, int s, int rows, int rows2) {
   PMX_CHECK(rows2 >= 1 && rows2 <= 4096, "s-step PCG: pass-2 tile rows must be in [1, 4096]");
   t.rows2 = rows2;
   t.tiles_i2 = (G.nx + rows2 - 1) / rows2;
+  // interior rectangles (k_ca_sweep's `fast`): rows i0 - s .. i1 + s and columns j0 - he .. j0 - he + 127
+  // strictly inside the grid, full width.  i0 = 1 + ti rows: ti >= 1 and (ti + 1) rows <= nx - s; j0 = 1 +
+  // tj wo: tj >= 1 and tj wo + 128 - he <= ny.  Checked tile by tile against the kernel's condition.
+  auto fast = [&](int ti, int tj, int r) {
+    const int i0 = 1 + ti * r, i1 = std::min(i0 + r - 1, G.nx);
+    const int j0 = 1 + tj * t.wo, j1 = std::min(j0 + t.wo - 1, G.ny);
+    return j1 == j0 + t.wo - 1 && G.gi0 + i0 - s >= 1 && G.gi0 + i1 + s <= G.M - 1 && G.gj0 + j0 - t.he >= 1 &&
+           G.gj0 + j0 - t.he + 127 <= G.N - 1;
+  };
+  t.tj_lo = std::min(1, t.tiles_j);
+  t.tj_hi = std::max(t.tj_lo, std::min(t.tiles_j, (G.ny - 128 + t.he) / t.wo + 1));
+  auto rect = [&](int r, int tiles_i, int& lo, int& hi) {
+    lo = std::min(1, tiles_i);
+    hi = std::max(lo, std::min(tiles_i, (G.nx - s) / r));
+    if (hi <= lo || t.tj_hi <= t.tj_lo) { lo = hi = 0; return; }
+    for (int ti = 0; ti < tiles_i; ++ti)
+      for (int tj = 0; tj < t.tiles_j; ++tj) {
+        const bool in = ti >= lo && ti < hi && tj >= t.tj_lo && tj < t.tj_hi;
+        PMX_CHECK(!in || fast(ti, tj, r), "s-step PCG: interior tile (" << ti << ", " << tj << ") is not fast");
+      }
+  };
+  rect(rows, t.tiles_i, t.ti_lo, t.ti_hi);
+  rect(rows2, t.tiles_i2, t.ti_lo2, t.ti_hi2);
+  if (t.ti_hi <= t.ti_lo || t.ti_hi2 <= t.ti_lo2) t.split = 0;
   t.cwords = (G.nx + 2 * s + 2 * kCaRowOff + 15) / 16 + 1;
   return t;
 }
@@ -850,6 +936,12 @@ void ca_build_classes(const DevGeom& G, const DevTables& Tb, const CaTiles& t, u
   HIP_CHECK(hipGetLastError());
 }
 
+void ca_build_faces(const DevGeom& G, const DevTables& Tb, double* fa, double* fb, hipStream_t s) {
+  PMX_CHECK(G.nx + 4 <= 65535, "k_ca_faces: grid.y limit");
+  hipLaunchKernelGGL(k_ca_faces, dim3((G.ny + 4 + 255) / 256, G.nx + 4), dim3(256), 0, s, G, Tb, fa, fb);
+  HIP_CHECK(hipGetLastError());
+}
+
 template <typename T>
 void launch_ca_init(const DevGeom& G, const DevTables& Tb, T* z, T* p, hipStream_t s) {
   PMX_CHECK(G.nx <= 65535, "k_ca_init: grid.y limit");
@@ -859,33 +951,55 @@ void launch_ca_init(const DevGeom& G, const DevTables& Tb, T* z, T* p, hipStream
 
 template <typename T>
 void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, T* p0, T* p1, double* partials,
-                     const PcgState* S, const CaState* C, const CaTiles& t, bool upd, hipStream_t s) {
+                     const PcgState* S, const CaState* C, const CaTiles& t, bool upd, hipStream_t s,
+                     hipStream_t sframe) {
   PMX_CHECK(G.nb == 0, "s-step PCG runs undecomposed grids");
-  PMX_CHECK(t.tbl != nullptr, "s-step PCG: row-class table missing");
+  if (!sframe) sframe = s;
+  PMX_CHECK(t.tbl != nullptr && t.fa != nullptr && t.fb != nullptr, "s-step PCG: row-class / face tables missing");
+  PMX_CHECK(sizeof(T) == 8 || !t.dma, "s-step PCG: LDS-DMA rows need fp64");
   const int n = upd ? t.ntiles2() : t.ntiles();
   const int rows = upd ? t.rows2 : t.rows;
   const int64_t pbase = upd ? int64_t(ca_nq(t.s) - t.s) * t.ntiles() : 0;  // norms after the Gram products
-#define PMX_CA_K(SS, U, MW, D)                                                                                \
-  hipLaunchKernelGGL((k_ca_sweep<T, SS, U, MW, D>), dim3(n), dim3(64), 0, s, G, Tb, w, z0, z1, p0, p1, partials, S, C, \
-                     rows, t.tiles_j, t.tbl, t.cwords, pbase)
-#define PMX_CA(SS)                                                                                              \
-  do {                                                                                                          \
-    if (upd) {                                                                                                  \
-      if (t.waves_upd == 2) PMX_CA_K(SS, true, 2, false);                                                       \
-      else PMX_CA_K(SS, true, 3, false);                                                                        \
-    } else if (t.dma) {                                                                                         \
-      if (t.waves_gram == 3) PMX_CA_K(SS, false, 3, true);                                                      \
-      else PMX_CA_K(SS, false, 2, true);                                                                        \
-    } else {                                                                                                    \
-      if (t.waves_gram == 3) PMX_CA_K(SS, false, 3, false);                                                     \
-      else PMX_CA_K(SS, false, 2, false);                                                                       \
-    }                                                                                                           \
+  const int ti_lo = upd ? t.ti_lo2 : t.ti_lo, ti_hi = upd ? t.ti_hi2 : t.ti_hi;
+  const int tiles_i = upd ? t.tiles_i2 : t.tiles_i;
+  const int nin = (ti_hi - ti_lo) * (t.tj_hi - t.tj_lo);
+  const CaFaces F{t.fa, t.fb};
+  const CaPart P1{1, tiles_i, ti_lo, ti_hi, t.tj_lo, t.tj_hi}, P2{2, tiles_i, ti_lo, ti_hi, t.tj_lo, t.tj_hi},
+      P0{0, tiles_i, 0, 0, 0, 0};
+#define PMX_CA_K(SS, U, MW, D, PT, PP, NB)                                                                          \
+  do {                                                                                                              \
+    if ((NB) > 0)                                                                                                   \
+      hipLaunchKernelGGL((k_ca_sweep<T, SS, U, MW, D, PT>), dim3(NB), dim3(64), 0, (PT) == 2 ? sframe : s, G, Tb, w, \
+                         z0, z1, p0, p1, partials, S, C, rows, t.tiles_j, t.tbl, t.cwords, pbase, F, PP, n);        \
   } while (0)
-  PMX_CHECK(sizeof(T) == 8 || !t.dma, "s-step PCG: LDS-DMA rows need fp64");
+  // split (default): the interior tiles with the fast-only kernel at 3 waves per SIMD, the frame with
+  // the general one at 2; else every tile general at waves_gram / waves_upd
+#define PMX_CA(SS)                                                                                                   \
+  do {                                                                                                               \
+    if (t.split && nin > 0) {                                                                                        \
+      if (upd) {                                                                                                     \
+        PMX_CA_K(SS, true, 2, false, 2, P2, n - nin);                                                                \
+        PMX_CA_K(SS, true, 3, false, 1, P1, nin);                                                                    \
+      } else {                                                                                                       \
+        PMX_CA_K(SS, false, 2, false, 2, P2, n - nin);                                                               \
+        if (t.dma) PMX_CA_K(SS, false, 3, true, 1, P1, nin);                                                         \
+        else PMX_CA_K(SS, false, 2, false, 1, P1, nin); /* register rows: 3 waves would spill */                     \
+      }                                                                                                              \
+    } else if (upd) {                                                                                                \
+      if (t.waves_upd == 2) PMX_CA_K(SS, true, 2, false, 0, P0, n);                                                  \
+      else PMX_CA_K(SS, true, 3, false, 0, P0, n);                                                                   \
+    } else if (t.dma) {                                                                                              \
+      if (t.waves_gram == 3) PMX_CA_K(SS, false, 3, true, 0, P0, n);                                                 \
+      else PMX_CA_K(SS, false, 2, true, 0, P0, n);                                                                   \
+    } else {                                                                                                         \
+      if (t.waves_gram == 3) PMX_CA_K(SS, false, 3, false, 0, P0, n);                                                \
+      else PMX_CA_K(SS, false, 2, false, 0, P0, n);                                                                  \
+    }                                                                                                                \
+  } while (0)
   if (t.s == 2) PMX_CA(2);
   else PMX_CA(3);
-#undef PMX_CA_K
 #undef PMX_CA
+#undef PMX_CA_K
   HIP_CHECK(hipGetLastError());
 }
 
@@ -905,6 +1019,7 @@ void launch_ca_reduce(const double* partials, int n, int n2, int s_, double h, d
 
 template void launch_ca_init<double>(const DevGeom&, const DevTables&, double*, double*, hipStream_t);
 template void launch_ca_sweep<double>(const DevGeom&, const DevTables&, double*, double*, double*, double*, double*,
-                                      double*, const PcgState*, const CaState*, const CaTiles&, bool, hipStream_t);
+                                      double*, const PcgState*, const CaState*, const CaTiles&, bool, hipStream_t,
+                                      hipStream_t);
 
 }  // namespace pmx

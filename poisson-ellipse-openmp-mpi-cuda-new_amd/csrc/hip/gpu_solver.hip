@@ -119,6 +119,9 @@ GpuOptions resolve_options(const GpuOptions& in) {
   PMX_CHECK(o.ca_s == 2 || o.ca_s == 3, "s-step PCG: s must be 2 or 3");
   PMX_CHECK(o.ca_rows >= 0 && o.ca_rows <= 4096, "s-step PCG: tile rows must be 0 (auto) .. 4096");
   env_int("PMX_CA_DMA", o.ca_dma);
+  env_int("PMX_CA_SPLIT", o.ca_split);
+  env_int("PMX_CA_FRAME_STREAM", o.ca_frame_stream);
+  PMX_CHECK(o.ca_split == 0 || o.ca_split == 1, "s-step PCG: ca_split must be 0 or 1");
   env_int("PMX_CA_WAVES_GRAM", o.ca_waves_gram);
   env_int("PMX_CA_WAVES_UPD", o.ca_waves_upd);
   PMX_CHECK(o.ca_dma == 0 || o.ca_dma == 1, "s-step PCG: ca_dma must be 0 or 1");
@@ -228,7 +231,7 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   field_off_ = size_t(G.pitch) + align_elems - 1;
   field_bytes_ = round_up((align_elems - 1 + size_t(sd.nx + 4) * G.pitch) * elem_, 256);
   {  // fail with a sizing message instead of a bare hipErrorOutOfMemory
-    const size_t need = estimate_device_bytes(spec, sd, opt.dtype, pcg1_ || ca_);
+    const size_t need = estimate_device_bytes(spec, sd, opt.dtype, pcg1_ || ca_) + (ca_ ? 2 * field_bytes_ : 0);
     PMX_CHECK(need <= free_b,
               "subdomain " << sd.nx << "x" << sd.ny << " (" << (pcg1_ ? "pcg1, 5" : "pcg2, 4")
                            << " fields) needs " << need / 1e9 << " GB on device " << opt.device
@@ -333,7 +336,18 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   if (ca_) {
     r2_ = field_raw(4);  // the second z buffer
     ca_tiles_ = make_ca_tiles(G, opt_.ca_s, opt_.ca_rows, opt_.ca_rows2);
+    // the face coefficients of every node, read on the rows the ellipse cuts (2 more field-sized arrays)
+    HIP_CHECK(hipMalloc(&ca_faces_, 2 * field_bytes_));
+    ca_tiles_.fa = reinterpret_cast<const double*>(ca_faces_ + field_off_ * elem_);
+    ca_tiles_.fb = reinterpret_cast<const double*>(ca_faces_ + field_bytes_ + field_off_ * elem_);
+    ca_build_faces(G, tables_, const_cast<double*>(ca_tiles_.fa), const_cast<double*>(ca_tiles_.fb), nullptr);
     ca_tiles_.dma = opt_.ca_dma;
+    if (!opt_.ca_split) ca_tiles_.split = 0;
+    if (ca_tiles_.split && opt_.ca_frame_stream) {
+      HIP_CHECK(hipStreamCreateWithFlags(&ca_side_, hipStreamNonBlocking));
+      HIP_CHECK(hipEventCreateWithFlags(&ca_ev_fork_, hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&ca_ev_join_, hipEventDisableTiming));
+    }
     ca_tiles_.waves_gram = opt_.ca_waves_gram;
     ca_tiles_.waves_upd = opt_.ca_waves_upd;
     HIP_CHECK(hipMalloc(&ca_tbl_, size_t(ca_tiles_.tiles_j) * ca_tiles_.cwords * sizeof(unsigned)));
@@ -530,6 +544,13 @@ void GpuSubdomainSolver::release() noexcept {
   if (tile_order_) (void)hipFree(tile_order_);
   if (tile_order_w_) (void)hipFree(tile_order_w_);
   if (ca_tbl_) (void)hipFree(ca_tbl_);
+  if (ca_faces_) (void)hipFree(ca_faces_);
+  if (ca_side_) (void)hipStreamDestroy(ca_side_);
+  if (ca_ev_fork_) (void)hipEventDestroy(ca_ev_fork_);
+  if (ca_ev_join_) (void)hipEventDestroy(ca_ev_join_);
+  ca_side_ = nullptr;
+  ca_ev_fork_ = ca_ev_join_ = nullptr;
+  ca_faces_ = nullptr;
   if (ca_state_) (void)hipFree(ca_state_);
   if (ca_chunk_) (void)hipFree(ca_chunk_);
   ca_tbl_ = nullptr;
@@ -585,7 +606,7 @@ size_t GpuSubdomainSolver::device_bytes() const {
   const size_t tables = (4 * size_t(spec_.M + 2) + 4 * size_t(spec_.N + 2)) * sizeof(double) +
                         8 * size_t(spec_.M + 2) * sizeof(int);
   return (r2_ ? 5 : 4) * field_stride_ + tables + (npart_ * 5 + kReduceWsDoubles) * sizeof(double) +
-         (own_arena_ ? layout_.bytes : 0);
+         (own_arena_ ? layout_.bytes : 0) + (ca_faces_ ? 2 * field_bytes_ : 0);
 }
 
 void* GpuSubdomainSolver::field_base(int which) const {
@@ -649,38 +670,46 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
   }
 }
 
-void GpuSubdomainSolver::enqueue_ca_block(hipStream_t s, int n) {
-  PMX_CHECK(ca_ && elem_ == 8, "enqueue_ca_block: not an s-step solver");
+// One s-step pass: with the split kernels the frame tiles run on a side stream, concurrently with the
+// interior (their few long marches would otherwise trail the pass by ~0.1 ms)
+void GpuSubdomainSolver::ca_sweep(hipStream_t s, bool upd) {
   double* w = static_cast<double*>(field_base(0));
   double* z0 = static_cast<double*>(field_base(1));
   double* z1 = reinterpret_cast<double*>(r2_ + field_off_ * elem_);
   double* p0 = static_cast<double*>(field_base(2));
   double* p1 = static_cast<double*>(field_base(3));
-  const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
-  launch_ca_sweep<double>(geom_, tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, false, s);
+  if (ca_side_) {
+    HIP_CHECK(hipEventRecord(ca_ev_fork_, s));
+    HIP_CHECK(hipStreamWaitEvent(ca_side_, ca_ev_fork_, 0));
+    launch_ca_sweep<double>(geom_, tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, upd, s,
+                            ca_side_);
+    HIP_CHECK(hipEventRecord(ca_ev_join_, ca_side_));
+    HIP_CHECK(hipStreamWaitEvent(s, ca_ev_join_, 0));
+  } else {
+    launch_ca_sweep<double>(geom_, tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, upd, s);
+  }
   after_launch(s);
+}
+
+void GpuSubdomainSolver::enqueue_ca_block(hipStream_t s, int n) {
+  PMX_CHECK(ca_ && elem_ == 8, "enqueue_ca_block: not an s-step solver");
+  const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
+  ca_sweep(s, false);
   launch_ca_reduce(partials_, ca_tiles_.ntiles(), ca_tiles_.ntiles2(), ca_tiles_.s, g_.h1h2, wdiff, n, false, state_, ca_state_,
                    ca_chunk_, s, progress_dev_);
   after_launch(s);
-  launch_ca_sweep<double>(geom_, tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, true, s);
-  after_launch(s);
+  ca_sweep(s, true);
   host_k_ += n;
 }
 
 void GpuSubdomainSolver::enqueue_ca_check(hipStream_t s) {
   PMX_CHECK(ca_ && elem_ == 8, "enqueue_ca_check: not an s-step solver");
-  double* w = static_cast<double*>(field_base(0));
-  double* z0 = static_cast<double*>(field_base(1));
-  double* z1 = reinterpret_cast<double*>(r2_ + field_off_ * elem_);
-  double* p0 = static_cast<double*>(field_base(2));
-  double* p1 = static_cast<double*>(field_base(3));
   const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
   launch_ca_reduce(partials_, ca_tiles_.ntiles(), ca_tiles_.ntiles2(), ca_tiles_.s, g_.h1h2, wdiff, 1, true, state_, ca_state_, ca_chunk_,
                    s, progress_dev_);
   after_launch(s);
   // a stop inside the last block rewinds w (every workgroup returns at once otherwise)
-  launch_ca_sweep<double>(geom_, tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, true, s);
-  after_launch(s);
+  ca_sweep(s, true);
 }
 
 template <typename T>

@@ -80,7 +80,13 @@ struct GpuOptions {
   // registers must allow (2 or 3).  PMX_CA_DMA / PMX_CA_WAVES_GRAM / PMX_CA_WAVES_UPD.  Same-process
   // A/B at 16384^2 (profiles/r5/ca/): pass 1 1712 us with registers vs 1815 with LDS-DMA, 2407 at 3
   // waves (spills); pass 2 3025 at 2 waves vs 3105 at 3 (56 B of spills) -- within noise
-  int ca_dma = 0, ca_waves_gram = 2, ca_waves_upd = 3;
+  int ca_dma = 1, ca_waves_gram = 2, ca_waves_upd = 3;
+  // s-step: the interior tiles of each pass by a kernel without the Dirichlet / partial-tile paths, whose
+  // registers fit 3 waves per SIMD (pass 1 with LDS-DMA rows), the frame by the general kernel (1), or
+  // every tile by the general kernel (0).  PMX_CA_SPLIT.
+  int ca_split = 1;
+  // ... the frame kernel on a side stream, overlapping the interior (1), or after it (0).  PMX_CA_FRAME_STREAM.
+  int ca_frame_stream = 1;
   // pcg1 tile shape (rows1 = 0: auto).  VEC=2 x 1 wave/workgroup won the 16384^2 sweeps
   // (bench/gpu_pcg1_sweep.sh; VEC=4 needs 256 VGPRs and is 35% slower).
   int vec1 = 2, waves1 = 1, rows1 = 0;
@@ -334,6 +340,10 @@ class GpuSubdomainSolver {
   bool ca_ = false;             // s-step PCG
   CaTiles ca_tiles_{};
   unsigned* ca_tbl_ = nullptr;  // its row-class table
+  char* ca_faces_ = nullptr;    // its face-coefficient fields (a, b)
+  hipStream_t ca_side_ = nullptr;  // the frame tiles' stream (split kernels)
+  hipEvent_t ca_ev_fork_ = nullptr, ca_ev_join_ = nullptr;
+  void ca_sweep(hipStream_t s, bool upd);
   CaState* ca_state_ = nullptr;
   double* ca_chunk_ = nullptr;  // its reduction's chunk sums
   long long host_k_ = 0;

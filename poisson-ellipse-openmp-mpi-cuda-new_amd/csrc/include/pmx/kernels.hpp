@@ -143,7 +143,13 @@ struct CaTiles {
   int rows2 = 0, tiles_i2 = 0;  // pass 2's tile rows (same columns)
   int cwords = 0;   // row-class words per tile column (16 rows each)
   unsigned* tbl = nullptr;  // row classes (ca_build_classes), tiles_j * cwords words, owned by the caller
-  int dma = 0;         // pass 1: interior tiles prefetch their rows by LDS-DMA (0: registers)
+  const double* fa = nullptr;  // face coefficients a, b at every local node (ca_build_faces), pitched as
+  const double* fb = nullptr;  // the fields, local (0, 0); read on the rows the ellipse cuts
+  // interior rectangles of the two tilings (every tile "fast": no Dirichlet node or partial width in
+  // reach): [ti_lo, ti_hi) x [tj_lo, tj_hi) for pass 1, [ti_lo2, ti_hi2) x (same columns) for pass 2
+  int ti_lo = 0, ti_hi = 0, tj_lo = 0, tj_hi = 0, ti_lo2 = 0, ti_hi2 = 0;
+  int split = 1;       // interior tiles by a fast-only kernel at 3 waves per SIMD, the frame by the general one
+  int dma = 1;         // pass 1: interior tiles prefetch their rows by LDS-DMA (0: registers)
   int waves_gram = 2;  // waves per SIMD the pass-1 registers must allow (2 or 3)
   int waves_upd = 3;   // ... pass 2 (2 or 3)
   int ntiles() const { return tiles_i * tiles_j; }
@@ -152,12 +158,16 @@ struct CaTiles {
 CaTiles make_ca_tiles(const DevGeom& G, int s, int rows, int rows2 = 0);
 int ca_nq(int s);  // partials per tile (pass 1's Gram products + pass 2's norms)
 void ca_build_classes(const DevGeom& G, const DevTables& Tb, const CaTiles& t, unsigned* tbl, hipStream_t s);
+// fa / fb: local (0, 0) of two field-sized arrays (rows -1 .. nx+2 allocated)
+void ca_build_faces(const DevGeom& G, const DevTables& Tb, double* fa, double* fb, hipStream_t s);
 // z = D^-1 r in place, p = z (the first block's set 0)
 template <typename T>
 void launch_ca_init(const DevGeom& G, const DevTables& Tb, T* z, T* p, hipStream_t s);
 template <typename T>
+// sframe: the stream of the frame tiles' kernel with t.split (nullptr: s); the caller forks and joins it
 void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, T* p0, T* p1, double* partials,
-                     const PcgState* S, const CaState* C, const CaTiles& t, bool upd, hipStream_t s);
+                     const PcgState* S, const CaState* C, const CaTiles& t, bool upd, hipStream_t s,
+                     hipStream_t sframe = nullptr);
 // chunk: kCaReduceMaxBlocks * ca_nq(s) doubles of workspace; nmax: iterations this block may run
 constexpr int kCaReduceMaxBlocks = 256;
 // check_only: the pending stop test alone (after the last block of a batch; pass 2 then rewinds w if
