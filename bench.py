@@ -584,10 +584,12 @@ def measure(args) -> int:
         comm_used = "gloo" if world > 1 else "self"
     elif world == 1:
         models = importlib.import_module(pkg_name + ".models")
-        # auto on one GPU: the s-step PCG (ca_kernels.hip) where it applies -- fp64, fast arithmetic
-        # (same iteration counts, 64 instead of 3 x 37.3 B/pt per 3 iterations); else pcg1 / pcg2
+        # auto on one GPU: the s-step PCG (ca_kernels.hip) where it applies and wins -- fp64, fast
+        # arithmetic, bandwidth-bound grids (same iteration counts, 64 instead of 3 x 37.3 B/pt per 3
+        # iterations; 16384^2 1.23-1.32 vs 1.90 ms on one box).  Below ~6M points pcg1's block tiles
+        # win (1600x2400 54.2 vs 63.1 us/iteration, 2400x3200 92.2 vs 87.2: profiles/r5/ca/small.log)
         algo = args.algo
-        if algo == "auto" and args.dtype == "fp64" and not args.exact:
+        if algo == "auto" and args.dtype == "fp64" and not args.exact and (args.M - 1) * (args.N - 1) >= 6_000_000:
             algo = "ca"
         runner = ds.SessionRunner(models.make_session(problem, ranks=1, device=info.local_rank,
                                                       block_tiles={"auto": -1, "on": 1, "off": 0}[args.block_tiles],
