@@ -549,8 +549,6 @@ def measure(args) -> int:
     info = launch.init_distributed(backend=backend if env.world > 1 else None,
                                    device_type="cpu" if (dry or share or backend == "gloo") else None)
     world = info.world
-    if args.algo == "ca" and world > 1:
-        raise SystemExit("[bench] --algo ca (the s-step PCG) runs undecomposed grids on one GPU; use auto / pcg1")
     device = 0 if share else info.local_rank
     if not dry:
         if not torch.cuda.is_available():
@@ -575,6 +573,16 @@ def measure(args) -> int:
     pkw = dict(placement=0 if share else args.placement, placement_budget_s=args.placement_budget,
                placement_keep_free=args.placement_keep_free)
     dkw = dict(kw, **pkw, phase=watch.phase, init_timeout=COMM_INIT_TIMEOUT)
+    # the s-step PCG (ca_kernels.hip) where it applies and wins: fp64 with the fast arithmetic, >= 6M
+    # points (below, pcg1's block tiles win: profiles/r5/ca/small.log), undecomposed or row strips, and
+    # a transport that moves its ghost rows straight between the fields (RCCL, not IPC / torch)
+    strips = world == 1 or process_grid(world, args.M, args.N, args.split)[1] == 1
+    ca_ok = (args.dtype == "fp64" and not args.exact and strips and
+             (world == 1 or (not share and cfg["comm"] == "native")))
+    if args.algo == "ca" and not ca_ok:
+        raise SystemExit("[bench] --algo ca (the s-step PCG) needs fp64, row strips and the native RCCL transport")
+    use_ca = args.algo == "ca" or (args.algo == "auto" and ca_ok and (args.M - 1) * (args.N - 1) >= 6_000_000)
+    algo_id = 3 if use_ca else {"auto": -1, "pcg1": 1, "pcg2": 2}[args.algo]
     if dry:
         tp = importlib.import_module(pkg_name + ".models.torch_pcg")
         comm = importlib.import_module(pkg_name + ".parallel.comm")
@@ -584,16 +592,10 @@ def measure(args) -> int:
         comm_used = "gloo" if world > 1 else "self"
     elif world == 1:
         models = importlib.import_module(pkg_name + ".models")
-        # auto on one GPU: the s-step PCG (ca_kernels.hip) where it applies and wins -- fp64, fast
-        # arithmetic, bandwidth-bound grids (same iteration counts, 64 instead of 3 x 37.3 B/pt per 3
-        # iterations; 16384^2 1.23-1.32 vs 1.90 ms on one box).  Below ~6M points pcg1's block tiles
-        # win (1600x2400 54.2 vs 63.1 us/iteration, 2400x3200 92.2 vs 87.2: profiles/r5/ca/small.log)
-        algo = args.algo
-        if algo == "auto" and args.dtype == "fp64" and not args.exact and (args.M - 1) * (args.N - 1) >= 6_000_000:
-            algo = "ca"
+
         runner = ds.SessionRunner(models.make_session(problem, ranks=1, device=info.local_rank,
                                                       block_tiles={"auto": -1, "on": 1, "off": 0}[args.block_tiles],
-                                                      algo=algo, ca_s=args.ca_s, **pkw, **kw), problem, info)
+                                                      algo=algo_id, ca_s=args.ca_s, **pkw, **kw), problem, info)
         comm_used = "self"
     elif share and cfg["comm"] == "ipc":
         runner = ds.DistGpuPCG(problem, info, comm="ipc", device=0, **dkw)
@@ -605,7 +607,7 @@ def measure(args) -> int:
         runner = ds.DistGpuPCG(problem, info, comm="ipc", **dkw)
         comm_used = "ipc"
     elif cfg["comm"] == "native":
-        runner = ds.DistGpuPCG(problem, info, comm="native", rccl_graph=cfg["rccl_graph"], **dkw)
+        runner = ds.DistGpuPCG(problem, info, comm="native", rccl_graph=cfg["rccl_graph"], algo=algo_id, **dkw)
         comm_used = "rccl"
     else:
         runner = ds.DistGpuPCG(problem, info, comm="torch", **dkw)
@@ -796,10 +798,17 @@ def measure_loopback(args) -> int:
     if not 0 <= args.loopback_rank < args.gpus:
         raise SystemExit("--loopback-rank must be in [0, --gpus)")
     problem = pmx.PoissonEllipse(M=args.M, N=args.N, breakdown_tol=args.breakdown_tol)
+    # the algorithm the real N-GPU run would use (see measure: the s-step PCG on big fp64 row strips)
+    decomp = importlib.import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.parallel.decomp")
+    strips = decomp.process_grid(args.gpus, args.M, args.N, args.split)[1] == 1
+    ca_ok = args.dtype == "fp64" and not args.exact and strips
+    use_ca = args.algo == "ca" or (args.algo == "auto" and ca_ok and (args.M - 1) * (args.N - 1) >= 6_000_000)
+    algo_id = 3 if use_ca else {"auto": -1, "pcg1": 1, "pcg2": 2, "ca": 3}[args.algo]
     s = native.Session(problem.to_native(), world=args.gpus, comm="loopback", split=getattr(native.Split, args.split),
                        ranks=[args.loopback_rank], devices=[0], dtype=args.dtype, graph_batch=args.graph_batch,
                        overlap=args.overlap == "on", placement=args.placement,
-                       placement_budget_s=args.placement_budget, placement_keep_free=args.placement_keep_free)
+                       placement_budget_s=args.placement_budget, placement_keep_free=args.placement_keep_free,
+                       algo=algo_id, ca_s=args.ca_s)
     sd = s.subdomain(0)
     s.init()
     s.step(args.warmup)

@@ -74,9 +74,10 @@ class LocalComm final : public Comm {
       PMX_CHECK(local[i]->sd().rank == int(i), "LocalComm needs local[i].rank == i");
     }
     HIP_CHECK(hipSetDevice(dev));
-    // device table of the all-reduce buffers: [which][rank] for red_a, red_b, red_c
+    // device table of the all-reduce buffers: [which][rank] for red_a, red_b, red_c and the s-step
+    // sums (nullptr without the s-step solver: never all-reduced then)
     std::vector<double*> p;
-    for (int which = 0; which < 3; ++which)
+    for (int which = 0; which < 4; ++which)
       for (auto* s : local) p.push_back(s->reduce_buf(which));
     HIP_CHECK(hipMalloc(&ptrs_, p.size() * sizeof(double*)));
     HIP_CHECK(hipMemcpy(ptrs_, p.data(), p.size() * sizeof(double*), hipMemcpyHostToDevice));

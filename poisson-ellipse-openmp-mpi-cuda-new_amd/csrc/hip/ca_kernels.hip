@@ -158,13 +158,14 @@ __device__ __forceinline__ int ca_row_cls(const unsigned* tbl, int m) {
 struct CaFaces {
   const double* a;
   const double* b;
+  int gh;  // ghost rows allocated on each side of the fields (rows 1-gh .. nx+gh exist): 2, or 3 for strips
 };
 
 // the coefficients of a lane's 2 columns at local row r (clamped into the allocated rows; rows
 // outside the grid only feed masked values)
 __device__ __forceinline__ void ca_faces(const CaFaces& F, const DevGeom& G, int r, int c0, int cmax,
                                          double (&a0)[2], double (&a1)[2], double (&b0)[2], double (&b1)[2]) {
-  const int rc = min(max(r, -1), G.nx + 1);
+  const int rc = min(max(r, 1 - F.gh), G.nx + F.gh - 1);
   const double* ra = F.a + int64_t(rc) * G.pitch;
   const double* rb = F.b + int64_t(rc) * G.pitch;
   vload<double, 2>(ca_col(ra, min(c0, cmax)), a0);
@@ -257,11 +258,11 @@ __device__ __forceinline__ void ca_march(const DevGeom& G, const DevTables& Tb, 
   auto interior_row = [&](int m) { return G.gi0 + m >= 1 && G.gi0 + m <= G.M - 1; };
 
   auto fetch = [&](int m, CaRow<T, S, UPD>& b) {
-    const int mc = min(max(m, -1), G.nx + 2);  // rows -1 .. nx+2 exist
+    const int mc = min(max(m, 1 - F.gh), G.nx + F.gh);  // the allocated rows
     ca_load2<T>(pin + int64_t(mc) * P, c0, cmax, b.p);
     ca_load2<T>(zin + int64_t(mc) * P, c0, cmax, b.z);
     if constexpr (UPD) {  // w of the row this step updates (S rows behind)
-      const int wc = min(max(m - S, -1), G.nx + 2);
+      const int wc = min(max(m - S, 1 - F.gh), G.nx + F.gh);
       ca_load2<T>(w + int64_t(wc) * P, c0, cmax, b.w);
     }
   };
@@ -619,9 +620,9 @@ __global__ void k_ca_row_classes(DevGeom G, DevTables Tb, int he, int wo, int ti
 
 // The face coefficients of every local node (rows -1 .. nx+2, columns -1 .. ny+2): a(gi, gj) and
 // b(gi, gj) by the exact formula (the class fast values are bit-identical to it).
-__global__ void __launch_bounds__(256) k_ca_faces(DevGeom G, DevTables Tb, double* fa, double* fb) {
+__global__ void __launch_bounds__(256) k_ca_faces(DevGeom G, DevTables Tb, double* fa, double* fb, int gh) {
   const int lj = -1 + int(blockIdx.x * blockDim.x + threadIdx.x);
-  const int li = -1 + int(blockIdx.y);
+  const int li = 1 - gh + int(blockIdx.y);
   if (lj > G.ny + 2) return;
   const int gi = min(max(G.gi0 + li, 0), G.M), gj = min(max(G.gj0 + lj, 0), G.N);
   const int64_t o = int64_t(li) * G.pitch + lj;
@@ -800,7 +801,7 @@ __device__ void ca_finish(const double* t, const double* u, double h, double wdi
 template <int S>
 __global__ void __launch_bounds__(256)
 k_ca_reduce(const double* __restrict__ part, int n, int n2, double h, double wdiff, int nmax, int check_only,
-            PcgState* St, CaState* C, double* chunk, long long* progress) {
+            int finish, PcgState* St, CaState* C, double* chunk, long long* progress) {
   using Sh = CaShape<S>;
   constexpr int NT = Sh::NQ + Sh::NN;
   __shared__ double lds[NT][256 / kWave];
@@ -868,10 +869,34 @@ k_ca_reduce(const double* __restrict__ part, int n, int n2, double h, double wdi
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   if (lane == 0) {
-    ca_finish<S>(tot, tot + Sh::NQ, h, wdiff, nmax, check_only != 0, St, C);
-    if (progress) __hip_atomic_store(progress, St->it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (finish) {
+      ca_finish<S>(tot, tot + Sh::NQ, h, wdiff, nmax, check_only != 0, St, C);
+      if (progress) __hip_atomic_store(progress, St->it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    } else {  // decomposed: the rank's sums, all-reduced before k_ca_finish
+      for (int q = 0; q < NT; ++q) C->red[q] = tot[q];
+    }
     if (nb > 1) C->ticket = 0u;  // re-arm for the next launch (stream order makes this visible to it)
   }
+}
+
+// Decomposed grids: ca_finish on the all-reduced sums (CaState::red), after the all-reduce.
+template <int S>
+__global__ void __launch_bounds__(64)
+k_ca_finish(double h, double wdiff, int nmax, int check_only, PcgState* St, CaState* C, long long* progress) {
+  if (threadIdx.x != 0) return;
+  if (St->done) {
+    C->nupd = 0;
+    return;
+  }
+  double t[7 * S];
+  bool bad = false;
+  for (int q = 0; q < 7 * S; ++q) {
+    t[q] = C->red[q];
+    bad |= !(t[q] == t[q]) || isinf(t[q]);
+  }
+  if (bad) St->nan_flag = 1;
+  ca_finish<S>(t, t + 6 * S, h, wdiff, nmax, check_only != 0, St, C);
+  if (progress) __hip_atomic_store(progress, St->it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace
@@ -936,9 +961,9 @@ void ca_build_classes(const DevGeom& G, const DevTables& Tb, const CaTiles& t, u
   HIP_CHECK(hipGetLastError());
 }
 
-void ca_build_faces(const DevGeom& G, const DevTables& Tb, double* fa, double* fb, hipStream_t s) {
-  PMX_CHECK(G.nx + 4 <= 65535, "k_ca_faces: grid.y limit");
-  hipLaunchKernelGGL(k_ca_faces, dim3((G.ny + 4 + 255) / 256, G.nx + 4), dim3(256), 0, s, G, Tb, fa, fb);
+void ca_build_faces(const DevGeom& G, const DevTables& Tb, double* fa, double* fb, int gh, hipStream_t s) {
+  PMX_CHECK(G.nx + 2 * gh <= 65535, "k_ca_faces: grid.y limit");
+  hipLaunchKernelGGL(k_ca_faces, dim3((G.ny + 4 + 255) / 256, G.nx + 2 * gh), dim3(256), 0, s, G, Tb, fa, fb, gh);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -963,7 +988,7 @@ void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, 
   const int ti_lo = upd ? t.ti_lo2 : t.ti_lo, ti_hi = upd ? t.ti_hi2 : t.ti_hi;
   const int tiles_i = upd ? t.tiles_i2 : t.tiles_i;
   const int nin = (ti_hi - ti_lo) * (t.tj_hi - t.tj_lo);
-  const CaFaces F{t.fa, t.fb};
+  const CaFaces F{t.fa, t.fb, t.gh};
   const CaPart P1{1, tiles_i, ti_lo, ti_hi, t.tj_lo, t.tj_hi}, P2{2, tiles_i, ti_lo, ti_hi, t.tj_lo, t.tj_hi},
       P0{0, tiles_i, 0, 0, 0, 0};
 #define PMX_CA_K(SS, U, MW, D, PT, PP, NB)                                                                          \
@@ -1004,16 +1029,27 @@ void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, 
 }
 
 void launch_ca_reduce(const double* partials, int n, int n2, int s_, double h, double wdiff, int nmax,
-                      bool check_only, PcgState* S, CaState* C, double* chunk, hipStream_t s, long long* progress) {
+                      bool check_only, PcgState* S, CaState* C, double* chunk, hipStream_t s, long long* progress,
+                      bool finish) {
   PMX_CHECK(nmax >= 1 && nmax <= s_, "s-step PCG: a block runs 1..s iterations");
   const int nb = std::max(1, std::min(kCaReduceMaxBlocks, std::max(n, n2) / 512));
-  const int co = check_only ? 1 : 0;
+  const int co = check_only ? 1 : 0, fi = finish ? 1 : 0;
   if (s_ == 2)
-    hipLaunchKernelGGL(k_ca_reduce<2>, dim3(nb), dim3(256), 0, s, partials, n, n2, h, wdiff, nmax, co, S, C, chunk,
+    hipLaunchKernelGGL(k_ca_reduce<2>, dim3(nb), dim3(256), 0, s, partials, n, n2, h, wdiff, nmax, co, fi, S, C, chunk,
                        progress);
   else
-    hipLaunchKernelGGL(k_ca_reduce<3>, dim3(nb), dim3(256), 0, s, partials, n, n2, h, wdiff, nmax, co, S, C, chunk,
+    hipLaunchKernelGGL(k_ca_reduce<3>, dim3(nb), dim3(256), 0, s, partials, n, n2, h, wdiff, nmax, co, fi, S, C, chunk,
                        progress);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_ca_finish(int s_, double h, double wdiff, int nmax, bool check_only, PcgState* S, CaState* C,
+                      hipStream_t s, long long* progress) {
+  const int co = check_only ? 1 : 0;
+  if (s_ == 2)
+    hipLaunchKernelGGL(k_ca_finish<2>, dim3(1), dim3(64), 0, s, h, wdiff, nmax, co, S, C, progress);
+  else
+    hipLaunchKernelGGL(k_ca_finish<3>, dim3(1), dim3(64), 0, s, h, wdiff, nmax, co, S, C, progress);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -216,8 +216,11 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   if (opt_.algo == -1) opt_.algo = choose_single_pass(spec, sd.grid, opt_, double(total_b), 1) ? 1 : 2;
   pcg1_ = opt_.algo == 1;
   ca_ = opt_.algo == 3;
-  PMX_CHECK(!ca_ || (opt.dtype == DType::kFp64 && !opt.exact && sd.grid.size() == 1),
-            "s-step PCG (algo 3) runs undecomposed fp64 grids with the fast arithmetic");
+  PMX_CHECK(!ca_ || (opt.dtype == DType::kFp64 && !opt.exact && sd.grid.Py == 1 && sd.nx >= opt.ca_s),
+            "s-step PCG (algo 3) runs fp64 grids with the fast arithmetic, undecomposed or as row strips of at "
+            "least s rows");
+  // ghost rows per side: 2 (the single-pass radius-2 halo); a decomposed s-step strip needs s = 3
+  gh_ = ca_ && sd.grid.size() > 1 ? 3 : 2;
   PMX_CHECK(!pcg1_ || (!opt.exact && opt.kernel == 1 && (sd.grid.size() == 1 || (sd.nx >= 2 && sd.ny >= 2))),
             "pcg1 needs the wave kernels, the fast arithmetic and a subdomain of at least 2 x 2 nodes");
 
@@ -228,8 +231,8 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
 
   // fields: element (li, lj), li = -1 .. nx+2, at base[li*pitch + lj]; base = alloc + pitch +
   // (align-1) so that every interior row starts 256-B aligned (lj = 1)
-  field_off_ = size_t(G.pitch) + align_elems - 1;
-  field_bytes_ = round_up((align_elems - 1 + size_t(sd.nx + 4) * G.pitch) * elem_, 256);
+  field_off_ = size_t(gh_ - 1) * size_t(G.pitch) + align_elems - 1;
+  field_bytes_ = round_up((align_elems - 1 + size_t(sd.nx + 2 * gh_) * G.pitch) * elem_, 256);
   {  // fail with a sizing message instead of a bare hipErrorOutOfMemory
     const size_t need = estimate_device_bytes(spec, sd, opt.dtype, pcg1_ || ca_) + (ca_ ? 2 * field_bytes_ : 0);
     PMX_CHECK(need <= free_b,
@@ -340,7 +343,8 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     HIP_CHECK(hipMalloc(&ca_faces_, 2 * field_bytes_));
     ca_tiles_.fa = reinterpret_cast<const double*>(ca_faces_ + field_off_ * elem_);
     ca_tiles_.fb = reinterpret_cast<const double*>(ca_faces_ + field_bytes_ + field_off_ * elem_);
-    ca_build_faces(G, tables_, const_cast<double*>(ca_tiles_.fa), const_cast<double*>(ca_tiles_.fb), nullptr);
+    ca_tiles_.gh = gh_;
+    ca_build_faces(G, tables_, const_cast<double*>(ca_tiles_.fa), const_cast<double*>(ca_tiles_.fb), gh_, nullptr);
     ca_tiles_.dma = opt_.ca_dma;
     if (!opt_.ca_split) ca_tiles_.split = 0;
     if (ca_tiles_.split && opt_.ca_frame_stream) {
@@ -371,7 +375,7 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   reduce_ws_ = partials_ + npart * 5;
   HIP_CHECK(hipMemset(reduce_ws_, 0, kReduceWsDoubles * sizeof(double)));
 
-  layout_ = comm_layout(sd, opt.dtype, pcg1_);
+  layout_ = comm_layout(sd, opt.dtype, pcg1_ || ca_);
   if (external_arena) {
     arena_ = reinterpret_cast<char*>(external_arena);
     own_arena_ = false;
@@ -664,6 +668,7 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
   if (ca_) {  // set 0: z^0 = D^-1 r^0 (in r's buffer), p^0 = z^0; block counter 0
     if constexpr (sizeof(T) == 8) {
       HIP_CHECK(hipMemsetAsync(ca_state_, 0, sizeof(CaState), s));
+      ca_blk_ = 0;
       launch_ca_init<double>(geom_, tables_, static_cast<double*>(field_base(1)), static_cast<double*>(field_base(2)), s);
       after_launch(s);
     }
@@ -691,25 +696,42 @@ void GpuSubdomainSolver::ca_sweep(hipStream_t s, bool upd) {
   after_launch(s);
 }
 
-void GpuSubdomainSolver::enqueue_ca_block(hipStream_t s, int n) {
-  PMX_CHECK(ca_ && elem_ == 8, "enqueue_ca_block: not an s-step solver");
+void GpuSubdomainSolver::enqueue_ca_pass(hipStream_t s, bool upd) {
+  PMX_CHECK(ca_ && elem_ == 8, "not an s-step solver");
+  ca_sweep(s, upd);
+}
+
+void GpuSubdomainSolver::enqueue_ca_reduce(hipStream_t s, int n, bool check_only, bool finish) {
+  PMX_CHECK(ca_ && elem_ == 8, "not an s-step solver");
   const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
-  ca_sweep(s, false);
-  launch_ca_reduce(partials_, ca_tiles_.ntiles(), ca_tiles_.ntiles2(), ca_tiles_.s, g_.h1h2, wdiff, n, false, state_, ca_state_,
-                   ca_chunk_, s, progress_dev_);
+  launch_ca_reduce(partials_, ca_tiles_.ntiles(), ca_tiles_.ntiles2(), ca_tiles_.s, g_.h1h2, wdiff,
+                   check_only ? 1 : n, check_only, state_, ca_state_, ca_chunk_, s, progress_dev_, finish);
   after_launch(s);
-  ca_sweep(s, true);
-  host_k_ += n;
+  if (!check_only) {  // a block the device applies (unless it stopped): the set its pass 2 writes
+    ++ca_blk_;
+    host_k_ += n;
+  }
+}
+
+void GpuSubdomainSolver::enqueue_ca_finish(hipStream_t s, int n, bool check_only) {
+  PMX_CHECK(ca_ && elem_ == 8, "not an s-step solver");
+  const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
+  launch_ca_finish(ca_tiles_.s, g_.h1h2, wdiff, check_only ? 1 : n, check_only, state_, ca_state_, s, progress_dev_);
+  after_launch(s);
+}
+
+void GpuSubdomainSolver::enqueue_ca_block(hipStream_t s, int n) {
+  PMX_CHECK(geom_.nb == 0, "enqueue_ca_block: undecomposed grids (the driver runs the steps otherwise)");
+  enqueue_ca_pass(s, false);
+  enqueue_ca_reduce(s, n, false, true);
+  enqueue_ca_pass(s, true);
 }
 
 void GpuSubdomainSolver::enqueue_ca_check(hipStream_t s) {
-  PMX_CHECK(ca_ && elem_ == 8, "enqueue_ca_check: not an s-step solver");
-  const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
-  launch_ca_reduce(partials_, ca_tiles_.ntiles(), ca_tiles_.ntiles2(), ca_tiles_.s, g_.h1h2, wdiff, 1, true, state_, ca_state_, ca_chunk_,
-                   s, progress_dev_);
-  after_launch(s);
+  PMX_CHECK(geom_.nb == 0, "enqueue_ca_check: undecomposed grids (the driver runs the steps otherwise)");
+  enqueue_ca_reduce(s, 1, true, true);
   // a stop inside the last block rewinds w (every workgroup returns at once otherwise)
-  ca_sweep(s, true);
+  enqueue_ca_pass(s, true);
 }
 
 template <typename T>
@@ -731,6 +753,26 @@ HaloMsgs GpuSubdomainSolver::halo_msgs() const {
     for (int slot = 0; slot < kHaloSlots; ++slot)
       if (layout_.active(slot))
         out.m[out.n++] = HaloMsg{slot, 0, layout_.peer[slot], layout_.edge_len[slot], send_dev(slot), recv_dev(slot)};
+    return out;
+  }
+  if (ca_) {
+    // s-step strips: the s owned edge rows of z and p of the set the next block reads (CaState::blk
+    // & 1, mirrored by ca_blk_) into the neighbour's s ghost rows, as ONE span per field: rows q,
+    // q+1 whole, row q+2's columns 0 .. ny+1 (columns <= 0 and >= ny+1 are Dirichlet on a strip)
+    const int s = ca_tiles_.s, set = int(ca_blk_ & 1);
+    char* fz = set ? r2_ + field_off_ * elem_ : static_cast<char*>(field_base(1));
+    char* fp = static_cast<char*>(field_base(set ? 3 : 2));
+    const int64_t P = geom_.pitch;
+    const int count = int((s - 1) * P + sd_.ny + 2);
+    for (int slot = 0; slot < 2; ++slot) {
+      if (layout_.peer[slot] < 0) continue;
+      const int64_t srow = slot == 0 ? 1 : sd_.nx - s + 1, rrow = slot == 0 ? 1 - s : sd_.nx + 1;
+      for (int f = 0; f < 2; ++f) {
+        char* base = f == 0 ? fz : fp;
+        out.m[out.n++] = HaloMsg{slot, f, layout_.peer[slot], count, base + srow * P * int64_t(elem_),
+                                 base + rrow * P * int64_t(elem_)};
+      }
+    }
     return out;
   }
   // sweep t reads r^{t-1} from (t & 1 ? r2 : r) and p^{t-1} from (t & 1 ? p0 : p1) (k_pcg1)
@@ -1115,16 +1157,17 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
   for (auto* s : local_)
     PMX_CHECK(s->single_pass() == single_pass_ && s->ca() == ca_,
               "local subdomains disagree on the iteration algorithm");
-  PMX_CHECK(!ca_ || (local_.size() == 1 && !any_nb && comm_->world_size() == 1),
-            "s-step PCG runs one undecomposed subdomain");
+
   overlap_ = any_nb && local_[0]->options().overlap;
   // Direct-row ghost exchange (row strips): no pack/unpack launches; PMX_DIRECT_ROWS=0 turns it off
   // (A/B).  Every local solver must qualify (they exchange with each other under LocalComm).
-  bool direct = single_pass_ && any_nb && comm_->direct_rows();
+  bool direct = (single_pass_ || ca_) && any_nb && comm_->direct_rows();
   for (auto* s : local_) direct &= s->can_direct_rows();
   if (const char* d = std::getenv("PMX_DIRECT_ROWS"); d && d[0] == '0') direct = false;
   direct_ = direct;
   for (auto* s : local_) s->set_direct_rows(direct_);
+  PMX_CHECK(!ca_ || !any_nb || direct_,
+            "s-step PCG on a decomposed grid needs the direct-row exchange (row strips, RCCL / local / loopback)");
   // One hardware queue per process (GPU_MAX_HW_QUEUES=1): every stream lands on it, so forking the
   // halo / frame work onto side streams cannot overlap anything -- and ROCm 7.2 segfaults inside
   // hipGraphLaunch on a captured graph with forked branches in that configuration (traced with
@@ -1214,8 +1257,12 @@ void PcgDriver::synchronize() {
 
 void PcgDriver::init() {
   TraceRange tr("pmx:init");
-  if (ca_) {  // fields, state and set 0 of the first block
-    local_[0]->enqueue_init(streams_[0]);
+  if (ca_) {  // fields, state and set 0 of the first block (and its ghost rows)
+    for (size_t i = 0; i < local_.size(); ++i) {
+      HIP_CHECK(hipSetDevice(local_[i]->device()));
+      local_[i]->enqueue_init(streams_[i]);
+    }
+    if (any_nb_) comm_->halo(local_, streams_);
     synchronize();
     return;
   }
@@ -1348,14 +1395,41 @@ void PcgDriver::enqueue_ca(int64_t n) {
   const int s = local_[0]->ca_s();
   HIP_CHECK(hipSetDevice(local_[0]->device()));
   if (n <= 0) return;
+  if (!any_nb_ && local_.size() == 1 && comm_->world_size() == 1) {
+    while (n > 0) {
+      const int m = int(std::min<int64_t>(s, n));
+      local_[0]->enqueue_ca_block(streams_[0], m);
+      n -= m;
+    }
+    // the last block's stop test (and its rewind): the state is exact at every batch boundary
+    local_[0]->enqueue_ca_check(streams_[0]);
+    return;
+  }
+  // decomposed: every rank's sums are all-reduced between the reduction and the scalars, and the s
+  // ghost rows of the new (z, p) set are exchanged after pass 2 (direct rows, one span per field)
+  auto each = [&](auto&& f) {
+    for (size_t i = 0; i < local_.size(); ++i) {
+      HIP_CHECK(hipSetDevice(local_[i]->device()));
+      f(local_[i], streams_[i]);
+    }
+  };
   while (n > 0) {
     const int m = int(std::min<int64_t>(s, n));
-    local_[0]->enqueue_ca_block(streams_[0], m);
+    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, false); });
+    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_reduce(st, m, false, false); });
+    comm_->allreduce(local_, 3, streams_);
+    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_finish(st, m, false); });
+    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, true); });
+    if (any_nb_) comm_->halo(local_, streams_);
     n -= m;
   }
-  // the last block's stop test (and its rewind): the state is exact at every batch boundary
-  local_[0]->enqueue_ca_check(streams_[0]);
+  each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_reduce(st, 1, true, false); });
+  comm_->allreduce(local_, 3, streams_);
+  each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_finish(st, 1, true); });
+  each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, true); });  // rewind
 }
+
+int PcgDriver::ca_phase() const { return any_nb_ ? int(local_[0]->ca_blocks() & 1) : 0; }
 
 void PcgDriver::enqueue_one_iteration() {
   if (ca_) {
@@ -1492,8 +1566,11 @@ hipGraphExec_t PcgDriver::build_graph(int phase, int len) {
     (void)hipGetLastError();
     return nullptr;
   }
-  std::vector<long long> k0;
-  for (auto* s : local_) k0.push_back(s->host_k());
+  std::vector<long long> k0, b0;
+  for (auto* s : local_) {
+    k0.push_back(s->host_k());
+    b0.push_back(s->ca_blocks());
+  }
   PMX_CHECK(!halo_pending_, "graph capture with an unjoined ghost exchange");
   PMX_GDBG("capture begun");
   try {
@@ -1502,14 +1579,20 @@ hipGraphExec_t PcgDriver::build_graph(int phase, int len) {
     join_halo();  // a captured batch is self-contained: every forked stream rejoins
   } catch (...) {  // e.g. an aborted communicator: end the capture so the stream stays usable
     halo_pending_ = false;
-    for (size_t i = 0; i < local_.size(); ++i) local_[i]->set_host_k(k0[i]);
+    for (size_t i = 0; i < local_.size(); ++i) {
+      local_[i]->set_host_k(k0[i]);
+      local_[i]->set_ca_blocks(b0[i]);
+    }
     hipGraph_t dead = nullptr;
     (void)hipStreamEndCapture(streams_[0], &dead);
     if (dead) (void)hipGraphDestroy(dead);
     (void)hipGetLastError();
     throw;
   }
-  for (size_t i = 0; i < local_.size(); ++i) local_[i]->set_host_k(k0[i]);
+  for (size_t i = 0; i < local_.size(); ++i) {
+    local_[i]->set_host_k(k0[i]);
+    local_[i]->set_ca_blocks(b0[i]);
+  }
   PMX_GDBG("enqueued; ending capture");
   if (hipStreamEndCapture(streams_[0], &g) != hipSuccess || !g) {
     (void)hipGetLastError();
@@ -1555,23 +1638,33 @@ void PcgDriver::note_graph(int len) {
 bool PcgDriver::prepare(int64_t n) {
   TraceRange tr("pmx:prepare");
   const int cyc = graph_period();
-  std::vector<long long> k0;
-  for (auto* s : local_) k0.push_back(s->host_k());
+  std::vector<long long> k0, b0;
+  for (auto* s : local_) {
+    k0.push_back(s->host_k());
+    b0.push_back(s->ca_blocks());
+  }
   bool ok = graph_batch_ > 0 && !graph_failed_;
   const int gb = ca_ ? ca_batch() : graph_batch_;
-  int64_t done = 0;
+  int64_t done = 0, blocks = 0;  // s-step: blocks enqueued by the batches before `done`
   auto at = [&](int64_t off) {  // host counters as they will be `off` iterations from now
-    for (size_t i = 0; i < local_.size(); ++i) local_[i]->set_host_k(k0[i] + off);
+    for (size_t i = 0; i < local_.size(); ++i) {
+      local_[i]->set_host_k(k0[i] + off);
+      local_[i]->set_ca_blocks(b0[i] + blocks);
+    }
   };
+  auto phase = [&]() { return ca_ ? ca_phase() : int((k0[0] + done) % cyc); };
+  const int s = ca_ ? local_[0]->ca_s() : 1;
   while (ok && done + gb <= n) {
     at(done);
-    ok = graph_for(int((k0[0] + done) % cyc), gb) != nullptr;
+    ok = graph_for(phase(), gb) != nullptr;
     done += gb;
+    blocks += (gb + s - 1) / s;
   }
   if (ok && done < n) {
     at(done);
-    ok = graph_for(int((k0[0] + done) % cyc), int(n - done)) != nullptr;
+    ok = graph_for(phase(), int(n - done)) != nullptr;
   }
+  blocks = 0;
   at(0);
   return ok;
 }
@@ -1591,12 +1684,16 @@ void PcgDriver::enqueue_iterations(int64_t n) {
   const int gb = ca_ ? ca_batch() : graph_batch_;
   while (done < n) {
     const int len = int(std::min<int64_t>(gb, n - done));
-    hipGraphExec_t e = len > 0 ? graph_for(int(local_[0]->host_k() % cyc), len) : nullptr;
+    hipGraphExec_t e = len > 0 ? graph_for(ca_ ? ca_phase() : int(local_[0]->host_k() % cyc), len) : nullptr;
     if (!e) break;
     PMX_GDBG("launch len %d", len);
     HIP_CHECK(hipGraphLaunch(e, streams_[0]));
     PMX_GDBG("launched");
     advance_host_k(len);
+    if (ca_) {
+      const int s = local_[0]->ca_s();
+      for (auto* g : local_) g->set_ca_blocks(g->ca_blocks() + (len + s - 1) / s);
+    }
     note_graph(len);
     done += len;
   }

@@ -102,6 +102,7 @@ struct alignas(64) CaState {
   double pa[kCaMaxS][kCaMaxNb];  // a_j (p_{k+j} = Y a_j) of the block's iterations: pass 2's norms
   double pc[kCaMaxS][kCaMaxNb];  // c_{j+1} of the pending block (the rewind target)
   double alpha[kCaMaxS];         // alpha_j of the pending block
+  double red[7 * kCaMaxS];       // decomposed grids: this rank's Gram + norm sums, all-reduced before the finish
   long long blk;          // blocks applied: pass 1 reads (p, z) from set blk & 1, pass 2 writes set (blk & 1)
   long long pend_k;       // iterations done before the pending block
   long long after_iters;  // iteration count reported with after_status

@@ -234,7 +234,7 @@ class GpuSubdomainSolver {
   // buffers (a row span, padding included, is contiguous).  The driver turns it on when its
   // communicator moves arbitrary device spans (Comm::direct_rows).
   bool can_direct_rows() const {
-    return pcg1_ && (geom_.nb & ~(kNbXlo | kNbXhi)) == 0 && sd_.nx >= 2;
+    return (pcg1_ || ca_) && (geom_.nb & ~(kNbXlo | kNbXhi)) == 0 && sd_.nx >= (ca_ ? ca_tiles_.s : 2);
   }
   void set_direct_rows(bool on);
   bool direct_rows() const { return direct_rows_; }
@@ -267,9 +267,13 @@ class GpuSubdomainSolver {
   double* red_a_dev() const { return state_->red_a; }
   double* red_b_dev() const { return state_->red_b; }
   double* red_c_dev() const { return state_->red_c; }
-  // all-reduce buffer `which` (0: red_a, 1 value; 1: red_b, 2; 2: red_c, 5) and its length
-  double* reduce_buf(int which) const { return which == 0 ? red_a_dev() : which == 1 ? red_b_dev() : red_c_dev(); }
-  static int reduce_len(int which) { return which == 0 ? 1 : which == 1 ? 2 : 5; }
+  // all-reduce buffer `which` (0: red_a, 1 value; 1: red_b, 2; 2: red_c, 5; 3: the s-step sums,
+  // CaState::red, 21 -- nullptr without the s-step solver) and its length
+  double* reduce_buf(int which) const {
+    return which == 0 ? red_a_dev() : which == 1 ? red_b_dev() : which == 2 ? red_c_dev()
+                                                    : (ca_state_ ? ca_state_->red : nullptr);
+  }
+  static int reduce_len(int which) { return which == 0 ? 1 : which == 1 ? 2 : which == 2 ? 5 : 7 * kCaMaxS; }
   void* send_dev(int side) const { return arena_ + layout_.send_off[side]; }
   void* recv_dev(int side) const { return arena_ + layout_.recv_off[side]; }
   const CommLayout& layout() const { return layout_; }
@@ -295,6 +299,14 @@ class GpuSubdomainSolver {
   int ca_s() const { return ca_ ? ca_tiles_.s : 0; }
   const CaTiles& ca_tiles() const { return ca_tiles_; }
   void enqueue_ca_block(hipStream_t s, int n);
+  // the same block in steps, for decomposed grids (the driver all-reduces CaState::red between
+  // reduce and finish, and exchanges the s ghost rows of the new (z, p) set after pass 2)
+  void enqueue_ca_pass(hipStream_t s, bool upd);
+  void enqueue_ca_reduce(hipStream_t s, int n, bool check_only, bool finish);
+  void enqueue_ca_finish(hipStream_t s, int n, bool check_only);
+  // host mirror of CaState::blk (blocks enqueued): the (z, p) set the next exchange sends
+  long long ca_blocks() const { return ca_blk_; }
+  void set_ca_blocks(long long b) { ca_blk_ = b; }
   // the pending stop test of the last block, and pass 2 rewinding w if it stopped inside that block
   void enqueue_ca_check(hipStream_t s);
   // pcg1: host mirror of the device iteration counter S->it -- the index of the next sweep this
@@ -346,6 +358,8 @@ class GpuSubdomainSolver {
   void ca_sweep(hipStream_t s, bool upd);
   CaState* ca_state_ = nullptr;
   double* ca_chunk_ = nullptr;  // its reduction's chunk sums
+  long long ca_blk_ = 0;        // blocks enqueued since init (CaState::blk's host mirror)
+  int gh_ = 2;                  // ghost rows of the fields on each side
   long long host_k_ = 0;
   bool direct_rows_ = false;
   long long halo_target_ = 0;
@@ -522,6 +536,7 @@ class PcgDriver {
   // s-step PCG: n iterations as blocks of ca_s() (the last one shorter), graphs of ca_batch()
   void enqueue_ca(int64_t n);
   int ca_batch() const;
+  int ca_phase() const;  // captured s-step batches on decomposed grids depend on the (z, p) set parity
   // pack -> comm -> unpack, filling the inputs of sweep `target` (direct rows: comm only)
   void halo_exchange_pcg1(std::vector<hipStream_t>& streams, long long target);
   void set_halo_target(long long k);

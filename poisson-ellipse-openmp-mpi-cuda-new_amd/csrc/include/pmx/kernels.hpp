@@ -145,6 +145,7 @@ struct CaTiles {
   unsigned* tbl = nullptr;  // row classes (ca_build_classes), tiles_j * cwords words, owned by the caller
   const double* fa = nullptr;  // face coefficients a, b at every local node (ca_build_faces), pitched as
   const double* fb = nullptr;  // the fields, local (0, 0); read on the rows the ellipse cuts
+  int gh = 2;                  // ghost rows of the fields on each side: 2, or 3 = s on a decomposed strip
   // interior rectangles of the two tilings (every tile "fast": no Dirichlet node or partial width in
   // reach): [ti_lo, ti_hi) x [tj_lo, tj_hi) for pass 1, [ti_lo2, ti_hi2) x (same columns) for pass 2
   int ti_lo = 0, ti_hi = 0, tj_lo = 0, tj_hi = 0, ti_lo2 = 0, ti_hi2 = 0;
@@ -159,7 +160,7 @@ CaTiles make_ca_tiles(const DevGeom& G, int s, int rows, int rows2 = 0);
 int ca_nq(int s);  // partials per tile (pass 1's Gram products + pass 2's norms)
 void ca_build_classes(const DevGeom& G, const DevTables& Tb, const CaTiles& t, unsigned* tbl, hipStream_t s);
 // fa / fb: local (0, 0) of two field-sized arrays (rows -1 .. nx+2 allocated)
-void ca_build_faces(const DevGeom& G, const DevTables& Tb, double* fa, double* fb, hipStream_t s);
+void ca_build_faces(const DevGeom& G, const DevTables& Tb, double* fa, double* fb, int gh, hipStream_t s);
 // z = D^-1 r in place, p = z (the first block's set 0)
 template <typename T>
 void launch_ca_init(const DevGeom& G, const DevTables& Tb, T* z, T* p, hipStream_t s);
@@ -173,9 +174,13 @@ constexpr int kCaReduceMaxBlocks = 256;
 // check_only: the pending stop test alone (after the last block of a batch; pass 2 then rewinds w if
 // the test stopped inside that block)
 // n / n2: pass 1 / pass 2 tiles (the partials of each)
+// finish = false (decomposed grids): the rank's sums go to CaState::red for the all-reduce, and
+// launch_ca_finish runs the scalars on the reduced sums afterwards
 void launch_ca_reduce(const double* partials, int n, int n2, int s_, double h, double wdiff, int nmax,
                       bool check_only, PcgState* S, CaState* C, double* chunk, hipStream_t s,
-                      long long* progress = nullptr);
+                      long long* progress = nullptr, bool finish = true);
+void launch_ca_finish(int s_, double h, double wdiff, int nmax, bool check_only, PcgState* S, CaState* C,
+                      hipStream_t s, long long* progress = nullptr);
 
 // pcg1 ghost exchange: pack (unpack=false) the radius-2 edges of the buffers sweep `target` reads
 // (parity of target) into H.send, or unpack H.recv into their ghost cells.

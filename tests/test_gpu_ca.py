@@ -98,8 +98,36 @@ def test_ca_matches_cpu_oracle(pkg):
     assert np.abs(w - ref.w).max() <= 1e-9 * np.abs(ref.w).max()
 
 
-def test_ca_rejects_decomposed_and_fp32(pkg):
+def test_ca_rejects_blocks_thin_strips_and_fp32(pkg):
     with pytest.raises(RuntimeError, match="s-step"):
-        _sess(pkg, 400, 600, "ca", 3, ranks=2)
+        _sess(pkg, 400, 600, "ca", 3, ranks=2, split="cols")  # column strips: no direct-row exchange
+    with pytest.raises(RuntimeError, match="s-step"):
+        _sess(pkg, 20, 600, "ca", 3, ranks=8, split="rows")  # strips of 2 rows < s
     with pytest.raises(RuntimeError, match="s-step"):
         _sess(pkg, 400, 600, "ca", 3, dtype="fp32")
+
+
+@pytest.mark.parametrize("ranks", [2, 3, 4])
+@pytest.mark.parametrize("graph_batch", [0, 32])
+def test_ca_row_strips(pkg, ranks, graph_batch):
+    """Row strips on one GPU (LocalComm): the s = 3 ghost rows of z and p exchanged after every pass 2,
+    the 21 sums all-reduced before the block's scalars.  The reference count and the undecomposed
+    solution to rounding (the strips sum their partials in another order)."""
+    one = _sess(pkg, 800, 1200, "ca", 3)
+    r1 = one.solve(1)
+    strips = _sess(pkg, 800, 1200, "ca", 3, ranks=ranks, split="rows", graph_batch=graph_batch)
+    assert strips.grid == (ranks, 1)
+    r = strips.solve(1)
+    assert r["status"] == r1["status"] == "converged"
+    assert r["iters"] == r1["iters"] == 989
+    w, w1 = strips.gather_local_w(), one.gather_local_w()
+    assert np.abs(w - w1).max() <= 1e-10 * np.abs(w1).max()
+
+
+def test_ca_row_strips_odd_sizes_and_max_iter(pkg):
+    """uneven strips (97x130 over 5 ranks) and a max_iter stop inside a block"""
+    for mi in (None, 40):
+        p = lambda: pkg.PoissonEllipse(M=97, N=130, max_iter=mi)  # noqa: E731
+        a = _sess(pkg, 0, 0, "ca", 3, problem=p(), ranks=5, split="rows").solve(1)
+        b = _sess(pkg, 0, 0, "pcg1", problem=p()).solve(1)
+        assert a["status"] == b["status"] and a["iters"] == b["iters"]
