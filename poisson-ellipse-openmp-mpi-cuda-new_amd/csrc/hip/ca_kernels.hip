@@ -978,7 +978,7 @@ template <typename T>
 void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, T* p0, T* p1, double* partials,
                      const PcgState* S, const CaState* C, const CaTiles& t, bool upd, hipStream_t s,
                      hipStream_t sframe) {
-  PMX_CHECK(G.nb == 0, "s-step PCG runs undecomposed grids");
+  PMX_CHECK((G.nb & ~(kNbXlo | kNbXhi)) == 0, "s-step PCG runs undecomposed grids or row strips");
   if (!sframe) sframe = s;
   PMX_CHECK(t.tbl != nullptr && t.fa != nullptr && t.fb != nullptr, "s-step PCG: row-class / face tables missing");
   PMX_CHECK(sizeof(T) == 8 || !t.dma, "s-step PCG: LDS-DMA rows need fp64");

@@ -121,6 +121,7 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_CA_DMA", o.ca_dma);
   env_int("PMX_CA_SPLIT", o.ca_split);
   env_int("PMX_CA_FRAME_STREAM", o.ca_frame_stream);
+  env_int("PMX_CA_DIRICHLET", o.ca_dirichlet);
   PMX_CHECK(o.ca_split == 0 || o.ca_split == 1, "s-step PCG: ca_split must be 0 or 1");
   env_int("PMX_CA_WAVES_GRAM", o.ca_waves_gram);
   env_int("PMX_CA_WAVES_UPD", o.ca_waves_upd);
@@ -256,6 +257,17 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
 
   // 1D face tables
   tables_ = upload_tables(spec, &tables_buf_);
+  ca_geom_ = geom_;
+  ca_tables_ = tables_;
+  if (ca_ && opt_.ca_dirichlet) {  // see ca_tables_
+    const int o = geom_.gi0;
+    ca_geom_.nb = 0;
+    ca_geom_.gi0 = 0;
+    ca_geom_.M = sd.nx + 1;
+    for (const double** t : {&ca_tables_.rv, &ca_tables_.xlo, &ca_tables_.xhi, &ca_tables_.x}) *t += o;
+    ca_tables_.acls += 4 * o;
+  }
+  ca_gh_ = ca_geom_.nb ? gh_ : 2;
 
   PMX_CHECK(opt.kernel == 1, "kernel must be 1 (wave tiles); the round-1 LDS-ring kernels are retired (bench/RETIRED.md)");
   // tile shapes per kernel (profiles/tile_counters_16384_fp64.md: pcg_a is fastest with 4
@@ -338,13 +350,13 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
 
   if (ca_) {
     r2_ = field_raw(4);  // the second z buffer
-    ca_tiles_ = make_ca_tiles(G, opt_.ca_s, opt_.ca_rows, opt_.ca_rows2);
+    ca_tiles_ = make_ca_tiles(ca_geom_, opt_.ca_s, opt_.ca_rows, opt_.ca_rows2);
     // the face coefficients of every node, read on the rows the ellipse cuts (2 more field-sized arrays)
     HIP_CHECK(hipMalloc(&ca_faces_, 2 * field_bytes_));
     ca_tiles_.fa = reinterpret_cast<const double*>(ca_faces_ + field_off_ * elem_);
     ca_tiles_.fb = reinterpret_cast<const double*>(ca_faces_ + field_bytes_ + field_off_ * elem_);
-    ca_tiles_.gh = gh_;
-    ca_build_faces(G, tables_, const_cast<double*>(ca_tiles_.fa), const_cast<double*>(ca_tiles_.fb), gh_, nullptr);
+    ca_tiles_.gh = ca_gh_;
+    ca_build_faces(ca_geom_, ca_tables_, const_cast<double*>(ca_tiles_.fa), const_cast<double*>(ca_tiles_.fb), ca_gh_, nullptr);
     ca_tiles_.dma = opt_.ca_dma;
     if (!opt_.ca_split) ca_tiles_.split = 0;
     if (ca_tiles_.split && opt_.ca_frame_stream) {
@@ -356,7 +368,7 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     ca_tiles_.waves_upd = opt_.ca_waves_upd;
     HIP_CHECK(hipMalloc(&ca_tbl_, size_t(ca_tiles_.tiles_j) * ca_tiles_.cwords * sizeof(unsigned)));
     ca_tiles_.tbl = ca_tbl_;
-    ca_build_classes(G, tables_, ca_tiles_, ca_tbl_, nullptr);
+    ca_build_classes(ca_geom_, ca_tables_, ca_tiles_, ca_tbl_, nullptr);
     HIP_CHECK(hipStreamSynchronize(nullptr));
     HIP_CHECK(hipMalloc(&ca_state_, sizeof(CaState)));
     HIP_CHECK(hipMemset(ca_state_, 0, sizeof(CaState)));
@@ -415,10 +427,15 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
 // (profiles/r4/placement/).  No ghost exchange (timing only); the driver's init() resets everything.
 void GpuSubdomainSolver::probe_iterations(hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   enqueue_init(s);
-  if (ca_) {  // s-step: one untimed block, then two (2 s iterations)
-    enqueue_ca_block(s, ca_tiles_.s);
+  if (ca_) {  // s-step: one untimed block, then two (2 s iterations); strips: this rank's sums only
+    const auto block = [&] {
+      enqueue_ca_pass(s, false);
+      enqueue_ca_reduce(s, ca_tiles_.s, false, true);
+      enqueue_ca_pass(s, true);
+    };
+    block();
     HIP_CHECK(hipEventRecord(e0, s));
-    for (int k = 0; k < 2; ++k) enqueue_ca_block(s, ca_tiles_.s);
+    for (int k = 0; k < 2; ++k) block();
     HIP_CHECK(hipEventRecord(e1, s));
     return;
   }
@@ -669,7 +686,7 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
     if constexpr (sizeof(T) == 8) {
       HIP_CHECK(hipMemsetAsync(ca_state_, 0, sizeof(CaState), s));
       ca_blk_ = 0;
-      launch_ca_init<double>(geom_, tables_, static_cast<double*>(field_base(1)), static_cast<double*>(field_base(2)), s);
+      launch_ca_init<double>(ca_geom_, ca_tables_, static_cast<double*>(field_base(1)), static_cast<double*>(field_base(2)), s);
       after_launch(s);
     }
   }
@@ -686,12 +703,12 @@ void GpuSubdomainSolver::ca_sweep(hipStream_t s, bool upd) {
   if (ca_side_) {
     HIP_CHECK(hipEventRecord(ca_ev_fork_, s));
     HIP_CHECK(hipStreamWaitEvent(ca_side_, ca_ev_fork_, 0));
-    launch_ca_sweep<double>(geom_, tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, upd, s,
+    launch_ca_sweep<double>(ca_geom_, ca_tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, upd, s,
                             ca_side_);
     HIP_CHECK(hipEventRecord(ca_ev_join_, ca_side_));
     HIP_CHECK(hipStreamWaitEvent(s, ca_ev_join_, 0));
   } else {
-    launch_ca_sweep<double>(geom_, tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, upd, s);
+    launch_ca_sweep<double>(ca_geom_, ca_tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, upd, s);
   }
   after_launch(s);
 }

@@ -53,6 +53,7 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
   for (size_t i = 0; i < cfg_.ranks.size(); ++i) {
     GpuOptions o = base;
     o.device = cfg_.devices[i];
+    if (cfg_.comm == CommKind::kLoopback) o.ca_dirichlet = 1;  // see GpuOptions::ca_dirichlet
     const Subdomain sd = decompose_2d(cfg_.spec.M, cfg_.spec.N, pg_, cfg_.ranks[i]);
     solvers_.push_back(std::make_unique<GpuSubdomainSolver>(cfg_.spec, sd, o));
   }

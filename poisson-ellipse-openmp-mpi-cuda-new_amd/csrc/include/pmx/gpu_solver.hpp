@@ -87,6 +87,11 @@ struct GpuOptions {
   int ca_split = 1;
   // ... the frame kernel on a side stream, overlapping the interior (1), or after it (0).  PMX_CA_FRAME_STREAM.
   int ca_frame_stream = 1;
+  // s-step kernels see the subdomain's ghost rows as a Dirichlet boundary (nb = 0) while the driver
+  // keeps the decomposed schedule: the loopback rehearsal, whose zero ghosts would otherwise break
+  // the basis recurrence (its redundant ghost-row levels need the neighbour's real rows).  Set by the
+  // Session for comm="loopback"; numerically a different (local) problem, timing-equivalent.
+  int ca_dirichlet = 0;
   // pcg1 tile shape (rows1 = 0: auto).  VEC=2 x 1 wave/workgroup won the 16384^2 sweeps
   // (bench/gpu_pcg1_sweep.sh; VEC=4 needs 256 VGPRs and is 35% slower).
   int vec1 = 2, waves1 = 1, rows1 = 0;
@@ -360,6 +365,12 @@ class GpuSubdomainSolver {
   double* ca_chunk_ = nullptr;  // its reduction's chunk sums
   long long ca_blk_ = 0;        // blocks enqueued since init (CaState::blk's host mirror)
   int gh_ = 2;                  // ghost rows of the fields on each side
+  // the s-step kernels' geometry and face tables: geom_ / tables_, or under ca_dirichlet a standalone
+  // grid of the subdomain's rows (gi0 = 0, M = nx + 1, tables shifted by gi0), whose rows 0 and nx + 1
+  // are boundary rows (the kernels tell boundary from interior rows by the global row index)
+  DevGeom ca_geom_{};
+  DevTables ca_tables_{};
+  int ca_gh_ = 2;               // ghost rows the s-step kernels compute on
   long long host_k_ = 0;
   bool direct_rows_ = false;
   long long halo_target_ = 0;
