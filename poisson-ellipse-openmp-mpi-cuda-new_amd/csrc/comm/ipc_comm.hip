@@ -64,8 +64,9 @@ struct alignas(256) IpcBlock {
   unsigned long long ack[kHaloSlots];  // exchanges pulled from the neighbour across slot s
   int err;                             // 1 = a wait timed out
   int pad;
-  double pub[2][8];                    // published local sums, by all-reduce parity
+  double pub[2][24];                   // published local sums, by all-reduce parity
 };
+constexpr int kIpcMaxReduce = 24;
 
 constexpr int kMaxIpcRanks = 64;
 
@@ -154,6 +155,29 @@ __global__ void __launch_bounds__(256) k_ipc_pull(IpcPeers P, int me, PcgState* 
     dst[i] = __builtin_nontemporal_load(src + i);
 }
 
+// s-step strips (direct rows): the spans of one exchange, read straight from the neighbours' fields
+struct IpcSpans {
+  const IpcBlock* nbr[4];
+  const void* src[4];
+  void* dst[4];
+  int len[4];
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) k_ipc_pull_spans(IpcPeers P, IpcSpans S4, int me, PcgState* S,
+                                                        long long timeout) {
+  const int q = blockIdx.y;
+  __shared__ int ok;
+  IpcBlock* own = P.all[me];
+  if (threadIdx.x == 0) ok = wait_ge(&S4.nbr[q]->halo_flag, own->halo_count, timeout, own, S) ? 1 : 0;
+  __syncthreads();
+  if (!ok) return;
+  const T* src = static_cast<const T*>(S4.src[q]);
+  T* dst = static_cast<T*>(S4.dst[q]);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < S4.len[q]; i += gridDim.x * 256)
+    dst[i] = __builtin_nontemporal_load(src + i);
+}
+
 __global__ void k_ipc_ack(IpcPeers P, int me) {
   if (threadIdx.x != 0) return;
   IpcBlock* own = P.all[me];
@@ -203,6 +227,18 @@ class IpcComm final : public Comm {
     std::string out(reinterpret_cast<const char*>(&dev), sizeof(dev));
     out += handle_bytes(reinterpret_cast<void*>(local_->arena_ptr()));
     out += handle_bytes(block_);
+    if (ca_) {  // s-step strips: the fields allocation and where each (set, slot, field) span starts in it
+      out += handle_bytes(local_->fields_alloc());
+      long long off[2][2][2];
+      std::memset(off, 0xff, sizeof(off));
+      for (int set = 0; set < 2; ++set) {
+        const HaloMsgs ms = local_->ca_halo_msgs(set);
+        for (int q = 0; q < ms.n; ++q)
+          off[set][ms.m[q].slot][ms.m[q].field] =
+              static_cast<long long>(static_cast<char*>(ms.m[q].send) - local_->fields_alloc());
+      }
+      out += std::string(reinterpret_cast<const char*>(off), sizeof(off));
+    }
     return out;
   }
 
@@ -213,9 +249,10 @@ class IpcComm final : public Comm {
     const size_t hs = sizeof(hipIpcMemHandle_t);
     std::vector<char*> arenas(size_t(world_), nullptr);
     std::memset(&P_, 0, sizeof(P_));
+    const CommLayout& L0 = local_->layout();
     for (int r = 0; r < world_; ++r) {
       const std::string& e = peers[size_t(r)];
-      PMX_CHECK(e.size() == sizeof(int) + 2 * hs, "bad IPC export of rank " << r);
+      PMX_CHECK(e.size() == sizeof(int) + 2 * hs + (ca_ ? hs + sizeof(ca_off_[0]) : 0), "bad IPC export of rank " << r);
       if (r == me) {
         arenas[size_t(r)] = reinterpret_cast<char*>(local_->arena_ptr());
         P_.all[r] = block_;
@@ -232,6 +269,14 @@ class IpcComm final : public Comm {
       opened_.push_back(arenas[size_t(r)]);
       P_.all[r] = static_cast<IpcBlock*>(open_handle(e.substr(sizeof(int) + hs, hs)));
       opened_.push_back(P_.all[r]);
+      if (ca_) {
+        for (int s = 0; s < 2; ++s) {
+          if (L0.peer[s] != r) continue;
+          ca_fields_[s] = static_cast<char*>(open_handle(e.substr(sizeof(int) + 2 * hs, hs)));
+          opened_.push_back(ca_fields_[s]);
+          std::memcpy(ca_off_[s], e.data() + sizeof(int) + 3 * hs, sizeof(ca_off_[s]));
+        }
+      }
     }
     const CommLayout& L = local_->layout();
     for (int s = 0; s < kHaloSlots; ++s) {
@@ -242,7 +287,7 @@ class IpcComm final : public Comm {
       // the same number of elements at its own send offset, which a rank computes locally from the
       // neighbour's subdomain (comm_layout is a pure function of it)
       const Subdomain nsd = decompose_2d(local_->spec().M, local_->spec().N, local_->sd().grid, q);
-      const CommLayout NL = GpuSubdomainSolver::comm_layout(nsd, local_->options().dtype, local_->single_pass());
+      const CommLayout NL = GpuSubdomainSolver::comm_layout(nsd, local_->options().dtype, local_->single_pass() || local_->ca());
       const int os = opposite_slot(s);
       PMX_CHECK(NL.edge_len[os] == L.edge_len[s], "IpcComm: slot lengths disagree with rank " << q);
       P_.nbr[s] = P_.all[q];
@@ -257,6 +302,7 @@ class IpcComm final : public Comm {
   void allreduce(std::vector<GpuSubdomainSolver*>& local, int which, std::vector<hipStream_t>& streams) override {
     require(local);
     if (world_ == 1) return;
+    PMX_CHECK(GpuSubdomainSolver::reduce_len(which) <= kIpcMaxReduce, "IpcComm: all-reduce longer than IpcBlock::pub");
     hipLaunchKernelGGL(k_ipc_allreduce, dim3(1), dim3(64), 0, streams[0], P_, world_, local_->sd().rank,
                        local_->reduce_buf(which), GpuSubdomainSolver::reduce_len(which), local_->state_dev(),
                        timeout_);
@@ -274,6 +320,31 @@ class IpcComm final : public Comm {
     if (maxlen_ == 0) return;
     const int me = local_->sd().rank;
     hipLaunchKernelGGL(k_ipc_post, dim3(1), dim3(64), 0, streams[0], P_, me);
+    if (ca_) {  // the s rows of z and p of the current set, from the neighbours' fields into our ghost rows
+      const HaloMsgs ms = local_->halo_msgs();
+      const int set = local_->ca_halo_set();
+      IpcSpans sp{};
+      int n = 0, maxc = 0;
+      for (int q = 0; q < ms.n; ++q) {
+        const HaloMsg& m = ms.m[q];
+        const long long off = ca_off_[m.slot][set][opposite_slot(m.slot)][m.field];
+        PMX_CHECK(n < 4 && off >= 0 && ca_fields_[m.slot] && P_.nbr[m.slot], "IpcComm: no peer span for slot " << m.slot);
+        sp.nbr[n] = P_.nbr[m.slot];
+        sp.src[n] = ca_fields_[m.slot] + off;
+        sp.dst[n] = m.recv;
+        sp.len[n] = m.count;
+        maxc = std::max(maxc, m.count);
+        ++n;
+      }
+      if (n) {
+        const int bx = std::max(1, std::min(64, (maxc + 255) / 256));
+        hipLaunchKernelGGL(k_ipc_pull_spans<double>, dim3(bx, n), dim3(256), 0, streams[0], P_, sp, me,
+                           local_->state_dev(), timeout_);
+      }
+      hipLaunchKernelGGL(k_ipc_ack, dim3(1), dim3(64), 0, streams[0], P_, me);
+      HIP_CHECK(hipGetLastError());
+      return;
+    }
     const int bx = std::max(1, std::min(64, (maxlen_ + 255) / 256));
     if (local_->layout().elem == 8)
       hipLaunchKernelGGL(k_ipc_pull<double>, dim3(bx, kHaloSlots), dim3(256), 0, streams[0], P_, me,
@@ -291,6 +362,7 @@ class IpcComm final : public Comm {
                         "was stopped");
   }
   bool prefers_split() const override { return true; }
+  bool direct_rows() const override { return ca_; }  // s-step strips read the neighbours' fields in place
   std::string name() const override { return "ipc"; }
   int world_size() const override { return world_; }
 
@@ -307,6 +379,10 @@ class IpcComm final : public Comm {
   int maxlen_ = 0;
   long long timeout_ = 0;
   bool attached_ = false;
+  // s-step strips: each x neighbour's fields allocation (mapped) and its span offsets [set][slot][field]
+  bool ca_ = local_->ca();
+  char* ca_fields_[2] = {nullptr, nullptr};
+  long long ca_off_[2][2][2][2] = {};
 };
 
 }  // namespace

@@ -266,6 +266,7 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     ca_geom_.M = sd.nx + 1;
     for (const double** t : {&ca_tables_.rv, &ca_tables_.xlo, &ca_tables_.xhi, &ca_tables_.x}) *t += o;
     ca_tables_.acls += 4 * o;
+    ca_tables_.bcls += 4 * o;
   }
   ca_gh_ = ca_geom_.nb ? gh_ : 2;
 
@@ -764,6 +765,29 @@ void GpuSubdomainSolver::set_direct_rows(bool on) {
   direct_rows_ = on;
 }
 
+HaloMsgs GpuSubdomainSolver::ca_halo_msgs(int set) const {
+  PMX_CHECK(ca_, "ca_halo_msgs: not an s-step solver");
+  HaloMsgs out;
+  // s-step strips: the s owned edge rows of z and p of the set the next block reads (CaState::blk
+  // & 1, mirrored by ca_blk_) into the neighbour's s ghost rows, as ONE span per field: rows q,
+  // q+1 whole, row q+2's columns 0 .. ny+1 (columns <= 0 and >= ny+1 are Dirichlet on a strip)
+  const int s = ca_tiles_.s;
+  char* fz = set ? r2_ + field_off_ * elem_ : static_cast<char*>(field_base(1));
+  char* fp = static_cast<char*>(field_base(set ? 3 : 2));
+  const int64_t P = geom_.pitch;
+  const int count = int((s - 1) * P + sd_.ny + 2);
+  for (int slot = 0; slot < 2; ++slot) {
+    if (layout_.peer[slot] < 0) continue;
+    const int64_t srow = slot == 0 ? 1 : sd_.nx - s + 1, rrow = slot == 0 ? 1 - s : sd_.nx + 1;
+    for (int f = 0; f < 2; ++f) {
+      char* base = f == 0 ? fz : fp;
+      out.m[out.n++] = HaloMsg{slot, f, layout_.peer[slot], count, base + srow * P * int64_t(elem_),
+                               base + rrow * P * int64_t(elem_)};
+    }
+  }
+  return out;
+}
+
 HaloMsgs GpuSubdomainSolver::halo_msgs() const {
   HaloMsgs out;
   if (!direct_rows_) {  // the packed slot buffers of the comm arena
@@ -772,26 +796,7 @@ HaloMsgs GpuSubdomainSolver::halo_msgs() const {
         out.m[out.n++] = HaloMsg{slot, 0, layout_.peer[slot], layout_.edge_len[slot], send_dev(slot), recv_dev(slot)};
     return out;
   }
-  if (ca_) {
-    // s-step strips: the s owned edge rows of z and p of the set the next block reads (CaState::blk
-    // & 1, mirrored by ca_blk_) into the neighbour's s ghost rows, as ONE span per field: rows q,
-    // q+1 whole, row q+2's columns 0 .. ny+1 (columns <= 0 and >= ny+1 are Dirichlet on a strip)
-    const int s = ca_tiles_.s, set = int(ca_blk_ & 1);
-    char* fz = set ? r2_ + field_off_ * elem_ : static_cast<char*>(field_base(1));
-    char* fp = static_cast<char*>(field_base(set ? 3 : 2));
-    const int64_t P = geom_.pitch;
-    const int count = int((s - 1) * P + sd_.ny + 2);
-    for (int slot = 0; slot < 2; ++slot) {
-      if (layout_.peer[slot] < 0) continue;
-      const int64_t srow = slot == 0 ? 1 : sd_.nx - s + 1, rrow = slot == 0 ? 1 - s : sd_.nx + 1;
-      for (int f = 0; f < 2; ++f) {
-        char* base = f == 0 ? fz : fp;
-        out.m[out.n++] = HaloMsg{slot, f, layout_.peer[slot], count, base + srow * P * int64_t(elem_),
-                                 base + rrow * P * int64_t(elem_)};
-      }
-    }
-    return out;
-  }
+  if (ca_) return ca_halo_msgs(int(ca_blk_ & 1));
   // sweep t reads r^{t-1} from (t & 1 ? r2 : r) and p^{t-1} from (t & 1 ? p0 : p1) (k_pcg1)
   const long long t = halo_target_;
   char* fr = (t & 1) ? r2_ + field_off_ * elem_ : static_cast<char*>(field_base(1));

@@ -120,3 +120,16 @@ def test_ipc_transport_bitwise_equals_localcomm(pkg, tmp_path):
         meta, w = _run(tmp_path, 4, M, N, 1, "reference", comm="ipc", graph_batch=gb)
         assert meta["iters"] == st["iters"]
         assert np.array_equal(w, ref), (gb, np.abs(w - ref).max())
+
+
+@pytest.mark.parametrize("world,graph_batch", [(2, 32), (3, 0), (4, 32)])
+def test_ipc_transport_sstep_strips(pkg, tmp_path, world, graph_batch):
+    """The s-step PCG (algo 3) on row strips between 2..4 processes: the IPC transport pulls the s edge
+    rows of z and p straight from the neighbours' fields (direct rows, the set of the next block) and
+    all-reduces the 21 Gram / norm sums per block -- the multi-process driver an N-GPU RCCL run uses."""
+    M, N = 400, 600
+    meta, w = _run(tmp_path, world, M, N, 3, "rows", comm="ipc", graph_batch=graph_batch)
+    assert meta["world"] == world and meta["algo"] == "ca" and meta["comm"] == "ipc"
+    ref = pkg.solve(pkg.PoissonEllipse(M=M, N=N), "hip", ranks=1, algo="ca")
+    assert meta["iters"] == ref.iters == 546 and meta["status"] == "converged"
+    assert np.abs(w - ref.w).max() <= 1e-10 * np.abs(ref.w).max()
