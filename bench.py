@@ -575,12 +575,12 @@ def measure(args) -> int:
     dkw = dict(kw, **pkw, phase=watch.phase, init_timeout=COMM_INIT_TIMEOUT)
     # the s-step PCG (ca_kernels.hip) where it applies and wins: fp64 with the fast arithmetic, >= 6M
     # points (below, pcg1's block tiles win: profiles/r5/ca/small.log), undecomposed or row strips, and
-    # a transport that moves its ghost rows straight between the fields (RCCL, not IPC / torch)
+    # a transport that moves its ghost rows straight between the fields (RCCL or IPC, not torch)
     strips = world == 1 or process_grid(world, args.M, args.N, args.split)[1] == 1
     ca_ok = (args.dtype == "fp64" and not args.exact and strips and
-             (world == 1 or (not share and cfg["comm"] == "native")))
+             (world == 1 or cfg["comm"] in ("native", "ipc")))
     if args.algo == "ca" and not ca_ok:
-        raise SystemExit("[bench] --algo ca (the s-step PCG) needs fp64, row strips and the native RCCL transport")
+        raise SystemExit("[bench] --algo ca (the s-step PCG) needs fp64, row strips and the RCCL or IPC transport")
     use_ca = args.algo == "ca" or (args.algo == "auto" and ca_ok and (args.M - 1) * (args.N - 1) >= 6_000_000)
     algo_id = 3 if use_ca else {"auto": -1, "pcg1": 1, "pcg2": 2}[args.algo]
     if dry:
@@ -598,13 +598,13 @@ def measure(args) -> int:
                                                       algo=algo_id, ca_s=args.ca_s, **pkw, **kw), problem, info)
         comm_used = "self"
     elif share and cfg["comm"] == "ipc":
-        runner = ds.DistGpuPCG(problem, info, comm="ipc", device=0, **dkw)
+        runner = ds.DistGpuPCG(problem, info, comm="ipc", device=0, algo=algo_id, **dkw)
         comm_used = "ipc"
     elif share:
         runner = ds.DistGpuPCG(problem, info, comm="torch", device=0, **dkw)
         comm_used = "gloo-host-staged"
     elif cfg["comm"] == "ipc":
-        runner = ds.DistGpuPCG(problem, info, comm="ipc", **dkw)
+        runner = ds.DistGpuPCG(problem, info, comm="ipc", algo=algo_id, **dkw)
         comm_used = "ipc"
     elif cfg["comm"] == "native":
         runner = ds.DistGpuPCG(problem, info, comm="native", rccl_graph=cfg["rccl_graph"], algo=algo_id, **dkw)

@@ -155,7 +155,8 @@ __global__ void __launch_bounds__(256) k_ipc_pull(IpcPeers P, int me, PcgState* 
     dst[i] = __builtin_nontemporal_load(src + i);
 }
 
-// s-step strips (direct rows): the spans of one exchange, read straight from the neighbours' fields
+// s-step strips (direct rows): the spans of one exchange.  Pack: our edge rows -> our staging buffer
+// (nbr = nullptr, no wait); pull: the neighbour's staging buffer -> our ghost rows (after its post).
 struct IpcSpans {
   const IpcBlock* nbr[4];
   const void* src[4];
@@ -169,7 +170,7 @@ __global__ void __launch_bounds__(256) k_ipc_pull_spans(IpcPeers P, IpcSpans S4,
   const int q = blockIdx.y;
   __shared__ int ok;
   IpcBlock* own = P.all[me];
-  if (threadIdx.x == 0) ok = wait_ge(&S4.nbr[q]->halo_flag, own->halo_count, timeout, own, S) ? 1 : 0;
+  if (threadIdx.x == 0) ok = !S4.nbr[q] || wait_ge(&S4.nbr[q]->halo_flag, own->halo_count, timeout, own, S) ? 1 : 0;
   __syncthreads();
   if (!ok) return;
   const T* src = static_cast<const T*>(S4.src[q]);
@@ -211,6 +212,11 @@ class IpcComm final : public Comm {
     else  // flags every device reads and writes coherently (see the memory-model notes above)
       HIP_CHECK(hipExtMallocWithFlags(reinterpret_cast<void**>(&block_), sizeof(IpcBlock), hipDeviceMallocUncached));
     HIP_CHECK(hipMemset(block_, 0, sizeof(IpcBlock)));
+    if (ca_) {
+      const HaloMsgs ms = local_->ca_halo_msgs(0);
+      ca_count_ = ms.n ? ms.m[0].count : 0;
+      HIP_CHECK(hipMalloc(&ca_buf_, std::max<size_t>(256, size_t(4) * size_t(ca_count_) * sizeof(double))));
+    }
     const char* t = std::getenv("PMX_IPC_TIMEOUT_MS");
     timeout_ = (t && t[0] ? std::atoll(t) : 20000LL) * 100000LL;  // wall_clock64: 100 MHz
   }
@@ -219,6 +225,7 @@ class IpcComm final : public Comm {
     (void)hipDeviceSynchronize();
     for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
     if (block_) (void)hipFree(block_);
+    if (ca_buf_) (void)hipFree(ca_buf_);
   }
 
   // this rank's exports: device id, arena handle, block handle
@@ -227,18 +234,7 @@ class IpcComm final : public Comm {
     std::string out(reinterpret_cast<const char*>(&dev), sizeof(dev));
     out += handle_bytes(reinterpret_cast<void*>(local_->arena_ptr()));
     out += handle_bytes(block_);
-    if (ca_) {  // s-step strips: the fields allocation and where each (set, slot, field) span starts in it
-      out += handle_bytes(local_->fields_alloc());
-      long long off[2][2][2];
-      std::memset(off, 0xff, sizeof(off));
-      for (int set = 0; set < 2; ++set) {
-        const HaloMsgs ms = local_->ca_halo_msgs(set);
-        for (int q = 0; q < ms.n; ++q)
-          off[set][ms.m[q].slot][ms.m[q].field] =
-              static_cast<long long>(static_cast<char*>(ms.m[q].send) - local_->fields_alloc());
-      }
-      out += std::string(reinterpret_cast<const char*>(off), sizeof(off));
-    }
+    if (ca_) out += handle_bytes(ca_buf_);  // s-step strips: the staging buffer of our edge rows
     return out;
   }
 
@@ -252,7 +248,7 @@ class IpcComm final : public Comm {
     const CommLayout& L0 = local_->layout();
     for (int r = 0; r < world_; ++r) {
       const std::string& e = peers[size_t(r)];
-      PMX_CHECK(e.size() == sizeof(int) + 2 * hs + (ca_ ? hs + sizeof(ca_off_[0]) : 0), "bad IPC export of rank " << r);
+      PMX_CHECK(e.size() == sizeof(int) + 2 * hs + (ca_ ? hs : 0), "bad IPC export of rank " << r);
       if (r == me) {
         arenas[size_t(r)] = reinterpret_cast<char*>(local_->arena_ptr());
         P_.all[r] = block_;
@@ -272,9 +268,8 @@ class IpcComm final : public Comm {
       if (ca_) {
         for (int s = 0; s < 2; ++s) {
           if (L0.peer[s] != r) continue;
-          ca_fields_[s] = static_cast<char*>(open_handle(e.substr(sizeof(int) + 2 * hs, hs)));
-          opened_.push_back(ca_fields_[s]);
-          std::memcpy(ca_off_[s], e.data() + sizeof(int) + 3 * hs, sizeof(ca_off_[s]));
+          ca_peer_buf_[s] = static_cast<char*>(open_handle(e.substr(sizeof(int) + 2 * hs, hs)));
+          opened_.push_back(ca_peer_buf_[s]);
         }
       }
     }
@@ -319,32 +314,44 @@ class IpcComm final : public Comm {
     require(local);
     if (maxlen_ == 0) return;
     const int me = local_->sd().rank;
-    hipLaunchKernelGGL(k_ipc_post, dim3(1), dim3(64), 0, streams[0], P_, me);
-    if (ca_) {  // the s rows of z and p of the current set, from the neighbours' fields into our ghost rows
+    if (ca_) {
+      // the s edge rows of z and p of the current set: wait until every neighbour pulled the last
+      // exchange, stage ours, post, pull the neighbours' staged rows into our ghost rows, acknowledge.
+      // (Mapping the neighbours' whole field allocations instead hung hipIpcOpenMemHandle with 4
+      // ranks of a 16384^2 grid on one GPU; the staging copy is ~1.5 MB per block.)
       const HaloMsgs ms = local_->halo_msgs();
-      const int set = local_->ca_halo_set();
-      IpcSpans sp{};
-      int n = 0, maxc = 0;
+      IpcSpans pack{}, pull{};
+      int maxc = 0;
+      PMX_CHECK(ms.n <= 4, "IpcComm: more than 4 s-step spans");
       for (int q = 0; q < ms.n; ++q) {
         const HaloMsg& m = ms.m[q];
-        const long long off = ca_off_[m.slot][set][opposite_slot(m.slot)][m.field];
-        PMX_CHECK(n < 4 && off >= 0 && ca_fields_[m.slot] && P_.nbr[m.slot], "IpcComm: no peer span for slot " << m.slot);
-        sp.nbr[n] = P_.nbr[m.slot];
-        sp.src[n] = ca_fields_[m.slot] + off;
-        sp.dst[n] = m.recv;
-        sp.len[n] = m.count;
+        PMX_CHECK(m.count == ca_count_ && ca_peer_buf_[m.slot] && P_.nbr[m.slot], "IpcComm: bad s-step span on slot " << m.slot);
+        const size_t mine = size_t(m.slot * 2 + m.field) * size_t(ca_count_) * sizeof(double);
+        const size_t theirs = size_t(opposite_slot(m.slot) * 2 + m.field) * size_t(ca_count_) * sizeof(double);
+        pack.nbr[q] = nullptr;
+        pack.src[q] = m.send;
+        pack.dst[q] = ca_buf_ + mine;
+        pack.len[q] = m.count;
+        pull.nbr[q] = P_.nbr[m.slot];
+        pull.src[q] = ca_peer_buf_[m.slot] + theirs;
+        pull.dst[q] = m.recv;
+        pull.len[q] = m.count;
         maxc = std::max(maxc, m.count);
-        ++n;
       }
-      if (n) {
-        const int bx = std::max(1, std::min(64, (maxc + 255) / 256));
-        hipLaunchKernelGGL(k_ipc_pull_spans<double>, dim3(bx, n), dim3(256), 0, streams[0], P_, sp, me,
+      if (ms.n) {
+        const dim3 grid(std::max(1, std::min(64, (maxc + 255) / 256)), ms.n);
+        hipLaunchKernelGGL(k_ipc_wait_acks, dim3(1), dim3(64), 0, streams[0], P_, me, local_->state_dev(), timeout_);
+        hipLaunchKernelGGL(k_ipc_pull_spans<double>, grid, dim3(256), 0, streams[0], P_, pack, me,
                            local_->state_dev(), timeout_);
+        hipLaunchKernelGGL(k_ipc_post, dim3(1), dim3(64), 0, streams[0], P_, me);
+        hipLaunchKernelGGL(k_ipc_pull_spans<double>, grid, dim3(256), 0, streams[0], P_, pull, me,
+                           local_->state_dev(), timeout_);
+        hipLaunchKernelGGL(k_ipc_ack, dim3(1), dim3(64), 0, streams[0], P_, me);
       }
-      hipLaunchKernelGGL(k_ipc_ack, dim3(1), dim3(64), 0, streams[0], P_, me);
       HIP_CHECK(hipGetLastError());
       return;
     }
+    hipLaunchKernelGGL(k_ipc_post, dim3(1), dim3(64), 0, streams[0], P_, me);
     const int bx = std::max(1, std::min(64, (maxlen_ + 255) / 256));
     if (local_->layout().elem == 8)
       hipLaunchKernelGGL(k_ipc_pull<double>, dim3(bx, kHaloSlots), dim3(256), 0, streams[0], P_, me,
@@ -362,7 +369,7 @@ class IpcComm final : public Comm {
                         "was stopped");
   }
   bool prefers_split() const override { return true; }
-  bool direct_rows() const override { return ca_; }  // s-step strips read the neighbours' fields in place
+  bool direct_rows() const override { return ca_; }  // s-step strips: spans of the fields (staged)
   std::string name() const override { return "ipc"; }
   int world_size() const override { return world_; }
 
@@ -380,9 +387,12 @@ class IpcComm final : public Comm {
   long long timeout_ = 0;
   bool attached_ = false;
   // s-step strips: each x neighbour's fields allocation (mapped) and its span offsets [set][slot][field]
+  // s-step strips: our staging buffer of edge rows ([slot][field] spans of ca_count_ elements) and each
+  // x neighbour's (mapped)
   bool ca_ = local_->ca();
-  char* ca_fields_[2] = {nullptr, nullptr};
-  long long ca_off_[2][2][2][2] = {};
+  int ca_count_ = 0;
+  char* ca_buf_ = nullptr;
+  char* ca_peer_buf_[2] = {nullptr, nullptr};
 };
 
 }  // namespace

@@ -252,8 +252,6 @@ class GpuSubdomainSolver {
   // s-step strips: the messages of an exchange of (z, p) set `set` (halo_msgs() = the current set's)
   HaloMsgs ca_halo_msgs(int set) const;
   int ca_halo_set() const { return int(ca_blk_ & 1); }
-  // the one allocation every field lives in (a transport that maps a peer's fields, IpcComm)
-  char* fields_alloc() const { return fields_; }
 
   // Checkpoint: the 4 fields with ghosts, the PCG scalars and the halo buffers,
   // i.e. everything the next iteration reads.  Synchronous; written at batch boundaries.
