@@ -910,9 +910,12 @@ CaTiles make_ca_tiles(const DevGeom& G, int s, int rows, int rows2) {
   t.tiles_j = (G.ny + t.wo - 1) / t.wo;
   if (rows <= 0) {
     // tall tiles keep the 2s re-marched halo rows cheap (their basis levels are recomputed); shorter
-    // only when the grid has too few tiles to fill the chip a few times over
+    // when the grid has fewer than ~4 rounds of tiles (3 waves x 4 SIMDs x 256 CUs = 3072 at a time):
+    // a tile's march is ~1.5 us per row with the SIMD shared, so a last round of long tiles trails.
+    // 8-GPU strip of 16384^2 (2048 rows): 64-row tiles (4050) 284 us per pass 1, 32-row 225 us;
+    // loopback per-rank iteration 8 GPUs 240 -> 221 us, 4 GPUs 388 -> 371 (profiles/r5/ca/rows/).
     rows = 64;
-    while (rows > 8 && int64_t((G.nx + rows - 1) / rows) * t.tiles_j < 4096) rows /= 2;
+    while (rows > 8 && int64_t((G.nx + rows - 1) / rows) * t.tiles_j < 12288) rows /= 2;
   }
   PMX_CHECK(rows >= 1 && rows <= 4096, "s-step PCG: tile rows must be in [1, 4096]");
   t.rows = rows;
@@ -920,7 +923,10 @@ CaTiles make_ca_tiles(const DevGeom& G, int s, int rows, int rows2) {
   // pass 2 (memory-bound, no Gram) marches shorter tiles: fewer DRAM rows in flight per wave and a
   // finer load balance win over the extra halo rows (16384^2: pass 2 2.87 ms at 32 rows, 2.66 at 16;
   // pass 1 1.78 at 32, 1.77 at 64, 2.17 at 16 -- profiles/r5/ca/)
-  if (rows2 <= 0) rows2 = std::max(8, rows / 4);
+  if (rows2 <= 0) {
+    rows2 = 16;
+    while (rows2 > 8 && int64_t((G.nx + rows2 - 1) / rows2) * t.tiles_j < 4096) rows2 /= 2;
+  }
   PMX_CHECK(rows2 >= 1 && rows2 <= 4096, "s-step PCG: pass-2 tile rows must be in [1, 4096]");
   t.rows2 = rows2;
   t.tiles_i2 = (G.nx + rows2 - 1) / rows2;
