@@ -701,14 +701,18 @@ void GpuSubdomainSolver::ca_sweep(hipStream_t s, bool upd) {
   double* z1 = reinterpret_cast<double*>(r2_ + field_off_ * elem_);
   double* p0 = static_cast<double*>(field_base(2));
   double* p1 = static_cast<double*>(field_base(3));
+  hipEvent_t wait = upd ? nullptr : ca_frame_wait_;
+  if (!upd) ca_frame_wait_ = nullptr;
   if (ca_side_) {
     HIP_CHECK(hipEventRecord(ca_ev_fork_, s));
     HIP_CHECK(hipStreamWaitEvent(ca_side_, ca_ev_fork_, 0));
+    if (wait) HIP_CHECK(hipStreamWaitEvent(ca_side_, wait, 0));  // the frame reads the ghost rows
     launch_ca_sweep<double>(ca_geom_, ca_tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, upd, s,
                             ca_side_);
     HIP_CHECK(hipEventRecord(ca_ev_join_, ca_side_));
     HIP_CHECK(hipStreamWaitEvent(s, ca_ev_join_, 0));
   } else {
+    if (wait) HIP_CHECK(hipStreamWaitEvent(s, wait, 0));
     launch_ca_sweep<double>(ca_geom_, ca_tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, upd, s);
   }
   after_launch(s);
@@ -1435,6 +1439,18 @@ void PcgDriver::enqueue_ca(int64_t n) {
       f(local_[i], streams_[i]);
     }
   };
+  // With the overlapped schedule the exchange runs on the comm stream: the next pass 1's interior
+  // tiles (which read no ghost row) start at once, its frame tiles wait for the exchange.  The batch
+  // joins the comm stream at its end, so a captured graph has no edge into the next one.
+  const bool ovl = any_nb_ && overlap_ && !comm_streams_.empty();
+  bool pending = false;
+  auto frame_waits = [&](bool on) {  // every solver, by the index of its (possibly shared) stream
+    size_t u = 0;
+    for (size_t i = 0; i < local_.size(); ++i) {
+      if (i > 0 && streams_[i] != streams_[i - 1]) ++u;
+      local_[i]->set_ca_frame_wait(on ? ev_halo_[u] : nullptr);
+    }
+  };
   while (n > 0) {
     const int m = int(std::min<int64_t>(s, n));
     each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, false); });
@@ -1442,13 +1458,28 @@ void PcgDriver::enqueue_ca(int64_t n) {
     comm_->allreduce(local_, 3, streams_);
     each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_finish(st, m, false); });
     each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, true); });
-    if (any_nb_) comm_->halo(local_, streams_);
+    if (any_nb_ && ovl) {
+      for_each_stream([&](size_t i, size_t u) {
+        HIP_CHECK(hipEventRecord(ev_packed_[u], streams_[i]));
+        HIP_CHECK(hipStreamWaitEvent(comm_streams_[i], ev_packed_[u], 0));
+      });
+      comm_->halo(local_, comm_streams_);
+      for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipEventRecord(ev_halo_[u], comm_streams_[i])); });
+      frame_waits(true);
+      pending = true;
+    } else if (any_nb_) {
+      comm_->halo(local_, streams_);
+    }
     n -= m;
   }
   each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_reduce(st, 1, true, false); });
   comm_->allreduce(local_, 3, streams_);
   each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_finish(st, 1, true); });
   each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, true); });  // rewind
+  if (pending) {  // the last block's exchange ran next to the check
+    for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipStreamWaitEvent(streams_[i], ev_halo_[u], 0)); });
+    frame_waits(false);
+  }
 }
 
 int PcgDriver::ca_phase() const { return any_nb_ ? int(local_[0]->ca_blocks() & 1) : 0; }

@@ -252,6 +252,10 @@ class GpuSubdomainSolver {
   // s-step strips: the messages of an exchange of (z, p) set `set` (halo_msgs() = the current set's)
   HaloMsgs ca_halo_msgs(int set) const;
   int ca_halo_set() const { return int(ca_blk_ & 1); }
+  // s-step strips: the next pass 1 runs its interior tiles at once and its frame tiles (the only ones
+  // that read ghost rows) after event e -- the ghost exchange on the driver's comm stream.  Without a
+  // frame stream the whole pass waits.  One-shot.
+  void set_ca_frame_wait(hipEvent_t e) { ca_frame_wait_ = e; }
 
   // Checkpoint: the 4 fields with ghosts, the PCG scalars and the halo buffers,
   // i.e. everything the next iteration reads.  Synchronous; written at batch boundaries.
@@ -363,6 +367,7 @@ class GpuSubdomainSolver {
   char* ca_faces_ = nullptr;    // its face-coefficient fields (a, b)
   hipStream_t ca_side_ = nullptr;  // the frame tiles' stream (split kernels)
   hipEvent_t ca_ev_fork_ = nullptr, ca_ev_join_ = nullptr;
+  hipEvent_t ca_frame_wait_ = nullptr;  // one-shot: the next pass 1's frame tiles wait for it
   void ca_sweep(hipStream_t s, bool upd);
   CaState* ca_state_ = nullptr;
   double* ca_chunk_ = nullptr;  // its reduction's chunk sums
