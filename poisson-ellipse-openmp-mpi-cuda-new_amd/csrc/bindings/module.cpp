@@ -620,12 +620,15 @@ PYBIND11_MODULE(_pmx, m) {
           d["algo"] = s.solver(0).single_pass() ? "pcg1" : "pcg2";
         }
         if (!s.solver(0).placement_ms().empty()) {
-          // 3 plain sweeps per candidate field block (rotating field roles), the fastest kept
+          // real iterations per candidate field block, the fastest kept (the slowest under
+          // GpuOptions::placement_pick = 1)
           std::vector<float> v = s.solver(0).placement_ms();
           py::list l;
           for (float x : v) l.append(x);
           d["placement_probe_ms"] = l;
-          const auto mn = std::min_element(v.begin(), v.end());
+          const bool slowest = s.solver(0).options().placement_pick == 1;
+          const auto mn = slowest ? std::max_element(v.begin(), v.end()) : std::min_element(v.begin(), v.end());
+          if (slowest) d["placement_pick"] = "slowest";
           py::dict q;
           q["candidates"] = v.size();
           q["kept"] = size_t(mn - v.begin());

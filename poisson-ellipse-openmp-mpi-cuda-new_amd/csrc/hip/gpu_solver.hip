@@ -122,6 +122,7 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_CA_SPLIT", o.ca_split);
   env_int("PMX_CA_FRAME_STREAM", o.ca_frame_stream);
   env_int("PMX_CA_DIRICHLET", o.ca_dirichlet);
+  if (const char* pk = std::getenv("PMX_PLACEMENT_PICK"); pk && pk[0]) o.placement_pick = std::string(pk) == "slowest" ? 1 : 0;
   PMX_CHECK(o.ca_split == 0 || o.ca_split == 1, "s-step PCG: ca_split must be 0 or 1");
   env_int("PMX_CA_WAVES_GRAM", o.ca_waves_gram);
   env_int("PMX_CA_WAVES_UPD", o.ca_waves_upd);
@@ -502,7 +503,9 @@ void GpuSubdomainSolver::place_fields() {
     placement_ms_.clear();
     throw;
   }
-  keep_only(size_t(std::min_element(placement_ms_.begin(), placement_ms_.end()) - placement_ms_.begin()));
+  const auto pick = opt_.placement_pick == 1 ? std::max_element(placement_ms_.begin(), placement_ms_.end())
+                                             : std::min_element(placement_ms_.begin(), placement_ms_.end());
+  keep_only(size_t(pick - placement_ms_.begin()));
   HIP_CHECK(hipEventDestroy(e0));
   HIP_CHECK(hipEventDestroy(e1));
   HIP_CHECK(hipStreamDestroy(s));

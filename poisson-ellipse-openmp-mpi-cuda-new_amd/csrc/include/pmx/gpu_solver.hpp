@@ -144,6 +144,9 @@ struct GpuOptions {
   int dma1 = 0, dma1w = -1;
   double placement_budget_s = 0.5;
   double placement_keep_free = 0.5;
+  // which probed block to keep: 0 the fastest (default), 1 the slowest -- for slow-class A/Bs and
+  // counter tables on one box (PMX_PLACEMENT_PICK=slowest)
+  int placement_pick = 0;
   bool resolved = false;  // environment overrides already applied (resolve_options)
 };
 
