@@ -108,16 +108,20 @@ def test_ipc_transport_matches_single_rank(pkg, tmp_path, world, split, algo, ex
     assert np.abs(w - ref.w).max() < 1e-11
 
 
-def test_ipc_transport_bitwise_equals_localcomm(pkg, tmp_path):
-    """Rank-ordered sums and exact ghost copies: 4 processes over IPC give bit-for-bit the solution
-    of one process driving the same 4 subdomains (LocalComm), eager and captured."""
+@pytest.mark.parametrize("world", [4, 8, 9])
+def test_ipc_transport_bitwise_equals_localcomm(pkg, tmp_path, world):
+    """Rank-ordered sums and exact ghost copies: P processes over IPC give bit-for-bit the solution
+    of one process driving the same P subdomains (LocalComm), eager and captured -- 2-D blocks of the
+    reference's process grids 2x2, 2x4 (BASELINE config 4's shape) and 3x3 (middle rank: 4 sides and
+    4 corners)."""
     M, N = 300, 500
     p = pkg.PoissonEllipse(M=M, N=N)
-    s = pkg.make_session(p, ranks=4, split="reference")
+    s = pkg.make_session(p, ranks=world, split="reference")
     st = s.solve(1)
     ref = s.gather_local_w()
     for gb in (0, 16):
-        meta, w = _run(tmp_path, 4, M, N, 1, "reference", comm="ipc", graph_batch=gb)
+        meta, w = _run(tmp_path, world, M, N, 1, "reference", comm="ipc", graph_batch=gb)
+        assert meta["grid"][0] * meta["grid"][1] == world and min(meta["grid"]) > 1
         assert meta["iters"] == st["iters"]
         assert np.array_equal(w, ref), (gb, np.abs(w - ref).max())
 
