@@ -123,10 +123,10 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_CA_FRAME_STREAM", o.ca_frame_stream);
   env_int("PMX_CA_DIRICHLET", o.ca_dirichlet);
   if (const char* pk = std::getenv("PMX_PLACEMENT_PICK"); pk && pk[0]) o.placement_pick = std::string(pk) == "slowest" ? 1 : 0;
-  PMX_CHECK(o.ca_split == 0 || o.ca_split == 1, "s-step PCG: ca_split must be 0 or 1");
+  PMX_CHECK(o.ca_split >= -1 && o.ca_split <= 1, "s-step PCG: ca_split must be -1, 0 or 1");
   env_int("PMX_CA_WAVES_GRAM", o.ca_waves_gram);
   env_int("PMX_CA_WAVES_UPD", o.ca_waves_upd);
-  PMX_CHECK(o.ca_dma == 0 || o.ca_dma == 1, "s-step PCG: ca_dma must be 0 or 1");
+  PMX_CHECK(o.ca_dma >= -1 && o.ca_dma <= 1, "s-step PCG: ca_dma must be -1, 0 or 1");
   PMX_CHECK((o.ca_waves_gram == 2 || o.ca_waves_gram == 3) && (o.ca_waves_upd == 2 || o.ca_waves_upd == 3),
             "s-step PCG: waves per SIMD must be 2 or 3");
   env_int("PMX_PCG1_DMA", o.dma1);
@@ -359,8 +359,9 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     ca_tiles_.fb = reinterpret_cast<const double*>(ca_faces_ + field_bytes_ + field_off_ * elem_);
     ca_tiles_.gh = ca_gh_;
     ca_build_faces(ca_geom_, ca_tables_, const_cast<double*>(ca_tiles_.fa), const_cast<double*>(ca_tiles_.fb), ca_gh_, nullptr);
-    ca_tiles_.dma = opt_.ca_dma;
-    if (!opt_.ca_split) ca_tiles_.split = 0;
+    const bool split = opt_.ca_split == -1 ? geom_.nb != 0 : opt_.ca_split == 1;  // see GpuOptions::ca_split
+    if (!split) ca_tiles_.split = 0;
+    ca_tiles_.dma = opt_.ca_dma == -1 ? int(split) : opt_.ca_dma;
     if (ca_tiles_.split && opt_.ca_frame_stream) {
       HIP_CHECK(hipStreamCreateWithFlags(&ca_side_, hipStreamNonBlocking));
       HIP_CHECK(hipEventCreateWithFlags(&ca_ev_fork_, hipEventDisableTiming));
