@@ -953,7 +953,7 @@ CaTiles make_ca_tiles(const DevGeom& G, int s, int rows, int rows2) {
   };
   rect(rows, t.tiles_i, t.ti_lo, t.ti_hi);
   rect(rows2, t.tiles_i2, t.ti_lo2, t.ti_hi2);
-  if (t.ti_hi <= t.ti_lo || t.ti_hi2 <= t.ti_lo2) t.split = 0;
+  if (t.ti_hi <= t.ti_lo || t.ti_hi2 <= t.ti_lo2) t.split = t.split_upd = 0;
   t.cwords = (G.nx + 2 * s + 2 * kCaRowOff + 15) / 16 + 1;
   return t;
 }
@@ -1007,7 +1007,7 @@ void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, 
   // the general one at 2; else every tile general at waves_gram / waves_upd
 #define PMX_CA(SS)                                                                                                   \
   do {                                                                                                               \
-    if (t.split && nin > 0) {                                                                                        \
+    if ((upd ? t.split_upd : t.split) && nin > 0) {                                                                  \
       if (upd) {                                                                                                     \
         PMX_CA_K(SS, true, 2, false, 2, P2, n - nin);                                                                \
         PMX_CA_K(SS, true, 3, false, 1, P1, nin);                                                                    \

@@ -120,10 +120,12 @@ GpuOptions resolve_options(const GpuOptions& in) {
   PMX_CHECK(o.ca_rows >= 0 && o.ca_rows <= 4096, "s-step PCG: tile rows must be 0 (auto) .. 4096");
   env_int("PMX_CA_DMA", o.ca_dma);
   env_int("PMX_CA_SPLIT", o.ca_split);
+  env_int("PMX_CA_SPLIT_UPD", o.ca_split_upd);
   env_int("PMX_CA_FRAME_STREAM", o.ca_frame_stream);
   env_int("PMX_CA_DIRICHLET", o.ca_dirichlet);
   if (const char* pk = std::getenv("PMX_PLACEMENT_PICK"); pk && pk[0]) o.placement_pick = std::string(pk) == "slowest" ? 1 : 0;
   PMX_CHECK(o.ca_split >= -1 && o.ca_split <= 1, "s-step PCG: ca_split must be -1, 0 or 1");
+  PMX_CHECK(o.ca_split_upd >= -1 && o.ca_split_upd <= 1, "s-step PCG: ca_split_upd must be -1, 0 or 1");
   env_int("PMX_CA_WAVES_GRAM", o.ca_waves_gram);
   env_int("PMX_CA_WAVES_UPD", o.ca_waves_upd);
   PMX_CHECK(o.ca_dma >= -1 && o.ca_dma <= 1, "s-step PCG: ca_dma must be -1, 0 or 1");
@@ -361,6 +363,8 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     ca_build_faces(ca_geom_, ca_tables_, const_cast<double*>(ca_tiles_.fa), const_cast<double*>(ca_tiles_.fb), ca_gh_, nullptr);
     const bool split = opt_.ca_split == -1 ? geom_.nb != 0 : opt_.ca_split == 1;  // see GpuOptions::ca_split
     if (!split) ca_tiles_.split = 0;
+    if (!(opt_.ca_split_upd == -1 ? split : opt_.ca_split_upd == 1)) ca_tiles_.split_upd = 0;
+    if (!ca_tiles_.split) ca_tiles_.split_upd = ca_tiles_.split_upd && opt_.ca_split_upd == 1;
     ca_tiles_.dma = opt_.ca_dma == -1 ? int(split) : opt_.ca_dma;
     if (ca_tiles_.split && opt_.ca_frame_stream) {
       HIP_CHECK(hipStreamCreateWithFlags(&ca_side_, hipStreamNonBlocking));

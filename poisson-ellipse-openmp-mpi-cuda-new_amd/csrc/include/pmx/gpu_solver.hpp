@@ -82,15 +82,16 @@ struct GpuOptions {
   // waves (spills); pass 2 3025 at 2 waves vs 3105 at 3 (56 B of spills) -- within noise
   // ca_dma -1: LDS-DMA rows with the split kernels (below), registers without
   int ca_dma = -1, ca_waves_gram = 2, ca_waves_upd = 3;
-  // s-step: the interior tiles of each pass by a kernel without the Dirichlet / partial-tile paths, whose
-  // registers fit 3 waves per SIMD (pass 1 with LDS-DMA rows), the frame by the general kernel (1), or
-  // every tile by the general kernel (0).  PMX_CA_SPLIT.  -1 (auto): split on row strips, whose
-  // frame tiles wait for the ghost exchange while the interior runs (loopback rank 3 of 8: 220-226 vs
-  // 234-243 us unsplit); one general kernel on undecomposed grids, which no exchange splits and where
-  // the side stream's cross-queue edges cost more than the 3-wave interior kernel gains (16384^2
-  // same-process medians 1319.6 split vs 1278.6 unsplit, the split bimodal 1238-1324:
-  // profiles/r5/ca/split/).
-  int ca_split = -1;
+  // s-step: the interior tiles of a pass by a kernel without the Dirichlet / partial-tile paths, whose
+  // registers fit 3 waves per SIMD (pass 1 with LDS-DMA rows), the frame by the general kernel on a
+  // side stream (1), or every tile by the general kernel (0); -1 = split on row strips only.
+  // PMX_CA_SPLIT / PMX_CA_SPLIT_UPD (pass 2; -1: as pass 1).  16384^2, every session on the fastest
+  // of 20 probed blocks, 5 same-process rounds: 1169 us/iteration with pass 1 split and pass 2 one
+  // kernel, 1178 both split, 1222 neither (profiles/r5/ca/split/placed_ab16384.log; without the probe
+  // the placement lottery hid the difference).  On row strips pass 1's frame tiles also wait for the
+  // ghost exchange while its interior runs.
+  int ca_split = 1;
+  int ca_split_upd = 0;
   // ... the frame kernel on a side stream, overlapping the interior (1), or after it (0).  PMX_CA_FRAME_STREAM.
   int ca_frame_stream = 1;
   // s-step kernels see the subdomain's ghost rows as a Dirichlet boundary (nb = 0) while the driver

@@ -150,6 +150,7 @@ struct CaTiles {
   // reach): [ti_lo, ti_hi) x [tj_lo, tj_hi) for pass 1, [ti_lo2, ti_hi2) x (same columns) for pass 2
   int ti_lo = 0, ti_hi = 0, tj_lo = 0, tj_hi = 0, ti_lo2 = 0, ti_hi2 = 0;
   int split = 1;       // interior tiles by a fast-only kernel at 3 waves per SIMD, the frame by the general one
+  int split_upd = 1;   // the same for pass 2
   int dma = 1;         // pass 1: interior tiles prefetch their rows by LDS-DMA (0: registers)
   int waves_gram = 2;  // waves per SIMD the pass-1 registers must allow (2 or 3)
   int waves_upd = 3;   // ... pass 2 (2 or 3)
