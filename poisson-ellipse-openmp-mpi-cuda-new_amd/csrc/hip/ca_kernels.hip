@@ -111,15 +111,15 @@ __device__ __forceinline__ CaK ca_consts(const DevGeom& G) {
 }
 
 // Columns c0 .. c0 + 127 of a row, 2 per lane (c0 - 1 even: 16-B aligned chunks); chunks clamped to
-// start <= cmax.  The row pointer is wave-uniform and every column is >= -HE, so row - 4 plus an
-// unsigned byte offset keeps the SGPR-base addressing of pcg1_march's col_ptr.
+// start <= cmax.  The row pointer is wave-uniform and every column is >= -HE >= -8, so row - 8 plus
+// an unsigned byte offset keeps the SGPR-base addressing of pcg1_march's col_ptr.
 template <typename T>
 __device__ __forceinline__ const T* ca_col(const T* row, int c) {
-  return reinterpret_cast<const T*>(reinterpret_cast<const char*>(row - 4) + unsigned(c + 4) * unsigned(sizeof(T)));
+  return reinterpret_cast<const T*>(reinterpret_cast<const char*>(row - 8) + unsigned(c + 8) * unsigned(sizeof(T)));
 }
 template <typename T>
 __device__ __forceinline__ T* ca_col(T* row, int c) {
-  return reinterpret_cast<T*>(reinterpret_cast<char*>(row - 4) + unsigned(c + 4) * unsigned(sizeof(T)));
+  return reinterpret_cast<T*>(reinterpret_cast<char*>(row - 8) + unsigned(c + 8) * unsigned(sizeof(T)));
 }
 
 template <typename T>
@@ -229,7 +229,7 @@ struct CaRow {
 // One wave's march over one tile (see the header).  UPD = false: the Gram products into acc; true:
 // p, z, w updated with the block's coefficient vectors ca / cb / cc and ||Y pa_j||^2 into acc
 // (REW: w += Y cc only).
-template <typename T, int S, bool UPD, bool FAST, int PF, bool REW, int DPF = 0>
+template <typename T, int S, bool UPD, bool FAST, int PF, bool REW, int DPF = 0, int HE = CaShape<S>::HE>
 __device__ __forceinline__ void ca_march(const DevGeom& G, const DevTables& Tb, const CaK& K,
                                          const T* __restrict__ pin, const T* __restrict__ zin, T* __restrict__ pout,
                                          T* __restrict__ zout, T* __restrict__ w, int i0, int i1, int j0, int j1,
@@ -241,7 +241,7 @@ __device__ __forceinline__ void ca_march(const DevGeom& G, const DevTables& Tb, 
   constexpr int NB = Sh::NB, A = Sh::AGES;
   const int64_t P = G.pitch;
   const int lane = threadIdx.x & 63;
-  const int c0 = j0 - Sh::HE + 2 * lane;
+  const int c0 = j0 - HE + 2 * lane;
   const int cmax = G.ny + 1 + (G.ny & 1);
   bool colin[2], own[2];
   int gj[2];
@@ -595,6 +595,355 @@ marched:
   }
 }
 
+// ---- the fused pass: pass 2 of block b and pass 1 of block b + 1 in ONE march ----
+// Pass 1 of block b + 1 reads exactly the (p, z) that pass 2 of block b writes, so one wave can form
+// them and go on: stage 1 builds block b's basis from (p_b, z_b) (radius s), forms p_{b+1}, z_{b+1}
+// (and w, and block b's norms on the owned rows), and stage 2 builds block b+1's basis from those
+// values still in registers (radius s again) and sums its Gram products.  The tile loads radius 2s
+// (2s extra rows above and below, HE = 2s extra columns per side), and the block costs 48 B/pt of
+// HBM traffic (read p, z, w; write p, z, w) instead of 64: pass 1's re-read of p, z disappears.  The
+// reduction that follows sees what it saw after pass 1 (the Gram partials of block b + 1) plus the
+// norms of block b, which the pass 2 of the unfused schedule left; the scalars are unchanged.
+template <int S>
+struct CaFuseShape {
+  static constexpr int HE = 2 * S;         // even: 16-B aligned column chunks
+  static constexpr int WO = 128 - 2 * HE;  // owned columns per wave tile
+};
+
+template <typename T>
+struct CaFRow {
+  T p[2], z[2], w[2];
+};
+
+// The two halves run in two waves of one workgroup: wave 0 (the producer) marches stage 1 and writes
+// each new (p, z) row into a 2-slot LDS ring, wave 1 (the consumer) marches stage 2 from the ring, one
+// workgroup barrier per row step.  One wave holding both chains' register windows, the Gram sums and
+// the prefetch rows needs ~300 VGPRs (1 wave per SIMD, latency-bound: measured 1.38-2.3 ms/iteration
+// against 1.20 unfused at 16384^2); split, each wave holds half and the SIMDs keep 3 of them.
+template <typename T, int S, bool FAST, int PF, int ROLE>
+__device__ __forceinline__ void ca_march_fused(const DevGeom& G, const CaK& K, const T* __restrict__ pin,
+                                               const T* __restrict__ zin, T* __restrict__ pout, T* __restrict__ zout,
+                                               T* __restrict__ w, int i0, int i1, int j0, int j1,
+                                               const unsigned* __restrict__ ctbl, const CaFaces& F,
+                                               double (&acc)[CaShape<S>::NQ], double (&nacc)[S],
+                                               const double (&ca)[CaShape<S>::NB], const double (&cb)[CaShape<S>::NB],
+                                               const double (&cc)[CaShape<S>::NB],
+                                               const double (&pa)[S][CaShape<S>::NB], double* ring) {
+  using Sh = CaShape<S>;
+  constexpr int NB = Sh::NB, HE = CaFuseShape<S>::HE;
+  const int64_t P = G.pitch;
+  const int lane = threadIdx.x & 63;
+  const int c0 = j0 - HE + 2 * lane;
+  const int cmax = G.ny + 1 + (G.ny & 1);
+  bool colin[2], own[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int c = c0 + u, g = G.gj0 + c;
+    colin[u] = g >= 1 && g <= G.N - 1;
+    own[u] = c >= j0 && c <= j1;
+  }
+  const bool own_all = own[0] && own[1];
+  const bool own_any = own[0] || own[1];
+  auto interior_row = [&](int m) { return G.gi0 + m >= 1 && G.gi0 + m <= G.M - 1; };
+  // ring slot k: the new p row at ring + k * 256, z at + 128 (2 doubles per lane)
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  auto sync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  };
+
+  // register windows as ca_march's: level l of a chain at row r in slot (r - mfirst) & 3.  The
+  // producer's chain (block b's basis) trails the loaded row by l rows, the consumer's (block b+1's)
+  // trails the producer's output row by l more.
+  double XP[S + 1][4][2], XZ[S][4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+#pragma unroll
+      for (int l = 0; l <= S; ++l) XP[l][a][u] = 0.0;
+#pragma unroll
+      for (int l = 0; l < S; ++l) XZ[l][a][u] = 0.0;
+    }
+  int ch[4] = {0, 0, 0, 0};  // row classes, same slots
+
+  const int mfirst = i0 - 2 * S, mlast = i1 + 2 * S;
+  // level l of a chain at row rb - l (slot q = slot of row rb) from level l-1 at rows rb-l-1 .. rb-l+1
+  // and level l-2 at row rb-l
+  auto level = [&](auto lc, auto qc, int rb, auto& X) {
+    constexpr int l = decltype(lc)::value, q = decltype(qc)::value;
+    constexpr int sc = (q - l) & 3, sm = (q - l - 1) & 3, sp = (q - l + 1) & 3;
+    const int r = rb - l;
+    const double(&ctr)[2] = X[l - 1][sc];
+    const double left = dpp_shift0<kWaveShr1>(ctr[1]);
+    const double right = dpp_shift0<kWaveShl1>(ctr[0]);
+    double lt[2];
+    ca_lt(ch[sc], r, ctr, X[l - 1][sm], X[l - 1][sp], left, right, K, G, F, c0, cmax, lt);
+    const bool rin = FAST || interior_row(r);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      double v;
+      if constexpr (l == 1) v = lt[u];
+      else v = __builtin_fma(2.0, lt[u], -X[l - 2][sc][u]);
+      X[l][sc][u] = (FAST || (rin && colin[u])) ? v : 0.0;
+    }
+  };
+  auto chains = [&](auto qc, int rb) {
+    static_for_while<S>([&](auto l1) {
+      level(std::integral_constant<int, decltype(l1)::value + 1>{}, qc, rb, XP);
+      return true;
+    });
+    static_for_while<S - 1>([&](auto l1) {
+      level(std::integral_constant<int, decltype(l1)::value + 1>{}, qc, rb, XZ);
+      return true;
+    });
+  };
+  auto gather = [&](auto sc, double (&Y)[NB][2]) {
+    constexpr int sl = decltype(sc)::value;
+#pragma unroll
+    for (int l = 0; l <= S; ++l) {
+      Y[l][0] = XP[l][sl][0];
+      Y[l][1] = XP[l][sl][1];
+    }
+#pragma unroll
+    for (int l = 0; l < S; ++l) {
+      Y[S + 1 + l][0] = XZ[l][sl][0];
+      Y[S + 1 + l][1] = XZ[l][sl][1];
+    }
+  };
+
+  if constexpr (ROLE == 0) {
+    // ---- producer: rows mfirst .. mlast of (p_b, z_b); at step m the basis of row g1 = m - S is
+    // complete: the new (p, z) of rows i0 - S .. i1 + S into the ring, w and block b's norms on the
+    // owned rows
+    auto fetch = [&](int m, CaFRow<T>& b) {
+      const int mc = min(max(m, 1 - F.gh), G.nx + F.gh);
+      ca_load2<T>(pin + int64_t(mc) * P, c0, cmax, b.p);
+      ca_load2<T>(zin + int64_t(mc) * P, c0, cmax, b.z);
+      const int wc = min(max(m - S, 1 - F.gh), G.nx + F.gh);
+      ca_load2<T>(w + int64_t(wc) * P, c0, cmax, b.w);
+    };
+    auto core = [&](auto qc, int m, const CaFRow<T>& cur) {
+      constexpr int q = decltype(qc)::value;
+      ch[q] = ca_row_cls(ctbl, m);
+      const bool rin = FAST || interior_row(m);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bool in = FAST || (rin && colin[u]);
+        XP[0][q][u] = in ? double(cur.p[u]) : 0.0;
+        XZ[0][q][u] = in ? double(cur.z[u]) : 0.0;
+      }
+      chains(qc, m);
+      const int g1 = m - S;
+      if (g1 < i0 - S) return;
+      double Y[NB][2];
+      gather(std::integral_constant<int, (q - S) & 3>{}, Y);
+      T pn[2], zn[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        double sp = 0.0, sz = 0.0;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          sp = __builtin_fma(ca[i], Y[i][u], sp);
+          sz = __builtin_fma(cb[i], Y[i][u], sz);
+        }
+        pn[u] = static_cast<T>(sp);
+        zn[u] = static_cast<T>(sz);
+      }
+      double* sl = ring + (q & 1) * 256;
+      *reinterpret_cast<d2*>(sl + 2 * lane) = d2{double(pn[0]), double(pn[1])};
+      *reinterpret_cast<d2*>(sl + 128 + 2 * lane) = d2{double(zn[0]), double(zn[1])};
+      if (g1 < i0 || g1 > i1) return;
+      // an owned row: w, the stores and block b's ||p_{k+j}||^2
+      T wn[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        double sw = double(cur.w[u]);
+#pragma unroll
+        for (int i = 0; i < NB; ++i) sw = __builtin_fma(cc[i], Y[i][u], sw);
+        wn[u] = static_cast<T>(sw);
+        if (FAST || own[u]) {
+          nacc[0] = __builtin_fma(Y[0][u], Y[0][u], nacc[0]);
+#pragma unroll
+          for (int j = 1; j < S; ++j) {
+            double v = 0.0;
+#pragma unroll
+            for (int i = 0; i <= j; ++i) v = __builtin_fma(pa[j][i], Y[i][u], v);
+#pragma unroll
+            for (int i = 0; i < j; ++i) v = __builtin_fma(pa[j][S + 1 + i], Y[S + 1 + i][u], v);
+            nacc[j] = __builtin_fma(v, v, nacc[j]);
+          }
+        }
+      }
+      if (FAST ? own_all : own_any) {
+        const int64_t o = int64_t(g1) * P;
+        ca_store2<T>(pout + o, c0, pn, FAST || own_all, own);
+        ca_store2<T>(zout + o, c0, zn, FAST || own_all, own);
+        ca_store2<T>(w + o, c0, wn, FAST || own_all, own);
+      }
+    };
+    static_assert(PF == 1 || PF == 3, "ca_march_fused: prefetch depth 1 or 3");
+    constexpr int NBUF = PF + 1;
+    CaFRow<T> buf[NBUF];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) fetch(min(mfirst + q, mlast), buf[q]);
+    bool more = true;
+    for (int m = mfirst; more && m <= mlast; m += 4) {
+      more = static_for_while<4>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        if (m + q > mlast) return false;
+        fetch(min(m + q + PF, mlast), buf[(q + PF) % NBUF]);
+        core(qc, m + q, buf[q % NBUF]);
+        sync();  // the row is in the ring; the consumer has read the slot the next step rewrites
+        return true;
+      });
+    }
+    if constexpr (FAST) {
+#pragma unroll
+      for (int j = 0; j < S; ++j) nacc[j] = own_all ? nacc[j] : 0.0;
+    }
+  } else {
+    // ---- consumer: after the producer's step m, row g1 = m - S of the new (p, z) is in the ring: block
+    // b+1's basis from it (exactly as pass 1 would build it from the stored values) and, S rows
+    // behind, the Gram products of the owned rows
+    auto core = [&](auto qc, int m) {
+      constexpr int q = decltype(qc)::value;
+      const int g1 = m - S;
+      if (g1 < i0 - S) return;
+      constexpr int s1 = (q - S) & 3;
+      const double* sl = ring + (q & 1) * 256;
+      const d2 pv = *reinterpret_cast<const d2*>(sl + 2 * lane);
+      const d2 zv = *reinterpret_cast<const d2*>(sl + 128 + 2 * lane);
+      ch[s1] = ca_row_cls(ctbl, g1);
+      XP[0][s1][0] = pv.x;
+      XP[0][s1][1] = pv.y;
+      XZ[0][s1][0] = zv.x;
+      XZ[0][s1][1] = zv.y;
+      chains(std::integral_constant<int, s1>{}, g1);
+      const int g2 = g1 - S;
+      if (g2 < i0) return;
+      constexpr int s2 = (q - 2 * S) & 3;
+      double Y2[NB][2];
+      gather(std::integral_constant<int, s2>{}, Y2);
+      double d[2];
+      ca_diag(ch[s2], g2, K, G, F, c0, cmax, d);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        if (!(FAST || own[u])) continue;
+#pragma unroll
+        for (int qq = 0; qq < Sh::NQ; ++qq)
+          acc[qq] = __builtin_fma(Y2[ca_prod_i<S>(qq)][u], d[u] * Y2[ca_prod_j<S>(qq)][u], acc[qq]);
+      }
+    };
+    bool more = true;
+    for (int m = mfirst; more && m <= mlast; m += 4) {
+      more = static_for_while<4>([&](auto qc) {
+        constexpr int q = decltype(qc)::value;
+        if (m + q > mlast) return false;
+        sync();
+        core(qc, m + q);
+        return true;
+      });
+    }
+    if constexpr (FAST) {
+#pragma unroll
+      for (int q = 0; q < Sh::NQ; ++q) acc[q] = own_all ? acc[q] : 0.0;
+    }
+  }
+}
+
+#ifndef PMX_CA_PF_FUSE
+#define PMX_CA_PF_FUSE 1
+#endif
+
+// The fused pass (see ca_march_fused): one workgroup of two waves per tile.  After the reduction of
+// block b (CaState::nupd > 0) it applies block b and sums block b+1's Gram products; after a reduction
+// that stopped inside block b - 1 (nupd < 0) wave 0 rewinds w, as pass 2 would.  Partials: the Gram
+// products q at [q][tile] (wave 1), block b's norms j at NQ * ntiles + [j][tile] (wave 0): the
+// reduction's n = n2 = ntiles.
+template <typename T, int S, int MW, int PART>
+__global__ void __launch_bounds__(128, MW)
+k_ca_fused(DevGeom G, T* w, T* z0, T* z1, T* p0, T* p1, double* __restrict__ partials, const CaState* C, int TI,
+           int tiles_j, const unsigned* __restrict__ ctbl, int cwords, CaFaces faces, CaPart part, int ntiles) {
+  using Sh = CaShape<S>;
+  using Fs = CaFuseShape<S>;
+  constexpr int NB = Sh::NB;
+  typedef const __attribute__((address_space(4))) CaState CCS;
+  const long long blk = ((CCS*)C)->blk;  // NOLINT
+  const int nupd = ((CCS*)C)->nupd;      // NOLINT
+  if (nupd == 0) return;
+  const int role = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6);
+  double ca[NB], cb[NB], cc[NB], pa[S][NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    ca[i] = ((CCS*)C)->coef[0][i];  // NOLINT
+    cb[i] = ((CCS*)C)->coef[1][i];  // NOLINT
+    cc[i] = ((CCS*)C)->coef[2][i];  // NOLINT
+#pragma unroll
+    for (int j = 0; j < S; ++j) pa[j][i] = ((CCS*)C)->pa[j][i];  // NOLINT
+  }
+  int ti = 0, tj = 0;
+  ca_part_tile(xcd_remap(blockIdx.x, gridDim.x), part, tiles_j, ti, tj);
+  const int id = ti * tiles_j + tj;
+  const int i0 = 1 + ti * TI, i1 = min(i0 + TI - 1, G.nx);
+  const int j0 = 1 + tj * Fs::WO, j1 = min(j0 + Fs::WO - 1, G.ny);
+  // the reduction advanced blk: block b's (p, z) are set (blk - 1) & 1 (a rewind leaves blk alone)
+  const int in = int((blk - 1) & 1);
+  T* pin = in ? p1 : p0;
+  T* zin = in ? z1 : z0;
+  T* pout = in ? p0 : p1;
+  T* zout = in ? z0 : z1;
+  const CaK K = ca_consts(G);
+  const int lane = threadIdx.x & 63;
+  const unsigned* tbl = ctbl + int64_t(tj) * cwords;
+  const bool fast = PART == 1 || (j1 == j0 + Fs::WO - 1 && G.gi0 + i0 - 2 * S >= 1 && G.gi0 + i1 + 2 * S <= G.M - 1 &&
+                                   G.gj0 + j0 - Fs::HE >= 1 && G.gj0 + j0 - Fs::HE + 127 <= G.N - 1);
+  double acc[Sh::NQ], nacc[S];
+#pragma unroll
+  for (int q = 0; q < Sh::NQ; ++q) acc[q] = 0.0;
+#pragma unroll
+  for (int j = 0; j < S; ++j) nacc[j] = 0.0;
+  if (nupd < 0) {  // rewind: w only, by wave 0 (no barrier on this path)
+    if (role != 0) return;
+    double pz[S][NB] = {};
+    if (PART == 1 || fast)
+      ca_march<T, S, true, true, kCaPfUpd, true, 0, Fs::HE>(G, DevTables{}, K, pin, zin, pout, zout, w, i0, i1, j0, j1,
+                                                            tbl, faces, acc, ca, cb, cc, pz);
+    else if constexpr (PART != 1)
+      ca_march<T, S, true, false, kCaPfUpd, true, 0, Fs::HE>(G, DevTables{}, K, pin, zin, pout, zout, w, i0, i1, j0,
+                                                             j1, tbl, faces, acc, ca, cb, cc, pz);
+    return;
+  }
+  __shared__ double ring[2 * 256];
+  constexpr int PF = PMX_CA_PF_FUSE;
+#define PMX_CAF_MARCH(FA, R)                                                                                        \
+  ca_march_fused<T, S, FA, PF, R>(G, K, pin, zin, pout, zout, w, i0, i1, j0, j1, tbl, faces, acc, nacc, ca, cb, cc, \
+                                  pa, ring)
+  if (role == 0) {
+    if (PART == 1 || fast) PMX_CAF_MARCH(true, 0);
+    else if constexpr (PART != 1) PMX_CAF_MARCH(false, 0);
+#pragma unroll
+    for (int j = 0; j + 1 < S; j += 2) wave_sum2_mfma(nacc[j], nacc[j + 1]);
+    if constexpr (S & 1) nacc[S - 1] = wave_sum_mfma(nacc[S - 1]);
+    if (lane == 0) {
+#pragma unroll
+      for (int j = 0; j < S; ++j) partials[int64_t(Sh::NQ + j) * ntiles + id] = nacc[j];
+    }
+  } else {
+    if (PART == 1 || fast) PMX_CAF_MARCH(true, 1);
+    else if constexpr (PART != 1) PMX_CAF_MARCH(false, 1);
+#pragma unroll
+    for (int q = 0; q + 1 < Sh::NQ; q += 2) wave_sum2_mfma(acc[q], acc[q + 1]);
+    if constexpr (Sh::NQ & 1) acc[Sh::NQ - 1] = wave_sum_mfma(acc[Sh::NQ - 1]);
+    if (lane == 0) {
+#pragma unroll
+      for (int q = 0; q < Sh::NQ; ++q) partials[int64_t(q) * ntiles + id] = acc[q];
+    }
+  }
+#undef PMX_CAF_MARCH
+}
+
 // Row classes of every tile column (one thread per 16-row word): 2 bits per local row, over the
 // columns the tile loads, as pcg1's k_pcg1_tile_classes.
 __global__ void k_ca_row_classes(DevGeom G, DevTables Tb, int he, int wo, int tiles_j, int cwords, unsigned* out) {
@@ -901,7 +1250,7 @@ k_ca_finish(double h, double wdiff, int nmax, int check_only, PcgState* St, CaSt
 
 }  // namespace
 
-CaTiles make_ca_tiles(const DevGeom& G, int s, int rows, int rows2) {
+CaTiles make_ca_tiles(const DevGeom& G, int s, int rows, int rows2, int rows_f) {
   PMX_CHECK(s == 2 || s == 3, "s-step PCG: s must be 2 or 3");
   CaTiles t;
   t.s = s;
@@ -942,7 +1291,9 @@ CaTiles make_ca_tiles(const DevGeom& G, int s, int rows, int rows2) {
   t.tj_lo = std::min(1, t.tiles_j);
   t.tj_hi = std::max(t.tj_lo, std::min(t.tiles_j, (G.ny - 128 + t.he) / t.wo + 1));
   auto rect = [&](int r, int tiles_i, int& lo, int& hi) {
-    lo = std::min(1, tiles_i);
+    // i0 - s >= 1: with tiles shorter than s the interior starts further down, so no interior tile
+    // reads a ghost row (they do not wait for the ghost exchange on strips)
+    lo = std::min((s + r - 1) / r, tiles_i);
     hi = std::max(lo, std::min(tiles_i, (G.nx - s) / r));
     if (hi <= lo || t.tj_hi <= t.tj_lo) { lo = hi = 0; return; }
     for (int ti = 0; ti < tiles_i; ++ti)
@@ -954,16 +1305,52 @@ CaTiles make_ca_tiles(const DevGeom& G, int s, int rows, int rows2) {
   rect(rows, t.tiles_i, t.ti_lo, t.ti_hi);
   rect(rows2, t.tiles_i2, t.ti_lo2, t.ti_hi2);
   if (t.ti_hi <= t.ti_lo || t.ti_hi2 <= t.ti_lo2) t.split = t.split_upd = 0;
-  t.cwords = (G.nx + 2 * s + 2 * kCaRowOff + 15) / 16 + 1;
+  // rows up to nx + 2s (the fused march's lowest loaded row), 16 per word from row -kCaRowOff
+  t.cwords = (G.nx + 4 * s + 2 * kCaRowOff + 15) / 16 + 1;
+  // the fused tiling: radius 2s (he_f = 2s columns per side), rows_f rows.  Auto: 64 (16384^2 at 3
+  // waves per SIMD, ms/iteration: 16 rows 1.41, 32 1.13, 64 1.01), halved while the grid has fewer
+  // than ~6 rounds of tiles (1536 two-wave workgroups at a time)
+  t.he_f = 2 * s;
+  t.wo_f = 128 - 2 * t.he_f;
+  t.tiles_j_f = (G.ny + t.wo_f - 1) / t.wo_f;
+  if (rows_f <= 0) {
+    rows_f = 64;
+    while (rows_f > 16 && int64_t((G.nx + rows_f - 1) / rows_f) * t.tiles_j_f < 9216) rows_f /= 2;
+  }
+  PMX_CHECK(rows_f >= 1 && rows_f <= 4096, "s-step PCG: fused tile rows must be in [1, 4096]");
+  t.rows_f = rows_f;
+  t.tiles_i_f = (G.nx + rows_f - 1) / rows_f;
+  {
+    const int r = 2 * s;  // the fused kernel's radius
+    auto fastf = [&](int ti, int tj) {
+      const int i0 = 1 + ti * rows_f, i1 = std::min(i0 + rows_f - 1, G.nx);
+      const int j0 = 1 + tj * t.wo_f, j1 = std::min(j0 + t.wo_f - 1, G.ny);
+      return j1 == j0 + t.wo_f - 1 && G.gi0 + i0 - r >= 1 && G.gi0 + i1 + r <= G.M - 1 && G.gj0 + j0 - t.he_f >= 1 &&
+             G.gj0 + j0 - t.he_f + 127 <= G.N - 1;
+    };
+    t.tj_lo_f = std::min(1, t.tiles_j_f);
+    t.tj_hi_f = std::max(t.tj_lo_f, std::min(t.tiles_j_f, (G.ny - 128 + t.he_f) / t.wo_f + 1));
+    t.ti_lo_f = std::min((r + rows_f - 1) / rows_f, t.tiles_i_f);  // i0 - r >= 1
+    t.ti_hi_f = std::max(t.ti_lo_f, std::min(t.tiles_i_f, (G.nx - r) / rows_f));
+    if (t.ti_hi_f <= t.ti_lo_f || t.tj_hi_f <= t.tj_lo_f) {
+      t.ti_lo_f = t.ti_hi_f = t.tj_lo_f = t.tj_hi_f = 0;
+      t.split_f = 0;
+    }
+    for (int ti = t.ti_lo_f; ti < t.ti_hi_f; ++ti)
+      for (int tj = t.tj_lo_f; tj < t.tj_hi_f; ++tj)
+        PMX_CHECK(fastf(ti, tj), "s-step PCG: interior fused tile (" << ti << ", " << tj << ") is not fast");
+  }
   return t;
 }
 
 int ca_nq(int s) { return s == 2 ? CaShape<2>::NQ + CaShape<2>::NN : CaShape<3>::NQ + CaShape<3>::NN; }
 
-void ca_build_classes(const DevGeom& G, const DevTables& Tb, const CaTiles& t, unsigned* tbl, hipStream_t s) {
-  const int n = t.tiles_j * t.cwords;
-  hipLaunchKernelGGL(k_ca_row_classes, dim3((n + 255) / 256), dim3(256), 0, s, G, Tb, t.he, t.wo, t.tiles_j,
-                     t.cwords, tbl);
+void ca_build_classes(const DevGeom& G, const DevTables& Tb, const CaTiles& t, unsigned* tbl, hipStream_t s,
+                      bool fused) {
+  const int tj = fused ? t.tiles_j_f : t.tiles_j;
+  const int n = tj * t.cwords;
+  hipLaunchKernelGGL(k_ca_row_classes, dim3((n + 255) / 256), dim3(256), 0, s, G, Tb, fused ? t.he_f : t.he,
+                     fused ? t.wo_f : t.wo, tj, t.cwords, tbl);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1034,6 +1421,41 @@ void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, 
   HIP_CHECK(hipGetLastError());
 }
 
+template <typename T>
+void launch_ca_fused(const DevGeom& G, T* w, T* z0, T* z1, T* p0, T* p1, double* partials, const CaState* C,
+                     const CaTiles& t, hipStream_t s, hipStream_t sframe) {
+  PMX_CHECK(G.nb == 0, "the fused s-step pass runs undecomposed grids");
+  PMX_CHECK(t.fuse && t.tbl_f != nullptr && t.fa != nullptr && t.fb != nullptr,
+            "s-step PCG: fused tiling / row classes / face tables missing");
+  if (!sframe) sframe = s;
+  const int n = t.ntilesf();
+  const int nin = (t.ti_hi_f - t.ti_lo_f) * (t.tj_hi_f - t.tj_lo_f);
+  const CaFaces F{t.fa, t.fb, t.gh};
+  const CaPart P1{1, t.tiles_i_f, t.ti_lo_f, t.ti_hi_f, t.tj_lo_f, t.tj_hi_f},
+      P2{2, t.tiles_i_f, t.ti_lo_f, t.ti_hi_f, t.tj_lo_f, t.tj_hi_f}, P0{0, t.tiles_i_f, 0, 0, 0, 0};
+#define PMX_CAF_K(SS, MW, PT, PP, NB)                                                                             \
+  do {                                                                                                            \
+    if ((NB) > 0)                                                                                                 \
+      hipLaunchKernelGGL((k_ca_fused<T, SS, MW, PT>), dim3(NB), dim3(128), 0, (PT) == 2 ? sframe : s, G, w, z0, z1, \
+                         p0, p1, partials, C, t.rows_f, t.tiles_j_f, t.tbl_f, t.cwords, F, PP, n);                 \
+  } while (0)
+#define PMX_CAF(SS)                                     \
+  do {                                                  \
+    if (t.split_f && nin > 0) {                         \
+      PMX_CAF_K(SS, 2, 2, P2, n - nin);                 \
+      if (t.waves_f == 3) PMX_CAF_K(SS, 3, 1, P1, nin); \
+      else PMX_CAF_K(SS, 2, 1, P1, nin);                \
+    } else {                                            \
+      PMX_CAF_K(SS, 2, 0, P0, n);                       \
+    }                                                   \
+  } while (0)
+  if (t.s == 2) PMX_CAF(2);
+  else PMX_CAF(3);
+#undef PMX_CAF
+#undef PMX_CAF_K
+  HIP_CHECK(hipGetLastError());
+}
+
 void launch_ca_reduce(const double* partials, int n, int n2, int s_, double h, double wdiff, int nmax,
                       bool check_only, PcgState* S, CaState* C, double* chunk, hipStream_t s, long long* progress,
                       bool finish) {
@@ -1063,5 +1485,7 @@ template void launch_ca_init<double>(const DevGeom&, const DevTables&, double*, 
 template void launch_ca_sweep<double>(const DevGeom&, const DevTables&, double*, double*, double*, double*, double*,
                                       double*, const PcgState*, const CaState*, const CaTiles&, bool, hipStream_t,
                                       hipStream_t);
+template void launch_ca_fused<double>(const DevGeom&, double*, double*, double*, double*, double*, double*,
+                                      const CaState*, const CaTiles&, hipStream_t, hipStream_t);
 
 }  // namespace pmx

@@ -122,6 +122,10 @@ GpuOptions resolve_options(const GpuOptions& in) {
   env_int("PMX_CA_SPLIT", o.ca_split);
   env_int("PMX_CA_SPLIT_UPD", o.ca_split_upd);
   env_int("PMX_CA_FRAME_STREAM", o.ca_frame_stream);
+  env_int("PMX_CA_FUSE", o.ca_fuse);
+  env_int("PMX_CA_ROWS_F", o.ca_rows_f);
+  PMX_CHECK(o.ca_fuse >= -1 && o.ca_fuse <= 1, "s-step PCG: ca_fuse must be -1, 0 or 1");
+  PMX_CHECK(o.ca_rows_f >= 0 && o.ca_rows_f <= 4096, "s-step PCG: fused tile rows must be 0 (auto) .. 4096");
   env_int("PMX_CA_DIRICHLET", o.ca_dirichlet);
   if (const char* pk = std::getenv("PMX_PLACEMENT_PICK"); pk && pk[0]) o.placement_pick = std::string(pk) == "slowest" ? 1 : 0;
   PMX_CHECK(o.ca_split >= -1 && o.ca_split <= 1, "s-step PCG: ca_split must be -1, 0 or 1");
@@ -354,7 +358,12 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
 
   if (ca_) {
     r2_ = field_raw(4);  // the second z buffer
-    ca_tiles_ = make_ca_tiles(ca_geom_, opt_.ca_s, opt_.ca_rows, opt_.ca_rows2);
+    ca_tiles_ = make_ca_tiles(ca_geom_, opt_.ca_s, opt_.ca_rows, opt_.ca_rows2, opt_.ca_rows_f);
+    // the fused pass: undecomposed grids (a strip's ghost rows hold radius s, the fused march reads 2s)
+    PMX_CHECK(opt_.ca_fuse != 1 || geom_.nb == 0, "the fused s-step pass runs undecomposed grids");
+    ca_tiles_.fuse = opt_.ca_fuse == 1 || (opt_.ca_fuse == -1 && geom_.nb == 0) ? 1 : 0;
+    if (const char* e = std::getenv("PMX_CA_WAVES_F"); e && e[0]) ca_tiles_.waves_f = std::atoi(e);
+    if (const char* e = std::getenv("PMX_CA_SPLIT_F"); e && e[0]) ca_tiles_.split_f = std::atoi(e);
     // the face coefficients of every node, read on the rows the ellipse cuts (2 more field-sized arrays)
     HIP_CHECK(hipMalloc(&ca_faces_, 2 * field_bytes_));
     ca_tiles_.fa = reinterpret_cast<const double*>(ca_faces_ + field_off_ * elem_);
@@ -376,6 +385,11 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     HIP_CHECK(hipMalloc(&ca_tbl_, size_t(ca_tiles_.tiles_j) * ca_tiles_.cwords * sizeof(unsigned)));
     ca_tiles_.tbl = ca_tbl_;
     ca_build_classes(ca_geom_, ca_tables_, ca_tiles_, ca_tbl_, nullptr);
+    if (ca_tiles_.fuse) {
+      HIP_CHECK(hipMalloc(&ca_tbl_f_, size_t(ca_tiles_.tiles_j_f) * ca_tiles_.cwords * sizeof(unsigned)));
+      ca_tiles_.tbl_f = ca_tbl_f_;
+      ca_build_classes(ca_geom_, ca_tables_, ca_tiles_, ca_tbl_f_, nullptr, true);
+    }
     HIP_CHECK(hipStreamSynchronize(nullptr));
     HIP_CHECK(hipMalloc(&ca_state_, sizeof(CaState)));
     HIP_CHECK(hipMemset(ca_state_, 0, sizeof(CaState)));
@@ -384,8 +398,9 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   init_tiles_ = make_tiles(G, 256, 0);
   // partials: 5 doubles per slot (the s-step Gram partials take ca_nq per tile)
   const int ca_slots =
-      ca_ ? int((int64_t(ca_tiles_.ntiles()) * (ca_nq(ca_tiles_.s) - ca_tiles_.s) +
-                 int64_t(ca_tiles_.ntiles2()) * ca_tiles_.s + 4) / 5)
+      ca_ ? int((std::max(int64_t(ca_tiles_.ntiles()) * (ca_nq(ca_tiles_.s) - ca_tiles_.s) +
+                              int64_t(ca_tiles_.ntiles2()) * ca_tiles_.s,
+                          int64_t(ca_tiles_.fuse ? ca_tiles_.ntilesf() : 0) * ca_nq(ca_tiles_.s)) + 4) / 5)
           : 0;
   const size_t npart = size_t(std::max({tiles_.ntiles(), tiles_b_.ntiles(), init_tiles_.ntiles(),
                                         pcg1_ ? std::max(tiles1_.ntiles(), tiles1w_.ntiles()) : 0, ca_slots}));
@@ -574,6 +589,8 @@ void GpuSubdomainSolver::release() noexcept {
   if (tile_order_) (void)hipFree(tile_order_);
   if (tile_order_w_) (void)hipFree(tile_order_w_);
   if (ca_tbl_) (void)hipFree(ca_tbl_);
+  if (ca_tbl_f_) (void)hipFree(ca_tbl_f_);
+  ca_tbl_f_ = nullptr;
   if (ca_faces_) (void)hipFree(ca_faces_);
   if (ca_side_) (void)hipStreamDestroy(ca_side_);
   if (ca_ev_fork_) (void)hipEventDestroy(ca_ev_fork_);
@@ -726,15 +743,49 @@ void GpuSubdomainSolver::ca_sweep(hipStream_t s, bool upd) {
   after_launch(s);
 }
 
+void GpuSubdomainSolver::drop_side_stream() {
+  if (!ca_side_) return;
+  HIP_CHECK(hipSetDevice(opt_.device));
+  HIP_CHECK(hipStreamSynchronize(ca_side_));
+  HIP_CHECK(hipStreamDestroy(ca_side_));
+  HIP_CHECK(hipEventDestroy(ca_ev_fork_));
+  HIP_CHECK(hipEventDestroy(ca_ev_join_));
+  ca_side_ = nullptr;
+  ca_ev_fork_ = ca_ev_join_ = nullptr;
+}
+
 void GpuSubdomainSolver::enqueue_ca_pass(hipStream_t s, bool upd) {
   PMX_CHECK(ca_ && elem_ == 8, "not an s-step solver");
   ca_sweep(s, upd);
 }
 
-void GpuSubdomainSolver::enqueue_ca_reduce(hipStream_t s, int n, bool check_only, bool finish) {
+void GpuSubdomainSolver::enqueue_ca_fused(hipStream_t s) {
+  PMX_CHECK(ca_fused() && elem_ == 8, "not an s-step solver with the fused pass");
+  double* w = static_cast<double*>(field_base(0));
+  double* z0 = static_cast<double*>(field_base(1));
+  double* z1 = reinterpret_cast<double*>(r2_ + field_off_ * elem_);
+  double* p0 = static_cast<double*>(field_base(2));
+  double* p1 = static_cast<double*>(field_base(3));
+  if (ca_side_) {  // the frame tiles on the side stream, as ca_sweep
+    HIP_CHECK(hipEventRecord(ca_ev_fork_, s));
+    HIP_CHECK(hipStreamWaitEvent(ca_side_, ca_ev_fork_, 0));
+    launch_ca_fused<double>(ca_geom_, w, z0, z1, p0, p1, partials_, ca_state_, ca_tiles_, s, ca_side_);
+    HIP_CHECK(hipEventRecord(ca_ev_join_, ca_side_));
+    HIP_CHECK(hipStreamWaitEvent(s, ca_ev_join_, 0));
+  } else {
+    launch_ca_fused<double>(ca_geom_, w, z0, z1, p0, p1, partials_, ca_state_, ca_tiles_, s);
+  }
+  after_launch(s);
+}
+
+void GpuSubdomainSolver::enqueue_ca_reduce(hipStream_t s, int n, bool check_only, bool finish, bool fused) {
   PMX_CHECK(ca_ && elem_ == 8, "not an s-step solver");
+  PMX_CHECK(!fused || ca_fused(), "fused reduction without the fused pass");
   const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
-  launch_ca_reduce(partials_, ca_tiles_.ntiles(), ca_tiles_.ntiles2(), ca_tiles_.s, g_.h1h2, wdiff,
+  // after the fused pass both the Gram products and the norms come from its tiling
+  const int n1 = fused ? ca_tiles_.ntilesf() : ca_tiles_.ntiles();
+  const int n2 = fused ? ca_tiles_.ntilesf() : ca_tiles_.ntiles2();
+  launch_ca_reduce(partials_, n1, n2, ca_tiles_.s, g_.h1h2, wdiff,
                    check_only ? 1 : n, check_only, state_, ca_state_, ca_chunk_, s, progress_dev_, finish);
   after_launch(s);
   if (!check_only) {  // a block the device applies (unless it stopped): the set its pass 2 writes
@@ -750,15 +801,24 @@ void GpuSubdomainSolver::enqueue_ca_finish(hipStream_t s, int n, bool check_only
   after_launch(s);
 }
 
-void GpuSubdomainSolver::enqueue_ca_block(hipStream_t s, int n) {
+void GpuSubdomainSolver::enqueue_ca_block(hipStream_t s, int n, bool first) {
   PMX_CHECK(geom_.nb == 0, "enqueue_ca_block: undecomposed grids (the driver runs the steps otherwise)");
-  enqueue_ca_pass(s, false);
-  enqueue_ca_reduce(s, n, false, true);
-  enqueue_ca_pass(s, true);
+  if (!ca_fused()) {
+    enqueue_ca_pass(s, false);
+    enqueue_ca_reduce(s, n, false, true);
+    enqueue_ca_pass(s, true);
+    return;
+  }
+  // fused schedule: pass 1 (first block of a batch) or the fused pass (which applies the previous
+  // block), then the reduction; the last block's pass 2 runs in enqueue_ca_check
+  if (first) enqueue_ca_pass(s, false);
+  else enqueue_ca_fused(s);
+  enqueue_ca_reduce(s, n, false, true, !first);
 }
 
 void GpuSubdomainSolver::enqueue_ca_check(hipStream_t s) {
   PMX_CHECK(geom_.nb == 0, "enqueue_ca_check: undecomposed grids (the driver runs the steps otherwise)");
+  if (ca_fused()) enqueue_ca_pass(s, true);  // the batch's last block
   enqueue_ca_reduce(s, 1, true, true);
   // a stop inside the last block rewinds w (every workgroup returns at once otherwise)
   enqueue_ca_pass(s, true);
@@ -1210,10 +1270,16 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
   // concurrently resident streams.
   if (const char* q = std::getenv("GPU_MAX_HW_QUEUES"); q && std::atoi(q) == 1) {
     const char* keep = std::getenv("PMX_FORK_ONE_QUEUE");
-    if (keep && keep[0] == '1')
-      graph_failed_ = overlap_;  // forked schedule, eager launches
-    else
+    if (keep && keep[0] == '1') {
+      bool forked = overlap_;
+      for (auto* s : local_) forked |= s->ca_side_stream();
+      graph_failed_ = forked;  // forked schedule, eager launches
+    } else {
       overlap_ = false;
+      // the s-step passes fork their frame tiles onto a side stream inside every block: run them
+      // in-stream instead (a forked graph on one queue is the crashing configuration)
+      for (auto* s : local_) s->drop_side_stream();
+    }
   }
   const char* env = std::getenv("PMX_POISON_HALOS");
   poison_ = any_nb && (local_[0]->options().poison_halos || (env && env[0] == '1'));
@@ -1430,9 +1496,11 @@ void PcgDriver::enqueue_ca(int64_t n) {
   HIP_CHECK(hipSetDevice(local_[0]->device()));
   if (n <= 0) return;
   if (!any_nb_ && local_.size() == 1 && comm_->world_size() == 1) {
+    bool first = true;
     while (n > 0) {
       const int m = int(std::min<int64_t>(s, n));
-      local_[0]->enqueue_ca_block(streams_[0], m);
+      local_[0]->enqueue_ca_block(streams_[0], m, first);
+      first = false;
       n -= m;
     }
     // the last block's stop test (and its rewind): the state is exact at every batch boundary

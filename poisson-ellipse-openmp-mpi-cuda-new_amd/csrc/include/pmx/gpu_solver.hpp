@@ -94,6 +94,10 @@ struct GpuOptions {
   int ca_split_upd = 0;
   // ... the frame kernel on a side stream, overlapping the interior (1), or after it (0).  PMX_CA_FRAME_STREAM.
   int ca_frame_stream = 1;
+  // s-step: pass 2 of block b and pass 1 of block b+1 as ONE fused pass (k_ca_fused, 48 instead of 64
+  // B/pt per block) between the first pass 1 and the last pass 2 of every batch: 1 on, 0 off, -1 auto
+  // (undecomposed grids).  ca_rows_f: its tile rows (0 = auto).
+  int ca_fuse = -1, ca_rows_f = 0;
   // s-step kernels see the subdomain's ghost rows as a Dirichlet boundary (nb = 0) while the driver
   // keeps the decomposed schedule: the loopback rehearsal, whose zero ghosts would otherwise break
   // the basis recurrence (its redundant ghost-row levels need the neighbour's real rows).  Set by the
@@ -266,6 +270,10 @@ class GpuSubdomainSolver {
   // that read ghost rows) after event e -- the ghost exchange on the driver's comm stream.  Without a
   // frame stream the whole pass waits.  One-shot.
   void set_ca_frame_wait(hipEvent_t e) { ca_frame_wait_ = e; }
+  // s-step: the frame tiles of a split pass run on a side stream (forked and joined inside every
+  // block); drop_side_stream() runs them in-stream from now on (one hardware queue: no forks)
+  bool ca_side_stream() const { return ca_side_ != nullptr; }
+  void drop_side_stream();
 
   // Checkpoint: the 4 fields with ghosts, the PCG scalars and the halo buffers,
   // i.e. everything the next iteration reads.  Synchronous; written at batch boundaries.
@@ -320,11 +328,17 @@ class GpuSubdomainSolver {
   bool ca() const { return ca_; }
   int ca_s() const { return ca_ ? ca_tiles_.s : 0; }
   const CaTiles& ca_tiles() const { return ca_tiles_; }
-  void enqueue_ca_block(hipStream_t s, int n);
+  // one block of n iterations: pass 1, reduction, pass 2 -- or with the fused pass, `first`: pass 1 +
+  // reduction, else fused pass + reduction (the batch's last pass 2 follows in enqueue_ca_check)
+  void enqueue_ca_block(hipStream_t s, int n, bool first = true);
   // the same block in steps, for decomposed grids (the driver all-reduces CaState::red between
   // reduce and finish, and exchanges the s ghost rows of the new (z, p) set after pass 2)
   void enqueue_ca_pass(hipStream_t s, bool upd);
-  void enqueue_ca_reduce(hipStream_t s, int n, bool check_only, bool finish);
+  // the fused pass (ca_fused()): pass 2 of the block just reduced + pass 1 of the next; its reduction
+  // is enqueue_ca_reduce(.., fused = true)
+  void enqueue_ca_fused(hipStream_t s);
+  bool ca_fused() const { return ca_ && ca_tiles_.fuse != 0; }
+  void enqueue_ca_reduce(hipStream_t s, int n, bool check_only, bool finish, bool fused = false);
   void enqueue_ca_finish(hipStream_t s, int n, bool check_only);
   // host mirror of CaState::blk (blocks enqueued): the (z, p) set the next exchange sends
   long long ca_blocks() const { return ca_blk_; }
@@ -374,6 +388,7 @@ class GpuSubdomainSolver {
   bool ca_ = false;             // s-step PCG
   CaTiles ca_tiles_{};
   unsigned* ca_tbl_ = nullptr;  // its row-class table
+  unsigned* ca_tbl_f_ = nullptr;  // ... of the fused pass's tiling
   char* ca_faces_ = nullptr;    // its face-coefficient fields (a, b)
   hipStream_t ca_side_ = nullptr;  // the frame tiles' stream (split kernels)
   hipEvent_t ca_ev_fork_ = nullptr, ca_ev_join_ = nullptr;

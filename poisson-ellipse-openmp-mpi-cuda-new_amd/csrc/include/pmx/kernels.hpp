@@ -154,12 +154,24 @@ struct CaTiles {
   int dma = 1;         // pass 1: interior tiles prefetch their rows by LDS-DMA (0: registers)
   int waves_gram = 2;  // waves per SIMD the pass-1 registers must allow (2 or 3)
   int waves_upd = 3;   // ... pass 2 (2 or 3)
+  // fused pass (k_ca_fused: pass 2 of block b + pass 1 of block b+1 in one march, radius 2s): its own
+  // tiling of rows_f x wo_f (= 128 - 4 s) tiles, its interior rectangle and its row-class table
+  int fuse = 0;
+  int rows_f = 0, tiles_i_f = 0, tiles_j_f = 0, wo_f = 116, he_f = 6;
+  int ti_lo_f = 0, ti_hi_f = 0, tj_lo_f = 0, tj_hi_f = 0;
+  int split_f = 1;     // interior tiles by the fast-only kernel, the frame by the general one
+  int waves_f = 3;     // waves per SIMD the fused interior kernel's registers must allow (2 or 3)
+  unsigned* tbl_f = nullptr;
   int ntiles() const { return tiles_i * tiles_j; }
   int ntiles2() const { return tiles_i2 * tiles_j; }
+  int ntilesf() const { return tiles_i_f * tiles_j_f; }
 };
-CaTiles make_ca_tiles(const DevGeom& G, int s, int rows, int rows2 = 0);
+// rows_f: the fused tiling's rows (0 = auto)
+CaTiles make_ca_tiles(const DevGeom& G, int s, int rows, int rows2 = 0, int rows_f = 0);
 int ca_nq(int s);  // partials per tile (pass 1's Gram products + pass 2's norms)
-void ca_build_classes(const DevGeom& G, const DevTables& Tb, const CaTiles& t, unsigned* tbl, hipStream_t s);
+// fused: the classes of the fused tiling (t.he_f, t.wo_f, t.tiles_j_f columns) instead of pass 1/2's
+void ca_build_classes(const DevGeom& G, const DevTables& Tb, const CaTiles& t, unsigned* tbl, hipStream_t s,
+                      bool fused = false);
 // fa / fb: local (0, 0) of two field-sized arrays (rows -1 .. nx+2 allocated)
 void ca_build_faces(const DevGeom& G, const DevTables& Tb, double* fa, double* fb, int gh, hipStream_t s);
 // z = D^-1 r in place, p = z (the first block's set 0)
@@ -170,6 +182,12 @@ template <typename T>
 void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, T* p0, T* p1, double* partials,
                      const PcgState* S, const CaState* C, const CaTiles& t, bool upd, hipStream_t s,
                      hipStream_t sframe = nullptr);
+// the fused pass (undecomposed grids, t.fuse): after the reduction of block b, block b's update and
+// block b+1's Gram partials (the reduction then takes n = n2 = t.ntilesf()); a pending rewind instead
+// rewinds w.  t.tbl_f: the fused tiling's row classes (ca_build_classes with fused = true).
+template <typename T>
+void launch_ca_fused(const DevGeom& G, T* w, T* z0, T* z1, T* p0, T* p1, double* partials, const CaState* C,
+                     const CaTiles& t, hipStream_t s, hipStream_t sframe = nullptr);
 // chunk: kCaReduceMaxBlocks * ca_nq(s) doubles of workspace; nmax: iterations this block may run
 constexpr int kCaReduceMaxBlocks = 256;
 // check_only: the pending stop test alone (after the last block of a batch; pass 2 then rewinds w if
