@@ -113,7 +113,8 @@ def parse(argv=None):
     ap.add_argument("--waves", type=int, default=4, help="wave kernels: wave tiles per workgroup")
     ap.add_argument("--tile-rows", type=int, default=0, help="tile height (0 = auto)")
     ap.add_argument("--algo", default="auto", choices=["auto", "pcg1", "pcg2", "ca"],
-                    help="iteration algorithm: auto (pcg1 / pcg2), or ca = s-step PCG (one GPU, ca_kernels.hip)")
+                    help="iteration algorithm: auto (the library's choice: the s-step PCG on big fp64 grids and "
+                         "row strips where its fields fit, else pcg1 / pcg2), pcg1, pcg2, or ca = the s-step PCG")
     ap.add_argument("--ca-s", type=int, default=3, choices=[2, 3], help="s-step PCG: iterations per block")
     ap.add_argument("--graph-batch", type=int, default=32,
                     help="iterations per captured hipGraph; the timed region replays graphs for any --steps "
@@ -556,8 +557,7 @@ def measure(args) -> int:
         if not share and torch.cuda.device_count() < world:
             raise SystemExit(f"[bench] {world} ranks need {world} visible GPUs, found {torch.cuda.device_count()}")
         torch.cuda.set_device(device)
-    if cfg["split"] is not None and not dry:
-        os.environ["PMX_PCG1_SPLIT"] = str(cfg["split"])  # read by the native driver at construction
+    split_sweep = -1 if cfg["split"] is None else int(cfg["split"])  # pcg1 split sweep of this rung
     overlap = (args.overlap == "on") if cfg["overlap"] is None else cfg["overlap"]
     tdev = "cuda" if info.backend == "nccl" else "cpu"
 
@@ -572,17 +572,18 @@ def measure(args) -> int:
               b_ring=args.b_kernel == "ring")
     pkw = dict(placement=0 if share else args.placement, placement_budget_s=args.placement_budget,
                placement_keep_free=args.placement_keep_free)
-    dkw = dict(kw, **pkw, phase=watch.phase, init_timeout=COMM_INIT_TIMEOUT)
-    # the s-step PCG (ca_kernels.hip) where it applies and wins: fp64 with the fast arithmetic, >= 6M
-    # points (below, pcg1's block tiles win: profiles/r5/ca/small.log), undecomposed or row strips, and
-    # a transport that moves its ghost rows straight between the fields (RCCL or IPC, not torch)
+    dkw = dict(kw, **pkw, phase=watch.phase, init_timeout=COMM_INIT_TIMEOUT, ca_s=args.ca_s,
+               split_sweep=split_sweep)
+    # --algo auto: the library decides (choose_algo) -- the s-step PCG (ca_kernels.hip) where it applies
+    # and wins (fp64 with the fast arithmetic, >= 6M points, undecomposed or row strips on a transport
+    # that moves its ghost rows straight between the fields: RCCL or IPC, not torch) and its 7 fields
+    # fit, else pcg1 / pcg2.  The JSON's config.tile.algo says which ran.
     strips = world == 1 or process_grid(world, args.M, args.N, args.split)[1] == 1
     ca_ok = (args.dtype == "fp64" and not args.exact and strips and
              (world == 1 or cfg["comm"] in ("native", "ipc")))
     if args.algo == "ca" and not ca_ok:
         raise SystemExit("[bench] --algo ca (the s-step PCG) needs fp64, row strips and the RCCL or IPC transport")
-    use_ca = args.algo == "ca" or (args.algo == "auto" and ca_ok and (args.M - 1) * (args.N - 1) >= 6_000_000)
-    algo_id = 3 if use_ca else {"auto": -1, "pcg1": 1, "pcg2": 2}[args.algo]
+    algo_id = {"auto": -1, "pcg1": 1, "pcg2": 2, "ca": 3}[args.algo]
     if dry:
         tp = importlib.import_module(pkg_name + ".models.torch_pcg")
         comm = importlib.import_module(pkg_name + ".parallel.comm")
@@ -802,8 +803,9 @@ def measure_loopback(args) -> int:
     decomp = importlib.import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.parallel.decomp")
     strips = decomp.process_grid(args.gpus, args.M, args.N, args.split)[1] == 1
     ca_ok = args.dtype == "fp64" and not args.exact and strips
-    use_ca = args.algo == "ca" or (args.algo == "auto" and ca_ok and (args.M - 1) * (args.N - 1) >= 6_000_000)
-    algo_id = 3 if use_ca else {"auto": -1, "pcg1": 1, "pcg2": 2, "ca": 3}[args.algo]
+    if args.algo == "ca" and not ca_ok:
+        raise SystemExit("[bench] --algo ca (the s-step PCG) needs fp64 and row strips")
+    algo_id = {"auto": -1, "pcg1": 1, "pcg2": 2, "ca": 3}[args.algo]  # auto: the library's choose_algo
     s = native.Session(problem.to_native(), world=args.gpus, comm="loopback", split=getattr(native.Split, args.split),
                        ranks=[args.loopback_rank], devices=[0], dtype=args.dtype, graph_batch=args.graph_batch,
                        overlap=args.overlap == "on", placement=args.placement,

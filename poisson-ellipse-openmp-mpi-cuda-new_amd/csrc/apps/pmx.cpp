@@ -61,7 +61,8 @@ struct Cli {
                "           [--dump FILE] [--dump-stride S] [--json] [--banner stage0..stage4]\n"
                "           [--profile-phases N] [--check] [--overlap on|off] [--poison-halos]\n"
                "           [--checkpoint FILE [--checkpoint-every K]] [--resume FILE]\n"
-               "           [--sweep-grids MxN,MxN,...] [--sweep-threads T,T,...] [--plan] [--placement K]\n";
+               "           [--sweep-grids MxN,MxN,...] [--sweep-threads T,T,...] [--plan] [--placement K]\n"
+               "           [--algo auto|pcg1|pcg2|ca] [--ca-s 2|3]\n";
   std::exit(msg ? 2 : 0);
 }
 
@@ -140,6 +141,19 @@ Cli parse(int argc, char** argv) {
     else if (a == "--poison-halos") c.opt.poison_halos = true;
     else if (a == "--plan") c.plan = true;
     else if (a == "--placement") c.opt.placement = std::atoi(val().c_str());  // probe K field blocks
+    else if (a == "--algo") {
+      // auto: the s-step PCG on big fp64 grids / row strips when its fields fit, else pcg1 / pcg2
+      // (choose_algo); pcg1 = single pass, pcg2 = two sweeps, ca = the s-step PCG (ca_kernels.hip)
+      const std::string v = val();
+      if (v == "auto") c.opt.algo = -1;
+      else if (v == "pcg1") c.opt.algo = 1;
+      else if (v == "pcg2") c.opt.algo = 2;
+      else if (v == "ca") c.opt.algo = 3;
+      else usage("--algo auto|pcg1|pcg2|ca");
+    } else if (a == "--ca-s") {
+      c.opt.ca_s = std::atoi(val().c_str());
+      if (c.opt.ca_s != 2 && c.opt.ca_s != 3) usage("--ca-s 2|3");
+    }
     else if (a == "--sweep-grids") {
       std::string v = val() + ",";
       for (size_t p = 0, q; (q = v.find(',', p)) != std::string::npos; p = q + 1) {
@@ -248,12 +262,16 @@ int run_plan(const Cli& c) {
             << pg.Py << ", dtype " << dtype_name(c.opt) << "\n"
             << "memory: " << dev_src << "\n";
   const int subs_per_device = c.gpus > 1 ? 1 : ranks;  // LocalComm: every subdomain on one device
-  const bool single_pass = choose_single_pass(s, pg, resolve_options(c.opt), dev_bytes, subs_per_device);
-  std::cout << "iteration: " << (single_pass ? "pcg1 (single pass, 5 fields)" : "pcg2 (two sweeps, 4 fields)") << "\n";
+  const int algo = choose_algo(s, pg, resolve_options(c.opt), dev_bytes, subs_per_device, true);
+  std::cout << "iteration: "
+            << (algo == 3   ? "s-step PCG (ca, s = " + std::to_string(c.opt.ca_s) + ": 5 fields + 2 face fields)"
+                : algo == 1 ? std::string("pcg1 (single pass, 5 fields)")
+                            : std::string("pcg2 (two sweeps, 4 fields)"))
+            << "\n";
   size_t worst = 0;
   for (int r = 0; r < ranks; ++r) {
     const Subdomain sd = decompose_2d(s.M, s.N, pg, r);
-    const size_t b = GpuSubdomainSolver::estimate_device_bytes(s, sd, c.opt.dtype, single_pass);
+    const size_t b = GpuSubdomainSolver::estimate_device_bytes_algo(s, sd, c.opt.dtype, algo);
     worst = std::max(worst, b);
     std::cout << "  rank " << r << ": " << sd.nx << " x " << sd.ny << " nodes, ~" << b / 1e9 << " GB\n";
   }
@@ -262,7 +280,10 @@ int run_plan(const Cli& c) {
   std::cout << "per device: ~" << per_device / 1e9 << " GB -> "
             << (double(per_device) <= dev_bytes ? "fits" : "DOES NOT FIT") << "\n"
             << "largest square grid on " << gpus << " such device(s): ~"
-            << max_square_grid(dev_bytes, gpus, c.opt.dtype) << "^2\n";
+            << max_square_grid(dev_bytes, gpus, c.opt.dtype, 0.1, -1) << "^2 (pcg1)";
+  if (c.opt.dtype == DType::kFp64)
+    std::cout << ", ~" << max_square_grid(dev_bytes, gpus, c.opt.dtype, 0.1, 3) << "^2 with the s-step PCG";
+  std::cout << "\n";
   return double(per_device) <= dev_bytes ? 0 : 4;
 }
 
@@ -325,7 +346,7 @@ int run_hip(Cli& c, double t_prog) {
     const ErrorNorms e = error_norms(s, w);
     JsonLine j;
     j.ks("backend", "hip").kv("M", s.M).kv("N", s.N).kv("ranks", cfg.world).ks("comm", sess.comm_name())
-        .ks("dtype", dtype_name(c.opt)).kv("iters", st.iters)
+        .ks("dtype", dtype_name(c.opt)).ks("algo", sess.algo_name()).kv("iters", st.iters)
         .ks("status", status_name(st.status)).kv("solve_seconds", st.solve_seconds)
         .kv("init_seconds", st.init_seconds)
         .kv("mlups", double(s.M - 1) * (s.N - 1) * st.iters / st.solve_seconds / 1e6)

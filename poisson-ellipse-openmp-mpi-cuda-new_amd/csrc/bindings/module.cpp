@@ -350,8 +350,10 @@ PYBIND11_MODULE(_pmx, m) {
         py::arg("kernel") = "wave", py::arg("exact") = false, py::arg("device") = 0, py::arg("algo") = -1,
         py::arg("sharing") = 1);
   m.def("record_comm_sequence", [](const ProblemSpec& s, int world, Split split, int graph_batch, int64_t iters,
-                                   const std::string& dtype, int device, bool overlap) {
+                                   const std::string& dtype, int device, bool overlap, int algo, int ca_s) {
           GpuOptions o = make_options(device, "wave", 256, 0, 4, 0, dtype, false, graph_batch, false, overlap);
+          o.algo = algo;
+          o.ca_s = ca_s;
           std::vector<std::vector<CommEvent>> logs;
           {
             py::gil_scoped_release nogil;
@@ -367,11 +369,29 @@ PYBIND11_MODULE(_pmx, m) {
           return out;
         }, py::arg("spec"), py::arg("world"), py::arg("split") = Split::kAuto, py::arg("graph_batch") = 4,
         py::arg("iters") = 8, py::arg("dtype") = "fp64", py::arg("device") = 0, py::arg("overlap") = true,
+        py::arg("algo") = -1, py::arg("ca_s") = 3,
         "every rank's communication calls on a recording comm (init + iters iterations, captured when "
         "graph_batch > 0): (comm, op, count, peer, stream) tuples");
-  m.def("max_square_grid", [](double bytes_per_gpu, int gpus, const std::string& dtype, double reserve) {
-    return max_square_grid(bytes_per_gpu, gpus, dtype == "fp64" ? DType::kFp64 : DType::kFp32, reserve);
-  }, py::arg("bytes_per_gpu"), py::arg("gpus"), py::arg("dtype") = "fp64", py::arg("reserve") = 0.1);
+  m.def("max_square_grid", [](double bytes_per_gpu, int gpus, const std::string& dtype, double reserve, int algo) {
+    return max_square_grid(bytes_per_gpu, gpus, dtype == "fp64" ? DType::kFp64 : DType::kFp32, reserve, algo);
+  }, py::arg("bytes_per_gpu"), py::arg("gpus"), py::arg("dtype") = "fp64", py::arg("reserve") = 0.1,
+     py::arg("algo") = -1);
+  // the iteration algorithm a Session would pick (choose_algo), without building one: 1 pcg1, 2 pcg2,
+  // 3 the s-step PCG.  device_bytes = 0 skips the memory test.
+  m.def("choose_algo", [](const ProblemSpec& s, int world, Split split, const std::string& dtype, double device_bytes,
+                          int per_device, int algo, bool exact) {
+    GpuOptions o = make_options(0, "wave", 256, 0, 4, 0, dtype, exact, 32, false);
+    o.algo = algo;
+    o = resolve_options(o);
+    return choose_algo(s, make_process_grid(world, s.M, s.N, split), o, device_bytes, std::max(1, per_device), true);
+  }, py::arg("spec"), py::arg("world") = 1, py::arg("split") = Split::kAuto, py::arg("dtype") = "fp64",
+     py::arg("device_bytes") = 0.0, py::arg("per_device") = 1, py::arg("algo") = -1, py::arg("exact") = false);
+  m.def("estimate_device_bytes", [](const ProblemSpec& s, int world, Split split, int rank, const std::string& dtype,
+                                    int algo) {
+    const Subdomain sd = decompose_2d(s.M, s.N, make_process_grid(world, s.M, s.N, split), rank);
+    return GpuSubdomainSolver::estimate_device_bytes_algo(s, sd, dtype == "fp64" ? DType::kFp64 : DType::kFp32, algo);
+  }, py::arg("spec"), py::arg("world") = 1, py::arg("split") = Split::kAuto, py::arg("rank") = 0,
+     py::arg("dtype") = "fp64", py::arg("algo") = 1);
 
   py::class_<OpContext>(m, "OpContext", py::module_local())
       .def(py::init<const ProblemSpec&, int, int, int, int64_t, int>(), py::arg("spec"),
@@ -452,7 +472,7 @@ PYBIND11_MODULE(_pmx, m) {
                        bool rccl_graph, bool overlap, int vec_b, int waves_b, int tile_rows_b,
                        bool poison_halos, bool b_ring, int algo, bool defer_connect, int threaded,
                        int placement, double placement_budget_s, double placement_keep_free, int sharing,
-                       int block_tiles, int ca_s) {
+                       int block_tiles, int ca_s, int split_sweep) {
              SessionConfig c;
              c.sharing = sharing;
              c.spec = s;
@@ -460,6 +480,7 @@ PYBIND11_MODULE(_pmx, m) {
                                   graph_batch, check, overlap, vec_b, waves_b, tile_rows_b, poison_halos,
                                   b_ring, algo, placement, placement_budget_s, placement_keep_free,
                                   block_tiles, ca_s);
+             c.opt.split_sweep = split_sweep;
              c.defer_connect = defer_connect;
              c.threaded = threaded;
              c.split = split;
@@ -488,7 +509,36 @@ PYBIND11_MODULE(_pmx, m) {
            py::arg("b_ring") = false, py::arg("algo") = -1, py::arg("defer_connect") = false,
            py::arg("threaded") = -1, py::arg("placement") = 0, py::arg("placement_budget_s") = 0.5,
            py::arg("placement_keep_free") = 0.5, py::arg("sharing") = 0, py::arg("block_tiles") = -1,
-           py::arg("ca_s") = 3)
+           py::arg("ca_s") = 3, py::arg("split_sweep") = -1)
+      .def("ca_probe",
+           [](Session& s, int i, py::array_t<double, py::array::c_style | py::array::forcecast> z,
+              py::array_t<double, py::array::c_style | py::array::forcecast> p,
+              py::array_t<double, py::array::c_style | py::array::forcecast> w,
+              py::array_t<double, py::array::c_style | py::array::forcecast> coef,
+              py::array_t<double, py::array::c_style | py::array::forcecast> pa, bool fused) {
+             auto vec = [](const py::array_t<double, py::array::c_style | py::array::forcecast>& a) {
+               return std::vector<double>(a.data(), a.data() + a.size());
+             };
+             GpuSubdomainSolver& g = s.solver(i);
+             GpuSubdomainSolver::CaProbe r;
+             {
+               const auto vz = vec(z), vp = vec(p), vw = vec(w), vc = vec(coef), va = vec(pa);
+               py::gil_scoped_release nogil;
+               r = g.ca_probe(vz, vp, vw, vc, va, fused, s.stream_of(i));
+             }
+             const py::ssize_t nx = g.sd().nx, ny = g.sd().ny;
+             py::dict d;
+             d["gram"] = to_numpy(r.gram, {py::ssize_t(r.gram.size())});
+             d["norms"] = to_numpy(r.norms, {py::ssize_t(r.norms.size())});
+             d["p"] = to_numpy(r.p, {nx, ny});
+             d["z"] = to_numpy(r.z, {nx, ny});
+             d["w"] = to_numpy(r.w, {nx, ny});
+             return d;
+           },
+           py::arg("i"), py::arg("z"), py::arg("p"), py::arg("w"), py::arg("coef"), py::arg("pa"),
+           py::arg("fused") = false,
+           "s-step kernel probe (tests): one pass 1 + pass 2 (or the fused pass) on the given fields")
+      .def("ca_ghost_rows", [](Session& s, int i) { return s.solver(i).ca_ghost_rows(); }, py::arg("i") = 0)
       .def("ipc_export", [](Session& s) { return py::bytes(s.ipc_export()); },
            "IPC session: this rank's memory handles (pass every rank's to connect_ipc)")
       .def("connect_ipc", [](Session& s, std::vector<py::bytes> ex) {
@@ -615,6 +665,12 @@ PYBIND11_MODULE(_pmx, m) {
           d["tiles_i"] = c.tiles_i;
           d["tiles_j"] = c.tiles_j;
           d["algo"] = "ca";
+          d["fused"] = c.fuse != 0;
+          if (c.fuse) {  // the fused pass's own tiling (k_ca_fused: two-wave workgroups)
+            d["rows_fused"] = c.rows_f;
+            d["block_fused"] = c.wo_f;
+            d["tiles_fused"] = c.ntilesf();
+          }
         } else {
           if (!s.solver(0).single_pass()) d["b"] = one(s.solver(0).tiles_b());
           d["algo"] = s.solver(0).single_pass() ? "pcg1" : "pcg2";

@@ -163,7 +163,7 @@ __global__ void __launch_bounds__(256) k_loopback_fill(LoopbackSpans sp) {
 }
 
 unsigned long long loopback_ticks(const char* env) {
-  const char* v = std::getenv(env);
+  const char* v = study_env(env);  // loopback stand-in delays are a study setting
   return v && v[0] ? static_cast<unsigned long long>(std::atof(v) * 100.0) : 0ull;  // 100 MHz clock
 }
 

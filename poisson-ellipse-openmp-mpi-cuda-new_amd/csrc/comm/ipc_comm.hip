@@ -206,7 +206,7 @@ class IpcComm final : public Comm {
   IpcComm(GpuSubdomainSolver* local, int world) : local_(local), world_(world) {
     PMX_CHECK(world >= 1 && world <= kMaxIpcRanks, "IpcComm supports 1.." << kMaxIpcRanks << " ranks");
     HIP_CHECK(hipSetDevice(local->device()));
-    const char* coarse = std::getenv("PMX_IPC_COARSE");
+    const char* coarse = study_env("PMX_IPC_COARSE");
     if (coarse && coarse[0] == '1')
       HIP_CHECK(hipMalloc(&block_, sizeof(IpcBlock)));
     else  // flags every device reads and writes coherently (see the memory-model notes above)

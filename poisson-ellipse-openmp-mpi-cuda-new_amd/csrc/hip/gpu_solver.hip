@@ -11,6 +11,9 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
+#include <unistd.h>
+#include <string>
 #include <vector>
 #include <istream>
 #include <ostream>
@@ -82,10 +85,47 @@ DevTables upload_tables(const ProblemSpec& spec, double** owner) {
   return T;
 }
 
+namespace {
+bool study_mode() {
+  const char* e = std::getenv("PMX_STUDY");
+  return e && e[0] == '1';
+}
+// one warning per process for knob variables that are set outside study mode
+void warn_ignored_knobs() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    std::string names;
+    for (char** e = ::environ; e && *e; ++e) {
+      const std::string kv = *e;
+      const std::string k = kv.substr(0, kv.find('='));
+      static const char* knobs[] = {"PMX_ALGO", "PMX_PAIR_W", "PMX_PCG1_", "PMX_CA_", "PMX_ARITH32", "PMX_PLACEMENT",
+                                    "PMX_DIRECT_ROWS", "PMX_FRAME_ON_COMM", "PMX_FORK_ONE_QUEUE", "PMX_LOOPBACK_",
+                                    "PMX_IPC_COARSE", "PMX_PROGRESS"};
+      for (const char* p : knobs)
+        if (k.rfind(p, 0) == 0) names += (names.empty() ? "" : ", ") + k;
+    }
+    if (!names.empty())
+      std::fprintf(stderr, "pmx: ignoring %s (kernel / schedule study knobs apply only with PMX_STUDY=1)\n",
+                   names.c_str());
+  });
+}
+}  // namespace
+
+const char* study_env(const char* name) {
+  if (!study_mode()) {
+    warn_ignored_knobs();
+    return nullptr;
+  }
+  return std::getenv(name);
+}
+
 GpuOptions resolve_options(const GpuOptions& in) {
   if (in.resolved) return in;
   GpuOptions o = in;
-  auto env_int = [](const char* name, int& v) {
+  const bool study = study_mode();
+  if (!study) warn_ignored_knobs();
+  auto env_int = [study](const char* name, int& v) {
+    if (!study) return;
     if (const char* e = std::getenv(name); e && e[0]) v = std::atoi(e);
   };
   env_int("PMX_PAIR_W", o.pair_w);
@@ -127,7 +167,10 @@ GpuOptions resolve_options(const GpuOptions& in) {
   PMX_CHECK(o.ca_fuse >= -1 && o.ca_fuse <= 1, "s-step PCG: ca_fuse must be -1, 0 or 1");
   PMX_CHECK(o.ca_rows_f >= 0 && o.ca_rows_f <= 4096, "s-step PCG: fused tile rows must be 0 (auto) .. 4096");
   env_int("PMX_CA_DIRICHLET", o.ca_dirichlet);
-  if (const char* pk = std::getenv("PMX_PLACEMENT_PICK"); pk && pk[0]) o.placement_pick = std::string(pk) == "slowest" ? 1 : 0;
+  if (const char* pk = study ? std::getenv("PMX_PLACEMENT_PICK") : nullptr; pk && pk[0])
+    o.placement_pick = std::string(pk) == "slowest" ? 1 : 0;
+  env_int("PMX_PCG1_SPLIT", o.split_sweep);
+  PMX_CHECK(o.split_sweep >= -1 && o.split_sweep <= 1, "split_sweep must be -1, 0 or 1");
   PMX_CHECK(o.ca_split >= -1 && o.ca_split <= 1, "s-step PCG: ca_split must be -1, 0 or 1");
   PMX_CHECK(o.ca_split_upd >= -1 && o.ca_split_upd <= 1, "s-step PCG: ca_split_upd must be -1, 0 or 1");
   env_int("PMX_CA_WAVES_GRAM", o.ca_waves_gram);
@@ -169,6 +212,25 @@ bool choose_single_pass(const ProblemSpec& spec, const ProcGrid& grid, const Gpu
     if (need > 0.95 * device_total_bytes) return false;
   }
   return true;
+}
+
+int choose_algo(const ProblemSpec& spec, const ProcGrid& grid, const GpuOptions& o, double device_total_bytes,
+                int subdomains_per_device, bool direct_rows) {
+  PMX_CHECK(o.resolved, "choose_algo needs resolve_options()");
+  if (o.algo == 3) return 3;  // validated by the solver
+  if (o.algo == -1) {
+    const bool strips = grid.Py == 1 && (grid.size() == 1 || (direct_rows && (spec.M - 1) / grid.Px >= 8));
+    bool ca = o.dtype == DType::kFp64 && !o.exact && o.kernel == 1 && strips &&
+              int64_t(spec.M - 1) * (spec.N - 1) >= kCaAutoPoints;
+    if (ca && device_total_bytes > 0) {  // rank 0 holds the largest strip
+      const Subdomain sd0 = decompose_2d(spec.M, spec.N, grid, 0);
+      const double need = double(GpuSubdomainSolver::estimate_device_bytes_algo(spec, sd0, o.dtype, 3)) *
+                          std::max(1, subdomains_per_device);
+      ca = need <= 0.95 * device_total_bytes;
+    }
+    if (ca) return 3;
+  }
+  return choose_single_pass(spec, grid, o, device_total_bytes, subdomains_per_device) ? 1 : 2;
 }
 
 CommLayout GpuSubdomainSolver::comm_layout(const Subdomain& sd, DType dtype, bool single_pass) {
@@ -221,7 +283,8 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
 
   // iteration algorithm (see GpuOptions::algo); a Session resolves it once for all its solvers
-  if (opt_.algo == -1) opt_.algo = choose_single_pass(spec, sd.grid, opt_, double(total_b), 1) ? 1 : 2;
+  // (a standalone decomposed solver cannot know its transport: no s-step by auto there)
+  if (opt_.algo == -1) opt_.algo = choose_algo(spec, sd.grid, opt_, double(total_b), 1, false);
   pcg1_ = opt_.algo == 1;
   ca_ = opt_.algo == 3;
   PMX_CHECK(!ca_ || (opt.dtype == DType::kFp64 && !opt.exact && sd.grid.Py == 1 && sd.nx >= opt.ca_s),
@@ -242,9 +305,9 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   field_off_ = size_t(gh_ - 1) * size_t(G.pitch) + align_elems - 1;
   field_bytes_ = round_up((align_elems - 1 + size_t(sd.nx + 2 * gh_) * G.pitch) * elem_, 256);
   {  // fail with a sizing message instead of a bare hipErrorOutOfMemory
-    const size_t need = estimate_device_bytes(spec, sd, opt.dtype, pcg1_ || ca_) + (ca_ ? 2 * field_bytes_ : 0);
+    const size_t need = estimate_device_bytes_algo(spec, sd, opt.dtype, opt_.algo);
     PMX_CHECK(need <= free_b,
-              "subdomain " << sd.nx << "x" << sd.ny << " (" << (pcg1_ ? "pcg1, 5" : "pcg2, 4")
+              "subdomain " << sd.nx << "x" << sd.ny << " (" << (ca_ ? "s-step, 7" : pcg1_ ? "pcg1, 5" : "pcg2, 4")
                            << " fields) needs " << need / 1e9 << " GB on device " << opt.device
                            << " but only " << free_b / 1e9 << " of " << total_b / 1e9
                            << " GB are free; the largest square grid for this precision on one such "
@@ -362,8 +425,9 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     // the fused pass: undecomposed grids (a strip's ghost rows hold radius s, the fused march reads 2s)
     PMX_CHECK(opt_.ca_fuse != 1 || geom_.nb == 0, "the fused s-step pass runs undecomposed grids");
     ca_tiles_.fuse = opt_.ca_fuse == 1 || (opt_.ca_fuse == -1 && geom_.nb == 0) ? 1 : 0;
-    if (const char* e = std::getenv("PMX_CA_WAVES_F"); e && e[0]) ca_tiles_.waves_f = std::atoi(e);
-    if (const char* e = std::getenv("PMX_CA_SPLIT_F"); e && e[0]) ca_tiles_.split_f = std::atoi(e);
+    if (const char* e = study_env("PMX_CA_WAVES_F"); e && e[0]) ca_tiles_.waves_f = std::atoi(e);
+    if (const char* e = study_env("PMX_CA_SPLIT_F"); e && e[0]) ca_tiles_.split_f = std::atoi(e);
+    PMX_CHECK(ca_tiles_.waves_f == 2 || ca_tiles_.waves_f == 3, "s-step PCG: fused waves per SIMD must be 2 or 3");
     // the face coefficients of every node, read on the rows the ellipse cuts (2 more field-sized arrays)
     HIP_CHECK(hipMalloc(&ca_faces_, 2 * field_bytes_));
     ca_tiles_.fa = reinterpret_cast<const double*>(ca_faces_ + field_off_ * elem_);
@@ -649,6 +713,21 @@ size_t GpuSubdomainSolver::estimate_device_bytes(const ProblemSpec& spec, const 
          (1u << 20);
 }
 
+size_t GpuSubdomainSolver::estimate_device_bytes_algo(const ProblemSpec& spec, const Subdomain& sd, DType dtype,
+                                                      int algo) {
+  if (algo != 3) return estimate_device_bytes(spec, sd, dtype, algo == 1);
+  // s-step: w, two (z, p) sets and the two face fields, rows -gh+1 .. nx+gh (gh = 3 on strips)
+  const size_t elem = dtype == DType::kFp64 ? 8 : 4, align = 256 / elem;
+  const int gh = sd.grid.size() > 1 ? 3 : 2;
+  const size_t pitch = round_up(size_t(sd.ny + 2 + 8), align);
+  const size_t field = round_up((align - 1 + size_t(sd.nx + 2 * gh) * pitch) * elem, 256);
+  const size_t face = round_up((31 + size_t(sd.nx + 2 * gh) * pitch) * 8, 256);
+  const size_t tables = (4 * size_t(spec.M + 2) + 4 * size_t(spec.N + 2)) * 8 + 8 * size_t(spec.M + 2) * 4;
+  // partials: 21 doubles per 8-row tile of 116 columns (the smallest tiling), row-class words
+  const size_t partials = (size_t(sd.nx) / 8 + 1) * (size_t(sd.ny) / 116 + 1) * 21 * 8 * 2;
+  return 5 * field + 2 * face + tables + partials + comm_layout(sd, dtype, true).bytes + (1u << 20);
+}
+
 size_t GpuSubdomainSolver::device_bytes() const {
   const size_t tables = (4 * size_t(spec_.M + 2) + 4 * size_t(spec_.N + 2)) * sizeof(double) +
                         8 * size_t(spec_.M + 2) * sizeof(int);
@@ -710,7 +789,9 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
   after_launch(s);
   if (ca_) {  // set 0: z^0 = D^-1 r^0 (in r's buffer), p^0 = z^0; block counter 0
     if constexpr (sizeof(T) == 8) {
-      HIP_CHECK(hipMemsetAsync(ca_state_, 0, sizeof(CaState), s));
+      std::memset(&ca_init_, 0, sizeof(CaState));
+      ca_init_.s = ca_tiles_.s;  // (checked by load_checkpoint)
+      HIP_CHECK(hipMemcpyAsync(ca_state_, &ca_init_, sizeof(CaState), hipMemcpyHostToDevice, s));
       ca_blk_ = 0;
       launch_ca_init<double>(ca_geom_, ca_tables_, static_cast<double*>(field_base(1)), static_cast<double*>(field_base(2)), s);
       after_launch(s);
@@ -801,27 +882,69 @@ void GpuSubdomainSolver::enqueue_ca_finish(hipStream_t s, int n, bool check_only
   after_launch(s);
 }
 
-void GpuSubdomainSolver::enqueue_ca_block(hipStream_t s, int n, bool first) {
-  PMX_CHECK(geom_.nb == 0, "enqueue_ca_block: undecomposed grids (the driver runs the steps otherwise)");
-  if (!ca_fused()) {
+GpuSubdomainSolver::CaProbe GpuSubdomainSolver::ca_probe(const std::vector<double>& z, const std::vector<double>& p,
+                                                         const std::vector<double>& w, const std::vector<double>& coef,
+                                                         const std::vector<double>& pa, bool fused, hipStream_t s) {
+  PMX_CHECK(ca_ && elem_ == 8, "ca_probe: not an s-step solver");
+  PMX_CHECK(!fused || ca_fused(), "ca_probe: the fused pass runs undecomposed grids");
+  const int S = ca_tiles_.s, NB = 2 * S + 1, NQ = 6 * S;
+  const size_t rows = size_t(sd_.nx + 2 * gh_), cols = size_t(sd_.ny + 2);
+  PMX_CHECK(z.size() == rows * cols && p.size() == rows * cols && w.size() == rows * cols,
+            "ca_probe: fields must be (nx + 2 gh) x (ny + 2)");
+  PMX_CHECK(coef.size() == size_t(3 * NB) && pa.size() == size_t(S * NB), "ca_probe: coefficient shapes");
+  HIP_CHECK(hipSetDevice(opt_.device));
+  enqueue_init(s);
+  HIP_CHECK(hipStreamSynchronize(s));
+  auto put = [&](void* base, const std::vector<double>& v) {
+    char* dst = static_cast<char*>(base) + int64_t(1 - gh_) * geom_.pitch * 8;
+    HIP_CHECK(hipMemcpy2D(dst, size_t(geom_.pitch) * 8, v.data(), cols * 8, cols * 8, rows, hipMemcpyHostToDevice));
+  };
+  put(field_base(1), z);
+  put(field_base(2), p);
+  put(field_base(0), w);
+  CaProbe out;
+  auto sums = [&](int64_t base, int nq, int n) {
+    const std::vector<double> h = read_partials(s);
+    std::vector<double> r(size_t(nq), 0.0);
+    for (int q = 0; q < nq; ++q)
+      for (int i = 0; i < n; ++i) r[size_t(q)] += h[size_t(base + int64_t(q) * n + i)];
+    return r;
+  };
+  CaState c{};
+  HIP_CHECK(hipMemcpy(&c, ca_state_, sizeof(CaState), hipMemcpyDeviceToHost));
+  c.blk = 1;  // as after the block's reduction: pass 2 / the fused pass read set 0, write set 1
+  c.nupd = S;
+  for (int k = 0; k < 3; ++k)
+    for (int i = 0; i < NB; ++i) c.coef[k][i] = coef[size_t(k * NB + i)];
+  for (int j = 0; j < S; ++j)
+    for (int i = 0; i < NB; ++i) c.pa[j][i] = pa[size_t(j * NB + i)];
+  if (!fused) {
     enqueue_ca_pass(s, false);
-    enqueue_ca_reduce(s, n, false, true);
+    HIP_CHECK(hipStreamSynchronize(s));
+    out.gram = sums(0, NQ, ca_tiles_.ntiles());
+    HIP_CHECK(hipMemcpy(ca_state_, &c, sizeof(CaState), hipMemcpyHostToDevice));
     enqueue_ca_pass(s, true);
-    return;
+    HIP_CHECK(hipStreamSynchronize(s));
+    out.norms = sums(int64_t(NQ) * ca_tiles_.ntiles(), S, ca_tiles_.ntiles2());
+  } else {
+    HIP_CHECK(hipMemcpy(ca_state_, &c, sizeof(CaState), hipMemcpyHostToDevice));
+    enqueue_ca_fused(s);
+    HIP_CHECK(hipStreamSynchronize(s));
+    const std::vector<double> gn = sums(0, NQ + S, ca_tiles_.ntilesf());
+    out.gram.assign(gn.begin(), gn.begin() + NQ);
+    out.norms.assign(gn.begin() + NQ, gn.end());
   }
-  // fused schedule: pass 1 (first block of a batch) or the fused pass (which applies the previous
-  // block), then the reduction; the last block's pass 2 runs in enqueue_ca_check
-  if (first) enqueue_ca_pass(s, false);
-  else enqueue_ca_fused(s);
-  enqueue_ca_reduce(s, n, false, true, !first);
-}
-
-void GpuSubdomainSolver::enqueue_ca_check(hipStream_t s) {
-  PMX_CHECK(geom_.nb == 0, "enqueue_ca_check: undecomposed grids (the driver runs the steps otherwise)");
-  if (ca_fused()) enqueue_ca_pass(s, true);  // the batch's last block
-  enqueue_ca_reduce(s, 1, true, true);
-  // a stop inside the last block rewinds w (every workgroup returns at once otherwise)
-  enqueue_ca_pass(s, true);
+  auto get = [&](const void* base) {
+    std::vector<double> h(size_t(sd_.nx) * sd_.ny);
+    const char* src = static_cast<const char*>(base) + (geom_.pitch + 1) * 8;
+    HIP_CHECK(hipMemcpy2D(h.data(), size_t(sd_.ny) * 8, src, size_t(geom_.pitch) * 8, size_t(sd_.ny) * 8,
+                          size_t(sd_.nx), hipMemcpyDeviceToHost));
+    return h;
+  };
+  out.p = get(field_base(3));
+  out.z = get(r2_ + field_off_ * elem_);
+  out.w = get(field_base(0));
+  return out;
 }
 
 template <typename T>
@@ -1030,13 +1153,18 @@ struct CkptHeader {
 constexpr char kCkptMagic[8] = {'P', 'M', 'X', 'C', 'K', 'P', 'T', '1'};
 }  // namespace
 
+// The version names the iteration algorithm and layout: v3 pcg2 (4 fields with 2 ghost rows), v5 pcg1
+// (+ its w-cycle state, r2 appended), v6 the s-step PCG (r2 = the second z buffer appended, then
+// CaState).  A checkpoint is written between batches, where every algorithm's state is exact: for the
+// s-step no block's stop test is pending and w holds every applied block.
+int GpuSubdomainSolver::ckpt_version() const { return ca_ ? 6 : pcg1_ ? 5 : 3; }
+
 void GpuSubdomainSolver::save_checkpoint(std::ostream& os, hipStream_t s) const {
-  PMX_CHECK(!ca_, "not available for the s-step solver");
   HIP_CHECK(hipSetDevice(opt_.device));
   HIP_CHECK(hipStreamSynchronize(s));
   CkptHeader h{};
   std::memcpy(h.magic, kCkptMagic, 8);
-  h.version = pcg1_ ? 5 : 3;  // v3: fields with 2 ghost rows; v5: + pcg1 state (w cycle), r2 appended
+  h.version = ckpt_version();
   h.M = spec_.M; h.N = spec_.N; h.gi0 = sd_.gi0(); h.gj0 = sd_.gj0();
   h.rank = sd_.rank; h.elem = int32_t(elem_); h.norm = int32_t(spec_.norm);
   h.nx = sd_.nx; h.ny = sd_.ny; h.pitch = geom_.pitch; h.field_bytes = int64_t(field_bytes_);
@@ -1048,21 +1176,26 @@ void GpuSubdomainSolver::save_checkpoint(std::ostream& os, hipStream_t s) const 
   os.write(buf.data(), std::streamsize(4 * field_bytes_));
   HIP_CHECK(hipMemcpy(buf.data(), arena_, layout_.bytes, hipMemcpyDeviceToHost));
   os.write(buf.data(), std::streamsize(layout_.bytes));
-  if (pcg1_) {
+  if (pcg1_ || ca_) {
     HIP_CHECK(hipMemcpy(buf.data(), r2_, field_bytes_, hipMemcpyDeviceToHost));
     os.write(buf.data(), std::streamsize(field_bytes_));
+  }
+  if (ca_) {
+    CaState c{};
+    HIP_CHECK(hipMemcpy(&c, ca_state_, sizeof(CaState), hipMemcpyDeviceToHost));
+    PMX_CHECK(c.pend_n == 0 && c.nupd <= 0, "s-step checkpoint inside a batch (a block's stop test is pending)");
+    os.write(reinterpret_cast<const char*>(&c), sizeof(c));
   }
   PMX_CHECK(os.good(), "checkpoint write failed");
 }
 
 void GpuSubdomainSolver::load_checkpoint(std::istream& is, hipStream_t s) {
-  PMX_CHECK(!ca_, "not available for the s-step solver");
   HIP_CHECK(hipSetDevice(opt_.device));
   CkptHeader h{};
   is.read(reinterpret_cast<char*>(&h), sizeof(h));
-  PMX_CHECK(is.good() && std::memcmp(h.magic, kCkptMagic, 8) == 0 &&
-                h.version == (pcg1_ ? 5 : 3),
-            "not a pmx checkpoint of this iteration algorithm and layout (v3 pcg2, v5 pcg1)");
+  PMX_CHECK(is.good() && std::memcmp(h.magic, kCkptMagic, 8) == 0 && h.version == ckpt_version(),
+            "not a pmx checkpoint of this iteration algorithm and layout (v3 pcg2, v5 pcg1, v6 s-step; file v"
+                << h.version << ", solver v" << ckpt_version() << ")");
   PMX_CHECK(h.M == spec_.M && h.N == spec_.N && h.gi0 == sd_.gi0() && h.gj0 == sd_.gj0() &&
                 h.nx == sd_.nx && h.ny == sd_.ny && h.rank == sd_.rank,
             "checkpoint is for a different grid/decomposition (M=" << h.M << " N=" << h.N << " rank "
@@ -1085,10 +1218,19 @@ void GpuSubdomainSolver::load_checkpoint(std::istream& is, hipStream_t s) {
   PcgState ck{};
   std::memcpy(&ck, buf.data() + layout_.state_off, sizeof(PcgState));
   host_k_ = ck.it;
-  if (pcg1_) {
+  if (pcg1_ || ca_) {
     is.read(buf.data(), std::streamsize(field_bytes_));
-    PMX_CHECK(is.good(), "truncated checkpoint (pcg1 r2)");
+    PMX_CHECK(is.good(), "truncated checkpoint (r2 / second z buffer)");
     HIP_CHECK(hipMemcpy(r2_, buf.data(), field_bytes_, hipMemcpyHostToDevice));
+  }
+  if (ca_) {
+    CaState c{};
+    is.read(reinterpret_cast<char*>(&c), sizeof(c));
+    PMX_CHECK(is.good(), "truncated checkpoint (s-step state)");
+    PMX_CHECK(c.s == ca_tiles_.s, "checkpoint was written with s = " << c.s << ", this solver runs s = " << ca_tiles_.s);
+    c.ticket = 0u;
+    HIP_CHECK(hipMemcpy(ca_state_, &c, sizeof(CaState), hipMemcpyHostToDevice));
+    ca_blk_ = c.blk;  // the (z, p) set the next block reads
   }
 }
 
@@ -1257,7 +1399,7 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
   // (A/B).  Every local solver must qualify (they exchange with each other under LocalComm).
   bool direct = (single_pass_ || ca_) && any_nb && comm_->direct_rows();
   for (auto* s : local_) direct &= s->can_direct_rows();
-  if (const char* d = std::getenv("PMX_DIRECT_ROWS"); d && d[0] == '0') direct = false;
+  if (const char* d = study_env("PMX_DIRECT_ROWS"); d && d[0] == '0') direct = false;
   direct_ = direct;
   for (auto* s : local_) s->set_direct_rows(direct_);
   PMX_CHECK(!ca_ || !any_nb || direct_,
@@ -1269,7 +1411,7 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
   // PMX_FORK_ONE_QUEUE=1 keeps the forks (eager only) to test that their event ordering needs no
   // concurrently resident streams.
   if (const char* q = std::getenv("GPU_MAX_HW_QUEUES"); q && std::atoi(q) == 1) {
-    const char* keep = std::getenv("PMX_FORK_ONE_QUEUE");
+    const char* keep = study_env("PMX_FORK_ONE_QUEUE");
     if (keep && keep[0] == '1') {
       bool forked = overlap_;
       for (auto* s : local_) forked |= s->ca_side_stream();
@@ -1302,10 +1444,10 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
   // in flight, frame tiles on their own stream once it has landed.  Default: on with RCCL, whose
   // xGMI exchange is the long pole; off with LocalComm, whose device copies are cheaper than the
   // extra launch (16384^2 as 2x2 subdomains on one GPU: 2.647 vs 2.602 ms; 2 strips: 2.416 vs
-  // 2.430).  PMX_PCG1_SPLIT=0/1 forces it.
-  const char* sp = std::getenv("PMX_PCG1_SPLIT");
+  // 2.430).  GpuOptions::split_sweep (study: PMX_PCG1_SPLIT) forces it.
+  const int sw = local_[0]->options().split_sweep;
   const bool split_default = comm_->prefers_split();
-  split_ = overlap_ && single_pass_ && (sp && sp[0] ? sp[0] == '1' : split_default);
+  split_ = overlap_ && single_pass_ && (sw >= 0 ? sw == 1 : split_default);
   if (split_) {
     auto ev = [](std::vector<hipEvent_t>& v) {
       hipEvent_t e;
@@ -1326,7 +1468,7 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
     // default on: loopback rank 3 of 8 284.2 / 284.5 vs 288.0 / 286.9 us, 301.8 vs 308.4 with the
     // 20 / 15-us exchange / all-reduce stand-ins (profiles/r4/loopback/r4al_*); PMX_FRAME_ON_COMM=0
     // restores the separate frame stream
-    const char* fc = std::getenv("PMX_FRAME_ON_COMM");
+    const char* fc = study_env("PMX_FRAME_ON_COMM");
     frame_on_comm_ = !(fc && fc[0] == '0');
   }
 }
@@ -1491,34 +1633,58 @@ int PcgDriver::ca_batch() const {
   return (b + s - 1) / s * s;  // whole blocks per captured batch
 }
 
-void PcgDriver::enqueue_ca(int64_t n) {
+void PcgDriver::enqueue_ca(int64_t n, const std::function<void(int)>& mark) {
   const int s = local_[0]->ca_s();
   HIP_CHECK(hipSetDevice(local_[0]->device()));
   if (n <= 0) return;
-  if (!any_nb_ && local_.size() == 1 && comm_->world_size() == 1) {
-    bool first = true;
-    while (n > 0) {
-      const int m = int(std::min<int64_t>(s, n));
-      local_[0]->enqueue_ca_block(streams_[0], m, first);
-      first = false;
-      n -= m;
-    }
-    // the last block's stop test (and its rewind): the state is exact at every batch boundary
-    local_[0]->enqueue_ca_check(streams_[0]);
-    return;
-  }
-  // decomposed: every rank's sums are all-reduced between the reduction and the scalars, and the s
-  // ghost rows of the new (z, p) set are exchanged after pass 2 (direct rows, one span per field)
+  auto mk = [&](int b) {
+    if (mark) mark(b);
+  };
   auto each = [&](auto&& f) {
     for (size_t i = 0; i < local_.size(); ++i) {
       HIP_CHECK(hipSetDevice(local_[i]->device()));
       f(local_[i], streams_[i]);
     }
+    HIP_CHECK(hipSetDevice(local_[0]->device()));
   };
+  if (!any_nb_ && local_.size() == 1 && comm_->world_size() == 1) {
+    // One grid: pass 1 -> reduce -> pass 2 per block, or with the fused pass
+    //   pass 1 -> reduce -> (fused -> reduce) x (blocks - 1) -> pass 2
+    // and then the last block's stop test (and its rewind): the state is exact at every batch end
+    GpuSubdomainSolver* g = local_[0];
+    hipStream_t st = streams_[0];
+    const bool fused = g->ca_fused();
+    bool first = true;
+    while (n > 0) {
+      const int m = int(std::min<int64_t>(s, n));
+      if (fused && !first) g->enqueue_ca_fused(st);
+      else g->enqueue_ca_pass(st, false);
+      mk(kPhA);
+      g->enqueue_ca_reduce(st, m, false, true, fused && !first);
+      mk(kPhRed);
+      if (!fused) {
+        g->enqueue_ca_pass(st, true);
+        mk(kPhB);
+      }
+      first = false;
+      n -= m;
+    }
+    if (fused) {
+      g->enqueue_ca_pass(st, true);
+      mk(kPhB);
+    }
+    g->enqueue_ca_reduce(st, 1, true, true);
+    mk(kPhRed);
+    g->enqueue_ca_pass(st, true);  // rewind (a no-op unless the test stopped inside the last block)
+    mk(kPhB);
+    return;
+  }
+  // decomposed: every rank's sums are all-reduced between the reduction and the scalars, and the s
+  // ghost rows of the new (z, p) set are exchanged after pass 2 (direct rows, one span per field).
   // With the overlapped schedule the exchange runs on the comm stream: the next pass 1's interior
   // tiles (which read no ghost row) start at once, its frame tiles wait for the exchange.  The batch
   // joins the comm stream at its end, so a captured graph has no edge into the next one.
-  const bool ovl = any_nb_ && overlap_ && !comm_streams_.empty();
+  const bool ovl = any_nb_ && overlap_ && !comm_streams_.empty() && !mark;
   bool pending = false;
   auto frame_waits = [&](bool on) {  // every solver, by the index of its (possibly shared) stream
     size_t u = 0;
@@ -1527,13 +1693,19 @@ void PcgDriver::enqueue_ca(int64_t n) {
       local_[i]->set_ca_frame_wait(on ? ev_halo_[u] : nullptr);
     }
   };
+  const bool ar = comm_->world_size() > 1;
   while (n > 0) {
     const int m = int(std::min<int64_t>(s, n));
     each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, false); });
+    mk(kPhA);
     each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_reduce(st, m, false, false); });
+    mk(kPhRed);
     comm_->allreduce(local_, 3, streams_);
+    if (ar) mk(kPhAr);
     each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_finish(st, m, false); });
+    mk(kPhRed);
     each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, true); });
+    mk(kPhB);
     if (any_nb_ && ovl) {
       for_each_stream([&](size_t i, size_t u) {
         HIP_CHECK(hipEventRecord(ev_packed_[u], streams_[i]));
@@ -1545,13 +1717,18 @@ void PcgDriver::enqueue_ca(int64_t n) {
       pending = true;
     } else if (any_nb_) {
       comm_->halo(local_, streams_);
+      mk(kPhHalo);
     }
     n -= m;
   }
   each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_reduce(st, 1, true, false); });
+  mk(kPhRed);
   comm_->allreduce(local_, 3, streams_);
+  if (ar) mk(kPhAr);
   each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_finish(st, 1, true); });
+  mk(kPhRed);
   each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, true); });  // rewind
+  mk(kPhB);
   if (pending) {  // the last block's exchange ran next to the check
     for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipStreamWaitEvent(streams_[i], ev_halo_[u], 0)); });
     frame_waits(false);
@@ -1883,13 +2060,14 @@ RunStats PcgDriver::profile_phases(int64_t n) {
   // pack + exchange + unpack.  A step with nothing to enqueue (the all-reduce of one rank, the
   // exchange of an undecomposed grid, pcg2's second half in pcg1) records no event: two back-to-back
   // timing events cost ~5 us of marker latency, which would otherwise show up as that bucket's time.
+  // s-step PCG: per block pass 1 (or the fused pass) = kernel_a, pass 2 = kernel_b, the reduction(s)
+  // and the scalars = reduce, the 21-double all-reduce, and the ghost-row exchange of strips
   RunStats st;
-  PMX_CHECK(!ca_, "profile_phases: not available for the s-step solver (rocprofv3 --kernel-trace times its passes)");
   HIP_CHECK(hipSetDevice(local_[0]->device()));
   hipStream_t s0 = streams_[0];
-  enum Bucket { kA, kB, kRed, kAr, kHalo };
+  enum Bucket { kA = kPhA, kB = kPhB, kRed = kPhRed, kAr = kPhAr, kHalo = kPhHalo };
   const bool ar = comm_->world_size() > 1;
-  std::vector<hipEvent_t> ev(size_t(n) * 7 + 1);
+  std::vector<hipEvent_t> ev(size_t(n) * 7 + 16);
   std::vector<int> bucket(ev.size(), -1);
   for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
   size_t ne = 0;
@@ -1905,7 +2083,8 @@ RunStats PcgDriver::profile_phases(int64_t n) {
     HIP_CHECK(hipSetDevice(local_[0]->device()));
   };
   mark(-1);
-  for (int64_t k = 0; k < n; ++k) {
+  if (ca_) enqueue_ca(n, mark);
+  for (int64_t k = 0; k < n && !ca_; ++k) {
     each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_kernel_a(s); });
     mark(kA);
     each([](GpuSubdomainSolver* g, hipStream_t s) { g->enqueue_reduce_a(s); });

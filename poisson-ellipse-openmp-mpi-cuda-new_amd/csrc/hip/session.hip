@@ -36,7 +36,7 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
     PMX_CHECK(cfg_.ranks.size() == 1, "loopback runs exactly one rank of the decomposition");
 
   // one iteration algorithm for every subdomain (and every process: the choice only depends on
-  // global data, see choose_single_pass)
+  // global data, see choose_algo)
   GpuOptions pre = cfg_.opt;
   // a multi-process RCCL run tracks device progress for its hang watchdog (GpuOptions::progress)
   if ((cfg_.comm == CommKind::kRccl || cfg_.comm == CommKind::kIpc) && cfg_.world > 1) pre.progress = 1;
@@ -48,7 +48,8 @@ Session::Session(const SessionConfig& cfg) : cfg_(cfg) {
     int per_device = 0;  // subdomains sharing the busiest device
     for (int d : cfg_.devices) per_device = std::max<int>(per_device, int(std::count(cfg_.devices.begin(), cfg_.devices.end(), d)));
     per_device = std::max(per_device, cfg_.sharing);
-    base.algo = choose_single_pass(cfg_.spec, pg_, base, double(total_b), per_device) ? 1 : 2;
+    // every transport of a Session moves ghost rows straight between the fields (direct rows)
+    base.algo = choose_algo(cfg_.spec, pg_, base, double(total_b), per_device, true);
   }
   for (size_t i = 0; i < cfg_.ranks.size(); ++i) {
     GpuOptions o = base;
@@ -330,7 +331,7 @@ std::vector<std::vector<CommEvent>> record_comm_sequence(const ProblemSpec& spec
                                                          const GpuOptions& opt, int64_t iters) {
   const ProcGrid pg = make_process_grid(world, spec.M, spec.N, split);
   GpuOptions o = resolve_options(opt);
-  if (o.algo == -1) o.algo = choose_single_pass(spec, pg, o, 0.0, world) ? 1 : 2;
+  if (o.algo == -1) o.algo = choose_algo(spec, pg, o, 0.0, world, true);
   std::vector<std::unique_ptr<GpuSubdomainSolver>> solvers;
   std::vector<std::vector<CommEvent>> logs(static_cast<size_t>(world));
   std::vector<std::unique_ptr<Comm>> comms;
@@ -351,9 +352,12 @@ std::vector<std::vector<CommEvent>> record_comm_sequence(const ProblemSpec& spec
   return logs;
 }
 
-int64_t max_square_grid(double bytes_per_gpu, int gpus, DType dtype, double reserve_fraction) {
-  // the default iteration (pcg1) keeps 5 fields in either precision; +1% pitch
-  const double bpp = 5.0 * (dtype == DType::kFp64 ? 8.0 : 4.0) * 1.01;
+int64_t max_square_grid(double bytes_per_gpu, int gpus, DType dtype, double reserve_fraction, int algo) {
+  // pcg1 keeps 5 fields in either precision, the s-step PCG (fp64) 5 fields plus 2 fp64 face fields,
+  // pcg2 4 fields; +1% pitch.  Auto (-1): the largest grid that fits SOME algorithm -- pcg1, to which
+  // auto falls back when the s-step's fields do not fit (choose_algo)
+  const double elem = dtype == DType::kFp64 ? 8.0 : 4.0;
+  const double bpp = (algo == 3 ? 5.0 * elem + 16.0 : algo == 2 ? 4.0 * elem : 5.0 * elem) * 1.01;
   const double pts = bytes_per_gpu * (1.0 - reserve_fraction) * gpus / bpp;
   return int64_t(std::floor(std::sqrt(pts)));
 }

@@ -153,6 +153,9 @@ struct GpuOptions {
   // LDS ring with exact vmcnt counting (2 or 3), 0 = register prefetch.  dma1w: the w sweep (-1 = as
   // dma1).  PMX_PCG1_DMA / PMX_PCG1_DMA_W override.
   int dma1 = 0, dma1w = -1;
+  // pcg1 split sweep on decomposed grids (interior tiles overlap the previous ghost exchange, the frame
+  // waits for it): -1 = the transport's default (Comm::prefers_split: RCCL on), 0 off, 1 on
+  int split_sweep = -1;
   double placement_budget_s = 0.5;
   double placement_keep_free = 0.5;
   // which probed block to keep: 0 the fastest (default), 1 the slowest -- for slow-class A/Bs and
@@ -166,13 +169,28 @@ inline const char* dtype_name(const GpuOptions& o) {
   return o.dtype == DType::kFp64 ? "fp64" : (o.arith32 ? "fp32" : "mixed");
 }
 
-// Environment overrides (PMX_ALGO, PMX_PAIR_W, PMX_PCG1_*) applied to a copy of `opt`.
+// Validates `opt` and marks it resolved.  Study mode (PMX_STUDY=1 in the environment) first applies
+// the kernel / schedule overrides of bench/ studies (PMX_ALGO, PMX_PAIR_W, PMX_PCG1_*, PMX_CA_*,
+// PMX_PLACEMENT*); without it those variables are ignored (one warning on stderr), so a stray
+// variable cannot change what a run or a test measures.
 GpuOptions resolve_options(const GpuOptions& opt);
+// getenv(name) in study mode, nullptr otherwise (driver-level study knobs: PMX_DIRECT_ROWS,
+// PMX_PCG1_SPLIT, PMX_FRAME_ON_COMM, PMX_FORK_ONE_QUEUE, PMX_CA_WAVES_F, PMX_CA_SPLIT_F)
+const char* study_env(const char* name);
 // Single-pass (pcg1) or two-sweep (pcg2) iteration for this problem/process grid/options.  A pure
 // function of global data (see GpuOptions::algo); `device_total_bytes` = 0 skips the size test.
 // `subdomains_per_device` subdomains share one device (LocalComm: all of them).
 bool choose_single_pass(const ProblemSpec& spec, const ProcGrid& grid, const GpuOptions& resolved,
                         double device_total_bytes, int subdomains_per_device);
+// The iteration algorithm (GpuOptions::algo) a run uses: an explicit 1 / 2 / 3 as given, auto (-1) the
+// s-step PCG (3) where it applies and wins -- fp64 with the fast arithmetic, undecomposed or row strips
+// of >= 8 rows on a transport that moves ghost rows between fields (`direct_rows`), at least
+// kCaAutoPoints grid points (below, pcg1's block tiles are faster: profiles/r5/ca/small.log) -- and
+// whose 7 fields fit into the device (`device_total_bytes` > 0; else no size test), otherwise
+// choose_single_pass.  A pure function of global data: every rank makes the same choice.
+constexpr int64_t kCaAutoPoints = 6000000;
+int choose_algo(const ProblemSpec& spec, const ProcGrid& grid, const GpuOptions& resolved, double device_total_bytes,
+                int subdomains_per_device, bool direct_rows = true);
 
 // The comm arena: PcgState (the all-reduce buffers) and one send + one receive buffer per halo
 // slot (pmx/device_types.hpp kHaloSlots), all sends first, then all receives.
@@ -225,6 +243,9 @@ class GpuSubdomainSolver {
   // allocating; used by `pmx --plan` and the pcg1/pcg2 choice.
   static size_t estimate_device_bytes(const ProblemSpec& spec, const Subdomain& sd, DType dtype,
                                       bool single_pass);
+  // ... for iteration algorithm `algo` (1 pcg1, 2 pcg2, 3 the s-step PCG: 5 fields with s ghost rows on
+  // strips, plus the two face-coefficient fields)
+  static size_t estimate_device_bytes_algo(const ProblemSpec& spec, const Subdomain& sd, DType dtype, int algo);
 
   // r=B, w=0, p=0, state reset, red_b <- (0, zr_0).  Single-pass: the driver then runs the ghost
   // exchange of r^0 (decomposed grids), sweep 0 (enqueue_phase_a) and the all-reduce of red_c.
@@ -275,10 +296,12 @@ class GpuSubdomainSolver {
   bool ca_side_stream() const { return ca_side_ != nullptr; }
   void drop_side_stream();
 
-  // Checkpoint: the 4 fields with ghosts, the PCG scalars and the halo buffers,
-  // i.e. everything the next iteration reads.  Synchronous; written at batch boundaries.
+  // Checkpoint: the fields with ghosts (pcg1 / s-step: also the second r / z buffer),
+  // the PCG scalars, the halo buffers and the s-step's CaState, i.e. everything the next iteration
+  // reads.  Synchronous; written at batch boundaries.
   void save_checkpoint(std::ostream& os, hipStream_t s) const;
   void load_checkpoint(std::istream& is, hipStream_t s);
+  int ckpt_version() const;  // file version of this solver's algorithm (3 pcg2, 5 pcg1, 6 s-step)
 
   PcgState read_state(hipStream_t s) const;  // synchronous D2H of the scalars
   std::vector<double> read_partials(hipStream_t s) const;  // the partials buffer (5 per tile slot)
@@ -328,9 +351,6 @@ class GpuSubdomainSolver {
   bool ca() const { return ca_; }
   int ca_s() const { return ca_ ? ca_tiles_.s : 0; }
   const CaTiles& ca_tiles() const { return ca_tiles_; }
-  // one block of n iterations: pass 1, reduction, pass 2 -- or with the fused pass, `first`: pass 1 +
-  // reduction, else fused pass + reduction (the batch's last pass 2 follows in enqueue_ca_check)
-  void enqueue_ca_block(hipStream_t s, int n, bool first = true);
   // the same block in steps, for decomposed grids (the driver all-reduces CaState::red between
   // reduce and finish, and exchanges the s ghost rows of the new (z, p) set after pass 2)
   void enqueue_ca_pass(hipStream_t s, bool upd);
@@ -340,11 +360,20 @@ class GpuSubdomainSolver {
   bool ca_fused() const { return ca_ && ca_tiles_.fuse != 0; }
   void enqueue_ca_reduce(hipStream_t s, int n, bool check_only, bool finish, bool fused = false);
   void enqueue_ca_finish(hipStream_t s, int n, bool check_only);
+  // Kernel test hook (tests/test_gpu_ca_gram.py): set 0 <- (z, p) and w <- w0 from host arrays of
+  // (nx + 2 gh) x (ny + 2) values (local rows 1-gh .. nx+gh, columns 0 .. ny+1, gh = ca_ghost_rows()),
+  // then pass 1 and pass 2 -- or the fused pass -- once each with pass 2's coefficient vectors coef
+  // (a, b, c: 3 x (2s+1)) and pa (s x (2s+1)).  Returns pass 1's 6s Gram sums over the tiles (the fused
+  // pass: of the NEW basis), pass 2's s norm sums, and the new p, z, w (nx x ny).  Resets the solver.
+  struct CaProbe {
+    std::vector<double> gram, norms, p, z, w;
+  };
+  CaProbe ca_probe(const std::vector<double>& z, const std::vector<double>& p, const std::vector<double>& w,
+                   const std::vector<double>& coef, const std::vector<double>& pa, bool fused, hipStream_t s);
+  int ca_ghost_rows() const { return gh_; }
   // host mirror of CaState::blk (blocks enqueued): the (z, p) set the next exchange sends
   long long ca_blocks() const { return ca_blk_; }
   void set_ca_blocks(long long b) { ca_blk_ = b; }
-  // the pending stop test of the last block, and pass 2 rewinding w if it stopped inside that block
-  void enqueue_ca_check(hipStream_t s);
   // pcg1: host mirror of the device iteration counter S->it -- the index of the next sweep this
   // solver enqueues.  init sets it to 0, every enqueued reduction (which bumps S->it on the
   // device) advances it, load_checkpoint reads it from the checkpoint.  It picks the plain or the
@@ -395,6 +424,7 @@ class GpuSubdomainSolver {
   hipEvent_t ca_frame_wait_ = nullptr;  // one-shot: the next pass 1's frame tiles wait for it
   void ca_sweep(hipStream_t s, bool upd);
   CaState* ca_state_ = nullptr;
+  CaState ca_init_{};           // host template of the state init() uploads
   double* ca_chunk_ = nullptr;  // its reduction's chunk sums
   long long ca_blk_ = 0;        // blocks enqueued since init (CaState::blk's host mirror)
   int gh_ = 2;                  // ghost rows of the fields on each side
@@ -577,8 +607,11 @@ class PcgDriver {
 
  private:
   void enqueue_one_iteration();
-  // s-step PCG: n iterations as blocks of ca_s() (the last one shorter), graphs of ca_batch()
-  void enqueue_ca(int64_t n);
+  // s-step PCG: n iterations as blocks of ca_s() (the last one shorter), graphs of ca_batch().  mark:
+  // profile_phases' event hook, called after every step with its bucket (PhaseBucket); with a hook the
+  // ghost exchange runs on the compute stream (each step's time is its own)
+  enum PhaseBucket { kPhA = 0, kPhB, kPhRed, kPhAr, kPhHalo };
+  void enqueue_ca(int64_t n, const std::function<void(int)>& mark = {});
   int ca_batch() const;
   int ca_phase() const;  // captured s-step batches on decomposed grids depend on the (z, p) set parity
   // pack -> comm -> unpack, filling the inputs of sweep `target` (direct rows: comm only)

@@ -34,8 +34,8 @@ struct SessionConfig {
   int threaded = -1;
   // Subdomains of the whole job that share the busiest device (0 = count this session's own
   // `devices`).  A multi-process job whose ranks share one GPU (bench.py --share-gpu, IPC
-  // rehearsals) passes its world size, so every transport makes the same pcg1/pcg2 choice
-  // (choose_single_pass) as the torch path's comm_layout(sharing=...).
+  // rehearsals) passes its world size, so every rank sizes the iteration algorithm's fields against
+  // the device it shares (choose_algo; the torch path's comm_layout(sharing=...) likewise).
   int sharing = 0;
 };
 
@@ -80,6 +80,10 @@ class Session {
   int num_local() const { return int(solvers_.size()); }
   GpuSubdomainSolver& solver(int i) { return *solvers_.at(size_t(i)); }
   const std::string comm_name() const { return comm_ ? comm_->name() : "unconnected"; }
+  // the iteration algorithm the solvers run: "ca" (s-step PCG), "pcg1" or "pcg2"
+  std::string algo_name() const {
+    return solvers_[0]->ca() ? "ca" : solvers_[0]->single_pass() ? "pcg1" : "pcg2";
+  }
   bool overlapped() const { return !drivers_.empty() && drivers_[0]->overlapped(); }
   bool poisoned() const { return !drivers_.empty() && drivers_[0]->poisoned(); }
   size_t device_bytes() const;
@@ -89,6 +93,7 @@ class Session {
   std::vector<double> local_w(int i = 0);
   // the per-tile partial sums (5 per tile slot) the last sweep wrote (tests of the reduction hand-off)
   std::vector<double> partials(int i = 0);
+  hipStream_t stream_of(int i) const;  // the compute stream of owned rank i
 
  private:
   void require_connected() const {
@@ -97,7 +102,6 @@ class Session {
   // f(driver index, driver) for every driver: inline, or one host thread per driver (each bound
   // to its rank's device) in threaded mode; the first exception is rethrown after all joined
   void for_drivers(const std::function<void(size_t, PcgDriver&)>& f);
-  hipStream_t stream_of(int i) const;  // the compute stream of owned rank i
   RunStats solve_impl(int poll_batches, bool do_init, int64_t every, const std::string& save_path);
 
   SessionConfig cfg_;
@@ -118,6 +122,6 @@ class Session {
 std::vector<std::vector<CommEvent>> record_comm_sequence(const ProblemSpec& spec, int world, Split split,
                                                          const GpuOptions& opt, int64_t iters);
 
-int64_t max_square_grid(double bytes_per_gpu, int gpus, DType dtype, double reserve_fraction = 0.1);
+int64_t max_square_grid(double bytes_per_gpu, int gpus, DType dtype, double reserve_fraction = 0.1, int algo = -1);
 
 }  // namespace pmx

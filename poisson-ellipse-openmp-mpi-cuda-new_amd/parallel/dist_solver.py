@@ -98,12 +98,14 @@ class DistGpuPCG:
                  overlap: bool = True, vec_b: int = 0, waves_b: int = 0, tile_rows_b: int = -1,
                  b_ring: bool = False, algo: int = -1, init_timeout: float = 90.0, device: int | None = None,
                  placement: int = 0, placement_budget_s: float = 0.5, placement_keep_free: float = 0.5,
-                 phase=None):
+                 phase=None, ca_s: int = 3, split_sweep: int = -1):
         """placement: candidate field blocks of the placement probe (0 = off; forced off when ranks share
         a device).  phase(name, seconds): progress-watchdog hook (bench.py's Watch.phase); called with
         "comm-init" before the blocking communicator initialisation, whose own watchdog is
         init_timeout.  overlap=False is the serialized schedule: one RCCL communicator, every call on
-        the compute stream in a fixed order."""
+        the compute stream in a fixed order.  algo: -1 = auto (the library's choose_algo: the s-step
+        PCG on big fp64 row strips where its fields fit), 1 / 2 / 3; ca_s: the s-step block size;
+        split_sweep: pcg1's split sweep (-1 = the transport's default, 0 off, 1 on)."""
         self.problem = problem
         self.info = info
         self.comm_kind = comm
@@ -134,7 +136,8 @@ class DistGpuPCG:
                     ranks=[info.rank], devices=[self.device], rccl_graph=rccl_graph, overlap=overlap,
                     vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b, b_ring=b_ring, algo=algo,
                     defer_connect=True, placement=placement, placement_budget_s=placement_budget_s,
-                    placement_keep_free=placement_keep_free, sharing=sharing)
+                    placement_keep_free=placement_keep_free, sharing=sharing, ca_s=ca_s,
+                    split_sweep=split_sweep)
             except Exception as e:  # sizing / allocation: reported collectively below
                 err = e
             agree(info, err is None, f"native solver setup ({err})" if err else "native solver setup",
@@ -161,7 +164,7 @@ class DistGpuPCG:
                     dtype=dtype, exact=exact, graph_batch=graph_batch, ranks=[info.rank], devices=[self.device],
                     overlap=overlap, vec_b=vec_b, waves_b=waves_b, tile_rows_b=tile_rows_b, b_ring=b_ring,
                     algo=algo, defer_connect=True, placement=placement, placement_budget_s=placement_budget_s,
-                    placement_keep_free=placement_keep_free, sharing=sharing)
+                    placement_keep_free=placement_keep_free, sharing=sharing, ca_s=ca_s, split_sweep=split_sweep)
                 mine = self.session.ipc_export()
             except Exception as e:
                 err, mine = e, b""

@@ -8,6 +8,10 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 PKG_NAME = "poisson-ellipse-openmp-mpi-cuda-new_amd"
+# The tests pin kernels and schedules with the library's study knobs (PMX_ALGO, PMX_PCG1_*, PMX_CA_*,
+# ...), which apply only in study mode (resolve_options); test_gpu_solver.py checks that they are
+# ignored without it.
+os.environ["PMX_STUDY"] = "1"
 
 
 def pytest_configure(config):

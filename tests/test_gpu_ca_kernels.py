@@ -1,0 +1,111 @@
+"""The s-step PCG's kernels, product by product, against plain PyTorch fp64 (models/sstep_pcg.py).
+
+pass 1 (k_ca_sweep, UPD = false) sums the 6s Gram products <Y_i, Y_j>_D of the Chebyshev basis
+Y = [P_0..P_s, Z_0..Z_{s-1}] of (p, z) -- the moment set of moment_gram -- per tile; pass 2 forms
+p = Y a, z = Y b, w += Y c and the ||Y a_j||^2 of the stop test; the fused pass (k_ca_fused) does pass
+2 and the NEXT block's pass 1 in one march.  Random fields, an undecomposed grid and a row strip with
+its s ghost rows; the ellipse cuts rows of every grid here (the cut-row face path).  End-to-end
+agreement (iteration counts, w) is in test_gpu_ca.py; this pins every product to rounding."""
+import importlib
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu(pkg):
+    assert torch.cuda.is_available() and pkg.load_native().device_count() > 0, "no HIP device"
+
+
+def prod_ij(s):
+    """(i, j) of the kernel's Gram product q (ca_kernels.hip: ca_prod_i / ca_prod_j)."""
+    out = []
+    for m in range(s + 1):
+        out.append((m, 0))
+    for m in range(s + 1, 2 * s + 1):
+        out.append(((m + 1) // 2, m // 2))
+    for m in range(s):
+        out.append((s + 1 + m, s + 1))
+    for m in range(s, 2 * s - 1):
+        out.append((s + 1 + (m + 1) // 2, s + 1 + m // 2))
+    for m in range(s + 1):
+        out.append((m, s + 1))
+    for b in range(1, s):
+        out.append((s, s + 1 + b))
+    assert len(out) == 6 * s
+    return out
+
+
+def _ref(pkg, M, N, s):
+    sp = importlib.import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.models.sstep_pcg")
+    return sp.TorchSStepPCG(pkg.PoissonEllipse(M=M, N=N), s=s)
+
+
+def _local(g, gi0, nx, gh):
+    """rows 1-gh .. nx+gh of a global (M+1) x (N+1) array (zero outside it)"""
+    M1, N1 = g.shape
+    out = np.zeros((nx + 2 * gh, N1))
+    for k, li in enumerate(range(1 - gh, nx + gh + 1)):
+        gi = gi0 + li
+        if 0 <= gi < M1:
+            out[k] = g[gi]
+    return out
+
+
+def _pad(x):
+    return np.pad(x, 1)
+
+
+def _close(got, want, scale, rtol, what):
+    err = np.abs(np.asarray(got) - np.asarray(want))
+    bad = err > rtol * np.asarray(scale) + 1e-300
+    assert not bad.any(), f"{what}: max err {err.max():.3e} at {np.argmax(err)}, scale {np.max(scale):.3e}"
+
+
+@pytest.mark.parametrize("s", [2, 3])
+@pytest.mark.parametrize("ranks,rank,fused", [(1, 0, False), (1, 0, True), (4, 1, False), (3, 2, False)])
+def test_ca_gram_products_and_updates(pkg, s, ranks, rank, fused):
+    M, N = 211, 300
+    rng = np.random.default_rng(1234 + 17 * s + ranks)
+    t = _ref(pkg, M, N, s)
+    pg = torch.from_numpy(rng.standard_normal((M - 1, N - 1)))
+    zg = torch.from_numpy(rng.standard_normal((M - 1, N - 1)))
+    wg = torch.from_numpy(rng.standard_normal((M - 1, N - 1)))
+    sess = pkg.make_session(pkg.PoissonEllipse(M=M, N=N), ranks=ranks, split="rows", algo="ca", ca_s=s,
+                            graph_batch=0)
+    sd = sess.subdomain(rank)
+    gi0, nx = sd["i_start"] - 1, sd["nx"]
+    gh = sess.ca_ghost_rows(rank)
+    nb = 2 * s + 1
+    coef = rng.standard_normal((3, nb))
+    pa = np.zeros((s, nb))
+    for j in range(s):  # a_j lives on P_0..P_j, Z_0..Z_{j-1} (the kernel reads only those)
+        pa[j, : j + 1] = rng.standard_normal(j + 1)
+        pa[j, s + 1: s + 1 + j] = rng.standard_normal(j)
+    pa[0] = 0.0
+    pa[0, 0] = 1.0
+    r = sess.ca_probe(rank, _local(_pad(zg.numpy()), gi0, nx, gh), _local(_pad(pg.numpy()), gi0, nx, gh),
+                      _local(_pad(wg.numpy()), gi0, nx, gh), coef, pa, fused)
+
+    Y = t._cheb(pg, s + 1) + t._cheb(zg, s)
+    rows = slice(gi0, gi0 + nx)  # the rank's owned rows of the interior arrays
+    D = t.D
+    comb = lambda v: sum(float(v[i]) * Y[i] for i in range(nb))  # noqa: E731
+    pn, zn = comb(coef[0]), comb(coef[1])
+    wn = wg + comb(coef[2])
+    ymax = max(float(y.abs().max()) for y in Y)
+    for name, want, c in (("p", pn, coef[0]), ("z", zn, coef[1]), ("w", wn, coef[2])):
+        _close(r[name], want[rows].numpy(), ymax * np.abs(c).sum() + (1.0 if name == "w" else 0.0), 1e-12, name)
+    # pass 2's norms ||Y a_j||^2 over the owned rows
+    for j in range(s):
+        v = comb(pa[j])[rows]
+        want = float((v * v).sum())
+        _close(r["norms"][j], want, want, 1e-12, f"norm {j}")
+    # the Gram products: pass 1 of (p, z) -- or, fused, of the new (p, z) (block b+1's basis)
+    B = t._cheb(pn, s + 1) + t._cheb(zn, s) if fused else Y
+    for q, (i, j) in enumerate(prod_ij(s)):
+        terms = (B[i] * D * B[j])[rows]
+        _close(r["gram"][q], float(terms.sum()), float(terms.abs().sum()), 1e-12, f"gram {q} <Y{i}, Y{j}>")
