@@ -716,10 +716,15 @@ def measure(args) -> int:
     if args.profile_phases > 0 and not dry:
         watch.phase("profile")
         ph = runner.profile(args.profile_phases)
+        ca = tile_desc.get("algo") == "ca"
         phases = {"phase_seconds_per_iter_max_over_ranks": {k: v / args.profile_phases for k, v in ph.items()},
-                  "phase_note": "compute = the whole fused sweep (A p, update, D^-1, A z); dot = the device "
-                                "reduction; comm = all-reduce + ghost exchange; copy and precond are 0 by "
-                                "construction (no host staging, D^-1 fused into the sweep)"}
+                  "phase_note": ("compute = the s-step passes (pass 1 / the fused pass: basis + Gram products; "
+                                 "pass 2: p, z, w); dot = the block reductions and scalars; comm = the 21-double "
+                                 "all-reduce + ghost-row exchange per block" if ca else
+                                 "compute = the whole fused sweep (A p, update, D^-1, A z); dot = the device "
+                                 "reduction; comm = all-reduce + ghost exchange") +
+                                "; copy and precond are 0 by construction (no host staging, D^-1 fused into "
+                                "the sweep)"}
         if info.rank == 0:
             print(f"[bench] {args.profile_phases} profiled iterations (MAX over {world} ranks):\n"
                   + ds.phase_table(ph), file=sys.stderr, flush=True)

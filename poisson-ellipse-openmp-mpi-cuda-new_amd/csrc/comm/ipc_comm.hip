@@ -326,8 +326,9 @@ class IpcComm final : public Comm {
       for (int q = 0; q < ms.n; ++q) {
         const HaloMsg& m = ms.m[q];
         PMX_CHECK(m.count == ca_count_ && ca_peer_buf_[m.slot] && P_.nbr[m.slot], "IpcComm: bad s-step span on slot " << m.slot);
-        const size_t mine = size_t(m.slot * 2 + m.field) * size_t(ca_count_) * sizeof(double);
-        const size_t theirs = size_t(opposite_slot(m.slot) * 2 + m.field) * size_t(ca_count_) * sizeof(double);
+        const size_t el = local_->layout().elem;  // fp64 or fp32 fields
+        const size_t mine = size_t(m.slot * 2 + m.field) * size_t(ca_count_) * el;
+        const size_t theirs = size_t(opposite_slot(m.slot) * 2 + m.field) * size_t(ca_count_) * el;
         pack.nbr[q] = nullptr;
         pack.src[q] = m.send;
         pack.dst[q] = ca_buf_ + mine;
@@ -341,11 +342,17 @@ class IpcComm final : public Comm {
       if (ms.n) {
         const dim3 grid(std::max(1, std::min(64, (maxc + 255) / 256)), ms.n);
         hipLaunchKernelGGL(k_ipc_wait_acks, dim3(1), dim3(64), 0, streams[0], P_, me, local_->state_dev(), timeout_);
-        hipLaunchKernelGGL(k_ipc_pull_spans<double>, grid, dim3(256), 0, streams[0], P_, pack, me,
-                           local_->state_dev(), timeout_);
+        auto spans = [&](const IpcSpans& sp) {
+          if (local_->layout().elem == 8)
+            hipLaunchKernelGGL(k_ipc_pull_spans<double>, grid, dim3(256), 0, streams[0], P_, sp, me,
+                               local_->state_dev(), timeout_);
+          else
+            hipLaunchKernelGGL(k_ipc_pull_spans<float>, grid, dim3(256), 0, streams[0], P_, sp, me,
+                               local_->state_dev(), timeout_);
+        };
+        spans(pack);
         hipLaunchKernelGGL(k_ipc_post, dim3(1), dim3(64), 0, streams[0], P_, me);
-        hipLaunchKernelGGL(k_ipc_pull_spans<double>, grid, dim3(256), 0, streams[0], P_, pull, me,
-                           local_->state_dev(), timeout_);
+        spans(pull);
         hipLaunchKernelGGL(k_ipc_ack, dim3(1), dim3(64), 0, streams[0], P_, me);
       }
       HIP_CHECK(hipGetLastError());

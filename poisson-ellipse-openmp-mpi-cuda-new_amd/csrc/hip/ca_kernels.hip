@@ -1370,7 +1370,7 @@ void launch_ca_init(const DevGeom& G, const DevTables& Tb, T* z, T* p, hipStream
 template <typename T>
 void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, T* p0, T* p1, double* partials,
                      const PcgState* S, const CaState* C, const CaTiles& t, bool upd, hipStream_t s,
-                     hipStream_t sframe) {
+                     hipStream_t sframe, hipEvent_t frame_wait) {
   PMX_CHECK((G.nb & ~(kNbXlo | kNbXhi)) == 0, "s-step PCG runs undecomposed grids or row strips");
   if (!sframe) sframe = s;
   PMX_CHECK(t.tbl != nullptr && t.fa != nullptr && t.fb != nullptr, "s-step PCG: row-class / face tables missing");
@@ -1387,14 +1387,18 @@ void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, 
 #define PMX_CA_K(SS, U, MW, D, PT, PP, NB)                                                                          \
   do {                                                                                                              \
     if ((NB) > 0)                                                                                                   \
-      hipLaunchKernelGGL((k_ca_sweep<T, SS, U, MW, D, PT>), dim3(NB), dim3(64), 0, (PT) == 2 ? sframe : s, G, Tb, w, \
+      hipLaunchKernelGGL((k_ca_sweep<T, SS, U, MW, (D) && sizeof(T) == 8, PT>), dim3(NB), dim3(64), 0,            \
+                         (PT) == 2 ? sframe : s, G, Tb, w,                                                           \
                          z0, z1, p0, p1, partials, S, C, rows, t.tiles_j, t.tbl, t.cwords, pbase, F, PP, n);        \
   } while (0)
   // split (default): the interior tiles with the fast-only kernel at 3 waves per SIMD, the frame with
   // the general one at 2; else every tile general at waves_gram / waves_upd
+  // the tiles that read ghost rows -- the frame on sframe, or every tile on s -- wait for frame_wait
+  const bool split = (upd ? t.split_upd : t.split) && nin > 0;
+  if (frame_wait) HIP_CHECK(hipStreamWaitEvent(split ? sframe : s, frame_wait, 0));
 #define PMX_CA(SS)                                                                                                   \
   do {                                                                                                               \
-    if ((upd ? t.split_upd : t.split) && nin > 0) {                                                                  \
+    if (split) {                                                                                                     \
       if (upd) {                                                                                                     \
         PMX_CA_K(SS, true, 2, false, 2, P2, n - nin);                                                                \
         PMX_CA_K(SS, true, 3, false, 1, P1, nin);                                                                    \
@@ -1423,8 +1427,9 @@ void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, 
 
 template <typename T>
 void launch_ca_fused(const DevGeom& G, T* w, T* z0, T* z1, T* p0, T* p1, double* partials, const CaState* C,
-                     const CaTiles& t, hipStream_t s, hipStream_t sframe) {
-  PMX_CHECK(G.nb == 0, "the fused s-step pass runs undecomposed grids");
+                     const CaTiles& t, hipStream_t s, hipStream_t sframe, hipEvent_t frame_wait) {
+  PMX_CHECK((G.nb & ~(kNbXlo | kNbXhi)) == 0 && (G.nb == 0 || t.gh >= 2 * t.s),
+            "the fused s-step pass runs undecomposed grids or row strips with 2 s ghost rows");
   PMX_CHECK(t.fuse && t.tbl_f != nullptr && t.fa != nullptr && t.fb != nullptr,
             "s-step PCG: fused tiling / row classes / face tables missing");
   if (!sframe) sframe = s;
@@ -1439,9 +1444,11 @@ void launch_ca_fused(const DevGeom& G, T* w, T* z0, T* z1, T* p0, T* p1, double*
       hipLaunchKernelGGL((k_ca_fused<T, SS, MW, PT>), dim3(NB), dim3(128), 0, (PT) == 2 ? sframe : s, G, w, z0, z1, \
                          p0, p1, partials, C, t.rows_f, t.tiles_j_f, t.tbl_f, t.cwords, F, PP, n);                 \
   } while (0)
+  const bool split = t.split_f && nin > 0;
+  if (frame_wait) HIP_CHECK(hipStreamWaitEvent(split ? sframe : s, frame_wait, 0));
 #define PMX_CAF(SS)                                     \
   do {                                                  \
-    if (t.split_f && nin > 0) {                         \
+    if (split) {                                        \
       PMX_CAF_K(SS, 2, 2, P2, n - nin);                 \
       if (t.waves_f == 3) PMX_CAF_K(SS, 3, 1, P1, nin); \
       else PMX_CAF_K(SS, 2, 1, P1, nin);                \
@@ -1481,11 +1488,15 @@ void launch_ca_finish(int s_, double h, double wdiff, int nmax, bool check_only,
   HIP_CHECK(hipGetLastError());
 }
 
-template void launch_ca_init<double>(const DevGeom&, const DevTables&, double*, double*, hipStream_t);
-template void launch_ca_sweep<double>(const DevGeom&, const DevTables&, double*, double*, double*, double*, double*,
-                                      double*, const PcgState*, const CaState*, const CaTiles&, bool, hipStream_t,
-                                      hipStream_t);
-template void launch_ca_fused<double>(const DevGeom&, double*, double*, double*, double*, double*, double*,
-                                      const CaState*, const CaTiles&, hipStream_t, hipStream_t);
+// fp64 and fp32 storage of w, z, p (the basis, the updates and the Gram sums in fp64 registers either way)
+#define PMX_CA_INST(T)                                                                                            \
+  template void launch_ca_init<T>(const DevGeom&, const DevTables&, T*, T*, hipStream_t);                         \
+  template void launch_ca_sweep<T>(const DevGeom&, const DevTables&, T*, T*, T*, T*, T*, double*, const PcgState*, \
+                                   const CaState*, const CaTiles&, bool, hipStream_t, hipStream_t, hipEvent_t);   \
+  template void launch_ca_fused<T>(const DevGeom&, T*, T*, T*, T*, T*, double*, const CaState*, const CaTiles&,    \
+                                   hipStream_t, hipStream_t, hipEvent_t);
+PMX_CA_INST(double)
+PMX_CA_INST(float)
+#undef PMX_CA_INST
 
 }  // namespace pmx

@@ -287,11 +287,16 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   if (opt_.algo == -1) opt_.algo = choose_algo(spec, sd.grid, opt_, double(total_b), 1, false);
   pcg1_ = opt_.algo == 1;
   ca_ = opt_.algo == 3;
-  PMX_CHECK(!ca_ || (opt.dtype == DType::kFp64 && !opt.exact && sd.grid.Py == 1 && sd.nx >= opt.ca_s),
-            "s-step PCG (algo 3) runs fp64 grids with the fast arithmetic, undecomposed or as row strips of at "
-            "least s rows");
-  // ghost rows per side: 2 (the single-pass radius-2 halo); a decomposed s-step strip needs s = 3
-  gh_ = ca_ && sd.grid.size() > 1 ? 3 : 2;
+  PMX_CHECK(!ca_ || (!opt.exact && sd.grid.Py == 1 && sd.nx >= opt.ca_s),
+            "s-step PCG (algo 3) runs the fast arithmetic, undecomposed or as row strips of at least s rows");
+  // the s-step's fused pass (GpuOptions::ca_fuse) reads radius 2s: on strips every strip must hold 2s
+  // rows -- decided from global data, so every rank runs the same schedule
+  const bool fuse_ok = sd.grid.size() == 1 || (spec.M - 1) / sd.grid.Px >= 2 * opt_.ca_s;
+  PMX_CHECK(!ca_ || opt_.ca_fuse != 1 || fuse_ok, "the fused s-step pass needs row strips of at least 2 s rows");
+  ca_fuse_ = ca_ && (opt_.ca_fuse == 1 || (opt_.ca_fuse == -1 && fuse_ok));
+  // ghost rows per side: 2 (the single-pass radius-2 halo); a decomposed s-step strip needs s, 2s with
+  // the fused pass
+  gh_ = ca_ && sd.grid.size() > 1 ? (ca_fuse_ ? 2 * opt_.ca_s : opt_.ca_s) : 2;
   PMX_CHECK(!pcg1_ || (!opt.exact && opt.kernel == 1 && (sd.grid.size() == 1 || (sd.nx >= 2 && sd.ny >= 2))),
             "pcg1 needs the wave kernels, the fast arithmetic and a subdomain of at least 2 x 2 nodes");
 
@@ -422,23 +427,24 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   if (ca_) {
     r2_ = field_raw(4);  // the second z buffer
     ca_tiles_ = make_ca_tiles(ca_geom_, opt_.ca_s, opt_.ca_rows, opt_.ca_rows2, opt_.ca_rows_f);
-    // the fused pass: undecomposed grids (a strip's ghost rows hold radius s, the fused march reads 2s)
-    PMX_CHECK(opt_.ca_fuse != 1 || geom_.nb == 0, "the fused s-step pass runs undecomposed grids");
-    ca_tiles_.fuse = opt_.ca_fuse == 1 || (opt_.ca_fuse == -1 && geom_.nb == 0) ? 1 : 0;
+    ca_tiles_.fuse = ca_fuse_ ? 1 : 0;
     if (const char* e = study_env("PMX_CA_WAVES_F"); e && e[0]) ca_tiles_.waves_f = std::atoi(e);
     if (const char* e = study_env("PMX_CA_SPLIT_F"); e && e[0]) ca_tiles_.split_f = std::atoi(e);
     PMX_CHECK(ca_tiles_.waves_f == 2 || ca_tiles_.waves_f == 3, "s-step PCG: fused waves per SIMD must be 2 or 3");
     // the face coefficients of every node, read on the rows the ellipse cuts (2 more field-sized arrays)
-    HIP_CHECK(hipMalloc(&ca_faces_, 2 * field_bytes_));
-    ca_tiles_.fa = reinterpret_cast<const double*>(ca_faces_ + field_off_ * elem_);
-    ca_tiles_.fb = reinterpret_cast<const double*>(ca_faces_ + field_bytes_ + field_off_ * elem_);
+    // fp64 whatever the fields' storage, in the fields' pitch (elements); column 1 of every row 256-B aligned
+    const size_t face_off = size_t(gh_ - 1) * size_t(geom_.pitch) + 31;
+    ca_face_bytes_ = round_up((31 + size_t(sd.nx + 2 * gh_) * size_t(geom_.pitch)) * 8, 256);
+    HIP_CHECK(hipMalloc(&ca_faces_, 2 * ca_face_bytes_));
+    ca_tiles_.fa = reinterpret_cast<const double*>(ca_faces_ + face_off * 8);
+    ca_tiles_.fb = reinterpret_cast<const double*>(ca_faces_ + ca_face_bytes_ + face_off * 8);
     ca_tiles_.gh = ca_gh_;
     ca_build_faces(ca_geom_, ca_tables_, const_cast<double*>(ca_tiles_.fa), const_cast<double*>(ca_tiles_.fb), ca_gh_, nullptr);
     const bool split = opt_.ca_split == -1 ? geom_.nb != 0 : opt_.ca_split == 1;  // see GpuOptions::ca_split
     if (!split) ca_tiles_.split = 0;
     if (!(opt_.ca_split_upd == -1 ? split : opt_.ca_split_upd == 1)) ca_tiles_.split_upd = 0;
     if (!ca_tiles_.split) ca_tiles_.split_upd = ca_tiles_.split_upd && opt_.ca_split_upd == 1;
-    ca_tiles_.dma = opt_.ca_dma == -1 ? int(split) : opt_.ca_dma;
+    ca_tiles_.dma = elem_ == 8 ? (opt_.ca_dma == -1 ? int(split) : opt_.ca_dma) : 0;  // LDS-DMA rows: fp64
     if (ca_tiles_.split && opt_.ca_frame_stream) {
       HIP_CHECK(hipStreamCreateWithFlags(&ca_side_, hipStreamNonBlocking));
       HIP_CHECK(hipEventCreateWithFlags(&ca_ev_fork_, hipEventDisableTiming));
@@ -716,9 +722,10 @@ size_t GpuSubdomainSolver::estimate_device_bytes(const ProblemSpec& spec, const 
 size_t GpuSubdomainSolver::estimate_device_bytes_algo(const ProblemSpec& spec, const Subdomain& sd, DType dtype,
                                                       int algo) {
   if (algo != 3) return estimate_device_bytes(spec, sd, dtype, algo == 1);
-  // s-step: w, two (z, p) sets and the two face fields, rows -gh+1 .. nx+gh (gh = 3 on strips)
+  // s-step: w, two (z, p) sets and the two face fields, rows -gh+1 .. nx+gh (gh = 2s = 6 on strips: the
+  // fused pass)
   const size_t elem = dtype == DType::kFp64 ? 8 : 4, align = 256 / elem;
-  const int gh = sd.grid.size() > 1 ? 3 : 2;
+  const int gh = sd.grid.size() > 1 ? 2 * kCaMaxS : 2;
   const size_t pitch = round_up(size_t(sd.ny + 2 + 8), align);
   const size_t field = round_up((align - 1 + size_t(sd.nx + 2 * gh) * pitch) * elem, 256);
   const size_t face = round_up((31 + size_t(sd.nx + 2 * gh) * pitch) * 8, 256);
@@ -732,7 +739,7 @@ size_t GpuSubdomainSolver::device_bytes() const {
   const size_t tables = (4 * size_t(spec_.M + 2) + 4 * size_t(spec_.N + 2)) * sizeof(double) +
                         8 * size_t(spec_.M + 2) * sizeof(int);
   return (r2_ ? 5 : 4) * field_stride_ + tables + (npart_ * 5 + kReduceWsDoubles) * sizeof(double) +
-         (own_arena_ ? layout_.bytes : 0) + (ca_faces_ ? 2 * field_bytes_ : 0);
+         (own_arena_ ? layout_.bytes : 0) + (ca_faces_ ? 2 * ca_face_bytes_ : 0);
 }
 
 void* GpuSubdomainSolver::field_base(int which) const {
@@ -788,38 +795,43 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
   launch_reduce(partials_, init_tiles_.ntiles(), 2, 0.0, g_.h1h2, state_->red_b, state_, 0, reduce_ws_, s);
   after_launch(s);
   if (ca_) {  // set 0: z^0 = D^-1 r^0 (in r's buffer), p^0 = z^0; block counter 0
-    if constexpr (sizeof(T) == 8) {
-      std::memset(&ca_init_, 0, sizeof(CaState));
-      ca_init_.s = ca_tiles_.s;  // (checked by load_checkpoint)
-      HIP_CHECK(hipMemcpyAsync(ca_state_, &ca_init_, sizeof(CaState), hipMemcpyHostToDevice, s));
-      ca_blk_ = 0;
-      launch_ca_init<double>(ca_geom_, ca_tables_, static_cast<double*>(field_base(1)), static_cast<double*>(field_base(2)), s);
-      after_launch(s);
-    }
+    std::memset(&ca_init_, 0, sizeof(CaState));
+    ca_init_.s = ca_tiles_.s;  // (checked by load_checkpoint)
+    HIP_CHECK(hipMemcpyAsync(ca_state_, &ca_init_, sizeof(CaState), hipMemcpyHostToDevice, s));
+    ca_blk_ = 0;
+    launch_ca_init<T>(ca_geom_, ca_tables_, static_cast<T*>(field_base(1)), static_cast<T*>(field_base(2)), s);
+    after_launch(s);
   }
 }
 
-// One s-step pass: with the split kernels the frame tiles run on a side stream, concurrently with the
-// interior (their few long marches would otherwise trail the pass by ~0.1 ms)
-void GpuSubdomainSolver::ca_sweep(hipStream_t s, bool upd) {
-  double* w = static_cast<double*>(field_base(0));
-  double* z0 = static_cast<double*>(field_base(1));
-  double* z1 = reinterpret_cast<double*>(r2_ + field_off_ * elem_);
-  double* p0 = static_cast<double*>(field_base(2));
-  double* p1 = static_cast<double*>(field_base(3));
-  hipEvent_t wait = upd ? nullptr : ca_frame_wait_;
-  if (!upd) ca_frame_wait_ = nullptr;
+// One s-step pass (kind 0: pass 1, 1: pass 2, 2: the fused pass): with the split kernels the frame tiles
+// run on a side stream, concurrently with the interior (their few long marches would otherwise trail
+// the pass by ~0.1 ms).  The first pass after a ghost exchange (pass 1 or the fused pass; with the fused
+// schedule also the batch's last pass 2) waits for it in the tiles that read ghost rows.
+template <typename T>
+void GpuSubdomainSolver::ca_pass_impl(hipStream_t s, int kind) {
+  T* w = static_cast<T*>(field_base(0));
+  T* z0 = static_cast<T*>(field_base(1));
+  T* z1 = reinterpret_cast<T*>(r2_ + field_off_ * elem_);
+  T* p0 = static_cast<T*>(field_base(2));
+  T* p1 = static_cast<T*>(field_base(3));
+  hipEvent_t wait = ca_frame_wait_;
+  ca_frame_wait_ = nullptr;
+  auto launch = [&](hipStream_t side) {
+    if (kind == 2)
+      launch_ca_fused<T>(ca_geom_, w, z0, z1, p0, p1, partials_, ca_state_, ca_tiles_, s, side, wait);
+    else
+      launch_ca_sweep<T>(ca_geom_, ca_tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, kind == 1,
+                         s, side, wait);
+  };
   if (ca_side_) {
     HIP_CHECK(hipEventRecord(ca_ev_fork_, s));
     HIP_CHECK(hipStreamWaitEvent(ca_side_, ca_ev_fork_, 0));
-    if (wait) HIP_CHECK(hipStreamWaitEvent(ca_side_, wait, 0));  // the frame reads the ghost rows
-    launch_ca_sweep<double>(ca_geom_, ca_tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, upd, s,
-                            ca_side_);
+    launch(ca_side_);
     HIP_CHECK(hipEventRecord(ca_ev_join_, ca_side_));
     HIP_CHECK(hipStreamWaitEvent(s, ca_ev_join_, 0));
   } else {
-    if (wait) HIP_CHECK(hipStreamWaitEvent(s, wait, 0));
-    launch_ca_sweep<double>(ca_geom_, ca_tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, upd, s);
+    launch(nullptr);
   }
   after_launch(s);
 }
@@ -836,31 +848,19 @@ void GpuSubdomainSolver::drop_side_stream() {
 }
 
 void GpuSubdomainSolver::enqueue_ca_pass(hipStream_t s, bool upd) {
-  PMX_CHECK(ca_ && elem_ == 8, "not an s-step solver");
-  ca_sweep(s, upd);
+  PMX_CHECK(ca_, "not an s-step solver");
+  if (elem_ == 8) ca_pass_impl<double>(s, upd ? 1 : 0);
+  else ca_pass_impl<float>(s, upd ? 1 : 0);
 }
 
 void GpuSubdomainSolver::enqueue_ca_fused(hipStream_t s) {
-  PMX_CHECK(ca_fused() && elem_ == 8, "not an s-step solver with the fused pass");
-  double* w = static_cast<double*>(field_base(0));
-  double* z0 = static_cast<double*>(field_base(1));
-  double* z1 = reinterpret_cast<double*>(r2_ + field_off_ * elem_);
-  double* p0 = static_cast<double*>(field_base(2));
-  double* p1 = static_cast<double*>(field_base(3));
-  if (ca_side_) {  // the frame tiles on the side stream, as ca_sweep
-    HIP_CHECK(hipEventRecord(ca_ev_fork_, s));
-    HIP_CHECK(hipStreamWaitEvent(ca_side_, ca_ev_fork_, 0));
-    launch_ca_fused<double>(ca_geom_, w, z0, z1, p0, p1, partials_, ca_state_, ca_tiles_, s, ca_side_);
-    HIP_CHECK(hipEventRecord(ca_ev_join_, ca_side_));
-    HIP_CHECK(hipStreamWaitEvent(s, ca_ev_join_, 0));
-  } else {
-    launch_ca_fused<double>(ca_geom_, w, z0, z1, p0, p1, partials_, ca_state_, ca_tiles_, s);
-  }
-  after_launch(s);
+  PMX_CHECK(ca_fused(), "not an s-step solver with the fused pass");
+  if (elem_ == 8) ca_pass_impl<double>(s, 2);
+  else ca_pass_impl<float>(s, 2);
 }
 
 void GpuSubdomainSolver::enqueue_ca_reduce(hipStream_t s, int n, bool check_only, bool finish, bool fused) {
-  PMX_CHECK(ca_ && elem_ == 8, "not an s-step solver");
+  PMX_CHECK(ca_, "not an s-step solver");
   PMX_CHECK(!fused || ca_fused(), "fused reduction without the fused pass");
   const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
   // after the fused pass both the Gram products and the norms come from its tiling
@@ -876,7 +876,7 @@ void GpuSubdomainSolver::enqueue_ca_reduce(hipStream_t s, int n, bool check_only
 }
 
 void GpuSubdomainSolver::enqueue_ca_finish(hipStream_t s, int n, bool check_only) {
-  PMX_CHECK(ca_ && elem_ == 8, "not an s-step solver");
+  PMX_CHECK(ca_, "not an s-step solver");
   const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
   launch_ca_finish(ca_tiles_.s, g_.h1h2, wdiff, check_only ? 1 : n, check_only, state_, ca_state_, s, progress_dev_);
   after_launch(s);
@@ -885,7 +885,7 @@ void GpuSubdomainSolver::enqueue_ca_finish(hipStream_t s, int n, bool check_only
 GpuSubdomainSolver::CaProbe GpuSubdomainSolver::ca_probe(const std::vector<double>& z, const std::vector<double>& p,
                                                          const std::vector<double>& w, const std::vector<double>& coef,
                                                          const std::vector<double>& pa, bool fused, hipStream_t s) {
-  PMX_CHECK(ca_ && elem_ == 8, "ca_probe: not an s-step solver");
+  PMX_CHECK(ca_ && elem_ == 8, "ca_probe: not an fp64 s-step solver");
   PMX_CHECK(!fused || ca_fused(), "ca_probe: the fused pass runs undecomposed grids");
   const int S = ca_tiles_.s, NB = 2 * S + 1, NQ = 6 * S;
   const size_t rows = size_t(sd_.nx + 2 * gh_), cols = size_t(sd_.ny + 2);
@@ -963,10 +963,11 @@ void GpuSubdomainSolver::set_direct_rows(bool on) {
 HaloMsgs GpuSubdomainSolver::ca_halo_msgs(int set) const {
   PMX_CHECK(ca_, "ca_halo_msgs: not an s-step solver");
   HaloMsgs out;
-  // s-step strips: the s owned edge rows of z and p of the set the next block reads (CaState::blk
-  // & 1, mirrored by ca_blk_) into the neighbour's s ghost rows, as ONE span per field: rows q,
-  // q+1 whole, row q+2's columns 0 .. ny+1 (columns <= 0 and >= ny+1 are Dirichlet on a strip)
-  const int s = ca_tiles_.s;
+  // s-step strips: the gh owned edge rows of z and p of the set the next block reads (CaState::blk
+  // & 1, mirrored by ca_blk_) into the neighbour's gh ghost rows (gh = s, 2s with the fused pass), as
+  // ONE span per field: rows q .. q+gh-2 whole, row q+gh-1's columns 0 .. ny+1 (columns <= 0 and >= ny+1
+  // are Dirichlet on a strip)
+  const int s = gh_;
   char* fz = set ? r2_ + field_off_ * elem_ : static_cast<char*>(field_base(1));
   char* fp = static_cast<char*>(field_base(set ? 3 : 2));
   const int64_t P = geom_.pitch;
@@ -1694,18 +1695,8 @@ void PcgDriver::enqueue_ca(int64_t n, const std::function<void(int)>& mark) {
     }
   };
   const bool ar = comm_->world_size() > 1;
-  while (n > 0) {
-    const int m = int(std::min<int64_t>(s, n));
-    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, false); });
-    mk(kPhA);
-    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_reduce(st, m, false, false); });
-    mk(kPhRed);
-    comm_->allreduce(local_, 3, streams_);
-    if (ar) mk(kPhAr);
-    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_finish(st, m, false); });
-    mk(kPhRed);
-    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, true); });
-    mk(kPhB);
+  // the s ghost rows of the (z, p) set just written (2s with the fused pass)
+  auto exchange = [&] {
     if (any_nb_ && ovl) {
       for_each_stream([&](size_t i, size_t u) {
         HIP_CHECK(hipEventRecord(ev_packed_[u], streams_[i]));
@@ -1719,7 +1710,38 @@ void PcgDriver::enqueue_ca(int64_t n, const std::function<void(int)>& mark) {
       comm_->halo(local_, streams_);
       mk(kPhHalo);
     }
+  };
+  // Unfused, per block: pass 1 -> reduce -> all-reduce -> scalars -> pass 2 -> exchange.  Fused: pass 1
+  // -> reduce -> all-reduce -> scalars, then per further block fused pass -> exchange (under the
+  // reduction, all-reduce and scalars) -> ..., and the last block's pass 2 -> exchange.  Every rank runs
+  // the same schedule (ca_fused() is decided from global data).
+  const bool fused = local_[0]->ca_fused();
+  bool first = true;
+  while (n > 0) {
+    const int m = int(std::min<int64_t>(s, n));
+    const bool f = fused && !first;
+    if (f) each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_fused(st); });
+    else each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, false); });
+    mk(kPhA);
+    if (f) exchange();
+    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_reduce(st, m, false, false, f); });
+    mk(kPhRed);
+    comm_->allreduce(local_, 3, streams_);
+    if (ar) mk(kPhAr);
+    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_finish(st, m, false); });
+    mk(kPhRed);
+    if (!fused) {
+      each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, true); });
+      mk(kPhB);
+      exchange();
+    }
+    first = false;
     n -= m;
+  }
+  if (fused) {
+    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, true); });
+    mk(kPhB);
+    exchange();
   }
   each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_reduce(st, 1, true, false); });
   mk(kPhRed);

@@ -274,7 +274,7 @@ class GpuSubdomainSolver {
   // buffers (a row span, padding included, is contiguous).  The driver turns it on when its
   // communicator moves arbitrary device spans (Comm::direct_rows).
   bool can_direct_rows() const {
-    return (pcg1_ || ca_) && (geom_.nb & ~(kNbXlo | kNbXhi)) == 0 && sd_.nx >= (ca_ ? ca_tiles_.s : 2);
+    return (pcg1_ || ca_) && (geom_.nb & ~(kNbXlo | kNbXhi)) == 0 && sd_.nx >= (ca_ ? gh_ : 2);
   }
   void set_direct_rows(bool on);
   bool direct_rows() const { return direct_rows_; }
@@ -422,12 +422,14 @@ class GpuSubdomainSolver {
   hipStream_t ca_side_ = nullptr;  // the frame tiles' stream (split kernels)
   hipEvent_t ca_ev_fork_ = nullptr, ca_ev_join_ = nullptr;
   hipEvent_t ca_frame_wait_ = nullptr;  // one-shot: the next pass 1's frame tiles wait for it
-  void ca_sweep(hipStream_t s, bool upd);
+  template <typename T> void ca_pass_impl(hipStream_t s, int kind);  // 0 pass 1, 1 pass 2, 2 fused
+  size_t ca_face_bytes_ = 0;    // one face-coefficient field (fp64)
   CaState* ca_state_ = nullptr;
   CaState ca_init_{};           // host template of the state init() uploads
   double* ca_chunk_ = nullptr;  // its reduction's chunk sums
   long long ca_blk_ = 0;        // blocks enqueued since init (CaState::blk's host mirror)
   int gh_ = 2;                  // ghost rows of the fields on each side
+  bool ca_fuse_ = false;        // the s-step's fused pass (GpuOptions::ca_fuse, decided at construction)
   // the s-step kernels' geometry and face tables: geom_ / tables_, or under ca_dirichlet a standalone
   // grid of the subdomain's rows (gi0 = 0, M = nx + 1, tables shifted by gi0), whose rows 0 and nx + 1
   // are boundary rows (the kernels tell boundary from interior rows by the global row index)

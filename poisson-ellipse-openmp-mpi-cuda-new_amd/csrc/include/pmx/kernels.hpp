@@ -178,16 +178,17 @@ void ca_build_faces(const DevGeom& G, const DevTables& Tb, double* fa, double* f
 template <typename T>
 void launch_ca_init(const DevGeom& G, const DevTables& Tb, T* z, T* p, hipStream_t s);
 template <typename T>
-// sframe: the stream of the frame tiles' kernel with t.split (nullptr: s); the caller forks and joins it
+// sframe: the stream of the frame tiles' kernel with t.split (nullptr: s); the caller forks and joins it.
+// frame_wait: an event the tiles that read ghost rows wait for (the frame on sframe, or the whole pass)
 void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, T* p0, T* p1, double* partials,
                      const PcgState* S, const CaState* C, const CaTiles& t, bool upd, hipStream_t s,
-                     hipStream_t sframe = nullptr);
+                     hipStream_t sframe = nullptr, hipEvent_t frame_wait = nullptr);
 // the fused pass (undecomposed grids, t.fuse): after the reduction of block b, block b's update and
 // block b+1's Gram partials (the reduction then takes n = n2 = t.ntilesf()); a pending rewind instead
 // rewinds w.  t.tbl_f: the fused tiling's row classes (ca_build_classes with fused = true).
 template <typename T>
 void launch_ca_fused(const DevGeom& G, T* w, T* z0, T* z1, T* p0, T* p1, double* partials, const CaState* C,
-                     const CaTiles& t, hipStream_t s, hipStream_t sframe = nullptr);
+                     const CaTiles& t, hipStream_t s, hipStream_t sframe = nullptr, hipEvent_t frame_wait = nullptr);
 // chunk: kCaReduceMaxBlocks * ca_nq(s) doubles of workspace; nmax: iterations this block may run
 constexpr int kCaReduceMaxBlocks = 256;
 // check_only: the pending stop test alone (after the last block of a batch; pass 2 then rewinds w if

@@ -66,7 +66,8 @@ def _close(got, want, scale, rtol, what):
 
 
 @pytest.mark.parametrize("s", [2, 3])
-@pytest.mark.parametrize("ranks,rank,fused", [(1, 0, False), (1, 0, True), (4, 1, False), (3, 2, False)])
+@pytest.mark.parametrize("ranks,rank,fused", [(1, 0, False), (1, 0, True), (4, 1, False), (3, 2, False), (4, 1, True),
+                                             (3, 2, True)])
 def test_ca_gram_products_and_updates(pkg, s, ranks, rank, fused):
     M, N = 211, 300
     rng = np.random.default_rng(1234 + 17 * s + ranks)

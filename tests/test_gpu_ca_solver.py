@@ -146,7 +146,7 @@ def test_study_knobs_are_ignored_outside_study_mode(pkg, monkeypatch):
 
 def _sequences(native, pkg, world, M, N, graph_batch, iters, overlap=True):
     spec = pkg.PoissonEllipse(M=M, N=N).to_native()
-    return native.record_comm_sequence(spec, world, native.Split.auto, graph_batch, iters, overlap=overlap, algo=3)
+    return native.record_comm_sequence(spec, world, native.Split.rows, graph_batch, iters, overlap=overlap, algo=3)
 
 
 @pytest.mark.parametrize("graph_batch,iters", [(0, 8), (32, 8), (4, 10), (32, 40)])
