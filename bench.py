@@ -579,10 +579,9 @@ def measure(args) -> int:
     # that moves its ghost rows straight between the fields: RCCL or IPC, not torch) and its 7 fields
     # fit, else pcg1 / pcg2.  The JSON's config.tile.algo says which ran.
     strips = world == 1 or process_grid(world, args.M, args.N, args.split)[1] == 1
-    ca_ok = (args.dtype == "fp64" and not args.exact and strips and
-             (world == 1 or cfg["comm"] in ("native", "ipc")))
+    ca_ok = not args.exact and strips and (world == 1 or cfg["comm"] in ("native", "ipc"))
     if args.algo == "ca" and not ca_ok:
-        raise SystemExit("[bench] --algo ca (the s-step PCG) needs fp64, row strips and the RCCL or IPC transport")
+        raise SystemExit("[bench] --algo ca (the s-step PCG) needs row strips and the RCCL or IPC transport")
     algo_id = {"auto": -1, "pcg1": 1, "pcg2": 2, "ca": 3}[args.algo]
     if dry:
         tp = importlib.import_module(pkg_name + ".models.torch_pcg")
@@ -807,9 +806,9 @@ def measure_loopback(args) -> int:
     # the algorithm the real N-GPU run would use (see measure: the s-step PCG on big fp64 row strips)
     decomp = importlib.import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.parallel.decomp")
     strips = decomp.process_grid(args.gpus, args.M, args.N, args.split)[1] == 1
-    ca_ok = args.dtype == "fp64" and not args.exact and strips
+    ca_ok = not args.exact and strips
     if args.algo == "ca" and not ca_ok:
-        raise SystemExit("[bench] --algo ca (the s-step PCG) needs fp64 and row strips")
+        raise SystemExit("[bench] --algo ca (the s-step PCG) needs row strips")
     algo_id = {"auto": -1, "pcg1": 1, "pcg2": 2, "ca": 3}[args.algo]  # auto: the library's choose_algo
     s = native.Session(problem.to_native(), world=args.gpus, comm="loopback", split=getattr(native.Split, args.split),
                        ranks=[args.loopback_rank], devices=[0], dtype=args.dtype, graph_batch=args.graph_batch,

@@ -16,6 +16,10 @@ Fixed studies (STUDIES) and parametrised ones (`<study> -- <arguments>`):
     validate  -- GPU suite, smoke(), default bench
     share     -- rank counts: supervised multi-rank rehearsal on the one GPU
     cli       -- quoted pmx argument strings
+    loopback  -- GPUS:RANK[:ENV=V,..]: one rank of an N-GPU job alone on the GPU (per-rank iteration)
+    ca_ab     -- bench/probe/ca_env_ab.py arguments: same-process A/B of s-step knobs
+    algos     -- MxN:algo:dtype: bench.py per grid x algorithm x storage
+    counters  -- kernel trace + SQ / EA counter passes of one bench.py configuration
 Studies that back kept profiles name themselves in the profile's README; bench/RETIRED.md maps
 the round-1/2 one-off gpu_*.sh scripts onto these.
 """
@@ -133,7 +137,7 @@ def pmc_study(study: str, configs: dict[str, str], args: str, passes=("ea_rd", "
     steps = []
     for tag, env in configs.items():
         for p in passes:
-            pre = f"env {env} " if env else ""
+            pre = f"env PMX_STUDY=1 {env} "  # the library applies PMX_* knobs only in study mode
             steps.append((f"{tag}_{p}", 100, f"{pre}timeout -s KILL 90 rocprofv3 --pmc {PMC_PASSES[p]} "
                                               f"--output-format csv -d gpurun_out/{study}/{tag}_{p} -o run -- "
                                               f"python3 bench.py {args}"))
@@ -208,12 +212,59 @@ def _cli(argv):
     return [(f"pmx{i}", 600, f"poisson-ellipse-openmp-mpi-cuda-new_amd/bin/pmx {a} --json") for i, a in enumerate(argv)]
 
 
+def _loopback(argv):
+    """one rank of an N-GPU job alone on the GPU (bench.py --loopback-rank): per-rank iteration time of
+    the real schedule.  Arguments: GPUS:RANK[:ENV=V,ENV=V] ... [-- bench.py args]"""
+    cut = argv.index("--") if "--" in argv else len(argv)
+    extra = " ".join(argv[cut + 1:]) or "--steps 60 --warmup 6"
+    steps = []
+    for spec in argv[:cut]:
+        parts = spec.split(":")
+        g, r = parts[0], parts[1]
+        env = " ".join(parts[2].split(",")) if len(parts) > 2 else ""
+        pre = f"env PMX_STUDY=1 {env} " if env else ""
+        tag = f"g{g}r{r}" + ("_" + parts[2].replace("=", "").replace(",", "_").replace("PMX_", "") if env else "")
+        steps.append((tag, 150, pre + bench(f"--gpus {g} --loopback-rank {r} {extra}")))
+    return steps
+
+
+def _ca_ab(argv):
+    """same-process A/B of s-step knobs: the arguments go to bench/probe/ca_env_ab.py"""
+    return [("ca_ab", 1000, "python -u bench/probe/ca_env_ab.py " + " ".join(shlex.quote(a) for a in argv))]
+
+
+def _algos(argv):
+    """bench.py per grid x algorithm x dtype: MxN:algo:dtype ... [-- bench.py args]"""
+    cut = argv.index("--") if "--" in argv else len(argv)
+    extra = " ".join(argv[cut + 1:]) or "--steps 20 --warmup 5"
+    steps = []
+    for spec in argv[:cut]:
+        g, algo, dt = spec.split(":")
+        m, n = g.split("x")
+        steps.append((f"{g}_{algo}_{dt}", 300, bench(f"--gpus 1 --M {m} --N {n} --algo {algo} --dtype {dt} {extra}")))
+    return steps
+
+
+def _counters(argv):
+    """kernel trace + SQ instruction / wait mix + EA traffic of one bench.py configuration:
+    [--args 'bench.py args'] [--env ENV=V,...]; summary by bench/pmc_summary.py"""
+    ap = argparse.ArgumentParser(prog="counters")
+    ap.add_argument("--args", default="--steps 30 --warmup 3 --graph-batch 0 --no-tol-solve")
+    ap.add_argument("--env", default="")
+    a = ap.parse_args(argv)
+    env = " ".join(a.env.split(",")) if a.env else ""
+    pre = f"env PMX_STUDY=1 {env} " if env else ""
+    steps = [("kt", 200, f"{pre}{ROCPROF} --output-format csv -d gpurun_out/counters/kt -o run -- python3 bench.py {a.args}")]
+    return steps + pmc_study("counters", {"c": env}, a.args, ("sq1", "sq2", "ea_rd", "ea_wr"))
+
+
 # Rounds 3-4: ~60 one-off studies (arith32 ... r4ba) were defined here; the profile READMEs that
 # cite them name the study, and the definitions stay in git history:
 # `git show 056f9cb:bench/gpurun.py` (bench/RETIRED.md, round 5).
 
 
-PARAMETRISED = {"ab": _ab, "pmc": _pmc, "timeline": _timeline, "validate": _validate, "share": _share, "cli": _cli}
+PARAMETRISED = {"ab": _ab, "pmc": _pmc, "timeline": _timeline, "validate": _validate, "share": _share, "cli": _cli,
+                "loopback": _loopback, "ca_ab": _ca_ab, "algos": _algos, "counters": _counters}
 
 
 def script(name: str, steps) -> str:
@@ -233,73 +284,9 @@ def script(name: str, steps) -> str:
     return "\n".join(lines) + "\n"
 
 
-# round 5: march occupancy / prefetch depth (bench/probe/dma_march.hip showed the access pattern
-# runs 9% faster at 8-10 than at 16 waves per CU); the shared-prologue tests
-_AB5 = "python -u bench/ab_env.py --fresh --shape 16384x16384 --rounds 2 --iters 200 "
-STUDIES["r5a"] = [
-    ("probe", 240, "bench/probe/dma_march 16384 3 10"),
-    ("tests_block", 400, f"{PYTEST} tests/test_gpu_block.py"),
-    ("ab_pf", 900, _AB5 + "--cfg base: --cfg pf2:PMX_PCG1_PF=2,PMX_PCG1_PF_W=1 "
-                    "--cfg pf2w12:PMX_PCG1_PF=2,PMX_PCG1_PF_W=1,PMX_PCG1_WPCU=12 "
-                    "--cfg pf2w10:PMX_PCG1_PF=2,PMX_PCG1_PF_W=1,PMX_PCG1_WPCU=10 "
-                    "--cfg pf3w12:PMX_PCG1_PF=3,PMX_PCG1_PF_W=1,PMX_PCG1_WPCU=12 "
-                    "--cfg pf3w10:PMX_PCG1_PF=3,PMX_PCG1_PF_W=1,PMX_PCG1_WPCU=10 "
-                    "--cfg wpf2w10:PMX_PCG1_PF_W=2,PMX_PCG1_WPCU_W=10"),
-]
-
-
-STUDIES["r5c"] = [
-    ("tests_dma", 600, f"{PYTEST} tests/test_gpu_pcg1.py -k 'dma or goldens'"),
-    ("ab_dma", 900, _AB5 + "--cfg base: --cfg d2:PMX_PCG1_DMA=2 --cfg d3:PMX_PCG1_DMA=3 "
-                    "--cfg d2w12:PMX_PCG1_DMA=2,PMX_PCG1_WPCU=12,PMX_PCG1_WPCU_W=10 "
-                    "--cfg d3w12:PMX_PCG1_DMA=3,PMX_PCG1_WPCU=12,PMX_PCG1_WPCU_W=10 "
-                    "--cfg d2w10:PMX_PCG1_DMA=2,PMX_PCG1_WPCU=10,PMX_PCG1_WPCU_W=8 "
-                    "--cfg d2p:PMX_PCG1_DMA=2,PMX_PCG1_DMA_W=0"),
-]
-
-
-STUDIES["r5e"] = [
-    ("tests_loop", 600, f"{PYTEST} tests/test_gpu_block.py -k 'looping or goldens'"),
-    ("ab_loop", 600, "python -u bench/ab_env.py --shape 800x1200 --shape 1200x1800 --shape 1600x2400 "
-                     "--shape 2400x3200 --rounds 3 --iters 600 --warmup 50 --cfg base: --cfg b0:PMX_PCG1_BLOCK=1 "
-                     "--cfg l1:PMX_PCG1_BLOCK=1,PMX_PCG1_BLOCK_LOOP=1 --cfg l2:PMX_PCG1_BLOCK=1,PMX_PCG1_BLOCK_LOOP=2 "
-                     "--cfg l2f:PMX_PCG1_BLOCK=1,PMX_PCG1_BLOCK_LOOP=2,PMX_PCG1_BLOCK_FUSED=1 "
-                     "--cfg l3:PMX_PCG1_BLOCK=1,PMX_PCG1_BLOCK_LOOP=3"),
-]
-
-
-STUDIES["r5f"] = [
-    ("tests_lock", 600, f"{PYTEST} tests/test_gpu_pcg1.py -k 'lockstep or goldens'"),
-    ("ab_lock", 900, _AB5 + "--shape 2048x16384 --cfg base: --cfg w8:PMX_PCG1_WAVES=8 "
-                     "--cfg w8w8:PMX_PCG1_WAVES=8,PMX_PCG1_WAVES_W=8 --cfg w4:PMX_PCG1_WAVES=4 "
-                     "--cfg w8r4:PMX_PCG1_WAVES=8,PMX_PCG1_ROWS=4 --cfg w8r12:PMX_PCG1_WAVES=8,PMX_PCG1_ROWS=12"),
-]
-
-
-STUDIES["r5g"] = [
-    ("ab_lock2", 900, _AB5 + "--cfg base: --cfg w4r12:PMX_PCG1_WAVES=4,PMX_PCG1_ROWS=12 "
-                      "--cfg w8r16:PMX_PCG1_WAVES=8,PMX_PCG1_ROWS=16 --cfg w4r16:PMX_PCG1_WAVES=4,PMX_PCG1_ROWS=16 "
-                      "--cfg r12:PMX_PCG1_ROWS=12"),
-]
-
-
-STUDIES["r5h"] = [
-    ("ab_rows", 1100, "python -u bench/ab_env.py --fresh --shape 16384x16384 --rounds 3 --iters 200 "
-                      "--cfg base: --cfg r12:PMX_PCG1_ROWS=12 --cfg w4r12:PMX_PCG1_WAVES=4,PMX_PCG1_ROWS=12 "
-                      "--cfg w4r12w1:PMX_PCG1_WAVES=4,PMX_PCG1_ROWS=12,PMX_PCG1_WAVES_W=1 "
-                      "--cfg w4r10:PMX_PCG1_WAVES=4,PMX_PCG1_ROWS=10 --cfg w4r14:PMX_PCG1_WAVES=4,PMX_PCG1_ROWS=14 "
-                      "--cfg r14:PMX_PCG1_ROWS=14"),
-]
-
-
-STUDIES["r5i"] = [
-    ("ab_rows_probe", 1100, "python -u bench/ab_env.py --fresh --shape 16384x16384 --shape 2048x16384 --rounds 2 "
-                            "--iters 200 --cfg base:PMX_PLACEMENT=20 --cfg r12:PMX_PLACEMENT=20,PMX_PCG1_ROWS=12 "
-                            "--cfg w4r12:PMX_PLACEMENT=20,PMX_PCG1_WAVES=4,PMX_PCG1_ROWS=12 "
-                            "--cfg w4r14:PMX_PLACEMENT=20,PMX_PCG1_WAVES=4,PMX_PCG1_ROWS=14"),
-    ("bench_w4r12", 300, "env PMX_PCG1_WAVES=4 PMX_PCG1_ROWS=12 " + bench("--gpus 1 --steps 20 --warmup 5")),
-    ("bench_base", 300, bench("--gpus 1 --steps 20 --warmup 5")),
-]
+# Rounds 3-5: the one-off studies (arith32 ... r4ba, r5a ... r5i) and round 5's bench/runs/*.sh
+# scripts were defined here / there; the profile READMEs that cite them name the study, and the
+# definitions stay in git history (bench/RETIRED.md).
 
 
 def main():

@@ -6,6 +6,8 @@ paths on small grids, then pass timings at 16384^2 (same process, same placement
 import importlib
 import os
 import sys
+
+os.environ["PMX_STUDY"] = "1"  # the library applies PMX_* kernel / schedule knobs only in study mode
 import time
 
 import numpy as np

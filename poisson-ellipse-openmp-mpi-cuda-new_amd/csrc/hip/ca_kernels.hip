@@ -1309,13 +1309,15 @@ CaTiles make_ca_tiles(const DevGeom& G, int s, int rows, int rows2, int rows_f) 
   t.cwords = (G.nx + 4 * s + 2 * kCaRowOff + 15) / 16 + 1;
   // the fused tiling: radius 2s (he_f = 2s columns per side), rows_f rows.  Auto: 64 (16384^2 at 3
   // waves per SIMD, ms/iteration: 16 rows 1.41, 32 1.13, 64 1.01), halved while the grid has fewer
-  // than ~6 rounds of tiles (1536 two-wave workgroups at a time)
+  // than ~4 rounds of tiles (1536 two-wave workgroups at a time): loopback per-rank ms/iteration of
+  // the 16384^2 strips, 8 GPUs (2048 rows) 16 / 32 / 48 / 64 rows 0.226 / 0.199 / 0.202 / 0.209,
+  // 4 GPUs 0.399 / 0.338 / 0.329 / 0.330 (profiles/r6/loopback/)
   t.he_f = 2 * s;
   t.wo_f = 128 - 2 * t.he_f;
   t.tiles_j_f = (G.ny + t.wo_f - 1) / t.wo_f;
   if (rows_f <= 0) {
     rows_f = 64;
-    while (rows_f > 16 && int64_t((G.nx + rows_f - 1) / rows_f) * t.tiles_j_f < 9216) rows_f /= 2;
+    while (rows_f > 16 && int64_t((G.nx + rows_f - 1) / rows_f) * t.tiles_j_f < 6000) rows_f /= 2;
   }
   PMX_CHECK(rows_f >= 1 && rows_f <= 4096, "s-step PCG: fused tile rows must be in [1, 4096]");
   t.rows_f = rows_f;

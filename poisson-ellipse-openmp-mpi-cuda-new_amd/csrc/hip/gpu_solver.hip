@@ -220,8 +220,9 @@ int choose_algo(const ProblemSpec& spec, const ProcGrid& grid, const GpuOptions&
   if (o.algo == 3) return 3;  // validated by the solver
   if (o.algo == -1) {
     const bool strips = grid.Py == 1 && (grid.size() == 1 || (direct_rows && (spec.M - 1) / grid.Px >= 8));
-    bool ca = o.dtype == DType::kFp64 && !o.exact && o.kernel == 1 && strips &&
-              int64_t(spec.M - 1) * (spec.N - 1) >= kCaAutoPoints;
+    // every storage type: with fp32 / mixed fields the s-step keeps its basis and sums in fp64 registers
+    // and beats pcg1 too (16384^2 0.951 vs 1.093 ms, 32768^2 3.356 vs 3.831; NOTES #124)
+    bool ca = !o.exact && o.kernel == 1 && strips && int64_t(spec.M - 1) * (spec.N - 1) >= kCaAutoPoints;
     if (ca && device_total_bytes > 0) {  // rank 0 holds the largest strip
       const Subdomain sd0 = decompose_2d(spec.M, spec.N, grid, 0);
       const double need = double(GpuSubdomainSolver::estimate_device_bytes_algo(spec, sd0, o.dtype, 3)) *

@@ -183,7 +183,7 @@ const char* study_env(const char* name);
 bool choose_single_pass(const ProblemSpec& spec, const ProcGrid& grid, const GpuOptions& resolved,
                         double device_total_bytes, int subdomains_per_device);
 // The iteration algorithm (GpuOptions::algo) a run uses: an explicit 1 / 2 / 3 as given, auto (-1) the
-// s-step PCG (3) where it applies and wins -- fp64 with the fast arithmetic, undecomposed or row strips
+// s-step PCG (3) where it applies and wins -- the fast arithmetic (any storage), undecomposed or row strips
 // of >= 8 rows on a transport that moves ghost rows between fields (`direct_rows`), at least
 // kCaAutoPoints grid points (below, pcg1's block tiles are faster: profiles/r5/ca/small.log) -- and
 // whose 7 fields fit into the device (`device_total_bytes` > 0; else no size test), otherwise
