@@ -1,4 +1,5 @@
-// GPU PCG orchestration.  See pmx/gpu_solver.hpp.
+// GPU PCG orchestration.  See pmx/gpu_solver.hpp.  The s-step solver's passes and its driver
+// schedule are in ca_solver.hip, pcg1's decomposed-grid schedules in pcg1_driver.hip.
 //
 // Reference call stack being replaced (stage4-mpi+cuda/poisson_mpi_cuda_f.cu:688-983): CPU
 // assembly + 3 H2D copies, 8 cudaMallocs, and per iteration 8 launches each followed by
@@ -805,149 +806,6 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
   }
 }
 
-// One s-step pass (kind 0: pass 1, 1: pass 2, 2: the fused pass): with the split kernels the frame tiles
-// run on a side stream, concurrently with the interior (their few long marches would otherwise trail
-// the pass by ~0.1 ms).  The first pass after a ghost exchange (pass 1 or the fused pass; with the fused
-// schedule also the batch's last pass 2) waits for it in the tiles that read ghost rows.
-template <typename T>
-void GpuSubdomainSolver::ca_pass_impl(hipStream_t s, int kind) {
-  T* w = static_cast<T*>(field_base(0));
-  T* z0 = static_cast<T*>(field_base(1));
-  T* z1 = reinterpret_cast<T*>(r2_ + field_off_ * elem_);
-  T* p0 = static_cast<T*>(field_base(2));
-  T* p1 = static_cast<T*>(field_base(3));
-  hipEvent_t wait = ca_frame_wait_;
-  ca_frame_wait_ = nullptr;
-  auto launch = [&](hipStream_t side) {
-    if (kind == 2)
-      launch_ca_fused<T>(ca_geom_, w, z0, z1, p0, p1, partials_, ca_state_, ca_tiles_, s, side, wait);
-    else
-      launch_ca_sweep<T>(ca_geom_, ca_tables_, w, z0, z1, p0, p1, partials_, state_, ca_state_, ca_tiles_, kind == 1,
-                         s, side, wait);
-  };
-  if (ca_side_) {
-    HIP_CHECK(hipEventRecord(ca_ev_fork_, s));
-    HIP_CHECK(hipStreamWaitEvent(ca_side_, ca_ev_fork_, 0));
-    launch(ca_side_);
-    HIP_CHECK(hipEventRecord(ca_ev_join_, ca_side_));
-    HIP_CHECK(hipStreamWaitEvent(s, ca_ev_join_, 0));
-  } else {
-    launch(nullptr);
-  }
-  after_launch(s);
-}
-
-void GpuSubdomainSolver::drop_side_stream() {
-  if (!ca_side_) return;
-  HIP_CHECK(hipSetDevice(opt_.device));
-  HIP_CHECK(hipStreamSynchronize(ca_side_));
-  HIP_CHECK(hipStreamDestroy(ca_side_));
-  HIP_CHECK(hipEventDestroy(ca_ev_fork_));
-  HIP_CHECK(hipEventDestroy(ca_ev_join_));
-  ca_side_ = nullptr;
-  ca_ev_fork_ = ca_ev_join_ = nullptr;
-}
-
-void GpuSubdomainSolver::enqueue_ca_pass(hipStream_t s, bool upd) {
-  PMX_CHECK(ca_, "not an s-step solver");
-  if (elem_ == 8) ca_pass_impl<double>(s, upd ? 1 : 0);
-  else ca_pass_impl<float>(s, upd ? 1 : 0);
-}
-
-void GpuSubdomainSolver::enqueue_ca_fused(hipStream_t s) {
-  PMX_CHECK(ca_fused(), "not an s-step solver with the fused pass");
-  if (elem_ == 8) ca_pass_impl<double>(s, 2);
-  else ca_pass_impl<float>(s, 2);
-}
-
-void GpuSubdomainSolver::enqueue_ca_reduce(hipStream_t s, int n, bool check_only, bool finish, bool fused) {
-  PMX_CHECK(ca_, "not an s-step solver");
-  PMX_CHECK(!fused || ca_fused(), "fused reduction without the fused pass");
-  const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
-  // after the fused pass both the Gram products and the norms come from its tiling
-  const int n1 = fused ? ca_tiles_.ntilesf() : ca_tiles_.ntiles();
-  const int n2 = fused ? ca_tiles_.ntilesf() : ca_tiles_.ntiles2();
-  launch_ca_reduce(partials_, n1, n2, ca_tiles_.s, g_.h1h2, wdiff,
-                   check_only ? 1 : n, check_only, state_, ca_state_, ca_chunk_, s, progress_dev_, finish);
-  after_launch(s);
-  if (!check_only) {  // a block the device applies (unless it stopped): the set its pass 2 writes
-    ++ca_blk_;
-    host_k_ += n;
-  }
-}
-
-void GpuSubdomainSolver::enqueue_ca_finish(hipStream_t s, int n, bool check_only) {
-  PMX_CHECK(ca_, "not an s-step solver");
-  const double wdiff = spec_.norm == Norm::kWeighted ? g_.h1h2 : 1.0;
-  launch_ca_finish(ca_tiles_.s, g_.h1h2, wdiff, check_only ? 1 : n, check_only, state_, ca_state_, s, progress_dev_);
-  after_launch(s);
-}
-
-GpuSubdomainSolver::CaProbe GpuSubdomainSolver::ca_probe(const std::vector<double>& z, const std::vector<double>& p,
-                                                         const std::vector<double>& w, const std::vector<double>& coef,
-                                                         const std::vector<double>& pa, bool fused, hipStream_t s) {
-  PMX_CHECK(ca_ && elem_ == 8, "ca_probe: not an fp64 s-step solver");
-  PMX_CHECK(!fused || ca_fused(), "ca_probe: the fused pass runs undecomposed grids");
-  const int S = ca_tiles_.s, NB = 2 * S + 1, NQ = 6 * S;
-  const size_t rows = size_t(sd_.nx + 2 * gh_), cols = size_t(sd_.ny + 2);
-  PMX_CHECK(z.size() == rows * cols && p.size() == rows * cols && w.size() == rows * cols,
-            "ca_probe: fields must be (nx + 2 gh) x (ny + 2)");
-  PMX_CHECK(coef.size() == size_t(3 * NB) && pa.size() == size_t(S * NB), "ca_probe: coefficient shapes");
-  HIP_CHECK(hipSetDevice(opt_.device));
-  enqueue_init(s);
-  HIP_CHECK(hipStreamSynchronize(s));
-  auto put = [&](void* base, const std::vector<double>& v) {
-    char* dst = static_cast<char*>(base) + int64_t(1 - gh_) * geom_.pitch * 8;
-    HIP_CHECK(hipMemcpy2D(dst, size_t(geom_.pitch) * 8, v.data(), cols * 8, cols * 8, rows, hipMemcpyHostToDevice));
-  };
-  put(field_base(1), z);
-  put(field_base(2), p);
-  put(field_base(0), w);
-  CaProbe out;
-  auto sums = [&](int64_t base, int nq, int n) {
-    const std::vector<double> h = read_partials(s);
-    std::vector<double> r(size_t(nq), 0.0);
-    for (int q = 0; q < nq; ++q)
-      for (int i = 0; i < n; ++i) r[size_t(q)] += h[size_t(base + int64_t(q) * n + i)];
-    return r;
-  };
-  CaState c{};
-  HIP_CHECK(hipMemcpy(&c, ca_state_, sizeof(CaState), hipMemcpyDeviceToHost));
-  c.blk = 1;  // as after the block's reduction: pass 2 / the fused pass read set 0, write set 1
-  c.nupd = S;
-  for (int k = 0; k < 3; ++k)
-    for (int i = 0; i < NB; ++i) c.coef[k][i] = coef[size_t(k * NB + i)];
-  for (int j = 0; j < S; ++j)
-    for (int i = 0; i < NB; ++i) c.pa[j][i] = pa[size_t(j * NB + i)];
-  if (!fused) {
-    enqueue_ca_pass(s, false);
-    HIP_CHECK(hipStreamSynchronize(s));
-    out.gram = sums(0, NQ, ca_tiles_.ntiles());
-    HIP_CHECK(hipMemcpy(ca_state_, &c, sizeof(CaState), hipMemcpyHostToDevice));
-    enqueue_ca_pass(s, true);
-    HIP_CHECK(hipStreamSynchronize(s));
-    out.norms = sums(int64_t(NQ) * ca_tiles_.ntiles(), S, ca_tiles_.ntiles2());
-  } else {
-    HIP_CHECK(hipMemcpy(ca_state_, &c, sizeof(CaState), hipMemcpyHostToDevice));
-    enqueue_ca_fused(s);
-    HIP_CHECK(hipStreamSynchronize(s));
-    const std::vector<double> gn = sums(0, NQ + S, ca_tiles_.ntilesf());
-    out.gram.assign(gn.begin(), gn.begin() + NQ);
-    out.norms.assign(gn.begin() + NQ, gn.end());
-  }
-  auto get = [&](const void* base) {
-    std::vector<double> h(size_t(sd_.nx) * sd_.ny);
-    const char* src = static_cast<const char*>(base) + (geom_.pitch + 1) * 8;
-    HIP_CHECK(hipMemcpy2D(h.data(), size_t(sd_.ny) * 8, src, size_t(geom_.pitch) * 8, size_t(sd_.ny) * 8,
-                          size_t(sd_.nx), hipMemcpyDeviceToHost));
-    return h;
-  };
-  out.p = get(field_base(3));
-  out.z = get(r2_ + field_off_ * elem_);
-  out.w = get(field_base(0));
-  return out;
-}
-
 template <typename T>
 void GpuSubdomainSolver::halo_impl(hipStream_t s, bool unpack) {
   launch_pcg1_halo<T>(geom_, static_cast<T*>(field_base(1)), reinterpret_cast<T*>(r2_ + field_off_ * elem_),
@@ -959,30 +817,6 @@ void GpuSubdomainSolver::halo_impl(hipStream_t s, bool unpack) {
 void GpuSubdomainSolver::set_direct_rows(bool on) {
   PMX_CHECK(!on || can_direct_rows(), "direct-row ghost exchange needs pcg1 on a row strip (x neighbours only)");
   direct_rows_ = on;
-}
-
-HaloMsgs GpuSubdomainSolver::ca_halo_msgs(int set) const {
-  PMX_CHECK(ca_, "ca_halo_msgs: not an s-step solver");
-  HaloMsgs out;
-  // s-step strips: the gh owned edge rows of z and p of the set the next block reads (CaState::blk
-  // & 1, mirrored by ca_blk_) into the neighbour's gh ghost rows (gh = s, 2s with the fused pass), as
-  // ONE span per field: rows q .. q+gh-2 whole, row q+gh-1's columns 0 .. ny+1 (columns <= 0 and >= ny+1
-  // are Dirichlet on a strip)
-  const int s = gh_;
-  char* fz = set ? r2_ + field_off_ * elem_ : static_cast<char*>(field_base(1));
-  char* fp = static_cast<char*>(field_base(set ? 3 : 2));
-  const int64_t P = geom_.pitch;
-  const int count = int((s - 1) * P + sd_.ny + 2);
-  for (int slot = 0; slot < 2; ++slot) {
-    if (layout_.peer[slot] < 0) continue;
-    const int64_t srow = slot == 0 ? 1 : sd_.nx - s + 1, rrow = slot == 0 ? 1 - s : sd_.nx + 1;
-    for (int f = 0; f < 2; ++f) {
-      char* base = f == 0 ? fz : fp;
-      out.m[out.n++] = HaloMsg{slot, f, layout_.peer[slot], count, base + srow * P * int64_t(elem_),
-                               base + rrow * P * int64_t(elem_)};
-    }
-  }
-  return out;
 }
 
 HaloMsgs GpuSubdomainSolver::halo_msgs() const {
@@ -1539,227 +1373,6 @@ void PcgDriver::poison(std::vector<hipStream_t>& streams) {
   }
 }
 
-void PcgDriver::set_halo_target(long long k) {
-  for (auto* s : local_) s->set_halo_target(k);
-}
-
-void PcgDriver::halo_exchange_pcg1(std::vector<hipStream_t>& streams, long long target) {
-  set_halo_target(target);
-  comm_->before_pack(local_, streams);
-  for (size_t i = 0; i < local_.size(); ++i) {
-    HIP_CHECK(hipSetDevice(local_[i]->device()));
-    local_[i]->enqueue_halo_pack(streams[i]);
-  }
-  poison(streams);
-  comm_->halo(local_, streams);
-  for (size_t i = 0; i < local_.size(); ++i) {
-    HIP_CHECK(hipSetDevice(local_[i]->device()));
-    local_[i]->enqueue_halo_unpack(streams[i]);
-  }
-}
-
-// Split sweep k (pcg1, decomposed, overlap on).  Default schedule: see frame_on_comm_ below.
-// With PMX_FRAME_ON_COMM=0, streams C (compute), F (frame), H (comm):
-//   C: [all-reduce k-1] -> ev_ar -> interior tiles of sweep k ----------> wait F -> ev_swept ->
-//   F:                     wait ev_ar (+ ev_halo of k-1) -> frame tiles -'
-//   C: reduce -> all-reduce k (no join: see the end of enqueue_split_iteration)
-//   H: wait ev_swept -> pack -> send/recv -> unpack -> ev_halo (joined by the next F, or
-//      by C at the end of the batch: join_halo)
-// So the ghost exchange of sweep k runs under the reduction, the all-reduce AND the interior of
-// sweep k+1; only the frame tiles (a few % of the sweep) wait for it.
-void PcgDriver::enqueue_split_iteration() {
-  // frame_on_comm_ (default): F is the comm stream H itself.  The exchange of sweep k reads only edge lines
-  // the frame tiles own (rows / columns 1, 2 and n-1, n: every tile whose march reaches a ghost cell
-  // is a frame tile, pcg1_tiles) and writes only ghost cells, which no interior tile reads; so H
-  // runs frame k -> exchange k -> (wait all-reduce k) frame k+1 in its own order, and the compute
-  // stream joins it once per iteration, before the reduction:
-  //   C: ev_ar -> interior k -> wait ev_fdone -> reduce -> all-reduce k -> ev_ar ...
-  //   H: wait ev_ar -> frame k -> ev_fdone -> pack -> send/recv -> unpack -> ev_halo
-  const bool fc = frame_on_comm_;
-  auto fstream = [&](size_t i) { return fc ? comm_streams_[i] : frame_streams_[i]; };
-  for_each_stream([&](size_t i, size_t u) {
-    HIP_CHECK(hipEventRecord(ev_ar_[u], streams_[i]));
-    HIP_CHECK(hipStreamWaitEvent(fstream(i), ev_ar_[u], 0));
-    if (halo_pending_ && !fc) HIP_CHECK(hipStreamWaitEvent(frame_streams_[i], ev_halo_[u], 0));
-  });
-  for (size_t i = 0; i < local_.size(); ++i) {
-    HIP_CHECK(hipSetDevice(local_[i]->device()));
-    local_[i]->enqueue_kernel_a_part(streams_[i], 1);
-    local_[i]->enqueue_kernel_a_part(fstream(i), 2);
-  }
-  for_each_stream([&](size_t i, size_t u) {
-    HIP_CHECK(hipEventRecord(ev_fdone_[u], fstream(i)));
-    HIP_CHECK(hipStreamWaitEvent(streams_[i], ev_fdone_[u], 0));
-    if (!fc) {
-      HIP_CHECK(hipEventRecord(ev_swept_[u], streams_[i]));
-      HIP_CHECK(hipStreamWaitEvent(comm_streams_[i], ev_swept_[u], 0));
-    }
-  });
-  set_halo_target(local_[0]->host_k() + 1);  // the sweep just enqueued is host_k; the next reads its outputs
-  comm_->before_pack(local_, comm_streams_);
-  for (size_t i = 0; i < local_.size(); ++i) {
-    HIP_CHECK(hipSetDevice(local_[i]->device()));
-    local_[i]->enqueue_halo_pack(comm_streams_[i]);
-  }
-  poison(comm_streams_);
-  comm_->halo(local_, comm_streams_);
-  for (size_t i = 0; i < local_.size(); ++i) {
-    HIP_CHECK(hipSetDevice(local_[i]->device()));
-    local_[i]->enqueue_halo_unpack(comm_streams_[i]);
-  }
-  for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipEventRecord(ev_halo_[u], comm_streams_[i])); });
-  halo_pending_ = true;
-  for (size_t i = 0; i < local_.size(); ++i) {
-    HIP_CHECK(hipSetDevice(local_[i]->device()));
-    local_[i]->enqueue_reduce_a(streams_[i]);
-  }
-  comm_->allreduce(local_, 2, streams_);
-  // No join of the comm stream here: the exchange (packed or direct rows) reads the edge lines of
-  // r_{k+1}, p_{k+1} and writes their ghost cells, with the buffer parity in its launch arguments;
-  // sweep k+1 writes the other parity (r_{k+2}, p_{k+2}), its interior tiles read no ghost cell and
-  // its frame tiles wait for ev_halo (or follow the exchange on H).  Sweep k+2, the next writer of these buffers, follows the
-  // all-reduce of k+1, which follows that frame.  So the next interior starts right after the
-  // all-reduce: one cross-queue wait per iteration instead of two (loopback strip 3 of 8: 293 ->
-  // 266 us, profiles/r4/loopback/).
-}
-
-void PcgDriver::join_halo() {
-  if (!halo_pending_) return;
-  for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipStreamWaitEvent(streams_[i], ev_halo_[u], 0)); });
-  halo_pending_ = false;
-}
-
-int PcgDriver::ca_batch() const {
-  const int s = local_[0]->ca_s();
-  const int b = graph_batch_ > 0 ? graph_batch_ : 16;
-  return (b + s - 1) / s * s;  // whole blocks per captured batch
-}
-
-void PcgDriver::enqueue_ca(int64_t n, const std::function<void(int)>& mark) {
-  const int s = local_[0]->ca_s();
-  HIP_CHECK(hipSetDevice(local_[0]->device()));
-  if (n <= 0) return;
-  auto mk = [&](int b) {
-    if (mark) mark(b);
-  };
-  auto each = [&](auto&& f) {
-    for (size_t i = 0; i < local_.size(); ++i) {
-      HIP_CHECK(hipSetDevice(local_[i]->device()));
-      f(local_[i], streams_[i]);
-    }
-    HIP_CHECK(hipSetDevice(local_[0]->device()));
-  };
-  if (!any_nb_ && local_.size() == 1 && comm_->world_size() == 1) {
-    // One grid: pass 1 -> reduce -> pass 2 per block, or with the fused pass
-    //   pass 1 -> reduce -> (fused -> reduce) x (blocks - 1) -> pass 2
-    // and then the last block's stop test (and its rewind): the state is exact at every batch end
-    GpuSubdomainSolver* g = local_[0];
-    hipStream_t st = streams_[0];
-    const bool fused = g->ca_fused();
-    bool first = true;
-    while (n > 0) {
-      const int m = int(std::min<int64_t>(s, n));
-      if (fused && !first) g->enqueue_ca_fused(st);
-      else g->enqueue_ca_pass(st, false);
-      mk(kPhA);
-      g->enqueue_ca_reduce(st, m, false, true, fused && !first);
-      mk(kPhRed);
-      if (!fused) {
-        g->enqueue_ca_pass(st, true);
-        mk(kPhB);
-      }
-      first = false;
-      n -= m;
-    }
-    if (fused) {
-      g->enqueue_ca_pass(st, true);
-      mk(kPhB);
-    }
-    g->enqueue_ca_reduce(st, 1, true, true);
-    mk(kPhRed);
-    g->enqueue_ca_pass(st, true);  // rewind (a no-op unless the test stopped inside the last block)
-    mk(kPhB);
-    return;
-  }
-  // decomposed: every rank's sums are all-reduced between the reduction and the scalars, and the s
-  // ghost rows of the new (z, p) set are exchanged after pass 2 (direct rows, one span per field).
-  // With the overlapped schedule the exchange runs on the comm stream: the next pass 1's interior
-  // tiles (which read no ghost row) start at once, its frame tiles wait for the exchange.  The batch
-  // joins the comm stream at its end, so a captured graph has no edge into the next one.
-  const bool ovl = any_nb_ && overlap_ && !comm_streams_.empty() && !mark;
-  bool pending = false;
-  auto frame_waits = [&](bool on) {  // every solver, by the index of its (possibly shared) stream
-    size_t u = 0;
-    for (size_t i = 0; i < local_.size(); ++i) {
-      if (i > 0 && streams_[i] != streams_[i - 1]) ++u;
-      local_[i]->set_ca_frame_wait(on ? ev_halo_[u] : nullptr);
-    }
-  };
-  const bool ar = comm_->world_size() > 1;
-  // the s ghost rows of the (z, p) set just written (2s with the fused pass)
-  auto exchange = [&] {
-    if (any_nb_ && ovl) {
-      for_each_stream([&](size_t i, size_t u) {
-        HIP_CHECK(hipEventRecord(ev_packed_[u], streams_[i]));
-        HIP_CHECK(hipStreamWaitEvent(comm_streams_[i], ev_packed_[u], 0));
-      });
-      comm_->halo(local_, comm_streams_);
-      for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipEventRecord(ev_halo_[u], comm_streams_[i])); });
-      frame_waits(true);
-      pending = true;
-    } else if (any_nb_) {
-      comm_->halo(local_, streams_);
-      mk(kPhHalo);
-    }
-  };
-  // Unfused, per block: pass 1 -> reduce -> all-reduce -> scalars -> pass 2 -> exchange.  Fused: pass 1
-  // -> reduce -> all-reduce -> scalars, then per further block fused pass -> exchange (under the
-  // reduction, all-reduce and scalars) -> ..., and the last block's pass 2 -> exchange.  Every rank runs
-  // the same schedule (ca_fused() is decided from global data).
-  const bool fused = local_[0]->ca_fused();
-  bool first = true;
-  while (n > 0) {
-    const int m = int(std::min<int64_t>(s, n));
-    const bool f = fused && !first;
-    if (f) each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_fused(st); });
-    else each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, false); });
-    mk(kPhA);
-    if (f) exchange();
-    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_reduce(st, m, false, false, f); });
-    mk(kPhRed);
-    comm_->allreduce(local_, 3, streams_);
-    if (ar) mk(kPhAr);
-    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_finish(st, m, false); });
-    mk(kPhRed);
-    if (!fused) {
-      each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, true); });
-      mk(kPhB);
-      exchange();
-    }
-    first = false;
-    n -= m;
-  }
-  if (fused) {
-    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, true); });
-    mk(kPhB);
-    exchange();
-  }
-  each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_reduce(st, 1, true, false); });
-  mk(kPhRed);
-  comm_->allreduce(local_, 3, streams_);
-  if (ar) mk(kPhAr);
-  each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_finish(st, 1, true); });
-  mk(kPhRed);
-  each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, true); });  // rewind
-  mk(kPhB);
-  if (pending) {  // the last block's exchange ran next to the check
-    for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipStreamWaitEvent(streams_[i], ev_halo_[u], 0)); });
-    frame_waits(false);
-  }
-}
-
-int PcgDriver::ca_phase() const { return any_nb_ ? int(local_[0]->ca_blocks() & 1) : 0; }
-
 void PcgDriver::enqueue_one_iteration() {
   if (ca_) {
     enqueue_ca(1);
@@ -1840,17 +1453,6 @@ void PcgDriver::enqueue_one_iteration() {
   }
   comm_->allreduce(local_, 1, streams_);
   for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipStreamWaitEvent(streams_[i], ev_halo_[u], 0)); });
-}
-
-template <typename F>
-void PcgDriver::for_each_stream(F&& f) {
-  // (index of the first solver using a stream, index of that unique stream)
-  size_t u = 0;
-  for (size_t i = 0; i < streams_.size(); ++i) {
-    if (i > 0 && streams_[i] == streams_[i - 1]) continue;
-    HIP_CHECK(hipSetDevice(local_[i]->device()));
-    f(i, u++);
-  }
 }
 
 void PcgDriver::advance_host_k(long long n) {

@@ -630,7 +630,16 @@ class PcgDriver {
   // nullptr when capture is impossible (graph_failed_ is then set)
   hipGraphExec_t graph_for(int phase, int len);
   hipGraphExec_t build_graph(int phase, int len);
-  template <typename F> void for_each_stream(F&& f);
+  // f(index of the first solver using a stream, index of that unique stream) per distinct stream
+  template <typename F>
+  void for_each_stream(F&& f) {
+    size_t u = 0;
+    for (size_t i = 0; i < streams_.size(); ++i) {
+      if (i > 0 && streams_[i] == streams_[i - 1]) continue;
+      HIP_CHECK(hipSetDevice(local_[i]->device()));
+      f(i, u++);
+    }
+  }
   void poison(std::vector<hipStream_t>& streams);
 
   std::vector<GpuSubdomainSolver*> local_;

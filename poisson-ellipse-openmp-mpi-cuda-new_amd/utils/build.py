@@ -39,6 +39,8 @@ HIP_SOURCES = [
     "hip/ca_kernels.hip",
     "hip/ops_kernels.hip",
     "hip/gpu_solver.hip",
+    "hip/ca_solver.hip",
+    "hip/pcg1_driver.hip",
     "hip/session.hip",
     "comm/comm.hip",
     "comm/ipc_comm.hip",
