@@ -191,8 +191,10 @@ def _timeline(argv):
 
 def _validate(argv):
     """the round-end tiers: GPU suite, smoke(), default bench (+ optional extra bench.py args)"""
-    extra = " ".join(argv)
-    return [("pytest_gpu", 1100, f"{PYTEST} tests -m gpu"),
+    keep = "--keep-going" in argv  # every failure of the suite, not only the first
+    extra = " ".join(a for a in argv if a != "--keep-going")
+    py = PYTEST.replace(" -x ", " ") if keep else PYTEST
+    return [("pytest_gpu", 1100, f"{py} tests -m gpu"),
             ("smoke", 200, "python -c 'import __graft_entry__ as g; g.smoke()'"),
             ("bench_default", 300, bench(f"--gpus 1 --steps 20 --warmup 5 {extra}"))]
 
@@ -256,11 +258,6 @@ def _counters(argv):
     pre = f"env PMX_STUDY=1 {env} " if env else ""
     steps = [("kt", 200, f"{pre}{ROCPROF} --output-format csv -d gpurun_out/counters/kt -o run -- python3 bench.py {a.args}")]
     return steps + pmc_study("counters", {"c": env}, a.args, ("sq1", "sq2", "ea_rd", "ea_wr"))
-
-
-# Rounds 3-4: ~60 one-off studies (arith32 ... r4ba) were defined here; the profile READMEs that
-# cite them name the study, and the definitions stay in git history:
-# `git show 056f9cb:bench/gpurun.py` (bench/RETIRED.md, round 5).
 
 
 PARAMETRISED = {"ab": _ab, "pmc": _pmc, "timeline": _timeline, "validate": _validate, "share": _share, "cli": _cli,

@@ -21,6 +21,7 @@ def _sess(pkg, monkeypatch, M, N, rows, **kw):
         monkeypatch.setenv("PMX_PCG1_BLOCK_ROWS", str(rows))
     else:
         monkeypatch.setenv("PMX_PCG1_BLOCK", "0")  # the march (auto picks block tiles on small grids)
+    kw.setdefault("algo", "pcg1")  # auto takes the s-step from 6M points (2400x3200)
     return pkg.make_session(pkg.PoissonEllipse(M=M, N=N), **kw)
 
 
