@@ -575,13 +575,12 @@ def measure(args) -> int:
     dkw = dict(kw, **pkw, phase=watch.phase, init_timeout=COMM_INIT_TIMEOUT, ca_s=args.ca_s,
                split_sweep=split_sweep)
     # --algo auto: the library decides (choose_algo) -- the s-step PCG (ca_kernels.hip) where it applies
-    # and wins (fp64 with the fast arithmetic, >= 6M points, undecomposed or row strips on a transport
-    # that moves its ghost rows straight between the fields: RCCL or IPC, not torch) and its 7 fields
+    # and wins (the fast arithmetic, >= 6M points, undecomposed, row strips or 2-D blocks -- BASELINE
+    # config 4, `--split reference` -- on a native transport: RCCL or IPC, not torch) and its 7 fields
     # fit, else pcg1 / pcg2.  The JSON's config.tile.algo says which ran.
-    strips = world == 1 or process_grid(world, args.M, args.N, args.split)[1] == 1
-    ca_ok = not args.exact and strips and (world == 1 or cfg["comm"] in ("native", "ipc"))
+    ca_ok = not args.exact and (world == 1 or cfg["comm"] in ("native", "ipc"))
     if args.algo == "ca" and not ca_ok:
-        raise SystemExit("[bench] --algo ca (the s-step PCG) needs row strips and the RCCL or IPC transport")
+        raise SystemExit("[bench] --algo ca (the s-step PCG) needs the RCCL or IPC transport")
     algo_id = {"auto": -1, "pcg1": 1, "pcg2": 2, "ca": 3}[args.algo]
     if dry:
         tp = importlib.import_module(pkg_name + ".models.torch_pcg")
@@ -804,11 +803,9 @@ def measure_loopback(args) -> int:
         raise SystemExit("--loopback-rank must be in [0, --gpus)")
     problem = pmx.PoissonEllipse(M=args.M, N=args.N, breakdown_tol=args.breakdown_tol)
     # the algorithm the real N-GPU run would use (see measure: the s-step PCG on big fp64 row strips)
-    decomp = importlib.import_module("poisson-ellipse-openmp-mpi-cuda-new_amd.parallel.decomp")
-    strips = decomp.process_grid(args.gpus, args.M, args.N, args.split)[1] == 1
-    ca_ok = not args.exact and strips
+    ca_ok = not args.exact
     if args.algo == "ca" and not ca_ok:
-        raise SystemExit("[bench] --algo ca (the s-step PCG) needs row strips")
+        raise SystemExit("[bench] --algo ca (the s-step PCG) runs the fast arithmetic")
     algo_id = {"auto": -1, "pcg1": 1, "pcg2": 2, "ca": 3}[args.algo]  # auto: the library's choose_algo
     s = native.Session(problem.to_native(), world=args.gpus, comm="loopback", split=getattr(native.Split, args.split),
                        ranks=[args.loopback_rank], devices=[0], dtype=args.dtype, graph_batch=args.graph_batch,

@@ -20,6 +20,7 @@ Fixed studies (STUDIES) and parametrised ones (`<study> -- <arguments>`):
     ca_ab     -- bench/probe/ca_env_ab.py arguments: same-process A/B of s-step knobs
     algos     -- MxN:algo:dtype: bench.py per grid x algorithm x storage
     counters  -- kernel trace + SQ / EA counter passes of one bench.py configuration
+    cmds      -- ad-hoc steps 'tag:seconds:command'
 Studies that back kept profiles name themselves in the profile's README; bench/RETIRED.md maps
 the round-1/2 one-off gpu_*.sh scripts onto these.
 """
@@ -260,7 +261,16 @@ def _counters(argv):
     return steps + pmc_study("counters", {"c": env}, a.args, ("sq1", "sq2", "ea_rd", "ea_wr"))
 
 
-PARAMETRISED = {"ab": _ab, "pmc": _pmc, "timeline": _timeline, "validate": _validate, "share": _share, "cli": _cli,
+def _cmds(argv):
+    """ad-hoc steps, one per argument 'tag:seconds:command' (python commands of this repo)"""
+    steps = []
+    for a in argv:
+        tag, lim, cmd = a.split(":", 2)
+        steps.append((tag, int(lim), cmd))
+    return steps
+
+
+PARAMETRISED = {"cmds": _cmds, "ab": _ab, "pmc": _pmc, "timeline": _timeline, "validate": _validate, "share": _share, "cli": _cli,
                 "loopback": _loopback, "ca_ab": _ca_ab, "algos": _algos, "counters": _counters}
 
 

@@ -26,9 +26,11 @@ def parse(spec):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=16384)
+    ap.add_argument("--m", type=int, default=0, help="rows M (default: --n)")
     ap.add_argument("--iters", type=int, default=99)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--placement", type=int, default=0)
+    ap.add_argument("--dtype", default="fp64")
     ap.add_argument("configs", nargs="+")
     a = ap.parse_args()
     cfgs = [parse(c) for c in a.configs]
@@ -38,8 +40,8 @@ def main():
             old = {k: os.environ.get(k) for k in env}
             os.environ.update(env)
             try:
-                c = pkg.make_session(pkg.PoissonEllipse(M=a.n, N=a.n), algo="ca", ca_s=int(env.get("PMX_CA_S", 3)),
-                                     placement=a.placement)
+                c = pkg.make_session(pkg.PoissonEllipse(M=a.m or a.n, N=a.n), algo="ca", ca_s=int(env.get("PMX_CA_S", 3)),
+                                     placement=a.placement, dtype=a.dtype)
             finally:
                 for k, v in old.items():
                     if v is None:

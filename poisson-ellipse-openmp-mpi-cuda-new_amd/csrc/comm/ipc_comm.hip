@@ -282,7 +282,8 @@ class IpcComm final : public Comm {
       // the same number of elements at its own send offset, which a rank computes locally from the
       // neighbour's subdomain (comm_layout is a pure function of it)
       const Subdomain nsd = decompose_2d(local_->spec().M, local_->spec().N, local_->sd().grid, q);
-      const CommLayout NL = GpuSubdomainSolver::comm_layout(nsd, local_->options().dtype, local_->single_pass() || local_->ca());
+      const CommLayout NL = GpuSubdomainSolver::comm_layout(nsd, local_->options().dtype, local_->single_pass() || local_->ca(),
+                                                            local_->ca() ? local_->ca_ghost_rows() : 0);
       const int os = opposite_slot(s);
       PMX_CHECK(NL.edge_len[os] == L.edge_len[s], "IpcComm: slot lengths disagree with rank " << q);
       P_.nbr[s] = P_.all[q];
@@ -396,7 +397,7 @@ class IpcComm final : public Comm {
   // s-step strips: each x neighbour's fields allocation (mapped) and its span offsets [set][slot][field]
   // s-step strips: our staging buffer of edge rows ([slot][field] spans of ca_count_ elements) and each
   // x neighbour's (mapped)
-  bool ca_ = local_->ca();
+  bool ca_ = local_->ca() && local_->can_direct_rows();  // s-step strips (2-D blocks: the packed slots)
   int ca_count_ = 0;
   char* ca_buf_ = nullptr;
   char* ca_peer_buf_[2] = {nullptr, nullptr};

@@ -158,8 +158,16 @@ __device__ __forceinline__ int ca_row_cls(const unsigned* tbl, int m) {
 struct CaFaces {
   const double* a;
   const double* b;
-  int gh;  // ghost rows allocated on each side of the fields (rows 1-gh .. nx+gh exist): 2, or 3 for strips
+  int gh;  // ghost rows (and, on 2-D blocks, columns) on each side of the fields: 2 undecomposed, s or 2s
 };
+
+// The last odd column a lane's 2-column load may start at (loads clamp to it; column 1 is 16-B
+// aligned, so pairs start at odd columns): the first odd column >= ny + 1 (the Dirichlet column) --
+// or, with a neighbour across y-hi (2-D blocks), the one whose pair reaches the last ghost column
+// ny + gh.  Lanes past it hold clamped copies; they only feed columns beyond the owned ones.
+__device__ __forceinline__ int ca_cmax(const DevGeom& G, const CaFaces& F) {
+  return (G.nb & kNbYhi) ? ((G.ny + F.gh - 1) | 1) : G.ny + 1 + (G.ny & 1);
+}
 
 // the coefficients of a lane's 2 columns at local row r (clamped into the allocated rows; rows
 // outside the grid only feed masked values)
@@ -242,7 +250,7 @@ __device__ __forceinline__ void ca_march(const DevGeom& G, const DevTables& Tb, 
   const int64_t P = G.pitch;
   const int lane = threadIdx.x & 63;
   const int c0 = j0 - HE + 2 * lane;
-  const int cmax = G.ny + 1 + (G.ny & 1);
+  const int cmax = ca_cmax(G, F);
   bool colin[2], own[2];
   int gj[2];
 #pragma unroll
@@ -620,7 +628,7 @@ struct CaFRow {
 // workgroup barrier per row step.  One wave holding both chains' register windows, the Gram sums and
 // the prefetch rows needs ~300 VGPRs (1 wave per SIMD, latency-bound: measured 1.38-2.3 ms/iteration
 // against 1.20 unfused at 16384^2); split, each wave holds half and the SIMDs keep 3 of them.
-template <typename T, int S, bool FAST, int PF, int ROLE>
+template <typename T, int S, bool FAST, int PF, int ROLE, int RG = 1>
 __device__ __forceinline__ void ca_march_fused(const DevGeom& G, const CaK& K, const T* __restrict__ pin,
                                                const T* __restrict__ zin, T* __restrict__ pout, T* __restrict__ zout,
                                                T* __restrict__ w, int i0, int i1, int j0, int j1,
@@ -628,13 +636,14 @@ __device__ __forceinline__ void ca_march_fused(const DevGeom& G, const CaK& K, c
                                                double (&acc)[CaShape<S>::NQ], double (&nacc)[S],
                                                const double (&ca)[CaShape<S>::NB], const double (&cb)[CaShape<S>::NB],
                                                const double (&cc)[CaShape<S>::NB],
-                                               const double (&pa)[S][CaShape<S>::NB], double* ring) {
+                                               const double (&pa)[S][CaShape<S>::NB], double* ring,
+                                               unsigned long long* tm = nullptr) {
   using Sh = CaShape<S>;
   constexpr int NB = Sh::NB, HE = CaFuseShape<S>::HE;
   const int64_t P = G.pitch;
   const int lane = threadIdx.x & 63;
   const int c0 = j0 - HE + 2 * lane;
-  const int cmax = G.ny + 1 + (G.ny & 1);
+  const int cmax = ca_cmax(G, F);
   bool colin[2], own[2];
 #pragma unroll
   for (int u = 0; u < 2; ++u) {
@@ -645,13 +654,42 @@ __device__ __forceinline__ void ca_march_fused(const DevGeom& G, const CaK& K, c
   const bool own_all = own[0] && own[1];
   const bool own_any = own[0] || own[1];
   auto interior_row = [&](int m) { return G.gi0 + m >= 1 && G.gi0 + m <= G.M - 1; };
-  // ring slot k: the new p row at ring + k * 256, z at + 128 (2 doubles per lane)
+  // ring slot k: the new p row at ring + k * 256, z at + 128 (2 doubles per lane).  2 RG slots: the
+  // waves meet once per RG row steps (the producer after its group's last step, the consumer before
+  // its group's first), so one wave's slow row is absorbed by the other's group; step t = m - mfirst
+  // uses slot t mod 2 RG (rhi: the unrolled iteration's offset, for RG = 4)
+  static_assert(RG == 1 || RG == 2 || RG == 4, "ca_march_fused: 1, 2 or 4 row steps per barrier");
+  int rhi = 0;
+  auto slot_of = [&](auto qc) {
+    constexpr int q = decltype(qc)::value;
+    if constexpr (RG == 4) return rhi + q;
+    else return q & (2 * RG - 1);
+  };
   typedef double d2 __attribute__((ext_vector_type(2)));
+#ifdef PMX_CAF_TIMING  // study builds: s_memtime ticks a wave spends in the row barriers
+  unsigned long long t_sync = 0;
+  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+  auto sync = [&] {
+    const unsigned long long a = __builtin_amdgcn_s_memtime();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    t_sync += __builtin_amdgcn_s_memtime() - a;
+  };
+  auto tdone = [&] {
+    if (tm) {
+      tm[0] = __builtin_amdgcn_s_memtime() - t_start;
+      tm[1] = t_sync;
+    }
+  };
+#else
   auto sync = [] {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   };
+  auto tdone = [] {};
+#endif
 
   // register windows as ca_march's: level l of a chain at row r in slot (r - mfirst) & 3.  The
   // producer's chain (block b's basis) trails the loaded row by l rows, the consumer's (block b+1's)
@@ -751,7 +789,7 @@ __device__ __forceinline__ void ca_march_fused(const DevGeom& G, const CaK& K, c
         pn[u] = static_cast<T>(sp);
         zn[u] = static_cast<T>(sz);
       }
-      double* sl = ring + (q & 1) * 256;
+      double* sl = ring + slot_of(qc) * 256;
       *reinterpret_cast<d2*>(sl + 2 * lane) = d2{double(pn[0]), double(pn[1])};
       *reinterpret_cast<d2*>(sl + 128 + 2 * lane) = d2{double(zn[0]), double(zn[1])};
       if (g1 < i0 || g1 > i1) return;
@@ -790,12 +828,14 @@ __device__ __forceinline__ void ca_march_fused(const DevGeom& G, const CaK& K, c
     for (int q = 0; q < PF; ++q) fetch(min(mfirst + q, mlast), buf[q]);
     bool more = true;
     for (int m = mfirst; more && m <= mlast; m += 4) {
+      rhi = (m - mfirst) & 4;
       more = static_for_while<4>([&](auto qc) {
         constexpr int q = decltype(qc)::value;
         if (m + q > mlast) return false;
         fetch(min(m + q + PF, mlast), buf[(q + PF) % NBUF]);
         core(qc, m + q, buf[q % NBUF]);
-        sync();  // the row is in the ring; the consumer has read the slot the next step rewrites
+        // the group's rows are in the ring; the consumer has read the slots the next group rewrites
+        if (q % RG == RG - 1 || m + q == mlast) sync();
         return true;
       });
     }
@@ -803,6 +843,7 @@ __device__ __forceinline__ void ca_march_fused(const DevGeom& G, const CaK& K, c
 #pragma unroll
       for (int j = 0; j < S; ++j) nacc[j] = own_all ? nacc[j] : 0.0;
     }
+    tdone();
   } else {
     // ---- consumer: after the producer's step m, row g1 = m - S of the new (p, z) is in the ring: block
     // b+1's basis from it (exactly as pass 1 would build it from the stored values) and, S rows
@@ -812,7 +853,7 @@ __device__ __forceinline__ void ca_march_fused(const DevGeom& G, const CaK& K, c
       const int g1 = m - S;
       if (g1 < i0 - S) return;
       constexpr int s1 = (q - S) & 3;
-      const double* sl = ring + (q & 1) * 256;
+      const double* sl = ring + slot_of(qc) * 256;
       const d2 pv = *reinterpret_cast<const d2*>(sl + 2 * lane);
       const d2 zv = *reinterpret_cast<const d2*>(sl + 128 + 2 * lane);
       ch[s1] = ca_row_cls(ctbl, g1);
@@ -838,10 +879,11 @@ __device__ __forceinline__ void ca_march_fused(const DevGeom& G, const CaK& K, c
     };
     bool more = true;
     for (int m = mfirst; more && m <= mlast; m += 4) {
+      rhi = (m - mfirst) & 4;
       more = static_for_while<4>([&](auto qc) {
         constexpr int q = decltype(qc)::value;
         if (m + q > mlast) return false;
-        sync();
+        if (q % RG == 0) sync();
         core(qc, m + q);
         return true;
       });
@@ -850,6 +892,7 @@ __device__ __forceinline__ void ca_march_fused(const DevGeom& G, const CaK& K, c
 #pragma unroll
       for (int q = 0; q < Sh::NQ; ++q) acc[q] = own_all ? acc[q] : 0.0;
     }
+    tdone();
   }
 }
 
@@ -862,7 +905,7 @@ __device__ __forceinline__ void ca_march_fused(const DevGeom& G, const CaK& K, c
 // that stopped inside block b - 1 (nupd < 0) wave 0 rewinds w, as pass 2 would.  Partials: the Gram
 // products q at [q][tile] (wave 1), block b's norms j at NQ * ntiles + [j][tile] (wave 0): the
 // reduction's n = n2 = ntiles.
-template <typename T, int S, int MW, int PART>
+template <typename T, int S, int MW, int PART, int RG>
 __global__ void __launch_bounds__(128, MW)
 k_ca_fused(DevGeom G, T* w, T* z0, T* z1, T* p0, T* p1, double* __restrict__ partials, const CaState* C, int TI,
            int tiles_j, const unsigned* __restrict__ ctbl, int cwords, CaFaces faces, CaPart part, int ntiles) {
@@ -915,11 +958,12 @@ k_ca_fused(DevGeom G, T* w, T* z0, T* z1, T* p0, T* p1, double* __restrict__ par
                                                              j1, tbl, faces, acc, ca, cb, cc, pz);
     return;
   }
-  __shared__ double ring[2 * 256];
+  __shared__ double ring[2 * RG * 256];
   constexpr int PF = PMX_CA_PF_FUSE;
+  unsigned long long tm[2] = {0, 0};
 #define PMX_CAF_MARCH(FA, R)                                                                                        \
-  ca_march_fused<T, S, FA, PF, R>(G, K, pin, zin, pout, zout, w, i0, i1, j0, j1, tbl, faces, acc, nacc, ca, cb, cc, \
-                                  pa, ring)
+  ca_march_fused<T, S, FA, PF, R, RG>(G, K, pin, zin, pout, zout, w, i0, i1, j0, j1, tbl, faces, acc, nacc, ca, cb, \
+                                      cc, pa, ring, tm)
   if (role == 0) {
     if (PART == 1 || fast) PMX_CAF_MARCH(true, 0);
     else if constexpr (PART != 1) PMX_CAF_MARCH(false, 0);
@@ -942,6 +986,10 @@ k_ca_fused(DevGeom G, T* w, T* z0, T* z1, T* p0, T* p1, double* __restrict__ par
     }
   }
 #undef PMX_CAF_MARCH
+#ifdef PMX_CAF_TIMING
+  if (lane == 0 && blk == 7 && id % 499 == 0)
+    printf("caf part %d role %d tile %d fast %d total %llu sync %llu\n", PART, role, id, int(fast), tm[0], tm[1]);
+#endif
 }
 
 // Row classes of every tile column (one thread per 16-row word): 2 bits per local row, over the
@@ -967,12 +1015,14 @@ __global__ void k_ca_row_classes(DevGeom G, DevTables Tb, int he, int wo, int ti
   out[t] = bits;
 }
 
-// The face coefficients of every local node (rows -1 .. nx+2, columns -1 .. ny+2): a(gi, gj) and
-// b(gi, gj) by the exact formula (the class fast values are bit-identical to it).
+// The face coefficients of every local node (rows 1-gh .. nx+gh, columns -1 .. ny+2; on 2-D blocks
+// with neighbours across y also the ghost columns: -8 .. ny+gh+2): a(gi, gj) and b(gi, gj) by the exact
+// formula (the class fast values are bit-identical to it).
 __global__ void __launch_bounds__(256) k_ca_faces(DevGeom G, DevTables Tb, double* fa, double* fb, int gh) {
-  const int lj = -1 + int(blockIdx.x * blockDim.x + threadIdx.x);
+  const int jlo = (G.nb & kNbYlo) ? -8 : -1, jhi = (G.nb & kNbYhi) ? G.ny + gh + 2 : G.ny + 2;
+  const int lj = jlo + int(blockIdx.x * blockDim.x + threadIdx.x);
   const int li = 1 - gh + int(blockIdx.y);
-  if (lj > G.ny + 2) return;
+  if (lj > jhi) return;
   const int gi = min(max(G.gi0 + li, 0), G.M), gj = min(max(G.gj0 + lj, 0), G.N);
   const int64_t o = int64_t(li) * G.pitch + lj;
   fa[o] = coef_a(Tb, G, gi, gj);
@@ -1142,6 +1192,23 @@ __device__ void ca_finish(const double* t, const double* u, double h, double wdi
   St->it = k + n;
 }
 
+// ca_finish's one lane reads and writes ~40 words of PcgState / CaState in a dependent order: on the
+// device structs that is a chain of L2 round trips (~19 us per reduction at 1600x2400).  The
+// finishing wave stages both structs in LDS (all lanes, one round trip), lane 0 runs on the copies,
+// the wave writes them back.
+template <typename X>
+__device__ __forceinline__ void wave_copy(X* dst, const X* src, int lane) {
+  static_assert(sizeof(X) % 8 == 0, "wave_copy: whole 8-byte words");
+  const unsigned long long* a = reinterpret_cast<const unsigned long long*>(src);
+  unsigned long long* b = reinterpret_cast<unsigned long long*>(dst);
+  for (int i = lane; i < int(sizeof(X) / 8); i += kWave) b[i] = a[i];
+}
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // Deterministic reduction of the partials (one array of n tile values per quantity: the Gram
 // products of pass 1, then the norms of the previous pass 2) + ca_finish.  Blocks sum contiguous tile
 // ranges (thread-strided, then waves in order) and publish their chunk sums; the last block to arrive
@@ -1217,14 +1284,87 @@ k_ca_reduce(const double* __restrict__ part, int n, int n2, double h, double wdi
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  if (lane == 0) {
-    if (finish) {
-      ca_finish<S>(tot, tot + Sh::NQ, h, wdiff, nmax, check_only != 0, St, C);
-      if (progress) __hip_atomic_store(progress, St->it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    } else {  // decomposed: the rank's sums, all-reduced before k_ca_finish
-      for (int q = 0; q < NT; ++q) C->red[q] = tot[q];
+  if (finish) {
+    __shared__ PcgState sst;
+    __shared__ CaState sc;
+    wave_copy(&sst, St, lane);
+    wave_copy(&sc, C, lane);
+    wave_lds_sync();
+    if (lane == 0) {
+      ca_finish<S>(tot, tot + Sh::NQ, h, wdiff, nmax, check_only != 0, &sst, &sc);
+      if (progress) __hip_atomic_store(progress, sst.it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      sc.ticket = 0u;  // re-arm for the next launch (every block has arrived; stream order publishes it)
     }
-    if (nb > 1) C->ticket = 0u;  // re-arm for the next launch (stream order makes this visible to it)
+    wave_lds_sync();
+    wave_copy(St, &sst, lane);
+    wave_copy(C, &sc, lane);
+  } else if (lane == 0) {  // decomposed: the rank's sums, all-reduced before k_ca_finish
+    for (int q = 0; q < NT; ++q) C->red[q] = tot[q];
+    if (nb > 1) C->ticket = 0u;
+  }
+}
+
+// The same reduction in ONE workgroup of 16 waves, for up to kCaReduce1Max tiles (the reference grids,
+// strips of 8 ranks): no chunk hand-off between workgroups (ticket, published chunks, a second wave
+// sum: ~7 of the ~19 us the multi-block reduction takes at 1600x2400), and the last wave stages the
+// solver state in LDS while the others still load partials.  Fixed order: thread-strided sums, wave
+// sums, then the 16 waves in index order.
+template <int S>
+__global__ void __launch_bounds__(1024)
+k_ca_reduce1(const double* __restrict__ part, int n, int n2, double h, double wdiff, int nmax, int check_only,
+             int finish, PcgState* St, CaState* C, long long* progress) {
+  using Sh = CaShape<S>;
+  constexpr int NT = Sh::NQ + Sh::NN, NW = 1024 / kWave;
+  __shared__ double lds[NT][NW];
+  __shared__ double tot[NT];
+  __shared__ PcgState sst;
+  __shared__ CaState sc;
+  if (St->done) {
+    if (threadIdx.x == 0) C->nupd = 0;
+    return;
+  }
+  const int wid = int(threadIdx.x) / kWave, lane = int(threadIdx.x) % kWave;
+  if (finish && wid == NW - 1) {
+    wave_copy(&sst, St, lane);
+    wave_copy(&sc, C, lane);
+  }
+  double sm[NT];
+#pragma unroll
+  for (int q = 0; q < NT; ++q) sm[q] = 0.0;
+  if (!check_only) {
+    for (int i = int(threadIdx.x); i < n; i += 1024) {
+#pragma unroll
+      for (int q = 0; q < Sh::NQ; ++q) sm[q] += part[int64_t(q) * n + i];
+    }
+  }
+  const double* p2 = part + int64_t(Sh::NQ) * n;
+  for (int i = int(threadIdx.x); i < n2; i += 1024) {
+#pragma unroll
+    for (int q = Sh::NQ; q < NT; ++q) sm[q] += p2[int64_t(q - Sh::NQ) * n2 + i];
+  }
+#pragma unroll
+  for (int q = 0; q < NT; ++q) {
+    sm[q] = wave_sum_mfma(sm[q]);
+    if (lane == 0) lds[q][wid] = sm[q];
+  }
+  __syncthreads();
+  if (wid != 0) return;
+  if (lane < NT) {
+    double v = 0.0;
+    for (int w = 0; w < NW; ++w) v += lds[lane][w];
+    tot[lane] = v;
+  }
+  wave_lds_sync();
+  if (finish) {
+    if (lane == 0) {
+      ca_finish<S>(tot, tot + Sh::NQ, h, wdiff, nmax, check_only != 0, &sst, &sc);
+      if (progress) __hip_atomic_store(progress, sst.it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    wave_lds_sync();
+    wave_copy(St, &sst, lane);
+    wave_copy(C, &sc, lane);
+  } else if (lane < NT) {  // decomposed: the rank's sums, all-reduced before k_ca_finish
+    C->red[lane] = tot[lane];
   }
 }
 
@@ -1232,23 +1372,87 @@ k_ca_reduce(const double* __restrict__ part, int n, int n2, double h, double wdi
 template <int S>
 __global__ void __launch_bounds__(64)
 k_ca_finish(double h, double wdiff, int nmax, int check_only, PcgState* St, CaState* C, long long* progress) {
-  if (threadIdx.x != 0) return;
-  if (St->done) {
-    C->nupd = 0;
-    return;
+  const int lane = int(threadIdx.x);
+  __shared__ PcgState sst;
+  __shared__ CaState sc;
+  wave_copy(&sst, St, lane);
+  wave_copy(&sc, C, lane);
+  wave_lds_sync();
+  if (lane == 0) {
+    if (sst.done) {
+      sc.nupd = 0;
+    } else {
+      double t[7 * S];
+      bool bad = false;
+      for (int q = 0; q < 7 * S; ++q) {
+        t[q] = sc.red[q];
+        bad |= !(t[q] == t[q]) || isinf(t[q]);
+      }
+      if (bad) sst.nan_flag = 1;
+      ca_finish<S>(t, t + 6 * S, h, wdiff, nmax, check_only != 0, &sst, &sc);
+      if (progress) __hip_atomic_store(progress, sst.it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
-  double t[7 * S];
-  bool bad = false;
-  for (int q = 0; q < 7 * S; ++q) {
-    t[q] = C->red[q];
-    bad |= !(t[q] == t[q]) || isinf(t[q]);
+  wave_lds_sync();
+  wave_copy(St, &sst, lane);
+  wave_copy(C, &sc, lane);
+}
+
+// Ghost exchange of the s-step on 2-D blocks (packed slots of the comm arena, 8 slots: 4 sides, 4
+// corners): the gh owned edge lines of z and p of one set, and the gh x gh corner blocks, once per
+// block of s iterations.  Slot layout [field][line q][pos]: x sides line q = row 1+q (x-lo) / nx-gh+1+q
+// (x-hi) when packing, ghost row 1-gh+q / nx+1+q when unpacking, pos = column - 1; y sides likewise
+// with columns; corners [field][q][t] = (row, column) offsets q, t into the gh x gh block.  A message
+// of slot s lands in the neighbour's opposite_slot(s) in the same order.  Grid: (ceil(max(nx, ny) /
+// 256), 8, 2 gh).
+template <typename T>
+__global__ void __launch_bounds__(256)
+k_ca_halo(DevGeom G, T* z, T* p, HaloBufs<T> H, int gh, int unpack, long long* progress) {
+  const int slot = blockIdx.y;
+  if (progress && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && threadIdx.x == 0)
+    __hip_atomic_fetch_add(progress + (unpack ? 2 : 1), 1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (!((G.nb >> slot) & 1)) return;
+  const int f = int(blockIdx.z) / gh, q = int(blockIdx.z) % gh;
+  const int t = int(blockIdx.x) * 256 + int(threadIdx.x);
+  const int nx = G.nx, ny = G.ny;
+  int li, lj;
+  int64_t idx;
+  if (slot < 2) {  // x sides: rows
+    if (t >= ny) return;
+    li = slot == 0 ? (unpack ? 1 - gh + q : 1 + q) : (unpack ? nx + 1 + q : nx - gh + 1 + q);
+    lj = 1 + t;
+    idx = (int64_t(f) * gh + q) * ny + t;
+  } else if (slot < 4) {  // y sides: columns
+    if (t >= nx) return;
+    li = 1 + t;
+    lj = slot == 2 ? (unpack ? 1 - gh + q : 1 + q) : (unpack ? ny + 1 + q : ny - gh + 1 + q);
+    idx = (int64_t(f) * gh + q) * nx + t;
+  } else {  // corners: gh x gh blocks
+    if (t >= gh) return;
+    const bool xhi = slot >= 6, yhi = slot == 5 || slot == 7;
+    li = xhi ? (unpack ? nx + 1 + q : nx - gh + 1 + q) : (unpack ? 1 - gh + q : 1 + q);
+    lj = yhi ? (unpack ? ny + 1 + t : ny - gh + 1 + t) : (unpack ? 1 - gh + t : 1 + t);
+    idx = (int64_t(f) * gh + q) * gh + t;
   }
-  if (bad) St->nan_flag = 1;
-  ca_finish<S>(t, t + 6 * S, h, wdiff, nmax, check_only != 0, St, C);
-  if (progress) __hip_atomic_store(progress, St->it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  T* fld = f == 0 ? z : p;
+  const int64_t o = int64_t(li) * G.pitch + lj;
+  if (unpack)
+    fld[o] = H.recv[slot][idx];
+  else
+    H.send[slot][idx] = fld[o];
 }
 
 }  // namespace
+
+template <typename T>
+void launch_ca_halo(const DevGeom& G, T* z, T* p, const HaloBufs<T>& H, int gh, bool unpack, hipStream_t s,
+                    long long* progress) {
+  PMX_CHECK(gh >= 1 && G.nx >= gh && G.ny >= gh, "s-step ghost exchange: blocks of at least gh x gh nodes");
+  const int n = std::max(G.nx, G.ny);
+  hipLaunchKernelGGL(k_ca_halo<T>, dim3((n + 255) / 256, kHaloSlots, 2 * gh), dim3(256), 0, s, G, z, p, H, gh,
+                     unpack ? 1 : 0, progress);
+  HIP_CHECK(hipGetLastError());
+}
 
 CaTiles make_ca_tiles(const DevGeom& G, int s, int rows, int rows2, int rows_f) {
   PMX_CHECK(s == 2 || s == 3, "s-step PCG: s must be 2 or 3");
@@ -1358,7 +1562,7 @@ void ca_build_classes(const DevGeom& G, const DevTables& Tb, const CaTiles& t, u
 
 void ca_build_faces(const DevGeom& G, const DevTables& Tb, double* fa, double* fb, int gh, hipStream_t s) {
   PMX_CHECK(G.nx + 2 * gh <= 65535, "k_ca_faces: grid.y limit");
-  hipLaunchKernelGGL(k_ca_faces, dim3((G.ny + 4 + 255) / 256, G.nx + 2 * gh), dim3(256), 0, s, G, Tb, fa, fb, gh);
+  hipLaunchKernelGGL(k_ca_faces, dim3((G.ny + gh + 12 + 255) / 256, G.nx + 2 * gh), dim3(256), 0, s, G, Tb, fa, fb, gh);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1373,7 +1577,7 @@ template <typename T>
 void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, T* p0, T* p1, double* partials,
                      const PcgState* S, const CaState* C, const CaTiles& t, bool upd, hipStream_t s,
                      hipStream_t sframe, hipEvent_t frame_wait) {
-  PMX_CHECK((G.nb & ~(kNbXlo | kNbXhi)) == 0, "s-step PCG runs undecomposed grids or row strips");
+  PMX_CHECK(G.nb == 0 || t.gh >= t.s, "s-step PCG: a decomposed grid needs s ghost rows / columns");
   if (!sframe) sframe = s;
   PMX_CHECK(t.tbl != nullptr && t.fa != nullptr && t.fb != nullptr, "s-step PCG: row-class / face tables missing");
   PMX_CHECK(sizeof(T) == 8 || !t.dma, "s-step PCG: LDS-DMA rows need fp64");
@@ -1430,8 +1634,7 @@ void launch_ca_sweep(const DevGeom& G, const DevTables& Tb, T* w, T* z0, T* z1, 
 template <typename T>
 void launch_ca_fused(const DevGeom& G, T* w, T* z0, T* z1, T* p0, T* p1, double* partials, const CaState* C,
                      const CaTiles& t, hipStream_t s, hipStream_t sframe, hipEvent_t frame_wait) {
-  PMX_CHECK((G.nb & ~(kNbXlo | kNbXhi)) == 0 && (G.nb == 0 || t.gh >= 2 * t.s),
-            "the fused s-step pass runs undecomposed grids or row strips with 2 s ghost rows");
+  PMX_CHECK(G.nb == 0 || t.gh >= 2 * t.s, "the fused s-step pass needs 2 s ghost rows / columns on a decomposed grid");
   PMX_CHECK(t.fuse && t.tbl_f != nullptr && t.fa != nullptr && t.fb != nullptr,
             "s-step PCG: fused tiling / row classes / face tables missing");
   if (!sframe) sframe = s;
@@ -1440,23 +1643,28 @@ void launch_ca_fused(const DevGeom& G, T* w, T* z0, T* z1, T* p0, T* p1, double*
   const CaFaces F{t.fa, t.fb, t.gh};
   const CaPart P1{1, t.tiles_i_f, t.ti_lo_f, t.ti_hi_f, t.tj_lo_f, t.tj_hi_f},
       P2{2, t.tiles_i_f, t.ti_lo_f, t.ti_hi_f, t.tj_lo_f, t.tj_hi_f}, P0{0, t.tiles_i_f, 0, 0, 0, 0};
-#define PMX_CAF_K(SS, MW, PT, PP, NB)                                                                             \
-  do {                                                                                                            \
-    if ((NB) > 0)                                                                                                 \
-      hipLaunchKernelGGL((k_ca_fused<T, SS, MW, PT>), dim3(NB), dim3(128), 0, (PT) == 2 ? sframe : s, G, w, z0, z1, \
-                         p0, p1, partials, C, t.rows_f, t.tiles_j_f, t.tbl_f, t.cwords, F, PP, n);                 \
+#define PMX_CAF_K(SS, MW, PT, PP, NB, RG)                                                                          \
+  do {                                                                                                              \
+    if ((NB) > 0)                                                                                                   \
+      hipLaunchKernelGGL((k_ca_fused<T, SS, MW, PT, RG>), dim3(NB), dim3(128), 0, (PT) == 2 ? sframe : s, G, w, z0, \
+                         z1, p0, p1, partials, C, t.rows_f, t.tiles_j_f, t.tbl_f, t.cwords, F, PP, n);              \
   } while (0)
   const bool split = t.split_f && nin > 0;
   if (frame_wait) HIP_CHECK(hipStreamWaitEvent(split ? sframe : s, frame_wait, 0));
-#define PMX_CAF(SS)                                     \
-  do {                                                  \
-    if (split) {                                        \
-      PMX_CAF_K(SS, 2, 2, P2, n - nin);                 \
-      if (t.waves_f == 3) PMX_CAF_K(SS, 3, 1, P1, nin); \
-      else PMX_CAF_K(SS, 2, 1, P1, nin);                \
-    } else {                                            \
-      PMX_CAF_K(SS, 2, 0, P0, n);                       \
-    }                                                   \
+  // interior kernel: rows per barrier group (rg_f), 3 waves per SIMD (2: RG 1 only)
+#define PMX_CAF(SS)                                                 \
+  do {                                                              \
+    if (split) {                                                    \
+      PMX_CAF_K(SS, 2, 2, P2, n - nin, 1);                          \
+      if (t.waves_f == 2) PMX_CAF_K(SS, 2, 1, P1, nin, 1);          \
+      else if (t.rg_f == 4) PMX_CAF_K(SS, 3, 1, P1, nin, 4);        \
+      else if (t.rg_f == 2) PMX_CAF_K(SS, 3, 1, P1, nin, 2);        \
+      else PMX_CAF_K(SS, 3, 1, P1, nin, 1);                         \
+    } else if (t.waves_f == 3) {                                    \
+      PMX_CAF_K(SS, 3, 0, P0, n, 1);                                \
+    } else {                                                        \
+      PMX_CAF_K(SS, 2, 0, P0, n, 1);                                \
+    }                                                               \
   } while (0)
   if (t.s == 2) PMX_CAF(2);
   else PMX_CAF(3);
@@ -1471,6 +1679,16 @@ void launch_ca_reduce(const double* partials, int n, int n2, int s_, double h, d
   PMX_CHECK(nmax >= 1 && nmax <= s_, "s-step PCG: a block runs 1..s iterations");
   const int nb = std::max(1, std::min(kCaReduceMaxBlocks, std::max(n, n2) / 512));
   const int co = check_only ? 1 : 0, fi = finish ? 1 : 0;
+  if (std::max(n, n2) <= kCaReduce1Max) {
+    if (s_ == 2)
+      hipLaunchKernelGGL(k_ca_reduce1<2>, dim3(1), dim3(1024), 0, s, partials, n, n2, h, wdiff, nmax, co, fi, S, C,
+                         progress);
+    else
+      hipLaunchKernelGGL(k_ca_reduce1<3>, dim3(1), dim3(1024), 0, s, partials, n, n2, h, wdiff, nmax, co, fi, S, C,
+                         progress);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (s_ == 2)
     hipLaunchKernelGGL(k_ca_reduce<2>, dim3(nb), dim3(256), 0, s, partials, n, n2, h, wdiff, nmax, co, fi, S, C, chunk,
                        progress);
@@ -1495,6 +1713,8 @@ void launch_ca_finish(int s_, double h, double wdiff, int nmax, bool check_only,
   template void launch_ca_init<T>(const DevGeom&, const DevTables&, T*, T*, hipStream_t);                         \
   template void launch_ca_sweep<T>(const DevGeom&, const DevTables&, T*, T*, T*, T*, T*, double*, const PcgState*, \
                                    const CaState*, const CaTiles&, bool, hipStream_t, hipStream_t, hipEvent_t);   \
+  template void launch_ca_halo<T>(const DevGeom&, T*, T*, const HaloBufs<T>&, int, bool, hipStream_t,          \
+                                  long long*);                                                                   \
   template void launch_ca_fused<T>(const DevGeom&, T*, T*, T*, T*, T*, double*, const CaState*, const CaTiles&,    \
                                    hipStream_t, hipStream_t, hipEvent_t);
 PMX_CA_INST(double)

@@ -182,6 +182,27 @@ HaloMsgs GpuSubdomainSolver::ca_halo_msgs(int set) const {
   return out;
 }
 
+// One s-step ghost exchange on `streams`: direct rows (strips), or packed (2-D blocks): pack -> send /
+// recv of the slots -> unpack
+void PcgDriver::ca_exchange(std::vector<hipStream_t>& streams) {
+  if (direct_) {
+    comm_->halo(local_, streams);
+    return;
+  }
+  comm_->before_pack(local_, streams);
+  for (size_t i = 0; i < local_.size(); ++i) {
+    HIP_CHECK(hipSetDevice(local_[i]->device()));
+    local_[i]->enqueue_halo_pack(streams[i]);
+  }
+  poison(streams);
+  comm_->halo(local_, streams);
+  for (size_t i = 0; i < local_.size(); ++i) {
+    HIP_CHECK(hipSetDevice(local_[i]->device()));
+    local_[i]->enqueue_halo_unpack(streams[i]);
+  }
+  HIP_CHECK(hipSetDevice(local_[0]->device()));
+}
+
 int PcgDriver::ca_batch() const {
   const int s = local_[0]->ca_s();
   const int b = graph_batch_ > 0 ? graph_batch_ : 16;
@@ -235,7 +256,8 @@ void PcgDriver::enqueue_ca(int64_t n, const std::function<void(int)>& mark) {
     return;
   }
   // decomposed: every rank's sums are all-reduced between the reduction and the scalars, and the s
-  // ghost rows of the new (z, p) set are exchanged after pass 2 (direct rows, one span per field).
+  // ghost rows of the new (z, p) set are exchanged after pass 2 (strips: direct rows, one span per field;
+  // 2-D blocks: ghost rows, columns and corners through the packed slots, ca_exchange).
   // With the overlapped schedule the exchange runs on the comm stream: the next pass 1's interior
   // tiles (which read no ghost row) start at once, its frame tiles wait for the exchange.  The batch
   // joins the comm stream at its end, so a captured graph has no edge into the next one.
@@ -256,12 +278,12 @@ void PcgDriver::enqueue_ca(int64_t n, const std::function<void(int)>& mark) {
         HIP_CHECK(hipEventRecord(ev_packed_[u], streams_[i]));
         HIP_CHECK(hipStreamWaitEvent(comm_streams_[i], ev_packed_[u], 0));
       });
-      comm_->halo(local_, comm_streams_);
+      ca_exchange(comm_streams_);
       for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipEventRecord(ev_halo_[u], comm_streams_[i])); });
       frame_waits(true);
       pending = true;
     } else if (any_nb_) {
-      comm_->halo(local_, streams_);
+      ca_exchange(streams_);
       mk(kPhHalo);
     }
   };

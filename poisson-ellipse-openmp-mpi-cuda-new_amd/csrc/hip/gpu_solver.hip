@@ -220,7 +220,10 @@ int choose_algo(const ProblemSpec& spec, const ProcGrid& grid, const GpuOptions&
   PMX_CHECK(o.resolved, "choose_algo needs resolve_options()");
   if (o.algo == 3) return 3;  // validated by the solver
   if (o.algo == -1) {
-    const bool strips = grid.Py == 1 && (grid.size() == 1 || (direct_rows && (spec.M - 1) / grid.Px >= 8));
+    // one grid, or (native transports) row strips of >= 8 rows / 2-D blocks of >= 8 x 8 nodes (BASELINE
+    // config 4: packed ghost rows, columns and corners once per block of s iterations)
+    const bool strips = grid.size() == 1 || (direct_rows && (spec.M - 1) / grid.Px >= 8 &&
+                                             (grid.Py == 1 || (spec.N - 1) / grid.Py >= 8));
     // every storage type: with fp32 / mixed fields the s-step keeps its basis and sums in fp64 registers
     // and beats pcg1 too (16384^2 0.951 vs 1.093 ms, 32768^2 3.356 vs 3.831; NOTES #124)
     bool ca = !o.exact && o.kernel == 1 && strips && int64_t(spec.M - 1) * (spec.N - 1) >= kCaAutoPoints;
@@ -235,7 +238,7 @@ int choose_algo(const ProblemSpec& spec, const ProcGrid& grid, const GpuOptions&
   return choose_single_pass(spec, grid, o, device_total_bytes, subdomains_per_device) ? 1 : 2;
 }
 
-CommLayout GpuSubdomainSolver::comm_layout(const Subdomain& sd, DType dtype, bool single_pass) {
+CommLayout GpuSubdomainSolver::comm_layout(const Subdomain& sd, DType dtype, bool single_pass, int ca_gh) {
   CommLayout L;
   L.elem = dtype == DType::kFp64 ? 8 : 4;
   L.single_pass = single_pass;
@@ -247,6 +250,8 @@ CommLayout GpuSubdomainSolver::comm_layout(const Subdomain& sd, DType dtype, boo
     // pcg2: one line of r per side; pcg1: 2 lines x (r, p) per side, one (r, p) per corner
     const int line = s < 2 ? sd.ny : sd.nx;
     L.edge_len[s] = single_pass ? (s < 4 ? 4 * line : 2) : (s < 4 ? line : 0);
+    // s-step (packed, k_ca_halo): ca_gh lines x (z, p) per side, a ca_gh x ca_gh block per corner
+    if (ca_gh > 0) L.edge_len[s] = 2 * ca_gh * (s < 4 ? line : ca_gh);
   }
   for (int s = 0; s < kHaloSlots; ++s) {
     L.send_off[s] = off;
@@ -289,22 +294,28 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   if (opt_.algo == -1) opt_.algo = choose_algo(spec, sd.grid, opt_, double(total_b), 1, false);
   pcg1_ = opt_.algo == 1;
   ca_ = opt_.algo == 3;
-  PMX_CHECK(!ca_ || (!opt.exact && sd.grid.Py == 1 && sd.nx >= opt.ca_s),
-            "s-step PCG (algo 3) runs the fast arithmetic, undecomposed or as row strips of at least s rows");
-  // the s-step's fused pass (GpuOptions::ca_fuse) reads radius 2s: on strips every strip must hold 2s
-  // rows -- decided from global data, so every rank runs the same schedule
-  const bool fuse_ok = sd.grid.size() == 1 || (spec.M - 1) / sd.grid.Px >= 2 * opt_.ca_s;
-  PMX_CHECK(!ca_ || opt_.ca_fuse != 1 || fuse_ok, "the fused s-step pass needs row strips of at least 2 s rows");
+  PMX_CHECK(!ca_ || (!opt.exact && sd.nx >= opt.ca_s && (sd.grid.Py == 1 || sd.ny >= opt.ca_s)),
+            "s-step PCG (algo 3) runs the fast arithmetic, on subdomains of at least s rows (and s columns on "
+            "2-D blocks)");
+  // the s-step's fused pass (GpuOptions::ca_fuse) reads radius 2s: every subdomain must hold 2s rows (and
+  // columns on 2-D blocks) -- decided from global data, so every rank runs the same schedule
+  const bool fuse_ok = sd.grid.size() == 1 || ((spec.M - 1) / sd.grid.Px >= 2 * opt_.ca_s &&
+                                               (sd.grid.Py == 1 || (spec.N - 1) / sd.grid.Py >= 2 * opt_.ca_s));
+  PMX_CHECK(!ca_ || opt_.ca_fuse != 1 || fuse_ok, "the fused s-step pass needs subdomains of at least 2 s rows / columns");
   ca_fuse_ = ca_ && (opt_.ca_fuse == 1 || (opt_.ca_fuse == -1 && fuse_ok));
-  // ghost rows per side: 2 (the single-pass radius-2 halo); a decomposed s-step strip needs s, 2s with
-  // the fused pass
+  // ghost rows per side: 2 (the single-pass radius-2 halo); a decomposed s-step subdomain needs s, 2s with
+  // the fused pass (rows, and columns on 2-D blocks)
   gh_ = ca_ && sd.grid.size() > 1 ? (ca_fuse_ ? 2 * opt_.ca_s : opt_.ca_s) : 2;
+  const bool ca_cols = ca_ && sd.grid.Py > 1;  // ghost columns: gh_ per side
   PMX_CHECK(!pcg1_ || (!opt.exact && opt.kernel == 1 && (sd.grid.size() == 1 || (sd.nx >= 2 && sd.ny >= 2))),
             "pcg1 needs the wave kernels, the fast arithmetic and a subdomain of at least 2 x 2 nodes");
 
   // +8 columns of padding: vector loads of VEC <= 4 columns starting at <= ny+3 stay in the row,
   // and the last padding element of a row is column -1 of the next one
-  geom_ = make_dev_geom(spec, sd, int64_t(round_up(size_t(sd.ny + 2 + 8), align_elems)));
+  // (s-step blocks: + 2 gh + 8, so that the right ghost columns ny+1 .. ny+gh of a row and the left ones of
+  // the next row -- that row's padding read as columns -gh .. -1 -- never overlap)
+  geom_ = make_dev_geom(spec, sd,
+                        int64_t(round_up(size_t(sd.ny + 2 + 8 + (ca_cols ? 2 * gh_ + 8 : 0)), align_elems)));
   const DevGeom& G = geom_;
 
   // fields: element (li, lj), li = -1 .. nx+2, at base[li*pitch + lj]; base = alloc + pitch +
@@ -341,6 +352,10 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     ca_geom_.nb = 0;
     ca_geom_.gi0 = 0;
     ca_geom_.M = sd.nx + 1;
+    if (sd.grid.Py > 1) {  // 2-D blocks: also Dirichlet across y, on the problem's columns 1 .. ny
+      ca_geom_.gj0 = 0;
+      ca_geom_.N = sd.ny + 1;
+    }
     for (const double** t : {&ca_tables_.rv, &ca_tables_.xlo, &ca_tables_.xhi, &ca_tables_.x}) *t += o;
     ca_tables_.acls += 4 * o;
     ca_tables_.bcls += 4 * o;
@@ -432,6 +447,9 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     ca_tiles_.fuse = ca_fuse_ ? 1 : 0;
     if (const char* e = study_env("PMX_CA_WAVES_F"); e && e[0]) ca_tiles_.waves_f = std::atoi(e);
     if (const char* e = study_env("PMX_CA_SPLIT_F"); e && e[0]) ca_tiles_.split_f = std::atoi(e);
+    if (const char* e = study_env("PMX_CA_RG_F"); e && e[0]) ca_tiles_.rg_f = std::atoi(e);
+    PMX_CHECK(ca_tiles_.rg_f == 1 || ca_tiles_.rg_f == 2 || ca_tiles_.rg_f == 4,
+              "s-step PCG: fused row steps per barrier must be 1, 2 or 4");
     PMX_CHECK(ca_tiles_.waves_f == 2 || ca_tiles_.waves_f == 3, "s-step PCG: fused waves per SIMD must be 2 or 3");
     // the face coefficients of every node, read on the rows the ellipse cuts (2 more field-sized arrays)
     // fp64 whatever the fields' storage, in the fields' pitch (elements); column 1 of every row 256-B aligned
@@ -481,7 +499,7 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
   reduce_ws_ = partials_ + npart * 5;
   HIP_CHECK(hipMemset(reduce_ws_, 0, kReduceWsDoubles * sizeof(double)));
 
-  layout_ = comm_layout(sd, opt.dtype, pcg1_ || ca_);
+  layout_ = comm_layout(sd, opt.dtype, pcg1_ || ca_, ca_ && sd.grid.size() > 1 ? gh_ : 0);
   if (external_arena) {
     arena_ = reinterpret_cast<char*>(external_arena);
     own_arena_ = false;
@@ -728,13 +746,14 @@ size_t GpuSubdomainSolver::estimate_device_bytes_algo(const ProblemSpec& spec, c
   // fused pass)
   const size_t elem = dtype == DType::kFp64 ? 8 : 4, align = 256 / elem;
   const int gh = sd.grid.size() > 1 ? 2 * kCaMaxS : 2;
-  const size_t pitch = round_up(size_t(sd.ny + 2 + 8), align);
+  const size_t pitch = round_up(size_t(sd.ny + 2 + 8 + (sd.grid.Py > 1 ? 2 * gh + 8 : 0)), align);
   const size_t field = round_up((align - 1 + size_t(sd.nx + 2 * gh) * pitch) * elem, 256);
   const size_t face = round_up((31 + size_t(sd.nx + 2 * gh) * pitch) * 8, 256);
   const size_t tables = (4 * size_t(spec.M + 2) + 4 * size_t(spec.N + 2)) * 8 + 8 * size_t(spec.M + 2) * 4;
   // partials: 21 doubles per 8-row tile of 116 columns (the smallest tiling), row-class words
   const size_t partials = (size_t(sd.nx) / 8 + 1) * (size_t(sd.ny) / 116 + 1) * 21 * 8 * 2;
-  return 5 * field + 2 * face + tables + partials + comm_layout(sd, dtype, true).bytes + (1u << 20);
+  return 5 * field + 2 * face + tables + partials +
+         comm_layout(sd, dtype, true, sd.grid.size() > 1 ? gh : 0).bytes + (1u << 20);
 }
 
 size_t GpuSubdomainSolver::device_bytes() const {
@@ -814,6 +833,21 @@ void GpuSubdomainSolver::halo_impl(hipStream_t s, bool unpack) {
   after_launch(s);
 }
 
+// 2-D blocks (no direct rows): pack / unpack the gh edge lines and corners of the set ca_halo_msgs would
+// name (the set the next block reads, CaState::blk & 1 mirrored by ca_blk_) through the arena slots
+void GpuSubdomainSolver::ca_halo_impl(hipStream_t s, bool unpack) {
+  const int set = int(ca_blk_ & 1);
+  char* fz = set ? r2_ + field_off_ * elem_ : static_cast<char*>(field_base(1));
+  char* fp = static_cast<char*>(field_base(set ? 3 : 2));
+  if (elem_ == 8)
+    launch_ca_halo<double>(geom_, reinterpret_cast<double*>(fz), reinterpret_cast<double*>(fp), halo<double>(), gh_,
+                           unpack, s, progress_dev_);
+  else
+    launch_ca_halo<float>(geom_, reinterpret_cast<float*>(fz), reinterpret_cast<float*>(fp), halo<float>(), gh_, unpack,
+                          s, progress_dev_);
+  after_launch(s);
+}
+
 void GpuSubdomainSolver::set_direct_rows(bool on) {
   PMX_CHECK(!on || can_direct_rows(), "direct-row ghost exchange needs pcg1 on a row strip (x neighbours only)");
   direct_rows_ = on;
@@ -849,11 +883,19 @@ HaloMsgs GpuSubdomainSolver::halo_msgs() const {
 }
 
 void GpuSubdomainSolver::enqueue_halo_pack(hipStream_t s) {
+  if (ca_ && geom_.nb != 0 && !direct_rows_) {
+    ca_halo_impl(s, false);
+    return;
+  }
   if (!pcg1_ || geom_.nb == 0 || direct_rows_) return;
   if (opt_.dtype == DType::kFp64) halo_impl<double>(s, false); else halo_impl<float>(s, false);
 }
 
 void GpuSubdomainSolver::enqueue_halo_unpack(hipStream_t s) {
+  if (ca_ && geom_.nb != 0 && !direct_rows_) {
+    ca_halo_impl(s, true);
+    return;
+  }
   if (!pcg1_ || geom_.nb == 0 || direct_rows_) return;
   if (opt_.dtype == DType::kFp64) halo_impl<double>(s, true); else halo_impl<float>(s, true);
 }
@@ -1238,8 +1280,8 @@ PcgDriver::PcgDriver(std::vector<GpuSubdomainSolver*> local, Comm* comm, int gra
   if (const char* d = study_env("PMX_DIRECT_ROWS"); d && d[0] == '0') direct = false;
   direct_ = direct;
   for (auto* s : local_) s->set_direct_rows(direct_);
-  PMX_CHECK(!ca_ || !any_nb || direct_,
-            "s-step PCG on a decomposed grid needs the direct-row exchange (row strips, RCCL / local / loopback)");
+  // s-step: row strips move their ghost rows directly where the transport can; otherwise (2-D blocks, or
+  // a transport without direct rows) the packed slots carry rows, columns and corners (k_ca_halo)
   // One hardware queue per process (GPU_MAX_HW_QUEUES=1): every stream lands on it, so forking the
   // halo / frame work onto side streams cannot overlap anything -- and ROCm 7.2 segfaults inside
   // hipGraphLaunch on a captured graph with forked branches in that configuration (traced with
@@ -1340,7 +1382,7 @@ void PcgDriver::init() {
       HIP_CHECK(hipSetDevice(local_[i]->device()));
       local_[i]->enqueue_init(streams_[i]);
     }
-    if (any_nb_) comm_->halo(local_, streams_);
+    if (any_nb_) ca_exchange(streams_);
     synchronize();
     return;
   }

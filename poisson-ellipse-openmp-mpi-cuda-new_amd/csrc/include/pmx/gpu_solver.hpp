@@ -237,7 +237,8 @@ class GpuSubdomainSolver {
   GpuSubdomainSolver(const GpuSubdomainSolver&) = delete;
   GpuSubdomainSolver& operator=(const GpuSubdomainSolver&) = delete;
 
-  static CommLayout comm_layout(const Subdomain& sd, DType dtype, bool single_pass);
+  // ca_gh > 0: the s-step's packed slots (ca_gh ghost lines of z and p per side, ca_gh x ca_gh corners)
+  static CommLayout comm_layout(const Subdomain& sd, DType dtype, bool single_pass, int ca_gh = 0);
   // Upper bound of the device memory a solver for `sd` allocates (fields -- 4, or 5 for the
   // single-pass iteration -- tables, partials, comm arena).  Checked against hipMemGetInfo before
   // allocating; used by `pmx --plan` and the pcg1/pcg2 choice.
@@ -397,6 +398,7 @@ class GpuSubdomainSolver {
   template <typename T> void phase_a_kernel_only(hipStream_t s, int part = 0);
   template <typename T> void phase_b_kernel_only(hipStream_t s, bool pack = true);
   template <typename T> HaloBufs<T> halo() const;
+  void ca_halo_impl(hipStream_t s, bool unpack);  // k_ca_halo on the (z, p) set the next block reads
   template <typename T> void halo_impl(hipStream_t s, bool unpack);
   void after_launch(hipStream_t s) const;
   void construct(uintptr_t external_arena);
@@ -615,6 +617,7 @@ class PcgDriver {
   enum PhaseBucket { kPhA = 0, kPhB, kPhRed, kPhAr, kPhHalo };
   void enqueue_ca(int64_t n, const std::function<void(int)>& mark = {});
   int ca_batch() const;
+  void ca_exchange(std::vector<hipStream_t>& streams);
   int ca_phase() const;  // captured s-step batches on decomposed grids depend on the (z, p) set parity
   // pack -> comm -> unpack, filling the inputs of sweep `target` (direct rows: comm only)
   void halo_exchange_pcg1(std::vector<hipStream_t>& streams, long long target);

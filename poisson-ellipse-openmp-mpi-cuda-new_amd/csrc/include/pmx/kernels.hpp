@@ -161,6 +161,7 @@ struct CaTiles {
   int ti_lo_f = 0, ti_hi_f = 0, tj_lo_f = 0, tj_hi_f = 0;
   int split_f = 1;     // interior tiles by the fast-only kernel, the frame by the general one
   int waves_f = 3;     // waves per SIMD the fused interior kernel's registers must allow (2 or 3)
+  int rg_f = 1;        // fused interior tiles: row steps per producer / consumer barrier (1, 2, 4)
   unsigned* tbl_f = nullptr;
   int ntiles() const { return tiles_i * tiles_j; }
   int ntiles2() const { return tiles_i2 * tiles_j; }
@@ -174,6 +175,11 @@ void ca_build_classes(const DevGeom& G, const DevTables& Tb, const CaTiles& t, u
                       bool fused = false);
 // fa / fb: local (0, 0) of two field-sized arrays (rows -1 .. nx+2 allocated)
 void ca_build_faces(const DevGeom& G, const DevTables& Tb, double* fa, double* fb, int gh, hipStream_t s);
+// the s-step's packed ghost exchange on 2-D blocks (k_ca_halo): pack z, p of one set into the send
+// slots, or unpack the receive slots into the ghost rows / columns / corners
+template <typename T>
+void launch_ca_halo(const DevGeom& G, T* z, T* p, const HaloBufs<T>& H, int gh, bool unpack, hipStream_t s,
+                    long long* progress);
 // z = D^-1 r in place, p = z (the first block's set 0)
 template <typename T>
 void launch_ca_init(const DevGeom& G, const DevTables& Tb, T* z, T* p, hipStream_t s);
@@ -191,6 +197,8 @@ void launch_ca_fused(const DevGeom& G, T* w, T* z0, T* z1, T* p0, T* p1, double*
                      const CaTiles& t, hipStream_t s, hipStream_t sframe = nullptr, hipEvent_t frame_wait = nullptr);
 // chunk: kCaReduceMaxBlocks * ca_nq(s) doubles of workspace; nmax: iterations this block may run
 constexpr int kCaReduceMaxBlocks = 256;
+// up to this many tiles the s-step reduction runs in one workgroup (k_ca_reduce1: no chunk hand-off)
+constexpr int kCaReduce1Max = 12288;
 // check_only: the pending stop test alone (after the last block of a batch; pass 2 then rewinds w if
 // the test stopped inside that block)
 // n / n2: pass 1 / pass 2 tiles (the partials of each)

@@ -18,7 +18,9 @@ def test_auto_picks_the_sstep_on_big_fp64_grids_and_strips(native, spec):
 
 def test_auto_keeps_pcg1_where_the_sstep_does_not_apply(native, spec):
     big = spec(16384, 16384)
-    assert native.choose_algo(big, world=8, split=native.Split.reference) == 1  # 2 x 4 blocks
+    assert native.choose_algo(big, world=8, split=native.Split.reference) == 3  # 2 x 4 blocks (config 4)
+    assert native.choose_algo(spec(3000, 3000), world=64, split=native.Split.reference) == 3  # 375 x 375 blocks
+    assert native.choose_algo(spec(2600, 2600), world=1024, split=native.Split.rows) == 1  # 2-row strips
     assert native.choose_algo(big, dtype="fp32") == 3      # fp32 fields, fp64 basis and sums
     assert native.choose_algo(big, dtype="mixed") == 3
     assert native.choose_algo(spec(800, 1200), dtype="fp32") == 1

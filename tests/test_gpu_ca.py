@@ -98,11 +98,41 @@ def test_ca_matches_cpu_oracle(pkg):
     assert np.abs(w - ref.w).max() <= 1e-9 * np.abs(ref.w).max()
 
 
-def test_ca_rejects_blocks_and_thin_strips(pkg):
-    with pytest.raises(RuntimeError, match="s-step"):
-        _sess(pkg, 400, 600, "ca", 3, ranks=2, split="cols")  # column strips: no direct-row exchange
+def test_ca_rejects_thin_strips(pkg):
     with pytest.raises(RuntimeError, match="s-step"):
         _sess(pkg, 20, 600, "ca", 3, ranks=8, split="rows")  # strips of 2 rows < s
+
+
+@pytest.mark.parametrize("ranks,split,grid", [(4, "reference", (2, 2)), (8, "reference", (2, 4)),
+                                              (9, "reference", (3, 3)), (3, "cols", (1, 3))])
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_ca_blocks(pkg, monkeypatch, ranks, split, grid, fuse):
+    """2-D blocks on one GPU (LocalComm, BASELINE config 4): gh = 2s (fused) or s ghost rows AND columns
+    of z and p, plus the gh x gh corner blocks of the diagonal neighbours, packed through the comm arena
+    slots once per block of s iterations (k_ca_halo).  The reference count and the undecomposed solution
+    to rounding."""
+    monkeypatch.setenv("PMX_CA_FUSE", fuse)
+    one = _sess(pkg, 800, 1200, "ca", 3)
+    r1 = one.solve(1)
+    b = _sess(pkg, 800, 1200, "ca", 3, ranks=ranks, split=split)
+    assert tuple(b.grid) == grid
+    assert b.tile["algo"] == "ca" and bool(b.tile.get("fused")) == (fuse == "1")
+    r = b.solve(1)
+    assert r["status"] == r1["status"] == "converged"
+    assert r["iters"] == r1["iters"] == 989
+    w, w1 = b.gather_local_w(), one.gather_local_w()
+    assert np.abs(w - w1).max() <= 1e-10 * np.abs(w1).max()
+
+
+@pytest.mark.parametrize("graph_batch", [0, 32])
+def test_ca_blocks_odd_sizes_graphs_and_max_iter(pkg, graph_batch):
+    """uneven 2 x 2 blocks (97x130), captured and eager, and a max_iter stop inside a block"""
+    for mi in (None, 40):
+        p = lambda: pkg.PoissonEllipse(M=97, N=130, max_iter=mi)  # noqa: E731
+        a = _sess(pkg, 0, 0, "ca", 3, problem=p(), ranks=4, split="reference", graph_batch=graph_batch)
+        ra = a.solve(1)
+        rb = _sess(pkg, 0, 0, "pcg1", problem=p()).solve(1)
+        assert ra["status"] == rb["status"] and ra["iters"] == rb["iters"]
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "mixed"])
