@@ -144,9 +144,10 @@ def test_study_knobs_are_ignored_outside_study_mode(pkg, monkeypatch):
     assert not _ca(pkg, 400, 600).tile["fused"]
 
 
-def _sequences(native, pkg, world, M, N, graph_batch, iters, overlap=True):
+def _sequences(native, pkg, world, M, N, graph_batch, iters, overlap=True, split="rows"):
     spec = pkg.PoissonEllipse(M=M, N=N).to_native()
-    return native.record_comm_sequence(spec, world, native.Split.rows, graph_batch, iters, overlap=overlap, algo=3)
+    return native.record_comm_sequence(spec, world, getattr(native.Split, split), graph_batch, iters, overlap=overlap,
+                                       algo=3)
 
 
 @pytest.mark.parametrize("graph_batch,iters", [(0, 8), (32, 8), (4, 10), (32, 40)])
@@ -169,6 +170,26 @@ def test_sstep_strips_every_rank_issues_the_same_comm_sequence(native, pkg, grap
     for r, l in enumerate(logs):
         sends = [e for e in l if e[1] == "send"][:4]
         assert {e[3] for e in sends} <= {r - 1, r + 1}
+
+
+@pytest.mark.parametrize("graph_batch,iters", [(0, 8), (32, 40)])
+def test_sstep_blocks_every_rank_issues_the_same_comm_sequence(native, pkg, graph_batch, iters):
+    """2 x 4 blocks of the s-step (BASELINE config 4): the same collectives on every rank, one packed
+    exchange group per block with every send matched by the neighbour's receive of the same size --
+    sides (gh lines of z and p) and corners (gh x gh) -- to the 3..8 neighbours a block has."""
+    from test_gpu_launch_path import _check_sequences
+    logs = _sequences(native, pkg, 8, 257, 384, graph_batch, iters, split="reference")
+    _check_sequences(logs, 8)
+    batch = 0 if graph_batch == 0 else (graph_batch + 2) // 3 * 3
+    sizes = [iters] if batch == 0 else [min(batch, iters - k) for k in range(0, iters, batch)]
+    blocks = sum((n + 2) // 3 for n in sizes)
+    for l in logs:
+        ar = [e for e in l if e[1] == "allreduce"]
+        assert len(ar) == blocks + len(sizes) and all(e[2] == 21 for e in ar)
+        assert sum(1 for e in l if e[1] == "group_start") == 1 + blocks
+    # a corner block of 2 x 4 has 3 neighbours (two sides, one diagonal), an edge block 5
+    peers = [{e[3] for e in l if e[1] == "send"} for l in logs]
+    assert sorted(len(p) for p in peers) == [3, 3, 3, 3, 5, 5, 5, 5]
 
 
 def test_sstep_serialized_schedule_one_stream_one_communicator(native, pkg):
