@@ -223,20 +223,31 @@ void PcgDriver::enqueue_ca(int64_t n, const std::function<void(int)>& mark) {
     }
     HIP_CHECK(hipSetDevice(local_[0]->device()));
   };
+  // The fused schedule is carried across batches: a batch ends with a fused pass, which applies its
+  // last block AND sums the next block's Gram products, so the next batch starts at the reduction
+  // (primed) and only a solve's first batch runs pass 1.  Every block then costs one fused pass and one
+  // reduction wherever the batch boundaries fall (pass 1 + pass 2 at each boundary cost ~0.84 ms more
+  // than one fused pass at 16384^2).  The stop test of the batch's last block still runs at its end (a
+  // check-only reduction of the fused pass's norms, and the rewind), so w and the PcgState are exact
+  // at every batch end; the extra Gram sums of a solve's last fused pass are the one wasted half-pass.
+  const bool fused = local_[0]->ca_fused();
+  const bool primed = fused && local_[0]->ca_primed();
+  auto set_primed = [&](bool v) {
+    for (auto* g : local_) g->set_ca_primed(v);
+  };
   if (!any_nb_ && local_.size() == 1 && comm_->world_size() == 1) {
     // One grid: pass 1 -> reduce -> pass 2 per block, or with the fused pass
-    //   pass 1 -> reduce -> (fused -> reduce) x (blocks - 1) -> pass 2
+    //   [pass 1 unless primed] -> reduce -> (fused -> reduce) x (blocks - 1) -> fused
     // and then the last block's stop test (and its rewind): the state is exact at every batch end
     GpuSubdomainSolver* g = local_[0];
     hipStream_t st = streams_[0];
-    const bool fused = g->ca_fused();
     bool first = true;
     while (n > 0) {
       const int m = int(std::min<int64_t>(s, n));
       if (fused && !first) g->enqueue_ca_fused(st);
-      else g->enqueue_ca_pass(st, false);
-      mk(kPhA);
-      g->enqueue_ca_reduce(st, m, false, true, fused && !first);
+      else if (!primed) g->enqueue_ca_pass(st, false);
+      if (!(first && primed)) mk(kPhA);
+      g->enqueue_ca_reduce(st, m, false, true, fused && !(first && !primed));
       mk(kPhRed);
       if (!fused) {
         g->enqueue_ca_pass(st, true);
@@ -246,13 +257,14 @@ void PcgDriver::enqueue_ca(int64_t n, const std::function<void(int)>& mark) {
       n -= m;
     }
     if (fused) {
-      g->enqueue_ca_pass(st, true);
-      mk(kPhB);
+      g->enqueue_ca_fused(st);
+      mk(kPhA);
     }
-    g->enqueue_ca_reduce(st, 1, true, true);
+    g->enqueue_ca_reduce(st, 1, true, true, fused);
     mk(kPhRed);
     g->enqueue_ca_pass(st, true);  // rewind (a no-op unless the test stopped inside the last block)
     mk(kPhB);
+    set_primed(fused);
     return;
   }
   // decomposed: every rank's sums are all-reduced between the reduction and the scalars, and the s
@@ -288,19 +300,18 @@ void PcgDriver::enqueue_ca(int64_t n, const std::function<void(int)>& mark) {
     }
   };
   // Unfused, per block: pass 1 -> reduce -> all-reduce -> scalars -> pass 2 -> exchange.  Fused: pass 1
-  // -> reduce -> all-reduce -> scalars, then per further block fused pass -> exchange (under the
-  // reduction, all-reduce and scalars) -> ..., and the last block's pass 2 -> exchange.  Every rank runs
-  // the same schedule (ca_fused() is decided from global data).
-  const bool fused = local_[0]->ca_fused();
+  // (unless primed) -> reduce -> all-reduce -> scalars, then per further block fused pass -> exchange
+  // (under the reduction, all-reduce and scalars) -> ..., and a last fused pass -> exchange.  Every rank
+  // runs the same schedule (ca_fused() is decided from global data, primed by the same batches).
   bool first = true;
   while (n > 0) {
     const int m = int(std::min<int64_t>(s, n));
     const bool f = fused && !first;
     if (f) each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_fused(st); });
-    else each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, false); });
-    mk(kPhA);
+    else if (!primed) each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, false); });
+    if (!(first && primed)) mk(kPhA);
     if (f) exchange();
-    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_reduce(st, m, false, false, f); });
+    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_reduce(st, m, false, false, f || primed); });
     mk(kPhRed);
     comm_->allreduce(local_, 3, streams_);
     if (ar) mk(kPhAr);
@@ -315,11 +326,11 @@ void PcgDriver::enqueue_ca(int64_t n, const std::function<void(int)>& mark) {
     n -= m;
   }
   if (fused) {
-    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_pass(st, true); });
-    mk(kPhB);
+    each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_fused(st); });
+    mk(kPhA);
     exchange();
   }
-  each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_reduce(st, 1, true, false); });
+  each([&](GpuSubdomainSolver* g, hipStream_t st) { g->enqueue_ca_reduce(st, 1, true, false, fused); });
   mk(kPhRed);
   comm_->allreduce(local_, 3, streams_);
   if (ar) mk(kPhAr);
@@ -331,8 +342,13 @@ void PcgDriver::enqueue_ca(int64_t n, const std::function<void(int)>& mark) {
     for_each_stream([&](size_t i, size_t u) { HIP_CHECK(hipStreamWaitEvent(streams_[i], ev_halo_[u], 0)); });
     frame_waits(false);
   }
+  set_primed(fused);
 }
 
-int PcgDriver::ca_phase() const { return any_nb_ ? int(local_[0]->ca_blocks() & 1) : 0; }
+// the key of a captured s-step batch: the (z, p) set parity on decomposed grids (the exchange's spans),
+// and whether the batch starts primed (no pass 1)
+int PcgDriver::ca_phase() const {
+  return (any_nb_ ? int(local_[0]->ca_blocks() & 1) : 0) + (local_[0]->ca_primed() ? 2 : 0);
+}
 
 }  // namespace pmx

@@ -820,6 +820,7 @@ void GpuSubdomainSolver::init_impl(hipStream_t s) {
     ca_init_.s = ca_tiles_.s;  // (checked by load_checkpoint)
     HIP_CHECK(hipMemcpyAsync(ca_state_, &ca_init_, sizeof(CaState), hipMemcpyHostToDevice, s));
     ca_blk_ = 0;
+    ca_primed_ = false;
     launch_ca_init<T>(ca_geom_, ca_tables_, static_cast<T*>(field_base(1)), static_cast<T*>(field_base(2)), s);
     after_launch(s);
   }
@@ -1035,7 +1036,7 @@ constexpr char kCkptMagic[8] = {'P', 'M', 'X', 'C', 'K', 'P', 'T', '1'};
 // (+ its w-cycle state, r2 appended), v6 the s-step PCG (r2 = the second z buffer appended, then
 // CaState).  A checkpoint is written between batches, where every algorithm's state is exact: for the
 // s-step no block's stop test is pending and w holds every applied block.
-int GpuSubdomainSolver::ckpt_version() const { return ca_ ? 6 : pcg1_ ? 5 : 3; }
+int GpuSubdomainSolver::ckpt_version() const { return ca_ ? 7 : pcg1_ ? 5 : 3; }
 
 void GpuSubdomainSolver::save_checkpoint(std::ostream& os, hipStream_t s) const {
   HIP_CHECK(hipSetDevice(opt_.device));
@@ -1063,6 +1064,14 @@ void GpuSubdomainSolver::save_checkpoint(std::ostream& os, hipStream_t s) const 
     HIP_CHECK(hipMemcpy(&c, ca_state_, sizeof(CaState), hipMemcpyDeviceToHost));
     PMX_CHECK(c.pend_n == 0 && c.nupd <= 0, "s-step checkpoint inside a batch (a block's stop test is pending)");
     os.write(reinterpret_cast<const char*>(&c), sizeof(c));
+    // a carried fused schedule: the next block's Gram partials (so a resume continues bitwise)
+    const int32_t primed = ca_primed_ ? 1 : 0;
+    os.write(reinterpret_cast<const char*>(&primed), sizeof(primed));
+    if (primed) {
+      std::vector<double> part(ca_primed_doubles());
+      HIP_CHECK(hipMemcpy(part.data(), partials_, part.size() * sizeof(double), hipMemcpyDeviceToHost));
+      os.write(reinterpret_cast<const char*>(part.data()), std::streamsize(part.size() * sizeof(double)));
+    }
   }
   PMX_CHECK(os.good(), "checkpoint write failed");
 }
@@ -1072,7 +1081,7 @@ void GpuSubdomainSolver::load_checkpoint(std::istream& is, hipStream_t s) {
   CkptHeader h{};
   is.read(reinterpret_cast<char*>(&h), sizeof(h));
   PMX_CHECK(is.good() && std::memcmp(h.magic, kCkptMagic, 8) == 0 && h.version == ckpt_version(),
-            "not a pmx checkpoint of this iteration algorithm and layout (v3 pcg2, v5 pcg1, v6 s-step; file v"
+            "not a pmx checkpoint of this iteration algorithm and layout (v3 pcg2, v5 pcg1, v7 s-step; file v"
                 << h.version << ", solver v" << ckpt_version() << ")");
   PMX_CHECK(h.M == spec_.M && h.N == spec_.N && h.gi0 == sd_.gi0() && h.gj0 == sd_.gj0() &&
                 h.nx == sd_.nx && h.ny == sd_.ny && h.rank == sd_.rank,
@@ -1109,6 +1118,16 @@ void GpuSubdomainSolver::load_checkpoint(std::istream& is, hipStream_t s) {
     c.ticket = 0u;
     HIP_CHECK(hipMemcpy(ca_state_, &c, sizeof(CaState), hipMemcpyHostToDevice));
     ca_blk_ = c.blk;  // the (z, p) set the next block reads
+    int32_t primed = 0;
+    is.read(reinterpret_cast<char*>(&primed), sizeof(primed));
+    PMX_CHECK(is.good() && (primed == 0 || (primed == 1 && ca_fused())), "checkpoint: bad s-step schedule flag");
+    if (primed) {
+      std::vector<double> part(ca_primed_doubles());
+      is.read(reinterpret_cast<char*>(part.data()), std::streamsize(part.size() * sizeof(double)));
+      PMX_CHECK(is.good(), "truncated checkpoint (carried Gram partials)");
+      HIP_CHECK(hipMemcpy(partials_, part.data(), part.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+    ca_primed_ = primed != 0;
   }
 }
 
@@ -1540,9 +1559,11 @@ hipGraphExec_t PcgDriver::build_graph(int phase, int len) {
     return nullptr;
   }
   std::vector<long long> k0, b0;
+  std::vector<bool> pr0;
   for (auto* s : local_) {
     k0.push_back(s->host_k());
     b0.push_back(s->ca_blocks());
+    pr0.push_back(s->ca_primed());
   }
   PMX_CHECK(!halo_pending_, "graph capture with an unjoined ghost exchange");
   PMX_GDBG("capture begun");
@@ -1555,6 +1576,7 @@ hipGraphExec_t PcgDriver::build_graph(int phase, int len) {
     for (size_t i = 0; i < local_.size(); ++i) {
       local_[i]->set_host_k(k0[i]);
       local_[i]->set_ca_blocks(b0[i]);
+      local_[i]->set_ca_primed(pr0[i]);
     }
     hipGraph_t dead = nullptr;
     (void)hipStreamEndCapture(streams_[0], &dead);
@@ -1565,6 +1587,7 @@ hipGraphExec_t PcgDriver::build_graph(int phase, int len) {
   for (size_t i = 0; i < local_.size(); ++i) {
     local_[i]->set_host_k(k0[i]);
     local_[i]->set_ca_blocks(b0[i]);
+    local_[i]->set_ca_primed(pr0[i]);
   }
   PMX_GDBG("enqueued; ending capture");
   if (hipStreamEndCapture(streams_[0], &g) != hipSuccess || !g) {
@@ -1612,9 +1635,11 @@ bool PcgDriver::prepare(int64_t n) {
   TraceRange tr("pmx:prepare");
   const int cyc = graph_period();
   std::vector<long long> k0, b0;
+  std::vector<bool> pr0;
   for (auto* s : local_) {
     k0.push_back(s->host_k());
     b0.push_back(s->ca_blocks());
+    pr0.push_back(s->ca_primed());
   }
   bool ok = graph_batch_ > 0 && !graph_failed_;
   const int gb = ca_ ? ca_batch() : graph_batch_;
@@ -1623,6 +1648,8 @@ bool PcgDriver::prepare(int64_t n) {
     for (size_t i = 0; i < local_.size(); ++i) {
       local_[i]->set_host_k(k0[i] + off);
       local_[i]->set_ca_blocks(b0[i] + blocks);
+      // after a batch the fused s-step schedule is primed
+      local_[i]->set_ca_primed(off > 0 ? local_[i]->ca_fused() : bool(pr0[i]));
     }
   };
   auto phase = [&]() { return ca_ ? ca_phase() : int((k0[0] + done) % cyc); };
@@ -1665,7 +1692,10 @@ void PcgDriver::enqueue_iterations(int64_t n) {
     advance_host_k(len);
     if (ca_) {
       const int s = local_[0]->ca_s();
-      for (auto* g : local_) g->set_ca_blocks(g->ca_blocks() + (len + s - 1) / s);
+      for (auto* g : local_) {
+        g->set_ca_blocks(g->ca_blocks() + (len + s - 1) / s);
+        g->set_ca_primed(g->ca_fused());  // the batch ended with a fused pass
+      }
     }
     note_graph(len);
     done += len;

@@ -302,7 +302,7 @@ class GpuSubdomainSolver {
   // reads.  Synchronous; written at batch boundaries.
   void save_checkpoint(std::ostream& os, hipStream_t s) const;
   void load_checkpoint(std::istream& is, hipStream_t s);
-  int ckpt_version() const;  // file version of this solver's algorithm (3 pcg2, 5 pcg1, 6 s-step)
+  int ckpt_version() const;  // file version of this solver's algorithm (3 pcg2, 5 pcg1, 7 s-step)
 
   PcgState read_state(hipStream_t s) const;  // synchronous D2H of the scalars
   std::vector<double> read_partials(hipStream_t s) const;  // the partials buffer (5 per tile slot)
@@ -375,6 +375,12 @@ class GpuSubdomainSolver {
   // host mirror of CaState::blk (blocks enqueued): the (z, p) set the next exchange sends
   long long ca_blocks() const { return ca_blk_; }
   void set_ca_blocks(long long b) { ca_blk_ = b; }
+  // fused schedule carried across batches: a batch ends with a fused pass (block b applied AND block
+  // b+1's Gram partials summed), so the next batch starts at the reduction instead of pass 1 -- and the
+  // batch boundary no longer costs pass 1 + pass 2 in place of one fused pass.  init clears it.
+  bool ca_primed() const { return ca_primed_; }
+  void set_ca_primed(bool v) { ca_primed_ = v; }
+  size_t ca_primed_doubles() const { return size_t(ca_nq(ca_tiles_.s)) * size_t(ca_tiles_.ntilesf()); }
   // pcg1: host mirror of the device iteration counter S->it -- the index of the next sweep this
   // solver enqueues.  init sets it to 0, every enqueued reduction (which bumps S->it on the
   // device) advances it, load_checkpoint reads it from the checkpoint.  It picks the plain or the
@@ -430,6 +436,7 @@ class GpuSubdomainSolver {
   CaState ca_init_{};           // host template of the state init() uploads
   double* ca_chunk_ = nullptr;  // its reduction's chunk sums
   long long ca_blk_ = 0;        // blocks enqueued since init (CaState::blk's host mirror)
+  bool ca_primed_ = false;      // partials_ hold the next block's Gram sums from a batch-ending fused pass
   int gh_ = 2;                  // ghost rows of the fields on each side
   bool ca_fuse_ = false;        // the s-step's fused pass (GpuOptions::ca_fuse, decided at construction)
   // the s-step kernels' geometry and face tables: geom_ / tables_, or under ca_dirichlet a standalone
