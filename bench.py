@@ -858,9 +858,10 @@ def measure_loopback(args) -> int:
 # ~11.55-11.65 (1.92-1.95 ms/step), i.e. ~6.65 / ~6.9 / ~7.2 ps per point and iteration.  The
 # class says which one the timed run got, so a driver record can be read against the others.
 PLACEMENT_CLASS_PS = ((6.80, "fast"), (7.05, "mid"))
-# s-step PCG (6 iterations = 2 blocks per candidate): provisional limits from the round-5 boxes
-# (kept 8.61 / 8.80 / 9.03 / 9.45 ms at 16384^2 = 5.35 / 5.47 / 5.61 / 5.87 ps per point and iteration)
-PLACEMENT_CLASS_PS_CA = ((5.50, "fast"), (5.70, "mid"))
+# s-step PCG (6 iterations = 2 fused blocks per candidate, round 6): provisional limits from the
+# 16384^2 same-process A/Bs, whose sessions ran at ~0.95 or ~1.01-1.02 ms/iteration (fused pass ~2.85 /
+# ~3.05 ms: ~3.55 / ~3.8 ps per point and iteration, profiles/r6/shape/)
+PLACEMENT_CLASS_PS_CA = ((3.65, "fast"), (3.85, "mid"))
 
 
 def placement_class(kept_ms, points, dtype, algo="pcg1"):

@@ -1520,8 +1520,14 @@ CaTiles make_ca_tiles(const DevGeom& G, int s, int rows, int rows2, int rows_f) 
   t.wo_f = 128 - 2 * t.he_f;
   t.tiles_j_f = (G.ny + t.wo_f - 1) / t.wo_f;
   if (rows_f <= 0) {
-    rows_f = 64;
-    while (rows_f > 16 && int64_t((G.nx + rows_f - 1) / rows_f) * t.tiles_j_f < 6000) rows_f /= 2;
+    // 96 rows where that still leaves >= 20,000 tiles (~13 rounds of 1536 workgroups): a tile marches
+    // rows_f + 4s rows, so 96 instead of 64 cuts the redundant halo row steps from 19% to 12.5%.
+    // 16384^2 same-process A/B, fastest of 20 probed blocks per session, ms/iteration over 11
+    // sessions: 64 rows median 1.015, 96 rows 0.950 (each bimodal by placement: 0.94-0.95 / 1.01-1.02);
+    // fp32 32768^2 3.43 -> 3.13 ms, mixed 16384^2 0.942 -> 0.893 (profiles/r6/shape/).  The 2-GPU strip
+    // (12,212 tiles at 96 rows) keeps 64: loopback 0.576 (64) vs 0.586 ms (96).
+    rows_f = int64_t((G.nx + 95) / 96) * t.tiles_j_f >= 20000 ? 96 : 64;
+    while (rows_f > 16 && rows_f <= 64 && int64_t((G.nx + rows_f - 1) / rows_f) * t.tiles_j_f < 6000) rows_f /= 2;
   }
   PMX_CHECK(rows_f >= 1 && rows_f <= 4096, "s-step PCG: fused tile rows must be in [1, 4096]");
   t.rows_f = rows_f;

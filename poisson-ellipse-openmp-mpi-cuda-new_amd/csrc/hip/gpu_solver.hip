@@ -539,6 +539,19 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
 // (profiles/r4/placement/).  No ghost exchange (timing only); the driver's init() resets everything.
 void GpuSubdomainSolver::probe_iterations(hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   enqueue_init(s);
+  if (ca_ && ca_fused()) {  // fused schedule: pass 1 + reduction untimed, then two fused blocks -- the
+    // kernels a solve actually runs (pass 1 / pass 2 rank blocks differently from the fused pass:
+    // round 6, a probe of the unfused passes kept blocks on which the fused pass ran ~6% slower)
+    enqueue_ca_pass(s, false);
+    enqueue_ca_reduce(s, ca_tiles_.s, false, true);
+    HIP_CHECK(hipEventRecord(e0, s));
+    for (int k = 0; k < 2; ++k) {
+      enqueue_ca_fused(s);
+      enqueue_ca_reduce(s, ca_tiles_.s, false, true, true);
+    }
+    HIP_CHECK(hipEventRecord(e1, s));
+    return;
+  }
   if (ca_) {  // s-step: one untimed block, then two (2 s iterations); strips: this rank's sums only
     const auto block = [&] {
       enqueue_ca_pass(s, false);
