@@ -637,7 +637,7 @@ __device__ __forceinline__ void ca_march_fused(const DevGeom& G, const CaK& K, c
                                                const double (&ca)[CaShape<S>::NB], const double (&cb)[CaShape<S>::NB],
                                                const double (&cc)[CaShape<S>::NB],
                                                const double (&pa)[S][CaShape<S>::NB], double* ring,
-                                               unsigned long long* tm = nullptr) {
+                                               unsigned long long* tm = nullptr, double* dring = nullptr) {
   using Sh = CaShape<S>;
   constexpr int NB = Sh::NB, HE = CaFuseShape<S>::HE;
   const int64_t P = G.pitch;
@@ -821,7 +821,69 @@ __device__ __forceinline__ void ca_march_fused(const DevGeom& G, const CaK& K, c
         ca_store2<T>(w + o, c0, wn, FAST || own_all, own);
       }
     };
-    static_assert(PF == 1 || PF == 3, "ca_march_fused: prefetch depth 1 or 3");
+    static_assert(PF == 1 || PF == 3 || PF == 4, "ca_march_fused: prefetch depth 1 or 3 (registers), 4 (LDS-DMA)");
+    if constexpr (PF == 4) {
+      // LDS-DMA ring (fp64 FAST tiles): row mfirst + t of p, z (and w of row t - S) in slot t & 3, 4 rows
+      // ahead, no VGPR buffers.  global_load_lds_dwordx4 is invisible to hipcc, so the march counts
+      // vmcnt itself (as pcg1_march's DMA mode): before reading row m, the ops younger than its DMAs
+      // are the DMAs of rows m+1 .. m+3 (3 each) and the stores of the steps m-4 .. m-1 that stored
+      // (p, z, w of an owned row: 3 each).  Other vector ops (cut-row face loads) only add younger
+      // ops, and hipcc's own waits for them only drain more.
+      static_assert(FAST && sizeof(T) == 8, "ca_march_fused: LDS-DMA rows for fp64 FAST tiles");
+      constexpr int D = 4;
+      const unsigned voff = unsigned(c0 + 8) * 8u;  // bytes from row - 8 (ca_col's unsigned form)
+      const unsigned lds0 = unsigned(reinterpret_cast<uintptr_t>(dring));
+      auto dma_row = [&](int m, int slot) {
+        const unsigned l = lds0 + unsigned(slot) * 3072u;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's previous ds_reads have returned
+        const int mc = min(max(m, 1 - F.gh), G.nx + F.gh);
+        const int wc = min(max(m - S, 1 - F.gh), G.nx + F.gh);
+        dma16(pin + int64_t(mc) * P - 8, voff, l);
+        dma16(zin + int64_t(mc) * P - 8, voff, l + 1024u);
+        dma16(w + int64_t(wc) * P - 8, voff, l + 2048u);
+      };
+      // step t stores iff its row t - S is owned
+      auto stores = [&](int t) { return t >= mfirst && t - S >= i0 && t - S <= i1 ? 1 : 0; };
+#pragma unroll
+      for (int q = 0; q < D; ++q) dma_row(min(mfirst + q, mlast), q);
+      bool more = true;
+      for (int m = mfirst; more && m <= mlast; m += 4) {
+        rhi = (m - mfirst) & 4;
+        more = static_for_while<4>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          const int mm = m + q;
+          if (mm > mlast) return false;
+          const int nst = stores(mm - 4) + stores(mm - 3) + stores(mm - 2) + stores(mm - 1);
+          switch (nst) {
+            case 0: wait_vmcnt<3 * (D - 1)>(); break;
+            case 1: wait_vmcnt<3 * (D - 1) + 3>(); break;
+            case 2: wait_vmcnt<3 * (D - 1) + 6>(); break;
+            case 3: wait_vmcnt<3 * (D - 1) + 9>(); break;
+            default: wait_vmcnt<3 * (D - 1) + 12>(); break;
+          }
+          const double* sl = dring + q * 384;
+          const d2 pv = *reinterpret_cast<const d2*>(sl + 2 * lane);
+          const d2 zv = *reinterpret_cast<const d2*>(sl + 128 + 2 * lane);
+          const d2 wv = *reinterpret_cast<const d2*>(sl + 256 + 2 * lane);
+          CaFRow<T> cur;
+          cur.p[0] = pv.x;
+          cur.p[1] = pv.y;
+          cur.z[0] = zv.x;
+          cur.z[1] = zv.y;
+          cur.w[0] = wv.x;
+          cur.w[1] = wv.y;
+          dma_row(min(mm + D, mlast), q);
+          core(qc, mm, cur);
+          if (q % RG == RG - 1 || mm == mlast) sync();
+          return true;
+        });
+      }
+      wait_vmcnt<0>();  // no DMA may land after the wave has moved on (its LDS is the next tile's)
+#pragma unroll
+      for (int j = 0; j < S; ++j) nacc[j] = own_all ? nacc[j] : 0.0;
+      tdone();
+      return;
+    }
     constexpr int NBUF = PF + 1;
     CaFRow<T> buf[NBUF];
 #pragma unroll
@@ -905,7 +967,7 @@ __device__ __forceinline__ void ca_march_fused(const DevGeom& G, const CaK& K, c
 // that stopped inside block b - 1 (nupd < 0) wave 0 rewinds w, as pass 2 would.  Partials: the Gram
 // products q at [q][tile] (wave 1), block b's norms j at NQ * ntiles + [j][tile] (wave 0): the
 // reduction's n = n2 = ntiles.
-template <typename T, int S, int MW, int PART, int RG>
+template <typename T, int S, int MW, int PART, int RG, bool DMAF = false>
 __global__ void __launch_bounds__(128, MW)
 k_ca_fused(DevGeom G, T* w, T* z0, T* z1, T* p0, T* p1, double* __restrict__ partials, const CaState* C, int TI,
            int tiles_j, const unsigned* __restrict__ ctbl, int cwords, CaFaces faces, CaPart part, int ntiles) {
@@ -959,13 +1021,19 @@ k_ca_fused(DevGeom G, T* w, T* z0, T* z1, T* p0, T* p1, double* __restrict__ par
     return;
   }
   __shared__ double ring[2 * RG * 256];
+  // the producer's LDS-DMA rows (DMAF: fp64 interior tiles): 4 slots of p, z, w rows
+  __shared__ double dring[DMAF ? 4 * 384 : 2];
+  static_assert(!DMAF || (PART == 1 && sizeof(T) == 8), "k_ca_fused: LDS-DMA rows for fp64 interior tiles");
   constexpr int PF = PMX_CA_PF_FUSE;
   unsigned long long tm[2] = {0, 0};
 #define PMX_CAF_MARCH(FA, R)                                                                                        \
   ca_march_fused<T, S, FA, PF, R, RG>(G, K, pin, zin, pout, zout, w, i0, i1, j0, j1, tbl, faces, acc, nacc, ca, cb, \
                                       cc, pa, ring, tm)
   if (role == 0) {
-    if (PART == 1 || fast) PMX_CAF_MARCH(true, 0);
+    if constexpr (DMAF)
+      ca_march_fused<T, S, true, 4, 0, RG>(G, K, pin, zin, pout, zout, w, i0, i1, j0, j1, tbl, faces, acc, nacc, ca, cb,
+                                           cc, pa, ring, tm, dring);
+    else if (PART == 1 || fast) PMX_CAF_MARCH(true, 0);
     else if constexpr (PART != 1) PMX_CAF_MARCH(false, 0);
 #pragma unroll
     for (int j = 0; j + 1 < S; j += 2) wave_sum2_mfma(nacc[j], nacc[j + 1]);
@@ -1649,23 +1717,27 @@ void launch_ca_fused(const DevGeom& G, T* w, T* z0, T* z1, T* p0, T* p1, double*
   const CaFaces F{t.fa, t.fb, t.gh};
   const CaPart P1{1, t.tiles_i_f, t.ti_lo_f, t.ti_hi_f, t.tj_lo_f, t.tj_hi_f},
       P2{2, t.tiles_i_f, t.ti_lo_f, t.ti_hi_f, t.tj_lo_f, t.tj_hi_f}, P0{0, t.tiles_i_f, 0, 0, 0, 0};
-#define PMX_CAF_K(SS, MW, PT, PP, NB, RG)                                                                          \
+#define PMX_CAF_KD(SS, MW, PT, PP, NB, RG, DM)                                                                     \
   do {                                                                                                              \
     if ((NB) > 0)                                                                                                   \
-      hipLaunchKernelGGL((k_ca_fused<T, SS, MW, PT, RG>), dim3(NB), dim3(128), 0, (PT) == 2 ? sframe : s, G, w, z0, \
-                         z1, p0, p1, partials, C, t.rows_f, t.tiles_j_f, t.tbl_f, t.cwords, F, PP, n);              \
+      hipLaunchKernelGGL((k_ca_fused<T, SS, MW, PT, RG, DM>), dim3(NB), dim3(128), 0, (PT) == 2 ? sframe : s, G, w, \
+                         z0, z1, p0, p1, partials, C, t.rows_f, t.tiles_j_f, t.tbl_f, t.cwords, F, PP, n);          \
   } while (0)
+#define PMX_CAF_K(SS, MW, PT, PP, NB, RG) PMX_CAF_KD(SS, MW, PT, PP, NB, RG, false)
+  constexpr bool kDmaOk = sizeof(T) == 8;
   const bool split = t.split_f && nin > 0;
   if (frame_wait) HIP_CHECK(hipStreamWaitEvent(split ? sframe : s, frame_wait, 0));
   // interior kernel: rows per barrier group (rg_f), 3 waves per SIMD (2: RG 1 only)
 #define PMX_CAF(SS)                                                 \
   do {                                                              \
     if (split) {                                                    \
-      PMX_CAF_K(SS, 2, 2, P2, n - nin, 1);                          \
+      if (t.frame_first_f) PMX_CAF_K(SS, 2, 2, P2, n - nin, 1);     \
       if (t.waves_f == 2) PMX_CAF_K(SS, 2, 1, P1, nin, 1);          \
       else if (t.rg_f == 4) PMX_CAF_K(SS, 3, 1, P1, nin, 4);        \
       else if (t.rg_f == 2) PMX_CAF_K(SS, 3, 1, P1, nin, 2);        \
+      else if (kDmaOk && t.dma_f) PMX_CAF_KD(SS, 3, 1, P1, nin, 1, kDmaOk); \
       else PMX_CAF_K(SS, 3, 1, P1, nin, 1);                         \
+      if (!t.frame_first_f) PMX_CAF_K(SS, 2, 2, P2, n - nin, 1);    \
     } else if (t.waves_f == 3) {                                    \
       PMX_CAF_K(SS, 3, 0, P0, n, 1);                                \
     } else {                                                        \
@@ -1676,6 +1748,7 @@ void launch_ca_fused(const DevGeom& G, T* w, T* z0, T* z1, T* p0, T* p1, double*
   else PMX_CAF(3);
 #undef PMX_CAF
 #undef PMX_CAF_K
+#undef PMX_CAF_KD
   HIP_CHECK(hipGetLastError());
 }
 

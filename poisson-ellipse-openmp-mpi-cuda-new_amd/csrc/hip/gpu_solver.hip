@@ -448,6 +448,9 @@ void GpuSubdomainSolver::construct(uintptr_t external_arena) {
     if (const char* e = study_env("PMX_CA_WAVES_F"); e && e[0]) ca_tiles_.waves_f = std::atoi(e);
     if (const char* e = study_env("PMX_CA_SPLIT_F"); e && e[0]) ca_tiles_.split_f = std::atoi(e);
     if (const char* e = study_env("PMX_CA_RG_F"); e && e[0]) ca_tiles_.rg_f = std::atoi(e);
+    if (const char* e = study_env("PMX_CA_DMA_F"); e && e[0]) ca_tiles_.dma_f = std::atoi(e);
+    if (const char* e = study_env("PMX_CA_FRAME_FIRST_F"); e && e[0]) ca_tiles_.frame_first_f = std::atoi(e);
+    PMX_CHECK(ca_tiles_.dma_f == 0 || ca_tiles_.dma_f == 1, "s-step PCG: fused LDS-DMA rows must be 0 or 1");
     PMX_CHECK(ca_tiles_.rg_f == 1 || ca_tiles_.rg_f == 2 || ca_tiles_.rg_f == 4,
               "s-step PCG: fused row steps per barrier must be 1, 2 or 4");
     PMX_CHECK(ca_tiles_.waves_f == 2 || ca_tiles_.waves_f == 3, "s-step PCG: fused waves per SIMD must be 2 or 3");

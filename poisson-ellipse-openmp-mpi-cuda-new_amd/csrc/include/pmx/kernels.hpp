@@ -162,6 +162,12 @@ struct CaTiles {
   int split_f = 1;     // interior tiles by the fast-only kernel, the frame by the general one
   int waves_f = 3;     // waves per SIMD the fused interior kernel's registers must allow (2 or 3)
   int rg_f = 1;        // fused interior tiles: row steps per producer / consumer barrier (1, 2, 4)
+  // split fused pass: the frame kernel launched before (1) or after (0) the interior.  In a captured
+  // graph the first-launched node starts first: frame first delayed the interior by up to ~140 us and
+  // ran it slower; driver command 1.004-1.013 (frame first) vs 0.965-0.970 ms/step (frame last), three
+  // interleaved fresh-process runs each (profiles/r6/frame_order/)
+  int frame_first_f = 0;
+  int dma_f = 0;       // fp64 fused interior tiles: the producer's rows by LDS-DMA, 4 ahead (0: registers, 1 ahead)
   unsigned* tbl_f = nullptr;
   int ntiles() const { return tiles_i * tiles_j; }
   int ntiles2() const { return tiles_i2 * tiles_j; }
