@@ -99,8 +99,10 @@ def make_session(problem: PoissonEllipse, ranks: int = 1, split: str = "referenc
     block_tiles: -1 = auto (block-tile sweeps, pcg1_block.hip, on small undecomposed fp64 grids), 0 = off,
     1 = on for any undecomposed fp64 grid.
 
-    algo: -1 = auto (pcg1 / pcg2), "pcg1" / 1, "pcg2" / 2, or "ca" / 3 -- the s-step PCG
-    (ca_kernels.hip: ca_s = 2 or 3 iterations per two passes and one reduction; undecomposed fp64)."""
+    algo: -1 / "auto" (the library's choice: the s-step on grids of >= 6M points -- one GPU, row strips
+    or 2-D blocks -- when its fields fit, else pcg1 / pcg2), "pcg1" / 1, "pcg2" / 2, or "ca" / 3 -- the
+    s-step PCG (ca_kernels.hip: ca_s = 2 or 3 iterations per fused pass and one reduction; fp64, fp32
+    or mixed storage, fp64 basis and sums)."""
     n = _native()
     algo = {"auto": -1, "pcg1": 1, "pcg2": 2, "ca": 3}.get(algo, algo) if isinstance(algo, str) else algo
     return n.Session(problem.to_native(), world=int(ranks), comm="self" if ranks == 1 else "local",

@@ -100,8 +100,9 @@ import importlib, sys, numpy as np
 sys.path.insert(0, sys.argv[1])
 pkg = importlib.import_module("poisson-ellipse-openmp-mpi-cuda-new_amd")
 out = []
+algo = sys.argv[4] if len(sys.argv) > 4 else "auto"
 for gb in (0, 16):
-    s = pkg.make_session(pkg.PoissonEllipse(M=600, N=900), ranks=4, split=sys.argv[3], graph_batch=gb)
+    s = pkg.make_session(pkg.PoissonEllipse(M=600, N=900), ranks=4, split=sys.argv[3], graph_batch=gb, algo=algo)
     st = s.solve(1)
     out.append(np.concatenate([s.local_w(i).ravel() for i in range(4)]))
     out.append(np.array([st["iters"], float(s.overlapped), float(s.path_stats()["graph_iters"] > 0)]))
@@ -109,10 +110,10 @@ np.save(sys.argv[2], np.concatenate(out))
 """
 
 
-def _hwq_run(tmp_path, split, **env_extra):
-    out = str(tmp_path / f"hwq_{split}_{'_'.join(f'{k}{v}' for k, v in env_extra.items())}.npy")
+def _hwq_run(tmp_path, split, algo="auto", **env_extra):
+    out = str(tmp_path / f"hwq_{split}_{algo}_{'_'.join(f'{k}{v}' for k, v in env_extra.items())}.npy")
     env = dict(os.environ, PMX_PCG1_SPLIT="1", **env_extra)
-    p = subprocess.run([sys.executable, "-c", _HWQ_SCRIPT, ROOT, out, split], capture_output=True, text=True,
+    p = subprocess.run([sys.executable, "-c", _HWQ_SCRIPT, ROOT, out, split, algo], capture_output=True, text=True,
                        timeout=150, env=env)
     assert p.returncode == 0, p.stderr[-3000:]
     return np.load(out)
@@ -149,6 +150,30 @@ def test_split_sweep_needs_no_concurrent_queues(pkg, tmp_path, monkeypatch, spli
     check(_hwq_run(tmp_path, split, GPU_MAX_HW_QUEUES="1", PMX_FORK_ONE_QUEUE="1"), True, False)
     check(_hwq_run(tmp_path, split, GPU_MAX_HW_QUEUES="1"), False, True)
     check(_hwq_run(tmp_path, split, GPU_MAX_HW_QUEUES="2"), True, True)
+
+
+@pytest.mark.parametrize("split", ["reference", "rows"])
+def test_sstep_frame_stream_needs_no_concurrent_queues(pkg, tmp_path, split):
+    """the s-step's split passes fork their frame tiles onto a side stream inside every
+    block. With one hardware queue the driver drops that stream (the frame tiles run in-stream), so
+    no forked graph is built: the 16-iteration graph batches still replay, and w is bitwise the
+    default run's (4 row strips or 2 x 2 blocks of 600 x 900, both with ghost exchanges)."""
+    ref = []
+    for gb in (0, 16):
+        s = pkg.make_session(pkg.PoissonEllipse(M=600, N=900), ranks=4, split=split, graph_batch=gb, algo="ca")
+        st = s.solve(1)
+        assert s.tile["algo"] == "ca"
+        ref.append(np.concatenate([s.local_w(i).ravel() for i in range(4)]))
+        ref.append(np.array([st["iters"]]))
+    assert np.array_equal(ref[0], ref[2]) and ref[1][0] == ref[3][0]
+    n = ref[0].size
+    got = _hwq_run(tmp_path, split, "ca", GPU_MAX_HW_QUEUES="1")
+    for k in (0, 1):
+        o = k * (n + 3)
+        assert np.array_equal(got[o:o + n], ref[0]), k
+        assert got[o + n] == ref[1][0]
+        assert got[o + n + 1] == 0.0  # one queue: the exchange is not overlapped
+    assert got[n + 3 + n + 2] == 1.0  # graphs replayed
 
 
 def _check_sequences(logs, world):
