@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--ranks", type=int, default=1, help="LocalComm subdomains on the one GPU")
     ap.add_argument("--split", default="auto")
     ap.add_argument("--tol", action="store_true")
+    ap.add_argument("--placement", type=int, default=0, help="probe up to this many field blocks per session")
     ap.add_argument("--pkg", action="append", default=[], help="name=DIR: another copy of the package")
     ap.add_argument("--fresh", action="store_true",
                     help="every (round, shape, config) in a fresh child process: sessions created in a "
@@ -69,7 +70,8 @@ def main():
             os.environ.pop(k, None)
         os.environ.update(env)
         pkg = pkgs[name.partition("@")[2]]
-        return pkg.make_session(pkg.PoissonEllipse(M=M, N=N), ranks=a.ranks, split=a.split, dtype=a.dtype)
+        return pkg.make_session(pkg.PoissonEllipse(M=M, N=N), ranks=a.ranks, split=a.split, dtype=a.dtype,
+                                placement=a.placement)
 
     only = tuple(a.only.split(":")) if a.only else None
     for rnd in range(a.rounds):
