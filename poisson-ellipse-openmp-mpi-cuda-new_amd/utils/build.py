@@ -39,6 +39,7 @@ HIP_SOURCES = [
     "hip/ca_kernels.hip",
     "hip/ops_kernels.hip",
     "hip/gpu_solver.hip",
+    "hip/pcg_driver.hip",
     "hip/ca_solver.hip",
     "hip/pcg1_driver.hip",
     "hip/session.hip",
