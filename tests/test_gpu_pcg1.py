@@ -336,7 +336,7 @@ def test_pcg1_lds_dma_march_bitwise(pkg, monkeypatch, dma, grid, ranks):
     out = {}
     for d in (0, dma):
         monkeypatch.setenv("PMX_PCG1_DMA", str(d))
-        s = pkg.make_session(p, ranks=ranks, graph_batch=16)
+        s = pkg.make_session(p, ranks=ranks, graph_batch=16, algo="pcg1")
         assert s.tile.get("dpf", 0) == d
         r = s.solve(1)
         out[d] = (r["iters"], s.gather_local_w(), s.state(0)["red_c"])
@@ -362,7 +362,7 @@ def test_pcg1_lockstep_workgroups_bitwise(pkg, monkeypatch, waves, waves_w, grid
     for wv in (1, waves):
         monkeypatch.setenv("PMX_PCG1_WAVES", str(wv))
         monkeypatch.setenv("PMX_PCG1_WAVES_W", str(waves_w if wv > 1 else 0))
-        s = pkg.make_session(p, ranks=ranks, split=split, graph_batch=16)
+        s = pkg.make_session(p, ranks=ranks, split=split, graph_batch=16, algo="pcg1")
         assert s.tile["waves"] == wv
         r = s.solve(1)
         out[wv] = (r["iters"], s.gather_local_w(), s.state(0)["red_c"])
