@@ -575,7 +575,7 @@ def measure(args) -> int:
     dkw = dict(kw, **pkw, phase=watch.phase, init_timeout=COMM_INIT_TIMEOUT, ca_s=args.ca_s,
                split_sweep=split_sweep)
     # --algo auto: the library decides (choose_algo) -- the s-step PCG (ca_kernels.hip) where it applies
-    # and wins (the fast arithmetic, >= 3.5M points undecomposed / 6M on row strips or 2-D blocks -- BASELINE
+    # and wins (the fast arithmetic, >= 6M points, undecomposed, row strips or 2-D blocks -- BASELINE
     # config 4, `--split reference` -- on a native transport: RCCL or IPC, not torch) and its 7 fields
     # fit, else pcg1 / pcg2.  The JSON's config.tile.algo says which ran.
     ca_ok = not args.exact and (world == 1 or cfg["comm"] in ("native", "ipc"))

@@ -228,8 +228,7 @@ int choose_algo(const ProblemSpec& spec, const ProcGrid& grid, const GpuOptions&
                                              (grid.Py == 1 || (spec.N - 1) / grid.Py >= 8));
     // every storage type: with fp32 / mixed fields the s-step keeps its basis and sums in fp64 registers
     // and beats pcg1 too (16384^2 0.951 vs 1.093 ms, 32768^2 3.356 vs 3.831; NOTES #124)
-    const int64_t min_points = grid.size() == 1 ? kCaAutoPointsOne : kCaAutoPoints;
-    bool ca = !o.exact && o.kernel == 1 && strips && int64_t(spec.M - 1) * (spec.N - 1) >= min_points;
+    bool ca = !o.exact && o.kernel == 1 && strips && int64_t(spec.M - 1) * (spec.N - 1) >= kCaAutoPoints;
     if (ca && device_total_bytes > 0) {  // rank 0 holds the largest strip
       const Subdomain sd0 = decompose_2d(spec.M, spec.N, grid, 0);
       const double need = double(GpuSubdomainSolver::estimate_device_bytes_algo(spec, sd0, o.dtype, 3)) *

@@ -185,13 +185,10 @@ bool choose_single_pass(const ProblemSpec& spec, const ProcGrid& grid, const Gpu
 // The iteration algorithm (GpuOptions::algo) a run uses: an explicit 1 / 2 / 3 as given, auto (-1) the
 // s-step PCG (3) where it applies and wins -- the fast arithmetic (any storage), undecomposed or row strips
 // of >= 8 rows on a transport that moves ghost rows between fields (`direct_rows`), at least
-// kCaAutoPoints grid points (kCaAutoPointsOne on one undecomposed grid; below, pcg1's block tiles are
-// faster: same process 1200x1800 36.1 vs 44.9 us, while 1600x2400 runs 51.6 vs 53.9 on the s-step,
-// profiles/r6/small/ab_auto_vs_sstep.log) -- and
+// kCaAutoPoints grid points (below, pcg1's block tiles are faster: profiles/r5/ca/small.log) -- and
 // whose 7 fields fit into the device (`device_total_bytes` > 0; else no size test), otherwise
 // choose_single_pass.  A pure function of global data: every rank makes the same choice.
 constexpr int64_t kCaAutoPoints = 6000000;
-constexpr int64_t kCaAutoPointsOne = 3500000;
 int choose_algo(const ProblemSpec& spec, const ProcGrid& grid, const GpuOptions& resolved, double device_total_bytes,
                 int subdomains_per_device, bool direct_rows = true);
 

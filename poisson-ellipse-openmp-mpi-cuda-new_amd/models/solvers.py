@@ -99,8 +99,8 @@ def make_session(problem: PoissonEllipse, ranks: int = 1, split: str = "referenc
     block_tiles: -1 = auto (block-tile sweeps, pcg1_block.hip, on small undecomposed fp64 grids), 0 = off,
     1 = on for any undecomposed fp64 grid.
 
-    algo: -1 / "auto" (the library's choice: the s-step on grids of >= 3.5M points on one GPU, >= 6M
-    on row strips or 2-D blocks, when its fields fit, else pcg1 / pcg2), "pcg1" / 1, "pcg2" / 2, or "ca" / 3 -- the
+    algo: -1 / "auto" (the library's choice: the s-step on grids of >= 6M points -- one GPU, row strips
+    or 2-D blocks -- when its fields fit, else pcg1 / pcg2), "pcg1" / 1, "pcg2" / 2, or "ca" / 3 -- the
     s-step PCG (ca_kernels.hip: ca_s = 2 or 3 iterations per fused pass and one reduction; fp64, fp32
     or mixed storage, fp64 basis and sums)."""
     n = _native()

@@ -12,9 +12,7 @@ def test_auto_picks_the_sstep_on_big_fp64_grids_and_strips(native, spec):
     assert native.choose_algo(spec(16384, 16384)) == 3
     assert native.choose_algo(spec(16384, 16384), world=8) == 3           # 8 row strips (split auto)
     assert native.choose_algo(spec(2600, 2600)) == 3                      # >= 6M points
-    assert native.choose_algo(spec(1600, 2400)) == 3                      # one grid: from 3.5M points
-    assert native.choose_algo(spec(1600, 2400), world=2) == 1             # decomposed: from 6M points
-    assert native.choose_algo(spec(1200, 1800)) == 1                      # smaller reference grids: pcg1
+    assert native.choose_algo(spec(1600, 2400)) == 1                      # the reference grids: pcg1
     assert native.choose_algo(spec(800, 1200)) == 1
 
 

@@ -21,7 +21,7 @@ def _sess(pkg, monkeypatch, M, N, rows, **kw):
         monkeypatch.setenv("PMX_PCG1_BLOCK_ROWS", str(rows))
     else:
         monkeypatch.setenv("PMX_PCG1_BLOCK", "0")  # the march (auto picks block tiles on small grids)
-    kw.setdefault("algo", "pcg1")  # auto takes the s-step from 3.5M points (1600x2400)
+    kw.setdefault("algo", "pcg1")  # auto takes the s-step from 6M points (2400x3200)
     return pkg.make_session(pkg.PoissonEllipse(M=M, N=N), **kw)
 
 
@@ -45,7 +45,7 @@ def test_block_tiles_goldens_and_march_agreement(pkg, monkeypatch, rows, grid, i
 
 def test_block_tiles_auto_choice(pkg, monkeypatch):
     monkeypatch.delenv("PMX_PCG1_BLOCK", raising=False)
-    # pcg1's own choice of block tiles (auto takes the s-step on one grid from 3.5M points)
+    # pcg1's own choice of block tiles, whatever auto picks for the grid
     mk = lambda M, N, **kw: pkg.make_session(pkg.PoissonEllipse(M=M, N=N), algo="pcg1", **kw)  # noqa: E731
     assert mk(400, 600).tile.get("block_tiles") and mk(400, 600).tile["rows"] == 8   # 500 four-row tiles
     assert mk(800, 1200).tile.get("block_tiles") and mk(800, 1200).tile["rows"] == 12  # 2,000
